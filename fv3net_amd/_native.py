@@ -1,0 +1,142 @@
+"""ctypes binding of the C ABI in ``include/fv3net_amd.h``.
+
+The product path has exactly one implementation: the HIP library.  If it is
+missing or fails to load, every call raises ``NativeLibraryError`` — there is no
+CPU fallback anywhere in ``fv3net_amd``.
+"""
+import ctypes
+import os
+import threading
+
+from .build import LIB
+
+FV3_OK = 0
+FV3_ERR_INVALID = 1
+FV3_ERR_HIP = 2
+FV3_ERR_UNSUPPORTED = 3
+
+# every symbol include/fv3net_amd.h declares
+EXPORTED_SYMBOLS = (
+    "fv3_last_error",
+    "fv3_abi_version",
+    "fv3_mappm",
+    "fv3_mappm_ex",
+    "fv3_dense_create",
+    "fv3_dense_destroy",
+    "fv3_dense_k_in",
+    "fv3_dense_k_out",
+    "fv3_dense_forward",
+    "fv3_regrid_coarsen",
+    "fv3_column_integral",
+    "fv3_area_weighted_sums",
+)
+ABI_VERSION = 1
+
+
+class NativeLibraryError(RuntimeError):
+    """The HIP extension is missing or unusable (no fallback exists)."""
+
+
+class Layout(ctypes.Structure):
+    _fields_ = [("ncol_blk", ctypes.c_int64), ("ld", ctypes.c_int64), ("blk_stride", ctypes.c_int64)]
+
+
+class DenseDesc(ctypes.Structure):
+    _fields_ = [
+        ("n_in", ctypes.c_int),
+        ("in_nz", ctypes.POINTER(ctypes.c_int)),
+        ("in_clip", ctypes.POINTER(ctypes.c_int)),
+        ("in_mean", ctypes.POINTER(ctypes.c_float)),
+        ("in_sigma", ctypes.POINTER(ctypes.c_float)),
+        ("epsilon", ctypes.c_float),
+        ("width", ctypes.c_int),
+        ("n_hidden", ctypes.c_int),
+        ("hidden_kernel", ctypes.POINTER(ctypes.POINTER(ctypes.c_float))),
+        ("hidden_bias", ctypes.POINTER(ctypes.POINTER(ctypes.c_float))),
+        ("n_out", ctypes.c_int),
+        ("out_nz", ctypes.POINTER(ctypes.c_int)),
+        ("out_kernel", ctypes.POINTER(ctypes.POINTER(ctypes.c_float))),
+        ("out_bias", ctypes.POINTER(ctypes.POINTER(ctypes.c_float))),
+        ("out_mean", ctypes.POINTER(ctypes.c_float)),
+        ("out_sigma", ctypes.POINTER(ctypes.c_float)),
+        ("out_min", ctypes.POINTER(ctypes.c_float)),
+        ("out_max", ctypes.POINTER(ctypes.c_float)),
+        ("out_mask", ctypes.POINTER(ctypes.c_float)),
+    ]
+
+
+_lib = None
+_lock = threading.Lock()
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_I64 = ctypes.c_int64
+_F = ctypes.c_float
+_D = ctypes.c_double
+
+_SIGNATURES = {
+    "fv3_last_error": (ctypes.c_char_p, []),
+    "fv3_abi_version": (_I, []),
+    "fv3_mappm": (_I, [_P, _P, _P, _P, _I64, _I, _I, _I, _I, _F, _P]),
+    "fv3_mappm_ex": (_I, [_P, Layout, _P, Layout, _P, Layout, _P, Layout, _I64, _I, _I, _I, _I, _F, _P]),
+    "fv3_dense_create": (_I, [ctypes.POINTER(DenseDesc), ctypes.POINTER(_P)]),
+    "fv3_dense_destroy": (_I, [_P]),
+    "fv3_dense_k_in": (_I, [_P]),
+    "fv3_dense_k_out": (_I, [_P]),
+    "fv3_dense_forward": (_I, [_P, ctypes.POINTER(_P), ctypes.POINTER(Layout), ctypes.POINTER(_P),
+                               ctypes.POINTER(Layout), _I64, _P]),
+    "fv3_regrid_coarsen": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _P, _I, _I, _I,
+                                _I, _I, _I, _I, _D, _P]),
+    "fv3_column_integral": (_I, [_P, Layout, _P, Layout, _P, _I64, _I, _D, _P]),
+    "fv3_area_weighted_sums": (_I, [ctypes.POINTER(_P), _I, _P, _I64, _P, _P]),
+}
+
+
+def library_path() -> str:
+    return LIB
+
+
+def load():
+    """Load (once) and return the ctypes library; raise if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB):
+            raise NativeLibraryError(
+                f"fv3net_amd HIP extension not built: {LIB} is missing "
+                "(run `python -m fv3net_amd.build` or __graft_entry__.build()); "
+                "there is no CPU fallback"
+            )
+        try:
+            lib = ctypes.CDLL(LIB)
+        except OSError as e:
+            raise NativeLibraryError(f"cannot load {LIB}: {e}") from e
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.fv3_abi_version() != ABI_VERSION:
+            raise NativeLibraryError("fv3net_amd ABI version mismatch: rebuild the extension")
+        _lib = lib
+    return _lib
+
+
+def check(status: int, what: str = ""):
+    """Map a C-ABI status to the reference's exception types."""
+    if status == FV3_OK:
+        return
+    msg = load().fv3_last_error().decode(errors="replace")
+    if what:
+        msg = f"{what}: {msg}"
+    if status == FV3_ERR_INVALID:
+        raise ValueError(msg)
+    if status == FV3_ERR_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise RuntimeError(msg)
+
+
+def layout(ncol_blk: int, ld: int, blk_stride: int = 0) -> Layout:
+    return Layout(int(ncol_blk), int(ld), int(blk_stride))

@@ -1,0 +1,61 @@
+// fv3net_amd — shared plumbing for the HIP sources: error capture for the C ABI,
+// column-layout addressing, launch checks.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/fv3net_amd.h"
+
+namespace fv3 {
+
+void set_error(const char* fmt, ...);
+void clear_error();
+
+#define FV3_REQUIRE(cond, ...)                     \
+    do {                                           \
+        if (!(cond)) {                             \
+            ::fv3::set_error(__VA_ARGS__);         \
+            return FV3_ERR_INVALID;                \
+        }                                          \
+    } while (0)
+
+#define FV3_HIP(call)                                                                  \
+    do {                                                                               \
+        hipError_t e_ = (call);                                                        \
+        if (e_ != hipSuccess) {                                                        \
+            ::fv3::set_error("%s failed: %s (%s:%d)", #call, hipGetErrorString(e_),    \
+                             __FILE__, __LINE__);                                      \
+            return FV3_ERR_HIP;                                                        \
+        }                                                                              \
+    } while (0)
+
+#define FV3_LAUNCH_CHECK() FV3_HIP(hipGetLastError())
+
+// Device-side view of one column of one array under an fv3_layout.
+struct ColAddr {
+    int64_t ld;
+    int64_t off;  // (c / ncol_blk) * blk_stride + (c % ncol_blk)
+};
+
+__device__ __forceinline__ int64_t col_offset(const fv3_layout& l, int64_t c)
+{
+    if (l.ncol_blk <= 0 || c < l.ncol_blk) return c;  // single block: no division
+    const int64_t b = c / l.ncol_blk;
+    return b * l.blk_stride + (c - b * l.ncol_blk);
+}
+
+inline bool layout_ok(const fv3_layout& l, int64_t ncol)
+{
+    if (l.ld <= 0) return false;
+    if (l.ncol_blk <= 0) return false;
+    if (ncol > l.ncol_blk && l.blk_stride <= 0) return false;
+    return l.ld >= l.ncol_blk || l.ld == 0;
+}
+
+inline fv3_layout plain_layout(int64_t ncol) { return fv3_layout{ncol, ncol, 0}; }
+
+}  // namespace fv3

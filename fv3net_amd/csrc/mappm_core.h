@@ -1,0 +1,656 @@
+// fv3net_amd — streaming, one-pass formulation of FV3's vertical remap `mappm`.
+//
+// Reference semantics: /root/reference/external/mappm/mappm/mappm.f90
+//   mappm :10-126, cs_profile :132-532, cs_limiters :535-611,
+//   ppm_profile :614-851, ppm_limiters :854-931.
+//
+// The reference builds whole-column arrays (a4(4,km), dc, h2, delq, df2, d4)
+// and then walks output layers.  That needs ~2 KB of scratch per column, which
+// on gfx950 would either sink occupancy (LDS) or double HBM traffic (scratch).
+// Here one thread owns one column and walks the INPUT layers L = 1..km exactly
+// once ("lockstep over L"): a rolling register window produces the final PPM
+// coefficients of layer L (every value computed by the reference's own
+// expression tree, so results are bit-identical), and a small per-thread state
+// machine consumes the output layers whose edges fall in layer L.  Because the
+// reference's layer search only ever moves forward (k0 is carried,
+// mappm.f90:59,70-74,111), every output layer is finished from layers >= the
+// current one, so one forward sweep reproduces it.
+//
+// Arithmetic rules for bit parity with the x86 reference build:
+//   * compile with -ffp-contract=off (no FMA contraction), IEEE f32 division;
+//   * Fortran MAX/MIN as AMD flang emits them: a>b?a:b / a<b?a:b, left fold;
+//   * SIGN(a,b) = copysign(|a|, b).
+// Excluded from parity (reference UB): non-monotone pe1 where
+// the layer search fails (NaN here), qs for iv=-2 with kord>7 (0 here), and a
+// non-monotone pe2 that leaves the column below the old surface and re-enters.
+#pragma once
+
+#ifndef FV3_HD
+#define FV3_HD
+#endif
+
+#if !defined(__HIPCC__)
+#include <cmath>
+#include <cstdint>
+#endif
+
+namespace fv3 {
+
+FV3_HD inline float fmax2(float a, float b) { return a > b ? a : b; }
+FV3_HD inline float fmin2(float a, float b) { return a < b ? a : b; }
+FV3_HD inline float fmax3(float a, float b, float c) { return fmax2(fmax2(a, b), c); }
+FV3_HD inline float fmin3(float a, float b, float c) { return fmin2(fmin2(a, b), c); }
+FV3_HD inline float fsign(float a, float b) { return copysignf(fabsf(a), b); }
+
+// PPM coefficients of one layer: a1 = mean, al/ar = edges, a6 = curvature.
+struct Ppm {
+    float a1, al, ar, a6;
+};
+
+// ppm_limiters (mappm.f90:854-931) applied to one layer.
+FV3_HD inline void ppm_limit(float dm, Ppm& a, int lmt)
+{
+    const float r12 = 1.0f / 12.0f;
+    if (lmt == 3) return;
+    if (lmt == 0) {
+        if (dm == 0.0f) {
+            a.al = a.a1; a.ar = a.a1; a.a6 = 0.0f;
+        } else {
+            const float da1 = a.ar - a.al;
+            const float da2 = da1 * da1;
+            const float a6da = a.a6 * da1;
+            if (a6da < -da2) {
+                a.a6 = 3.0f * (a.al - a.a1);
+                a.ar = a.al - a.a6;
+            } else if (a6da > da2) {
+                a.a6 = 3.0f * (a.ar - a.a1);
+                a.al = a.ar - a.a6;
+            }
+        }
+    } else if (lmt == 1) {
+        const float qmp = 2.0f * dm;
+        a.al = a.a1 - fsign(fmin2(fabsf(qmp), fabsf(a.al - a.a1)), qmp);
+        a.ar = a.a1 + fsign(fmin2(fabsf(qmp), fabsf(a.ar - a.a1)), qmp);
+        a.a6 = 3.0f * (2.0f * a.a1 - (a.al + a.ar));
+    } else if (lmt == 2) {
+        if (fabsf(a.ar - a.al) < -a.a6) {
+            const float d = a.ar - a.al;
+            const float fmin = a.a1 + 0.25f * (d * d) / a.a6 + a.a6 * r12;
+            if (fmin < 0.0f) {
+                if (a.a1 < a.ar && a.a1 < a.al) {
+                    a.ar = a.a1; a.al = a.a1; a.a6 = 0.0f;
+                } else if (a.ar > a.al) {
+                    a.a6 = 3.0f * (a.al - a.a1);
+                    a.ar = a.al - a.a6;
+                } else {
+                    a.a6 = 3.0f * (a.ar - a.a1);
+                    a.al = a.ar - a.a6;
+                }
+            }
+        }
+    }
+}
+
+// cs_limiters (mappm.f90:535-611) applied to one layer.
+FV3_HD inline void cs_limit(bool extm, Ppm& a, int iv)
+{
+    const float r12 = 1.0f / 12.0f;
+    if (iv == 0) {
+        if (a.a1 <= 0.0f) {
+            a.al = a.a1; a.ar = a.a1; a.a6 = 0.0f;
+        } else if (fabsf(a.ar - a.al) < -a.a6) {
+            const float d = a.ar - a.al;
+            if ((a.a1 + 0.25f * (d * d) / a.a6 + a.a6 * r12) < 0.0f) {
+                if (a.a1 < a.ar && a.a1 < a.al) {
+                    a.ar = a.a1; a.al = a.a1; a.a6 = 0.0f;
+                } else if (a.ar > a.al) {
+                    a.a6 = 3.0f * (a.al - a.a1);
+                    a.ar = a.al - a.a6;
+                } else {
+                    a.a6 = 3.0f * (a.ar - a.a1);
+                    a.al = a.ar - a.a6;
+                }
+            }
+        }
+        return;
+    }
+    bool flat = (iv == 1) ? ((a.a1 - a.al) * (a.a1 - a.ar) >= 0.0f) : extm;
+    if (flat) {
+        a.al = a.a1; a.ar = a.a1; a.a6 = 0.0f;
+    } else {
+        const float da1 = a.ar - a.al;
+        const float da2 = da1 * da1;
+        const float a6da = a.a6 * da1;
+        if (a6da < -da2) {
+            a.a6 = 3.0f * (a.al - a.a1);
+            a.ar = a.al - a.a6;
+        } else if (a6da > da2) {
+            a.a6 = 3.0f * (a.ar - a.a1);
+            a.al = a.ar - a.a6;
+        }
+    }
+}
+
+FV3_HD inline float a6_of(const Ppm& a) { return 3.0f * (2.0f * a.a1 - (a.al + a.ar)); }
+
+// ---- ppm_profile pieces (mappm.f90:651-747), each the reference's expression ----
+
+// dc(k), interior k = 2..km-1 (mappm.f90:658-668); qm1,q0,qp1 = q(k-1..k+1),
+// dm1,d0,dp1 = delp(k-1..k+1).
+FV3_HD inline float ppm_dc(float qm1, float q0, float qp1, float dm1, float d0, float dp1)
+{
+    const float d4k = dm1 + d0;    // d4(k)
+    const float d4kp = d0 + dp1;   // d4(k+1)
+    const float c1 = (dm1 + 0.5f * d0) / d4kp;
+    const float c2 = (dp1 + 0.5f * d0) / d4k;
+    const float delq_k = qp1 - q0;   // delq(k)
+    const float delq_km = q0 - qm1;  // delq(k-1)
+    const float df2 = d0 * (c1 * delq_k + c2 * delq_km) / (d4k + dp1);
+    return fsign(fmin3(fabsf(df2), fmax3(qm1, q0, qp1) - q0, q0 - fmin3(qm1, q0, qp1)), df2);
+}
+
+// provisional left edge a4(2,k), interior k = 3..km-1 (mappm.f90:674-683);
+// d(-2..1) = delp(k-2..k+1), qm1,q0 = q(k-1), q(k); dcm1,dc0 = dc(k-1), dc(k).
+FV3_HD inline float ppm_al(float dm2, float dm1, float d0, float dp1, float qm1, float q0,
+                           float dcm1, float dc0)
+{
+    const float d4km = dm2 + dm1;  // d4(k-1)
+    const float d4k = dm1 + d0;    // d4(k)
+    const float d4kp = d0 + dp1;   // d4(k+1)
+    const float c1 = (q0 - qm1) * dm1 / d4k;
+    const float a1 = d4km / (d4k + dm1);
+    const float a2 = d4kp / (d4k + d0);
+    return qm1 + c1 + 2.0f / (d4km + d4kp) * (d0 * (c1 * (a1 - a2) + a2 * dcm1) - dm1 * a1 * dc0);
+}
+
+// h2(k) (mappm.f90:784-795), k = 2..km-1.
+FV3_HD inline float ppm_h2(float dcm1, float dcp1, float dm1, float d0, float dp1)
+{
+    return 2.0f * (dcp1 / dp1 - dcm1 / dm1) / (d0 + 0.5f * (dm1 + dp1)) * (d0 * d0);
+}
+
+// Huynh's 2nd constraint for an interior PPM layer (mappm.f90:799-821).
+FV3_HD inline void ppm_huynh(Ppm& a, float dc, float h2m, float h2p)
+{
+    const float fac = 1.5f;
+    const float pmp = 2.0f * dc;
+    float qmp = a.a1 + pmp;
+    float lac = a.a1 + fac * h2m + dc;
+    a.ar = fmin2(fmax2(a.ar, fmin3(a.a1, qmp, lac)), fmax3(a.a1, qmp, lac));
+    qmp = a.a1 - pmp;
+    lac = a.a1 + fac * h2p - dc;
+    a.al = fmin2(fmax2(a.al, fmin3(a.a1, qmp, lac)), fmax3(a.a1, qmp, lac));
+    a.a6 = a6_of(a);
+}
+
+// ---- remap consumer: the output-layer loop of mappm.f90:58-124, lockstep over L ----
+
+struct RemapState {
+    int k;          // current output layer (1-based)
+    bool accum;     // true: accumulating whole layers below the top edge (label 111 loop)
+    float qsum, dpsum;
+    float t, b;     // pe2(k), pe2(k+1)
+};
+
+// The column's input layer L as the consumer sees it.
+struct LayerView {
+    float pl0, pl1, dp, q1;  // pe1(L), pe1(L+1), dp1(L), q1(L)
+    Ppm a;
+};
+
+// Column-wide constants for the boundary branches (mappm.f90:62-67).
+struct ColumnEnds {
+    float pe_top, pe_bot, q_top, q_bot;  // pe1(1), pe1(km+1), q1(1), q1(km)
+};
+
+// Consume every output-layer event inside layer L.  `Out` provides
+// emit(k, value) and next_edge() -> pe2(k+2) for the layer after the current.
+template <class Out>
+FV3_HD inline void remap_layer(RemapState& s, const LayerView& v, const ColumnEnds& e, int kn, Out& out)
+{
+    const float r3 = 1.0f / 3.0f, r23 = 2.0f / 3.0f;
+    while (s.k <= kn) {
+        if (!s.accum) {
+            if (s.t <= e.pe_top) {
+                out.emit(s.k, e.q_top);
+            } else if (s.t >= e.pe_bot) {
+                out.emit(s.k, e.q_bot);
+            } else if (s.t >= v.pl0 && s.t <= v.pl1) {
+                const float pl = (s.t - v.pl0) / v.dp;
+                if (s.b <= v.pl1) {
+                    // entire new layer inside input layer L (mappm.f90:76-83)
+                    const float pr = (s.b - v.pl0) / v.dp;
+                    const float tt = r3 * (pr * (pr + pl) + pl * pl);
+                    out.emit(s.k, v.a.al + 0.5f * (v.a.a6 + v.a.ar - v.a.al) * (pr + pl) - v.a.a6 * tt);
+                } else {
+                    // fractional top piece (mappm.f90:85-92); continue in layers below
+                    const float delp = v.pl1 - s.t;
+                    const float tt = r3 * (1.0f + pl * (1.0f + pl));
+                    s.qsum = delp * (v.a.al + 0.5f * (v.a.a6 + v.a.ar - v.a.al) * (1.0f + pl) - v.a.a6 * tt);
+                    s.dpsum = delp;
+                    s.accum = true;
+                    return;
+                }
+            } else {
+                return;  // top edge lies further down: search continues at L+1
+            }
+        } else {
+            if (s.b > v.pl1) {
+                // whole layer (mappm.f90:99-104)
+                s.qsum = s.qsum + v.dp * v.q1;
+                s.dpsum = s.dpsum + v.dp;
+                return;
+            }
+            // bottom piece (mappm.f90:105-112)
+            const float delp = s.b - v.pl0;
+            const float esl = delp / v.dp;
+            s.qsum = s.qsum + delp * (v.a.al + 0.5f * esl * (v.a.ar - v.a.al + v.a.a6 * (1.0f - r23 * esl)));
+            s.dpsum = s.dpsum + delp;
+            out.emit(s.k, s.qsum / s.dpsum);
+            s.accum = false;
+        }
+        // advance to the next output layer; its search restarts at this L (k0 = L)
+        s.k += 1;
+        s.t = s.b;
+        s.b = out.next_edge(s.k);
+    }
+}
+
+// After the last input layer: extension below the old surface and the
+// boundary branches for what is left (mappm.f90:115-121, 62-67).
+template <class Out>
+FV3_HD inline void remap_finish(RemapState& s, const ColumnEnds& e, int kn, Out& out)
+{
+    while (s.k <= kn) {
+        if (s.accum) {
+            const float delp = s.b - e.pe_bot;
+            if (delp > 0.0f) {
+                s.qsum = s.qsum + delp * e.q_bot;
+                s.dpsum = s.dpsum + delp;
+            }
+            out.emit(s.k, s.qsum / s.dpsum);
+            s.accum = false;
+        } else if (s.t <= e.pe_top) {
+            out.emit(s.k, e.q_top);
+        } else if (s.t >= e.pe_bot) {
+            out.emit(s.k, e.q_bot);
+        } else {
+            out.emit(s.k, __builtin_nanf(""));  // search failed: reference UB
+        }
+        s.k += 1;
+        s.t = s.b;
+        s.b = out.next_edge(s.k);
+    }
+}
+
+// ---- one column, kord <= 7 (ppm_profile path), fully streaming ----
+//
+// `Col` provides (1-based levels):
+//   float q1(int k)   k = 1..km          float pe1(int k)  k = 1..km+1
+//   float pe2(int k)  k = 1..kn+1        void emit(int k, float v)
+//   float next_edge(int k) -> pe2(k+1) or 0 when k+1 > kn+1
+template <class Col>
+FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
+{
+    // window state E_L: q(L..L+3), dp(L..L+3), pe1(L..L+4), dc(L..L+2), ALraw(L..L+2), h2(L-1..L+1)
+    float qv[4], dpv[4], pev[5], dcv[3], alv[3], h2v[3];
+    float ar_km = 0.0f;
+    const bool huynh = kord >= 7;
+
+    // prologue (levels 1..4 exist because km >= 4)
+    for (int i = 0; i < 4; ++i) qv[i] = c.q1(1 + i);
+    for (int i = 0; i < 5; ++i) pev[i] = c.pe1(1 + i);
+    for (int i = 0; i < 4; ++i) dpv[i] = pev[i + 1] - pev[i];
+
+    const ColumnEnds ends{pev[0], c.pe1(km + 1), qv[0], c.q1(km)};
+
+    float dc1, dc2, dc3, al1, al2, al3;
+    dc2 = ppm_dc(qv[0], qv[1], qv[2], dpv[0], dpv[1], dpv[2]);
+    dc3 = ppm_dc(qv[1], qv[2], qv[3], dpv[1], dpv[2], dpv[3]);  // 3 <= km-1
+    al3 = ppm_al(dpv[0], dpv[1], dpv[2], dpv[3], qv[1], qv[2], dc2, dc3);
+    {   // top: area-preserving cubic (mappm.f90:689-725)
+        const float d1 = dpv[0], d2 = dpv[1];
+        const float q1 = qv[0], q2 = qv[1];
+        const float qm = (d2 * q1 + d1 * q2) / (d1 + d2);
+        const float dq = 2.0f * (q2 - q1) / (d1 + d2);
+        const float c1 = 4.0f * (al3 - qm - d2 * dq) / (d2 * (2.0f * d2 * d2 + d1 * (d2 + 3.0f * d1)));
+        const float c3 = dq - 0.5f * c1 * (d2 * (5.0f * d1 + d2) - 3.0f * d1 * d1);
+        al2 = qm - 0.25f * c1 * d1 * d2 * (d2 + 3.0f * d1);
+        al1 = d1 * (2.0f * c1 * (d1 * d1) - c3) + al2;
+        al2 = fmax2(al2, fmin2(q1, q2));
+        al2 = fmin2(al2, fmax2(q1, q2));
+        dc1 = 0.5f * (al2 - q1);
+        if (iv == 0) {
+            al1 = fmax2(0.0f, al1);
+            al2 = fmax2(0.0f, al2);
+        } else if (iv == -1) {
+            if (al1 * q1 <= 0.0f) al1 = 0.0f;
+        } else if (iv == 2 || iv == -2) {
+            al1 = q1;
+        }
+    }
+    dcv[0] = dc1; dcv[1] = dc2; dcv[2] = dc3;
+    alv[0] = al1; alv[1] = al2; alv[2] = al3;
+    h2v[0] = 0.0f; h2v[1] = 0.0f;
+    h2v[2] = huynh ? ppm_h2(dc1, dc3, dpv[0], dpv[1], dpv[2]) : 0.0f;  // h2(2)
+
+    int lmt = kord - 3;
+    lmt = lmt > 0 ? lmt : 0;
+    if (iv == 0) lmt = lmt < 2 ? lmt : 2;
+
+    RemapState s{1, false, 0.0f, 0.0f, c.pe2(1), c.pe2(2)};
+
+    for (int L = 1; L <= km; ++L) {
+        // ---- emit the final coefficients of layer L ----
+        Ppm a{qv[0], alv[0], (L < km) ? alv[1] : ar_km, 0.0f};
+        const float dcL = dcv[0];
+        if (L <= 2 || L >= km - 1) {
+            a.a6 = a6_of(a);
+            ppm_limit(dcL, a, 0);
+        } else if (huynh) {
+            ppm_huynh(a, dcL, h2v[0], h2v[2]);
+            if (iv == 0) ppm_limit(dcL, a, 2);
+        } else {
+            if (kord != 4) a.a6 = a6_of(a);
+            if (kord != 6) ppm_limit(dcL, a, lmt);
+        }
+        const LayerView v{pev[0], pev[1], dpv[0], qv[0], a};
+        remap_layer(s, v, ends, kn, c);
+
+        if (L == km) break;
+        // ---- advance the window E_L -> E_{L+1} ----
+        const int j = L + 4;  // level to ingest
+        float qn = 0.0f, pen = 0.0f, dpn = 0.0f;
+        if (j <= km) {
+            qn = c.q1(j);
+            pen = c.pe1(j + 1);
+            dpn = pen - pev[4];
+        }
+        const int m = L + 3;  // dc(m), ALraw(m)
+        float dcm = 0.0f, alm = 0.0f;
+        if (m <= km - 1) {
+            dcm = ppm_dc(qv[2], qv[3], qn, dpv[2], dpv[3], dpn);
+            alm = ppm_al(dpv[1], dpv[2], dpv[3], dpn, qv[2], qv[3], dcv[2], dcm);
+        } else if (m == km) {
+            // bottom: area-preserving cubic (mappm.f90:729-761)
+            const float d1 = dpv[3], d2 = dpv[2];
+            const float qk = qv[3], qk1 = qv[2];
+            const float qm = (d2 * qk + d1 * qk1) / (d1 + d2);
+            const float dq = 2.0f * (qk1 - qk) / (d1 + d2);
+            const float c1 = (alv[2] - qm - d2 * dq) / (d2 * (2.0f * d2 * d2 + d1 * (d2 + 3.0f * d1)));
+            const float c3 = dq - 2.0f * c1 * (d2 * (5.0f * d1 + d2) - 3.0f * d1 * d1);
+            alm = qm - c1 * d1 * d2 * (d2 + 3.0f * d1);
+            float ar = d1 * (8.0f * c1 * (d1 * d1) - c3) + alm;
+            alm = fmax2(alm, fmin2(qk, qk1));
+            alm = fmin2(alm, fmax2(qk, qk1));
+            dcm = 0.5f * (qk - alm);
+            if (iv == 0) {
+                alm = fmax2(0.0f, alm);
+                ar = fmax2(0.0f, ar);
+            } else if (iv < 0) {
+                if (qk * ar <= 0.0f) ar = 0.0f;
+            }
+            ar_km = ar;
+        }
+        float h2n = 0.0f;  // h2(L+2)
+        if (huynh && L + 2 <= km - 1) h2n = ppm_h2(dcv[1], dcm, dpv[1], dpv[2], dpv[3]);
+
+        qv[0] = qv[1]; qv[1] = qv[2]; qv[2] = qv[3]; qv[3] = qn;
+        dpv[0] = dpv[1]; dpv[1] = dpv[2]; dpv[2] = dpv[3]; dpv[3] = dpn;
+        pev[0] = pev[1]; pev[1] = pev[2]; pev[2] = pev[3]; pev[3] = pev[4]; pev[4] = pen;
+        dcv[0] = dcv[1]; dcv[1] = dcv[2]; dcv[2] = dcm;
+        alv[0] = alv[1]; alv[1] = alv[2]; alv[2] = alm;
+        h2v[0] = h2v[1]; h2v[1] = h2v[2]; h2v[2] = h2n;
+    }
+    remap_finish(s, ends, kn, c);
+}
+
+// ---- one column, kord > 7 (cs_profile path) ----
+//
+// `Scr` is per-column scratch of 2*(km+2) floats: edge(k) for k = 1..km+1 and
+// gam(k), addressed by scr.e(k) / scr.g(k) (LDS on the device).
+template <class Col, class Scr>
+FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int kord)
+{
+    const int akord = kord < 0 ? -kord : kord;
+    const float qs = 0.0f;  // mappm passes an uninitialised qs (mappm.f90:33,49)
+
+    // ---- tridiagonal edge solve (mappm.f90:153-205): forward sweep into scratch ----
+    {
+        float qm1 = c.q1(1), pe0 = c.pe1(1), pe1v = c.pe1(2);
+        float dpm1 = pe1v - pe0;
+        if (iv == -2) {
+            scr.g(2) = 0.5f;
+            float qprev = 1.5f * qm1;
+            scr.e(1) = qprev;
+            float gk = 0.5f;  // gam(k)
+            float pek = pe1v;
+            for (int k = 2; k <= km - 1; ++k) {
+                const float qk = c.q1(k);
+                const float pen = c.pe1(k + 1);
+                const float dpk = pen - pek;
+                const float grat = dpm1 / dpk;
+                const float bet = 2.0f + grat + grat - gk;
+                qprev = (3.0f * (qm1 + qk) - qprev) / bet;
+                scr.e(k) = qprev;
+                gk = grat / bet;
+                scr.g(k + 1) = gk;
+                qm1 = qk; dpm1 = dpk; pek = pen;
+            }
+            const float qkm = c.q1(km);
+            const float dpkm = c.pe1(km + 1) - pek;
+            const float grat = dpm1 / dpkm;
+            qprev = (3.0f * (qm1 + qkm) - grat * qs - qprev) / (2.0f + grat + grat - gk);
+            scr.e(km) = qprev;
+            scr.e(km + 1) = qs;
+            float qn = qprev;
+            for (int k = km - 1; k >= 1; --k) {
+                qn = scr.e(k) - scr.g(k + 1) * qn;
+                scr.e(k) = qn;
+            }
+        } else {
+            float q2v = c.q1(2);
+            float pe2v = c.pe1(3);
+            float dp2 = pe2v - pe1v;
+            float grat = dp2 / dpm1;
+            float bet = grat * (grat + 0.5f);
+            float qprev = ((grat + grat) * (grat + 1.0f) * qm1 + q2v) / bet;
+            float gprev = (1.0f + grat * (grat + 1.5f)) / bet;
+            scr.e(1) = qprev;
+            scr.g(1) = gprev;
+            float d4 = 0.0f;
+            float pek = pe1v;
+            float qkm1 = qm1;
+            float qk = qm1;
+            for (int k = 2; k <= km; ++k) {
+                qk = c.q1(k);
+                const float pen = c.pe1(k + 1);
+                const float dpk = pen - pek;
+                d4 = dpm1 / dpk;
+                bet = 2.0f + d4 + d4 - gprev;
+                qprev = (3.0f * (qkm1 + d4 * qk) - qprev) / bet;
+                gprev = d4 / bet;
+                scr.e(k) = qprev;
+                scr.g(k) = gprev;
+                qkm1 = qk; dpm1 = dpk; pek = pen;
+            }
+            // qkm1 == qk == q(km) here; need q(km-1)
+            const float a_bot = 1.0f + d4 * (d4 + 1.5f);
+            const float qkmm1 = c.q1(km - 1);
+            float qn = (2.0f * d4 * (d4 + 1.0f) * qk + qkmm1 - a_bot * qprev) / (d4 * (d4 + 0.5f) - a_bot * gprev);
+            scr.e(km + 1) = qn;
+            for (int k = km; k >= 1; --k) {
+                qn = scr.e(k) - scr.g(k) * qn;
+                scr.e(k) = qn;
+            }
+        }
+    }
+
+    const ColumnEnds ends{c.pe1(1), c.pe1(km + 1), c.q1(1), c.q1(km)};
+    RemapState s{1, false, 0.0f, 0.0f, c.pe2(1), c.pe2(2)};
+
+    // constrained edge qc(k) (mappm.f90:207-260) from the solved edge e(k) and
+    // q1(k-2..k+1); the large-scale constraints use gam(k) = q1(k) - q1(k-1).
+    auto edge_c = [&](int k, float qkm2, float qkm1, float qk0, float qkp1) -> float {
+        float q = scr.e(k);
+        if (akord > 16 || k <= 1 || k >= km + 1) return q;
+        if (k == 2 || k == km) {
+            q = fmin2(q, fmax2(qkm1, qk0));
+            q = fmax2(q, fmin2(qkm1, qk0));
+        } else {
+            const float gm = qkm1 - qkm2;  // gam(k-1)
+            const float gp = qkp1 - qk0;   // gam(k+1)
+            if (gm * gp > 0.0f) {
+                q = fmin2(q, fmax2(qkm1, qk0));
+                q = fmax2(q, fmin2(qkm1, qk0));
+            } else if (gm > 0.0f) {
+                q = fmax2(q, fmin2(qkm1, qk0));
+            } else {
+                q = fmin2(q, fmax2(qkm1, qk0));
+                if (iv == 0) q = fmax2(0.0f, q);
+            }
+        }
+        return q;
+    };
+    auto q1_or0 = [&](int k) -> float { return (k >= 1 && k <= km) ? c.q1(k) : 0.0f; };
+
+    // rolling windows at layer L: qw[i] = q1(L-2+i) (i=0..5), qcw[i] = qc(L-1+i) (i=0..3)
+    float qw[6], qcw[4];
+    for (int i = 0; i < 6; ++i) qw[i] = q1_or0(i - 1);
+    qcw[0] = 0.0f;
+    qcw[1] = edge_c(1, 0.0f, 0.0f, qw[2], qw[3]);
+    qcw[2] = edge_c(2, 0.0f, qw[2], qw[3], qw[4]);
+    qcw[3] = edge_c(3, qw[2], qw[3], qw[4], qw[5]);
+    float pl0 = c.pe1(1), pl1 = c.pe1(2);
+
+    for (int L = 1; L <= km; ++L) {
+        Ppm a{qw[2], qcw[1], qcw[2], 0.0f};
+        if (akord > 16) {
+            a.a6 = a6_of(a);  // perfectly linear scheme (mappm.f90:207-216)
+        } else {
+            // subgrid flags of layers L-1, L, L+1 (mappm.f90:269-288): index i = 0,1,2
+            bool extm[3], ext5[3], ext6[3];
+            for (int i = 0; i < 3; ++i) {
+                const int k = L - 1 + i;
+                const float qkm = qw[i], qk = qw[i + 1], qkp = qw[i + 2];
+                const float ql = qcw[i], qr = qcw[i + 1];
+                if (k == 1 || k == km)
+                    extm[i] = (ql - qk) * (qr - qk) > 0.0f;
+                else
+                    extm[i] = (qk - qkm) * (qkp - qk) < 0.0f;
+                const float x0 = 2.0f * qk - (ql + qr);
+                const float x1 = fabsf(ql - qr);
+                ext5[i] = fabsf(x0) > x1;
+                ext6[i] = fabsf(3.0f * x0) > x1;
+            }
+            const float g_m1 = qw[1] - qw[0];  // gam(L-1)
+            const float g_0 = qw[2] - qw[1];   // gam(L)
+            const float g_p1 = qw[3] - qw[2];  // gam(L+1)
+            const float g_p2 = qw[4] - qw[3];  // gam(L+2)
+            auto huynh_l = [&]() {
+                const float pmp_1 = a.a1 - 2.0f * g_p1;
+                const float lac_1 = pmp_1 + 1.5f * g_p2;
+                a.al = fmin2(fmax2(a.al, fmin3(a.a1, pmp_1, lac_1)), fmax3(a.a1, pmp_1, lac_1));
+            };
+            auto huynh_r = [&]() {
+                const float pmp_2 = a.a1 + 2.0f * g_0;
+                const float lac_2 = pmp_2 - 1.5f * g_m1;
+                a.ar = fmin2(fmax2(a.ar, fmin3(a.a1, pmp_2, lac_2)), fmax3(a.a1, pmp_2, lac_2));
+            };
+            auto a6_alt = [&]() { a.a6 = 6.0f * a.a1 - 3.0f * (a.al + a.ar); };
+            auto flat = [&]() { a.al = a.a1; a.ar = a.a1; };
+
+            if (L == 1) {
+                if (iv == 0) {
+                    a.al = fmax2(0.0f, a.al);
+                } else if (iv == -1) {
+                    if (a.al * a.a1 <= 0.0f) a.al = 0.0f;
+                } else if (iv == 2) {
+                    a.al = a.a1; a.ar = a.a1; a.a6 = 0.0f;
+                }
+                if (iv != 2) {
+                    a.a6 = a6_of(a);
+                    cs_limit(extm[1], a, 1);
+                }
+            } else if (L == 2) {
+                a.a6 = a6_of(a);
+                cs_limit(extm[1], a, 2);
+            } else if (L <= km - 2) {
+                // Huynh's 2nd constraint for the interior (mappm.f90:328-504)
+                if (akord < 9) {
+                    huynh_l(); huynh_r(); a.a6 = a6_of(a);
+                } else if (akord == 9) {
+                    if ((extm[1] && extm[0]) || (extm[1] && extm[2])) {
+                        flat(); a.a6 = 0.0f;
+                    } else {
+                        a6_alt();
+                        if (fabsf(a.a6) > fabsf(a.al - a.ar)) { huynh_l(); huynh_r(); a6_alt(); }
+                    }
+                } else if (akord == 10) {
+                    if (ext5[1]) {
+                        if (ext5[0] || ext5[2]) flat();
+                        else if (ext6[0] || ext6[2]) { huynh_l(); huynh_r(); }
+                    } else if (ext6[1]) {
+                        if (ext5[0] || ext5[2]) { huynh_l(); huynh_r(); }
+                    }
+                    a.a6 = a6_of(a);
+                } else if (akord == 12) {
+                    if (extm[1]) {
+                        flat(); a.a6 = 0.0f;
+                    } else {
+                        a6_alt();
+                        if (fabsf(a.a6) > fabsf(a.al - a.ar)) { huynh_l(); huynh_r(); a6_alt(); }
+                    }
+                } else if (akord == 13) {
+                    if (ext6[1] && ext6[0] && ext6[2]) flat();
+                    a.a6 = a6_of(a);
+                } else if (akord == 14) {
+                    a.a6 = a6_of(a);
+                } else if (akord == 15) {
+                    if (ext5[1]) {
+                        if (ext5[0] || ext5[2]) flat();
+                    } else if (ext6[1]) {
+                        huynh_l(); huynh_r();
+                    }
+                    a.a6 = a6_of(a);
+                } else if (akord == 16) {
+                    if (ext5[1]) {
+                        if (ext5[0] || ext5[2]) flat();
+                        else if (ext6[0] || ext6[2]) { huynh_l(); huynh_r(); }
+                    }
+                    a.a6 = a6_of(a);
+                } else {  // kord = 11
+                    if (ext5[1] && (ext5[0] || ext5[2])) {
+                        flat(); a.a6 = 0.0f;
+                    } else {
+                        a.a6 = a6_of(a);
+                    }
+                }
+                if (iv == 0) cs_limit(extm[1], a, 0);
+            } else if (L == km - 1) {
+                a.a6 = a6_of(a);
+                cs_limit(extm[1], a, 2);
+            } else {  // L == km (mappm.f90:514-530)
+                if (iv == 0) {
+                    a.ar = fmax2(0.0f, a.ar);
+                } else if (iv == -1) {
+                    if (a.ar * a.a1 <= 0.0f) a.ar = 0.0f;
+                }
+                a.a6 = a6_of(a);
+                cs_limit(extm[1], a, 1);
+            }
+        }
+        const LayerView v{pl0, pl1, pl1 - pl0, qw[2], a};
+        remap_layer(s, v, ends, kn, c);
+        if (L == km) break;
+        for (int i = 0; i < 5; ++i) qw[i] = qw[i + 1];
+        qw[5] = q1_or0(L + 4);
+        for (int i = 0; i < 3; ++i) qcw[i] = qcw[i + 1];
+        qcw[3] = (L + 3 <= km + 1) ? edge_c(L + 3, qw[2], qw[3], qw[4], qw[5]) : 0.0f;
+        pl0 = pl1;
+        pl1 = c.pe1(L + 2);
+    }
+    remap_finish(s, ends, kn, c);
+}
+
+}  // namespace fv3

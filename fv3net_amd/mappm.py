@@ -1,0 +1,61 @@
+"""Drop-in for the reference's f2py ``mappm`` module plus a device-resident API.
+
+Reference: ``external/mappm/mappm/__init__.py`` exports ``mappm`` (and
+``interpolate_2d``) compiled from ``mappm.f90``; ``vcm.cubedsphere.regridz``
+calls ``mappm.mappm(p_in, f_in, p_out, 1, n_columns, iv, kord, dummy_ptop)``
+with C-ordered ``(ncol, nlev)`` float64 arrays and gets ``(ncol, kn)`` float32
+back (``regridz.py:268-275``, dtype pinned by ``tests/test_mappm.py:14,28,42``).
+"""
+import numpy as np
+
+from . import _device, _native
+
+try:
+    import torch
+except ImportError:  # pragma: no cover
+    torch = None
+
+
+def mappm_device(pe1, q1, pe2, iv: int = 1, kord: int = 1, out=None, stream=None):
+    """Remap on device.  ``pe1 [km+1, ncol]``, ``q1 [km, ncol]``, ``pe2 [kn+1, ncol]``
+    float32 CUDA tensors (column fastest, the Fortran pe1(i,k) order); returns
+    ``q2 [kn, ncol]``.  Asynchronous on the current stream."""
+    _device.require_gpu()
+    pe1 = _device.to_device_f32(pe1)
+    q1 = _device.to_device_f32(q1)
+    pe2 = _device.to_device_f32(pe2)
+    if pe1.dim() != 2 or q1.dim() != 2 or pe2.dim() != 2:
+        raise ValueError("pe1, q1, pe2 must be 2-D [level, column]")
+    km, ncol = q1.shape
+    kn = pe2.shape[0] - 1
+    if pe1.shape[0] != km + 1:
+        raise ValueError("f_in must have a vertical dimension one shorter than p_in")
+    if pe1.shape[1] != ncol or pe2.shape[1] != ncol:
+        raise ValueError("All dimensions except vertical must be same size for p_in, f_in and p_out")
+    if out is None:
+        out = torch.empty((kn, ncol), dtype=torch.float32, device=q1.device)
+    lib = _native.load()
+    st = lib.fv3_mappm(
+        _device.ptr(pe1), _device.ptr(q1), _device.ptr(pe2), _device.ptr(out), ncol, km, kn,
+        int(iv), int(kord), 0.0, _device.stream_handle(stream),
+    )
+    _native.check(st, "mappm")
+    return out
+
+
+def mappm(pe1, q1, pe2, i1, i2, iv, kord, ptop):
+    """f2py-compatible signature of ``mappm.mappm`` (mappm.f90:10).
+
+    ``pe1 (ncol, km+1)``, ``q1 (ncol, km)``, ``pe2 (ncol, kn+1)`` host arrays; columns
+    ``i1..i2`` (1-based, inclusive) are remapped; returns float32 ``(i2-i1+1, kn)``.
+    """
+    i1 = int(i1)
+    i2 = int(i2)
+    pe1 = np.asarray(pe1, dtype=np.float32)
+    q1 = np.asarray(q1, dtype=np.float32)
+    pe2 = np.asarray(pe2, dtype=np.float32)
+    if pe1.ndim != 2 or q1.ndim != 2 or pe2.ndim != 2:
+        raise ValueError("mappm expects 2-D (column, level) arrays")
+    sl = slice(i1 - 1, i2)
+    res = mappm_device(pe1[sl].T, q1[sl].T, pe2[sl].T, iv=int(iv), kord=int(kord))
+    return res.T.contiguous().cpu().numpy()

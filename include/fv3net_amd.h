@@ -1,0 +1,143 @@
+/*
+ * fv3net_amd — MI355X (gfx950) C ABI for fv3net's per-timestep ML-physics hot path.
+ *
+ * Plain C, no torch or HIP types: pointers are DEVICE pointers (hipMalloc'd or
+ * torch CUDA tensors), `stream` is a hipStream_t passed as void* (NULL = default
+ * stream).  Every call is asynchronous on `stream` and returns an int status
+ * (FV3_OK = 0); on failure the message is in fv3_last_error() (thread-local).
+ * Nothing throws across this boundary.
+ *
+ * Reference interfaces each entry point replaces (paths under /root/reference):
+ *   fv3_mappm*            external/mappm/mappm/mappm.f90:10  (f2py `mappm.mappm(pe1, q1,
+ *                         pe2, i1, i2, iv, kord, ptop)`, bound at
+ *                         external/vcm/vcm/cubedsphere/regridz.py:273)
+ *   fv3_dense_*           the Keras predict of a DenseModel:
+ *                         external/fv3fit/fv3fit/keras/_models/shared/pure_keras.py:112
+ *                         (graph built in external/fv3fit/fv3fit/keras/_models/dense.py:234-305)
+ *   fv3_regrid_coarsen    external/vcm/vcm/cubedsphere/regridz.py:25-55 + 115-161 fused with
+ *                         external/vcm/vcm/cubedsphere/coarsen.py:183-218
+ *                         (as orchestrated by coarsen_restarts.py:411-516, 840-887)
+ *   fv3_column_reduce     per-rank partial sums behind
+ *                         workflows/prognostic_c48_run/runtime/metrics.py:18-32
+ */
+#ifndef FV3NET_AMD_H
+#define FV3NET_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FV3_OK 0
+#define FV3_ERR_INVALID 1     /* bad argument (shape, size, NULL) */
+#define FV3_ERR_HIP 2         /* HIP runtime failure */
+#define FV3_ERR_UNSUPPORTED 3 /* valid request this build does not implement */
+
+const char* fv3_last_error(void);
+int fv3_abi_version(void); /* bumped on any signature change */
+
+/*
+ * Column layout of a [level, column] field.  Element (column c, level k) lives at
+ *     base[(c / ncol_blk) * blk_stride + k * ld + (c % ncol_blk)]
+ * A plain [level][ncol] array is {ncol, ncol, 0}; a (tile, z, y, x) restart or
+ * prognostic-state array is {ny*nx, ny*nx, nz*ny*nx}, i.e. the stacked sample
+ * index of fv3fit's stack() is a zero-copy view (external/fv3fit/fv3fit/_shared/stacking.py:12-27).
+ */
+typedef struct {
+    int64_t ncol_blk;
+    int64_t ld;
+    int64_t blk_stride;
+} fv3_layout;
+
+/* ---- vertical remap: mappm.f90:10-126 ----------------------------------------
+ * pe1 [km+1][ncol] input edge pressures (top -> surface), q1 [km][ncol] layer means,
+ * pe2 [kn+1][ncol] output edges, q2 [kn][ncol] result.  float32, column fastest
+ * (exactly the Fortran pe1(i,k) order).  iv, kord as in the reference; ptop is
+ * accepted and ignored, as in the reference (regridz.py:270).  km >= 4. */
+int fv3_mappm(const float* pe1, const float* q1, const float* pe2, float* q2, int64_t ncol,
+              int km, int kn, int iv, int kord, float ptop, void* stream);
+
+/* Same with an explicit layout per array (e.g. (tile, z, y, x) data in place). */
+int fv3_mappm_ex(const float* pe1, fv3_layout pe1_l, const float* q1, fv3_layout q1_l,
+                 const float* pe2, fv3_layout pe2_l, float* q2, fv3_layout q2_l, int64_t ncol,
+                 int km, int kn, int iv, int kord, float ptop, void* stream);
+
+/* ---- dense column model: DenseModel predict graph (dense.py:234-305) ----------
+ * inputs -> per-input clip (clip.py:65-83) -> StandardNormLayer (x-mean)/(sigma+eps)
+ * (emulation/layers/normalization.py:121-139) -> concat (utils.py:65-86) ->
+ * n_hidden x Dense(width, relu) (dense_network.py:59-76) -> one linear Dense(out_nz)
+ * per output (dense.py:259-264) -> StandardDenormLayer y*sigma+mean
+ * (normalization.py:142-149) -> OutputLimit clamp (output_limit.py:29-47) ->
+ * zero mask of clipped levels (clip.py:33-46).  All host pointers; the model
+ * copies what it needs to the device at create time and is immutable after. */
+typedef struct {
+    int n_in;                          /* input variables, <= 16 */
+    const int* in_nz;                  /* [n_in] levels per input variable */
+    const int* in_clip;                /* [n_in][2] {start, stop} kept levels, or NULL = all */
+    const float* in_mean;              /* [k_in] k_in = sum of kept levels */
+    const float* in_sigma;             /* [k_in] population std (normalization.py:90-94) */
+    float epsilon;                     /* StandardNormLayer epsilon (1e-7) */
+    int width;                         /* hidden width, <= 256 */
+    int n_hidden;                      /* hidden Dense(relu) layers (= depth - 1), >= 1 */
+    const float* const* hidden_kernel; /* [n_hidden] -> [fan_in][width] (Keras kernel order) */
+    const float* const* hidden_bias;   /* [n_hidden] -> [width] */
+    int n_out;                         /* output variables, <= 16 */
+    const int* out_nz;                 /* [n_out] */
+    const float* const* out_kernel;    /* [n_out] -> [width][out_nz] */
+    const float* const* out_bias;      /* [n_out] -> [out_nz] */
+    const float* out_mean;             /* [k_out] StandardDenormLayer mean */
+    const float* out_sigma;            /* [k_out] StandardDenormLayer sigma */
+    const float* out_min;              /* [k_out] or NULL; -inf = no lower limit */
+    const float* out_max;              /* [k_out] or NULL; +inf = no upper limit */
+    const float* out_mask;             /* [k_out] or NULL; 0/1 zero-mask of clipped levels */
+} fv3_dense_desc;
+
+typedef struct fv3_dense_model fv3_dense_model;
+
+int fv3_dense_create(const fv3_dense_desc* desc, fv3_dense_model** out);
+int fv3_dense_destroy(fv3_dense_model* model);
+int fv3_dense_k_in(const fv3_dense_model* model);
+int fv3_dense_k_out(const fv3_dense_model* model);
+
+/* Forward over ncol columns.  inputs[v] is input variable v (all of its in_nz[v]
+ * levels) with layout in_l[v]; outputs[o] receives out_nz[o] levels.  All
+ * layouts must share ncol_blk.  Synchronous-free: enqueued on `stream`. */
+int fv3_dense_forward(const fv3_dense_model* model, const float* const* inputs,
+                      const fv3_layout* in_l, float* const* outputs, const fv3_layout* out_l,
+                      int64_t ncol, void* stream);
+
+/* ---- fused pressure-level coarse-graining (config #3) ----------------------------
+ * For every coarse cell (factor x factor fine columns of a tile):
+ *   delp_c = sum(delp*area)/sum(area)                     (coarsen.py:183-218)
+ *   phalf_f = cumsum([ptop_toa, delp_f]), phalf_c likewise  (vertically_dependent.py:41-66)
+ *   f_r = mappm(phalf_f, f, phalf_c_on_f, iv, kord)        (regridz.py:164-279)
+ *   w = area if phalf_c[k+1] < phalf_f[km+1] else 0        (regridz.py:150-161)
+ *   out = sum(f_r*w)/sum(w) per level                      (coarsen.py:183-218)
+ * delp, fields: (tile, km, ny, nx) float32; area (tile, ny, nx); out (tile, km, ny/f, nx/f);
+ * delp_out (tile, km, ny/f, nx/f) receives delp_c (area-weighted, not masked).
+ * phalf is accumulated in float64 and rounded once (bit-exact to the reference
+ * running on float64 restart data). */
+int fv3_regrid_coarsen(const float* delp, const float* area, const float* const* fields,
+                       float* const* out, int n_fields, float* delp_out, int ntile, int km,
+                       int ny, int nx, int factor, int iv, int kord, double ptop_toa,
+                       void* stream);
+
+/* ---- per-column reductions for stepper diagnostics --------------------------------
+ * out[c] = sum_k field[k][c] * delp[k][c] * scale  (vcm mass_integrate,
+ * external/vcm/vcm/calc/thermo/vertically_dependent.py:18-22, with scale = 1/g),
+ * accumulated in float64, written as float32. */
+int fv3_column_integral(const float* field, fv3_layout field_l, const float* delp,
+                        fv3_layout delp_l, float* out, int64_t ncol, int km, double scale,
+                        void* stream);
+
+/* Area-weighted global partial sums: partial[2*d+0] = sum(area*x_d), partial[2*d+1] =
+ * sum(area) in float64, over ncol columns, for n_diag 2-D diagnostics x_d (each [ncol]).
+ * Deterministic (fixed reduction tree).  metrics.py:18-24 partials. */
+int fv3_area_weighted_sums(const float* const* diags, int n_diag, const float* area,
+                           int64_t ncol, double* partial, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FV3NET_AMD_H */

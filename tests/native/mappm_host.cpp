@@ -1,0 +1,40 @@
+// TEST-ONLY host build of the product's streaming mappm (fv3net_amd/csrc/mappm_core.h).
+// Lets the CPU test suite check the one-pass algorithm bit-for-bit against the
+// oracle without a GPU.  Not part of the product library and never loaded by it.
+#include <cstdint>
+#include <vector>
+#include "../../fv3net_amd/csrc/mappm_core.h"
+
+namespace {
+struct Col {
+    const float *pe1_, *q1_, *pe2_;
+    float* q2_;
+    int64_t ncol, i;
+    int kn;
+    float q1(int k) const { return q1_[(int64_t)(k - 1) * ncol + i]; }
+    float pe1(int k) const { return pe1_[(int64_t)(k - 1) * ncol + i]; }
+    float pe2(int k) const { return pe2_[(int64_t)(k - 1) * ncol + i]; }
+    void emit(int k, float v) { q2_[(int64_t)(k - 1) * ncol + i] = v; }
+    float next_edge(int k) const { return (k + 1 <= kn + 1) ? pe2(k + 1) : 0.0f; }
+};
+struct Scr {
+    std::vector<float> ev, gv;
+    float& e(int k) { return ev[k]; }
+    float& g(int k) { return gv[k]; }
+};
+}  // namespace
+
+extern "C" int host_mappm(int km, const float* pe1, const float* q1, int kn, const float* pe2,
+                          float* q2, int64_t ncol, int iv, int kord)
+{
+    if (km < 4 || kn < 1) return -1;
+    Scr scr{std::vector<float>(km + 3), std::vector<float>(km + 3)};
+    for (int64_t i = 0; i < ncol; ++i) {
+        Col c{pe1, q1, pe2, q2, ncol, i, kn};
+        if (kord > 7)
+            fv3::mappm_cs_column(c, scr, km, kn, iv, kord);
+        else
+            fv3::mappm_ppm_column(c, km, kn, iv, kord);
+    }
+    return 0;
+}

@@ -1,0 +1,145 @@
+"""GPU parity tests for the HIP mappm (through the C ABI) against the reference
+golden vectors (flang build of mappm.f90) and the C oracle.  Bar: bit-exact.
+
+Reference: external/mappm/mappm/mappm.f90:10-126; KATs external/vcm/tests/test_mappm.py.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle.mappm import oracle_mappm
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits_equal(a, b):
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+    return bool(same.all())
+
+
+def test_reference_kats_through_f2py_signature(gpu):
+    from fv3net_amd import mappm as mappm_mod
+
+    # test_mappm.py:5-16
+    r = mappm_mod.mappm(np.asarray([0.0, 1.0, 2.0, 3.0, 4.0, 5.0])[None, :],
+                        np.asarray([0.0, 1.0, 2.0, 3.0, 4.0])[None, :],
+                        np.asarray([0.5, 1.2, 2.4, 2.8, 3.2, 4.5])[None, :], 1, 1.0, 1.0, 1.0, 0.0)
+    assert r.dtype == np.float32 and r.shape == (1, 5)
+    np.testing.assert_almost_equal(r, np.asarray([[0.35, 1.3, 2.1, 2.5, 3.35]], np.float32), decimal=5)
+    # test_mappm.py:19-30
+    r = mappm_mod.mappm(np.asarray([1.0, 2.0, 3.0, 4.0, 5.0])[None, :],
+                        np.asarray([1.5, 2.5, 3.5, 4.5])[None, :],
+                        np.asarray([0.0, 2.5, 3.5, 4.5, 50.0])[None, :], 1, 1.0, 1.0, 1.0, 0.0)
+    np.testing.assert_almost_equal(r, np.asarray([[1.5, 3.0, 4.0, 4.502747]], np.float32), decimal=5)
+    # test_mappm.py:33-44
+    r = mappm_mod.mappm(np.asarray([1.0, 2.0, 3.0, 2.0, 5.0])[None, :],
+                        np.asarray([np.nan] * 4)[None, :],
+                        np.asarray([0.0, 2.5, 3.5, 4.5, 50.0])[None, :], 1, 1.0, 1.0, 1.0, 0.0)
+    assert np.isnan(r).all()
+
+
+def test_golden_vectors_bit_exact(gpu):
+    from fv3net_amd.mappm import mappm_device
+
+    g = np.load(os.path.join(GOLDEN, "mappm_golden.npz"))
+    for ci in range(len(g["cases"])):
+        pe1, pe2 = g[f"c{ci}_pe1"], g[f"c{ci}_pe2"]
+        for kord in g["kords"]:
+            for iv in g["ivs"]:
+                for qn in ("qs", "qr"):
+                    res = mappm_device(pe1, g[f"c{ci}_{qn}"], pe2, int(iv), int(kord)).cpu().numpy()
+                    assert _bits_equal(res, g[f"c{ci}_{qn}_k{kord}_iv{iv}"]), (ci, qn, kord, iv)
+    for kord in (1, 10):
+        res = mappm_device(g["c12_pe1"], g["c12_q"], g["c12_pe2"], 1, kord).cpu().numpy()
+        assert _bits_equal(res, g[f"c12_k{kord}_iv1"])
+
+
+def _columns(rng, km, kn, ncol):
+    delp = rng.uniform(1, 3000, (km, ncol)).astype(np.float32)
+    pe1 = np.concatenate([np.full((1, ncol), 300, np.float32), 300 + np.cumsum(delp, 0, dtype=np.float32)])
+    pe2 = np.sort(rng.uniform(pe1[0] * 0.8, pe1[-1] * 1.1, (kn + 1, ncol)), 0).astype(np.float32)
+    m = min(km, kn) + 1
+    pe2[: m // 2] = pe1[: m // 2]
+    pe2 = np.sort(pe2, 0)
+    q = (rng.normal(0, 1, (km, ncol)) * rng.choice([1e-4, 1, 300], (km, ncol))).astype(np.float32)
+    return pe1, q, pe2
+
+
+@pytest.mark.parametrize("km,kn,ncol", [(4, 3, 1), (5, 9, 257), (79, 50, 1000), (79, 79, 777), (127, 40, 300)])
+def test_random_vs_oracle_bit_exact(gpu, km, kn, ncol):
+    from fv3net_amd.mappm import mappm_device
+
+    rng = np.random.default_rng(km + kn + ncol)
+    pe1, q, pe2 = _columns(rng, km, kn, ncol)
+    for kord in (1, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17):
+        for iv in (0, 1, -1, 2):
+            res = mappm_device(pe1, q, pe2, iv, kord).cpu().numpy()
+            assert _bits_equal(res, oracle_mappm(pe1, q, pe2, iv, kord)), (kord, iv)
+
+
+def test_tile_layout_in_place(gpu):
+    """(tile, z, y, x) restart-shaped arrays remapped in place via fv3_mappm_ex."""
+    import torch
+
+    from fv3net_amd import _device, _native
+
+    rng = np.random.default_rng(7)
+    ntile, km, ny, nx = 6, 79, 12, 12
+    ncol = ntile * ny * nx
+    pe1, q, pe2 = _columns(rng, km, km, ncol)
+    # [lev, ncol] -> (tile, lev, y, x)
+    to_t = lambda a: np.ascontiguousarray(a.reshape(a.shape[0], ntile, ny * nx).transpose(1, 0, 2)
+                                          .reshape(ntile, a.shape[0], ny, nx))
+    dev = [_device.to_device_f32(to_t(a)) for a in (pe1, q, pe2)]
+    out = torch.empty((ntile, km, ny, nx), dtype=torch.float32, device="cuda")
+    lays = [_device.level_layout(t, 1)[0] for t in dev + [out]]
+    lib = _native.load()
+    st = lib.fv3_mappm_ex(dev[0].data_ptr(), lays[0], dev[1].data_ptr(), lays[1], dev[2].data_ptr(), lays[2],
+                          out.data_ptr(), lays[3], ncol, km, km, 1, 1, 0.0, _device.stream_handle())
+    _native.check(st)
+    got = out.cpu().numpy().reshape(ntile, km, ny * nx).transpose(1, 0, 2).reshape(km, ncol)
+    assert _bits_equal(got, oracle_mappm(pe1, q, pe2, 1, 1))
+
+
+def test_empty_and_errors(gpu):
+    import torch
+
+    from fv3net_amd.mappm import mappm_device
+
+    e = mappm_device(np.zeros((80, 0)), np.zeros((79, 0)), np.zeros((51, 0)))
+    assert tuple(e.shape) == (50, 0)
+    with pytest.raises(ValueError, match="one shorter"):
+        mappm_device(np.zeros((80, 3)), np.zeros((78, 3)), np.zeros((51, 3)))
+    with pytest.raises(ValueError, match="same size"):
+        mappm_device(np.zeros((80, 3)), np.zeros((79, 3)), np.zeros((51, 4)))
+    with pytest.raises(ValueError, match="km must be >= 4"):
+        mappm_device(np.zeros((4, 3)), np.zeros((3, 3)), np.zeros((4, 3)))
+    torch.cuda.synchronize()
+
+
+def test_c384_scale_sampled_bit_exact(gpu):
+    """BASELINE config #3 size (6*384*384 fine columns, 79->79): sampled columns
+    bit-exact against the oracle, plus whole-array finiteness."""
+    import torch
+
+    from fv3net_amd.mappm import mappm_device
+
+    rng = np.random.default_rng(384)
+    ncol, km = 6 * 384 * 384, 79
+    base = np.linspace(200, 1800, km, dtype=np.float32)[:, None]
+    delp = (base * rng.uniform(0.99, 1.01, (km, ncol))).astype(np.float32)
+    pe1 = np.concatenate([np.full((1, ncol), 300, np.float32), 300 + np.cumsum(delp, 0, dtype=np.float32)])
+    d2 = (base * rng.uniform(0.99, 1.01, (km, ncol))).astype(np.float32)
+    pe2 = np.concatenate([np.full((1, ncol), 300, np.float32), 300 + np.cumsum(d2, 0, dtype=np.float32)])
+    q = rng.normal(250, 10, (km, ncol)).astype(np.float32)
+    res = mappm_device(pe1, q, pe2, 1, 1)
+    torch.cuda.synchronize()
+    res = res.cpu().numpy()
+    assert np.isfinite(res).all()
+    idx = np.sort(rng.choice(ncol, 4096, replace=False))
+    ref = oracle_mappm(pe1[:, idx], q[:, idx], pe2[:, idx], 1, 1)
+    assert _bits_equal(res[:, idx], ref)

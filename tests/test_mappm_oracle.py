@@ -1,0 +1,136 @@
+"""CPU tests: pin the mappm oracle, and check the product's streaming algorithm
+(compiled for the host, test-only) against it.  No GPU needed.
+
+Reference KATs: external/vcm/tests/test_mappm.py:5-44.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+from oracle.mappm import oracle_mappm, reference_available, reference_mappm
+
+HOST_SRC = os.path.join(ROOT, "tests", "native", "mappm_host.cpp")
+HOST_SO = os.path.join(ROOT, "tests", "_build", "libmappm_host.so")
+
+
+def _bits_equal(a, b):
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+    return bool(same.all())
+
+
+# --- test_mappm.py KATs (values copied as data) ---------------------------------
+KATS = [
+    # (p_in, f_in, p_out, expected)  test_mappm.py:5-16, 19-30, 33-44
+    ([0.0, 1.0, 2.0, 3.0, 4.0, 5.0], [0.0, 1.0, 2.0, 3.0, 4.0], [0.5, 1.2, 2.4, 2.8, 3.2, 4.5],
+     [0.35, 1.3, 2.1, 2.5, 3.35]),
+    ([1.0, 2.0, 3.0, 4.0, 5.0], [1.5, 2.5, 3.5, 4.5], [0.0, 2.5, 3.5, 4.5, 50.0],
+     [1.5, 3.0, 4.0, 4.502747]),
+    ([1.0, 2.0, 3.0, 2.0, 5.0], [np.nan] * 4, [0.0, 2.5, 3.5, 4.5, 50.0], [np.nan] * 4),
+]
+
+
+@pytest.mark.parametrize("kat", KATS, ids=["identity", "out_of_bounds", "nans"])
+def test_oracle_reproduces_reference_kats(kat):
+    p_in, f_in, p_out, expected = (np.asarray(v, np.float64)[:, None] for v in kat)
+    res = oracle_mappm(p_in, f_in, p_out, iv=1, kord=1)
+    assert res.dtype == np.float32
+    np.testing.assert_almost_equal(res, expected.astype(np.float32), decimal=5)
+
+
+def test_oracle_matches_reference_golden_vectors():
+    g = np.load(os.path.join(GOLDEN, "mappm_golden.npz"))
+    n = 0
+    for ci in range(len(g["cases"])):
+        pe1, pe2 = g[f"c{ci}_pe1"], g[f"c{ci}_pe2"]
+        for kord in g["kords"]:
+            for iv in g["ivs"]:
+                for qn in ("qs", "qr"):
+                    res = oracle_mappm(pe1, g[f"c{ci}_{qn}"], pe2, int(iv), int(kord))
+                    assert _bits_equal(res, g[f"c{ci}_{qn}_k{kord}_iv{iv}"]), (ci, qn, kord, iv)
+                    n += 1
+    for kord in (1, 10):
+        res = oracle_mappm(g["c12_pe1"], g["c12_q"], g["c12_pe2"], 1, kord)
+        assert _bits_equal(res, g[f"c12_k{kord}_iv1"])
+    assert n == len(g["cases"]) * len(g["kords"]) * len(g["ivs"]) * 2
+
+
+@pytest.mark.skipif(not reference_available(), reason="reference flang build not present")
+@pytest.mark.parametrize("kord", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, -3])
+def test_oracle_matches_live_reference(kord):
+    rng = np.random.default_rng(kord + 100)
+    for iv in (0, 1, -1, 2, -2):
+        if iv == -2 and kord > 7:
+            continue  # reference reads an uninitialised qs (mappm.f90:33,49): UB
+        km, kn, ncol = 79, 50, 300
+        delp = rng.uniform(100, 2000, (km, ncol)).astype(np.float32)
+        pe1 = np.concatenate([np.full((1, ncol), 300, np.float32),
+                              300 + np.cumsum(delp, 0, dtype=np.float32)])
+        pe2 = np.sort(rng.uniform(pe1[0] * 0.9, pe1[-1] * 1.02, (kn + 1, ncol)), axis=0).astype(np.float32)
+        q = (rng.normal(0, 1, (km, ncol)) * rng.choice([1e-4, 1, 300], (km, ncol))).astype(np.float32)
+        assert _bits_equal(oracle_mappm(pe1, q, pe2, iv, kord), reference_mappm(pe1, q, pe2, iv, kord))
+
+
+# --- the product algorithm, host-compiled (test-only build) ----------------------
+@pytest.fixture(scope="module")
+def host_lib():
+    os.makedirs(os.path.dirname(HOST_SO), exist_ok=True)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+                    "-o", HOST_SO, HOST_SRC], check=True)
+    lib = ctypes.CDLL(HOST_SO)
+    lib.host_mappm.restype = ctypes.c_int
+    lib.host_mappm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                               ctypes.c_int]
+    return lib
+
+
+def _host(lib, pe1, q, pe2, iv, kord):
+    pe1, q, pe2 = (np.ascontiguousarray(a, np.float32) for a in (pe1, q, pe2))
+    out = np.empty((pe2.shape[0] - 1, q.shape[1]), np.float32)
+    rc = lib.host_mappm(q.shape[0], pe1.ctypes.data, q.ctypes.data, pe2.shape[0] - 1,
+                        pe2.ctypes.data, out.ctypes.data, q.shape[1], iv, kord)
+    assert rc == 0
+    return out
+
+
+def test_streaming_algorithm_matches_golden(host_lib):
+    g = np.load(os.path.join(GOLDEN, "mappm_golden.npz"))
+    for ci in range(len(g["cases"])):
+        pe1, pe2 = g[f"c{ci}_pe1"], g[f"c{ci}_pe2"]
+        for kord in g["kords"]:
+            for iv in g["ivs"]:
+                for qn in ("qs", "qr"):
+                    res = _host(host_lib, pe1, g[f"c{ci}_{qn}"], pe2, int(iv), int(kord))
+                    assert _bits_equal(res, g[f"c{ci}_{qn}_k{kord}_iv{iv}"]), (ci, qn, kord, iv)
+
+
+@pytest.mark.parametrize("kat", KATS, ids=["identity", "out_of_bounds", "nans"])
+def test_streaming_algorithm_kats(host_lib, kat):
+    p_in, f_in, p_out, expected = (np.asarray(v, np.float64)[:, None] for v in kat)
+    res = _host(host_lib, p_in, f_in, p_out, 1, 1)
+    np.testing.assert_almost_equal(res, expected.astype(np.float32), decimal=5)
+
+
+@pytest.mark.parametrize("km,kn", [(4, 3), (5, 9), (6, 2), (79, 79), (79, 50), (127, 40)])
+def test_streaming_algorithm_matches_oracle_random(host_lib, km, kn):
+    rng = np.random.default_rng(km * 1000 + kn)
+    for kord in (1, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17):
+        for iv in (0, 1, -1, 2):
+            ncol = 64
+            delp = rng.uniform(1, 3000, (km, ncol)).astype(np.float32)
+            pe1 = np.concatenate([np.full((1, ncol), 300, np.float32),
+                                  300 + np.cumsum(delp, 0, dtype=np.float32)])
+            pe2 = np.sort(rng.uniform(pe1[0] * 0.8, pe1[-1] * 1.1, (kn + 1, ncol)), 0).astype(np.float32)
+            # shared edges exercise the equality branches of the layer search
+            m = min(km, kn) + 1
+            pe2[: m // 2] = pe1[: m // 2]
+            pe2 = np.sort(pe2, 0)
+            q = (rng.normal(0, 1, (km, ncol)) * rng.choice([1e-4, 1, 300], (km, ncol))).astype(np.float32)
+            assert _bits_equal(_host(host_lib, pe1, q, pe2, iv, kord),
+                               oracle_mappm(pe1, q, pe2, iv, kord)), (kord, iv)
