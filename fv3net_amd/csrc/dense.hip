@@ -59,9 +59,9 @@ struct DenseArgs {
     const float* in_denom;  // [KP] f32(sigma + eps)
     const f32x4* w1;        // [KP/4][HT/4][64]
     const float* b1;        // [HP]
-    const f32x4* wh;        // [n_hidden-1][HP][HT/4][64]
+    const f32x4* wh;        // [n_hidden-1][HP/4][HT/4][64]
     const float* bh;        // [n_hidden-1][HP]
-    const f32x2* wo;        // [n_chunks][HP][64]
+    const f32x2* wo;        // [n_chunks][HP/4][64]
     const float* bo;        // [KOP]
     const float* o_sigma;   // [KOP]
     const float* o_mean;    // [KOP]
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256) void dense_forward_kernel(DenseArgs p)
     // ---- further hidden layers ----
     for (int l = 0; l < p.n_hidden_extra; ++l) {
         f32x4 g[HT];
-        hidden_layer<HT>(h, g, p.wh + (size_t)l * HP * (HT / 4) * 64, p.bh + (size_t)l * HP, lane, kr);
+        hidden_layer<HT>(h, g, p.wh + (size_t)l * (HP / 4) * (HT / 4) * 64, p.bh + (size_t)l * HP, lane, kr);
 #pragma unroll
         for (int m = 0; m < HT; ++m) h[m] = g[m];
     }
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) void dense_forward_kernel(DenseArgs p)
     for (int ch = 0; ch < p.n_chunks; ++ch) {
         f32x4 o0 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         f32x4 o1 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        const f32x2* wc = p.wo + (size_t)ch * HP * 64 + lane;
+        const f32x2* wc = p.wo + (size_t)ch * (HP / 4) * 64 + lane;
 #pragma unroll
         for (int t = 0; t < HT; ++t) {
 #pragma unroll
@@ -330,12 +330,12 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
                 }
     std::vector<float> b1(HP, 0.0f);
     for (int u = 0; u < W; ++u) b1[u] = d->hidden_bias[0][u];
-    // hidden layers 2..n: W[W][W] -> [HP][HT/4][64][4] with permuted k
+    // hidden layers 2..n: W[W][W] -> [HP/4][HT/4][64][4] with permuted k
     const int nhx = d->n_hidden - 1;
     std::vector<float> wh((size_t)std::max(nhx, 1) * HP * HP, 0.0f), bh((size_t)std::max(nhx, 1) * HP, 0.0f);
     for (int li = 0; li < nhx; ++li) {
         const float* K = d->hidden_kernel[li + 1];
-        for (int s = 0; s < HP; ++s) {
+        for (int s = 0; s < HP / 4; ++s) {
             const int t = s / 4, r = s % 4;
             for (int mq = 0; mq < HT / 4; ++mq)
                 for (int l = 0; l < 64; ++l)
@@ -349,7 +349,7 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
         }
         for (int u = 0; u < W; ++u) bh[(size_t)li * HP + u] = d->hidden_bias[li + 1][u];
     }
-    // output layer: concat of out kernels [W][out_nz] -> [n_chunks][HP][64][2]
+    // output layer: concat of out kernels [W][out_nz] -> [n_chunks][HP/4][64][2]
     std::vector<int> ocol_var(k_out), ocol_z(k_out);
     {
         int o = 0;
@@ -359,9 +359,9 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
                 ocol_z[o] = z;
             }
     }
-    std::vector<float> wo((size_t)m->n_chunks * HP * 64 * 2, 0.0f);
+    std::vector<float> wo((size_t)m->n_chunks * (HP / 4) * 64 * 2, 0.0f);
     for (int ch = 0; ch < m->n_chunks; ++ch)
-        for (int s = 0; s < HP; ++s) {
+        for (int s = 0; s < HP / 4; ++s) {
             const int t = s / 4, r = s % 4;
             for (int l = 0; l < 64; ++l)
                 for (int mm = 0; mm < 2; ++mm) {
@@ -373,7 +373,7 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
                         const int ov = ocol_var[src], oz = ocol_z[src];
                         v = d->out_kernel[ov][(size_t)in * d->out_nz[ov] + oz];
                     }
-                    wo[(((size_t)ch * HP + s) * 64 + l) * 2 + mm] = v;
+                    wo[(((size_t)ch * (HP / 4) + s) * 64 + l) * 2 + mm] = v;
                 }
         }
     std::vector<float> bo(kop, 0.0f), osig(kop, 1.0f), omean(kop, 0.0f), olo(kop, -INFINITY),

@@ -1,0 +1,345 @@
+"""Column-wise DenseModel (fv3fit ``dense``) on MI355X.
+
+Mirrors the predict graph of ``external/fv3fit/fv3fit/keras/_models/dense.py:234-305``
+(clip -> StandardNorm -> concat -> Dense(width, relu) x (depth-1) -> Dense(nz) per
+output -> StandardDenorm -> OutputLimit -> zero mask) with one fused HIP kernel
+(``csrc/dense.hip``) behind ``fv3_dense_create`` / ``fv3_dense_forward``.
+
+Weights are held in Keras' own layout (kernel ``[fan_in, fan_out]``, bias
+``[fan_out]``), so a trained Keras/TF model converts with a plain weight dump
+(see INTEGRATION.md); the model directory format is npz + yaml.
+"""
+import ctypes
+import dataclasses
+import os
+from typing import Dict, List, Mapping, Optional, Sequence, Tuple
+
+import numpy as np
+import yaml
+
+from . import _device, _native
+
+try:
+    import torch
+except ImportError:  # pragma: no cover
+    torch = None
+
+
+@dataclasses.dataclass
+class DenseModelConfig:
+    """Shape/configuration of a DenseModel (DenseHyperparameters, dense.py:39-106)."""
+
+    input_variables: List[str]
+    output_variables: List[str]
+    in_nz: List[int]
+    out_nz: List[int]
+    width: int = 256  # DenseNetworkConfig.width
+    depth: int = 3  # DenseNetworkConfig.depth: depth-1 hidden layers (dense_network.py:59-76)
+    epsilon: float = 1e-7  # StandardNormLayer epsilon
+    clip: Dict[str, Tuple[int, int]] = dataclasses.field(default_factory=dict)  # ClipConfig
+    output_limits: Dict[str, Tuple[Optional[float], Optional[float]]] = dataclasses.field(
+        default_factory=dict
+    )  # OutputLimitConfig
+
+    @property
+    def n_hidden(self) -> int:
+        return self.depth - 1
+
+    def in_clip(self) -> List[Tuple[int, int]]:
+        out = []
+        for name, nz in zip(self.input_variables, self.in_nz):
+            s, e = self.clip.get(name, (0, nz))
+            out.append((0 if s is None else int(s), nz if e is None else int(e)))
+        return out
+
+    @property
+    def k_in(self) -> int:
+        return sum(e - s for s, e in self.in_clip())
+
+    @property
+    def k_out(self) -> int:
+        return sum(self.out_nz)
+
+    def flops_per_column(self) -> int:
+        w = self.width
+        return 2 * (self.k_in * w + (self.n_hidden - 1) * w * w + w * self.k_out)
+
+    def to_dict(self):
+        d = dataclasses.asdict(self)
+        d["clip"] = {k: list(v) for k, v in self.clip.items()}
+        d["output_limits"] = {k: list(v) for k, v in self.output_limits.items()}
+        return d
+
+    @classmethod
+    def from_dict(cls, d):
+        d = dict(d)
+        d["clip"] = {k: tuple(v) for k, v in d.get("clip", {}).items()}
+        d["output_limits"] = {k: tuple(v) for k, v in d.get("output_limits", {}).items()}
+        return cls(**d)
+
+
+def _glorot(rng, fan_in, fan_out):
+    lim = np.sqrt(6.0 / (fan_in + fan_out))  # keras glorot_uniform (Dense default)
+    return rng.uniform(-lim, lim, size=(fan_in, fan_out)).astype(np.float32)
+
+
+class DenseColumnModel:
+    """Weights + normalisation of a DenseModel, plus its device handle."""
+
+    def __init__(self, config: DenseModelConfig, params: Mapping[str, object]):
+        self.config = config
+        self.params = dict(params)
+        self._handles: Dict[int, int] = {}
+        self._validate()
+
+    # ---- construction ----------------------------------------------------------
+    @classmethod
+    def random(
+        cls,
+        config: DenseModelConfig,
+        seed: int = 1,
+        sample_inputs: Optional[Sequence[np.ndarray]] = None,
+        sample_outputs: Optional[Sequence[np.ndarray]] = None,
+        bias_scale: float = 0.0,
+    ) -> "DenseColumnModel":
+        """Glorot-uniform kernels (Keras default), biases ``bias_scale * N(0,1)``
+        (Keras: zeros), normalisation fitted on samples like build_model does
+        (dense.py:279-289, normalization.py:63-94: mean, population std, f32)."""
+        from . import normalization
+
+        rng = np.random.default_rng(seed)
+        w = config.width
+        k_in = config.k_in
+        hk, hb = [], []
+        fan = k_in
+        for _ in range(config.n_hidden):
+            hk.append(_glorot(rng, fan, w))
+            hb.append((bias_scale * rng.normal(size=w)).astype(np.float32))
+            fan = w
+        ok, ob = [], []
+        for nz in config.out_nz:
+            ok.append(_glorot(rng, w, nz))
+            ob.append((bias_scale * rng.normal(size=nz)).astype(np.float32))
+        clips = config.in_clip()
+        in_mean, in_sigma = [], []
+        for v, nz in enumerate(config.in_nz):
+            s, e = clips[v]
+            if sample_inputs is not None:
+                m, sd = normalization.fit_mean_std(np.asarray(sample_inputs[v]).reshape(-1, nz)[:, s:e])
+            else:
+                m, sd = np.zeros(e - s, np.float32), np.ones(e - s, np.float32)
+            in_mean.append(m)
+            in_sigma.append(sd)
+        out_mean, out_sigma = [], []
+        for o, nz in enumerate(config.out_nz):
+            if sample_outputs is not None:
+                m, sd = normalization.fit_mean_std(np.asarray(sample_outputs[o]).reshape(-1, nz))
+            else:
+                m, sd = np.zeros(nz, np.float32), np.ones(nz, np.float32)
+            out_mean.append(m)
+            out_sigma.append(sd)
+        params = dict(hidden_kernels=hk, hidden_biases=hb, out_kernels=ok, out_biases=ob,
+                      in_mean=in_mean, in_sigma=in_sigma, out_mean=out_mean, out_sigma=out_sigma)
+        return cls(config, params)
+
+    def _validate(self):
+        c, p = self.config, self.params
+        if len(c.input_variables) != len(c.in_nz) or len(c.output_variables) != len(c.out_nz):
+            raise ValueError("variables and level counts disagree")
+        if len(p["hidden_kernels"]) != c.n_hidden or len(p["hidden_biases"]) != c.n_hidden:
+            raise ValueError(f"expected {c.n_hidden} hidden layers")
+        fan = c.k_in
+        for k, b in zip(p["hidden_kernels"], p["hidden_biases"]):
+            if tuple(np.shape(k)) != (fan, c.width) or tuple(np.shape(b)) != (c.width,):
+                raise ValueError(f"hidden kernel shape {np.shape(k)} != {(fan, c.width)}")
+            fan = c.width
+        for o, nz in enumerate(c.out_nz):
+            if tuple(np.shape(p["out_kernels"][o])) != (c.width, nz):
+                raise ValueError(f"output kernel {o} shape {np.shape(p['out_kernels'][o])}")
+
+    def oracle_params(self) -> dict:
+        """Parameters in the layout of oracle.dense.dense_predict (tests only)."""
+        c = self.config
+        d = dict(self.params)
+        d["in_clip"] = c.in_clip()
+        d["epsilon"] = c.epsilon
+        d["out_min"] = [c.output_limits.get(n, (None, None))[0] for n in c.output_variables]
+        d["out_max"] = [c.output_limits.get(n, (None, None))[1] for n in c.output_variables]
+        d["out_mask"] = [self._out_mask(o) for o in range(len(c.output_variables))]
+        return d
+
+    def _out_mask(self, o) -> Optional[np.ndarray]:
+        name, nz = self.config.output_variables[o], self.config.out_nz[o]
+        if name not in self.config.clip:
+            return None
+        s, e = self.config.clip[name]
+        s = 0 if s is None else s
+        e = nz if e is None else e
+        return np.hstack([np.zeros(s), np.ones(e - s), np.zeros(nz - e)]).astype(np.float32)
+
+    # ---- device handle ---------------------------------------------------------
+    def handle(self) -> int:
+        _device.require_gpu()
+        dev = torch.cuda.current_device()
+        if dev in self._handles:
+            return self._handles[dev]
+        c, p = self.config, self.params
+        keep = []  # keep ctypes buffers alive during create
+
+        def farr(a):
+            a = np.ascontiguousarray(np.asarray(a, dtype=np.float32).ravel())
+            keep.append(a)
+            return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+        def iarr(a):
+            a = np.ascontiguousarray(np.asarray(a, dtype=np.int32).ravel())
+            keep.append(a)
+            return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+
+        def parr(arrs):
+            ptrs = (ctypes.POINTER(ctypes.c_float) * len(arrs))(*[farr(a) for a in arrs])
+            keep.append(ptrs)
+            return ctypes.cast(ptrs, ctypes.POINTER(ctypes.POINTER(ctypes.c_float)))
+
+        k_out = c.k_out
+        out_min = np.full(k_out, -np.inf, np.float32)
+        out_max = np.full(k_out, np.inf, np.float32)
+        out_mask = np.ones(k_out, np.float32)
+        off = 0
+        for o, (name, nz) in enumerate(zip(c.output_variables, c.out_nz)):
+            lo, hi = c.output_limits.get(name, (None, None))
+            if lo is not None:
+                out_min[off:off + nz] = lo
+            if hi is not None:
+                out_max[off:off + nz] = hi
+            m = self._out_mask(o)
+            if m is not None:
+                out_mask[off:off + nz] = m
+            off += nz
+        desc = _native.DenseDesc(
+            n_in=len(c.input_variables), in_nz=iarr(c.in_nz), in_clip=iarr(np.array(c.in_clip()).ravel()),
+            in_mean=farr(np.concatenate([np.ravel(m) for m in p["in_mean"]])),
+            in_sigma=farr(np.concatenate([np.ravel(s) for s in p["in_sigma"]])),
+            epsilon=float(c.epsilon), width=int(c.width), n_hidden=int(c.n_hidden),
+            hidden_kernel=parr(p["hidden_kernels"]), hidden_bias=parr(p["hidden_biases"]),
+            n_out=len(c.output_variables), out_nz=iarr(c.out_nz),
+            out_kernel=parr(p["out_kernels"]), out_bias=parr(p["out_biases"]),
+            out_mean=farr(np.concatenate([np.ravel(m) for m in p["out_mean"]])),
+            out_sigma=farr(np.concatenate([np.ravel(s) for s in p["out_sigma"]])),
+            out_min=farr(out_min), out_max=farr(out_max), out_mask=farr(out_mask),
+        )
+        h = ctypes.c_void_p()
+        lib = _native.load()
+        _native.check(lib.fv3_dense_create(ctypes.byref(desc), ctypes.byref(h)), "dense_create")
+        self._handles[dev] = h.value
+        return h.value
+
+    def close(self):
+        if not self._handles:
+            return
+        lib = _native.load()
+        for h in self._handles.values():
+            lib.fv3_dense_destroy(h)
+        self._handles.clear()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- forward -----------------------------------------------------------------
+    def forward(self, inputs: Sequence, level_axes: Optional[Sequence[int]] = None,
+                outputs: Optional[Sequence] = None, out_level_axis: int = 0, stream=None):
+        """Predict on device.  ``inputs[v]``: CUDA tensor whose axis ``level_axes[v]``
+        (default 0) holds that variable's levels and whose other axes are columns
+        (any leading axes are blocks, e.g. tiles).  A 2-D input may omit the level
+        axis (pass ``None``).  Returns output tensors shaped like the first input
+        with the level axis sized ``out_nz``; pass ``outputs`` to write in place."""
+        c = self.config
+        if len(inputs) != len(c.input_variables):
+            raise ValueError(f"expected {len(c.input_variables)} inputs")
+        level_axes = list(level_axes) if level_axes is not None else [0] * len(inputs)
+        ts, lays = [], []
+        ncol = None
+        for v, (t, ax) in enumerate(zip(inputs, level_axes)):
+            t = _device.to_device_f32(t)
+            if ax is None:
+                t = t.unsqueeze(0)
+                ax = 0
+            lay, n, nz = _device.level_layout(t, ax)
+            if nz != c.in_nz[v]:
+                raise ValueError(f"input {c.input_variables[v]} has {nz} levels, model expects {c.in_nz[v]}")
+            if ncol is not None and n != ncol:
+                raise ValueError("inputs disagree on the number of columns")
+            ncol = n
+            ts.append(t)
+            lays.append(lay)
+        ref = ts[0]
+        ax0 = level_axes[0] if level_axes[0] is not None else 0
+        if outputs is None:
+            outputs = []
+            for nz in c.out_nz:
+                shape = list(ref.shape)
+                shape[ax0] = nz
+                outputs.append(torch.empty(shape, dtype=torch.float32, device=ref.device))
+            out_axes = [ax0] * len(c.out_nz)
+        else:
+            out_axes = [out_level_axis] * len(outputs)
+        olays = []
+        for o, (t, ax) in enumerate(zip(outputs, out_axes)):
+            lay, n, nz = _device.level_layout(t, ax)
+            if nz != c.out_nz[o] or n != ncol:
+                raise ValueError(f"output {o} has shape {tuple(t.shape)}")
+            olays.append(lay)
+        if any(l.ncol_blk != lays[0].ncol_blk for l in lays + olays):
+            raise ValueError("all inputs/outputs must share the horizontal layout")
+        in_ptrs = (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+        out_ptrs = (ctypes.c_void_p * len(outputs))(*[t.data_ptr() for t in outputs])
+        in_l = (_native.Layout * len(lays))(*lays)
+        out_l = (_native.Layout * len(olays))(*olays)
+        lib = _native.load()
+        st = lib.fv3_dense_forward(self.handle(), in_ptrs, in_l, out_ptrs, out_l, int(ncol),
+                                   _device.stream_handle(stream))
+        _native.check(st, "dense_forward")
+        return outputs
+
+    # ---- persistence -------------------------------------------------------------
+    _WEIGHTS = "weights.npz"
+    _CONFIG = "dense_config.yaml"
+
+    def dump(self, path: str):
+        os.makedirs(path, exist_ok=True)
+        arrays = {}
+        p = self.params
+        for i, (k, b) in enumerate(zip(p["hidden_kernels"], p["hidden_biases"])):
+            arrays[f"hidden_{i}/kernel"] = k
+            arrays[f"hidden_{i}/bias"] = b
+        for o, (k, b) in enumerate(zip(p["out_kernels"], p["out_biases"])):
+            arrays[f"output_{o}/kernel"] = k
+            arrays[f"output_{o}/bias"] = b
+            arrays[f"output_{o}/mean"] = p["out_mean"][o]
+            arrays[f"output_{o}/sigma"] = p["out_sigma"][o]
+        for v in range(len(p["in_mean"])):
+            arrays[f"input_{v}/mean"] = p["in_mean"][v]
+            arrays[f"input_{v}/sigma"] = p["in_sigma"][v]
+        np.savez(os.path.join(path, self._WEIGHTS), **arrays)
+        with open(os.path.join(path, self._CONFIG), "w") as f:
+            yaml.safe_dump(self.config.to_dict(), f)
+
+    @classmethod
+    def load(cls, path: str) -> "DenseColumnModel":
+        with open(os.path.join(path, cls._CONFIG)) as f:
+            config = DenseModelConfig.from_dict(yaml.safe_load(f))
+        z = np.load(os.path.join(path, cls._WEIGHTS), allow_pickle=False)
+        p = dict(
+            hidden_kernels=[z[f"hidden_{i}/kernel"] for i in range(config.n_hidden)],
+            hidden_biases=[z[f"hidden_{i}/bias"] for i in range(config.n_hidden)],
+            out_kernels=[z[f"output_{o}/kernel"] for o in range(len(config.out_nz))],
+            out_biases=[z[f"output_{o}/bias"] for o in range(len(config.out_nz))],
+            out_mean=[z[f"output_{o}/mean"] for o in range(len(config.out_nz))],
+            out_sigma=[z[f"output_{o}/sigma"] for o in range(len(config.out_nz))],
+            in_mean=[z[f"input_{v}/mean"] for v in range(len(config.in_nz))],
+            in_sigma=[z[f"input_{v}/sigma"] for v in range(len(config.in_nz))],
+        )
+        return cls(config, p)
