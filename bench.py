@@ -1,0 +1,246 @@
+#!/usr/bin/env python
+"""bench.py — fv3net ML-physics hot path on MI355X (driver contract).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A "step" is one pass of the hot path over one batch: BASELINE config #2, the
+column-wise DenseModel predict (fv3fit PureKerasModel.predict -> Keras predict,
+pure_keras.py:98-118) of dQ1/dQ2 from T/q on a C48 79-level state, 13,824
+columns per GPU, inputs resident in HBM, one fused HIP kernel per step.
+Multi-GPU: each rank owns its own C48 state (columns shard with no data-path
+collective) -> "scaling": "weak"; value = all ranks' columns / max-over-ranks time.
+
+Rank 0 prints ONE JSON line on stdout (everything else goes to stderr), with
+  roofline:     the fused kernel's algorithmic FLOP per launch / its mean launch
+                duration (HIP events on the kernel's own stream, inside the timed
+                region) vs the f32 MFMA peak; traffic = HBM bytes per launch from the
+                committed rocprofv3 PMC pass (profiles/), or null;
+  cpu_baseline: the numpy restatement of the same graph (oracle/dense.py) on the
+                host cores, Keras-style batch_size=32 chunks (pure_keras.py:112 calls
+                model.predict without batch_size), on a bounded sample (N=1, rank 0);
+  extra:        other configs measured on the same GPU (N=1, rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "grid-columns/s ML-physics step (C48 & C384, 79L); HBM GB/s vs gfx950 peak"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--res", type=int, default=48, help="cubed-sphere resolution per GPU (C48)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-extra", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    return p.parse_args()
+
+
+def timed_steps(step, steps, warmup, dist=None):
+    """W untimed steps, then exactly K timed steps bracketed by barrier + sync.
+    Returns (wall seconds, per-launch kernel seconds from HIP events)."""
+    import torch
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        starts[i].record()  # current stream == the stream the kernel is launched on
+        step()
+        ends[i].record()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern = [s.elapsed_time(e) * 1e-3 for s, e in zip(starts, ends)]
+    return wall, kern
+
+
+def pmc_traffic(kernel_key):
+    """HBM bytes per launch from the committed PMC pass (tools/profile.sh), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(kernel_key, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(wl, seconds):
+    """Reference-arithmetic CPU restatement (oracle/dense.py) on a bounded sample."""
+    from threadpoolctl import threadpool_info
+
+    from oracle.dense import dense_predict
+
+    p = wl.model.oracle_params()
+    # one C48 tile of columns, [N, z] sample-major as Keras sees them (pure_keras.py:111)
+    T = wl.inputs[0][0].reshape(79, -1).T.contiguous().cpu().numpy()
+    q = wl.inputs[1][0].reshape(79, -1).T.contiguous().cpu().numpy()
+    n = T.shape[0]
+    cols = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for s in range(0, n, 32):  # Keras model.predict default batch_size=32
+            dense_predict([T[s:s + 32], q[s:s + 32]], p, np.float32)
+        cols += n
+    dt = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    reps = 0
+    while time.perf_counter() - t1 < max(1.0, seconds / 5):
+        dense_predict([T, q], p, np.float32)
+        reps += 1
+    single = reps * n / (time.perf_counter() - t1)
+    threads = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
+    return {
+        "value": cols / dt,
+        "unit": "columns/s",
+        "cores": int(threads),
+        "kind": "port",
+        "sample": f"{cols} columns of one C48 tile ({n} columns/pass) through oracle/dense.py "
+                  f"float32 in Keras-default batch_size=32 chunks, {dt:.1f} s; numpy BLAS threads="
+                  f"{threads}; single-batch (no Keras chunking) = {single:.3e} columns/s",
+    }
+
+
+def extra_measurements(dev):
+    import torch
+
+    from fv3net_amd import workloads as W
+
+    out = {}
+    # config #2 at C384 (one GPU, 884,736 columns): MFMA-bound predict
+    wl = W.make_dense_workload(384, seed=3, device=dev)
+    wall, kern = timed_steps(wl.step, 10, 3)
+    t = float(np.mean(kern))
+    out["dense_c384"] = {
+        "columns_per_s": wl.ncol / t, "ms_per_step": t * 1e3,
+        "tflops": wl.ncol * wl.flops_per_column / t / 1e12,
+        "frac_f32_mfma_peak": wl.ncol * wl.flops_per_column / t / 1e12 / W.FP32_MFMA_PEAK_TFLOPS,
+    }
+    del wl
+    # mappm: config #3 fine columns (C384 79->79) and config #1 (C12 79->50)
+    for name, ncol, kn, kord in (("mappm_c384_79to79_kord1", W.c_columns(384), 79, 1),
+                                 ("mappm_c384_79to79_kord10", W.c_columns(384), 79, 10),
+                                 ("mappm_c12_79to50_kord1", W.c_columns(12), 50, 1)):
+        wl = W.make_mappm_workload(ncol, 79, kn, kord, seed=5, device=dev)
+        wall, kern = timed_steps(wl.step, 10, 3)
+        t = float(np.mean(kern))
+        gbs = wl.bytes_per_column * ncol / t / 1e9
+        out[name] = {"columns_per_s": ncol / t, "ms_per_step": t * 1e3, "hbm_gbs": gbs,
+                     "frac_hbm_peak": gbs / W.HBM_PEAK_GBS}
+        del wl
+    torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as tdist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        tdist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        dist = tdist
+
+    from fv3net_amd import workloads as W
+
+    wl = W.make_dense_workload(args.res, seed=1000 + rank, device=dev)
+    wall, kern = timed_steps(wl.step, args.steps, args.warmup, dist)
+    if dist is not None:
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    total_cols = wl.ncol * world * args.steps
+    value = total_cols / wall
+    kmean = float(np.mean(kern))
+    flops_launch = wl.ncol * wl.flops_per_column
+    achieved = flops_launch / kmean / 1e12
+
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "columns/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (T~N(260,15) K, q~U(0,0.02); random Glorot weights, norms fitted on the sample)",
+        "config": {
+            "workload": "config #2: fv3fit DenseModel (2x256) column-wise predict of dQ1/dQ2 from T/q, "
+                        f"C{args.res} 79L per GPU, fused normalize->MLP->denormalize kernel",
+            "columns_per_gpu": wl.ncol,
+            "levels": 79,
+            "global_batch": wl.ncol * world,
+            "parallelism": f"columns sharded, 1 process/GPU x {world}",
+        },
+        "roofline": {
+            "kernel": "dense_forward_kernel<16>",
+            "bound": "mfma",
+            "achieved": achieved,
+            "peak": W.FP32_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved / W.FP32_MFMA_PEAK_TFLOPS,
+            "traffic": pmc_traffic("dense_forward_kernel<16>"),
+            "algorithmic_flop_per_launch": flops_launch,
+            "algorithmic_bytes_per_launch": wl.ncol * wl.bytes_per_column,
+            "mean_launch_us": kmean * 1e6,
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            result["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds)
+        except Exception as e:  # the baseline is a report, never fatal
+            log("cpu_baseline failed:", repr(e))
+    if rank == 0 and world == 1 and not args.no_extra:
+        del wl
+        torch.cuda.empty_cache()
+        try:
+            result["extra"] = extra_measurements(dev)
+        except Exception as e:
+            log("extra measurements failed:", repr(e))
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,112 @@
+"""Synthetic workloads of BASELINE.json's configs, shared by
+bench.py, __graft_entry__.smoke() and the tests.  Inputs are created directly in
+HBM (no host round trip inside timed regions)."""
+import dataclasses
+from typing import List, Optional
+
+import numpy as np
+
+from .dense import DenseColumnModel, DenseModelConfig
+
+try:
+    import torch
+except ImportError:  # pragma: no cover
+    torch = None
+
+NZ = 79
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, dense f32 MFMA (= vector) peak
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
+
+
+def c_columns(res: int, ntile: int = 6) -> int:
+    return ntile * res * res
+
+
+def dense_2x256_config() -> DenseModelConfig:
+    """config #2: DenseModel width 256, depth 3 (two hidden layers), T/q -> dQ1/dQ2."""
+    return DenseModelConfig(
+        input_variables=["air_temperature", "specific_humidity"],
+        output_variables=["dQ1", "dQ2"],
+        in_nz=[NZ, NZ], out_nz=[NZ, NZ], width=256, depth=3,
+    )
+
+
+def synthetic_state(res: int, seed: int, device, ntile: int = 6):
+    """T ~ N(260, 15) K, q ~ U(0, 0.02) kg/kg, (tile, z, y, x) float32 on device."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    shape = (ntile, NZ, res, res)
+    T = torch.randn(shape, generator=g, device=device) * 15.0 + 260.0
+    q = torch.rand(shape, generator=g, device=device) * 0.02
+    return T, q
+
+
+@dataclasses.dataclass
+class DenseWorkload:
+    model: DenseColumnModel
+    inputs: List
+    outputs: List
+    ncol: int
+    flops_per_column: int
+    bytes_per_column: int
+
+    def step(self):
+        self.model.forward(self.inputs, level_axes=[1, 1], outputs=self.outputs, out_level_axis=1)
+
+
+def make_dense_workload(res: int, seed: int = 0, device=None, model: Optional[DenseColumnModel] = None):
+    device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    T, q = synthetic_state(res, seed, device)
+    if model is None:
+        # normalisation fitted on a sample of the synthetic state (build_model fits on data)
+        sample_T = T[0, :, :8, :8].reshape(NZ, -1).T.cpu().numpy()
+        sample_q = q[0, :, :8, :8].reshape(NZ, -1).T.cpu().numpy()
+        model = DenseColumnModel.random(dense_2x256_config(), seed=1, sample_inputs=[sample_T, sample_q])
+    outs = [torch.empty_like(T), torch.empty_like(T)]
+    cfg = model.config
+    return DenseWorkload(model, [T, q], outs, c_columns(res), cfg.flops_per_column(),
+                         4 * (cfg.k_in + cfg.k_out))
+
+
+@dataclasses.dataclass
+class MappmWorkload:
+    pe1: object
+    q1: object
+    pe2: object
+    q2: object
+    ncol: int
+    km: int
+    kn: int
+    kord: int
+    iv: int = 1
+
+    @property
+    def bytes_per_column(self) -> int:
+        return 4 * ((self.km + 1) + self.km + (self.kn + 1) + self.kn)
+
+    def step(self):
+        from .mappm import mappm_device
+
+        mappm_device(self.pe1, self.q1, self.pe2, self.iv, self.kord, out=self.q2)
+
+
+def make_mappm_workload(ncol: int, km: int = NZ, kn: int = NZ, kord: int = 1, seed: int = 0, device=None):
+    """Monotone columns: delp ~ D(k) * U(0.99, 1.01) (a 79-level reference profile,
+    cf. synth/_restarts.py:36-38), p_out = a neighbour's edges (kn == km) or kn+1
+    evenly spaced edges (config #1), shared 300 Pa top."""
+    device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    base = torch.linspace(200.0, 1800.0, km, device=device)[:, None]
+    delp = base * (0.99 + 0.02 * torch.rand((km, ncol), generator=g, device=device))
+    top = torch.full((1, ncol), 300.0, device=device)
+    pe1 = torch.cat([top, 300.0 + torch.cumsum(delp, 0)])
+    if kn == km:
+        d2 = base * (0.99 + 0.02 * torch.rand((km, ncol), generator=g, device=device))
+        pe2 = torch.cat([top, 300.0 + torch.cumsum(d2, 0)])
+    else:
+        frac = torch.linspace(0.0, 1.0, kn + 1, device=device)[:, None]
+        pe2 = pe1[:1] + frac * (pe1[-1:] - pe1[:1])
+    q1 = torch.randn((km, ncol), generator=g, device=device) * 10.0 + 250.0
+    q2 = torch.empty((kn, ncol), device=device)
+    return MappmWorkload(pe1.contiguous(), q1, pe2.contiguous(), q2, ncol, km, kn, kord)
