@@ -210,13 +210,13 @@ def main():
             "parallelism": f"columns sharded, 1 process/GPU x {world}",
         },
         "roofline": {
-            "kernel": "dense_forward_kernel<16>",
+            "kernel": "fv3::dense_forward_kernel<4,2> (csrc/dense.hip)",
             "bound": "mfma",
             "achieved": achieved,
             "peak": W.FP32_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved / W.FP32_MFMA_PEAK_TFLOPS,
-            "traffic": pmc_traffic("dense_forward_kernel<16>"),
+            "traffic": pmc_traffic("dense_c48"),
             "algorithmic_flop_per_launch": flops_launch,
             "algorithmic_bytes_per_launch": wl.ncol * wl.bytes_per_column,
             "mean_launch_us": kmean * 1e6,

@@ -27,6 +27,7 @@ EXPORTED_SYMBOLS = (
     "fv3_dense_k_out",
     "fv3_dense_forward",
     "fv3_regrid_coarsen",
+    "fv3_regrid_coarsen_f64",
     "fv3_column_integral",
     "fv3_area_weighted_sums",
 )
@@ -87,6 +88,8 @@ _SIGNATURES = {
                                ctypes.POINTER(Layout), _I64, _P]),
     "fv3_regrid_coarsen": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _P, _I, _I, _I,
                                 _I, _I, _I, _I, _D, _P]),
+    "fv3_regrid_coarsen_f64": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _P, _I, _I, _I,
+                                    _I, _I, _I, _I, _D, _P]),
     "fv3_column_integral": (_I, [_P, Layout, _P, Layout, _P, _I64, _I, _D, _P]),
     "fv3_area_weighted_sums": (_I, [ctypes.POINTER(_P), _I, _P, _I64, _P, _P]),
 }

@@ -1,0 +1,80 @@
+"""Pressure-level coarse-graining (vcm.cubedsphere) on MI355X.
+
+``coarsen_on_pressure`` fuses, for the masked area-weighted variables of
+``coarsen_restarts_on_pressure`` (external/vcm/vcm/cubedsphere/coarsen_restarts.py:411-516,
+840-887), the whole ``regrid_to_area_weighted_pressure`` (regridz.py:25-55) ->
+``weighted_block_average`` (coarsen.py:183-218) chain into one HIP kernel
+(csrc/coarsen.hip).  ``regrid_vertical`` mirrors regridz.py:164-279 on device.
+"""
+import ctypes
+from typing import Dict, Mapping, Sequence
+
+import numpy as np
+
+from . import _device, _native
+
+try:
+    import torch
+except ImportError:  # pragma: no cover
+    torch = None
+
+TOA_PRESSURE = 300.0  # external/vcm/vcm/calc/thermo/constants.py:17
+
+
+def coarsen_on_pressure(delp, area, fields: Mapping[str, object], factor: int, iv: int = 1, kord: int = 1,
+                        ptop: float = TOA_PRESSURE, stream=None):
+    """delp and fields (tile, z, y, x), area (tile, y, x) -> dict of coarse fields
+    (tile, z, y/f, x/f) and the area-weighted coarse delp.  Device tensors in and out."""
+    _device.require_gpu()
+    delp64 = (isinstance(delp, np.ndarray) and delp.dtype == np.float64) or (
+        torch is not None and isinstance(delp, torch.Tensor) and delp.dtype == torch.float64)
+    if delp64:  # keep restart precision: pressures are cumulated in float64 on device
+        delp = (torch.as_tensor(delp) if not isinstance(delp, torch.Tensor) else delp).to(
+            device=torch.device("cuda", torch.cuda.current_device()), dtype=torch.float64).contiguous()
+    else:
+        delp = _device.to_device_f32(delp)
+    area = _device.to_device_f32(area)
+    if delp.dim() != 4 or area.dim() != 3:
+        raise ValueError("delp must be (tile, z, y, x) and area (tile, y, x)")
+    nt, km, ny, nx = delp.shape
+    if tuple(area.shape) != (nt, ny, nx):
+        raise ValueError(f"area shape {tuple(area.shape)} does not match delp {tuple(delp.shape)}")
+    names = list(fields)
+    tens = []
+    for n in names:
+        t = _device.to_device_f32(fields[n])
+        if tuple(t.shape) != tuple(delp.shape):
+            raise ValueError(f"{n} shape {tuple(t.shape)} != delp shape {tuple(delp.shape)}")
+        tens.append(t)
+    if ny % factor or nx % factor:
+        raise ValueError(f"grid {ny}x{nx} is not divisible by the coarsening factor {factor}")
+    cshape = (nt, km, ny // factor, nx // factor)
+    outs = [torch.empty(cshape, dtype=torch.float32, device=delp.device) for _ in names]
+    delp_c = torch.empty(cshape, dtype=torch.float32, device=delp.device)
+    fptr = (ctypes.c_void_p * max(1, len(tens)))(*[t.data_ptr() for t in tens])
+    optr = (ctypes.c_void_p * max(1, len(outs)))(*[t.data_ptr() for t in outs])
+    lib = _native.load()
+    fn = lib.fv3_regrid_coarsen_f64 if delp64 else lib.fv3_regrid_coarsen
+    st = fn(delp.data_ptr(), area.data_ptr(), fptr, optr, len(tens), delp_c.data_ptr(), nt, km, ny, nx,
+            int(factor), int(iv), int(kord), float(ptop), _device.stream_handle(stream))
+    _native.check(st, "regrid_coarsen")
+    return dict(zip(names, outs)), delp_c
+
+
+def regrid_vertical(p_in, f_in, p_out, iv: int = 1, kord: int = 1, z_axis: int = -1):
+    """Device regrid_vertical (regridz.py:164-279) on arrays whose vertical axis is
+    ``z_axis`` (default last, as the reference transposes to); float32 result with
+    the input's axis order.  Raises the reference's ValueErrors."""
+    from .mappm import mappm_device
+
+    p_in, f_in, p_out = (_device.to_device_f32(a) for a in (p_in, f_in, p_out))
+    ax = z_axis % p_in.dim()
+    if f_in.shape[ax] != p_in.shape[ax] - 1:
+        raise ValueError("f_in must have a vertical dimension one shorter than p_in")
+    cols = lambda t: t.movedim(ax, 0).reshape(t.shape[ax], -1)
+    if cols(p_in).shape[1] != cols(f_in).shape[1] or cols(p_out).shape[1] != cols(f_in).shape[1]:
+        raise ValueError("All dimensions except vertical must be same size for p_in, f_in and p_out")
+    q2 = mappm_device(cols(p_in).contiguous(), cols(f_in).contiguous(), cols(p_out).contiguous(), iv, kord)
+    shape = list(f_in.movedim(ax, 0).shape)
+    shape[0] = q2.shape[0]
+    return q2.reshape(shape).movedim(0, ax).contiguous()

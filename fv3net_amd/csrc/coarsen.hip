@@ -1,0 +1,233 @@
+// fv3net_amd — fused pressure-level coarse-graining (BASELINE config #3) on gfx950.
+//
+// Replaces, for the masked area-weighted variables of coarsen_restarts_on_pressure
+// (external/vcm/vcm/cubedsphere/coarsen_restarts.py:411-516, 840-887):
+//   regrid_to_area_weighted_pressure   regridz.py:25-55
+//     delp_c = weighted_block_average(delp, area, f)       coarsen.py:183-218
+//     _regrid_given_delp                                   regridz.py:115-147
+//       block_upsample_like(delp_c)                        coarsen.py:900-938
+//       pressure_at_interface (phalf = cumsum([300, delp])) vertically_dependent.py:41-66
+//       regrid_vertical -> mappm(p_fine, f, p_coarse, iv, kord)  regridz.py:164-279
+//     _mask_weights: area where phalf_c[k+1] < phalf_f[-1]  regridz.py:150-161
+//   weighted_block_average(f_regrid, masked_area, f)        coarsen.py:183-218
+// in ONE kernel and one pass over each input field.
+//
+// Mapping: one wave per coarse cell; lane (dy, dx) owns fine column (f*Y+dy, f*X+dx)
+// (f <= 8, lanes >= f*f idle).  Pass 1 streams delp once: every lane keeps its own
+// float64 cumsum (fine phalf; the surface value is kept for the mask), and a fixed
+// xor-shuffle tree forms sum(delp*area) per level -> delp_c and the coarse phalf
+// (float64, identical on every lane; stored in LDS).  Per field: each lane runs the
+// one-pass streaming mappm (mappm_core.h) with p_in recomputed from L2-hot delp,
+// stages its remapped column in LDS [level][65] (padded: conflict-free), then lane k
+// reduces level k over the block in a fixed order.  Deterministic run to run.
+// Roofline: HBM-bound, (79 delp + 79*n_fields + 1 area) * 4 B per fine column read
+// once (+ ~4/f^2 of that written); delp is re-read per field from L2, not HBM.
+#define FV3_HD __host__ __device__
+#include "common.h"
+#include "mappm_core.h"
+
+namespace fv3 {
+namespace {
+
+constexpr int kMaxLev = 128;
+constexpr int kStride = 65;  // LDS row stride (floats) of the per-field staging buffer
+constexpr int kOffPb = 1040;                    // after pc[kMaxLev + 1] doubles, 16-aligned
+constexpr int kOffArea = kOffPb + 64 * 8;
+constexpr int kOffStage = kOffArea + 64 * 4;    // 1808: 16-aligned
+
+template <typename DT>
+struct CoarsenArgs {
+    const DT* delp;
+    const float* area;
+    const float* const* fields;
+    float* const* out;
+    float* delp_out;
+    int n_fields, ntile, km, ny, nx, f, iv, kord;
+    double ptop;
+};
+
+__device__ __forceinline__ double wave_sum(double v)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// fine column of this lane: p_in streamed from a running float64 cumsum of delp
+template <typename DT>
+struct FineCol {
+    const float* q;   // field at level 0 of this column
+    const DT* dp;     // delp at level 0 of this column
+    int64_t plane;    // ny*nx
+    const double* pc; // coarse phalf[k], k = 0..km (LDS)
+    float* stage;     // LDS staging, this lane's column: stage[k * kStride]
+    double ptop, pbot, run;
+    int next;         // next fine interface index (0-based) the running sum will produce
+    int km, kn;
+    __device__ __forceinline__ float q1(int k) const { return q[(int64_t)(k - 1) * plane]; }
+    __device__ __forceinline__ float pe1(int k)
+    {
+        // reference: phalf = cumsum([ptop, delp]) in float64, cast to float32 by f2py
+        if (k == 1) return (float)ptop;
+        if (k == km + 1) return (float)pbot;
+        while (next < k - 1) {  // interface k-1 (0-based) = ptop + sum delp[0..k-2]
+            run += (double)dp[(int64_t)next * plane];
+            ++next;
+        }
+        return (float)run;
+    }
+    __device__ __forceinline__ float pe2(int k) const { return (float)pc[k - 1]; }
+    __device__ __forceinline__ void emit(int k, float v) { stage[(k - 1) * kStride] = v; }
+    __device__ __forceinline__ float next_edge(int k) const { return (k + 1 <= kn + 1) ? pe2(k + 1) : 0.0f; }
+};
+
+template <typename DT>
+__global__ __launch_bounds__(64) void regrid_coarsen_kernel(CoarsenArgs<DT> a)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double* pc = reinterpret_cast<double*>(smem);                    // [km+1] coarse phalf
+    double* lpb = reinterpret_cast<double*>(smem + kOffPb);          // [64] fine surface phalf
+    float* lar = reinterpret_cast<float*>(smem + kOffArea);          // [64] fine area
+    float* stage = reinterpret_cast<float*>(smem + kOffStage);       // [km][kStride]
+
+    const int lane = threadIdx.x;
+    const int f = a.f;
+    const int nyc = a.ny / f, nxc = a.nx / f;
+    const int64_t cell = blockIdx.x;
+    const int tile = (int)(cell / ((int64_t)nyc * nxc));
+    const int rem = (int)(cell - (int64_t)tile * nyc * nxc);
+    const int Y = rem / nxc, X = rem - (rem / nxc) * nxc;
+    const bool active = lane < f * f;
+    const int dy = active ? lane / f : 0, dx = active ? lane - (lane / f) * f : 0;
+    const int64_t plane = (int64_t)a.ny * a.nx;
+    const int64_t fine = (int64_t)(Y * f + dy) * a.nx + (X * f + dx);
+    const int64_t cplane = (int64_t)nyc * nxc;
+    const int64_t cidx = (int64_t)Y * nxc + X;
+    const int km = a.km;
+
+    // ---- pass 1: fine phalf (per lane) and area-weighted coarse delp / phalf ----
+    const double area = active ? (double)a.area[(int64_t)tile * plane + fine] : 0.0;
+    const double asum = wave_sum(area);
+    const DT* dp = a.delp + (int64_t)tile * km * plane + fine;
+    double run = a.ptop;   // fine phalf, float64 cumsum (vertically_dependent.py:62-63)
+    double pcr = a.ptop;   // coarse phalf
+    if (lane == 0) pc[0] = a.ptop;
+    for (int k = 0; k < km; ++k) {
+        const double d = (double)dp[(int64_t)k * plane];
+        run += d;
+        const double num = wave_sum(active ? d * area : 0.0);
+        const double dc = num / asum;  // weighted_block_average: sum(delp*area)/sum(area)
+        pcr += dc;
+        if (lane == 0) {
+            pc[k + 1] = pcr;
+            if (a.delp_out) a.delp_out[((int64_t)tile * km + k) * cplane + cidx] = (float)dc;
+        }
+    }
+    const double pbot = run;  // phalf_fine[-1] of this fine column
+    lpb[lane] = pbot;
+    lar[lane] = active ? (float)area : 0.0f;
+    __syncthreads();
+
+    // ---- per field: remap every fine column, then masked area-weighted block mean ----
+    for (int v = 0; v < a.n_fields; ++v) {
+        FineCol<DT> c;
+        c.q = a.fields[v] + (int64_t)tile * km * plane + fine;
+        c.dp = dp;
+        c.plane = plane;
+        c.pc = pc;
+        c.stage = stage + lane;
+        c.ptop = a.ptop;
+        c.pbot = pbot;
+        c.run = a.ptop;
+        c.next = 0;
+        c.km = km;
+        c.kn = km;
+        mappm_ppm_column(c, km, km, a.iv, a.kord);
+        __syncthreads();
+        // lane j reduces levels k = j, j+64, ... over the block's fine columns in a fixed order
+        float* o = a.out[v] + (int64_t)tile * km * cplane + cidx;
+        for (int k = lane; k < km; k += 64) {
+            const double pk = pc[k + 1];
+            double num = 0.0, den = 0.0;
+            for (int j = 0; j < f * f; ++j) {
+                // _mask_weights: area where phalf_c_on_f[k+1] < phalf_f[-1] (float64 compare);
+                // the masked area keeps area's float32 dtype, products/sums per coarsen.py
+                const float w = (pk < lpb[j]) ? lar[j] : 0.0f;
+                num += (double)(stage[k * kStride + j] * w);
+                den += (double)w;
+            }
+            o[(int64_t)k * cplane] = (float)(num / den);
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+template <typename DT>
+int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* fields, float* const* out,
+                        int n_fields, float* delp_out, int ntile, int km, int ny, int nx, int factor, int iv,
+                        int kord, double ptop_toa, void* stream)
+{
+    using namespace fv3;
+    clear_error();
+    FV3_REQUIRE(ntile >= 1 && ny >= 1 && nx >= 1, "regrid_coarsen: bad grid (%d, %d, %d)", ntile, ny, nx);
+    FV3_REQUIRE(km >= 4 && km <= kMaxLev, "regrid_coarsen: km must be in [4, %d] (got %d)", kMaxLev, km);
+    FV3_REQUIRE(factor >= 1 && factor <= 8, "regrid_coarsen: coarsening factor must be in [1, 8]");
+    FV3_REQUIRE(ny % factor == 0 && nx % factor == 0, "regrid_coarsen: %dx%d not divisible by factor %d", ny, nx,
+                factor);
+    FV3_REQUIRE(n_fields >= 0 && n_fields <= 64, "regrid_coarsen: n_fields must be in [0, 64]");
+    FV3_REQUIRE(delp && area, "regrid_coarsen: NULL delp/area");
+    if (kord > 7) {
+        set_error("regrid_coarsen: kord > 7 (cs_profile) is not fused in this build; use fv3_mappm_ex");
+        return FV3_ERR_UNSUPPORTED;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    const size_t tab = sizeof(void*) * (size_t)std::max(n_fields, 1);
+    void* dtab = nullptr;
+    if (n_fields > 0) {
+        FV3_REQUIRE(fields && out, "regrid_coarsen: NULL field tables");
+        FV3_HIP(hipMallocAsync(&dtab, 2 * tab, s));
+        FV3_HIP(hipMemcpyAsync(dtab, fields, tab, hipMemcpyHostToDevice, s));
+        FV3_HIP(hipMemcpyAsync((char*)dtab + tab, out, tab, hipMemcpyHostToDevice, s));
+    }
+    CoarsenArgs<DT> a;
+    a.delp = delp;
+    a.area = area;
+    a.fields = (const float* const*)dtab;
+    a.out = (float* const*)((char*)dtab + tab);
+    a.delp_out = delp_out;
+    a.n_fields = n_fields;
+    a.ntile = ntile;
+    a.km = km;
+    a.ny = ny;
+    a.nx = nx;
+    a.f = factor;
+    a.iv = iv;
+    a.kord = kord;
+    a.ptop = ptop_toa;
+    const int64_t cells = (int64_t)ntile * (ny / factor) * (nx / factor);
+    const size_t lds = kOffStage + sizeof(float) * (size_t)km * kStride;
+    hipLaunchKernelGGL(regrid_coarsen_kernel<DT>, dim3((unsigned)cells), dim3(64), lds, s, a);
+    FV3_LAUNCH_CHECK();
+    if (dtab) FV3_HIP(hipFreeAsync(dtab, s));
+    return FV3_OK;
+}
+
+}  // namespace fv3
+
+extern "C" int fv3_regrid_coarsen(const float* delp, const float* area, const float* const* fields,
+                                  float* const* out, int n_fields, float* delp_out, int ntile, int km, int ny,
+                                  int nx, int factor, int iv, int kord, double ptop_toa, void* stream)
+{
+    return fv3::regrid_coarsen_impl<float>(delp, area, fields, out, n_fields, delp_out, ntile, km, ny, nx, factor,
+                                           iv, kord, ptop_toa, stream);
+}
+
+extern "C" int fv3_regrid_coarsen_f64(const double* delp, const float* area, const float* const* fields,
+                                      float* const* out, int n_fields, float* delp_out, int ntile, int km, int ny,
+                                      int nx, int factor, int iv, int kord, double ptop_toa, void* stream)
+{
+    return fv3::regrid_coarsen_impl<double>(delp, area, fields, out, n_fields, delp_out, ntile, km, ny, nx,
+                                            factor, iv, kord, ptop_toa, stream);
+}

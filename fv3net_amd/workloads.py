@@ -50,8 +50,13 @@ class DenseWorkload:
     flops_per_column: int
     bytes_per_column: int
 
+    _bound: object = None
+
     def step(self):
-        self.model.forward(self.inputs, level_axes=[1, 1], outputs=self.outputs, out_level_axis=1)
+        if self._bound is None:
+            self._bound = self.model.bind(self.inputs, level_axes=[1, 1], outputs=self.outputs, out_level_axis=1)
+        else:
+            self._bound()
 
 
 def make_dense_workload(res: int, seed: int = 0, device=None, model: Optional[DenseColumnModel] = None):

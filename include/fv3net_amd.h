@@ -123,6 +123,13 @@ int fv3_regrid_coarsen(const float* delp, const float* area, const float* const*
                        int ny, int nx, int factor, int iv, int kord, double ptop_toa,
                        void* stream);
 
+/* Same with float64 delp (FV3 fv_core restarts store delp in double precision; the
+ * pressures are cumulated in float64 either way). */
+int fv3_regrid_coarsen_f64(const double* delp, const float* area, const float* const* fields,
+                           float* const* out, int n_fields, float* delp_out, int ntile, int km,
+                           int ny, int nx, int factor, int iv, int kord, double ptop_toa,
+                           void* stream);
+
 /* ---- per-column reductions for stepper diagnostics --------------------------------
  * out[c] = sum_k field[k][c] * delp[k][c] * scale  (vcm mass_integrate,
  * external/vcm/vcm/calc/thermo/vertically_dependent.py:18-22, with scale = 1/g),

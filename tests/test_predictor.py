@@ -1,0 +1,162 @@
+"""The fv3fit Predictor boundary: registry, stack semantics, ConstantOutputPredictor
+(CPU), and the MI355X DenseColumnPredictor end to end (GPU).
+
+Mirrors external/fv3fit/tests/test_stacking.py:24-94, test_io.py / test_register_model.py
+(duplicate names, name file), test_constant_predictor.py, and pure_keras.py:98-118.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from fv3net_amd import dataset as D
+from fv3net_amd import predictor as P
+from fv3net_amd.predictor import SAMPLE_DIM_NAME, Z_DIM_NAMES, stack
+
+
+def _gridded(zdim, ydim=10, xdim=10):
+    var = np.array([[[(100 * k) + (10 * j) + i for i in range(xdim)] for j in range(ydim)] for k in range(zdim)],
+                   dtype=np.float64)
+    return D.Dataset({"var": D.DataArray(var, ["z", "y", "x"],
+                                         coords={"z": range(zdim), "y": range(ydim), "x": range(xdim)})})
+
+
+@pytest.mark.parametrize("zdim", [1, 10])
+def test_stack_dims(zdim):
+    ds = _gridded(zdim)
+    out = stack(ds, unstacked_dims=Z_DIM_NAMES)
+    assert set(out.dims) == {SAMPLE_DIM_NAME, "z"}
+    assert out["var"].dims[0] == SAMPLE_DIM_NAME
+    assert out["var"].shape == (100, zdim)
+
+
+def test_stack_order_is_alphabetical_and_bit_exact():
+    """sample s = ix * ny + iy: stack dims are iterated sorted (x before y), C order."""
+    ds = _gridded(3, ydim=4, xdim=5)
+    out = stack(ds, unstacked_dims=["z"]).data_vars["var"].data
+    v = ds["var"].values  # (z, y, x)
+    for ix in range(5):
+        for iy in range(4):
+            np.testing.assert_array_equal(out[ix * 4 + iy], v[:, iy, ix])
+
+
+def test_stack_no_stacked_dims():
+    ds = _gridded(10)
+    out = stack(ds, unstacked_dims=["x", "y", "z"])
+    assert list(out["var"].dims) == [SAMPLE_DIM_NAME, "x", "y", "z"]
+    assert out["var"].shape[0] == 1
+
+
+def test_stack_no_unstacked_dims():
+    ds = _gridded(10)
+    out = stack(ds)
+    assert list(out["var"].dims) == [SAMPLE_DIM_NAME]
+    assert out["var"].shape[0] == 1000
+
+
+@pytest.mark.parametrize("dims", [("time", "x", "y", "z"), ("time", "z", "y", "x")])
+def test_multiple_unstacked_dims_are_alphabetically_ordered(dims):
+    ds = D.Dataset({"var1": D.DataArray(np.zeros([2, 12, 12, 15]), dims)})
+    out = stack(ds, unstacked_dims=["x", "y", "z"])
+    assert list(out["var1"].dims) == [SAMPLE_DIM_NAME, "x", "y", "z"]
+
+
+def test_stack_refuses_broadcast():
+    ds = D.Dataset({"a": D.DataArray(np.zeros((3, 4, 5)), ["z", "y", "x"]),
+                    "b": D.DataArray(np.zeros((3, 4)), ["z", "y"])})
+    with pytest.raises(ValueError, match="broadcast"):
+        stack(ds, unstacked_dims=["z"])
+
+
+def test_register_duplicate_name_raises():
+    with pytest.raises(ValueError, match="already registered"):
+        P.register("constant-output")(type("X", (), {}))
+
+
+def test_constant_output_predictor_roundtrip(tmp_path):
+    ds = D.Dataset({"a": D.DataArray(np.random.rand(5, 3, 4), ["z", "y", "x"]),
+                    "b": D.DataArray(np.random.rand(3, 4), ["y", "x"])})
+    p = P.ConstantOutputPredictor(["a", "b"], ["out_z", "out_s"])
+    p.set_outputs(out_z=np.arange(5.0), out_s=2.5)
+    out = p.predict(ds)
+    assert out["out_z"].dims == ("z", "y", "x")
+    assert out["out_s"].dims == ("y", "x")
+    np.testing.assert_array_equal(out["out_z"].values[:, 1, 2], np.arange(5.0))
+    assert (out["out_s"].values == 2.5).all()
+    P.dump(p, str(tmp_path / "m"))
+    with open(tmp_path / "m" / "name") as f:
+        assert f.read() == "constant-output"
+    q = P.load(str(tmp_path / "m"))
+    np.testing.assert_array_equal(q.predict(ds)["out_z"].values, out["out_z"].values)
+
+
+def test_constant_predictor_missing_input_raises_keyerror():
+    ds = D.Dataset({"a": D.DataArray(np.zeros((5, 3, 4)), ["z", "y", "x"])})
+    p = P.ConstantOutputPredictor(["a", "missing"], ["o"])
+    with pytest.raises(KeyError):
+        p.predict(ds)
+
+
+def test_predictor_rejects_unknown_kwargs():
+    with pytest.raises(TypeError):
+        P.ConstantOutputPredictor.__mro__[1].__init__(P.ConstantOutputPredictor(["a"], ["b"]), ["a"], ["b"],
+                                                     bogus=1)
+
+
+def test_dense_model_dump_load_roundtrip(tmp_path):
+    from fv3net_amd.dense import DenseColumnModel, DenseModelConfig
+
+    cfg = DenseModelConfig(["T", "q"], ["dQ1", "dQ2"], [7, 7], [7, 7], width=16, depth=3,
+                           clip={"T": (1, 6)}, output_limits={"dQ2": (None, 0.5)})
+    m = DenseColumnModel.random(cfg, seed=3, bias_scale=0.1)
+    pred = P.DenseColumnPredictor(cfg.input_variables, cfg.output_variables, m)
+    P.dump(pred, str(tmp_path / "dense"))
+    with open(tmp_path / "dense" / "name") as f:
+        assert f.read() == "mi355x-dense"
+    q = P.load(str(tmp_path / "dense"))
+    assert q.model.config == cfg
+    for k in ("hidden_kernels", "out_kernels", "in_mean", "out_sigma"):
+        for a, b in zip(m.params[k], q.model.params[k]):
+            np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.gpu
+def test_dense_predictor_end_to_end(gpu):
+    """DenseColumnPredictor.predict on a (z, y, x) state == the Keras graph applied
+    per column (oracle), same dims/coords as the input, float32."""
+    import torch
+
+    from fv3net_amd.dense import DenseColumnModel, DenseModelConfig
+    from oracle.dense import dense_predict
+
+    rng = np.random.default_rng(5)
+    nz, ny, nx = 79, 48, 48
+    T = rng.normal(260, 15, (nz, ny, nx)).astype(np.float64)
+    q = rng.uniform(0, 0.02, (nz, ny, nx)).astype(np.float64)
+    ps = rng.normal(1e5, 300, (ny, nx))
+    X = D.Dataset({"air_temperature": D.DataArray(T, ["z", "y", "x"], coords={"x": np.arange(nx)}),
+                   "specific_humidity": D.DataArray(q, ["z", "y", "x"]),
+                   "surface_pressure": D.DataArray(ps, ["y", "x"])})
+    cfg = DenseModelConfig(["air_temperature", "specific_humidity", "surface_pressure"],
+                           ["dQ1", "dQ2", "total_precip"], [79, 79, 1], [79, 79, 1], width=256, depth=3)
+    sT = T.transpose(1, 2, 0).reshape(-1, nz)
+    sq = q.transpose(1, 2, 0).reshape(-1, nz)
+    sps = ps.reshape(-1, 1)
+    m = DenseColumnModel.random(cfg, seed=2, sample_inputs=[sT, sq, sps], bias_scale=0.1)
+    pred = P.DenseColumnPredictor(cfg.input_variables, cfg.output_variables, m)
+    out = pred.predict(X)
+    assert out["dQ1"].dims == ("z", "y", "x") and out["total_precip"].dims == ("y", "x")
+    assert out["dQ1"].values.dtype == np.float32
+    ref = dense_predict([sT, sq, sps], m.oracle_params(), np.float64)
+    got1 = out["dQ1"].values.transpose(1, 2, 0).reshape(-1, nz)
+    got3 = out["total_precip"].values.reshape(-1, 1)
+    for g, r in ((got1, ref[0]), (got3, ref[2])):
+        assert np.abs(g - r).max() / np.abs(r).max() <= 1e-5
+    np.testing.assert_array_equal(out.coords["x"], np.arange(nx))
+    # device-resident input stays on device
+    Xd = D.Dataset({k: D.DataArray(torch.from_numpy(X[k].values.astype(np.float32)).cuda(), X[k].dims)
+                    for k in X})
+    outd = pred.predict(Xd)
+    assert isinstance(outd["dQ1"].data, torch.Tensor) and outd["dQ1"].data.is_cuda
+    with pytest.raises(KeyError):
+        pred.predict(D.Dataset({"air_temperature": X["air_temperature"]}))

@@ -14,6 +14,7 @@ gfx950 correction of MI355X_MICROARCH.md §HBM (FETCH_SIZE counts half of the by
 of wide coalesced streaming reads).  Both raw counters are kept in the summary.
 """
 import csv
+import re
 import json
 import os
 import shutil
@@ -24,8 +25,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
-    for key in ("dense_forward_kernel<16>", "dense_forward_kernel<8>", "dense_forward_kernel<4>",
-                "mappm_ppm_kernel", "mappm_cs_kernel", "regrid_coarsen", "column_integral",
+    m = re.search(r"dense_forward_kernel<[^>]*>", name)
+    if m:
+        return m.group(0).replace(" ", "")
+    for key in ("mappm_ppm_kernel", "mappm_cs_kernel", "regrid_coarsen", "column_integral",
                 "area_sums"):
         if key in name:
             return key
@@ -94,16 +97,17 @@ def main():
                   "```", json.dumps({k: bench.get(k) for k in ("value", "ms_per_step", "roofline")}), "```"]
     with open(os.path.join(prof, f"{tag}_summary.md"), "w") as fh:
         fh.write("\n".join(lines) + "\n")
-    # dominant kernel of the default bench (C48 predict): grid = ceil(13824/16/4) blocks * 256
-    c48_grid = ((13824 + 15) // 16 + 3) // 4 * 256
-    dom = summary.get(f"dense_forward_kernel<16>@{c48_grid}")
+    # dominant kernel of the default bench (C48 predict): the dense kernel launched
+    # with one block per 32 columns -> grid = ceil(13824/32) blocks * 256 threads
+    c48_grid = (13824 + 31) // 32 * 256
+    dom = None
+    for k, v in summary.items():
+        if k.startswith("dense_forward_kernel") and k.endswith(f"@{c48_grid}"):
+            dom = v
     traffic = {}
     tpath = os.path.join(prof, "pmc_traffic.json")
-    if os.path.exists(tpath):
-        with open(tpath) as fh:
-            traffic = json.load(fh)
     if dom and dom["hbm_bytes_per_launch"] is not None:
-        traffic["dense_forward_kernel<16>"] = {"hbm_bytes_per_launch": dom["hbm_bytes_per_launch"],
+        traffic["dense_c48"] = {"hbm_bytes_per_launch": dom["hbm_bytes_per_launch"],
                                                "fetch_kib": dom["fetch_kib"], "write_kib": dom["write_kib"],
                                                "workload": "C48 bench step", "profile": tag}
     with open(tpath, "w") as fh:
