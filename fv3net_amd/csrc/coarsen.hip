@@ -14,12 +14,18 @@
 //
 // Mapping: one wave per coarse cell; lane (dy, dx) owns fine column (f*Y+dy, f*X+dx)
 // (f <= 8, lanes >= f*f idle).  Pass 1 streams delp once: every lane keeps its own
-// float64 cumsum (fine phalf; the surface value is kept for the mask), and a fixed
-// xor-shuffle tree forms sum(delp*area) per level -> delp_c and the coarse phalf
-// (float64, identical on every lane; stored in LDS).  Per field: each lane runs the
-// one-pass streaming mappm (mappm_core.h) with p_in recomputed from L2-hot delp,
-// stages its remapped column in LDS [level][65] (padded: conflict-free), then lane k
-// reduces level k over the block in a fixed order.  Deterministic run to run.
+// cumsum (fine phalf; the surface value is kept for the mask) and stages delp*area in
+// LDS, 16 levels at a time, from which delp_c and the coarse phalf are formed.  Per
+// field: each lane runs the one-pass streaming mappm (mappm_core.h) with p_in
+// recomputed from L2-hot delp, stages its remapped column in LDS [level][65]
+// (padded: conflict-free), then lane k reduces level k over the block.
+//
+// Arithmetic follows the reference's dtype flow exactly (oracle/coarsen.py): delp
+// products, sums, delp_c and both cumsums in delp's dtype DT (float64 for restart
+// data), area and masked-field sums in float32, and every f x f block sum in
+// numpy's order for a C-order (.., Y, f, X, f) reshape summed over the two f axes:
+// each x-row reduced on its own (sequentially for f < 8, numpy's 8-way pairwise
+// kernel for f = 8), rows then added in y order.  Deterministic run to run.
 // Roofline: HBM-bound, (79 delp + 79*n_fields + 1 area) * 4 B per fine column read
 // once (+ ~4/f^2 of that written); delp is re-read per field from L2, not HBM.
 #define FV3_HD __host__ __device__
@@ -46,32 +52,48 @@ struct CoarsenArgs {
     double ptop;
 };
 
-__device__ __forceinline__ double wave_sum(double v)
+constexpr int kChunk = 16;   // delp*area levels staged per pass-1 round
+
+// numpy's np.sum over the two f axes of a C-order (.., Y, f, X, f) block: val(j) is
+// element j = dy*f + dx.  A reduced contiguous row goes through pairwise_sum
+// (n < 8: sequential; n == 8: eight partials combined as a fixed tree) and is added
+// to the running sum.
+template <typename T, typename V>
+__device__ __forceinline__ T block_sum(int f, V val)
 {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+    auto row = [&](int r) -> T {
+        const int b = r * f;
+        if (f == 8)
+            return ((val(b) + val(b + 1)) + (val(b + 2) + val(b + 3))) +
+                   ((val(b + 4) + val(b + 5)) + (val(b + 6) + val(b + 7)));
+        T s = val(b);
+        for (int c = 1; c < f; ++c) s = s + val(b + c);
+        return s;
+    };
+    T acc = row(0);
+    for (int r = 1; r < f; ++r) acc = acc + row(r);
+    return acc;
 }
 
-// fine column of this lane: p_in streamed from a running float64 cumsum of delp
+// fine column of this lane: p_in streamed from a running cumsum of delp (in DT)
 template <typename DT>
 struct FineCol {
     const float* q;   // field at level 0 of this column
     const DT* dp;     // delp at level 0 of this column
     int64_t plane;    // ny*nx
-    const double* pc; // coarse phalf[k], k = 0..km (LDS)
+    const DT* pc;     // coarse phalf[k], k = 0..km (LDS)
     float* stage;     // LDS staging, this lane's column: stage[k * kStride]
-    double ptop, pbot, run;
+    DT ptop, pbot, run;
     int next;         // next fine interface index (0-based) the running sum will produce
     int km, kn;
     __device__ __forceinline__ float q1(int k) const { return q[(int64_t)(k - 1) * plane]; }
     __device__ __forceinline__ float pe1(int k)
     {
-        // reference: phalf = cumsum([ptop, delp]) in float64, cast to float32 by f2py
+        // reference: phalf = cumsum([ptop, delp]) in delp's dtype, cast to float32 by f2py
         if (k == 1) return (float)ptop;
         if (k == km + 1) return (float)pbot;
         while (next < k - 1) {  // interface k-1 (0-based) = ptop + sum delp[0..k-2]
-            run += (double)dp[(int64_t)next * plane];
+            run = run + dp[(int64_t)next * plane];
             ++next;
         }
         return (float)run;
@@ -85,19 +107,21 @@ template <typename DT>
 __global__ __launch_bounds__(64) void regrid_coarsen_kernel(CoarsenArgs<DT> a)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    double* pc = reinterpret_cast<double*>(smem);                    // [km+1] coarse phalf
-    double* lpb = reinterpret_cast<double*>(smem + kOffPb);          // [64] fine surface phalf
+    DT* pc = reinterpret_cast<DT*>(smem);                            // [km+1] coarse phalf
+    DT* lpb = reinterpret_cast<DT*>(smem + kOffPb);                  // [64] fine surface phalf
     float* lar = reinterpret_cast<float*>(smem + kOffArea);          // [64] fine area
     float* stage = reinterpret_cast<float*>(smem + kOffStage);       // [km][kStride]
+    DT* pstage = reinterpret_cast<DT*>(smem + kOffStage);            // pass 1: [kChunk][kStride]
 
     const int lane = threadIdx.x;
     const int f = a.f;
+    const int nn = f * f;
     const int nyc = a.ny / f, nxc = a.nx / f;
     const int64_t cell = blockIdx.x;
     const int tile = (int)(cell / ((int64_t)nyc * nxc));
     const int rem = (int)(cell - (int64_t)tile * nyc * nxc);
     const int Y = rem / nxc, X = rem - (rem / nxc) * nxc;
-    const bool active = lane < f * f;
+    const bool active = lane < nn;
     const int dy = active ? lane / f : 0, dx = active ? lane - (lane / f) * f : 0;
     const int64_t plane = (int64_t)a.ny * a.nx;
     const int64_t fine = (int64_t)(Y * f + dy) * a.nx + (X * f + dx);
@@ -106,26 +130,36 @@ __global__ __launch_bounds__(64) void regrid_coarsen_kernel(CoarsenArgs<DT> a)
     const int km = a.km;
 
     // ---- pass 1: fine phalf (per lane) and area-weighted coarse delp / phalf ----
-    const double area = active ? (double)a.area[(int64_t)tile * plane + fine] : 0.0;
-    const double asum = wave_sum(area);
+    const float area = active ? a.area[(int64_t)tile * plane + fine] : 0.0f;
+    lar[lane] = area;
+    __syncthreads();
+    // weights.coarsen().sum(): float32 (area's dtype)
+    const float asum = block_sum<float>(f, [&](int j) { return lar[j]; });
     const DT* dp = a.delp + (int64_t)tile * km * plane + fine;
-    double run = a.ptop;   // fine phalf, float64 cumsum (vertically_dependent.py:62-63)
-    double pcr = a.ptop;   // coarse phalf
-    if (lane == 0) pc[0] = a.ptop;
-    for (int k = 0; k < km; ++k) {
-        const double d = (double)dp[(int64_t)k * plane];
-        run += d;
-        const double num = wave_sum(active ? d * area : 0.0);
-        const double dc = num / asum;  // weighted_block_average: sum(delp*area)/sum(area)
-        pcr += dc;
-        if (lane == 0) {
-            pc[k + 1] = pcr;
-            if (a.delp_out) a.delp_out[((int64_t)tile * km + k) * cplane + cidx] = (float)dc;
+    const DT ptop = (DT)a.ptop;
+    DT run = ptop;  // fine phalf = cumsum([ptop, delp]) (vertically_dependent.py:62-63)
+    for (int k0 = 0; k0 < km; k0 += kChunk) {
+        const int nk = min(kChunk, km - k0);
+        for (int kk = 0; kk < nk; ++kk) {
+            const DT d = active ? dp[(int64_t)(k0 + kk) * plane] : (DT)0;
+            run = run + d;
+            pstage[kk * kStride + lane] = d * (DT)area;  // (delp * area) in delp's dtype
         }
+        __syncthreads();
+        if (lane < nk) {
+            const DT num = block_sum<DT>(f, [&](int j) { return pstage[lane * kStride + j]; });
+            const DT dc = num / (DT)asum;  // weighted_block_average (coarsen.py:213-215)
+            pc[k0 + lane + 1] = dc;
+            if (a.delp_out) a.delp_out[((int64_t)tile * km + k0 + lane) * cplane + cidx] = (float)dc;
+        }
+        __syncthreads();
     }
-    const double pbot = run;  // phalf_fine[-1] of this fine column
+    if (lane == 0) {  // coarse phalf = cumsum([ptop, delp_c]), sequential like np.cumsum
+        pc[0] = ptop;
+        for (int k = 0; k < km; ++k) pc[k + 1] = pc[k] + pc[k + 1];
+    }
+    const DT pbot = run;  // phalf_fine[-1] of this fine column
     lpb[lane] = pbot;
-    lar[lane] = active ? (float)area : 0.0f;
     __syncthreads();
 
     // ---- per field: remap every fine column, then masked area-weighted block mean ----
@@ -136,9 +170,9 @@ __global__ __launch_bounds__(64) void regrid_coarsen_kernel(CoarsenArgs<DT> a)
         c.plane = plane;
         c.pc = pc;
         c.stage = stage + lane;
-        c.ptop = a.ptop;
+        c.ptop = ptop;
         c.pbot = pbot;
-        c.run = a.ptop;
+        c.run = ptop;
         c.next = 0;
         c.km = km;
         c.kn = km;
@@ -147,16 +181,14 @@ __global__ __launch_bounds__(64) void regrid_coarsen_kernel(CoarsenArgs<DT> a)
         // lane j reduces levels k = j, j+64, ... over the block's fine columns in a fixed order
         float* o = a.out[v] + (int64_t)tile * km * cplane + cidx;
         for (int k = lane; k < km; k += 64) {
-            const double pk = pc[k + 1];
-            double num = 0.0, den = 0.0;
-            for (int j = 0; j < f * f; ++j) {
-                // _mask_weights: area where phalf_c_on_f[k+1] < phalf_f[-1] (float64 compare);
-                // the masked area keeps area's float32 dtype, products/sums per coarsen.py
-                const float w = (pk < lpb[j]) ? lar[j] : 0.0f;
-                num += (double)(stage[k * kStride + j] * w);
-                den += (double)w;
-            }
-            o[(int64_t)k * cplane] = (float)(num / den);
+            // _mask_weights (regridz.py:150-161): area where phalf_c_on_f[k+1] < phalf_f[-1]
+            // (compared in delp's dtype); the masked area stays float32, so the product,
+            // both block sums and the quotient are float32 (coarsen.py:213-215)
+            const DT pk = pc[k + 1];
+            const float* sk = stage + k * kStride;
+            const float num = block_sum<float>(f, [&](int j) { return sk[j] * ((pk < lpb[j]) ? lar[j] : 0.0f); });
+            const float den = block_sum<float>(f, [&](int j) { return (pk < lpb[j]) ? lar[j] : 0.0f; });
+            o[(int64_t)k * cplane] = num / den;
         }
         __syncthreads();
     }
@@ -207,7 +239,7 @@ int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* f
     a.kord = kord;
     a.ptop = ptop_toa;
     const int64_t cells = (int64_t)ntile * (ny / factor) * (nx / factor);
-    const size_t lds = kOffStage + sizeof(float) * (size_t)km * kStride;
+    const size_t lds = kOffStage + std::max(sizeof(float) * (size_t)km * kStride, sizeof(DT) * kChunk * kStride);
     hipLaunchKernelGGL(regrid_coarsen_kernel<DT>, dim3((unsigned)cells), dim3(64), lds, s, a);
     FV3_LAUNCH_CHECK();
     if (dtab) FV3_HIP(hipFreeAsync(dtab, s));

@@ -71,8 +71,17 @@ def test_oracle_mask_weights_kat():
     np.testing.assert_allclose(got, expected)
 
 
+def _bits_equal(a, b):
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    assert a.shape == b.shape
+    bad = a.view(np.uint32) != b.view(np.uint32)
+    assert not bad.any(), f"{bad.sum()} / {bad.size} differ, e.g. {a[bad][:4]} vs {b[bad][:4]}"
+
+
 @pytest.mark.gpu
 def test_kernel_reproduces_reference_kat(gpu):
+    """float64 delp (as in the restart files): within the reference test's own
+    tolerance of its regression data, and bit-identical to the oracle."""
     from fv3net_amd.coarsen import coarsen_on_pressure
 
     delp, area, T = _kat_inputs()
@@ -80,8 +89,9 @@ def test_kernel_reproduces_reference_kat(gpu):
     got = out["T"].cpu().numpy()
     np.testing.assert_allclose(got, _expected(), rtol=1e-5, atol=1e-8)
     np.testing.assert_array_equal(got, out["W"].cpu().numpy())
-    np.testing.assert_allclose(delp_c.cpu().numpy(), OC.weighted_block_average(delp, area[:, None], FACTOR),
-                               rtol=1e-6)
+    (ref,), ref_dc = OC.coarsen_on_pressure(delp, area, [T], FACTOR)
+    _bits_equal(got, ref)
+    _bits_equal(delp_c.cpu().numpy(), ref_dc)
 
 
 def _smooth_state(rng, nt, km, ny, nx):
@@ -95,18 +105,40 @@ def _smooth_state(rng, nt, km, ny, nx):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("factor,n", [(2, 16), (4, 24), (8, 48)])
-def test_kernel_vs_oracle_random(gpu, factor, n):
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("factor,n", [(1, 4), (2, 16), (3, 12), (4, 24), (8, 48)])
+def test_kernel_vs_oracle_random(gpu, factor, n, dtype):
+    """Bit-identical to the oracle for every factor (numpy's block-sum order) and
+    both delp dtypes (the arithmetic follows delp's dtype, as the reference does)."""
     from fv3net_amd.coarsen import coarsen_on_pressure
 
     rng = np.random.default_rng(factor * 100 + n)
     delp, area, T, q = _smooth_state(rng, 6, 79, n, n)
+    delp = delp.astype(dtype)
     out, delp_c = coarsen_on_pressure(delp, area, {"T": T, "q": q}, factor)
-    ref, ref_dc = OC.coarsen_on_pressure(delp.astype(np.float64), area, [T, q], factor)
+    ref, ref_dc = OC.coarsen_on_pressure(delp, area, [T, q], factor)
     for name, r in zip(("T", "q"), ref):
-        g = out[name].cpu().numpy()
-        np.testing.assert_allclose(g, r, rtol=1e-5, atol=1e-8 * np.abs(r).max())
-    np.testing.assert_allclose(delp_c.cpu().numpy(), ref_dc, rtol=1e-6)
+        _bits_equal(out[name].cpu().numpy(), r)
+    _bits_equal(delp_c.cpu().numpy(), ref_dc)
+
+
+@pytest.mark.gpu
+def test_kernel_masked_levels_and_kord(gpu):
+    """Strongly varying surface pressure so the mask drops fine columns at the lowest
+    coarse levels; iv/kord variants of the PPM path; kord > 7 is refused loudly."""
+    from fv3net_amd.coarsen import coarsen_on_pressure
+
+    rng = np.random.default_rng(7)
+    delp, area, T, q = _smooth_state(rng, 2, 40, 16, 16)
+    delp[:, -5:] *= rng.uniform(0.2, 3.0, (2, 1, 16, 16)).astype(np.float32)
+    for iv, kord in ((1, 1), (0, 4), (1, 6), (-1, 7)):
+        out, _ = coarsen_on_pressure(delp, area, {"q": q}, 4, iv=iv, kord=kord)
+        (r,), _ = OC.coarsen_on_pressure(delp, area, [q], 4, iv=iv, kord=kord)
+        _bits_equal(out["q"].cpu().numpy(), r)
+    with pytest.raises(NotImplementedError):
+        coarsen_on_pressure(delp, area, {"q": q}, 4, kord=9)
+    with pytest.raises(ValueError):
+        coarsen_on_pressure(delp[..., :15], area[..., :15], {"q": q[..., :15]}, 4)
 
 
 @pytest.mark.gpu
@@ -126,8 +158,8 @@ def test_kernel_c384_to_c48_sampled_and_deterministic(gpu):
     assert (a.view(np.uint32) == b.view(np.uint32)).all()
     assert np.isfinite(a).all()
     sl = (slice(2, 3), slice(None), slice(64, 128), slice(192, 256))  # one tile, 8x8 coarse cells
-    (r,), _ = OC.coarsen_on_pressure(delp[sl].astype(np.float64), area[2:3, 64:128, 192:256], [T[sl]], 8)
-    np.testing.assert_allclose(a[2:3, :, 8:16, 24:32], r, rtol=1e-5, atol=1e-5)
+    (r,), _ = OC.coarsen_on_pressure(delp[sl], area[2:3, 64:128, 192:256], [T[sl]], 8)
+    _bits_equal(a[2:3, :, 8:16, 24:32], r)
 
 
 @pytest.mark.gpu
