@@ -14,9 +14,9 @@ collective) -> "scaling": "weak"; value = all ranks' columns / max-over-ranks ti
 
 Rank 0 prints ONE JSON line on stdout (everything else goes to stderr), with
   roofline:     the fused kernel's algorithmic FLOP per launch / its mean launch
-                duration (HIP events on the kernel's own stream, inside the timed
-                region) vs the f32 MFMA peak; traffic = HBM bytes per launch from the
-                committed rocprofv3 PMC pass (profiles/), or null;
+                duration (two HIP events on the kernel's own stream bracketing the K
+                timed launches) vs the f32 MFMA peak; traffic = HBM bytes per launch
+                from the committed rocprofv3 PMC pass (profiles/), or null;
   cpu_baseline: the numpy restatement of the same graph (oracle/dense.py) on the
                 host cores, Keras-style batch_size=32 chunks (pure_keras.py:112 calls
                 model.predict without batch_size), on a bounded sample (N=1, rank 0);
@@ -54,7 +54,11 @@ def parse():
 
 def timed_steps(step, steps, warmup, dist=None):
     """W untimed steps, then exactly K timed steps bracketed by barrier + sync.
-    Returns (wall seconds, per-launch kernel seconds from HIP events)."""
+    Returns (wall seconds, mean seconds per launch).  The launch time comes from two
+    HIP events recorded on the stream the kernels run on (torch's current stream,
+    which the product passes to every launch) around the K back-to-back launches:
+    each step is exactly one kernel, so span / K is its average duration.  Events per
+    launch would add ~6 us of queue overhead per step to the wall clock."""
     import torch
 
     for _ in range(warmup):
@@ -63,20 +67,19 @@ def timed_steps(step, steps, warmup, dist=None):
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for i in range(steps):
-        starts[i].record()  # current stream == the stream the kernel is launched on
+    e0.record()
+    for _ in range(steps):
         step()
-        ends[i].record()
+    e1.record()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kern = [s.elapsed_time(e) * 1e-3 for s, e in zip(starts, ends)]
-    return wall, kern
+    return wall, e0.elapsed_time(e1) * 1e-3 / steps
 
 
 def pmc_traffic(kernel_key):
@@ -134,8 +137,7 @@ def extra_measurements(dev):
     out = {}
     # config #2 at C384 (one GPU, 884,736 columns): MFMA-bound predict
     wl = W.make_dense_workload(384, seed=3, device=dev)
-    wall, kern = timed_steps(wl.step, 10, 3)
-    t = float(np.mean(kern))
+    wall, t = timed_steps(wl.step, 10, 3)
     out["dense_c384"] = {
         "columns_per_s": wl.ncol / t, "ms_per_step": t * 1e3,
         "tflops": wl.ncol * wl.flops_per_column / t / 1e12,
@@ -147,11 +149,19 @@ def extra_measurements(dev):
                                  ("mappm_c384_79to79_kord10", W.c_columns(384), 79, 10),
                                  ("mappm_c12_79to50_kord1", W.c_columns(12), 50, 1)):
         wl = W.make_mappm_workload(ncol, 79, kn, kord, seed=5, device=dev)
-        wall, kern = timed_steps(wl.step, 10, 3)
-        t = float(np.mean(kern))
+        wall, t = timed_steps(wl.step, 10, 3)
         gbs = wl.bytes_per_column * ncol / t / 1e9
         out[name] = {"columns_per_s": ncol / t, "ms_per_step": t * 1e3, "hbm_gbs": gbs,
                      "frac_hbm_peak": gbs / W.HBM_PEAK_GBS}
+        del wl
+    # config #3: fused C384 -> C48 pressure-level coarsen (1 and 4 fields), fine columns/s
+    for nf in (1, 4):
+        wl = W.make_coarsen_workload(384, 8, nf, seed=7, device=dev)
+        wall, t = timed_steps(wl.step, 10, 3)
+        gbs = wl.bytes_per_column * wl.ncol_fine / t / 1e9
+        out[f"coarsen_c384_to_c48_{nf}field"] = {
+            "fine_columns_per_s": wl.ncol_fine / t, "ms_per_step": t * 1e3, "hbm_gbs": gbs,
+            "frac_hbm_peak": gbs / W.HBM_PEAK_GBS}
         del wl
     torch.cuda.empty_cache()
     return out
@@ -177,14 +187,13 @@ def main():
     from fv3net_amd import workloads as W
 
     wl = W.make_dense_workload(args.res, seed=1000 + rank, device=dev)
-    wall, kern = timed_steps(wl.step, args.steps, args.warmup, dist)
+    wall, kmean = timed_steps(wl.step, args.steps, args.warmup, dist)
     if dist is not None:
         t = torch.tensor([wall], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
     total_cols = wl.ncol * world * args.steps
     value = total_cols / wall
-    kmean = float(np.mean(kern))
     flops_launch = wl.ncol * wl.flops_per_column
     achieved = flops_launch / kmean / 1e12
 

@@ -36,6 +36,7 @@ namespace fv3 {
 namespace {
 
 constexpr int kMaxLev = 128;
+constexpr int kMaxFields = 32;  // field/output pointers travel in the kernel arguments
 constexpr int kStride = 65;  // LDS row stride (floats) of the per-field staging buffer
 constexpr int kOffPb = 1040;                    // after pc[kMaxLev + 1] doubles, 16-aligned
 constexpr int kOffArea = kOffPb + 64 * 8;
@@ -45,8 +46,8 @@ template <typename DT>
 struct CoarsenArgs {
     const DT* delp;
     const float* area;
-    const float* const* fields;
-    float* const* out;
+    const float* fields[kMaxFields];
+    float* out[kMaxFields];
     float* delp_out;
     int n_fields, ntile, km, ny, nx, f, iv, kord;
     double ptop;
@@ -208,26 +209,23 @@ int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* f
     FV3_REQUIRE(factor >= 1 && factor <= 8, "regrid_coarsen: coarsening factor must be in [1, 8]");
     FV3_REQUIRE(ny % factor == 0 && nx % factor == 0, "regrid_coarsen: %dx%d not divisible by factor %d", ny, nx,
                 factor);
-    FV3_REQUIRE(n_fields >= 0 && n_fields <= 64, "regrid_coarsen: n_fields must be in [0, 64]");
+    FV3_REQUIRE(n_fields >= 0 && n_fields <= kMaxFields, "regrid_coarsen: n_fields must be in [0, %d]",
+                kMaxFields);
     FV3_REQUIRE(delp && area, "regrid_coarsen: NULL delp/area");
     if (kord > 7) {
         set_error("regrid_coarsen: kord > 7 (cs_profile) is not fused in this build; use fv3_mappm_ex");
         return FV3_ERR_UNSUPPORTED;
     }
     hipStream_t s = (hipStream_t)stream;
-    const size_t tab = sizeof(void*) * (size_t)std::max(n_fields, 1);
-    void* dtab = nullptr;
-    if (n_fields > 0) {
-        FV3_REQUIRE(fields && out, "regrid_coarsen: NULL field tables");
-        FV3_HIP(hipMallocAsync(&dtab, 2 * tab, s));
-        FV3_HIP(hipMemcpyAsync(dtab, fields, tab, hipMemcpyHostToDevice, s));
-        FV3_HIP(hipMemcpyAsync((char*)dtab + tab, out, tab, hipMemcpyHostToDevice, s));
+    CoarsenArgs<DT> a{};
+    if (n_fields > 0) FV3_REQUIRE(fields && out, "regrid_coarsen: NULL field tables");
+    for (int v = 0; v < n_fields; ++v) {
+        FV3_REQUIRE(fields[v] && out[v], "regrid_coarsen: NULL field/output %d", v);
+        a.fields[v] = fields[v];
+        a.out[v] = out[v];
     }
-    CoarsenArgs<DT> a;
     a.delp = delp;
     a.area = area;
-    a.fields = (const float* const*)dtab;
-    a.out = (float* const*)((char*)dtab + tab);
     a.delp_out = delp_out;
     a.n_fields = n_fields;
     a.ntile = ntile;
@@ -242,7 +240,6 @@ int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* f
     const size_t lds = kOffStage + std::max(sizeof(float) * (size_t)km * kStride, sizeof(DT) * kChunk * kStride);
     hipLaunchKernelGGL(regrid_coarsen_kernel<DT>, dim3((unsigned)cells), dim3(64), lds, s, a);
     FV3_LAUNCH_CHECK();
-    if (dtab) FV3_HIP(hipFreeAsync(dtab, s));
     return FV3_OK;
 }
 

@@ -250,10 +250,17 @@ class DenseColumnPredictor(Predictor):
             lv = _level_dim(da.dims, self._unstacked_dims)
             if set(d for d in da.dims if d != lv) != set(col_dims):
                 raise ValueError(f"{name} dims {da.dims} do not share the horizontal dims {col_dims}")
-            order = ([lv] if lv else []) + col_dims
             data = dsmod.variable_data(X, name)
+            is_torch = torch is not None and isinstance(data, torch.Tensor)
+            if lv and [d for d in da.dims if d != lv] == col_dims:
+                # horizontal dims already in column order: the kernel reads the array in
+                # place with the level axis where it is, e.g. (tile, z, y, x)
+                tensors.append(data if is_torch else np.asarray(data))
+                axes.append(da.dims.index(lv))
+                continue
+            order = ([lv] if lv else []) + col_dims
             perm = [da.dims.index(d) for d in order]
-            if torch is not None and isinstance(data, torch.Tensor):
+            if is_torch:
                 t = data.permute(*perm) if perm != list(range(len(perm))) else data
             else:
                 t = np.transpose(np.asarray(data), perm) if perm != list(range(len(perm))) else np.asarray(data)
@@ -263,6 +270,7 @@ class DenseColumnPredictor(Predictor):
         # back to the input's dim order (match_prediction_to_input_coords)
         order = dsmod.infer_dimension_order(X)
         result = {}
+        ax0 = axes[0]  # the outputs carry their level axis where the first input had it
         for o, name in enumerate(self.output_variables):
             nz = cfg.out_nz[o]
             t = outs[o]
@@ -270,7 +278,8 @@ class DenseColumnPredictor(Predictor):
                 dims = list(col_dims)
                 t = t.reshape(col_shape)
             else:
-                dims = [self._unstacked_dims[0]] + list(col_dims)
+                dims = list(col_dims)
+                dims.insert(ax0, self._unstacked_dims[0])
             tgt = [d for d in order if d in dims] + [d for d in dims if d not in order]
             t = t.permute(*[dims.index(d) for d in tgt]).contiguous()
             result[name] = (tgt, t)

@@ -115,3 +115,39 @@ def make_mappm_workload(ncol: int, km: int = NZ, kn: int = NZ, kord: int = 1, se
     q1 = torch.randn((km, ncol), generator=g, device=device) * 10.0 + 250.0
     q2 = torch.empty((kn, ncol), device=device)
     return MappmWorkload(pe1.contiguous(), q1, pe2.contiguous(), q2, ncol, km, kn, kord)
+
+
+@dataclasses.dataclass
+class CoarsenWorkload:
+    """BASELINE config #3: C384 -> C48 (f = 8) pressure-level coarsen of T, 79 levels."""
+    delp: object
+    area: object
+    fields: dict
+    factor: int
+    ncol_fine: int
+    km: int
+
+    @property
+    def bytes_per_column(self) -> float:
+        """Algorithmic HBM bytes per FINE column: delp + fields + area read once,
+        coarse fields + coarse delp written (636 B + writes)."""
+        nf = len(self.fields)
+        return 4.0 * (self.km * (1 + nf) + 1) + 4.0 * self.km * (nf + 1) / self.factor ** 2
+
+    def step(self):
+        from .coarsen import coarsen_on_pressure
+
+        return coarsen_on_pressure(self.delp, self.area, self.fields, self.factor)
+
+
+def make_coarsen_workload(res: int = 384, factor: int = 8, nfields: int = 1, seed: int = 0, device=None):
+    """delp ~ D(k) * U(0.99, 1.01) (79-level profile), area ~ U(0.5, 1), T ~ N(250, 10); float32."""
+    device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    shape = (6, NZ, res, res)
+    base = torch.linspace(200.0, 1800.0, NZ, device=device)[None, :, None, None]
+    delp = base * (0.99 + 0.02 * torch.rand(shape, generator=g, device=device))
+    area = 0.5 + 0.5 * torch.rand((6, res, res), generator=g, device=device)
+    fields = {f"f{i}": torch.randn(shape, generator=g, device=device) * 10.0 + 250.0 for i in range(nfields)}
+    return CoarsenWorkload(delp, area, fields, factor, 6 * res * res, NZ)

@@ -116,8 +116,11 @@ int fv3_dense_forward(const fv3_dense_model* model, const float* const* inputs,
  *   out = sum(f_r*w)/sum(w) per level                      (coarsen.py:183-218)
  * delp, fields: (tile, km, ny, nx) float32; area (tile, ny, nx); out (tile, km, ny/f, nx/f);
  * delp_out (tile, km, ny/f, nx/f) receives delp_c (area-weighted, not masked).
- * phalf is accumulated in float64 and rounded once (bit-exact to the reference
- * running on float64 restart data). */
+ * fields/out are HOST arrays of n_fields <= 32 device pointers (passed by value to the
+ * kernel, nothing is allocated per call); 4 <= km <= 128, 1 <= factor <= 8, kord <= 7.
+ * Arithmetic follows the reference's dtype flow: delp products, delp_c and the phalf
+ * cumsums in delp's dtype, area and field sums in float32, block sums in numpy's
+ * order for the reshaped coarsen().sum() — bit-exact to oracle/coarsen.py. */
 int fv3_regrid_coarsen(const float* delp, const float* area, const float* const* fields,
                        float* const* out, int n_fields, float* delp_out, int ntile, int km,
                        int ny, int nx, int factor, int iv, int kord, double ptop_toa,

@@ -160,3 +160,46 @@ def test_dense_predictor_end_to_end(gpu):
     assert isinstance(outd["dQ1"].data, torch.Tensor) and outd["dQ1"].data.is_cuda
     with pytest.raises(KeyError):
         pred.predict(D.Dataset({"air_temperature": X["air_temperature"]}))
+
+
+def test_load_without_name_file_tries_every_registered_type(tmp_path):
+    """io.py:76-88: a missing ``name`` file warns and tries each registered class."""
+    ds = D.Dataset({"a": D.DataArray(np.random.rand(5, 3, 4), ["z", "y", "x"])})
+    p = P.ConstantOutputPredictor(["a"], ["o"])
+    p.set_outputs(o=np.arange(5.0))
+    P.dump(p, str(tmp_path / "m"))
+    (tmp_path / "m" / "name").unlink()
+    with pytest.warns(UserWarning, match="one-by-one"):
+        q = P.load(str(tmp_path / "m"))
+    np.testing.assert_array_equal(q.predict(ds)["o"].values, p.predict(ds)["o"].values)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dims", [("tile", "z", "y", "x"), ("y", "x", "z")])
+def test_dense_predictor_level_axis_anywhere(gpu, dims):
+    """(tile, z, y, x) is read in place (level axis 1); (y, x, z) goes through the
+    permute path.  Output dims follow the input's order; values == per-column oracle."""
+    import torch
+
+    from fv3net_amd.dense import DenseColumnModel, DenseModelConfig
+    from oracle.dense import dense_predict
+
+    rng = np.random.default_rng(11)
+    sizes = {"tile": 2, "z": 9, "y": 5, "x": 6}
+    shape = [sizes[d] for d in dims]
+    T = rng.normal(260, 15, shape).astype(np.float32)
+    q = rng.uniform(0, 0.02, shape).astype(np.float32)
+    X = D.Dataset({"T": D.DataArray(torch.from_numpy(T).cuda(), list(dims)),
+                   "q": D.DataArray(torch.from_numpy(q).cuda(), list(dims))})
+    cfg = DenseModelConfig(["T", "q"], ["dQ1", "pr"], [9, 9], [9, 1], width=64, depth=3)
+    zax = dims.index("z")
+    cols = lambda a: np.moveaxis(a, zax, -1).reshape(-1, 9)
+    m = DenseColumnModel.random(cfg, seed=4, sample_inputs=[cols(T), cols(q)], bias_scale=0.1)
+    out = P.DenseColumnPredictor(cfg.input_variables, cfg.output_variables, m).predict(X)
+    assert out["dQ1"].dims == tuple(dims)
+    assert out["pr"].dims == tuple(d for d in dims if d != "z")
+    ref = dense_predict([cols(T), cols(q)], m.oracle_params(), np.float64)
+    g1 = cols(out["dQ1"].data.cpu().numpy())
+    g2 = out["pr"].data.cpu().numpy().reshape(-1, 1)
+    for g, r in ((g1, ref[0]), (g2, ref[1])):
+        assert np.abs(g - r).max() / np.abs(r).max() <= 1e-5
