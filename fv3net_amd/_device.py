@@ -23,15 +23,29 @@ def stream_handle(stream=None) -> int:
     return int(s.cuda_stream)
 
 
-def to_device_f32(x, device=None):
-    """numpy / torch -> contiguous float32 CUDA tensor (copy only when needed)."""
+def to_device_f32(x, device=None, contiguous: bool = True):
+    """numpy / torch -> float32 CUDA tensor (copy only when needed).  With
+    ``contiguous=False`` a float32 CUDA view is returned as is (strides kept)."""
     require_gpu()
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
     if isinstance(x, torch.Tensor):
         t = x.to(device=dev, dtype=torch.float32)
     else:
         t = torch.from_numpy(np.ascontiguousarray(np.asarray(x, dtype=np.float32))).to(dev)
-    return t.contiguous()
+    return t.contiguous() if contiguous else t
+
+
+def column_view(x, level_axis: int):
+    """(tensor, fv3_layout, ncol, nz) for ``x`` with levels on ``level_axis``: strided
+    CUDA views the layout can express are used in place, anything else is copied to a
+    contiguous device tensor first."""
+    t = to_device_f32(x, contiguous=False)
+    try:
+        lay, ncol, nz = level_layout(t, level_axis)
+    except ValueError:
+        t = t.contiguous()
+        lay, ncol, nz = level_layout(t, level_axis)
+    return t, lay, ncol, nz
 
 
 def ptr(t) -> int:
@@ -39,14 +53,30 @@ def ptr(t) -> int:
 
 
 def level_layout(t, level_axis: int):
-    """fv3_layout for a contiguous tensor whose columns are every axis but
-    ``level_axis``: axes before it are 'blocks' (e.g. tile), axes after it are the
-    horizontal plane (e.g. y, x)."""
-    shape = tuple(t.shape)
-    if not t.is_contiguous():
-        raise ValueError("expected a contiguous tensor")
-    plane = int(np.prod(shape[level_axis + 1:], dtype=np.int64)) if level_axis + 1 < len(shape) else 1
-    nz = int(shape[level_axis])
-    nblk = int(np.prod(shape[:level_axis], dtype=np.int64)) if level_axis > 0 else 1
-    ncol = nblk * plane
-    return _native.layout(plane, plane, nz * plane), ncol, nz
+    """fv3_layout for a tensor whose columns are every axis but ``level_axis``: axes
+    before it are 'blocks' (e.g. tile), axes after it the horizontal plane (e.g. y, x).
+    Views are fine as long as the plane is contiguous and the block axes flatten to a
+    single stride, e.g. a (tile, z, y, x) array, its (z, rows, x) row band, or a
+    tile slice; the level stride may be anything."""
+    shape = tuple(int(n) for n in t.shape)
+    st = tuple(int(x) for x in t.stride())
+    nz = shape[level_axis]
+    inner = shape[level_axis + 1:]
+    plane = int(np.prod(inner, dtype=np.int64)) if inner else 1
+    if t.numel() == 0:  # nothing to address: any layout will do
+        nblk = int(np.prod(shape[:level_axis], dtype=np.int64)) if level_axis > 0 else 1
+        p = max(plane, 1)
+        return _native.layout(p, p, max(nz, 1) * p), nblk * plane, nz
+    expect = 1
+    for n, x in zip(reversed(inner), reversed(st[level_axis + 1:])):
+        if n != 1 and x != expect:
+            raise ValueError(f"the horizontal plane of a {shape} tensor with strides {st} is not contiguous")
+        expect *= n
+    blocks = [(n, x) for n, x in zip(shape[:level_axis], st[:level_axis]) if n != 1]
+    nblk = int(np.prod([n for n, _ in blocks], dtype=np.int64)) if blocks else 1
+    blk_stride = blocks[-1][1] if blocks else nz * plane
+    for (n0, x0), (n1, x1) in zip(blocks[:-1], blocks[1:]):
+        if x0 != x1 * n1:
+            raise ValueError(f"the block axes of a {shape} tensor with strides {st} do not flatten")
+    ld = st[level_axis] if nz > 1 else plane
+    return _native.layout(plane, ld, blk_stride), nblk * plane, nz

@@ -7,6 +7,8 @@
 //                          workflows/prognostic_c48_run/runtime/steppers/machine_learning.py:258-303
 //   fv3_area_weighted_sums the per-rank (sum area*x, sum area) partials behind
 //                          runtime/metrics.py:18-24 (globally_average_2d_diagnostics)
+//   fv3_level_sums         the per-rank per-level horizontal sums behind
+//                          runtime/metrics.py:27-32 (globally_sum_3d_diagnostics)
 //
 // Both are HBM-bound streams.  Column integral: one thread per column, levels
 // walked in order (coalesced [level][column] rows), float64 accumulation.
@@ -86,8 +88,33 @@ __global__ __launch_bounds__(kSumBlock) void area_sums_stage2(const double* __re
     }
 }
 
+// out[k] = sum over columns of x[k][c]: one block per level, grid-stride lanes then
+// the fixed LDS tree (bitwise reproducible)
+__global__ __launch_bounds__(kSumBlock) void level_sums_kernel(const float* __restrict__ x, fv3_layout xl,
+                                                               int64_t ncol, double* __restrict__ out)
+{
+    __shared__ double sh[kSumBlock];
+    const int k = blockIdx.x;
+    double s = 0.0;
+    for (int64_t c = threadIdx.x; c < ncol; c += kSumBlock) s += (double)x[col_offset(xl, c) + (int64_t)k * xl.ld];
+    const double tot = block_sum(s, sh);
+    if (threadIdx.x == 0) out[k] = tot;
+}
+
 }  // namespace
 }  // namespace fv3
+
+extern "C" int fv3_level_sums(const float* x, fv3_layout x_l, int64_t ncol, int nz, double* out, void* stream)
+{
+    fv3::clear_error();
+    FV3_REQUIRE(ncol >= 0 && nz >= 1, "level_sums: bad sizes ncol=%lld nz=%d", (long long)ncol, nz);
+    FV3_REQUIRE(x && out, "level_sums: NULL array");
+    FV3_REQUIRE(ncol == 0 || fv3::layout_ok(x_l, ncol), "level_sums: bad layout");
+    hipLaunchKernelGGL(fv3::level_sums_kernel, dim3(nz), dim3(fv3::kSumBlock), 0, (hipStream_t)stream, x, x_l,
+                       ncol, out);
+    FV3_LAUNCH_CHECK();
+    return FV3_OK;
+}
 
 extern "C" int fv3_column_integral(const float* field, fv3_layout field_l, const float* delp,
                                    fv3_layout delp_l, float* out, int64_t ncol, int km, double scale,

@@ -263,11 +263,10 @@ class DenseColumnModel:
         ts, lays = [], []
         ncol = None
         for v, (t, ax) in enumerate(zip(inputs, level_axes)):
-            t = _device.to_device_f32(t)
             if ax is None:
-                t = t.unsqueeze(0)
+                t = _device.to_device_f32(t, contiguous=False).unsqueeze(0)
                 ax = 0
-            lay, n, nz = _device.level_layout(t, ax)
+            t, lay, n, nz = _device.column_view(t, ax)  # strided views read in place
             if nz != c.in_nz[v]:
                 raise ValueError(f"input {c.input_variables[v]} has {nz} levels, model expects {c.in_nz[v]}")
             if ncol is not None and n != ncol:

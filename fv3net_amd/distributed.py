@@ -1,0 +1,178 @@
+"""Multi-GPU: column sharding and the path's one collective (global means).
+
+Columns are independent on this path (mappm loops columns independently,
+mappm.f90:58-124; the dense model has n_halo = 0, dense.py:228), so ranks own
+disjoint column bands and the data path has no exchange at all.  The only
+collective in the reference's per-step loop is the global average of 2-D
+diagnostics (workflows/prognostic_c48_run/runtime/metrics.py:18-24:
+``comm.reduce((area * x).sum())`` and ``comm.reduce(area.sum())``), done here as
+one all-gather of float64 per-rank partials [n_diag, 2] summed in fixed rank order,
+so every rank gets the same bits whatever the backend's reduction tree.
+
+One process per GPU; backend "nccl" (RCCL over xGMI) on the GPU box, "gloo" in
+the CPU tests.
+"""
+import ctypes
+from dataclasses import dataclass
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+from . import _device, _native
+
+try:
+    import torch
+    import torch.distributed as dist
+except ImportError:  # pragma: no cover
+    torch = None
+    dist = None
+
+
+@dataclass(frozen=True)
+class Segment:
+    """Rows [y0, y1) of one tile: a contiguous run of (y, x) columns per level."""
+    tile: int
+    y0: int
+    y1: int
+
+
+def row_band(n_rows: int, rank: int, world: int, align: int = 1) -> Tuple[int, int]:
+    """Contiguous band [start, stop) of ``n_rows`` rows for ``rank`` of ``world``;
+    boundaries are multiples of ``align`` (e.g. the coarsening factor, so a coarse
+    cell never straddles two ranks).  Bands differ in size by at most ``align``."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} of world {world}")
+    if align < 1 or n_rows % align:
+        raise ValueError(f"{n_rows} rows are not divisible by align={align}")
+    units = n_rows // align
+    lo = rank * units // world
+    hi = (rank + 1) * units // world
+    return lo * align, hi * align
+
+
+def column_segments(ntile: int, ny: int, rank: int, world: int, align: int = 1) -> List[Segment]:
+    """The rank's band of the flattened (tile, y) rows, split at tile
+    boundaries: at most ceil(band / ny) + 1 segments, each an in-place view of a
+    (tile, z, y, x) array."""
+    if ny % align:
+        raise ValueError(f"ny={ny} is not divisible by align={align}")
+    start, stop = row_band(ntile * ny, rank, world, align)
+    segs = []
+    r = start
+    while r < stop:
+        t, y = divmod(r, ny)
+        y1 = min(ny, y + (stop - r))
+        segs.append(Segment(t, y, y1))
+        r += y1 - y
+    return segs
+
+
+def segment_view(arr, seg: Segment):
+    """(tile, z, y, x) -> the (z, rows, x) view of one segment (no copy)."""
+    return arr[seg.tile, :, seg.y0:seg.y1]
+
+
+def area_weighted_partials(diags: Sequence, area, stream=None):
+    """Device float64 partials [n_diag, 2] = (sum(area * x_d), sum(area)) over this
+    rank's columns, computed by the deterministic two-stage HIP reduction
+    (csrc/reduce.hip).  ``diags``: float32 CUDA tensors shaped like ``area``."""
+    _device.require_gpu()
+    area = _device.to_device_f32(area).contiguous()
+    xs = [_device.to_device_f32(d).contiguous() for d in diags]
+    for d in xs:
+        if d.shape != area.shape:
+            raise ValueError(f"diagnostic shape {tuple(d.shape)} != area shape {tuple(area.shape)}")
+    out = torch.empty((len(xs), 2), dtype=torch.float64, device=area.device)
+    if not xs:
+        return out
+    tab = (ctypes.c_void_p * len(xs))(*[d.data_ptr() for d in xs])
+    st = _native.load().fv3_area_weighted_sums(tab, len(xs), area.data_ptr(), area.numel(), out.data_ptr(),
+                                               _device.stream_handle(stream))
+    _native.check(st, "area_weighted_sums")
+    return out
+
+
+def _backend_device(group=None):
+    backend = dist.get_backend(group)
+    if backend == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def combine_partials(partials, group=None):
+    """All-gather float64 partials [n_diag, 2] and sum them in rank order 0..N-1.
+    Returns the global [n_diag, 2] sums (identical bits on every rank)."""
+    p = torch.as_tensor(partials, dtype=torch.float64)
+    if dist is None or not dist.is_available() or not dist.is_initialized():
+        return p.clone()
+    dev = _backend_device(group)
+    world = dist.get_world_size(group)
+    local = p.to(dev).contiguous()
+    gathered = [torch.empty_like(local) for _ in range(world)]
+    dist.all_gather(gathered, local, group=group)
+    total = gathered[0].clone()
+    for g in gathered[1:]:  # fixed order: bitwise reproducible on every rank
+        total += g
+    return total.to(p.device)
+
+
+def global_average(partials, group=None) -> np.ndarray:
+    """metrics.py:18-24 global_average for n_diag diagnostics at once: global
+    sum(area*x) / sum(area).  Unlike the reference (which returns -1 off rank 0)
+    every rank gets the value."""
+    total = combine_partials(partials, group).cpu().numpy()
+    return total[:, 0] / total[:, 1]
+
+
+def _is_2d(v, area_shape) -> bool:
+    dims = getattr(v, "dims", None)
+    if dims is not None and not callable(dims):
+        return set(dims) == {"x", "y"}
+    return tuple(v.shape) == tuple(area_shape)
+
+
+def _data(v):
+    d = getattr(v, "data", v)
+    return d if (torch is not None and isinstance(d, torch.Tensor)) else getattr(v, "values", d)
+
+
+def globally_average_2d_diagnostics(diagnostics: dict, exclude: Sequence[str] = None, group=None) -> dict:
+    """metrics.py:33-43: the global area-weighted mean of every (x, y) diagnostic not
+    in ``exclude`` (area from ``diagnostics["area"]``, itself included, as in the
+    reference) — one HIP reduction for all of them plus one all-gather."""
+    exclude = set(exclude or ())
+    area = _data(diagnostics["area"])
+    names = [k for k, v in diagnostics.items() if k not in exclude and _is_2d(v, np.shape(area))]
+    if not names:
+        return {}
+    means = global_average(area_weighted_partials([_data(diagnostics[k]) for k in names], area), group)
+    return {k: float(m) for k, m in zip(names, means)}
+
+
+def level_sums(field, stream=None):
+    """Device float64 per-level horizontal sums of a (z, ...) field (deterministic
+    fixed-tree HIP reduction): the per-rank part of metrics.py:27-32."""
+    _device.require_gpu()
+    t = _device.to_device_f32(field)
+    lay, ncol, nz = _device.level_layout(t, 0)
+    out = torch.empty(nz, dtype=torch.float64, device=t.device)
+    st = _native.load().fv3_level_sums(t.data_ptr(), lay, ncol, nz, out.data_ptr(), _device.stream_handle(stream))
+    _native.check(st, "level_sums")
+    return out
+
+
+def globally_sum_3d_diagnostics(diagnostics: dict, include: Sequence[str], group=None) -> dict:
+    """metrics.py:46-55: ``{name}_global_sum`` = per-level sums over x, y and all
+    ranks of each included (z, y, x) diagnostic (rank partials summed in rank order)."""
+    sums = {}
+    for k, v in diagnostics.items():
+        dims = getattr(v, "dims", None)
+        if k in include and dims is not None and set(dims) == {"x", "y", "z"}:
+            data = _data(v)
+            if tuple(dims) != ("z", "y", "x"):
+                data = data.permute(*[dims.index(d) for d in ("z", "y", "x")]) if hasattr(data, "permute") \
+                    else np.transpose(data, [dims.index(d) for d in ("z", "y", "x")])
+            part = level_sums(data)[:, None]
+            total = combine_partials(part, group)[:, 0]
+            sums[f"{k}_global_sum"] = [float(x) for x in total.cpu().numpy()]
+    return sums

@@ -18,27 +18,29 @@ except ImportError:  # pragma: no cover
 
 def mappm_device(pe1, q1, pe2, iv: int = 1, kord: int = 1, out=None, stream=None):
     """Remap on device.  ``pe1 [km+1, ncol]``, ``q1 [km, ncol]``, ``pe2 [kn+1, ncol]``
-    float32 CUDA tensors (column fastest, the Fortran pe1(i,k) order); returns
-    ``q2 [kn, ncol]``.  Asynchronous on the current stream."""
+    float32 CUDA tensors (column fastest, the Fortran pe1(i,k) order; strided views
+    such as a column slice are read in place); returns ``q2 [kn, ncol]`` (or writes
+    ``out``).  Asynchronous on the current stream."""
     _device.require_gpu()
-    pe1 = _device.to_device_f32(pe1)
-    q1 = _device.to_device_f32(q1)
-    pe2 = _device.to_device_f32(pe2)
-    if pe1.dim() != 2 or q1.dim() != 2 or pe2.dim() != 2:
-        raise ValueError("pe1, q1, pe2 must be 2-D [level, column]")
-    km, ncol = q1.shape
-    kn = pe2.shape[0] - 1
-    if pe1.shape[0] != km + 1:
+    for a in (pe1, q1, pe2):
+        if len(getattr(a, "shape", ())) != 2:
+            raise ValueError("pe1, q1, pe2 must be 2-D [level, column]")
+    pe1, l1, n1, kp1 = _device.column_view(pe1, 0)
+    q1, lq, ncol, km = _device.column_view(q1, 0)
+    pe2, l2, n2, kp2 = _device.column_view(pe2, 0)
+    kn = kp2 - 1
+    if kp1 != km + 1:
         raise ValueError("f_in must have a vertical dimension one shorter than p_in")
-    if pe1.shape[1] != ncol or pe2.shape[1] != ncol:
+    if n1 != ncol or n2 != ncol:
         raise ValueError("All dimensions except vertical must be same size for p_in, f_in and p_out")
     if out is None:
         out = torch.empty((kn, ncol), dtype=torch.float32, device=q1.device)
+    if tuple(out.shape) != (kn, ncol) or out.dtype != torch.float32:
+        raise ValueError(f"out must be float32 ({kn}, {ncol})")
+    lo, _, _ = _device.level_layout(out, 0)
     lib = _native.load()
-    st = lib.fv3_mappm(
-        _device.ptr(pe1), _device.ptr(q1), _device.ptr(pe2), _device.ptr(out), ncol, km, kn,
-        int(iv), int(kord), 0.0, _device.stream_handle(stream),
-    )
+    st = lib.fv3_mappm_ex(_device.ptr(pe1), l1, _device.ptr(q1), lq, _device.ptr(pe2), l2, _device.ptr(out), lo,
+                          ncol, km, kn, int(iv), int(kord), 0.0, _device.stream_handle(stream))
     _native.check(st, "mappm")
     return out
 

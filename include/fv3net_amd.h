@@ -147,6 +147,10 @@ int fv3_column_integral(const float* field, fv3_layout field_l, const float* del
 int fv3_area_weighted_sums(const float* const* diags, int n_diag, const float* area,
                            int64_t ncol, double* partial, void* stream);
 
+/* Per-level horizontal sums out[k] = sum_c x[k][c] in float64 (fixed reduction tree):
+ * the per-rank part of metrics.py:27-32 global_horizontal_sum. */
+int fv3_level_sums(const float* x, fv3_layout x_l, int64_t ncol, int nz, double* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,98 @@
+"""Multi-rank path: column bands with no data-path exchange, and
+the one collective — global means (runtime/metrics.py:18-55) — as an all-gather
+of float64 partials summed in fixed rank order.  gloo world_size 2..4 on CPU."""
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import dist_helpers as H
+from fv3net_amd import distributed as D
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("n_rows,world,align", [(576, 8, 1), (576, 3, 1), (2304, 8, 8), (72, 5, 8), (10, 4, 1)])
+def test_row_band_partitions_exactly(n_rows, world, align):
+    bands = [D.row_band(n_rows, r, world, align) for r in range(world)]
+    assert bands[0][0] == 0 and bands[-1][1] == n_rows
+    for (a0, a1), (b0, b1) in zip(bands[:-1], bands[1:]):
+        assert a1 == b0
+    sizes = [b - a for a, b in bands]
+    assert all(a % align == 0 for a, _ in bands)
+    assert max(sizes) - min(sizes) <= align
+
+
+def test_row_band_rejects_bad_arguments():
+    with pytest.raises(ValueError):
+        D.row_band(10, 3, 3)
+    with pytest.raises(ValueError):
+        D.row_band(10, 0, 2, align=4)
+
+
+@pytest.mark.parametrize("res,world", [(96, 8), (96, 4), (48, 8), (384, 8), (12, 5)])
+def test_column_segments_cover_the_sphere_once(res, world):
+    seen = np.zeros((6, res), dtype=int)
+    for r in range(world):
+        for s in D.column_segments(6, res, r, world):
+            assert 0 <= s.y0 < s.y1 <= res
+            seen[s.tile, s.y0:s.y1] += 1
+    assert (seen == 1).all()
+
+
+def test_segment_view_is_a_view():
+    import torch
+
+    a = torch.arange(2 * 3 * 4 * 5, dtype=torch.float32).reshape(2, 3, 4, 5)
+    v = D.segment_view(a, D.Segment(1, 1, 3))
+    assert v.shape == (3, 2, 5) and v.data_ptr() == a[1, 0, 1].data_ptr()
+
+
+def _spawn(fn, world, *args):
+    mp.start_processes(fn, args=(world, _port()) + args, nprocs=world, join=True, start_method="spawn")
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_global_average_matches_single_process(tmp_path, world):
+    _spawn(H.global_average_worker, world, str(tmp_path), False)
+    res = [np.load(tmp_path / f"rank{r}.npy") for r in range(world)]
+    rng = np.random.default_rng(0)
+    x = rng.normal(280, 20, (6, 12, 12)).astype(np.float32).astype(np.float64)
+    area = rng.uniform(0.5, 1.0, (6, 12, 12)).astype(np.float32).astype(np.float64)
+    expect = np.array([np.sum(area * x), np.sum(area * x * 2)]) / np.sum(area)
+    for r in res:
+        assert (r.view(np.uint64) == res[0].view(np.uint64)).all()  # identical bits on every rank
+        np.testing.assert_allclose(r, expect, rtol=1e-13)
+
+
+def test_gloo_partials_summed_in_rank_order(tmp_path):
+    _spawn(H.rank_order_worker, 4, str(tmp_path))
+    tot = [np.load(tmp_path / f"rank{r}.npy") for r in range(4)]
+    expect = ((1e16 + 1.0) + -1e16) + 3.0  # == 3.0 (the 1.0 is absorbed), not 4.0
+    for t in tot:
+        assert t[0, 0] == expect and t[0, 1] == 4.0
+
+
+def test_combine_without_process_group_is_identity():
+    import torch
+
+    p = torch.tensor([[2.0, 4.0]], dtype=torch.float64)
+    assert D.global_average(p)[0] == 0.5
+
+
+@pytest.mark.gpu
+def test_gpu_global_average_two_ranks(gpu, tmp_path):
+    """HIP partials on the GPU per rank + gloo all-gather (2 processes on one GPU)."""
+    _spawn(H.global_average_worker, 2, str(tmp_path), True)
+    res = [np.load(tmp_path / f"rank{r}.npy") for r in range(2)]
+    rng = np.random.default_rng(0)
+    x = rng.normal(280, 20, (6, 12, 12)).astype(np.float32).astype(np.float64)
+    area = rng.uniform(0.5, 1.0, (6, 12, 12)).astype(np.float32).astype(np.float64)
+    expect = np.array([np.sum(area * x), np.sum(area * x * 2)]) / np.sum(area)
+    assert (res[0].view(np.uint64) == res[1].view(np.uint64)).all()
+    np.testing.assert_allclose(res[0], expect, rtol=1e-12)
