@@ -26,6 +26,7 @@ EXPORTED_SYMBOLS = (
     "fv3_dense_k_in",
     "fv3_dense_k_out",
     "fv3_dense_forward",
+    "fv3_dense_set_trace",
     "fv3_regrid_coarsen",
     "fv3_regrid_coarsen_f64",
     "fv3_column_integral",
@@ -83,6 +84,7 @@ _SIGNATURES = {
     "fv3_mappm_ex": (_I, [_P, Layout, _P, Layout, _P, Layout, _P, Layout, _I64, _I, _I, _I, _I, _F, _P]),
     "fv3_dense_create": (_I, [ctypes.POINTER(DenseDesc), ctypes.POINTER(_P)]),
     "fv3_dense_destroy": (_I, [_P]),
+    "fv3_dense_set_trace": (_I, [_P, _P]),
     "fv3_dense_k_in": (_I, [_P]),
     "fv3_dense_k_out": (_I, [_P]),
     "fv3_dense_forward": (_I, [_P, ctypes.POINTER(_P), ctypes.POINTER(Layout), ctypes.POINTER(_P),

@@ -10,29 +10,38 @@
 // tendencies are written straight into [level][column] outputs (the unstack).
 //
 // Mapping (CDNA4, wave64, v_mfma_f32_16x16x4_f32 — exact f32, no xf32 on gfx950):
-//  * one 256-thread block (4 waves, one per SIMD) owns a 16-column tile for the
-//    whole network; wave w owns hidden-unit tiles [w*T4, (w+1)*T4) of every hidden
-//    layer (T4 = width/64 tiles of 16 units) and every 4th output tile, so four
-//    independent accumulators per wave keep the MFMA pipe busy and a C48 step
-//    (864 tiles) puts ~3.4 waves on every SIMD;
-//  * lane l holds column (l & 15) and k-slot (l >> 4) of every B operand;
+//  * a 256-thread block (4 waves, one per SIMD) owns a tile of NC x 16 columns for
+//    the whole network; wave w owns hidden-unit tiles [w*T4, (w+1)*T4) of every
+//    hidden layer (T4 = width/64 tiles of 16 units); lane l holds column (l & 15)
+//    and k-slot (l >> 4) of every B operand;
 //  * a layer's output is written to LDS in the MFMA accumulator layout
 //    ([tile][lane] x 4 regs, register r of tile t = unit 16t + 4(l>>4) + r) and the
 //    next layer reads it back with one ds_read_b128 per 4 k-steps: k-step s = 4t + r
 //    takes register r of tile t, i.e. the contraction order over hidden units is
 //    permuted and the packed weights carry the same permutation (no shuffles);
-//  * two 16 KiB LDS buffers ping-pong between layers (one barrier per layer);
-//    the normalised inputs are staged once per block in the second buffer;
+//  * ONE activation buffer is updated in place (read, barrier, write, barrier) and
+//    the staged inputs alias it: ~37 KB of LDS per block -> 3 blocks per CU;
+//  * inputs are loaded by "slots" (256 threads x one feature row each, the
+//    variable uniform per slot), all slots of a tile in flight at once; blocks are
+//    persistent over column tiles and load the NEXT tile's inputs into registers
+//    while the current tile runs its hidden and output layers;
 //  * weights are pre-packed at create time into [k-step][wave][lane][T4] fragment
-//    order: every A-operand fetch is one T4*4 B/lane fully coalesced load;
+//    order (every A-operand fetch is one coalesced T4*4 B/lane load) and stream
+//    through 3-deep compile-time register rings; each layer's first two groups are
+//    loaded before the barrier that precedes it, so no layer starts on a cold ring;
+//  * the output layer: unit (otile m, column tile c) with c = wave % NC fixed per
+//    wave; every wave runs all its units in one pass (up to kMaxUnits accumulators)
+//    and the bias/denorm/limit/mask epilogue reads its constants from LDS;
 //  * each input variable's features and each output tile are padded so a k-step
-//    (4 features) never straddles two variables: the source pointer is uniform.
+//    (4 features) never straddles two variables.
 // Roofline: fp32 MFMA-bound.  2*(k_in*w + (n_hidden-1)*w*w + w*k_out) FLOP per
 // column (292,864 for the 2x256 C48 model) against (k_in + k_out) * 4 B of HBM.
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <utility>
 #include <vector>
 
@@ -45,6 +54,9 @@ namespace fv3 {
 
 constexpr int kMaxVars = 16;
 constexpr int kMaxOutTiles = 64;
+constexpr int kMaxSlots = 96;   // input feature rows per tile / (256 / columns per tile)
+constexpr int kRawSlots = 20;   // slots prefetched into registers across tiles
+constexpr int kMaxUnits = 3;    // output units per wave per pass (register budget: 3 waves/SIMD)
 
 struct DenseInVar {
     const float* ptr;
@@ -70,23 +82,39 @@ struct DenseArgs {
     const float* wh;        // [n_hidden-1][HP/4][4 waves][64][T4]
     const float* bh;        // [n_hidden-1][HP]
     const float* wo;        // [n_otiles][HP/16][64][4]: 4 k-steps per lane
-    const float* bo;        // [KOP]
-    const float* o_sigma;   // [KOP]
-    const float* o_mean;    // [KOP]
-    const float* o_lo;      // [KOP]
-    const float* o_hi;      // [KOP]
-    const float* o_mask;    // [KOP]
-    DenseInVar in[kMaxVars];
+    const float* oep;       // [6][KOP]: bias, sigma, mean, lo, hi, mask
+    const float* wbase;     // the model allocation: weights are fetched as buffer loads
+    int w1_off, wh_off, wo_off;  // byte offsets of w1 / wh / wo in it
+    int wbytes;             // its size (buffer range)
+    // input slots (per launch): slot q covers feature rows [fdst, fdst + 256/NCOL) of one
+    // variable; thread row fq reads base[blk * bs + ii + fq * ld] if fq < nk, writes
+    // padded feature fdst + fq if fq < nf.  meta = fdst << 16 | nk << 8 | nf
+    const float* slot_base[kMaxSlots];
+    int slot_bs[kMaxSlots];
+    int slot_ld[kMaxSlots];
+    int slot_meta[kMaxSlots];
     float* out_ptr[kMaxVars];
     int64_t out_ld[kMaxVars];
     int64_t out_bs[kMaxVars];
     DenseOutTile otile[kMaxOutTiles];
-    int64_t ncol, ncol_blk;
+    int64_t ncol, ncol_blk, ntiles;
     int n_in, n_hidden_extra, n_otiles, kp;
-    int in_steps_total, pad_;
+    int in_steps_total, nslots;
+    int lds_x;              // f32x4 offset of the constants area (after activations / inputs)
+    int pad_;
+    long long* trace;       // profiling hook (fv3_dense_set_trace): [tiles][8] timestamps, or NULL
 };
 
-typedef float f32x1 __attribute__((ext_vector_type(1)));
+// phase timestamps of tile t (thread 0): 0 start, 5 prologue done (constants in LDS),
+// 1 inputs staged, 2 layer 1 done, 3 hidden layers done, 4 end; slot 7 = hardware CU id
+__device__ __forceinline__ void trace_mark(__attribute__((address_space(4))) const DenseArgs& p, int64_t tile,
+                                           int slot)
+{
+    if (p.trace && threadIdx.x == 0) {
+        p.trace[tile * 8 + slot] = wall_clock64();
+        if (slot == 0) p.trace[tile * 8 + 7] = (long long)__smid();
+    }
+}
 
 // compile-time loop: f(std::integral_constant<int, i>) for i = 0..N-1 (register
 // rings indexed by i stay in registers with no copies between iterations)
@@ -125,6 +153,8 @@ __device__ __forceinline__ float frag_at(const typename Frag<T4>::type& a, int j
         return a[j];
 }
 
+__device__ __forceinline__ f32x4 zero4() { return f32x4{0.0f, 0.0f, 0.0f, 0.0f}; }
+
 // relu(acc + bias) for this wave's T4 tiles (x NC column tiles), stored in accumulator layout
 template <int T4, int NC>
 __device__ __forceinline__ void bias_relu_store(f32x4 (&acc)[NC][T4], const float* __restrict__ b, int wave,
@@ -148,33 +178,60 @@ __device__ __forceinline__ void bias_relu_store(f32x4 (&acc)[NC][T4], const floa
     }
 }
 
+// Weights are read with buffer loads from one resource over the model allocation:
+// the lane offset is one VGPR and every per-group offset is a scalar, so nothing
+// per-address is kept in VGPRs (with 64-bit pointers, the compile-time group offsets
+// of every layer become loop-invariant VGPR pairs in the persistent tile loop).
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+
+__device__ __forceinline__ Rsrc make_rsrc(const void* base, int bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
+}
+
+template <typename FT>
+__device__ __forceinline__ FT bload(Rsrc r, int voff, int soff)
+{
+    if constexpr (sizeof(FT) == 16)
+        return __builtin_bit_cast(FT, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+    else if constexpr (sizeof(FT) == 8)
+        return __builtin_bit_cast(FT, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+    else
+        return __builtin_bit_cast(FT, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+
+// first RD-1 groups (4 k-steps each) of a [k-step][wave][lane] fragment stream
+// starting at byte offset soff (voff = this lane's (wave * 64 + lane) * sizeof(FT)).
+// RD = ring depth: a ring of RD groups is refilled RD-1 groups ahead of use.
+template <int RD, typename FT>
+__device__ __forceinline__ void prime_ring(FT (&g)[RD][4], Rsrc r, int voff, int soff)
+{
+    constexpr int KS = 256 * sizeof(FT);  // bytes per k-step
+#pragma unroll
+    for (int d = 0; d + 1 < RD; ++d)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) g[d][q] = bload<FT>(r, voff, soff + (4 * d + q) * KS);
+}
+
 // acc[c][j] += W^T h over all HT*4 k-steps, h read from LDS in accumulator layout.
-// Weight fragments stream through a 3-group register ring (groups of 4 k-steps),
-// two groups (8 k-steps, 8*T4*NC MFMAs) ahead of use, so the L2 latency of a
-// fragment is covered by this wave's own MFMAs.  The ring is indexed at compile
-// time (static_for): no register copies, hence no premature vmcnt(0).
-template <int T4, int NC>
-__device__ __forceinline__ void gemm_from_lds(f32x4 (&acc)[NC][T4], const f32x4* __restrict__ src,
-                                              const typename Frag<T4>::type* __restrict__ w, int wave,
-                                              int lane)
+// Weight fragments stream through the RD-group ring g (groups 0..RD-2 primed by the
+// caller), RD-1 groups (4*T4*NC MFMAs each) ahead of use.
+template <int T4, int NC, int RD>
+__device__ __forceinline__ void gemm_hidden(f32x4 (&acc)[NC][T4], const f32x4* __restrict__ src, Rsrc rw,
+                                            int voff, int soff, typename Frag<T4>::type (&g)[RD][4], int lane)
 {
     constexpr int HT = 4 * T4;
     typedef typename Frag<T4>::type FT;
-    const FT* wp = w + (size_t)wave * 64 + lane;  // k-step s at wp[s * 256]
-    FT g[3][4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        g[0][r] = wp[(size_t)r * 256];
-        g[1][r] = wp[(size_t)(4 + r) * 256];
-    }
+    constexpr int KS = 256 * sizeof(FT);
     f32x4 bq[2][NC];  // B operands, one group ahead
 #pragma unroll
     for (int c = 0; c < NC; ++c) bq[0][c] = src[(c * HT) * 64 + lane];
     static_for<HT>([&](auto tc) {
         constexpr int t = decltype(tc)::value;
-        if constexpr (t + 2 < HT) {
+        if constexpr (t + RD - 1 < HT) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) g[(t + 2) % 3][r] = wp[(size_t)(4 * (t + 2) + r) * 256];
+            for (int r = 0; r < 4; ++r)
+                g[(t + RD - 1) % RD][r] = bload<FT>(rw, voff, soff + (4 * (t + RD - 1) + r) * KS);
         }
         if constexpr (t + 1 < HT) {
 #pragma unroll
@@ -187,228 +244,311 @@ __device__ __forceinline__ void gemm_from_lds(f32x4 (&acc)[NC][T4], const f32x4*
             for (int j = 0; j < T4; ++j)
 #pragma unroll
                 for (int c = 0; c < NC; ++c)
-                    acc[c][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(frag_at<T4>(g[t % 3][r], j), bq[t % 2][c][r],
+                    acc[c][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(frag_at<T4>(g[t % RD][r], j), bq[t % 2][c][r],
                                                                      acc[c][j], 0, 0, 0);
     });
 }
 
-// one or two output units (16 output rows x one 16-column tile each) over all
-// k-steps; unit u reads weight rows w[u] and the B operands of column tile cs[u];
-// weights pipelined two groups ahead as in gemm_from_lds
-template <int T4, int NC, int NT>
-__device__ __forceinline__ void out_units(f32x4 (&o)[2], const f32x4* __restrict__ cur, const f32x4* __restrict__ w0,
-                                          const f32x4* __restrict__ w1, int c0, int c1)
+// output units of this wave: unit i = wave + 4 * (i0 + i), otile m = unit / NC;
+// soff[i] = byte offset of unit i's weights (group 0) in the model allocation
+struct OutPlan {
+    int soff[kMaxUnits];
+    int n;  // units in this pass
+};
+
+template <int RD>
+__device__ __forceinline__ void prime_out(f32x4 (&g)[RD][kMaxUnits], Rsrc rw, int voff, const OutPlan& pl)
+{
+#pragma unroll
+    for (int i = 0; i < kMaxUnits; ++i)
+        if (i < pl.n) {
+#pragma unroll
+            for (int d = 0; d + 1 < RD; ++d) g[d][i] = bload<f32x4>(rw, voff, pl.soff[i] + d * 1024);
+        }
+}
+
+// o[i] = W_m^T h for N units over all HT*4 k-steps; B operands of column tile cw
+template <int T4, int N, int RD>
+__device__ __forceinline__ void gemm_out(f32x4 (&o)[kMaxUnits], const f32x4* __restrict__ src, Rsrc rw, int voff,
+                                         const OutPlan& pl, f32x4 (&g)[RD][kMaxUnits])
 {
     constexpr int HT = 4 * T4;
-    f32x4 g[3][NT];  // weight fragments of 4 k-steps per unit
-    const f32x4* wt[2] = {w0, w1};
-    const int cs[2] = {c0, c1};
-#pragma unroll
-    for (int u = 0; u < NT; ++u) {
-        g[0][u] = wt[u][0];
-        g[1][u] = wt[u][64];
-    }
-    f32x4 bq[2][NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) bq[0][c] = cur[(c * HT) * 64];
+    f32x4 bq[2];
+    bq[0] = src[0];
     static_for<HT>([&](auto tc) {
         constexpr int t = decltype(tc)::value;
-        if constexpr (t + 2 < HT) {
+        if constexpr (t + RD - 1 < HT) {
 #pragma unroll
-            for (int u = 0; u < NT; ++u) g[(t + 2) % 3][u] = wt[u][(t + 2) * 64];
+            for (int i = 0; i < N; ++i)
+                g[(t + RD - 1) % RD][i] = bload<f32x4>(rw, voff, pl.soff[i] + (t + RD - 1) * 1024);
         }
-        if constexpr (t + 1 < HT) {
-#pragma unroll
-            for (int c = 0; c < NC; ++c) bq[(t + 1) % 2][c] = cur[(c * HT + t + 1) * 64];
-        }
+        if constexpr (t + 1 < HT) bq[(t + 1) % 2] = src[(t + 1) * 64];
         __builtin_amdgcn_sched_barrier(0);
-        f32x4 bu[NT];
-#pragma unroll
-        for (int u = 0; u < NT; ++u) {
-            bu[u] = bq[t % 2][0];
-#pragma unroll
-            for (int c = 1; c < NC; ++c)
-                if (cs[u] == c) bu[u] = bq[t % 2][c];
-        }
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int u = 0; u < NT; ++u)
-                o[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(g[t % 3][u][r], bu[u][r], o[u], 0, 0, 0);
+            for (int i = 0; i < N; ++i)
+                o[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(g[t % RD][i][r], bq[t % 2][r], o[i], 0, 0, 0);
     });
 }
 
-// T4: hidden tiles per wave (width/64); NC: 16-column tiles per block
-template <int T4, int NC>
-__global__ __launch_bounds__(256) void dense_forward_kernel(DenseArgs p)
+typedef __attribute__((address_space(4))) const DenseArgs KArgs;
+
+// WPE: waves per SIMD the register allocation targets (2: no limit below 256 VGPRs;
+// 3: <= 168, letting three blocks share a CU)
+// RD: weight ring depth (groups of 4 k-steps held; refilled RD-1 groups ahead)
+template <int T4, int NC, int WPE, int RD>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void dense_forward_kernel(DenseArgs pa)
 {
-    constexpr int HT = 4 * T4;  // hidden tiles of 16 units
-    constexpr int HP = 16 * HT; // padded width
+    // read the arguments in place in the kernarg segment (constant address space):
+    // capturing a by-value kernel parameter by reference would copy it to scratch
+    (void)pa;
+    KArgs& p = *(KArgs*)(__builtin_amdgcn_kernarg_segment_ptr());
+    constexpr int HT = 4 * T4;   // hidden tiles of 16 units
+    constexpr int HP = 16 * HT;  // padded width
     constexpr int NCOL = 16 * NC;
+    constexpr int FPS = 256 / NCOL;  // feature rows per slot
     typedef typename Frag<T4>::type FT;
-    extern __shared__ __attribute__((aligned(16))) f32x4 lds[];  // buf0 [NC][HT][64], buf1 >= same
-    f32x4* buf0 = lds;
-    f32x4* buf1 = lds + NC * HT * 64;
+    extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
+    f32x4* hbuf = lds;  // activations [NC][HT][64]; the staged inputs [NC][kp/16][64] alias it
+    float* s_mean = reinterpret_cast<float*>(lds + p.lds_x);  // [kp]
+    float* s_denom = s_mean + p.kp;                            // [kp]
+    float* s_ep = s_denom + p.kp;                              // [6][kop]
+    const int kop = 16 * p.n_otiles;
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int cl = lane & 15;
     const int kr = lane >> 4;
-    const int64_t col0 = (int64_t)blockIdx.x * NCOL;
+    const int cb = threadIdx.x % NCOL;   // column of this thread in the input slots
+    const int fq0 = threadIdx.x / NCOL;  // feature row of this thread within a slot
 
-    // ---- stage normalised inputs into buf1 in MFMA B-operand order ----
-    // x for column tile c, k-step s = 4g + r, k-slot kr, column cl lives at float
-    // index c*kp*16 + (g*64 + kr*16 + cl)*4 + r: one ds_read_b128 per lane yields the
-    // B operands of a whole group of 4 k-steps.
-    {
-        float* xs = reinterpret_cast<float*>(buf1);
-        const int cb = threadIdx.x % NCOL;  // column within the block
-        const int64_t col = col0 + cb;
+    // ---- input slots: issue every load of a tile at once ----
+    float raw[kRawSlots];
+    auto col_of = [&](int64_t tile, int64_t& blk, int64_t& ii) {
+        const int64_t col = tile * NCOL + cb;
         const bool valid = col < p.ncol;
-        const int64_t cc = valid ? col : col0;
-        const int64_t blk = cc / p.ncol_blk;
-        const int64_t ii = cc - blk * p.ncol_blk;
-        float* xc = xs + (cb >> 4) * (p.kp * 16);
-        const int cl16 = cb & 15;
-        constexpr int FSTRIDE = 256 / NCOL;
-        auto xidx = [&](int f) { return ((f >> 4) * 64 + (f & 3) * 16 + cl16) * 4 + ((f >> 2) & 3); };
-        for (int v = 0; v < p.n_in; ++v) {
-            const DenseInVar iv = p.in[v];
-            const float* src = iv.ptr + blk * iv.bs + ii;
-            const int nf = 4 * iv.nsteps;
-            for (int f0 = threadIdx.x / NCOL; f0 < nf; f0 += 16 * FSTRIDE) {
-                float raw[16];
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {  // sixteen HBM loads in flight per thread
-                    const int fz = f0 + q * FSTRIDE;
-                    raw[q] = (fz < iv.nkeep && valid) ? src[(int64_t)(iv.z0 + fz) * iv.ld] : 0.0f;
-                }
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    const int fz = f0 + q * FSTRIDE;
-                    if (fz < nf) {
-                        const int f = 4 * iv.step0 + fz;
-                        xc[xidx(f)] = (fz < iv.nkeep && valid) ? (raw[q] - p.in_mean[f]) / p.in_denom[f] : 0.0f;
-                    }
-                }
+        const int64_t cc = valid ? col : 0;
+        blk = cc / p.ncol_blk;
+        ii = cc - blk * p.ncol_blk;
+        return valid;
+    };
+    auto load_raw = [&](KArgs& pk, int64_t tile, int fq) {
+        int64_t blk, ii;
+        const bool valid = col_of(tile, blk, ii);
+        static_for<kRawSlots>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            if (q < pk.nslots) {
+                const int nk = (pk.slot_meta[q] >> 8) & 0xff;
+                raw[q] = (valid && fq < nk)
+                             ? pk.slot_base[q][blk * pk.slot_bs[q] + ii + (int64_t)fq * pk.slot_ld[q]]
+                             : 0.0f;
             }
+        });
+    };
+    // normalise and write the staged inputs in B-operand order: for column tile c,
+    // k-step s = 4g + r, k-slot kr, column cl the float index is
+    // c*kp*16 + (g*64 + kr*16 + cl)*4 + r (one ds_read_b128 = a group's B operands)
+    float* xc = reinterpret_cast<float*>(hbuf) + (cb >> 4) * (p.kp * 16);
+    const int cl16 = cb & 15;
+    auto xidx = [&](int f) { return ((f >> 4) * 64 + (f & 3) * 16 + cl16) * 4 + ((f >> 2) & 3); };
+    auto put = [&](int meta, float x, bool valid, int fq) {
+        if (fq < (meta & 0xff)) {
+            const int f = (meta >> 16) + fq;
+            xc[xidx(f)] = (valid && fq < ((meta >> 8) & 0xff)) ? (x - s_mean[f]) / s_denom[f] : 0.0f;
         }
-        for (int f = 4 * p.in_steps_total + threadIdx.x / NCOL; f < p.kp; f += FSTRIDE) xc[xidx(f)] = 0.0f;
+    };
+    auto store_x = [&](KArgs& pk, int64_t tile, int fq) {
+        int64_t blk, ii;
+        const bool valid = col_of(tile, blk, ii);
+        static_for<kRawSlots>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            if (q < pk.nslots) put(pk.slot_meta[q], raw[q], valid, fq);
+            if constexpr (q % 2 == 1) __builtin_amdgcn_sched_barrier(0);  // don't interleave 20 divisions
+        });
+        for (int q = kRawSlots; q < pk.nslots; ++q) {  // inputs wider than the register prefetch
+            const int meta = pk.slot_meta[q];
+            const float x = (valid && fq < ((meta >> 8) & 0xff))
+                                ? pk.slot_base[q][blk * pk.slot_bs[q] + ii + (int64_t)fq * pk.slot_ld[q]]
+                                : 0.0f;
+            put(meta, x, valid, fq);
+        }
+        for (int f = 4 * p.in_steps_total + fq; f < p.kp; f += FPS) xc[xidx(f)] = 0.0f;
+    };
+
+    // ---- prologue: this tile's inputs and the layer-1 ring in flight, constants to LDS ----
+    int64_t tile = blockIdx.x;
+    trace_mark(p, tile, 0);
+    if (tile < p.ntiles) load_raw(p, tile, fq0);
+    const Rsrc rw = make_rsrc(p.wbase, p.wbytes);
+    const int voff = (wave * 64 + lane) * (int)sizeof(FT);  // hidden-layer fragments
+    const int voff_o = lane * 16;                           // output-layer fragments
+    constexpr int KS = 256 * sizeof(FT);
+    FT g1[RD][4];
+    prime_ring<RD, FT>(g1, rw, voff, p.w1_off);
+    for (int i = threadIdx.x; i < p.kp; i += 256) {
+        s_mean[i] = p.in_mean[i];
+        s_denom[i] = p.in_denom[i];
     }
+    for (int i = threadIdx.x; i < 6 * kop; i += 256) s_ep[i] = p.oep[i];
+
+    // output plan of this wave
+    const int nunits = p.n_otiles * NC;
+    const int cw = wave % NC;  // (wave + 4i) % NC: one column tile per wave
+    const int ucnt = nunits > wave ? (nunits - wave + 3) / 4 : 0;
+    auto plan = [&](int i0) {
+        OutPlan pl;
+        pl.n = min(kMaxUnits, ucnt - i0);
+#pragma unroll
+        for (int i = 0; i < kMaxUnits; ++i) {
+            const int u = wave + 4 * (i0 + min(i, pl.n - 1));
+            pl.soff[i] = p.wo_off + (u / NC) * (HP / 16) * 1024;
+        }
+        return pl;
+    };
+    f32x4 go[RD][kMaxUnits];
+    FT gh[RD][4];
+    auto prime_after = [&](int l) {  // prime the ring of the layer that follows hidden layer l
+        if (l + 1 < p.n_hidden_extra) {
+            prime_ring<RD, FT>(gh, rw, voff, p.wh_off + (l + 1) * (HP / 4) * KS);
+        } else if (ucnt > 0) {
+            prime_out<RD>(go, rw, voff_o, plan(0));
+        }
+    };
     __syncthreads();
 
-    // ---- layer 1: Dense(width) over the padded input features ----
-    f32x4 acc[NC][T4];
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int j = 0; j < T4; ++j) acc[c][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    {
-        const f32x4* xq = buf1 + lane;  // + c*kp*4 + g*64
-        const FT* w1 = reinterpret_cast<const FT*>(p.w1) + (size_t)wave * 64 + lane;
-        const int ngroups = p.kp / 16;
-        // weights of the next group and B operands of the next group in flight
-        FT g[2][4];
-        f32x4 xb[2][NC];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) g[0][r] = w1[(size_t)r * 256];
-#pragma unroll
-        for (int c = 0; c < NC; ++c) xb[0][c] = xq[c * p.kp * 4];
-        for (int gi = 0; gi < ngroups; gi += 2) {
-            static_for<2>([&](auto hc) {
-                constexpr int h = decltype(hc)::value;
-                const int grp = gi + h;
-                if (grp < ngroups) {
-                    if (grp + 1 < ngroups) {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) g[1 - h][r] = w1[(size_t)(4 * (grp + 1) + r) * 256];
-#pragma unroll
-                        for (int c = 0; c < NC; ++c) xb[1 - h][c] = xq[c * p.kp * 4 + (grp + 1) * 64];
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-#pragma unroll
-                        for (int j = 0; j < T4; ++j)
-#pragma unroll
-                            for (int c = 0; c < NC; ++c)
-                                acc[c][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(frag_at<T4>(g[h][r], j), xb[h][c][r],
-                                                                                 acc[c][j], 0, 0, 0);
-                }
-            });
-        }
-    }
-    __syncthreads();  // every wave is done with the staged inputs (buf1)
-    bias_relu_store<T4, NC>(acc, p.b1, wave, lane, kr, buf0);
-    __syncthreads();
+    for (; tile < p.ntiles; tile += gridDim.x) {  // persistent over column tiles
+        trace_mark(p, tile, 5);
+        // opaque per tile: addresses derived from the thread's feature row are rebuilt
+        // each tile instead of being hoisted out of the loop as 20 live 64-bit values
+        int fq = fq0;
+        asm volatile("" : "+v"(fq));
+        // likewise the slot descriptors: reloaded per tile (scalar-cache hits) rather than
+        // ~100 loop-invariant scalars spilled into VGPRs for the whole loop
+        KArgs* pt = &p;
+        asm volatile("" : "+s"(pt));
+        store_x(*pt, tile, fq);
+        __syncthreads();
+        trace_mark(p, tile, 1);
 
-    // ---- further hidden layers (ping-pong) ----
-    f32x4* cur = buf0;
-    f32x4* nxt = buf1;
-    for (int l = 0; l < p.n_hidden_extra; ++l) {
+        // ---- layer 1: Dense(width) over the padded input features ----
+        f32x4 acc[NC][T4];
 #pragma unroll
         for (int c = 0; c < NC; ++c)
 #pragma unroll
-            for (int j = 0; j < T4; ++j) acc[c][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        gemm_from_lds<T4, NC>(acc, cur, reinterpret_cast<const FT*>(p.wh) + (size_t)l * (HP / 4) * 4 * 64, wave,
-                              lane);
-        bias_relu_store<T4, NC>(acc, p.bh + (size_t)l * HP, wave, lane, kr, nxt);
-        __syncthreads();
-        f32x4* t = cur;
-        cur = nxt;
-        nxt = t;
-    }
-
-    // ---- output Dense layers + denorm/limit/mask epilogue ----
-    // units u = (tile m = u / NC, column tile c = u % NC); wave w takes u = w, w+4, ...
-    // two at a time, so the 4 waves share the n_otiles*NC units evenly
-    const int nunits = p.n_otiles * NC;
-    for (int u0 = wave; u0 < nunits; u0 += 8) {
-        const int u1 = u0 + 4;
-        const bool two = u1 < nunits;
-        const int m0 = u0 / NC, c0 = u0 % NC;
-        const int m1 = two ? u1 / NC : m0, c1 = two ? u1 % NC : c0;
-        f32x4 o[2] = {f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}};
-        const f32x4* w0 = reinterpret_cast<const f32x4*>(p.wo) + (size_t)m0 * (HP / 16) * 64 + lane;
-        const f32x4* w1p = reinterpret_cast<const f32x4*>(p.wo) + (size_t)m1 * (HP / 16) * 64 + lane;
-        if (two)
-            out_units<T4, NC, 2>(o, cur + lane, w0, w1p, c0, c1);
-        else
-            out_units<T4, NC, 1>(o, cur + lane, w0, w1p, c0, c1);
+            for (int j = 0; j < T4; ++j) acc[c][j] = zero4();
+        {
+            const f32x4* xq = hbuf + lane;  // + c*kp*4 + g*64
+            const int ngroups = p.kp / 16;
+            f32x4 xb[RD][NC];
 #pragma unroll
-        for (int uu = 0; uu < 2; ++uu) {
-            if (uu == 1 && !two) break;
-            const int m = uu == 0 ? m0 : m1;
-            const int c = uu == 0 ? c0 : c1;
-            const DenseOutTile ot = p.otile[m];
-            if (ot.var < 0) continue;
-            const int64_t col = col0 + 16 * c + cl;
-            const bool valid = col < p.ncol;
-            const int64_t cc = valid ? col : col0;
-            const int64_t blk = cc / p.ncol_blk;
-            const int64_t ii = cc - blk * p.ncol_blk;
-            const f32x4 ov = o[uu];
-            float* dst = p.out_ptr[ot.var] + blk * p.out_bs[ot.var] + ii;
-            const int64_t ld = p.out_ld[ot.var];
-            const int fo = 16 * m + 4 * kr;
-            const f32x4 bo = *reinterpret_cast<const f32x4*>(p.bo + fo);
-            const f32x4 sg = *reinterpret_cast<const f32x4*>(p.o_sigma + fo);
-            const f32x4 mu = *reinterpret_cast<const f32x4*>(p.o_mean + fo);
-            const f32x4 lo = *reinterpret_cast<const f32x4*>(p.o_lo + fo);
-            const f32x4 hi = *reinterpret_cast<const f32x4*>(p.o_hi + fo);
-            const f32x4 mk = *reinterpret_cast<const f32x4*>(p.o_mask + fo);
+            for (int c = 0; c < NC; ++c) xb[0][c] = xq[c * p.kp * 4];
+            for (int gi = 0; gi < ngroups; gi += RD) {
+                static_for<RD>([&](auto hc) {
+                    constexpr int h = decltype(hc)::value;
+                    const int grp = gi + h;
+                    // RD == 2: kp is a multiple of 32, so every pair is whole and the
+                    // loads past the last group read (in-bounds) padding never used
+                    if (RD == 2 || grp < ngroups) {
+                        if (RD == 2 || grp + RD - 1 < ngroups) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = 4 * kr + r;
-                float y = ov[r] + bo[r];
-                y = y * sg[r];
-                y = y + mu[r];
-                if (y < lo[r]) y = lo[r];
-                if (y >= hi[r]) y = hi[r];
-                y = y * mk[r];
-                if (valid && row < ot.nrow) dst[(int64_t)(ot.z0 + row) * ld] = y;
+                            for (int r = 0; r < 4; ++r)
+                                g1[(h + RD - 1) % RD][r] = bload<FT>(rw, voff, p.w1_off + (4 * (grp + RD - 1) + r) * KS);
+                        }
+                        if (RD == 2 || grp + 1 < ngroups) {
+#pragma unroll
+                            for (int c = 0; c < NC; ++c)
+                                xb[(h + 1) % RD][c] = xq[c * p.kp * 4 + min(grp + 1, ngroups - 1) * 64];
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+#pragma unroll
+                            for (int j = 0; j < T4; ++j)
+#pragma unroll
+                                for (int c = 0; c < NC; ++c)
+                                    acc[c][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(frag_at<T4>(g1[h][r], j),
+                                                                                     xb[h][c][r], acc[c][j], 0, 0, 0);
+                    }
+                });
             }
         }
+        // the next tile's inputs travel while this tile runs its remaining layers
+        if (tile + gridDim.x < p.ntiles) {
+            KArgs* pn = &p;
+            asm volatile("" : "+s"(pn));
+            load_raw(*pn, tile + gridDim.x, fq);
+        }
+        prime_after(-1);
+        __syncthreads();  // every wave is done with the staged inputs
+        bias_relu_store<T4, NC>(acc, p.b1, wave, lane, kr, hbuf);
+        __syncthreads();
+        trace_mark(p, tile, 2);
+
+        // ---- further hidden layers, in place ----
+        for (int l = 0; l < p.n_hidden_extra; ++l) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+#pragma unroll
+                for (int j = 0; j < T4; ++j) acc[c][j] = zero4();
+            gemm_hidden<T4, NC, RD>(acc, hbuf, rw, voff, p.wh_off + l * (HP / 4) * KS, gh, lane);
+            prime_after(l);
+            __syncthreads();  // every wave is done reading this layer's input
+            bias_relu_store<T4, NC>(acc, p.bh + (size_t)l * HP, wave, lane, kr, hbuf);
+            __syncthreads();
+        }
+        trace_mark(p, tile, 3);
+
+        // ---- output Dense layers + bias/denorm/limit/mask epilogue ----
+        const f32x4* src = hbuf + (cw * HT) * 64 + lane;
+        const int64_t colw = tile * NCOL + 16 * cw + (lane & 15);
+        const bool cvalid = colw < p.ncol;
+        const int64_t cc = cvalid ? colw : 0;
+        const int64_t oblk = cc / p.ncol_blk;
+        const int64_t oii = cc - oblk * p.ncol_blk;
+        for (int i0 = 0; i0 < ucnt; i0 += kMaxUnits) {
+            const OutPlan pl = plan(i0);
+            if (i0 > 0) prime_out<RD>(go, rw, voff_o, pl);
+            f32x4 o[kMaxUnits];
+#pragma unroll
+            for (int i = 0; i < kMaxUnits; ++i) o[i] = zero4();
+            switch (pl.n) {
+                case 1: gemm_out<T4, 1, RD>(o, src, rw, voff_o, pl, go); break;
+                case 2: gemm_out<T4, 2, RD>(o, src, rw, voff_o, pl, go); break;
+                default: gemm_out<T4, kMaxUnits, RD>(o, src, rw, voff_o, pl, go); break;
+            }
+#pragma unroll
+            for (int i = 0; i < kMaxUnits; ++i) {
+                if (i >= pl.n) break;
+                const int m = (wave + 4 * (i0 + i)) / NC;
+                const int ovar = p.otile[m].var, oz0 = p.otile[m].z0, onrow = p.otile[m].nrow;
+                if (ovar < 0) continue;
+                float* dst = p.out_ptr[ovar] + oblk * p.out_bs[ovar] + oii;
+                const int64_t ld = p.out_ld[ovar];
+                int fo = 16 * m + 4 * kr;
+                asm volatile("" : "+v"(fo));  // keep this unit's constant reads here, not hoisted above the GEMM
+                const f32x4 bo = *reinterpret_cast<const f32x4*>(s_ep + fo);
+                const f32x4 sg = *reinterpret_cast<const f32x4*>(s_ep + kop + fo);
+                const f32x4 mu = *reinterpret_cast<const f32x4*>(s_ep + 2 * kop + fo);
+                const f32x4 lo = *reinterpret_cast<const f32x4*>(s_ep + 3 * kop + fo);
+                const f32x4 hi = *reinterpret_cast<const f32x4*>(s_ep + 4 * kop + fo);
+                const f32x4 mk = *reinterpret_cast<const f32x4*>(s_ep + 5 * kop + fo);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = 4 * kr + r;
+                    float y = o[i][r] + bo[r];
+                    y = y * sg[r];
+                    y = y + mu[r];
+                    if (y < lo[r]) y = lo[r];
+                    if (y >= hi[r]) y = hi[r];
+                    y = y * mk[r];
+                    if (cvalid && row < onrow) dst[(int64_t)(oz0 + row) * ld] = y;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        prime_ring<RD, FT>(g1, rw, voff, p.w1_off);  // the next tile's layer 1
+        __syncthreads();         // the activations are free for the next tile's inputs
+        trace_mark(p, tile, 4);
     }
 }
 
@@ -481,7 +621,7 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
     }
     m->k_in = k_in;
     m->steps_total = step;
-    while (step % 4) {  // whole groups of 4 k-steps for the layer-1 pipeline
+    while (step % 8) {  // whole pairs of groups of 4 k-steps: the layer-1 loop has no tail
         for (int i = 0; i < 4; ++i) feat_src.push_back(-1);
         ++step;
     }
@@ -579,18 +719,21 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
                 wo[(((size_t)mt * (HP / 16) + t) * 64 + l) * 4 + r] = v;
             }
         }
-    std::vector<float> bo(kop, 0.0f), osig(kop, 1.0f), omean(kop, 0.0f), olo(kop, -INFINITY),
-        ohi(kop, INFINITY), omask(kop, 1.0f);
+    // epilogue constants [6][KOP]: bias, sigma, mean, lo, hi, mask
+    std::vector<float> oep((size_t)6 * kop);
     for (int row = 0; row < kop; ++row) {
+        float v[6] = {0.0f, 1.0f, 0.0f, -INFINITY, INFINITY, 1.0f};
         const int src = ofeat_src[row];
-        if (src < 0) continue;
-        const int ov = ocol_var[src], oz = ocol_z[src];
-        bo[row] = d->out_bias[ov][oz];
-        osig[row] = d->out_sigma[src];
-        omean[row] = d->out_mean[src];
-        if (d->out_min) olo[row] = d->out_min[src];
-        if (d->out_max) ohi[row] = d->out_max[src];
-        if (d->out_mask) omask[row] = d->out_mask[src];
+        if (src >= 0) {
+            const int ov = ocol_var[src], oz = ocol_z[src];
+            v[0] = d->out_bias[ov][oz];
+            v[1] = d->out_sigma[src];
+            v[2] = d->out_mean[src];
+            if (d->out_min) v[3] = d->out_min[src];
+            if (d->out_max) v[4] = d->out_max[src];
+            if (d->out_mask) v[5] = d->out_mask[src];
+        }
+        for (int k = 0; k < 6; ++k) oep[(size_t)k * kop + row] = v[k];
     }
 
     // ---- one device allocation ----
@@ -603,17 +746,16 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
         {in_mean.data(), in_mean.size() * 4, 0}, {in_denom.data(), in_denom.size() * 4, 0},
         {w1.data(), w1.size() * 4, 0},           {b1.data(), b1.size() * 4, 0},
         {wh.data(), wh.size() * 4, 0},           {bh.data(), bh.size() * 4, 0},
-        {wo.data(), wo.size() * 4, 0},           {bo.data(), bo.size() * 4, 0},
-        {osig.data(), osig.size() * 4, 0},       {omean.data(), omean.size() * 4, 0},
-        {olo.data(), olo.size() * 4, 0},         {ohi.data(), ohi.size() * 4, 0},
-        {omask.data(), omask.size() * 4, 0},
+        {wo.data(), wo.size() * 4, 0},           {oep.data(), oep.size() * 4, 0},
     };
     size_t total = 0;
     for (auto& p : pcs) {
         p.off = total;
         total += (p.bytes + 255) / 256 * 256;
     }
-    FV3_HIP(hipMalloc(&m->dbuf, total));
+    size_t alloc = total;
+    if (const char* e = getenv("FV3_DENSE_PAD_MB")) alloc = std::max(alloc, (size_t)atoi(e) << 20);
+    FV3_HIP(hipMalloc(&m->dbuf, alloc));
     for (auto& p : pcs) FV3_HIP(hipMemcpy((char*)m->dbuf + p.off, p.src, p.bytes, hipMemcpyHostToDevice));
     auto at = [&](int i) { return (char*)m->dbuf + pcs[i].off; };
     DenseArgs& a = m->tmpl;
@@ -624,18 +766,13 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
     a.wh = (const float*)at(4);
     a.bh = (const float*)at(5);
     a.wo = (const float*)at(6);
-    a.bo = (const float*)at(7);
-    a.o_sigma = (const float*)at(8);
-    a.o_mean = (const float*)at(9);
-    a.o_lo = (const float*)at(10);
-    a.o_hi = (const float*)at(11);
-    a.o_mask = (const float*)at(12);
-    for (int v = 0; v < m->n_in; ++v) {
-        a.in[v].step0 = m->in_step0[v];
-        a.in[v].nsteps = m->in_nsteps[v];
-        a.in[v].z0 = m->in_z0[v];
-        a.in[v].nkeep = m->in_nkeep[v];
-    }
+    a.oep = (const float*)at(7);
+    FV3_REQUIRE(total < (1u << 31), "dense_create: model too large for 32-bit buffer offsets");
+    a.wbase = (const float*)m->dbuf;
+    a.w1_off = (int)pcs[2].off;
+    a.wh_off = (int)pcs[4].off;
+    a.wo_off = (int)pcs[6].off;
+    a.wbytes = (int)total;
     for (int t = 0; t < m->n_otiles; ++t) a.otile[t] = m->otiles[t];
     a.n_in = m->n_in;
     a.n_hidden_extra = nhx;
@@ -643,6 +780,14 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
     a.kp = m->kp;
     a.in_steps_total = m->steps_total;
     *out = guard.release();
+    return FV3_OK;
+}
+
+extern "C" int fv3_dense_set_trace(fv3_dense_model* m, long long* trace)
+{
+    fv3::clear_error();
+    FV3_REQUIRE(m, "dense_set_trace: NULL model");
+    m->tmpl.trace = trace;
     return FV3_OK;
 }
 
@@ -673,9 +818,8 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
         FV3_REQUIRE(inputs[v], "dense_forward: input %d is NULL", v);
         FV3_REQUIRE(layout_ok(in_l[v], ncol) && in_l[v].ncol_blk == nb,
                     "dense_forward: input %d layout invalid or ncol_blk differs", v);
-        a.in[v].ptr = inputs[v];
-        a.in[v].ld = in_l[v].ld;
-        a.in[v].bs = in_l[v].blk_stride;
+        FV3_REQUIRE(in_l[v].ld < (1LL << 31) && in_l[v].blk_stride < (1LL << 31),
+                    "dense_forward: input %d strides exceed 2^31 elements", v);
     }
     for (int v = 0; v < m->n_out; ++v) {
         FV3_REQUIRE(outputs[v], "dense_forward: output %d is NULL", v);
@@ -687,33 +831,78 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
     }
     a.ncol = ncol;
     a.ncol_blk = nb;
-    // columns per block: two 16-column tiles (measured fastest at C48/C96/C384:
-    // halves weight traffic per FLOP; 2 blocks/CU by LDS)
+    // columns per tile: two 16-column tiles (halves weight traffic per FLOP; measured
+    // fastest at C48 and C384); FV3_DENSE_NC=1 for A/B
     int nc = 2;
-    if (const char* e = getenv("FV3_DENSE_NC")) {
-        nc = atoi(e) == 1 ? 1 : 2;  // A/B switch; 2 is fastest at C48, C96 and C384
+    if (const char* e = getenv("FV3_DENSE_NC")) nc = atoi(e) == 1 ? 1 : 2;
+    const int ncol_tile = 16 * nc;
+    a.ntiles = (ncol + ncol_tile - 1) / ncol_tile;
+    // input slots: 256 threads read 256 / ncol_tile feature rows of one variable
+    const int fps = 256 / ncol_tile;
+    a.nslots = 0;
+    for (int v = 0; v < m->n_in; ++v) {
+        const int nf_v = 4 * m->in_nsteps[v], nk_v = m->in_nkeep[v];
+        for (int f0 = 0; f0 < nf_v; f0 += fps) {
+            FV3_REQUIRE(a.nslots < kMaxSlots, "dense_forward: %d input features are too many", m->kp);
+            const int q = a.nslots++;
+            const int zf = std::min(m->in_z0[v] + f0, m->in_nz[v] - 1);  // never dereferenced past nk
+            a.slot_base[q] = inputs[v] + (int64_t)zf * in_l[v].ld;
+            a.slot_bs[q] = (int)in_l[v].blk_stride;
+            a.slot_ld[q] = (int)in_l[v].ld;
+            const int nk = std::max(0, std::min(nk_v - f0, 255));
+            const int nf = std::min(nf_v - f0, 255);
+            a.slot_meta[q] = ((4 * m->in_step0[v] + f0) << 16) | (nk << 8) | nf;
+        }
     }
-    const int64_t grid = (ncol + 16 * nc - 1) / (16 * nc);
-    FV3_REQUIRE(grid < (int64_t)0x7fffffff, "dense_forward: ncol too large");
     hipStream_t s = (hipStream_t)stream;
-    // buf0: one layer of activations (NC x HT tiles x 64 lanes x 16 B); buf1: the other
-    // layer, or the staged inputs (NC x kp features x 16 columns) if those are larger
+    // LDS: activations (NC x HT tiles x 64 lanes x 16 B) or the staged inputs
+    // (NC x kp features x 16 columns), whichever is larger, then the constants
     const size_t hbytes = (size_t)nc * 16 * 64 * (size_t)m->ht;
     const size_t xbytes = (size_t)nc * sizeof(float) * 16 * (size_t)m->kp;
-    const size_t lds = hbytes + std::max(hbytes, xbytes);
+    const size_t abytes = std::max(hbytes, xbytes);
+    a.lds_x = (int)(abytes / 16);
+    const size_t lds = abytes + sizeof(float) * (2 * (size_t)m->kp + 6 * 16 * (size_t)m->n_otiles);
     FV3_REQUIRE(lds <= 160 * 1024, "dense_forward: %d input features need too much LDS", m->kp);
-#define FV3_DENSE_LAUNCH(T4, NC) \
-    hipLaunchKernelGGL((dense_forward_kernel<T4, NC>), dim3((unsigned)grid), dim3(256), lds, s, a)
-    if (nc == 1) {
-        if (m->ht == 4) FV3_DENSE_LAUNCH(1, 1);
-        else if (m->ht == 8) FV3_DENSE_LAUNCH(2, 1);
-        else FV3_DENSE_LAUNCH(4, 1);
-    } else {
-        if (m->ht == 4) FV3_DENSE_LAUNCH(1, 2);
-        else if (m->ht == 8) FV3_DENSE_LAUNCH(2, 2);
-        else FV3_DENSE_LAUNCH(4, 2);
+    // (waves per SIMD targeted by register allocation, weight ring depth):
+    // FV3_DENSE_CFG = "3,2" (default) | "2,3" | "4,2" (A/B; NC=1 only builds "2,3")
+    int wpe = 3, rd = 2;  // measured best at C48 and C384
+    if (const char* e = getenv("FV3_DENSE_CFG")) {
+        if (!strcmp(e, "2,3")) wpe = 2, rd = 3;
+        else if (!strcmp(e, "4,2")) wpe = 4, rd = 2;
     }
-#undef FV3_DENSE_LAUNCH
+    if (nc == 1) wpe = 2, rd = 3;
+    auto kernel_of = [&](int t4) -> const void* {
+#define FV3_K(T4, NC, W, R) (const void*)dense_forward_kernel<T4, NC, W, R>
+        if (nc == 1) return t4 == 1 ? FV3_K(1, 1, 2, 3) : t4 == 2 ? FV3_K(2, 1, 2, 3) : FV3_K(4, 1, 2, 3);
+        if (wpe == 3) return t4 == 1 ? FV3_K(1, 2, 3, 2) : t4 == 2 ? FV3_K(2, 2, 3, 2) : FV3_K(4, 2, 3, 2);
+        if (wpe == 4) return t4 == 1 ? FV3_K(1, 2, 4, 2) : t4 == 2 ? FV3_K(2, 2, 4, 2) : FV3_K(4, 2, 4, 2);
+        return t4 == 1 ? FV3_K(1, 2, 2, 3) : t4 == 2 ? FV3_K(2, 2, 2, 3) : FV3_K(4, 2, 2, 3);
+#undef FV3_K
+    };
+    const void* kfn = kernel_of(m->ht / 4);
+    // persistent blocks: resident blocks per CU x CUs (queried once per kernel);
+    // FV3_DENSE_GRID overrides (A/B)
+    static std::mutex mu;
+    static int n_cu = 0;
+    static std::vector<std::pair<const void*, int>> resident;
+    std::lock_guard<std::mutex> lock(mu);
+    if (!n_cu) {
+        int dev = 0;
+        FV3_HIP(hipGetDevice(&dev));
+        FV3_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    int res = 0;
+    for (auto& r : resident)
+        if (r.first == kfn) res = r.second;
+    if (!res) {
+        FV3_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&res, kfn, 256, lds));
+        res = std::max(1, res);
+        resident.push_back({kfn, res});
+    }
+    int64_t grid = std::min<int64_t>(a.ntiles, (int64_t)res * n_cu);
+    if (const char* e = getenv("FV3_DENSE_GRID")) grid = std::min<int64_t>(a.ntiles, std::max(1, atoi(e)));
+    void* kargs[] = {&a};
+    FV3_HIP(hipLaunchKernel(kfn, dim3((unsigned)grid), dim3(256), kargs, lds, s));
     FV3_LAUNCH_CHECK();
     return FV3_OK;
 }

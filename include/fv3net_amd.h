@@ -100,6 +100,11 @@ int fv3_dense_destroy(fv3_dense_model* model);
 int fv3_dense_k_in(const fv3_dense_model* model);
 int fv3_dense_k_out(const fv3_dense_model* model);
 
+/* Profiling hook: when `trace` (device, >= 8 * n_blocks int64) is non-NULL, every
+ * forward writes per-block phase timestamps (wall_clock64, 100 MHz) and the CU id.
+ * Not for concurrent use; pass NULL to disable (the default). */
+int fv3_dense_set_trace(fv3_dense_model* model, long long* trace);
+
 /* Forward over ncol columns.  inputs[v] is input variable v (all of its in_nz[v]
  * levels) with layout in_l[v]; outputs[o] receives out_nz[o] levels.  All
  * layouts must share ncol_blk.  Synchronous-free: enqueued on `stream`. */
