@@ -864,16 +864,19 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
     const size_t lds = abytes + sizeof(float) * (2 * (size_t)m->kp + 6 * 16 * (size_t)m->n_otiles);
     FV3_REQUIRE(lds <= 160 * 1024, "dense_forward: %d input features need too much LDS", m->kp);
     // (waves per SIMD targeted by register allocation, weight ring depth):
-    // FV3_DENSE_CFG = "3,2" (default) | "2,3" | "4,2" (A/B; NC=1 only builds "2,3")
+    // FV3_DENSE_CFG = "3,2" (default) | "2,3" | "4,2" (A/B)
     int wpe = 3, rd = 2;  // measured best at C48 and C384
     if (const char* e = getenv("FV3_DENSE_CFG")) {
         if (!strcmp(e, "2,3")) wpe = 2, rd = 3;
         else if (!strcmp(e, "4,2")) wpe = 4, rd = 2;
     }
-    if (nc == 1) wpe = 2, rd = 3;
     auto kernel_of = [&](int t4) -> const void* {
 #define FV3_K(T4, NC, W, R) (const void*)dense_forward_kernel<T4, NC, W, R>
-        if (nc == 1) return t4 == 1 ? FV3_K(1, 1, 2, 3) : t4 == 2 ? FV3_K(2, 1, 2, 3) : FV3_K(4, 1, 2, 3);
+        if (nc == 1) {
+            if (wpe == 3) return t4 == 1 ? FV3_K(1, 1, 3, 2) : t4 == 2 ? FV3_K(2, 1, 3, 2) : FV3_K(4, 1, 3, 2);
+            if (wpe == 4) return t4 == 1 ? FV3_K(1, 1, 4, 2) : t4 == 2 ? FV3_K(2, 1, 4, 2) : FV3_K(4, 1, 4, 2);
+            return t4 == 1 ? FV3_K(1, 1, 2, 3) : t4 == 2 ? FV3_K(2, 1, 2, 3) : FV3_K(4, 1, 2, 3);
+        }
         if (wpe == 3) return t4 == 1 ? FV3_K(1, 2, 3, 2) : t4 == 2 ? FV3_K(2, 2, 3, 2) : FV3_K(4, 2, 3, 2);
         if (wpe == 4) return t4 == 1 ? FV3_K(1, 2, 4, 2) : t4 == 2 ? FV3_K(2, 2, 4, 2) : FV3_K(4, 2, 4, 2);
         return t4 == 1 ? FV3_K(1, 2, 2, 3) : t4 == 2 ? FV3_K(2, 2, 2, 3) : FV3_K(4, 2, 2, 3);
