@@ -100,7 +100,9 @@ _SIGNATURES = {
 
 
 def library_path() -> str:
-    return LIB
+    """The HIP library; FV3NET_AMD_LIB points at an alternative build (A/B of kernel
+    variants in tools/), which must export the same ABI."""
+    return os.environ.get("FV3NET_AMD_LIB", LIB)
 
 
 def load():
@@ -111,16 +113,17 @@ def load():
     with _lock:
         if _lib is not None:
             return _lib
-        if not os.path.exists(LIB):
+        path = library_path()
+        if not os.path.exists(path):
             raise NativeLibraryError(
-                f"fv3net_amd HIP extension not built: {LIB} is missing "
+                f"fv3net_amd HIP extension not built: {path} is missing "
                 "(run `python -m fv3net_amd.build` or __graft_entry__.build()); "
                 "there is no CPU fallback"
             )
         try:
-            lib = ctypes.CDLL(LIB)
+            lib = ctypes.CDLL(path)
         except OSError as e:
-            raise NativeLibraryError(f"cannot load {LIB}: {e}") from e
+            raise NativeLibraryError(f"cannot load {path}: {e}") from e
         for name, (res, args) in _SIGNATURES.items():
             fn = getattr(lib, name)
             fn.restype = res

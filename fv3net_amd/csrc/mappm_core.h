@@ -405,6 +405,229 @@ FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
     remap_finish(s, ends, kn, c);
 }
 
+// ---- resumable PPM column (kord <= 7): one OUTPUT level per call ----
+//
+// The arithmetic of mappm_ppm_column, in the same order, restructured so that the
+// caller drives it by output level: next() returns q2(k) for k = 1, 2, ... kn.
+// Each call ingests as many input layers as this column needs (a per-lane,
+// data-dependent loop); between calls every lane of a wave is reconverged, which the
+// fused coarse-graining kernel uses to combine neighbouring columns level by level
+// with cross-lane shuffles instead of staging whole columns in LDS.
+// `Col` as for mappm_ppm_column (emit() unused).
+
+// One output-layer event of remap_layer: true (value in `val`, state advanced to the
+// next output layer) or false (this input layer is exhausted: move to L+1).
+template <class Out>
+FV3_HD inline bool remap_one(RemapState& s, const LayerView& v, const ColumnEnds& e, Out& out, float& val)
+{
+    const float r3 = 1.0f / 3.0f, r23 = 2.0f / 3.0f;
+    if (!s.accum) {
+        if (s.t <= e.pe_top) {
+            val = e.q_top;
+        } else if (s.t >= e.pe_bot) {
+            val = e.q_bot;
+        } else if (s.t >= v.pl0 && s.t <= v.pl1) {
+            const float pl = (s.t - v.pl0) / v.dp;
+            if (s.b <= v.pl1) {
+                const float pr = (s.b - v.pl0) / v.dp;
+                const float tt = r3 * (pr * (pr + pl) + pl * pl);
+                val = v.a.al + 0.5f * (v.a.a6 + v.a.ar - v.a.al) * (pr + pl) - v.a.a6 * tt;
+            } else {
+                const float delp = v.pl1 - s.t;
+                const float tt = r3 * (1.0f + pl * (1.0f + pl));
+                s.qsum = delp * (v.a.al + 0.5f * (v.a.a6 + v.a.ar - v.a.al) * (1.0f + pl) - v.a.a6 * tt);
+                s.dpsum = delp;
+                s.accum = true;
+                return false;
+            }
+        } else {
+            return false;
+        }
+    } else {
+        if (s.b > v.pl1) {
+            s.qsum = s.qsum + v.dp * v.q1;
+            s.dpsum = s.dpsum + v.dp;
+            return false;
+        }
+        const float delp = s.b - v.pl0;
+        const float esl = delp / v.dp;
+        s.qsum = s.qsum + delp * (v.a.al + 0.5f * esl * (v.a.ar - v.a.al + v.a.a6 * (1.0f - r23 * esl)));
+        s.dpsum = s.dpsum + delp;
+        val = s.qsum / s.dpsum;
+        s.accum = false;
+    }
+    s.k += 1;
+    s.t = s.b;
+    s.b = out.next_edge(s.k);
+    return true;
+}
+
+template <class Col>
+struct PpmCursor {
+    Col& c;
+    int km, kn, iv, kord, lmt;
+    bool huynh;
+    float qv[4], dpv[4], pev[5], dcv[3], alv[3], h2v[3];
+    float ar_km;
+    ColumnEnds ends;
+    RemapState s;
+    LayerView v;
+    int L;      // current input layer (1-based); km + 1 once all are consumed
+    bool have;  // v holds layer L's final coefficients
+
+    FV3_HD PpmCursor(Col& col, int km_, int kn_, int iv_, int kord_)
+        : c(col), km(km_), kn(kn_), iv(iv_), kord(kord_), ar_km(0.0f), L(1), have(false)
+    {
+        huynh = kord >= 7;
+        for (int i = 0; i < 4; ++i) qv[i] = c.q1(1 + i);
+        for (int i = 0; i < 5; ++i) pev[i] = c.pe1(1 + i);
+        for (int i = 0; i < 4; ++i) dpv[i] = pev[i + 1] - pev[i];
+        ends = ColumnEnds{pev[0], c.pe1(km + 1), qv[0], c.q1(km)};
+        float dc1, dc2, dc3, al1, al2, al3;
+        dc2 = ppm_dc(qv[0], qv[1], qv[2], dpv[0], dpv[1], dpv[2]);
+        dc3 = ppm_dc(qv[1], qv[2], qv[3], dpv[1], dpv[2], dpv[3]);
+        al3 = ppm_al(dpv[0], dpv[1], dpv[2], dpv[3], qv[1], qv[2], dc2, dc3);
+        {   // top: area-preserving cubic (mappm.f90:689-725)
+            const float d1 = dpv[0], d2 = dpv[1];
+            const float q1 = qv[0], q2 = qv[1];
+            const float qm = (d2 * q1 + d1 * q2) / (d1 + d2);
+            const float dq = 2.0f * (q2 - q1) / (d1 + d2);
+            const float c1 = 4.0f * (al3 - qm - d2 * dq) / (d2 * (2.0f * d2 * d2 + d1 * (d2 + 3.0f * d1)));
+            const float c3 = dq - 0.5f * c1 * (d2 * (5.0f * d1 + d2) - 3.0f * d1 * d1);
+            al2 = qm - 0.25f * c1 * d1 * d2 * (d2 + 3.0f * d1);
+            al1 = d1 * (2.0f * c1 * (d1 * d1) - c3) + al2;
+            al2 = fmax2(al2, fmin2(q1, q2));
+            al2 = fmin2(al2, fmax2(q1, q2));
+            dc1 = 0.5f * (al2 - q1);
+            if (iv == 0) {
+                al1 = fmax2(0.0f, al1);
+                al2 = fmax2(0.0f, al2);
+            } else if (iv == -1) {
+                if (al1 * q1 <= 0.0f) al1 = 0.0f;
+            } else if (iv == 2 || iv == -2) {
+                al1 = q1;
+            }
+        }
+        dcv[0] = dc1; dcv[1] = dc2; dcv[2] = dc3;
+        alv[0] = al1; alv[1] = al2; alv[2] = al3;
+        h2v[0] = 0.0f; h2v[1] = 0.0f;
+        h2v[2] = huynh ? ppm_h2(dc1, dc3, dpv[0], dpv[1], dpv[2]) : 0.0f;
+        lmt = kord - 3;
+        lmt = lmt > 0 ? lmt : 0;
+        if (iv == 0) lmt = lmt < 2 ? lmt : 2;
+        s = RemapState{1, false, 0.0f, 0.0f, c.pe2(1), c.pe2(2)};
+    }
+
+    // final coefficients of layer L (the top of mappm_ppm_column's L loop)
+    FV3_HD void load_layer()
+    {
+        Ppm a{qv[0], alv[0], (L < km) ? alv[1] : ar_km, 0.0f};
+        const float dcL = dcv[0];
+        if (L <= 2 || L >= km - 1) {
+            a.a6 = a6_of(a);
+            ppm_limit(dcL, a, 0);
+        } else if (huynh) {
+            ppm_huynh(a, dcL, h2v[0], h2v[2]);
+            if (iv == 0) ppm_limit(dcL, a, 2);
+        } else {
+            if (kord != 4) a.a6 = a6_of(a);
+            if (kord != 6) ppm_limit(dcL, a, lmt);
+        }
+        v = LayerView{pev[0], pev[1], dpv[0], qv[0], a};
+        have = true;
+    }
+
+    // window E_L -> E_{L+1} (the bottom of mappm_ppm_column's L loop)
+    FV3_HD void advance()
+    {
+        have = false;
+        if (L == km) {
+            L = km + 1;
+            return;
+        }
+        const int j = L + 4;
+        float qn = 0.0f, pen = 0.0f, dpn = 0.0f;
+        if (j <= km) {
+            qn = c.q1(j);
+            pen = c.pe1(j + 1);
+            dpn = pen - pev[4];
+        }
+        const int m = L + 3;
+        float dcm = 0.0f, alm = 0.0f;
+        if (m <= km - 1) {
+            dcm = ppm_dc(qv[2], qv[3], qn, dpv[2], dpv[3], dpn);
+            alm = ppm_al(dpv[1], dpv[2], dpv[3], dpn, qv[2], qv[3], dcv[2], dcm);
+        } else if (m == km) {
+            const float d1 = dpv[3], d2 = dpv[2];
+            const float qk = qv[3], qk1 = qv[2];
+            const float qm = (d2 * qk + d1 * qk1) / (d1 + d2);
+            const float dq = 2.0f * (qk1 - qk) / (d1 + d2);
+            const float c1 = (alv[2] - qm - d2 * dq) / (d2 * (2.0f * d2 * d2 + d1 * (d2 + 3.0f * d1)));
+            const float c3 = dq - 2.0f * c1 * (d2 * (5.0f * d1 + d2) - 3.0f * d1 * d1);
+            alm = qm - c1 * d1 * d2 * (d2 + 3.0f * d1);
+            float ar = d1 * (8.0f * c1 * (d1 * d1) - c3) + alm;
+            alm = fmax2(alm, fmin2(qk, qk1));
+            alm = fmin2(alm, fmax2(qk, qk1));
+            dcm = 0.5f * (qk - alm);
+            if (iv == 0) {
+                alm = fmax2(0.0f, alm);
+                ar = fmax2(0.0f, ar);
+            } else if (iv < 0) {
+                if (qk * ar <= 0.0f) ar = 0.0f;
+            }
+            ar_km = ar;
+        }
+        float h2n = 0.0f;
+        if (huynh && L + 2 <= km - 1) h2n = ppm_h2(dcv[1], dcm, dpv[1], dpv[2], dpv[3]);
+        qv[0] = qv[1]; qv[1] = qv[2]; qv[2] = qv[3]; qv[3] = qn;
+        dpv[0] = dpv[1]; dpv[1] = dpv[2]; dpv[2] = dpv[3]; dpv[3] = dpn;
+        pev[0] = pev[1]; pev[1] = pev[2]; pev[2] = pev[3]; pev[3] = pev[4]; pev[4] = pen;
+        dcv[0] = dcv[1]; dcv[1] = dcv[2]; dcv[2] = dcm;
+        alv[0] = alv[1]; alv[1] = alv[2]; alv[2] = alm;
+        h2v[0] = h2v[1]; h2v[1] = h2v[2]; h2v[2] = h2n;
+        L += 1;
+    }
+
+    // q2(k) for the next output layer k = s.k (remap_layer / remap_finish semantics)
+    FV3_HD float next()
+    {
+        float val = 0.0f;
+        while (L <= km) {
+            if (!have) load_layer();
+            if (remap_one(s, v, ends, c, val)) return val;
+            advance();
+        }
+        // below the last input layer (mappm.f90:115-121, 62-67)
+        if (s.accum) {
+            const float delp = s.b - ends.pe_bot;
+            if (delp > 0.0f) {
+                s.qsum = s.qsum + delp * ends.q_bot;
+                s.dpsum = s.dpsum + delp;
+            }
+            val = s.qsum / s.dpsum;
+            s.accum = false;
+        } else if (s.t <= ends.pe_top) {
+            val = ends.q_top;
+        } else if (s.t >= ends.pe_bot) {
+            val = ends.q_bot;
+        } else {
+            val = __builtin_nanf("");  // search failed: reference UB
+        }
+        s.k += 1;
+        s.t = s.b;
+        s.b = c.next_edge(s.k);
+        return val;
+    }
+};
+
+// mappm_ppm_column driven through the cursor (host test of the cursor's equivalence)
+template <class Col>
+FV3_HD inline void mappm_ppm_column_by_output(Col& c, int km, int kn, int iv, int kord)
+{
+    PpmCursor<Col> cur(c, km, kn, iv, kord);
+    for (int k = 1; k <= kn; ++k) c.emit(k, cur.next());
+}
+
 // ---- one column, kord > 7 (cs_profile path) ----
 //
 // `Scr` is per-column scratch of 2*(km+2) floats: edge(k) for k = 1..km+1 and

@@ -38,3 +38,15 @@ extern "C" int host_mappm(int km, const float* pe1, const float* q1, int kn, con
     }
     return 0;
 }
+
+// same through the output-driven cursor (kord <= 7), as the fused coarsen kernel uses it
+extern "C" int host_mappm_cursor(int km, const float* pe1, const float* q1, int kn, const float* pe2,
+                                 float* q2, int64_t ncol, int iv, int kord)
+{
+    if (km < 4 || kn < 1 || kord > 7) return -1;
+    for (int64_t i = 0; i < ncol; ++i) {
+        Col c{pe1, q1, pe2, q2, ncol, i, kn};
+        fv3::mappm_ppm_column_by_output(c, km, kn, iv, kord);
+    }
+    return 0;
+}

@@ -83,18 +83,19 @@ def host_lib():
     subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
                     "-o", HOST_SO, HOST_SRC], check=True)
     lib = ctypes.CDLL(HOST_SO)
-    lib.host_mappm.restype = ctypes.c_int
-    lib.host_mappm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
-                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
-                               ctypes.c_int]
+    for fn in (lib.host_mappm, lib.host_mappm_cursor):
+        fn.restype = ctypes.c_int
+        fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                       ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
     return lib
 
 
-def _host(lib, pe1, q, pe2, iv, kord):
+def _host(lib, pe1, q, pe2, iv, kord, cursor=False):
     pe1, q, pe2 = (np.ascontiguousarray(a, np.float32) for a in (pe1, q, pe2))
     out = np.empty((pe2.shape[0] - 1, q.shape[1]), np.float32)
-    rc = lib.host_mappm(q.shape[0], pe1.ctypes.data, q.ctypes.data, pe2.shape[0] - 1,
-                        pe2.ctypes.data, out.ctypes.data, q.shape[1], iv, kord)
+    fn = lib.host_mappm_cursor if cursor else lib.host_mappm
+    rc = fn(q.shape[0], pe1.ctypes.data, q.ctypes.data, pe2.shape[0] - 1, pe2.ctypes.data, out.ctypes.data,
+            q.shape[1], iv, kord)
     assert rc == 0
     return out
 
@@ -134,3 +135,38 @@ def test_streaming_algorithm_matches_oracle_random(host_lib, km, kn):
             q = (rng.normal(0, 1, (km, ncol)) * rng.choice([1e-4, 1, 300], (km, ncol))).astype(np.float32)
             assert _bits_equal(_host(host_lib, pe1, q, pe2, iv, kord),
                                oracle_mappm(pe1, q, pe2, iv, kord)), (kord, iv)
+
+
+@pytest.mark.parametrize("km,kn", [(4, 3), (5, 9), (6, 2), (79, 79), (79, 50), (127, 40)])
+def test_output_driven_cursor_is_bit_identical(host_lib, km, kn):
+    """The output-driven PpmCursor (fused coarsen kernel) == the streaming column ==
+    the oracle, bit for bit, for every PPM kord and iv, incl. shared edges and
+    output edges beyond the input column."""
+    rng = np.random.default_rng(km * 7 + kn)
+    for kord in (0, 1, 2, 3, 4, 5, 6, 7):
+        for iv in (0, 1, -1, 2, -2):
+            ncol = 64
+            delp = rng.uniform(1, 3000, (km, ncol)).astype(np.float32)
+            pe1 = np.concatenate([np.full((1, ncol), 300, np.float32),
+                                  300 + np.cumsum(delp, 0, dtype=np.float32)])
+            pe2 = np.sort(rng.uniform(pe1[0] * 0.8, pe1[-1] * 1.1, (kn + 1, ncol)), 0).astype(np.float32)
+            m = min(km, kn) + 1
+            pe2[: m // 2] = pe1[: m // 2]
+            pe2 = np.sort(pe2, 0)
+            q = (rng.normal(0, 1, (km, ncol)) * rng.choice([1e-4, 1, 300], (km, ncol))).astype(np.float32)
+            cur = _host(host_lib, pe1, q, pe2, iv, kord, cursor=True)
+            assert _bits_equal(cur, _host(host_lib, pe1, q, pe2, iv, kord)), (kord, iv)
+            assert _bits_equal(cur, oracle_mappm(pe1, q, pe2, iv, kord)), (kord, iv)
+
+
+def test_output_driven_cursor_golden(host_lib):
+    g = np.load(os.path.join(GOLDEN, "mappm_golden.npz"))
+    for ci in range(len(g["cases"])):
+        pe1, pe2 = g[f"c{ci}_pe1"], g[f"c{ci}_pe2"]
+        for kord in g["kords"]:
+            if kord > 7:
+                continue
+            for iv in g["ivs"]:
+                for qn in ("qs", "qr"):
+                    res = _host(host_lib, pe1, g[f"c{ci}_{qn}"], pe2, int(iv), int(kord), cursor=True)
+                    assert _bits_equal(res, g[f"c{ci}_{qn}_k{kord}_iv{iv}"]), (ci, qn, kord, iv)
