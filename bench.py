@@ -219,7 +219,7 @@ def main():
             "parallelism": f"columns sharded, 1 process/GPU x {world}",
         },
         "roofline": {
-            "kernel": "fv3::dense_forward_kernel<4,2> (csrc/dense.hip)",
+            "kernel": "fv3::dense_forward_kernel<4,2,3,2> (csrc/dense.hip)",
             "bound": "mfma",
             "achieved": achieved,
             "peak": W.FP32_MFMA_PEAK_TFLOPS,

@@ -12,22 +12,28 @@
 //   weighted_block_average(f_regrid, masked_area, f)        coarsen.py:183-218
 // in ONE kernel and one pass over each input field.
 //
-// Mapping: one wave per coarse cell; lane (dy, dx) owns fine column (f*Y+dy, f*X+dx)
-// (f <= 8, lanes >= f*f idle).  Pass 1 streams delp once: every lane keeps its own
-// cumsum (fine phalf; the surface value is kept for the mask) and stages delp*area in
-// LDS, 16 levels at a time, from which delp_c and the coarse phalf are formed.  Per
-// field: each lane runs the one-pass streaming mappm (mappm_core.h) with p_in
-// recomputed from L2-hot delp, stages its remapped column in LDS [level][65]
-// (padded: conflict-free), then lane k reduces level k over the block.
+// Mapping: a block is one coarse row segment: f waves, wave dy = fine row dy of the
+// coarse row, lane = one of 64 consecutive fine columns (C = 64 / f coarse cells x f),
+// so every per-level load is one coalesced 256 B row.  Pass 1 streams delp once:
+// each lane keeps its fine phalf cumsum, delp*area is combined over the block per
+// level (row sums by cross-lane shuffles, rows through LDS) into delp_c and the
+// coarse phalf.  Per field: every lane runs the output-driven streaming mappm
+// (PpmCursor, mappm_core.h) on its column with p_in rebuilt from delp; after each
+// output level the wave is reconverged, so the masked products are row-summed by
+// shuffles right away and only [level][row][cell] partials go to LDS.
 //
 // Arithmetic follows the reference's dtype flow exactly (oracle/coarsen.py): delp
 // products, sums, delp_c and both cumsums in delp's dtype DT (float64 for restart
 // data), area and masked-field sums in float32, and every f x f block sum in
 // numpy's order for a C-order (.., Y, f, X, f) reshape summed over the two f axes:
 // each x-row reduced on its own (sequentially for f < 8, numpy's 8-way pairwise
-// kernel for f = 8), rows then added in y order.  Deterministic run to run.
+// kernel for f = 8, which is exactly an xor-shuffle tree over 8 aligned lanes), rows
+// then added in y order; NaN terms count as 0 (xarray's NaN-skipping sum).
+// Deterministic run to run.
 // Roofline: HBM-bound, (79 delp + 79*n_fields + 1 area) * 4 B per fine column read
-// once (+ ~4/f^2 of that written); delp is re-read per field from L2, not HBM.
+// once (+ ~(1 + n_fields) * 79 * 4 / f^2 written); delp is re-read per field (L2/MALL).
+// Measured VALU-bound like the standalone mappm (the PPM arithmetic with its IEEE
+// divisions dominates).
 #define FV3_HD __host__ __device__
 #include "common.h"
 #include "mappm_core.h"
@@ -37,10 +43,6 @@ namespace {
 
 constexpr int kMaxLev = 128;
 constexpr int kMaxFields = 32;  // field/output pointers travel in the kernel arguments
-constexpr int kStride = 65;  // LDS row stride (floats) of the per-field staging buffer
-constexpr int kOffPb = 1040;                    // after pc[kMaxLev + 1] doubles, 16-aligned
-constexpr int kOffArea = kOffPb + 64 * 8;
-constexpr int kOffStage = kOffArea + 64 * 4;    // 1808: 16-aligned
 
 template <typename DT>
 struct CoarsenArgs {
@@ -53,7 +55,10 @@ struct CoarsenArgs {
     double ptop;
 };
 
-constexpr int kChunk = 16;   // delp*area levels staged per pass-1 round
+constexpr int kChunk = 16;  // delp*area levels staged per pass-1 round
+
+template <typename T>
+__device__ __forceinline__ T nan0(T x) { return x != x ? T(0) : x; }  // nansum: NaN terms count as 0
 
 // numpy's np.sum over the two f axes of a C-order (.., Y, f, X, f) block: val(j) is
 // element j = dy*f + dx.  A reduced contiguous row goes through pairwise_sum
@@ -76,6 +81,22 @@ __device__ __forceinline__ T block_sum(int f, V val)
     return acc;
 }
 
+// the same row sum across the f lanes of this lane's cell (every lane of the cell
+// gets the identical value): f == 8 pairwise == xor tree over aligned 8-lane groups
+template <typename T>
+__device__ __forceinline__ T row_sum(T v, int f, int base)
+{
+    if (f == 8) {
+        v = v + __shfl_xor(v, 1, 64);
+        v = v + __shfl_xor(v, 2, 64);
+        v = v + __shfl_xor(v, 4, 64);
+        return v;
+    }
+    T s = __shfl(v, base, 64);
+    for (int i = 1; i < f; ++i) s = s + __shfl(v, base + i, 64);
+    return s;
+}
+
 // fine column of this lane: p_in streamed from a running cumsum of delp (in DT)
 template <typename DT>
 struct FineCol {
@@ -83,7 +104,6 @@ struct FineCol {
     const DT* dp;     // delp at level 0 of this column
     int64_t plane;    // ny*nx
     const DT* pc;     // coarse phalf[k], k = 0..km (LDS)
-    float* stage;     // LDS staging, this lane's column: stage[k * kStride]
     DT ptop, pbot, run;
     int next;         // next fine interface index (0-based) the running sum will produce
     int km, kn;
@@ -100,42 +120,51 @@ struct FineCol {
         return (float)run;
     }
     __device__ __forceinline__ float pe2(int k) const { return (float)pc[k - 1]; }
-    __device__ __forceinline__ void emit(int k, float v) { stage[(k - 1) * kStride] = v; }
+    __device__ __forceinline__ void emit(int, float) {}
     __device__ __forceinline__ float next_edge(int k) const { return (k + 1 <= kn + 1) ? pe2(k + 1) : 0.0f; }
 };
 
 template <typename DT>
-__global__ __launch_bounds__(64) void regrid_coarsen_kernel(CoarsenArgs<DT> a)
+__global__ __launch_bounds__(512) void regrid_coarsen_kernel(CoarsenArgs<DT> a)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    DT* pc = reinterpret_cast<DT*>(smem);                            // [km+1] coarse phalf
-    DT* lpb = reinterpret_cast<DT*>(smem + kOffPb);                  // [64] fine surface phalf
-    float* lar = reinterpret_cast<float*>(smem + kOffArea);          // [64] fine area
-    float* stage = reinterpret_cast<float*>(smem + kOffStage);       // [km][kStride]
-    DT* pstage = reinterpret_cast<DT*>(smem + kOffStage);            // pass 1: [kChunk][kStride]
-
-    const int lane = threadIdx.x;
-    const int f = a.f;
-    const int nn = f * f;
-    const int nyc = a.ny / f, nxc = a.nx / f;
-    const int64_t cell = blockIdx.x;
-    const int tile = (int)(cell / ((int64_t)nyc * nxc));
-    const int rem = (int)(cell - (int64_t)tile * nyc * nxc);
-    const int Y = rem / nxc, X = rem - (rem / nxc) * nxc;
-    const bool active = lane < nn;
-    const int dy = active ? lane / f : 0, dx = active ? lane - (lane / f) * f : 0;
+    const int f = a.f, km = a.km;
+    const int C = 64 / f;                 // coarse cells per wave
+    const int lane = threadIdx.x & 63;
+    const int dy = threadIdx.x >> 6;      // fine row within the coarse row
+    const int nxc = a.nx / f, nyc = a.ny / f;
+    const int nseg = (nxc + C - 1) / C;
+    int64_t bi = blockIdx.x;
+    const int seg = (int)(bi % nseg);
+    bi /= nseg;
+    const int Y = (int)(bi % nyc);
+    const int tile = (int)(bi / nyc);
+    const int lc = lane / f;              // cell of this lane (>= C: spare lane)
+    const int cell = min(lc, C - 1);
+    const int dx = lane - lc * f;
+    const int X = seg * C + cell;
+    const bool active = lc < C && X < nxc;
+    const int base = cell * f;            // first lane of this cell
     const int64_t plane = (int64_t)a.ny * a.nx;
-    const int64_t fine = (int64_t)(Y * f + dy) * a.nx + (X * f + dx);
+    const int64_t fine = (int64_t)(Y * f + dy) * a.nx + (int64_t)min(X, nxc - 1) * f + (active ? dx : 0);
     const int64_t cplane = (int64_t)nyc * nxc;
-    const int64_t cidx = (int64_t)Y * nxc + X;
-    const int km = a.km;
+    const int64_t crow = (int64_t)Y * nxc + (int64_t)seg * C;  // first coarse cell of this block
+
+    DT* pc = reinterpret_cast<DT*>(smem);            // [C][km+1] coarse phalf
+    DT* lpb = pc + C * (km + 1);                     // [f][64] fine surface phalf
+    float* lar = reinterpret_cast<float*>(lpb + f * 64);  // [f][64] fine area
+    float* asum = lar + f * 64;                      // [C]
+    char* rsb = reinterpret_cast<char*>(asum + 64);  // partials: [km][f][C] f32, or [kChunk][f][C] DT
+    float* rs = reinterpret_cast<float*>(rsb);
+    DT* rsd = reinterpret_cast<DT*>(rsb);
 
     // ---- pass 1: fine phalf (per lane) and area-weighted coarse delp / phalf ----
     const float area = active ? a.area[(int64_t)tile * plane + fine] : 0.0f;
-    lar[lane] = area;
+    lar[dy * 64 + lane] = area;
     __syncthreads();
-    // weights.coarsen().sum(): float32 (area's dtype)
-    const float asum = block_sum<float>(f, [&](int j) { return lar[j]; });
+    if ((int)threadIdx.x < C)  // weights.coarsen().sum(): float32 (area's dtype)
+        asum[threadIdx.x] = block_sum<float>(
+            f, [&](int j) { return nan0(lar[(j / f) * 64 + (int)threadIdx.x * f + j % f]); });
     const DT* dp = a.delp + (int64_t)tile * km * plane + fine;
     const DT ptop = (DT)a.ptop;
     DT run = ptop;  // fine phalf = cumsum([ptop, delp]) (vertically_dependent.py:62-63)
@@ -144,52 +173,68 @@ __global__ __launch_bounds__(64) void regrid_coarsen_kernel(CoarsenArgs<DT> a)
         for (int kk = 0; kk < nk; ++kk) {
             const DT d = active ? dp[(int64_t)(k0 + kk) * plane] : (DT)0;
             run = run + d;
-            pstage[kk * kStride + lane] = d * (DT)area;  // (delp * area) in delp's dtype
+            const DT r = row_sum<DT>(nan0(d * (DT)area), f, base);  // (delp * area) in delp's dtype
+            if (active && dx == 0) rsd[(kk * f + dy) * C + cell] = r;
         }
         __syncthreads();
-        if (lane < nk) {
-            const DT num = block_sum<DT>(f, [&](int j) { return pstage[lane * kStride + j]; });
-            const DT dc = num / (DT)asum;  // weighted_block_average (coarsen.py:213-215)
-            pc[k0 + lane + 1] = dc;
-            if (a.delp_out) a.delp_out[((int64_t)tile * km + k0 + lane) * cplane + cidx] = (float)dc;
+        for (int i = threadIdx.x; i < nk * C; i += blockDim.x) {
+            const int kk = i / C, c = i - (i / C) * C;
+            if (seg * C + c < nxc) {
+                DT acc = rsd[(kk * f) * C + c];
+                for (int r = 1; r < f; ++r) acc = acc + rsd[(kk * f + r) * C + c];
+                const DT dc = acc / (DT)asum[c];  // weighted_block_average (coarsen.py:213-215)
+                pc[c * (km + 1) + k0 + kk + 1] = dc;
+                if (a.delp_out) a.delp_out[((int64_t)tile * km + k0 + kk) * cplane + crow + c] = (float)dc;
+            }
         }
         __syncthreads();
     }
-    if (lane == 0) {  // coarse phalf = cumsum([ptop, delp_c]), sequential like np.cumsum
-        pc[0] = ptop;
-        for (int k = 0; k < km; ++k) pc[k + 1] = pc[k] + pc[k + 1];
+    if ((int)threadIdx.x < C) {  // coarse phalf = cumsum([ptop, delp_c]), sequential like np.cumsum
+        DT* p = pc + threadIdx.x * (km + 1);
+        p[0] = ptop;
+        for (int k = 0; k < km; ++k) p[k + 1] = p[k] + p[k + 1];
     }
     const DT pbot = run;  // phalf_fine[-1] of this fine column
-    lpb[lane] = pbot;
+    lpb[dy * 64 + lane] = pbot;
     __syncthreads();
 
-    // ---- per field: remap every fine column, then masked area-weighted block mean ----
+    // ---- per field: remap every fine column level by level, masked area-weighted mean ----
+    const DT* pcc = pc + cell * (km + 1);
     for (int v = 0; v < a.n_fields; ++v) {
-        FineCol<DT> c;
-        c.q = a.fields[v] + (int64_t)tile * km * plane + fine;
-        c.dp = dp;
-        c.plane = plane;
-        c.pc = pc;
-        c.stage = stage + lane;
-        c.ptop = ptop;
-        c.pbot = pbot;
-        c.run = ptop;
-        c.next = 0;
-        c.km = km;
-        c.kn = km;
-        mappm_ppm_column(c, km, km, a.iv, a.kord);
-        __syncthreads();
-        // lane j reduces levels k = j, j+64, ... over the block's fine columns in a fixed order
-        float* o = a.out[v] + (int64_t)tile * km * cplane + cidx;
-        for (int k = lane; k < km; k += 64) {
+        FineCol<DT> col;
+        col.q = a.fields[v] + (int64_t)tile * km * plane + fine;
+        col.dp = dp;
+        col.plane = plane;
+        col.pc = pcc;
+        col.ptop = ptop;
+        col.pbot = pbot;
+        col.run = ptop;
+        col.next = 0;
+        col.km = km;
+        col.kn = km;
+        PpmCursor<FineCol<DT>> cur(col, km, km, a.iv, a.kord);
+        for (int k = 0; k < km; ++k) {
+            const float q2 = cur.next();
             // _mask_weights (regridz.py:150-161): area where phalf_c_on_f[k+1] < phalf_f[-1]
-            // (compared in delp's dtype); the masked area stays float32, so the product,
-            // both block sums and the quotient are float32 (coarsen.py:213-215)
-            const DT pk = pc[k + 1];
-            const float* sk = stage + k * kStride;
-            const float num = block_sum<float>(f, [&](int j) { return sk[j] * ((pk < lpb[j]) ? lar[j] : 0.0f); });
-            const float den = block_sum<float>(f, [&](int j) { return (pk < lpb[j]) ? lar[j] : 0.0f; });
-            o[(int64_t)k * cplane] = num / den;
+            // (compared in delp's dtype); the masked area stays float32 (coarsen.py:213-215)
+            const float w = (pcc[k + 1] < pbot) ? area : 0.0f;
+            const float r = row_sum<float>(nan0(q2 * w), f, base);
+            if (active && dx == 0) rs[(k * f + dy) * C + cell] = r;
+        }
+        __syncthreads();
+        float* o = a.out[v] + (int64_t)tile * km * cplane + crow;
+        for (int i = threadIdx.x; i < km * C; i += blockDim.x) {
+            const int k = i / C, c = i - (i / C) * C;
+            if (seg * C + c < nxc) {
+                float num = rs[(k * f) * C + c];
+                for (int r = 1; r < f; ++r) num = num + rs[(k * f + r) * C + c];
+                const DT pk = pc[c * (km + 1) + k + 1];
+                const float den = block_sum<float>(f, [&](int j) {
+                    const int l = (j / f) * 64 + c * f + j % f;
+                    return (pk < lpb[l]) ? nan0(lar[l]) : 0.0f;
+                });
+                o[(int64_t)k * cplane + c] = num / den;
+            }
         }
         __syncthreads();
     }
@@ -236,9 +281,16 @@ int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* f
     a.iv = iv;
     a.kord = kord;
     a.ptop = ptop_toa;
-    const int64_t cells = (int64_t)ntile * (ny / factor) * (nx / factor);
-    const size_t lds = kOffStage + std::max(sizeof(float) * (size_t)km * kStride, sizeof(DT) * kChunk * kStride);
-    hipLaunchKernelGGL(regrid_coarsen_kernel<DT>, dim3((unsigned)cells), dim3(64), lds, s, a);
+    // one block per coarse row segment of C = 64 / f cells: f waves
+    const int C = 64 / factor;
+    const int nxc = nx / factor;
+    const int64_t nseg = (nxc + C - 1) / C;
+    const int64_t blocks = (int64_t)ntile * (ny / factor) * nseg;
+    const size_t lds = sizeof(DT) * ((size_t)C * (km + 1) + (size_t)factor * 64) + sizeof(float) * (factor * 64 + 64) +
+                       std::max(sizeof(float) * (size_t)km * 64, sizeof(DT) * kChunk * 64);
+    FV3_REQUIRE(lds <= 160 * 1024, "regrid_coarsen: %zu B of LDS needed", lds);
+    FV3_REQUIRE(blocks < (int64_t)0x7fffffff, "regrid_coarsen: grid too large");
+    hipLaunchKernelGGL(regrid_coarsen_kernel<DT>, dim3((unsigned)blocks), dim3(64 * factor), lds, s, a);
     FV3_LAUNCH_CHECK();
     return FV3_OK;
 }
