@@ -32,6 +32,7 @@ EXPORTED_SYMBOLS = (
     "fv3_column_integral",
     "fv3_area_weighted_sums",
     "fv3_level_sums",
+    "fv3_ml_epilogue",
 )
 ABI_VERSION = 1
 
@@ -68,6 +69,24 @@ class DenseDesc(ctypes.Structure):
     ]
 
 
+class EpilogueIO(ctypes.Structure):
+    _fields_ = [
+        ("dq1", ctypes.c_void_p),
+        ("dq2", ctypes.c_void_p),
+        ("sphum", ctypes.c_void_p),
+        ("delp", ctypes.c_void_p),
+        ("temperature", ctypes.c_void_p),
+        ("physics_precip", ctypes.c_void_p),
+        ("dq1_out", ctypes.c_void_p),
+        ("dq2_out", ctypes.c_void_p),
+        ("limiter_active", ctypes.c_void_p),
+        ("temperature_out", ctypes.c_void_p),
+        ("sphum_out", ctypes.c_void_p),
+        ("column", ctypes.c_void_p),
+        ("column_ld", ctypes.c_int64),
+    ]
+
+
 _lib = None
 _lock = threading.Lock()
 
@@ -96,6 +115,7 @@ _SIGNATURES = {
     "fv3_column_integral": (_I, [_P, Layout, _P, Layout, _P, _I64, _I, _D, _P]),
     "fv3_area_weighted_sums": (_I, [ctypes.POINTER(_P), _I, _P, _I64, _P, _P]),
     "fv3_level_sums": (_I, [_P, Layout, _I64, _I, _P, _P]),
+    "fv3_ml_epilogue": (_I, [ctypes.POINTER(EpilogueIO), Layout, _I64, _I, _I, _D, _I, _I, _P]),
 }
 
 

@@ -1,0 +1,167 @@
+// fv3net_amd — the ML stepper's epilogue, one pass per column on gfx950.
+//
+// Everything the prognostic loop does with a (dQ1, dQ2) prediction, fused:
+//   humidity limiter, MSE-conserving or legacy
+//       workflows/prognostic_c48_run/runtime/steppers/machine_learning.py:67-99, 258-299
+//       (vcm moist_static_energy_tendency / temperature_tendency,
+//        external/vcm/vcm/calc/thermo/local.py:317-360)
+//   limiter diagnostics (column heating / moistening change, limiter_active)
+//       machine_learning.py:267-303
+//   compute_diagnostics: net moistening, column heating   diagnostics/compute.py:77-106
+//       (vcm mass_integrate, vertically_dependent.py:18-22, 255-301)
+//   fillna_tendency + filled fraction                       loop.py:103-110
+//   add_tendency: T += dQ1 dt, q += dQ2 dt                   loop.py:202-219
+//   precipitation_sum                                        diagnostics/compute.py:21-39
+// One thread per column walking the levels in order (coalesced [level][column] rows).
+// The arithmetic replays the reference's dtype flow: f32 model tendencies combined
+// with Python-float constants stay f32, anything mixed with the state is in the
+// state's dtype DT, column sums run over z in order from +0.0 skipping NaN (xarray's
+// sum).  Bit-identical to oracle/stepper.py.
+// Roofline: HBM-bound: (2*4 + 3*sizeof(DT)) B read + (2 + 2)*sizeof(DT) + 1 B written per
+// level (inputs dQ1, dQ2, sphum, delp, T; outputs dQ1, dQ2, T, q, limiter flag).
+#include "common.h"
+
+namespace fv3 {
+namespace {
+
+constexpr double kGravity = 9.80665;  // vcm/calc/thermo/constants.py
+constexpr double kRdgas = 287.05;
+constexpr double kCp = 1004.0;
+constexpr double kLv = 2.5e6;         // latent_heat_vaporization(273.15 K)
+
+template <typename DT>
+struct EpilogueArgs {
+    const float* dq1;
+    const float* dq2;
+    const DT* sphum;
+    const DT* delp;
+    const DT* temp;
+    const DT* precip;      // [col] physics precipitation, or NULL
+    DT* dq1_out;           // [z][col] limited tendencies (pre-fill), or NULL
+    DT* dq2_out;
+    uint8_t* active;       // [z][col] limiter flag, or NULL
+    DT* temp_out;          // [z][col] T + fill(dQ1) dt, or NULL (may alias temp)
+    DT* sphum_out;         // [z][col] q + fill(dQ2) dt, or NULL (may alias sphum)
+    DT* col;               // [8][col] column diagnostics (see fv3net_amd.h), or NULL
+    fv3_layout lay;        // every [z][col] array
+    int64_t ncol, col_ld;  // column diagnostics: row stride
+    int nz, mse, hydrostatic;
+    double dt;
+};
+
+template <typename DT>
+__device__ __forceinline__ DT nan0(DT x) { return x != x ? DT(0) : x; }
+
+template <typename DT>
+__global__ __launch_bounds__(256) void ml_epilogue_kernel(EpilogueArgs<DT> a)
+{
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.ncol) return;
+    const int64_t off = col_offset(a.lay, c);
+    const float dtf = (float)a.dt;        // f32 array * Python float -> f32
+    const DT dtd = (DT)a.dt;
+    const float cvf = (float)(kCp - kRdgas), lvf = (float)kLv;
+    const DT cv = (DT)(kCp - kRdgas), lv = (DT)kLv, g = (DT)kGravity;
+    DT s_h = 0, s_m = 0, s_nm = 0, s_ch = 0;
+    int n1 = 0, n2 = 0;
+    for (int k = 0; k < a.nz; ++k) {
+        const int64_t i = off + (int64_t)k * a.lay.ld;
+        const float q1 = a.dq1[i], q2 = a.dq2[i];
+        const DT sp = a.sphum[i], dp = a.delp[i];
+        DT q1n, q2n;
+        if (a.mse) {
+            // update_moisture_tendency_to_ensure_non_negative_humidity (machine_learning.py:77-80)
+            const float d = q2 * dtf;
+            q2n = (sp + (DT)d >= (DT)0) ? (DT)q2 : (-sp) / dtd;
+            // update_temperature_tendency_to_conserve_mse (:83-88)
+            const float m = cvf * q1 + lvf * q2;
+            q1n = ((DT)m - lv * q2n) / cv;
+        } else {
+            // non_negative_sphum (:67-74)
+            const float delta = q2 * dtf;
+            const DT ratio = (-sp) / (DT)(dtf * q2);
+            const bool keep = sp + (DT)delta >= (DT)0;
+            q1n = keep ? (DT)q1 : ratio * (DT)q1;
+            q2n = keep ? (DT)q2 : ratio * (DT)q2;
+        }
+        // mass_integrate terms: (x * delp) / g, NaN-skipping sum from +0.0
+        s_h = s_h + nan0((q1n - (DT)q1) * dp / g);
+        s_m = s_m + nan0((q2n - (DT)q2) * dp / g);
+        s_nm = s_nm + nan0(q2n * dp / g);
+        s_ch = s_ch + nan0(q1n * dp / g);
+        if (a.dq1_out) {
+            a.dq1_out[i] = q1n;
+            a.dq2_out[i] = q2n;
+        }
+        if (a.active) a.active[i] = ((DT)q2 != q2n) ? 1 : 0;
+        // fillna_tendency + add_tendency
+        const bool nan1 = q1n != q1n, nan2 = q2n != q2n;
+        n1 += nan1;
+        n2 += nan2;
+        if (a.temp_out) a.temp_out[i] = a.temp[i] + (nan1 ? (DT)0 : q1n) * dtd;
+        if (a.sphum_out) a.sphum_out[i] = sp + (nan2 ? (DT)0 : q2n) * dtd;
+    }
+    if (a.col) {
+        const DT ch = a.hydrostatic ? (DT)kCp : cv;
+        DT* o = a.col + c;
+        o[0 * a.col_ld] = ch * s_h;  // column_integrated_dQ1_change_non_neg_sphum_constraint
+        o[1 * a.col_ld] = s_m;       // column_integrated_dQ2_change_non_neg_sphum_constraint
+        o[2 * a.col_ld] = s_nm;      // net_moistening_due_to_<label>
+        o[3 * a.col_ld] = ch * s_ch; // column_heating_due_to_<label>
+        o[4 * a.col_ld] = (DT)((double)n1 / a.nz);  // dQ1_filled_frac
+        o[5 * a.col_ld] = (DT)((double)n2 / a.nz);  // dQ2_filled_frac
+        if (a.precip) {
+            const DT total = a.precip[c] + ((-s_nm) * dtd) * (DT)(1.0 / 1000);
+            o[6 * a.col_ld] = total >= (DT)0 ? total : (DT)0;  // total_precipitation
+        }
+    }
+}
+
+template <typename DT>
+int epilogue_impl(const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, int nz, double dt, int mse_conserving,
+                  int hydrostatic, void* stream)
+{
+    clear_error();
+    FV3_REQUIRE(io, "ml_epilogue: NULL io");
+    FV3_REQUIRE(ncol >= 0 && nz >= 1, "ml_epilogue: bad sizes ncol=%lld nz=%d", (long long)ncol, nz);
+    if (ncol == 0) return FV3_OK;
+    FV3_REQUIRE(io->dq1 && io->dq2 && io->sphum && io->delp && io->temperature,
+                "ml_epilogue: dQ1, dQ2, specific humidity, delp and air temperature are required");
+    FV3_REQUIRE(layout_ok(lay, ncol), "ml_epilogue: bad layout");
+    FV3_REQUIRE(!io->dq1_out == !io->dq2_out, "ml_epilogue: dq1_out and dq2_out go together");
+    EpilogueArgs<DT> a;
+    a.dq1 = io->dq1;
+    a.dq2 = io->dq2;
+    a.sphum = (const DT*)io->sphum;
+    a.delp = (const DT*)io->delp;
+    a.temp = (const DT*)io->temperature;
+    a.precip = (const DT*)io->physics_precip;
+    a.dq1_out = (DT*)io->dq1_out;
+    a.dq2_out = (DT*)io->dq2_out;
+    a.active = io->limiter_active;
+    a.temp_out = (DT*)io->temperature_out;
+    a.sphum_out = (DT*)io->sphum_out;
+    a.col = (DT*)io->column;
+    a.lay = lay;
+    a.ncol = ncol;
+    a.col_ld = io->column_ld > 0 ? io->column_ld : ncol;
+    a.nz = nz;
+    a.mse = mse_conserving != 0;
+    a.hydrostatic = hydrostatic != 0;
+    a.dt = dt;
+    const int block = 256;
+    const int64_t grid = (ncol + block - 1) / block;
+    hipLaunchKernelGGL(ml_epilogue_kernel<DT>, dim3((unsigned)grid), dim3(block), 0, (hipStream_t)stream, a);
+    FV3_LAUNCH_CHECK();
+    return FV3_OK;
+}
+
+}  // namespace
+}  // namespace fv3
+
+extern "C" int fv3_ml_epilogue(const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, int nz, int state_f64,
+                               double dt, int mse_conserving, int hydrostatic, void* stream)
+{
+    return state_f64 ? fv3::epilogue_impl<double>(io, lay, ncol, nz, dt, mse_conserving, hydrostatic, stream)
+                     : fv3::epilogue_impl<float>(io, lay, ncol, nz, dt, mse_conserving, hydrostatic, stream);
+}

@@ -17,8 +17,12 @@
  *   fv3_regrid_coarsen    external/vcm/vcm/cubedsphere/regridz.py:25-55 + 115-161 fused with
  *                         external/vcm/vcm/cubedsphere/coarsen.py:183-218
  *                         (as orchestrated by coarsen_restarts.py:411-516, 840-887)
- *   fv3_column_reduce     per-rank partial sums behind
- *                         workflows/prognostic_c48_run/runtime/metrics.py:18-32
+ *   fv3_column_integral,  per-rank partial sums behind
+ *   fv3_area_weighted_sums, workflows/prognostic_c48_run/runtime/metrics.py:18-55
+ *   fv3_level_sums
+ *   fv3_ml_epilogue       the PureMLStepper limiter + diagnostics and the loop's
+ *                         fillna/add_tendency/precipitation_sum
+ *                         (runtime/steppers/machine_learning.py:239-315, runtime/loop.py:103-219)
  */
 #ifndef FV3NET_AMD_H
 #define FV3NET_AMD_H
@@ -155,6 +159,40 @@ int fv3_area_weighted_sums(const float* const* diags, int n_diag, const float* a
 /* Per-level horizontal sums out[k] = sum_c x[k][c] in float64 (fixed reduction tree):
  * the per-rank part of metrics.py:27-32 global_horizontal_sum. */
 int fv3_level_sums(const float* x, fv3_layout x_l, int64_t ncol, int nz, double* out, void* stream);
+
+/* ---- ML stepper epilogue: limiter + diagnostics + apply (config #4) --------------
+ * One pass per column over everything the prognostic loop does with a (dQ1, dQ2)
+ * prediction: the non-negative-humidity limiter (MSE-conserving, machine_learning.py:
+ * 77-99, or legacy :67-74), its column diagnostics (:267-303), compute_diagnostics'
+ * net moistening / column heating (diagnostics/compute.py:77-106), fillna + filled
+ * fraction (loop.py:103-110), add_tendency (loop.py:202-219) and precipitation_sum
+ * (diagnostics/compute.py:21-39).  dq1/dq2 are the model's float32 [z][col] outputs;
+ * the state arrays and every output are float64 (state_f64 = 1, as the FV3 state is)
+ * or float32; all [z][col] arrays share `lay`.  Bit-identical to the reference's
+ * dtype flow (oracle/stepper.py).  Outputs may be NULL; temperature_out / sphum_out
+ * may alias the inputs (in-place update). */
+typedef struct {
+    const float* dq1;            /* [z][col] model heating tendency, K/s */
+    const float* dq2;            /* [z][col] model moistening tendency, kg/kg/s */
+    const void* sphum;           /* [z][col] specific humidity */
+    const void* delp;            /* [z][col] pressure thickness, Pa */
+    const void* temperature;     /* [z][col] air temperature, K */
+    const void* physics_precip;  /* [col] physics precipitation (m), or NULL */
+    void* dq1_out;               /* [z][col] limited dQ1 (before fillna), or NULL */
+    void* dq2_out;               /* [z][col] limited dQ2, or NULL (with dq1_out) */
+    unsigned char* limiter_active; /* [z][col] 1 where the limiter changed dQ2, or NULL */
+    void* temperature_out;       /* [z][col] T + fillna(dQ1) dt, or NULL */
+    void* sphum_out;             /* [z][col] q + fillna(dQ2) dt, or NULL */
+    void* column;                /* [7][column_ld] column diagnostics, or NULL:
+                                  * 0 dQ1 limiter heating change (W/m2), 1 dQ2 limiter moistening
+                                  * change (kg/m2/s), 2 net moistening, 3 column heating,
+                                  * 4 dQ1 filled fraction, 5 dQ2 filled fraction,
+                                  * 6 total precipitation (m; only with physics_precip) */
+    int64_t column_ld;           /* row stride of `column` (0 = ncol) */
+} fv3_epilogue_io;
+
+int fv3_ml_epilogue(const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, int nz, int state_f64,
+                    double dt, int mse_conserving, int hydrostatic, void* stream);
 
 #ifdef __cplusplus
 }
