@@ -154,6 +154,13 @@ def extra_measurements(dev):
         out[name] = {"columns_per_s": ncol / t, "ms_per_step": t * 1e3, "hbm_gbs": gbs,
                      "frac_hbm_peak": gbs / W.HBM_PEAK_GBS}
         del wl
+    # config #4: one ML-stepper step (predict + fused limiter/diagnostics/apply + global
+    # means) on a float64 C96 state, one GPU
+    wl = W.make_stepper_workload(96, seed=11, device=dev)
+    wall, t = timed_steps(wl.step, 20, 3)
+    out["stepper_c96"] = {"columns_per_s": wl.ncol / (wall / 20), "ms_per_step": wall / 20 * 1e3,
+                          "note": "wall clock per step (several kernels + host glue)"}
+    del wl
     # config #3: fused C384 -> C48 pressure-level coarsen (1 and 4 fields), fine columns/s
     for nf in (1, 4):
         wl = W.make_coarsen_workload(384, 8, nf, seed=7, device=dev)

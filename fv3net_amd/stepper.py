@@ -35,10 +35,11 @@ COLUMN_DIAGNOSTICS = (
 
 def ml_epilogue(dq1, dq2, sphum, delp, temperature, dt: float, physics_precip=None,
                 mse_conserving: bool = True, hydrostatic: bool = False, label: str = "machine_learning",
-                in_place: bool = False, stream=None) -> Dict[str, object]:
+                in_place: bool = False, level_axis: int = 0, stream=None) -> Dict[str, object]:
     """Limiter + diagnostics + apply for one (dQ1, dQ2) prediction, one kernel.
 
-    Returns device tensors: limited ``dQ1``/``dQ2`` (pre-fillna, as the stepper
+    ``level_axis`` is the vertical axis of every 3-D array (axes before it are
+    blocks such as tiles).  Returns device tensors: limited ``dQ1``/``dQ2`` (pre-fillna, as the stepper
     returns them), ``specific_humidity_limiter_active`` (uint8), the updated
     ``air_temperature``/``specific_humidity`` (written into the inputs when
     ``in_place``), the column diagnostics of COLUMN_DIAGNOSTICS and, with
@@ -60,8 +61,8 @@ def ml_epilogue(dq1, dq2, sphum, delp, temperature, dt: float, physics_precip=No
     for name, t in (("dQ1", dq1), ("dQ2", dq2), (DELP, delp), (TEMP, temperature)):
         if tuple(t.shape) != tuple(sphum.shape):
             raise ValueError(f"{name} shape {tuple(t.shape)} != specific humidity shape {tuple(sphum.shape)}")
-    lay, ncol, nz = _device.level_layout(sphum, 0)
-    col_shape = tuple(sphum.shape[1:])
+    lay, ncol, nz = _device.level_layout(sphum, level_axis)  # e.g. (z, y, x) or (tile, z, y, x)
+    col_shape = tuple(s for i, s in enumerate(sphum.shape) if i != level_axis)
     out = {
         "dQ1": torch.empty_like(sphum),
         "dQ2": torch.empty_like(sphum),

@@ -151,3 +151,50 @@ def make_coarsen_workload(res: int = 384, factor: int = 8, nfields: int = 1, see
     area = 0.5 + 0.5 * torch.rand((6, res, res), generator=g, device=device)
     fields = {f"f{i}": torch.randn(shape, generator=g, device=device) * 10.0 + 250.0 for i in range(nfields)}
     return CoarsenWorkload(delp, area, fields, factor, 6 * res * res, NZ)
+
+
+@dataclasses.dataclass
+class StepperWorkload:
+    """BASELINE config #4 per GPU: one ML-stepper step on a float64 (tile, z, y, x)
+    state: float32 model inputs, the fused dense predict of dQ1/dQ2, the fused
+    limiter/diagnostics/apply epilogue (in place) and the global means of the 2-D
+    diagnostics (area-weighted partials + one all-gather when distributed)."""
+    model: DenseColumnModel
+    state: dict
+    area: object
+    dt: float
+    ncol: int
+    group: object = None
+
+    def step(self):
+        from .distributed import area_weighted_partials, combine_partials
+        from .stepper import ml_epilogue
+
+        T, q = self.state["air_temperature"], self.state["specific_humidity"]
+        t32, q32 = T.to(torch.float32), q.to(torch.float32)
+        dq1, dq2 = self.model.forward([t32, q32], level_axes=[1, 1])
+        res = ml_epilogue(dq1, dq2, q, self.state["pressure_thickness_of_atmospheric_layer"], T, self.dt,
+                          self.state["total_precipitation"], in_place=True, level_axis=1)
+        self.state["total_precipitation"] = res["total_precipitation"]
+        diags = [res["net_moistening_due_to_machine_learning"], res["column_heating_due_to_machine_learning"],
+                 res["total_precipitation"]]
+        part = area_weighted_partials([d.to(torch.float32) for d in diags], self.area)
+        return combine_partials(part, self.group)
+
+
+def make_stepper_workload(res: int = 96, seed: int = 0, device=None, group=None):
+    device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    shape = (6, NZ, res, res)
+    base = torch.linspace(200.0, 1800.0, NZ, device=device, dtype=torch.float64)[None, :, None, None]
+    state = {
+        "air_temperature": 260.0 + 15.0 * torch.randn(shape, generator=g, device=device, dtype=torch.float64),
+        "specific_humidity": 0.02 * torch.rand(shape, generator=g, device=device, dtype=torch.float64),
+        "pressure_thickness_of_atmospheric_layer":
+            base * (0.99 + 0.02 * torch.rand(shape, generator=g, device=device, dtype=torch.float64)),
+        "total_precipitation": 1e-3 * torch.rand((6, res, res), generator=g, device=device, dtype=torch.float64),
+    }
+    area = 0.5 + 0.5 * torch.rand((6, res, res), generator=g, device=device)
+    wl = make_dense_workload(min(res, 48), seed=seed, device=device)
+    return StepperWorkload(wl.model, state, area, 900.0, 6 * res * res, group)

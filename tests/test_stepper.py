@@ -85,3 +85,64 @@ def test_epilogue_in_place_on_tile_state(gpu):
                     torch.from_numpy(as4(delp)[t]).cuda(), Tt[t], 450.0, in_place=True)
     _bits(qt.cpu().numpy(), as4(ref["specific_humidity"]))
     _bits(Tt.cpu().numpy(), as4(ref["air_temperature"]))
+
+
+@pytest.mark.gpu
+def test_stepper_workload_step(gpu):
+    """Config #4 step (predict -> epilogue in place -> global means) on a C12 state."""
+    import torch
+
+    from fv3net_amd import workloads as W
+
+    wl = W.make_stepper_workload(12, seed=2)
+    q0 = wl.state["specific_humidity"].clone()
+    sums = wl.step()
+    torch.cuda.synchronize()
+    q1 = wl.state["specific_humidity"]
+    assert not torch.equal(q0, q1)
+    assert (q1 >= -1e-15).all()  # the limiter keeps humidity non-negative
+    assert sums.shape == (3, 2) and torch.isfinite(sums).all()
+
+
+@pytest.mark.gpu
+def test_pure_ml_stepper_mirror(gpu):
+    """PureMLStepper (machine_learning.py:239-315) over a DenseColumnPredictor: the
+    tendencies/diagnostics equal the oracle epilogue applied to the model's own
+    prediction."""
+    import torch
+
+    from fv3net_amd import dataset as D
+    from fv3net_amd.dense import DenseColumnModel, DenseModelConfig
+    from fv3net_amd.predictor import DenseColumnPredictor
+    from fv3net_amd.stepper import PureMLStepper
+
+    rng = np.random.default_rng(9)
+    nz, ny, nx = 79, 12, 12
+    dq1, dq2, q, delp, T, precip = _state(rng, nz, ny * nx)
+    to3 = lambda a: a.reshape(nz, ny, nx)
+    state = {"air_temperature": D.DataArray(torch.from_numpy(to3(T)).cuda(), ("z", "y", "x")),
+             "specific_humidity": D.DataArray(torch.from_numpy(to3(q)).cuda(), ("z", "y", "x")),
+             "pressure_thickness_of_atmospheric_layer": D.DataArray(torch.from_numpy(to3(delp)).cuda(),
+                                                                    ("z", "y", "x")),
+             "total_precipitation": D.DataArray(torch.from_numpy(precip.reshape(ny, nx)).cuda(), ("y", "x"))}
+    cfg = DenseModelConfig(["air_temperature", "specific_humidity"], ["dQ1", "dQ2"], [nz, nz], [nz, nz],
+                           width=64, depth=3)
+    model = DenseColumnModel.random(cfg, seed=4, sample_inputs=[T.T.astype(np.float32), q.T.astype(np.float32)])
+    pred = DenseColumnPredictor(cfg.input_variables, cfg.output_variables, model)
+    stepper = PureMLStepper(pred, 900.0)
+    tend, diags, updates = stepper(None, state)
+    # the model's prediction on the same float32 inputs
+    X = D.Dataset({"air_temperature": D.DataArray(torch.from_numpy(to3(T).astype(np.float32)).cuda(), ("z", "y", "x")),
+                   "specific_humidity": D.DataArray(torch.from_numpy(to3(q).astype(np.float32)).cuda(),
+                                                    ("z", "y", "x"))})
+    p = pred.predict(X)
+    d1 = p["dQ1"].data.cpu().numpy().reshape(nz, -1)
+    d2 = p["dQ2"].data.cpu().numpy().reshape(nz, -1)
+    ref = OS.epilogue(d1, d2, q, delp, T, precip, 900.0)
+    _bits(tend["dQ1"].cpu().numpy().reshape(nz, -1), ref["dQ1"])
+    _bits(tend["dQ2"].cpu().numpy().reshape(nz, -1), ref["dQ2"])
+    net, _ = stepper.get_diagnostics(state, tend)
+    _bits(net["net_moistening_due_to_machine_learning"].cpu().numpy().reshape(-1), ref["net_moistening"])
+    updated, fracs = stepper.apply()
+    _bits(updated["specific_humidity"].cpu().numpy().reshape(nz, -1), ref["specific_humidity"])
+    _bits(updated["total_precipitation"].cpu().numpy().reshape(-1), ref["total_precipitation"])
