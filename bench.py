@@ -161,6 +161,14 @@ def extra_measurements(dev):
     out["stepper_c96"] = {"columns_per_s": wl.ncol / (wall / 20), "ms_per_step": wall / 20 * 1e3,
                           "note": "wall clock per step (several kernels + host glue)"}
     del wl
+    # config #5: Zhao-Carr microphysics emulator on a C384 state (float32 MFMA path)
+    wl = W.make_emulator_workload(384, seed=13, device=dev)
+    wall, t = timed_steps(wl.step, 10, 3)
+    out["emulator_c384"] = {"columns_per_s": wl.ncol / t, "ms_per_step": t * 1e3,
+                            "tflops": wl.ncol * wl.flops_per_column / t / 1e12,
+                            "frac_f32_mfma_peak": wl.ncol * wl.flops_per_column / t / 1e12 / W.FP32_MFMA_PEAK_TFLOPS,
+                            "hbm_gbs": wl.ncol * wl.bytes_per_column / t / 1e9}
+    del wl
     # config #3: fused C384 -> C48 pressure-level coarsen (1 and 4 fields), fine columns/s
     for nf in (1, 4):
         wl = W.make_coarsen_workload(384, 8, nf, seed=7, device=dev)

@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = (
     "fv3_level_sums",
     "fv3_ml_epilogue",
 )
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class NativeLibraryError(RuntimeError):
@@ -66,6 +66,8 @@ class DenseDesc(ctypes.Structure):
         ("out_min", ctypes.POINTER(ctypes.c_float)),
         ("out_max", ctypes.POINTER(ctypes.c_float)),
         ("out_mask", ctypes.POINTER(ctypes.c_float)),
+        ("in_log_eps", ctypes.POINTER(ctypes.c_float)),
+        ("out_residual", ctypes.POINTER(ctypes.c_int)),
     ]
 
 

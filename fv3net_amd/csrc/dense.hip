@@ -93,10 +93,17 @@ struct DenseArgs {
     int slot_bs[kMaxSlots];
     int slot_ld[kMaxSlots];
     int slot_meta[kMaxSlots];
+    unsigned char slot_var[kMaxSlots];  // input variable of each slot
+    float in_log_eps[kMaxVars];         // > 0: the variable enters as log(max(x, eps)) (emulator LogTransform)
     float* out_ptr[kMaxVars];
     int64_t out_ld[kMaxVars];
     int64_t out_bs[kMaxVars];
     DenseOutTile otile[kMaxOutTiles];
+    // residual outputs (emulator Difference.backward: after = before + to): the raw
+    // input added to output variable o after de-normalisation, or NULL
+    const float* res_ptr[kMaxVars];
+    int res_ld[kMaxVars];
+    int res_bs[kMaxVars];
     int64_t ncol, ncol_blk, ntiles;
     int n_in, n_hidden_extra, n_otiles, kp;
     int in_steps_total, nslots;
@@ -104,6 +111,7 @@ struct DenseArgs {
     int pad_;
     long long* trace;       // profiling hook (fv3_dense_set_trace): [tiles][8] timestamps, or NULL
 };
+static_assert(sizeof(DenseArgs) <= 4096, "kernel arguments are limited to 4 KiB");
 
 // phase timestamps of tile t (thread 0): 0 start, 5 prologue done (constants in LDS),
 // 1 inputs staged, 2 layer 1 done, 3 hidden layers done, 4 end; slot 7 = hardware CU id
@@ -154,6 +162,9 @@ __device__ __forceinline__ float frag_at(const typename Frag<T4>::type& a, int j
 }
 
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.0f, 0.0f, 0.0f, 0.0f}; }
+
+// log(max(x, eps)) with tf.maximum's NaN propagation and a correctly rounded-class log
+__device__ __forceinline__ float __logf_exact(float x, float eps) { return x != x ? x : logf(x > eps ? x : eps); }
 
 // relu(acc + bias) for this wave's T4 tiles (x NC column tiles), stored in accumulator layout
 template <int T4, int NC>
@@ -351,9 +362,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     float* xc = reinterpret_cast<float*>(hbuf) + (cb >> 4) * (p.kp * 16);
     const int cl16 = cb & 15;
     auto xidx = [&](int f) { return ((f >> 4) * 64 + (f & 3) * 16 + cl16) * 4 + ((f >> 2) & 3); };
-    auto put = [&](int meta, float x, bool valid, int fq) {
+    auto put = [&](int meta, float x, bool valid, int fq, float leps) {
         if (fq < (meta & 0xff)) {
             const int f = (meta >> 16) + fq;
+            if (leps > 0.0f) x = __logf_exact(x, leps);  // LogTransform.forward (transforms.py:123-124)
             xc[xidx(f)] = (valid && fq < ((meta >> 8) & 0xff)) ? (x - s_mean[f]) / s_denom[f] : 0.0f;
         }
     };
@@ -362,7 +374,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         const bool valid = col_of(tile, blk, ii);
         static_for<kRawSlots>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
-            if (q < pk.nslots) put(pk.slot_meta[q], raw[q], valid, fq);
+            if (q < pk.nslots) put(pk.slot_meta[q], raw[q], valid, fq, pk.in_log_eps[pk.slot_var[q]]);
             if constexpr (q % 2 == 1) __builtin_amdgcn_sched_barrier(0);  // don't interleave 20 divisions
         });
         for (int q = kRawSlots; q < pk.nslots; ++q) {  // inputs wider than the register prefetch
@@ -370,7 +382,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
             const float x = (valid && fq < ((meta >> 8) & 0xff))
                                 ? pk.slot_base[q][blk * pk.slot_bs[q] + ii + (int64_t)fq * pk.slot_ld[q]]
                                 : 0.0f;
-            put(meta, x, valid, fq);
+            put(meta, x, valid, fq, pk.in_log_eps[pk.slot_var[q]]);
         }
         for (int f = 4 * p.in_steps_total + fq; f < p.kp; f += FPS) xc[xidx(f)] = 0.0f;
     };
@@ -524,6 +536,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
                 if (ovar < 0) continue;
                 float* dst = p.out_ptr[ovar] + oblk * p.out_bs[ovar] + oii;
                 const int64_t ld = p.out_ld[ovar];
+                const float* rsrc = p.res_ptr[ovar] ? p.res_ptr[ovar] + oblk * p.res_bs[ovar] + oii : nullptr;
+                const int64_t rld = p.res_ld[ovar];
                 int fo = 16 * m + 4 * kr;
                 asm volatile("" : "+v"(fo));  // keep this unit's constant reads here, not hoisted above the GEMM
                 const f32x4 bo = *reinterpret_cast<const f32x4*>(s_ep + fo);
@@ -541,6 +555,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
                     if (y < lo[r]) y = lo[r];
                     if (y >= hi[r]) y = hi[r];
                     y = y * mk[r];
+                    if (rsrc) y = rsrc[(int64_t)(oz0 + row) * rld] + y;  // after = before + to
                     if (cvalid && row < onrow) dst[(int64_t)(oz0 + row) * ld] = y;
                 }
                 __builtin_amdgcn_sched_barrier(0);
@@ -560,7 +575,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 struct fv3_dense_model {
     int n_in = 0, n_out = 0, k_in = 0, k_out = 0, width = 0, ht = 0, hp = 0, n_hidden = 0;
     int kp = 0, n_otiles = 0, steps_total = 0;
-    std::vector<int> in_nz, out_nz, in_z0, in_nkeep, in_step0, in_nsteps;
+    std::vector<int> in_nz, out_nz, in_z0, in_nkeep, in_step0, in_nsteps, out_residual;
+    std::vector<float> in_log_eps;
     std::vector<fv3::DenseOutTile> otiles;
     void* dbuf = nullptr;
     fv3::DenseArgs tmpl{};  // device pointers filled, per-call fields empty
@@ -611,6 +627,7 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
         const int nkeep = z1 - z0;
         const int nsteps = (nkeep + 3) / 4;
         m->in_nz.push_back(nz);
+        m->in_log_eps.push_back(d->in_log_eps ? d->in_log_eps[v] : 0.0f);
         m->in_z0.push_back(z0);
         m->in_nkeep.push_back(nkeep);
         m->in_step0.push_back(step);
@@ -634,6 +651,11 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
         const int nz = d->out_nz[v];
         FV3_REQUIRE(nz >= 1, "dense_create: output %d has no levels", v);
         m->out_nz.push_back(nz);
+        const int res = d->out_residual ? d->out_residual[v] : -1;
+        FV3_REQUIRE(res < d->n_in, "dense_create: output %d residual input %d out of range", v, res);
+        if (res >= 0)
+            FV3_REQUIRE(d->in_nz[res] >= nz, "dense_create: residual input %d has fewer levels than output %d", res, v);
+        m->out_residual.push_back(res < 0 ? -1 : res);
         for (int z0 = 0; z0 < nz; z0 += 16) {
             DenseOutTile t{v, z0, std::min(16, nz - z0), 0};
             m->otiles.push_back(t);
@@ -774,6 +796,7 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
     a.wo_off = (int)pcs[6].off;
     a.wbytes = (int)total;
     for (int t = 0; t < m->n_otiles; ++t) a.otile[t] = m->otiles[t];
+    for (int v = 0; v < m->n_in; ++v) a.in_log_eps[v] = m->in_log_eps[v];
     a.n_in = m->n_in;
     a.n_hidden_extra = nhx;
     a.n_otiles = m->n_otiles;
@@ -828,6 +851,10 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
         a.out_ptr[v] = outputs[v];
         a.out_ld[v] = out_l[v].ld;
         a.out_bs[v] = out_l[v].blk_stride;
+        const int r = m->out_residual[v];
+        a.res_ptr[v] = r >= 0 ? inputs[r] : nullptr;
+        a.res_ld[v] = r >= 0 ? (int)in_l[r].ld : 0;
+        a.res_bs[v] = r >= 0 ? (int)in_l[r].blk_stride : 0;
     }
     a.ncol = ncol;
     a.ncol_blk = nb;
@@ -852,6 +879,7 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
             const int nk = std::max(0, std::min(nk_v - f0, 255));
             const int nf = std::min(nf_v - f0, 255);
             a.slot_meta[q] = ((4 * m->in_step0[v] + f0) << 16) | (nk << 8) | nf;
+            a.slot_var[q] = (unsigned char)v;
         }
     }
     hipStream_t s = (hipStream_t)stream;

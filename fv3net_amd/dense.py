@@ -40,6 +40,12 @@ class DenseModelConfig:
     output_limits: Dict[str, Tuple[Optional[float], Optional[float]]] = dataclasses.field(
         default_factory=dict
     )  # OutputLimitConfig
+    # microphysics-emulator graph (fv3fit/emulation/transforms/transforms.py):
+    # input name -> eps of a LogTransform log(max(x, eps)) applied before normalisation
+    input_log_eps: Dict[str, float] = dataclasses.field(default_factory=dict)
+    # output name -> input name whose raw values are added after de-normalisation
+    # (Difference.backward: after = before + to)
+    output_residuals: Dict[str, str] = dataclasses.field(default_factory=dict)
 
     @property
     def n_hidden(self) -> int:
@@ -216,6 +222,9 @@ class DenseColumnModel:
             if m is not None:
                 out_mask[off:off + nz] = m
             off += nz
+        log_eps = [float(c.input_log_eps.get(n, 0.0)) for n in c.input_variables]
+        residual = [c.input_variables.index(c.output_residuals[n]) if n in c.output_residuals else -1
+                    for n in c.output_variables]
         desc = _native.DenseDesc(
             n_in=len(c.input_variables), in_nz=iarr(c.in_nz), in_clip=iarr(np.array(c.in_clip()).ravel()),
             in_mean=farr(np.concatenate([np.ravel(m) for m in p["in_mean"]])),
@@ -227,6 +236,7 @@ class DenseColumnModel:
             out_mean=farr(np.concatenate([np.ravel(m) for m in p["out_mean"]])),
             out_sigma=farr(np.concatenate([np.ravel(s) for s in p["out_sigma"]])),
             out_min=farr(out_min), out_max=farr(out_max), out_mask=farr(out_mask),
+            in_log_eps=farr(log_eps), out_residual=iarr(residual),
         )
         h = ctypes.c_void_p()
         lib = _native.load()

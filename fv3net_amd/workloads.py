@@ -198,3 +198,49 @@ def make_stepper_workload(res: int = 96, seed: int = 0, device=None, group=None)
     area = 0.5 + 0.5 * torch.rand((6, res, res), generator=g, device=device)
     wl = make_dense_workload(min(res, 48), seed=seed, device=device)
     return StepperWorkload(wl.model, state, area, 900.0, 6 * res * res, group)
+
+
+@dataclasses.dataclass
+class EmulatorWorkload:
+    """BASELINE config #5 per GPU: the Zhao-Carr microphysics emulator on every column
+    of a C384 79-level state (inputs in the Fortran [feature, sample] layout)."""
+    emulator: object
+    state: dict
+    out: dict
+    ncol: int
+    flops_per_column: int
+    bytes_per_column: int
+
+    def step(self):
+        return self.emulator(self.state, out=self.out)
+
+
+def make_emulator_workload(res: int = 384, seed: int = 0, device=None):
+    from .emulator import MicrophysicsEmulator, zhao_carr_outputs
+
+    device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    ncol = c_columns(res)
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    lev = lambda a, b: torch.linspace(a, b, NZ, device=device)[:, None]
+    T = lev(200.0, 300.0) + 5.0 * torch.randn((NZ, ncol), generator=g, device=device)
+    q = 0.02 * torch.exp(-lev(0.0, 6.0)) * (0.2 + 0.8 * torch.rand((NZ, ncol), generator=g, device=device))
+    qc = 1e-4 * torch.rand((NZ, ncol), generator=g, device=device) * (
+        torch.rand((NZ, ncol), generator=g, device=device) < 0.3)
+    delp = lev(200.0, 1800.0) * (0.98 + 0.04 * torch.rand((NZ, ncol), generator=g, device=device))
+    state = {"air_temperature_input": T, "specific_humidity_input": q, "cloud_water_mixing_ratio_input": qc,
+             "pressure_thickness_of_atmospheric_layer": delp,
+             "air_temperature_after_last_gscond": T + 0.1 * torch.randn((NZ, ncol), generator=g, device=device),
+             "specific_humidity_after_last_gscond": q * (0.95 + 0.1 * torch.rand((NZ, ncol), generator=g,
+                                                                                 device=device))}
+    sample = {k: v[:, :4096].T.contiguous().cpu().numpy() for k, v in state.items()}
+    rng = np.random.default_rng(seed)
+    sample_out = {}
+    for o in zhao_carr_outputs(NZ):
+        sc = 1e-3 if o.name == "total_precipitation" else (1e-5 if ("humid" in o.name or "cloud" in o.name) else 0.5)
+        sample_out[o.name] = rng.normal(0, sc, (4096, o.nz)).astype(np.float32)
+    emu = MicrophysicsEmulator.random(sample, sample_out, seed=seed)
+    out = {(o.after or o.name): torch.empty((o.nz, ncol), device=device) for o in emu.outputs}
+    cfg = emu.model.config
+    return EmulatorWorkload(emu, state, out, ncol, cfg.flops_per_column(),
+                            4 * (6 * NZ + cfg.k_out))

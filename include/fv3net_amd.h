@@ -39,7 +39,7 @@ extern "C" {
 #define FV3_ERR_UNSUPPORTED 3 /* valid request this build does not implement */
 
 const char* fv3_last_error(void);
-int fv3_abi_version(void); /* bumped on any signature change */
+int fv3_abi_version(void); /* bumped on any signature change (2: emulator fields in fv3_dense_desc) */
 
 /*
  * Column layout of a [level, column] field.  Element (column c, level k) lives at
@@ -95,6 +95,10 @@ typedef struct {
     const float* out_min;              /* [k_out] or NULL; -inf = no lower limit */
     const float* out_max;              /* [k_out] or NULL; +inf = no upper limit */
     const float* out_mask;             /* [k_out] or NULL; 0/1 zero-mask of clipped levels */
+    /* microphysics-emulator graph extensions (emulation/transforms/transforms.py): */
+    const float* in_log_eps;           /* [n_in] or NULL; > 0: input v enters as log(max(x, eps)) */
+    const int* out_residual;           /* [n_out] or NULL; r >= 0: output o is written as
+                                        * input_r + denormalised output (Difference.backward) */
 } fv3_dense_desc;
 
 typedef struct fv3_dense_model fv3_dense_model;

@@ -1,0 +1,99 @@
+"""Zhao-Carr microphysics emulator (BASELINE config #5): the fused
+kernel vs the numpy restatement of the inference graph (oracle/emulator.py).
+Contract: 1e-3 rel (north_star); the float32 MFMA path is held to 1e-5."""
+import numpy as np
+import pytest
+
+from oracle import emulator as OE
+
+
+def test_product_spec_matches_the_reference_restatement():
+    from fv3net_amd import emulator as E
+
+    spec = OE.zhao_carr_spec()
+    assert [f.name for f in E.zhao_carr_features()] == [f["name"] for f in spec["features"]]
+    assert [f.source for f in E.zhao_carr_features()] == [f["source"] for f in spec["features"]]
+    assert [f.log_eps for f in E.zhao_carr_features()] == [f.get("log_eps") for f in spec["features"]]
+    assert [(o.name, o.nz, o.residual_of, o.after) for o in E.zhao_carr_outputs()] == \
+        [(o["name"], o["nz"], o.get("residual_of"), o.get("after")) for o in spec["outputs"]]
+
+
+def test_norm_fits_match_oracle():
+    from fv3net_amd import emulator as E
+
+    x = np.random.default_rng(0).normal(3, 2, (500, 79)).astype(np.float32)
+    np.testing.assert_array_equal(E.fit_center_per_feature(x), OE.fit_center_per_feature(x))
+    assert E.fit_scale_all(x) == OE.fit_scale_all(x)
+
+
+def test_oracle_bf16_rounding():
+    # bf16 keeps 7 explicit mantissa bits: ulp(1) = 2**-7
+    x = np.array([1.0078125, 1.00390625, 1.01171875, 1.001953125, -3.14159, np.nan], np.float32)
+    r = OE.to_bf16(x)
+    assert r[0] == 1.0078125                      # representable
+    assert r[1] == 1.0 and r[2] == 1.015625       # ties go to the even mantissa
+    assert r[3] == 1.0                            # below half an ulp
+    assert r[4] == -3.140625 and np.isnan(r[5])
+
+
+def _emulator(ncol=2048, seed=1):
+    from fv3net_amd.emulator import MicrophysicsEmulator, zhao_carr_outputs
+
+    raw = OE.synthetic_raw(ncol, seed=seed)
+    rng = np.random.default_rng(seed + 1)
+    sample_out = {}
+    for o in zhao_carr_outputs():
+        s = 1e-3 if o.name == "total_precipitation" else (1e-5 if ("humid" in o.name or "cloud" in o.name) else 0.5)
+        sample_out[o.name] = rng.normal(0, s, (4096, o.nz)).astype(np.float32)
+    emu = MicrophysicsEmulator.random(raw, sample_out, seed=seed)
+    return emu, raw
+
+
+@pytest.mark.gpu
+def test_emulator_matches_oracle(gpu):
+    import torch
+
+    emu, raw = _emulator()
+    ref = OE.forward(raw, OE.zhao_carr_spec(), emu.params_by_name(), np.float64)
+    state = {k: torch.from_numpy(np.ascontiguousarray(v.T)).cuda() for k, v in raw.items()}  # [feature, sample]
+    got = emu(state)
+    for o in OE.zhao_carr_spec()["outputs"]:
+        name = o.get("after") or o["name"]
+        g = got[name].cpu().numpy()
+        r = ref[name]
+        r = r[:, 0] if o["nz"] == 1 else r.T
+        err = np.abs(g - r).max() / np.abs(r).max()
+        assert err <= 1e-5, (name, err)
+        if o.get("residual_of"):  # the difference itself, recovered from the after-state
+            d = g.astype(np.float64) - raw[o["residual_of"]].T.astype(np.float64)
+            derr = np.abs(d - ref[o["name"]].T).max() / np.abs(ref[o["name"]]).max()
+            assert derr <= 1e-3, (o["name"], derr)
+
+
+@pytest.mark.gpu
+def test_microphysics_hook_updates_state_in_place(gpu):
+    import torch
+
+    from fv3net_amd.emulator import MicrophysicsHook
+
+    emu, raw = _emulator(ncol=300, seed=3)
+    state = {k: torch.from_numpy(np.ascontiguousarray(v.T)).cuda() for k, v in raw.items()}
+    hook = MicrophysicsHook(emu)
+    hook.microphysics(state)
+    assert "air_temperature_after_precpd" in state and state["total_precipitation"].shape == (300,)
+    with pytest.raises(KeyError):
+        emu({"air_temperature_input": state["air_temperature_input"]})
+
+
+@pytest.mark.gpu
+def test_emulator_workload_c12(gpu):
+    import torch
+
+    from fv3net_amd import workloads as W
+
+    wl = W.make_emulator_workload(12, seed=1)
+    res = wl.step()
+    torch.cuda.synchronize()
+    assert res["total_precipitation"].shape == (W.c_columns(12),)
+    assert all(torch.isfinite(v).all() for v in res.values())
+    assert wl.flops_per_column == 2 * (711 * 256 + 256 * 256 + 256 * 396)
