@@ -555,8 +555,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
                     if (y < lo[r]) y = lo[r];
                     if (y >= hi[r]) y = hi[r];
                     y = y * mk[r];
-                    if (rsrc) y = rsrc[(int64_t)(oz0 + row) * rld] + y;  // after = before + to
-                    if (cvalid && row < onrow) dst[(int64_t)(oz0 + row) * ld] = y;
+                    if (cvalid && row < onrow) {  // padding rows of the last tile: no reads either
+                        if (rsrc) y = rsrc[(int64_t)(oz0 + row) * rld] + y;  // after = before + to
+                        dst[(int64_t)(oz0 + row) * ld] = y;
+                    }
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -915,7 +917,12 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
     // FV3_DENSE_GRID overrides (A/B)
     static std::mutex mu;
     static int n_cu = 0;
-    static std::vector<std::pair<const void*, int>> resident;
+    struct Resident {
+        const void* fn;
+        size_t lds;
+        int blocks;
+    };
+    static std::vector<Resident> resident;  // keyed by kernel and LDS size (models differ in LDS)
     std::lock_guard<std::mutex> lock(mu);
     if (!n_cu) {
         int dev = 0;
@@ -924,11 +931,11 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
     }
     int res = 0;
     for (auto& r : resident)
-        if (r.first == kfn) res = r.second;
+        if (r.fn == kfn && r.lds == lds) res = r.blocks;
     if (!res) {
         FV3_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&res, kfn, 256, lds));
         res = std::max(1, res);
-        resident.push_back({kfn, res});
+        resident.push_back({kfn, lds, res});
     }
     int64_t grid = std::min<int64_t>(a.ntiles, (int64_t)res * n_cu);
     if (const char* e = getenv("FV3_DENSE_GRID")) grid = std::min<int64_t>(a.ntiles, std::max(1, atoi(e)));
