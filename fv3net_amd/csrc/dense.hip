@@ -862,7 +862,9 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
     a.ncol_blk = nb;
     // columns per tile: two 16-column tiles (halves weight traffic per FLOP; measured
     // fastest at C48 and C384); FV3_DENSE_NC=1 for A/B
-    int nc = 2;
+    // wide-input models (the microphysics emulator: 736 padded features) stage 32
+    // columns in > 64 KiB of LDS, i.e. one block per CU: use 16-column tiles there
+    int nc = (size_t)2 * 16 * 4 * m->kp > 64 * 1024 ? 1 : 2;
     if (const char* e = getenv("FV3_DENSE_NC")) nc = atoi(e) == 1 ? 1 : 2;
     const int ncol_tile = 16 * nc;
     a.ntiles = (ncol + ncol_tile - 1) / ncol_tile;
