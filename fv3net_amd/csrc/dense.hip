@@ -88,12 +88,13 @@ struct DenseArgs {
     int wbytes;             // its size (buffer range)
     // input slots (per launch): slot q covers feature rows [fdst, fdst + 256/NCOL) of one
     // variable; thread row fq reads base[blk * bs + ii + fq * ld] if fq < nk, writes
-    // padded feature fdst + fq if fq < nf.  meta = fdst << 16 | nk << 8 | nf
+    // padded feature fdst + fq if fq < nf.  meta = var << 27 | fdst << 16 | nk << 8 | nf
+    // (var: the slot's input variable; every field is read with scalar loads — a byte
+    // array here would be a vector load and a vmcnt(0) wait per slot)
     const float* slot_base[kMaxSlots];
     int slot_bs[kMaxSlots];
     int slot_ld[kMaxSlots];
     int slot_meta[kMaxSlots];
-    unsigned char slot_var[kMaxSlots];  // input variable of each slot
     float in_log_eps[kMaxVars];         // > 0: the variable enters as log(max(x, eps)) (emulator LogTransform)
     float* out_ptr[kMaxVars];
     int64_t out_ld[kMaxVars];
@@ -364,7 +365,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     auto xidx = [&](int f) { return ((f >> 4) * 64 + (f & 3) * 16 + cl16) * 4 + ((f >> 2) & 3); };
     auto put = [&](int meta, float x, bool valid, int fq, float leps) {
         if (fq < (meta & 0xff)) {
-            const int f = (meta >> 16) + fq;
+            const int f = ((meta >> 16) & 0x7ff) + fq;
             if (leps > 0.0f) x = __logf_exact(x, leps);  // LogTransform.forward (transforms.py:123-124)
             xc[xidx(f)] = (valid && fq < ((meta >> 8) & 0xff)) ? (x - s_mean[f]) / s_denom[f] : 0.0f;
         }
@@ -374,15 +375,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         const bool valid = col_of(tile, blk, ii);
         static_for<kRawSlots>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
-            if (q < pk.nslots) put(pk.slot_meta[q], raw[q], valid, fq, pk.in_log_eps[pk.slot_var[q]]);
+            if (q < pk.nslots) {
+                const int meta = pk.slot_meta[q];
+                put(meta, raw[q], valid, fq, pk.in_log_eps[(meta >> 27) & 0xf]);
+            }
             if constexpr (q % 2 == 1) __builtin_amdgcn_sched_barrier(0);  // don't interleave 20 divisions
         });
-        for (int q = kRawSlots; q < pk.nslots; ++q) {  // inputs wider than the register prefetch
-            const int meta = pk.slot_meta[q];
-            const float x = (valid && fq < ((meta >> 8) & 0xff))
-                                ? pk.slot_base[q][blk * pk.slot_bs[q] + ii + (int64_t)fq * pk.slot_ld[q]]
-                                : 0.0f;
-            put(meta, x, valid, fq, pk.in_log_eps[pk.slot_var[q]]);
+        // inputs wider than the register prefetch: batches of 8 loads in flight
+        for (int q0 = kRawSlots; q0 < pk.nslots; q0 += 8) {
+            float xt[8];
+            static_for<8>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                const int q = q0 + i;
+                xt[i] = 0.0f;
+                if (q < pk.nslots && valid && fq < ((pk.slot_meta[q] >> 8) & 0xff))
+                    xt[i] = pk.slot_base[q][blk * pk.slot_bs[q] + ii + (int64_t)fq * pk.slot_ld[q]];
+            });
+            static_for<8>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                const int q = q0 + i;
+                if (q < pk.nslots) {
+                    const int meta = pk.slot_meta[q];
+                    put(meta, xt[i], valid, fq, pk.in_log_eps[(meta >> 27) & 0xf]);
+                }
+            });
         }
         for (int f = 4 * p.in_steps_total + fq; f < p.kp; f += FPS) xc[xidx(f)] = 0.0f;
     };
@@ -882,8 +898,7 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
             a.slot_ld[q] = (int)in_l[v].ld;
             const int nk = std::max(0, std::min(nk_v - f0, 255));
             const int nf = std::min(nf_v - f0, 255);
-            a.slot_meta[q] = ((4 * m->in_step0[v] + f0) << 16) | (nk << 8) | nf;
-            a.slot_var[q] = (unsigned char)v;
+            a.slot_meta[q] = (v << 27) | ((4 * m->in_step0[v] + f0) << 16) | (nk << 8) | nf;
         }
     }
     hipStream_t s = (hipStream_t)stream;

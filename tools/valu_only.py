@@ -1,5 +1,5 @@
 """Drivers for counter passes: `mappm` (C384 79->79 kord 1) or `coarsen` (C384 -> C48,
-1 field) or `dense` (C48), N launches."""
+1 field) or `dense` (C48) / `dense384`, N launches."""
 import os
 import sys
 
@@ -15,6 +15,8 @@ if __name__ == "__main__":
         wl = W.make_mappm_workload(W.c_columns(384), 79, 79, 1, seed=5, device=dev)
     elif what == "coarsen":
         wl = W.make_coarsen_workload(384, 8, 1, seed=7, device=dev)
+    elif what == "dense384":
+        wl = W.make_dense_workload(384, seed=1, device=dev)
     else:
         wl = W.make_dense_workload(48, seed=1, device=dev)
     for _ in range(n):
