@@ -42,6 +42,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -71,7 +72,6 @@ struct DenseOutTile {
     int var;  // output variable or -1 (padding tile)
     int z0;   // level of the tile's first row
     int nrow; // valid rows in this tile (<= 16)
-    int pad;
 };
 
 struct DenseArgs {
@@ -89,13 +89,14 @@ struct DenseArgs {
     // input slots (per launch): slot q covers feature rows [fdst, fdst + 256/NCOL) of one
     // variable; thread row fq reads base[blk * bs + ii + fq * ld] if fq < nk, writes
     // padded feature fdst + fq if fq < nf.  meta = var << 27 | fdst << 16 | nk << 8 | nf
-    // (var: the slot's input variable; every field is read with scalar loads — a byte
-    // array here would be a vector load and a vmcnt(0) wait per slot)
+    // (var: the slot's input variable).  Slots past nslots are all zero (no rows).
+    // Every field is 4-byte: read with scalar loads (a byte array here would be a
+    // vector load and a vmcnt(0) wait per slot)
     const float* slot_base[kMaxSlots];
     int slot_bs[kMaxSlots];
     int slot_ld[kMaxSlots];
     int slot_meta[kMaxSlots];
-    float in_log_eps[kMaxVars];         // > 0: the variable enters as log(max(x, eps)) (emulator LogTransform)
+    float slot_leps[kMaxSlots];  // > 0: the slot's variable enters as log(max(x, eps)) (emulator LogTransform)
     float* out_ptr[kMaxVars];
     int64_t out_ld[kMaxVars];
     int64_t out_bs[kMaxVars];
@@ -109,7 +110,7 @@ struct DenseArgs {
     int n_in, n_hidden_extra, n_otiles, kp;
     int in_steps_total, nslots;
     int lds_x;              // f32x4 offset of the constants area (after activations / inputs)
-    int pad_;
+    int has_log;            // any slot with a LogTransform (selects the staging variant)
     long long* trace;       // profiling hook (fv3_dense_set_trace): [tiles][8] timestamps, or NULL
 };
 static_assert(sizeof(DenseArgs) <= 4096, "kernel arguments are limited to 4 KiB");
@@ -340,21 +341,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         const int64_t col = tile * NCOL + cb;
         const bool valid = col < p.ncol;
         const int64_t cc = valid ? col : 0;
-        blk = cc / p.ncol_blk;
-        ii = cc - blk * p.ncol_blk;
+        if (p.ncol_blk >= p.ncol) {  // one block (uniform): no 64-bit division
+            blk = 0;
+            ii = cc;
+        } else {
+            blk = cc / p.ncol_blk;
+            ii = cc - blk * p.ncol_blk;
+        }
         return valid;
+    };
+    // slot q's value in this thread's feature row (0 past the variable's kept levels,
+    // past the last column, and in unused slots: meta 0).  No branch per slot, so the
+    // scalar reads of all slot descriptors can be in flight together.
+    auto slot_load = [&](KArgs& pk, int q, int meta, bool valid, int64_t blk, int64_t ii, int fq) {
+        return (valid && fq < ((meta >> 8) & 0xff))
+                   ? pk.slot_base[q][blk * pk.slot_bs[q] + ii + (int64_t)fq * pk.slot_ld[q]]
+                   : 0.0f;
     };
     auto load_raw = [&](KArgs& pk, int64_t tile, int fq) {
         int64_t blk, ii;
         const bool valid = col_of(tile, blk, ii);
         static_for<kRawSlots>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
-            if (q < pk.nslots) {
-                const int nk = (pk.slot_meta[q] >> 8) & 0xff;
-                raw[q] = (valid && fq < nk)
-                             ? pk.slot_base[q][blk * pk.slot_bs[q] + ii + (int64_t)fq * pk.slot_ld[q]]
-                             : 0.0f;
-            }
+            raw[q] = slot_load(pk, q, pk.slot_meta[q], valid, blk, ii, fq);
         });
     };
     // normalise and write the staged inputs in B-operand order: for column tile c,
@@ -363,41 +372,61 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     float* xc = reinterpret_cast<float*>(hbuf) + (cb >> 4) * (p.kp * 16);
     const int cl16 = cb & 15;
     auto xidx = [&](int f) { return ((f >> 4) * 64 + (f & 3) * 16 + cl16) * 4 + ((f >> 2) & 3); };
-    auto put = [&](int meta, float x, bool valid, int fq, float leps) {
-        if (fq < (meta & 0xff)) {
-            const int f = ((meta >> 16) & 0x7ff) + fq;
+    float* s_dummy = s_ep + 6 * 16 * p.n_otiles;  // write-only sink
+    // branch-free: lanes past the slot's rows store to s_dummy, so the slots of a batch
+    // schedule together (no divergent region between them)
+    // (x - mean) / denom as x' * rcp + one residual correction (within an ulp of the
+    // IEEE quotient; the 1e-5 contract does not need the exact division sequence)
+    auto put = [&](int meta, float x, float leps, float mu, float dn, bool valid, int fq, auto logc) {
+        const int f = min(((meta >> 16) & 0x7ff) + fq, p.kp - 1);
+        if constexpr (decltype(logc)::value)
             if (leps > 0.0f) x = __logf_exact(x, leps);  // LogTransform.forward (transforms.py:123-124)
-            xc[xidx(f)] = (valid && fq < ((meta >> 8) & 0xff)) ? (x - s_mean[f]) / s_denom[f] : 0.0f;
-        }
+        const float a = x - mu;
+        const float r = __builtin_amdgcn_rcpf(dn);
+        const float q0 = a * r;
+        float y = __builtin_fmaf(__builtin_fmaf(-q0, dn, a), r, q0);
+        asm volatile("" : "+v"(y));  // computed by every lane, then selected: no divergent branch
+        y = (valid && fq < ((meta >> 8) & 0xff)) ? y : 0.0f;
+        *(fq < (meta & 0xff) ? xc + xidx(f) : s_dummy) = y;
     };
-    auto store_x = [&](KArgs& pk, int64_t tile, int fq) {
+    auto feat = [&](int meta, int fq) { return min(((meta >> 16) & 0x7ff) + fq, p.kp - 1); };
+    auto store_x = [&](KArgs& pk, int64_t tile, int fq, auto logc) {
         int64_t blk, ii;
         const bool valid = col_of(tile, blk, ii);
-        static_for<kRawSlots>([&](auto qc) {
-            constexpr int q = decltype(qc)::value;
-            if (q < pk.nslots) {
-                const int meta = pk.slot_meta[q];
-                put(meta, raw[q], valid, fq, pk.in_log_eps[(meta >> 27) & 0xf]);
-            }
-            if constexpr (q % 2 == 1) __builtin_amdgcn_sched_barrier(0);  // don't interleave 20 divisions
+        constexpr int B = 5;  // slots per batch: descriptors and constants read before any use
+        static_assert(kRawSlots % B == 0, "");
+        static_for<kRawSlots / B>([&](auto bc) {
+            constexpr int b = decltype(bc)::value;
+            int mt[B];
+            float le[B], mu[B], dn[B];
+            static_for<B>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                mt[i] = pk.slot_meta[b * B + i];
+                le[i] = pk.slot_leps[b * B + i];
+            });
+            static_for<B>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                mu[i] = s_mean[feat(mt[i], fq)];
+                dn[i] = s_denom[feat(mt[i], fq)];
+            });
+            static_for<B>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                put(mt[i], raw[b * B + i], le[i], mu[i], dn[i], valid, fq, logc);
+            });
         });
         // inputs wider than the register prefetch: batches of 8 loads in flight
         for (int q0 = kRawSlots; q0 < pk.nslots; q0 += 8) {
             float xt[8];
+            int mt[8];
             static_for<8>([&](auto ic) {
                 constexpr int i = decltype(ic)::value;
-                const int q = q0 + i;
-                xt[i] = 0.0f;
-                if (q < pk.nslots && valid && fq < ((pk.slot_meta[q] >> 8) & 0xff))
-                    xt[i] = pk.slot_base[q][blk * pk.slot_bs[q] + ii + (int64_t)fq * pk.slot_ld[q]];
+                mt[i] = q0 + i < pk.nslots ? pk.slot_meta[q0 + i] : 0;
+                xt[i] = slot_load(pk, q0 + i, mt[i], valid, blk, ii, fq);
             });
             static_for<8>([&](auto ic) {
                 constexpr int i = decltype(ic)::value;
-                const int q = q0 + i;
-                if (q < pk.nslots) {
-                    const int meta = pk.slot_meta[q];
-                    put(meta, xt[i], valid, fq, pk.in_log_eps[(meta >> 27) & 0xf]);
-                }
+                put(mt[i], xt[i], mt[i] ? pk.slot_leps[q0 + i] : 0.0f, s_mean[feat(mt[i], fq)],
+                    s_denom[feat(mt[i], fq)], valid, fq, logc);
             });
         }
         for (int f = 4 * p.in_steps_total + fq; f < p.kp; f += FPS) xc[xidx(f)] = 0.0f;
@@ -454,7 +483,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         // ~100 loop-invariant scalars spilled into VGPRs for the whole loop
         KArgs* pt = &p;
         asm volatile("" : "+s"(pt));
-        store_x(*pt, tile, fq);
+        if (p.has_log)
+            store_x(*pt, tile, fq, std::true_type{});
+        else
+            store_x(*pt, tile, fq, std::false_type{});
         __syncthreads();
         trace_mark(p, tile, 1);
 
@@ -675,7 +707,7 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
             FV3_REQUIRE(d->in_nz[res] >= nz, "dense_create: residual input %d has fewer levels than output %d", res, v);
         m->out_residual.push_back(res < 0 ? -1 : res);
         for (int z0 = 0; z0 < nz; z0 += 16) {
-            DenseOutTile t{v, z0, std::min(16, nz - z0), 0};
+            DenseOutTile t{v, z0, std::min(16, nz - z0)};
             m->otiles.push_back(t);
             for (int r = 0; r < 16; ++r) ofeat_src.push_back(r < t.nrow ? k_out + z0 + r : -1);
         }
@@ -814,7 +846,6 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
     a.wo_off = (int)pcs[6].off;
     a.wbytes = (int)total;
     for (int t = 0; t < m->n_otiles; ++t) a.otile[t] = m->otiles[t];
-    for (int v = 0; v < m->n_in; ++v) a.in_log_eps[v] = m->in_log_eps[v];
     a.n_in = m->n_in;
     a.n_hidden_extra = nhx;
     a.n_otiles = m->n_otiles;
@@ -899,6 +930,8 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
             const int nk = std::max(0, std::min(nk_v - f0, 255));
             const int nf = std::min(nf_v - f0, 255);
             a.slot_meta[q] = (v << 27) | ((4 * m->in_step0[v] + f0) << 16) | (nk << 8) | nf;
+            a.slot_leps[q] = m->in_log_eps[v];
+            a.has_log |= m->in_log_eps[v] > 0.0f;
         }
     }
     hipStream_t s = (hipStream_t)stream;
@@ -908,7 +941,8 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
     const size_t xbytes = (size_t)nc * sizeof(float) * 16 * (size_t)m->kp;
     const size_t abytes = std::max(hbytes, xbytes);
     a.lds_x = (int)(abytes / 16);
-    const size_t lds = abytes + sizeof(float) * (2 * (size_t)m->kp + 6 * 16 * (size_t)m->n_otiles);
+    // + one dummy f32x4: the staging stores of lanes past a slot's rows land there
+    const size_t lds = abytes + sizeof(float) * (2 * (size_t)m->kp + 6 * 16 * (size_t)m->n_otiles) + 16;
     FV3_REQUIRE(lds <= 160 * 1024, "dense_forward: %d input features need too much LDS", m->kp);
     // (waves per SIMD targeted by register allocation, weight ring depth):
     // FV3_DENSE_CFG = "3,2" (default) | "2,3" | "4,2" (A/B)
