@@ -123,6 +123,9 @@ __device__ __forceinline__ void trace_mark(__attribute__((address_space(4))) con
     if (p.trace && threadIdx.x == 0) {
         p.trace[tile * 8 + slot] = wall_clock64();
         if (slot == 0) p.trace[tile * 8 + 7] = (long long)__smid();
+        // slot 6: shader-clock cycles from tile start (5) to tile end (4)
+        if (slot == 5) p.trace[tile * 8 + 6] = (long long)__builtin_amdgcn_s_memtime();
+        if (slot == 4) p.trace[tile * 8 + 6] = (long long)__builtin_amdgcn_s_memtime() - p.trace[tile * 8 + 6];
     }
 }
 
@@ -205,6 +208,9 @@ __device__ __forceinline__ Rsrc make_rsrc(const void* base, int bytes)
 template <typename FT>
 __device__ __forceinline__ FT bload(Rsrc r, int voff, int soff)
 {
+#ifdef FV3_EXP_L1_WEIGHTS  // experiment only: every weight fragment from one 4 KiB window (L1 hits)
+    soff &= 0xfff;
+#endif
     if constexpr (sizeof(FT) == 16)
         return __builtin_bit_cast(FT, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
     else if constexpr (sizeof(FT) == 8)
@@ -563,7 +569,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         const int64_t colw = tile * NCOL + 16 * cw + (lane & 15);
         const bool cvalid = colw < p.ncol;
         const int64_t cc = cvalid ? colw : 0;
-        const int64_t oblk = cc / p.ncol_blk;
+        const int64_t oblk = p.ncol_blk >= p.ncol ? 0 : cc / p.ncol_blk;
         const int64_t oii = cc - oblk * p.ncol_blk;
         for (int i0 = 0; i0 < ucnt; i0 += kMaxUnits) {
             const OutPlan pl = plan(i0);

@@ -41,6 +41,11 @@ def run(res, nc, wpe=2):
     for i, n in enumerate(names):
         print(f"   {n:7s} mean {d[:, i].mean():6.2f}  p10 {np.percentile(d[:, i], 10):6.2f}  "
               f"p90 {np.percentile(d[:, i], 90):6.2f}  max {d[:, i].max():6.2f}")
+    cyc = t[:, 6].astype(np.float64)
+    dur = ts[:, 5] - ts[:, 1]  # tile start (5) -> end (4), us
+    ok = dur > 0
+    print(f"   shader clock over tiles: median {np.median(cyc[ok] / dur[ok]) / 1e3:.3f} GHz "
+          f"(p10 {np.percentile(cyc[ok] / dur[ok], 10) / 1e3:.3f}, p90 {np.percentile(cyc[ok] / dur[ok], 90) / 1e3:.3f})")
     starts = np.sort(ts[:, 0])
     print("   start times pct 0/25/50/75/90/100:",
           " ".join(f"{np.percentile(starts, q):.1f}" for q in (0, 25, 50, 75, 90, 100)))
