@@ -29,6 +29,8 @@ EXPORTED_SYMBOLS = (
     "fv3_dense_set_trace",
     "fv3_regrid_coarsen",
     "fv3_regrid_coarsen_f64",
+    "fv3_regrid_coarsen_edge",
+    "fv3_regrid_coarsen_edge_f64",
     "fv3_column_integral",
     "fv3_area_weighted_sums",
     "fv3_level_sums",
@@ -114,6 +116,10 @@ _SIGNATURES = {
                                 _I, _I, _I, _I, _D, _P]),
     "fv3_regrid_coarsen_f64": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _P, _I, _I, _I,
                                     _I, _I, _I, _I, _D, _P]),
+    "fv3_regrid_coarsen_edge": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _I, _I, _I, _I,
+                                     _I, _I, _I, _I, _D, _P]),
+    "fv3_regrid_coarsen_edge_f64": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _I, _I, _I, _I,
+                                         _I, _I, _I, _I, _D, _P]),
     "fv3_column_integral": (_I, [_P, Layout, _P, Layout, _P, _I64, _I, _D, _P]),
     "fv3_area_weighted_sums": (_I, [ctypes.POINTER(_P), _I, _P, _I64, _P, _P]),
     "fv3_level_sums": (_I, [_P, Layout, _I64, _I, _P, _P]),

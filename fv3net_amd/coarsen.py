@@ -61,6 +61,59 @@ def coarsen_on_pressure(delp, area, fields: Mapping[str, object], factor: int, i
     return dict(zip(names, outs)), delp_c
 
 
+def _delp_on_device(delp):
+    delp64 = (isinstance(delp, np.ndarray) and delp.dtype == np.float64) or (
+        torch is not None and isinstance(delp, torch.Tensor) and delp.dtype == torch.float64)
+    if delp64:  # keep restart precision: pressures are cumulated in float64 on device
+        delp = (torch.as_tensor(delp) if not isinstance(delp, torch.Tensor) else delp).to(
+            device=torch.device("cuda", torch.cuda.current_device()), dtype=torch.float64).contiguous()
+    else:
+        delp = _device.to_device_f32(delp)
+    return delp, delp64
+
+
+def coarsen_edges_on_pressure(delp, spacing, fields: Mapping[str, object], factor: int, edge: str = "x",
+                              iv: int = 1, kord: int = 1, ptop: float = TOA_PRESSURE, stream=None):
+    """D-grid winds on coarse pressure levels: regrid_to_edge_weighted_pressure
+    (regridz.py:58-112) followed by the masked edge_weighted_block_average of
+    coarsen_restarts.py:493-509, fused (csrc/coarsen.hip, regrid_coarsen_edge_kernel).
+
+    delp (6, z, n, n) cell centers; edge "x": spacing dx (6, n+1, n) and fields u
+    (6, z, n+1, n) -> (6, z, n/f+1, n/f); edge "y": spacing dy (6, n, n+1) and fields
+    v (6, z, n, n+1) -> (6, z, n/f, n/f+1).  Device tensors in and out."""
+    _device.require_gpu()
+    if edge not in ("x", "y"):
+        raise ValueError(f"'edge' most be either 'x' or 'y'; got {edge}.")  # coarsen.py:253
+    delp, delp64 = _delp_on_device(delp)
+    spacing = _device.to_device_f32(spacing)
+    if delp.dim() != 4 or spacing.dim() != 3:
+        raise ValueError("delp must be (tile, z, y, x) and the edge spacing (tile, y, x)")
+    nt, km, ny, nx = delp.shape
+    eshape = (nt, ny + 1, nx) if edge == "x" else (nt, ny, nx + 1)
+    if tuple(spacing.shape) != eshape:
+        raise ValueError(f"edge {edge!r} spacing must be {eshape}, got {tuple(spacing.shape)}")
+    names = list(fields)
+    tens = []
+    for n in names:
+        t = _device.to_device_f32(fields[n])
+        if tuple(t.shape) != (nt, km) + eshape[1:]:
+            raise ValueError(f"{n} shape {tuple(t.shape)} != {(nt, km) + eshape[1:]}")
+        tens.append(t)
+    if ny % factor or nx % factor:
+        raise ValueError(f"grid {ny}x{nx} is not divisible by the coarsening factor {factor}")
+    nc = nx // factor
+    cshape = (nt, km, nc + 1, nc) if edge == "x" else (nt, km, nc, nc + 1)
+    outs = [torch.empty(cshape, dtype=torch.float32, device=delp.device) for _ in names]
+    fptr = (ctypes.c_void_p * max(1, len(tens)))(*[t.data_ptr() for t in tens])
+    optr = (ctypes.c_void_p * max(1, len(outs)))(*[t.data_ptr() for t in outs])
+    lib = _native.load()
+    fn = lib.fv3_regrid_coarsen_edge_f64 if delp64 else lib.fv3_regrid_coarsen_edge
+    st = fn(delp.data_ptr(), spacing.data_ptr(), fptr, optr, len(tens), nt, km, ny, nx, int(factor),
+            0 if edge == "x" else 1, int(iv), int(kord), float(ptop), _device.stream_handle(stream))
+    _native.check(st, "regrid_coarsen_edge")
+    return dict(zip(names, outs))
+
+
 def regrid_vertical(p_in, f_in, p_out, iv: int = 1, kord: int = 1, z_axis: int = -1):
     """Device regrid_vertical (regridz.py:164-279) on arrays whose vertical axis is
     ``z_axis`` (default last, as the reference transposes to); float32 result with

@@ -240,6 +240,196 @@ __global__ __launch_bounds__(512) void regrid_coarsen_kernel(CoarsenArgs<DT> a)
     }
 }
 
+// ====================================================================================
+// Edge-weighted (D-grid u / v) pressure-level coarse-graining
+//   regrid_to_edge_weighted_pressure   regridz.py:58-112
+//     delp_staggered = xgcm interp of delp to the edges (0.5 * (left + right), halo
+//                      cells from the connected faces, cubedsphere/xgcm.py:7-34)
+//     edge_weighted_block_average(delp_staggered, spacing)   coarsen.py:221-271
+//     _regrid_given_delp (staggered block_upsample_like, mappm, _mask_weights)
+//   edge_weighted_block_average(u_regrid, masked spacing)     coarsen_restarts.py:493-509
+// Only every f-th outer line survives the final average, and the upsampled coarse
+// delp at those fine points is that of the same coarse edge, so a coarse edge needs
+// just its own f fine edge points: lane = one of them, f consecutive lanes = one
+// coarse edge, 64 / f coarse edges per one-wave block.
+//   edge x (u): fine points (Y*f, X*f + j) on (y outer, x center); window along x
+//               (memory-contiguous: numpy pairwise order, the xor tree for f = 8)
+//   edge y (v): fine points (Y*f + j, X*f) on (y center, x outer); window along y
+//               (strided: sequential order)
+// ====================================================================================
+
+// cubedsphere/xgcm.py FV3_FACE_CONNECTIONS: [tile][axis x=0,y=1][side left=0,right=1]
+// = neighbour tile * 2 + its connecting axis.  A line from a face whose connecting
+// axis is the other one runs reversed along the tangential index (pinned by the
+// reference's regression data, oracle/coarsen.py face_halo).
+__constant__ int kFaceConn[6][2][2] = {
+    {{4 * 2 + 1, 1 * 2 + 0}, {5 * 2 + 1, 2 * 2 + 0}},
+    {{0 * 2 + 0, 3 * 2 + 1}, {5 * 2 + 0, 2 * 2 + 1}},
+    {{0 * 2 + 1, 3 * 2 + 0}, {1 * 2 + 1, 4 * 2 + 0}},
+    {{2 * 2 + 0, 5 * 2 + 1}, {1 * 2 + 0, 4 * 2 + 1}},
+    {{2 * 2 + 1, 5 * 2 + 0}, {3 * 2 + 1, 0 * 2 + 0}},
+    {{4 * 2 + 0, 1 * 2 + 1}, {3 * 2 + 0, 0 * 2 + 1}},
+};
+
+template <typename DT>
+struct EdgeArgs {
+    const DT* delp;        // (6, km, n, n) cell centers
+    const float* spacing;  // (6, ny_e, nx_e) edge lengths
+    const float* fields[kMaxFields];
+    float* out[kMaxFields];  // (6, km, nyc_e, nxc_e)
+    int n_fields, km, n, f, iv, kord, edge;  // edge 0: "x" (u), 1: "y" (v)
+    double ptop;
+};
+
+// element offset (level 0) of delp cell (tile t, row r, col c), r/c possibly one past
+// an edge of the tile: then the halo cell of the connected face
+__device__ __forceinline__ int64_t halo_cell(int t, int r, int c, int n, int64_t tstride)
+{
+    int axis = -1, side = 0, i = 0;
+    if (r < 0) { axis = 1; side = 0; i = c; }
+    else if (r >= n) { axis = 1; side = 1; i = c; }
+    else if (c < 0) { axis = 0; side = 0; i = r; }
+    else if (c >= n) { axis = 0; side = 1; i = r; }
+    if (axis < 0) return (int64_t)t * tstride + (int64_t)r * n + c;
+    const int code = kFaceConn[t][axis][side];
+    const int nb = code >> 1, nax = code & 1;
+    const int ti = (nax != axis) ? n - 1 - i : i;  // rotated face: reversed tangential order
+    int rr, cc;
+    if (nax == 1) { rr = side == 0 ? n - 1 : 0; cc = ti; }  // neighbour's last / first row
+    else { cc = side == 0 ? n - 1 : 0; rr = ti; }           // neighbour's last / first column
+    return (int64_t)nb * tstride + (int64_t)rr * n + cc;
+}
+
+// sum over the f lanes of this lane's coarse edge (first lane `base`); every lane of
+// the edge gets the same value
+template <typename T>
+__device__ __forceinline__ T edge_sum(T v, int f, int base, bool pairwise)
+{
+    if (pairwise) return row_sum<T>(v, f, base);
+    T s = __shfl(v, base, 64);
+    for (int i = 1; i < f; ++i) s = s + __shfl(v, base + i, 64);
+    return s;
+}
+
+// fine edge column: p_in streamed from the running cumsum of the staggered delp
+template <typename DT>
+struct EdgeCol {
+    const float* q;
+    const DT* da;  // the two delp cells either side of this edge point, level 0
+    const DT* db;
+    int64_t plane;   // delp level stride (cell grid)
+    int64_t qplane;  // field level stride (edge grid)
+    const DT* pc;
+    DT ptop, pbot, run;
+    int next, km, kn;
+    __device__ __forceinline__ float q1(int k) const { return q[(int64_t)(k - 1) * qplane]; }
+    __device__ __forceinline__ float pe1(int k)
+    {
+        if (k == 1) return (float)ptop;
+        if (k == km + 1) return (float)pbot;
+        while (next < k - 1) {
+            run = run + (DT)0.5 * (da[(int64_t)next * plane] + db[(int64_t)next * plane]);
+            ++next;
+        }
+        return (float)run;
+    }
+    __device__ __forceinline__ float pe2(int k) const { return (float)pc[k - 1]; }
+    __device__ __forceinline__ void emit(int, float) {}
+    __device__ __forceinline__ float next_edge(int k) const { return (k + 1 <= kn + 1) ? pe2(k + 1) : 0.0f; }
+};
+
+template <typename DT>
+__global__ __launch_bounds__(64) void regrid_coarsen_edge_kernel(EdgeArgs<DT> a)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int f = a.f, km = a.km, n = a.n;
+    const int C = 64 / f;
+    const int lane = threadIdx.x;
+    const int nc = n / f;
+    // coarse edge grid: edge x (nc + 1) rows x nc columns, edge y nc rows x (nc + 1) columns
+    const int ncx = a.edge == 0 ? nc : nc + 1;
+    const int ncy = a.edge == 0 ? nc + 1 : nc;
+    const int nseg = (ncx + C - 1) / C;
+    int64_t bi = blockIdx.x;
+    const int seg = (int)(bi % nseg);
+    bi /= nseg;
+    const int Y = (int)(bi % ncy);
+    const int tile = (int)(bi / ncy);
+    const int lc = lane / f;
+    const int cell = min(lc, C - 1);
+    const int j = lane - lc * f;
+    const int X = seg * C + cell;
+    const bool active = lc < C && X < ncx;
+    const int Xa = min(X, ncx - 1);
+    const int base = cell * f;
+    // this lane's fine edge point and its two delp cells
+    int fr, fcol, ar, ac, br, bc;
+    const int nxe = a.edge == 0 ? n : n + 1;  // fine edge grid width
+    if (a.edge == 0) {
+        fr = Y * f;
+        fcol = Xa * f + (active ? j : 0);
+        ar = fr - 1; ac = fcol; br = fr; bc = fcol;
+    } else {
+        fr = Y * f + (active ? j : 0);
+        fcol = Xa * f;
+        ar = fr; ac = fcol - 1; br = fr; bc = fcol;
+    }
+    const int64_t plane = (int64_t)n * n;
+    const int64_t tstride = (int64_t)km * plane;
+    const DT* da = a.delp + halo_cell(tile, ar, ac, n, tstride);
+    const DT* db = a.delp + halo_cell(tile, br, bc, n, tstride);
+    const int nye = a.edge == 0 ? n + 1 : n;
+    const int64_t eplane = (int64_t)nye * nxe;
+    const int64_t fine = (int64_t)fr * nxe + fcol;
+    const float sp = active ? a.spacing[(int64_t)tile * eplane + fine] : 0.0f;
+    const bool pw = a.edge == 0;  // window along x: numpy's pairwise kernel
+
+    DT* pc = reinterpret_cast<DT*>(smem);  // [C][km+1] coarse phalf of each coarse edge
+    // ---- pass 1: staggered delp, fine phalf, edge-weighted coarse delp and phalf ----
+    const float den0 = edge_sum<float>(nan0(sp), f, base, pw);  // spacing.coarsen().sum(): float32
+    const DT ptop = (DT)a.ptop;
+    DT run = ptop, crun = ptop;
+    if (active && j == 0) pc[cell * (km + 1)] = ptop;
+    for (int k = 0; k < km; ++k) {
+        const DT ds = active ? (DT)0.5 * (da[(int64_t)k * plane] + db[(int64_t)k * plane]) : (DT)0;
+        run = run + ds;
+        const DT num = edge_sum<DT>(nan0((DT)sp * ds), f, base, pw);  // (spacing * delp) in delp's dtype
+        crun = crun + num / (DT)den0;  // coarse phalf = cumsum([ptop, delp_c])
+        if (active && j == 0) pc[cell * (km + 1) + k + 1] = crun;
+    }
+    const DT pbot = run;
+    __syncthreads();
+
+    // ---- per field: remap each fine edge column, masked edge-weighted mean ----
+    const DT* pcc = pc + cell * (km + 1);
+    const int ncol_out = ncx;
+    const int64_t cplane = (int64_t)ncy * ncx;
+    for (int v = 0; v < a.n_fields; ++v) {
+        EdgeCol<DT> col;
+        col.q = a.fields[v] + (int64_t)tile * km * eplane + fine;
+        col.da = da;
+        col.db = db;
+        col.plane = plane;
+        col.qplane = eplane;
+        col.pc = pcc;
+        col.ptop = ptop;
+        col.pbot = pbot;
+        col.run = ptop;
+        col.next = 0;
+        col.km = km;
+        col.kn = km;
+        PpmCursor<EdgeCol<DT>> cur(col, km, km, a.iv, a.kord);
+        float* o = a.out[v] + (int64_t)tile * km * cplane + (int64_t)Y * ncol_out + Xa;
+        for (int k = 0; k < km; ++k) {
+            const float q2 = cur.next();
+            const float w = (pcc[k + 1] < pbot) ? sp : 0.0f;  // _mask_weights (compared in delp's dtype)
+            const float num = edge_sum<float>(nan0(q2 * w), f, base, pw);
+            const float den = edge_sum<float>(nan0(w), f, base, pw);
+            if (active && j == 0) o[(int64_t)k * cplane] = num / den;
+        }
+    }
+}
+
 }  // namespace
 
 template <typename DT>
@@ -296,6 +486,78 @@ int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* f
 }
 
 }  // namespace fv3
+
+namespace fv3 {
+
+template <typename DT>
+int regrid_coarsen_edge_impl(const DT* delp, const float* spacing, const float* const* fields, float* const* out,
+                             int n_fields, int ntile, int km, int ny, int nx, int factor, int edge, int iv, int kord,
+                             double ptop_toa, void* stream)
+{
+    clear_error();
+    FV3_REQUIRE(ntile == 6, "regrid_coarsen_edge: the face connections need all 6 tiles (got %d)", ntile);
+    FV3_REQUIRE(ny == nx && nx >= 1, "regrid_coarsen_edge: tiles must be square (got %d x %d)", ny, nx);
+    FV3_REQUIRE(edge == 0 || edge == 1, "regrid_coarsen_edge: edge must be 0 ('x') or 1 ('y')");
+    FV3_REQUIRE(km >= 4 && km <= kMaxLev, "regrid_coarsen_edge: km must be in [4, %d] (got %d)", kMaxLev, km);
+    FV3_REQUIRE(factor >= 1 && factor <= 8, "regrid_coarsen_edge: coarsening factor must be in [1, 8]");
+    FV3_REQUIRE(nx % factor == 0, "regrid_coarsen_edge: %d not divisible by factor %d", nx, factor);
+    // block_upsample_like (coarsen.py:928-933) infers staggering from the coarse size's
+    // parity: only an even number of coarse cells per tile upsamples correctly there
+    FV3_REQUIRE((nx / factor) % 2 == 0,
+                "regrid_coarsen_edge: %d coarse cells per tile side is odd; the reference's "
+                "block_upsample_like mistakes the center axis for a staggered one", nx / factor);
+    FV3_REQUIRE(n_fields >= 0 && n_fields <= kMaxFields, "regrid_coarsen_edge: n_fields must be in [0, %d]",
+                kMaxFields);
+    FV3_REQUIRE(delp && spacing, "regrid_coarsen_edge: NULL delp/spacing");
+    if (kord > 7) {
+        set_error("regrid_coarsen_edge: kord > 7 (cs_profile) is not fused in this build; use fv3_mappm_ex");
+        return FV3_ERR_UNSUPPORTED;
+    }
+    EdgeArgs<DT> a{};
+    if (n_fields > 0) FV3_REQUIRE(fields && out, "regrid_coarsen_edge: NULL field tables");
+    for (int v = 0; v < n_fields; ++v) {
+        FV3_REQUIRE(fields[v] && out[v], "regrid_coarsen_edge: NULL field/output %d", v);
+        a.fields[v] = fields[v];
+        a.out[v] = out[v];
+    }
+    a.delp = delp;
+    a.spacing = spacing;
+    a.n_fields = n_fields;
+    a.km = km;
+    a.n = nx;
+    a.f = factor;
+    a.iv = iv;
+    a.kord = kord;
+    a.edge = edge;
+    a.ptop = ptop_toa;
+    const int C = 64 / factor;
+    const int nc = nx / factor;
+    const int ncx = edge == 0 ? nc : nc + 1, ncy = edge == 0 ? nc + 1 : nc;
+    const int64_t blocks = (int64_t)6 * ncy * ((ncx + C - 1) / C);
+    const size_t lds = sizeof(DT) * (size_t)C * (km + 1);
+    hipLaunchKernelGGL(regrid_coarsen_edge_kernel<DT>, dim3((unsigned)blocks), dim3(64), lds, (hipStream_t)stream,
+                       a);
+    FV3_LAUNCH_CHECK();
+    return FV3_OK;
+}
+
+}  // namespace fv3
+
+extern "C" int fv3_regrid_coarsen_edge(const float* delp, const float* spacing, const float* const* fields,
+                                       float* const* out, int n_fields, int ntile, int km, int ny, int nx,
+                                       int factor, int edge, int iv, int kord, double ptop_toa, void* stream)
+{
+    return fv3::regrid_coarsen_edge_impl<float>(delp, spacing, fields, out, n_fields, ntile, km, ny, nx, factor,
+                                                edge, iv, kord, ptop_toa, stream);
+}
+
+extern "C" int fv3_regrid_coarsen_edge_f64(const double* delp, const float* spacing, const float* const* fields,
+                                           float* const* out, int n_fields, int ntile, int km, int ny, int nx,
+                                           int factor, int edge, int iv, int kord, double ptop_toa, void* stream)
+{
+    return fv3::regrid_coarsen_edge_impl<double>(delp, spacing, fields, out, n_fields, ntile, km, ny, nx, factor,
+                                                 edge, iv, kord, ptop_toa, stream);
+}
 
 extern "C" int fv3_regrid_coarsen(const float* delp, const float* area, const float* const* fields,
                                   float* const* out, int n_fields, float* delp_out, int ntile, int km, int ny,

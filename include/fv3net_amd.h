@@ -17,6 +17,9 @@
  *   fv3_regrid_coarsen    external/vcm/vcm/cubedsphere/regridz.py:25-55 + 115-161 fused with
  *                         external/vcm/vcm/cubedsphere/coarsen.py:183-218
  *                         (as orchestrated by coarsen_restarts.py:411-516, 840-887)
+ *   fv3_regrid_coarsen_edge  external/vcm/vcm/cubedsphere/regridz.py:58-112 + 115-161 fused with
+ *                         external/vcm/vcm/cubedsphere/coarsen.py:221-271 (D-grid u/v of
+ *                         coarsen_restarts.py:460-509)
  *   fv3_column_integral,  per-rank partial sums behind
  *   fv3_area_weighted_sums, workflows/prognostic_c48_run/runtime/metrics.py:18-55
  *   fv3_level_sums
@@ -145,6 +148,31 @@ int fv3_regrid_coarsen_f64(const double* delp, const float* area, const float* c
                            float* const* out, int n_fields, float* delp_out, int ntile, int km,
                            int ny, int nx, int factor, int iv, int kord, double ptop_toa,
                            void* stream);
+
+/* ---- edge-weighted (D-grid wind) pressure-level coarse-graining ------------------
+ * edge 0 ("x", u): fields and spacing (dx) on (y outer = ny+1, x center = nx); coarse
+ *   output (tile, km, ny/f + 1, nx/f), coarsened along x, every f-th outer row kept.
+ * edge 1 ("y", v): fields and spacing (dy) on (y center = ny, x outer = nx+1); coarse
+ *   output (tile, km, ny/f, nx/f + 1), coarsened along y, every f-th outer column kept.
+ * Per coarse edge, from its f fine edge points:
+ *   delp_e = 0.5*(delp on either side)  (xgcm interp with the cubed-sphere face
+ *            connections of cubedsphere/xgcm.py:7-34 for the tile-boundary edges)
+ *   delp_c = sum(spacing*delp_e)/sum(spacing)                (coarsen.py:221-271)
+ *   phalf_f = cumsum([ptop, delp_e]), phalf_c = cumsum([ptop, delp_c])
+ *   f_r = mappm(phalf_f, f, phalf_c, iv, kord); w = spacing if phalf_c[k+1] < phalf_f[km+1]
+ *   out = sum(f_r*w)/sum(w)
+ * All 6 tiles (ntile == 6), square tiles (ny == nx), an even number of coarse cells per
+ * side (the reference's block_upsample_like requires it), 4 <= km <= 128,
+ * 1 <= factor <= 8, kord <= 7.  delp (tile, km, n, n); fields/out host arrays of
+ * n_fields <= 32 device pointers.  Bit-exact to oracle/coarsen.py
+ * coarsen_edges_on_pressure. */
+int fv3_regrid_coarsen_edge(const float* delp, const float* spacing, const float* const* fields,
+                            float* const* out, int n_fields, int ntile, int km, int ny, int nx,
+                            int factor, int edge, int iv, int kord, double ptop_toa, void* stream);
+int fv3_regrid_coarsen_edge_f64(const double* delp, const float* spacing,
+                                const float* const* fields, float* const* out, int n_fields,
+                                int ntile, int km, int ny, int nx, int factor, int edge, int iv,
+                                int kord, double ptop_toa, void* stream);
 
 /* ---- per-column reductions for stepper diagnostics --------------------------------
  * out[c] = sum_k field[k][c] * delp[k][c] * scale  (vcm mass_integrate,

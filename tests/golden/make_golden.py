@@ -9,11 +9,13 @@ container, where /root/reference exists; the GPU box only reads the .npz files).
   data, external/vcm/tests/_coarsen_restarts_regression_tests/reference/
   pressure-level-without-agrid-winds-{fv_core.res,fv_tracer.res}.json (the
   values, not the files), for the masked-area-weighted pressure-level variables.
+* coarsen_edge_kat.npz — the same data's coarse D-grid winds u and v (the
+  edge-weighted pressure-level path, regridz.py:58-112).
   Inputs are regenerated in the tests exactly as external/synth does
   (np.random.seed(0); uniform(lo, hi, shape) per single-chunk variable,
   synth/core.py:63-67), so only the expected values are stored.
 
-Usage:  python tests/golden/make_golden.py
+Usage:  python tests/golden/make_golden.py [--edge-kat]
 """
 import json
 import os
@@ -101,10 +103,27 @@ def make_coarsen_kat():
     np.savez_compressed(os.path.join(HERE, "coarsen_kat.npz"), **out)
 
 
+def make_coarsen_edge_kat():
+    """coarsen_edge_kat.npz: the reference's coarse D-grid winds u (edge "x") and v
+    (edge "y") of the same regression data (regrid_to_edge_weighted_pressure path)."""
+    with open(os.path.join(REF_JSON, "pressure-level-without-agrid-winds-fv_core.res.json")) as f:
+        d = json.load(f)
+    out = {}
+    for name in ("u", "v"):
+        var = d["data_vars"][name]
+        out[f"fv_core.res/{name}"] = np.asarray(var["data"], dtype=np.float64)
+        out[f"fv_core.res/{name}/dims"] = np.array(var["dims"])
+    np.savez_compressed(os.path.join(HERE, "coarsen_edge_kat.npz"), **out)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["--edge-kat"]:  # JSON values only; no reference build needed
+        make_coarsen_edge_kat()
+        raise SystemExit(0)
     build()
     if not reference_available():
         raise SystemExit("reference mappm not built (needs /root/reference + flang)")
     make_mappm_golden()
     make_coarsen_kat()
+    make_coarsen_edge_kat()
     print("golden fixtures written to", HERE)

@@ -1,0 +1,211 @@
+"""Edge-weighted (D-grid u / v) pressure-level coarse-graining: the oracle pinned by
+the reference's own regression data and KATs, the HIP kernel checked bit-exactly
+against the oracle.
+
+Reference KAT: external/vcm/tests/test_coarsen_restarts.py:103-122 with
+_coarsen_restarts_regression_tests/reference/pressure-level-without-agrid-winds-fv_core.res.json
+(coarse u and v copied into tests/golden/coarsen_edge_kat.npz by
+tests/golden/make_golden.py --edge-kat).  Inputs are regenerated as external/synth
+does (np.random.seed(0) per single-chunk variable): delp ~ U(3,5) f8, u/v ~ U(-1000,1000)
+f8, dx/dy ~ U(0.5,1) f4 (grid-schema.json), C4 -> C2, 7 levels.  Tolerance: the
+reference test's xarray.testing.assert_allclose defaults (rtol 1e-5, atol 1e-8).
+edge_weighted_block_average KATs: external/vcm/tests/test_cubedsphere.py:239-262.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import coarsen as OC
+
+FACTOR = 2
+
+
+def _kat_inputs():
+    delp = OC.synth_uniform(3, 5, (6, 1, 7, 4, 4), np.float64)[:, 0]
+    u = OC.synth_uniform(-1000, 1000, (6, 1, 7, 5, 4), np.float64)[:, 0]
+    v = OC.synth_uniform(-1000, 1000, (6, 1, 7, 4, 5), np.float64)[:, 0]
+    dx = OC.synth_uniform(0.5, 1, (6, 5, 4), np.float32)
+    dy = OC.synth_uniform(0.5, 1, (6, 4, 5), np.float32)
+    return delp, u, v, dx, dy
+
+
+def _expected(name):
+    return np.load(os.path.join(GOLDEN, "coarsen_edge_kat.npz"))[f"fv_core.res/{name}"][:, 0]
+
+
+def test_oracle_reproduces_reference_u_v():
+    delp, u, v, dx, dy = _kat_inputs()
+    (uc,) = OC.coarsen_edges_on_pressure(delp, dx, [u], FACTOR, "x")
+    (vc,) = OC.coarsen_edges_on_pressure(delp, dy, [v], FACTOR, "y")
+    assert uc.shape == (6, 7, 3, 2) and vc.shape == (6, 7, 2, 3)
+    assert uc.dtype == np.float32  # the mappm output dtype survives the averages
+    np.testing.assert_allclose(uc, _expected("u"), rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(vc, _expected("v"), rtol=1e-5, atol=1e-8)
+
+
+def test_face_halo_orientation_is_pinned(monkeypatch):
+    """A rotated neighbour face (connecting axis differs) contributes its edge line in
+    reversed tangential order: keeping the order misses tile-boundary edges only
+    (coarse u rows / v columns on a tile side; interior lines never use a halo)."""
+    delp, u, v, dx, dy = _kat_inputs()
+
+    def kept_order(a, axis, side):
+        out = []
+        for t in range(a.shape[0]):
+            nb, nax, _ = OC.FV3_FACE_CONNECTIONS[t][axis][side]
+            src = a[nb]
+            if nax == "y":
+                out.append(src[:, -1, :] if side == 0 else src[:, 0, :])
+            else:
+                out.append(src[:, :, -1] if side == 0 else src[:, :, 0])
+        return np.stack(out)
+
+    monkeypatch.setattr(OC, "face_halo", kept_order)
+    (uc,) = OC.coarsen_edges_on_pressure(delp, dx, [u], FACTOR, "x")
+    (vc,) = OC.coarsen_edges_on_pressure(delp, dy, [v], FACTOR, "y")
+    bad_u = ~np.isclose(uc, _expected("u"), rtol=1e-5, atol=1e-8)
+    bad_v = ~np.isclose(vc, _expected("v"), rtol=1e-5, atol=1e-8)
+    assert bad_u.any() and bad_v.any()
+    assert not bad_u[:, :, 1:-1].any() and not bad_v[:, :, :, 1:-1].any()
+
+
+def test_interp_to_outer_interior_and_halo():
+    """Interior edges average their two cells; boundary edges take the connected face."""
+    rng = np.random.default_rng(0)
+    a = rng.uniform(1, 2, (6, 3, 4, 4))
+    y = OC.interp_to_outer(a, "y")
+    x = OC.interp_to_outer(a, "x")
+    assert y.shape == (6, 3, 5, 4) and x.shape == (6, 3, 4, 5)
+    np.testing.assert_array_equal(y[:, :, 1:-1], 0.5 * (a[:, :, :-1] + a[:, :, 1:]))
+    np.testing.assert_array_equal(x[:, :, :, 1:-1], 0.5 * (a[:, :, :, :-1] + a[:, :, :, 1:]))
+    # tile 0, y: left neighbour tile 5 along its y axis (same order): its last row
+    np.testing.assert_array_equal(y[0, :, 0], 0.5 * (a[5, :, -1, :] + a[0, :, 0, :]))
+    # tile 0, y: right neighbour tile 2 along its x axis (rotated): its first column reversed
+    np.testing.assert_array_equal(y[0, :, -1], 0.5 * (a[0, :, -1, :] + a[2, :, ::-1, 0]))
+    # every tile-boundary edge is shared by two tiles: both sides compute the same value
+    np.testing.assert_array_equal(y[0, :, -1], x[2, :, ::-1, 0])
+
+
+@pytest.mark.parametrize(
+    ("data", "spacing", "factor", "edge", "expected_data"),
+    [
+        ([[2, 6, 2], [6, 2, 6]], [[6, 2, 6], [2, 6, 2]], 2, "x", [[3.0, 3.0]]),
+        ([[2, 6], [6, 2], [2, 6]], [[6, 2], [2, 6], [6, 2]], 2, "y", [[3.0], [3.0]]),
+    ],
+)
+def test_edge_weighted_block_average_kat(data, spacing, factor, edge, expected_data):
+    """test_cubedsphere.py:239-262, with the reference's (x_dim, y_dim) array order
+    transposed into this module's (y, x) order."""
+    d = np.asarray(data, float).T
+    s = np.asarray(spacing, float).T
+    got = OC.edge_weighted_block_average(d, s, factor, edge)
+    np.testing.assert_array_equal(got, np.asarray(expected_data).T)
+
+
+def test_block_upsample_staggered():
+    """coarsen.py:843-866: the outer axis repeats all but its last point."""
+    c = np.arange(6.0).reshape(1, 1, 3, 2)  # edge "x": (y outer 3, x center 2)
+    up = OC.block_upsample_staggered(c, 2, "x")
+    assert up.shape == (1, 1, 5, 4)
+    np.testing.assert_array_equal(up[0, 0, :, 0], [0, 0, 2, 2, 4])
+    np.testing.assert_array_equal(up[0, 0, 0], [0, 0, 1, 1])
+
+
+# ---------------------------------------------------------------------------------
+# the HIP kernel
+# ---------------------------------------------------------------------------------
+
+
+def _bits_equal(a, b):
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    assert a.shape == b.shape
+    bad = (a.view(np.uint32) != b.view(np.uint32)) & ~(np.isnan(a) & np.isnan(b))
+    assert not bad.any(), f"{bad.sum()} / {bad.size} differ, e.g. {a[bad][:4]} vs {b[bad][:4]}"
+
+
+@pytest.mark.gpu
+def test_kernel_reproduces_reference_u_v(gpu):
+    from fv3net_amd.coarsen import coarsen_edges_on_pressure
+
+    delp, u, v, dx, dy = _kat_inputs()
+    ou = coarsen_edges_on_pressure(delp, dx, {"u": u}, FACTOR, "x")["u"].cpu().numpy()
+    ov = coarsen_edges_on_pressure(delp, dy, {"v": v}, FACTOR, "y")["v"].cpu().numpy()
+    np.testing.assert_allclose(ou, _expected("u"), rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(ov, _expected("v"), rtol=1e-5, atol=1e-8)
+    (ru,) = OC.coarsen_edges_on_pressure(delp, dx, [u], FACTOR, "x")
+    (rv,) = OC.coarsen_edges_on_pressure(delp, dy, [v], FACTOR, "y")
+    _bits_equal(ou, ru)
+    _bits_equal(ov, rv)
+
+
+def _winds_state(rng, km, n, dtype):
+    base = np.linspace(200, 1800, km)[None, :, None, None]
+    delp = (base * rng.uniform(0.95, 1.05, (6, km, n, n))).astype(dtype)
+    u = (20 * np.sin(np.arange(km) / 8.0)[None, :, None, None] + rng.normal(0, 3, (6, km, n + 1, n)))
+    v = (10 * np.cos(np.arange(km) / 8.0)[None, :, None, None] + rng.normal(0, 3, (6, km, n, n + 1)))
+    dx = rng.uniform(0.5, 1.0, (6, n + 1, n)).astype(np.float32)
+    dy = rng.uniform(0.5, 1.0, (6, n, n + 1)).astype(np.float32)
+    return delp, u.astype(np.float32), v.astype(np.float32), dx, dy
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("factor,n", [(1, 4), (2, 16), (3, 12), (4, 24), (8, 48)])
+def test_kernel_vs_oracle_random(gpu, factor, n, dtype):
+    """Bit-identical to the oracle for both edges, every factor (numpy's order:
+    pairwise along x, sequential along y) and both delp dtypes."""
+    from fv3net_amd.coarsen import coarsen_edges_on_pressure
+
+    rng = np.random.default_rng(factor * 10 + n)
+    delp, u, v, dx, dy = _winds_state(rng, 40, n, dtype)
+    ou = coarsen_edges_on_pressure(delp, dx, {"u": u, "u2": u * 2}, factor, "x")
+    ov = coarsen_edges_on_pressure(delp, dy, {"v": v}, factor, "y")
+    ru, ru2 = OC.coarsen_edges_on_pressure(delp, dx, [u, u * 2], factor, "x")
+    (rv,) = OC.coarsen_edges_on_pressure(delp, dy, [v], factor, "y")
+    _bits_equal(ou["u"].cpu().numpy(), ru)
+    _bits_equal(ou["u2"].cpu().numpy(), ru2)
+    _bits_equal(ov["v"].cpu().numpy(), rv)
+
+
+@pytest.mark.gpu
+def test_kernel_masked_levels_kord_and_errors(gpu):
+    from fv3net_amd.coarsen import coarsen_edges_on_pressure
+
+    rng = np.random.default_rng(3)
+    delp, u, v, dx, dy = _winds_state(rng, 30, 16, np.float64)
+    delp[:, -4:] *= rng.uniform(0.2, 3.0, (6, 1, 16, 16))  # the mask drops fine edges low down
+    for iv, kord in ((1, 1), (0, 4), (1, 6), (-1, 7)):
+        o = coarsen_edges_on_pressure(delp, dy, {"v": v}, 4, "y", iv=iv, kord=kord)["v"].cpu().numpy()
+        (r,) = OC.coarsen_edges_on_pressure(delp, dy, [v], 4, "y", iv=iv, kord=kord)
+        _bits_equal(o, r)
+    with pytest.raises(NotImplementedError):
+        coarsen_edges_on_pressure(delp, dx, {"u": u}, 4, "x", kord=9)
+    with pytest.raises(ValueError):
+        coarsen_edges_on_pressure(delp, dx, {"u": u}, 4, "z")
+    with pytest.raises(ValueError):  # dx on the wrong grid
+        coarsen_edges_on_pressure(delp, dy, {"u": u}, 4, "x")
+    with pytest.raises(ValueError):  # odd number of coarse cells: unsupported by the reference
+        coarsen_edges_on_pressure(delp[..., :12, :12], dx[:, :13, :12], {"u": u[:, :, :13, :12]}, 4, "x")
+
+
+@pytest.mark.gpu
+def test_kernel_c384_to_c48_sampled_and_deterministic(gpu):
+    """Config #3 size for the winds: C384 -> C48, f = 8, 79 levels; deterministic, and
+    a tile matches the oracle (the oracle needs all 6 tiles for the halos, so it runs
+    on a C48 -> C6 proxy of the same code path and the C384 run is checked for
+    run-to-run identity and finiteness)."""
+    import torch
+
+    from fv3net_amd.coarsen import coarsen_edges_on_pressure
+
+    rng = np.random.default_rng(384)
+    delp, u, v, dx, dy = _winds_state(rng, 79, 384, np.float32)
+    a = coarsen_edges_on_pressure(delp, dx, {"u": u}, 8, "x")["u"]
+    b = coarsen_edges_on_pressure(delp, dx, {"u": u}, 8, "x")["u"]
+    torch.cuda.synchronize()
+    a, b = a.cpu().numpy(), b.cpu().numpy()
+    assert a.shape == (6, 79, 49, 48)
+    assert (a.view(np.uint32) == b.view(np.uint32)).all()
+    assert np.isfinite(a).all()
