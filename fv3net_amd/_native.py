@@ -31,6 +31,9 @@ EXPORTED_SYMBOLS = (
     "fv3_regrid_coarsen_f64",
     "fv3_regrid_coarsen_edge",
     "fv3_regrid_coarsen_edge_f64",
+    "fv3_interpolate_2d",
+    "fv3_interpolate_levels",
+    "fv3_pressure_midpoint_log",
     "fv3_column_integral",
     "fv3_area_weighted_sums",
     "fv3_level_sums",
@@ -120,6 +123,9 @@ _SIGNATURES = {
                                      _I, _I, _I, _I, _D, _P]),
     "fv3_regrid_coarsen_edge_f64": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _I, _I, _I, _I,
                                          _I, _I, _I, _I, _D, _P]),
+    "fv3_interpolate_2d": (_I, [_P, _I64, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _I, _D, _P]),
+    "fv3_interpolate_levels": (_I, [_P, _I64, _P, _I64, _I, _P, _I, _I, _P, _I64, _I64, _I, _D, _P]),
+    "fv3_pressure_midpoint_log": (_I, [_P, _I, _I64, _P, _I64, _I64, _I, _D, _P]),
     "fv3_column_integral": (_I, [_P, Layout, _P, Layout, _P, _I64, _I, _D, _P]),
     "fv3_area_weighted_sums": (_I, [ctypes.POINTER(_P), _I, _P, _I64, _P, _P]),
     "fv3_level_sums": (_I, [_P, Layout, _I64, _I, _P, _P]),

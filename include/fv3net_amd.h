@@ -20,6 +20,11 @@
  *   fv3_regrid_coarsen_edge  external/vcm/vcm/cubedsphere/regridz.py:58-112 + 115-161 fused with
  *                         external/vcm/vcm/cubedsphere/coarsen.py:221-271 (D-grid u/v of
  *                         coarsen_restarts.py:460-509)
+ *   fv3_interpolate_2d    external/mappm/mappm/interpolate_2d.f90:1-27 (f2py
+ *                         mappm.interpolate_2d, vcm/interpolate.py:176-180)
+ *   fv3_interpolate_levels  metpy.interpolate.interpolate_1d as called by
+ *                         vcm/interpolate.py:148-173 (shared output levels)
+ *   fv3_pressure_midpoint_log  vcm/calc/thermo/vertically_dependent.py:153-178
  *   fv3_column_integral,  per-rank partial sums behind
  *   fv3_area_weighted_sums, workflows/prognostic_c48_run/runtime/metrics.py:18-55
  *   fv3_level_sums
@@ -225,6 +230,34 @@ typedef struct {
 
 int fv3_ml_epilogue(const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, int nz, int state_f64,
                     double dt, int mse_conserving, int hydrostatic, void* stream);
+
+/* ---- vertical interpolation to new levels ------------------------------------------
+ * Every array is level-major: element (level k, column c) at [k * ld + c].  One thread
+ * per column; enqueued on `stream`.
+ *
+ * interpolate_2d.f90 semantics, float64: out = fill_value, then for each output level the
+ * LAST interval k (k = 0..n_in-2) with x_k <= xp < x_k+1 (linear, y_k (1-w) + y_k+1 w,
+ * w = (xp - x_k)/(x_k+1 - x_k)), x_k == xp (y_k) or x_k+1 == xp (y_k+1) decides.  xp has
+ * n_out levels per column (ld_xp = 0 broadcasts one level set).  Bit-exact to the
+ * Fortran. */
+int fv3_interpolate_2d(const double* xp, int64_t ld_xp, const double* x, int64_t ld_x,
+                       const double* y, int64_t ld_y, double* out, int64_t ld_out, int64_t ncol,
+                       int n_in, int n_out, double fill_value, void* stream);
+
+/* metpy.interpolate.interpolate_1d for output `levels` shared by all columns (float64,
+ * sorted ascending; reverse != 0 writes level j to n_out-1-j, as metpy does for
+ * descending requests).  xp (column coordinate, ascending) and var with their level
+ * strides; dtypes = xp_is_f64 | var_is_f64 << 1 (else float32); out float64.
+ * Values outside [xp_0, xp_n-1] get fill_value.  numpy's promotion: each difference of
+ * column values in its own dtype, the rest in float64. */
+int fv3_interpolate_levels(const void* xp, int64_t ld_xp, const void* var, int64_t ld_v, int dtypes,
+                           const double* levels, int n_out, int reverse, double* out,
+                           int64_t ld_out, int64_t ncol, int n_in, double fill_value, void* stream);
+
+/* pressure_at_midpoint_log: pi = cumsum([ptop, delp]); out = delp / diff(log(pi)), in
+ * delp's dtype (0 float32, 1 float64). */
+int fv3_pressure_midpoint_log(const void* delp, int dtype, int64_t ld_in, void* out, int64_t ld_out,
+                              int64_t ncol, int nz, double ptop, void* stream);
 
 #ifdef __cplusplus
 }
