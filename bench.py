@@ -49,18 +49,30 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--settle-ms", type=float, default=300.0,
+                   help="untimed clock-settle phase before the W warmup steps (see timed_steps)")
     return p.parse_args()
 
 
-def timed_steps(step, steps, warmup, dist=None):
-    """W untimed steps, then exactly K timed steps bracketed by barrier + sync.
-    Returns (wall seconds, mean seconds per launch).  The launch time comes from two
-    HIP events recorded on the stream the kernels run on (torch's current stream,
+def timed_steps(step, steps, warmup, dist=None, settle_ms=0.0):
+    """Clock settle, W untimed steps, then exactly K timed steps bracketed by barrier +
+    sync.  Returns (wall seconds, mean seconds per launch).  The launch time comes from
+    two HIP events recorded on the stream the kernels run on (torch's current stream,
     which the product passes to every launch) around the K back-to-back launches:
     each step is exactly one kernel, so span / K is its average duration.  Events per
-    launch would add ~6 us of queue overhead per step to the wall clock."""
+    launch would add ~6 us of queue overhead per step to the wall clock.
+
+    Settle: the same step runs untimed for ``settle_ms`` of wall time first.  The
+    MI355X shader clock ramps over ~100 ms of sustained load: a C48 launch measured
+    after 20 launches runs at ~2.13 GHz, after 3,000 at ~2.38 GHz (52.9 vs 47.3 us,
+    tools/dense_trace.py), so without it a short K times the ramp, not the kernel."""
     import torch
 
+    t_end = time.perf_counter() + settle_ms * 1e-3
+    while settle_ms > 0 and time.perf_counter() < t_end:
+        for _ in range(100):
+            step()
+        torch.cuda.synchronize()
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
@@ -129,7 +141,7 @@ def cpu_baseline(wl, seconds):
     }
 
 
-def extra_measurements(dev):
+def extra_measurements(dev, settle_ms=150.0):
     import torch
 
     from fv3net_amd import workloads as W
@@ -137,7 +149,7 @@ def extra_measurements(dev):
     out = {}
     # config #2 at C384 (one GPU, 884,736 columns): MFMA-bound predict
     wl = W.make_dense_workload(384, seed=3, device=dev)
-    wall, t = timed_steps(wl.step, 10, 3)
+    wall, t = timed_steps(wl.step, 10, 3, settle_ms=settle_ms)
     out["dense_c384"] = {
         "columns_per_s": wl.ncol / t, "ms_per_step": t * 1e3,
         "tflops": wl.ncol * wl.flops_per_column / t / 1e12,
@@ -149,7 +161,7 @@ def extra_measurements(dev):
                                  ("mappm_c384_79to79_kord10", W.c_columns(384), 79, 10),
                                  ("mappm_c12_79to50_kord1", W.c_columns(12), 50, 1)):
         wl = W.make_mappm_workload(ncol, 79, kn, kord, seed=5, device=dev)
-        wall, t = timed_steps(wl.step, 10, 3)
+        wall, t = timed_steps(wl.step, 10, 3, settle_ms=settle_ms)
         gbs = wl.bytes_per_column * ncol / t / 1e9
         out[name] = {"columns_per_s": ncol / t, "ms_per_step": t * 1e3, "hbm_gbs": gbs,
                      "frac_hbm_peak": gbs / W.HBM_PEAK_GBS}
@@ -157,13 +169,13 @@ def extra_measurements(dev):
     # config #4: one ML-stepper step (predict + fused limiter/diagnostics/apply + global
     # means) on a float64 C96 state, one GPU
     wl = W.make_stepper_workload(96, seed=11, device=dev)
-    wall, t = timed_steps(wl.step, 20, 3)
+    wall, t = timed_steps(wl.step, 20, 3, settle_ms=settle_ms)
     out["stepper_c96"] = {"columns_per_s": wl.ncol / (wall / 20), "ms_per_step": wall / 20 * 1e3,
                           "note": "wall clock per step (several kernels + host glue)"}
     del wl
     # config #5: Zhao-Carr microphysics emulator on a C384 state (float32 MFMA path)
     wl = W.make_emulator_workload(384, seed=13, device=dev)
-    wall, t = timed_steps(wl.step, 10, 3)
+    wall, t = timed_steps(wl.step, 10, 3, settle_ms=settle_ms)
     out["emulator_c384"] = {"columns_per_s": wl.ncol / t, "ms_per_step": t * 1e3,
                             "tflops": wl.ncol * wl.flops_per_column / t / 1e12,
                             "frac_f32_mfma_peak": wl.ncol * wl.flops_per_column / t / 1e12 / W.FP32_MFMA_PEAK_TFLOPS,
@@ -172,7 +184,7 @@ def extra_measurements(dev):
     # config #3: fused C384 -> C48 pressure-level coarsen (1 and 4 fields), fine columns/s
     for nf in (1, 4):
         wl = W.make_coarsen_workload(384, 8, nf, seed=7, device=dev)
-        wall, t = timed_steps(wl.step, 10, 3)
+        wall, t = timed_steps(wl.step, 10, 3, settle_ms=settle_ms)
         gbs = wl.bytes_per_column * wl.ncol_fine / t / 1e9
         out[f"coarsen_c384_to_c48_{nf}field"] = {
             "fine_columns_per_s": wl.ncol_fine / t, "ms_per_step": t * 1e3, "hbm_gbs": gbs,
@@ -202,7 +214,7 @@ def main():
     from fv3net_amd import workloads as W
 
     wl = W.make_dense_workload(args.res, seed=1000 + rank, device=dev)
-    wall, kmean = timed_steps(wl.step, args.steps, args.warmup, dist)
+    wall, kmean = timed_steps(wl.step, args.steps, args.warmup, dist, settle_ms=args.settle_ms)
     if dist is not None:
         t = torch.tensor([wall], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -219,6 +231,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "settle_ms": args.settle_ms,
         "ms_per_step": wall / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
@@ -256,7 +269,7 @@ def main():
         del wl
         torch.cuda.empty_cache()
         try:
-            result["extra"] = extra_measurements(dev)
+            result["extra"] = extra_measurements(dev, settle_ms=min(args.settle_ms, 150.0))
         except Exception as e:
             log("extra measurements failed:", repr(e))
     if rank == 0:

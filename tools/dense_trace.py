@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fv3net_amd import _native, workloads as W  # noqa: E402
 
 
-def run(res, nc, wpe=2):
+def run(res, nc, wpe=2, warm=20):
     os.environ["FV3_DENSE_NC"] = str(nc)
     os.environ["FV3_DENSE_WPE"] = str(wpe)
     dev = torch.device("cuda", 0)
@@ -23,7 +23,7 @@ def run(res, nc, wpe=2):
     nblk = (wl.ncol + 16 * nc - 1) // (16 * nc)
     buf = torch.zeros(nblk * 8, dtype=torch.int64, device=dev)
     lib = _native.load()
-    for _ in range(20):
+    for _ in range(warm):
         wl.step()
     _native.check(lib.fv3_dense_set_trace(wl.model.handle(), buf.data_ptr()))
     wl.step()
@@ -86,11 +86,14 @@ def main():
     ap.add_argument("--res", type=int, nargs="+", default=[48, 384])
     ap.add_argument("--nc", type=int, nargs="+", default=[2, 1])
     ap.add_argument("--wpe", type=int, nargs="+", default=[2, 3])
+    ap.add_argument("--warm", type=int, nargs="+", default=[20], help="launches before the traced one")
     a = ap.parse_args()
     for res in a.res:
         for nc in a.nc:
             for wpe in a.wpe:
-                run(res, nc, wpe)
+                for warm in a.warm:
+                    print(f"-- after {warm} launches")
+                    run(res, nc, wpe, warm)
 
 
 if __name__ == "__main__":
