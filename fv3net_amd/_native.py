@@ -26,6 +26,7 @@ EXPORTED_SYMBOLS = (
     "fv3_dense_k_in",
     "fv3_dense_k_out",
     "fv3_dense_forward",
+    "fv3_dense_forward_ex",
     "fv3_dense_set_trace",
     "fv3_regrid_coarsen",
     "fv3_regrid_coarsen_f64",
@@ -39,7 +40,11 @@ EXPORTED_SYMBOLS = (
     "fv3_level_sums",
     "fv3_ml_epilogue",
 )
-ABI_VERSION = 2
+ABI_VERSION = 3
+
+# fv3_dense_forward_ex precisions
+DENSE_F32 = 0
+DENSE_BF16X3 = 1
 
 
 class NativeLibraryError(RuntimeError):
@@ -115,6 +120,8 @@ _SIGNATURES = {
     "fv3_dense_k_out": (_I, [_P]),
     "fv3_dense_forward": (_I, [_P, ctypes.POINTER(_P), ctypes.POINTER(Layout), ctypes.POINTER(_P),
                                ctypes.POINTER(Layout), _I64, _P]),
+    "fv3_dense_forward_ex": (_I, [_P, ctypes.POINTER(_P), ctypes.POINTER(Layout), ctypes.POINTER(_P),
+                                  ctypes.POINTER(Layout), _I64, _I, _P]),
     "fv3_regrid_coarsen": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _P, _I, _I, _I,
                                 _I, _I, _I, _I, _D, _P]),
     "fv3_regrid_coarsen_f64": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _P, _I, _I, _I,

@@ -1,0 +1,659 @@
+// fv3net_amd — fused column-wise dense predict on bf16 MFMA with a 3-term split ("bf16x3").
+//
+// Same graph and boundary as dense.hip (the DenseModel of external/fv3fit/fv3fit/keras/
+// _models/dense.py:234-305 and the microphysics emulator's MLP, external/fv3fit/fv3fit/
+// emulation/layers/architecture.py:228-345): inputs read in place from [level][column]
+// arrays, LogTransform / StandardNorm, n x Dense(relu), one linear Dense per output,
+// de-normalisation, OutputLimit, zero mask, residual outputs, written in place.
+//
+// Arithmetic: every f32 operand x is split into bf16 hi = rne(x) and lo = rne(x - hi),
+// and a product a*b is taken as hi_a*hi_b + lo_a*hi_b + hi_a*lo_b on
+// v_mfma_f32_32x32x16_bf16 (f32 accumulate).  That keeps ~16 mantissa bits of each
+// operand: measured 8e-6 rel on the 2x256 DenseModel and 9e-6 on the Zhao-Carr emulator
+// against the float64 graph (plain bf16: 4.7e-3, outside BASELINE config #5's 1e-3).
+// Three bf16 MFMAs cost 48 cycles per 16x32x32 block against 512 for exact f32
+// (v_mfma_f32_32x32x2_f32), i.e. ~5.3x the f32 MFMA rate.
+//
+// Mapping (one 256-thread block per CU, 1 wave per SIMD, persistent over column tiles):
+//  * a block tile is 128 columns; wave w owns columns [32w, 32w+32) for the WHOLE network,
+//    so activations never leave registers: the 32x32 accumulator of a layer (units on
+//    the 16 registers, column on the lane) is, after bias + relu + split, exactly the
+//    B operand of the next layer's 32x32x16 MFMA (k order permuted; the packed weights
+//    carry the permutation);
+//  * weights stream through LDS in 32 KiB chunks (2 k-steps x all unit tiles x hi/lo,
+//    MFMA A-fragment order, one ds_read_b128 per fragment), double-buffered: the chunk
+//    after next is loaded into registers while the current one runs (one barrier per
+//    chunk); the 4 waves share every chunk, so L2 traffic is 1/128 of a weight per column;
+//  * layer-1 inputs are loaded straight into the B-fragment layout (lane = column,
+//    8 consecutive levels per lane: 128-B coalesced rows), two chunks ahead, then
+//    log / normalised / split in registers: no LDS staging of inputs at all;
+//  * the output layer runs in passes of HT 32-row tiles over the packed output rows;
+//    the epilogue (bias, denorm, limits, mask, residual) reads per-row constants and
+//    destination addresses from LDS.
+// Roofline: bf16 MFMA (3 products per f32 product) — see DESIGN.md §3.5.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+#include "common.h"
+#include "dense_model.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float b3f16 __attribute__((ext_vector_type(16)));
+typedef float b3f4 __attribute__((ext_vector_type(4)));
+
+namespace fv3 {
+
+constexpr int kB3Groups = 128;  // 8-feature input groups (<= 1024 padded input features)
+constexpr int kB3Cols = 128;    // columns per block tile: 4 waves x 32
+
+struct B3Pack {
+    void* dbuf = nullptr;
+    int ht = 0, hp = 0, kp1 = 0, n1 = 0, nhx = 0, npass = 0, n_otile = 0, kop = 0, nch = 0;
+    int nconst = 0, wbytes = 0, any_log = 0;
+    std::vector<int> gmeta;  // per 8-feature group: var | zstart << 4 | nvalid << 24
+    size_t consts_off = 0;
+};
+
+namespace {
+
+struct B3InVar {
+    const float* ptr;
+    int64_t ld, bs;
+    float leps;  // > 0: LogTransform log(max(x, leps))
+    int pad_;
+};
+
+struct B3Args {
+    const void* wstream;  // [nch][CB]: the packed weight chunks of one column tile
+    const float* consts;  // [kp1] mean | [kp1] 1/(sigma+eps) | [nh][HP] bias | [6][kop] | [kop] int var|z<<8
+    int wbytes;
+    int nch, n1, nhx, npass, n_otile, kp1, kop, nconst, any_log;
+    int64_t ncol, ncol_blk, ntiles;
+    B3InVar in[kMaxVars];
+    int gmeta[kB3Groups];
+    float* out_ptr[kMaxVars];
+    int64_t out_ld[kMaxVars], out_bs[kMaxVars];
+    const float* res_ptr[kMaxVars];
+    int64_t res_ld[kMaxVars], res_bs[kMaxVars];
+};
+static_assert(sizeof(B3Args) <= 4096, "kernel arguments are limited to 4 KiB");
+
+typedef __attribute__((address_space(4))) const B3Args KB3;
+typedef __amdgpu_buffer_rsrc_t Rsrc3;
+
+template <typename F, int... I>
+__device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, I...>)
+{
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void sfor(F&& f)
+{
+    sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// this wave's LDS writes done, then the workgroup barrier; global loads in flight (the
+// next weight chunk, the next inputs) are NOT drained (a __syncthreads() fence would
+// wait vmcnt(0) on gfx9, where loads and stores share the counter)
+__device__ __forceinline__ void b3_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ float b3_log(float x, float eps) { return x != x ? x : logf(x > eps ? x : eps); }
+
+// y -> bf16 hi = rne(y), lo = rne(y - hi)  (y - hi is exact in f32)
+__device__ __forceinline__ void split8(const float (&y)[8], bf16x8& hi, bf16x8& lo)
+{
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const __bf16 h = (__bf16)y[j];
+        hi[j] = h;
+        lo[j] = (__bf16)(y[j] - (float)h);
+    }
+}
+
+__device__ __forceinline__ b3f16 mma3(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl,
+                                      b3f16 c)
+{
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
+    return c;
+}
+
+template <int HT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void dense_b3_kernel(B3Args pa)
+{
+    (void)pa;
+    KB3& p = *(KB3*)(__builtin_amdgcn_kernarg_segment_ptr());
+    constexpr int HP = 32 * HT;
+    constexpr int CB = 4096 * HT;  // chunk: 2 k-steps x HT tiles x {hi, lo} x 64 lanes x 16 B
+    extern __shared__ __attribute__((aligned(16))) b3f4 lds3[];
+    char* ring = reinterpret_cast<char*>(lds3);
+    float* s_mean = reinterpret_cast<float*>(ring + 2 * CB);
+    float* s_rs = s_mean + p.kp1;
+    float* s_bias = s_rs + p.kp1;             // [nh][HP]
+    float* s_oc = s_bias + (1 + p.nhx) * HP;  // [6][kop]: bias, sigma, mean, lo, hi, mask
+    long long* s_row = reinterpret_cast<long long*>(s_oc + 6 * p.kop);  // [4][kop]
+    const int kop = p.kop;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int hh = lane >> 5;  // lane half: k offset 8*hh inside a 16-deep k-step
+    const int cl = lane & 31;  // column of this lane inside the wave's 32
+
+    // ---- constants and per-row destinations to LDS ----
+    for (int i = tid; i < p.nconst; i += 256) s_mean[i] = p.consts[i];
+    {
+        const int* vz = reinterpret_cast<const int*>(p.consts + p.nconst);
+        for (int R = tid; R < kop; R += 256) {
+            const int e = vz[R];
+            const int v = e & 0xff, z = e >> 8;
+            long long oa = 0, ob = 0, ra = 0, rb = 0;
+            if (v < kMaxVars) {
+                oa = (long long)(p.out_ptr[v] + (int64_t)z * p.out_ld[v]);
+                ob = p.out_bs[v];
+                if (p.res_ptr[v]) {
+                    ra = (long long)(p.res_ptr[v] + (int64_t)z * p.res_ld[v]);
+                    rb = p.res_bs[v];
+                }
+            }
+            s_row[R] = oa;
+            s_row[kop + R] = ob;
+            s_row[2 * kop + R] = ra;
+            s_row[3 * kop + R] = rb;
+        }
+    }
+
+    // ---- weight stream: LDS ring of 2 chunks, the chunk after next in registers ----
+    const Rsrc3 rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.wstream), 0, p.wbytes, 0x00020000);
+    b3f4 stg[HT];
+    auto load_stage = [&](int j) {
+#pragma unroll
+        for (int q = 0; q < HT; ++q)
+            stg[q] = __builtin_bit_cast(b3f4, __builtin_amdgcn_raw_buffer_load_b128(rw, tid * 16, j * CB + q * 4096, 0));
+    };
+    auto write_stage = [&](int slot) {
+#pragma unroll
+        for (int q = 0; q < HT; ++q) *reinterpret_cast<b3f4*>(ring + slot * CB + q * 4096 + tid * 16) = stg[q];
+    };
+    int slot = 0;                             // ring slot of the chunk computed next
+    int jn2 = p.nch > 2 ? 2 : 2 % p.nch;      // stream index of the chunk after next
+    load_stage(0);
+    write_stage(0);
+    load_stage(p.nch > 1 ? 1 : 0);
+
+    b3f16 acc[HT];
+    auto zero_acc = [&]() {
+#pragma unroll
+        for (int t = 0; t < HT; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    };
+    // one chunk: 2 k-steps x (tiles < nact) x 3 MFMAs, A fragments from the ring; the
+    // fragments of the next tile are read while this tile's MFMAs run (1 wave per SIMD:
+    // nothing else hides the LDS latency)
+    auto mma_chunk = [&](int sl, const bf16x8 (&bh)[2], const bf16x8 (&bl)[2], int nact) {
+        const char* base = ring + sl * CB + lane * 16;
+        bf16x8 fa[2][2];  // [buffer][hi, lo]
+        fa[0][0] = *reinterpret_cast<const bf16x8*>(base);
+        fa[0][1] = *reinterpret_cast<const bf16x8*>(base + 1024);
+        sfor<2 * HT>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;  // i = s * HT + t
+            constexpr int s = i / HT, t = i % HT;
+            if constexpr (i + 1 < 2 * HT) {
+                fa[(i + 1) & 1][0] = *reinterpret_cast<const bf16x8*>(base + (i + 1) * 2048);
+                fa[(i + 1) & 1][1] = *reinterpret_cast<const bf16x8*>(base + (i + 1) * 2048 + 1024);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (t < nact) acc[t] = mma3(fa[i & 1][0], fa[i & 1][1], bh[s], bl[s], acc[t]);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+    };
+    auto step = [&](const bf16x8 (&bh)[2], const bf16x8 (&bl)[2], int nact) {
+#ifndef FV3_B3_EXP_NOSTAGE  // experiment switches (tools/b3_ab.sh): timing only, results invalid
+        write_stage(slot ^ 1);  // chunk +1 (its slot held chunk -1, released by the last barrier)
+        load_stage(jn2);        // chunk +2
+#endif
+#ifndef FV3_B3_EXP_NOMFMA
+        mma_chunk(slot, bh, bl, nact);
+#endif
+#ifndef FV3_B3_EXP_NOBARRIER
+        b3_barrier();
+#endif
+        slot ^= 1;
+        jn2 = jn2 + 1 == p.nch ? 0 : jn2 + 1;
+    };
+
+    // ---- layer-1 inputs: B fragments straight from the [level][column] arrays ----
+    int64_t lblk = 0, lii = 0;  // column address of the tile being loaded
+    bool lvalid = false;
+    auto set_load_tile = [&](int64_t tile) {
+        const int64_t c = tile * kB3Cols + wave * 32 + cl;
+        lvalid = c < p.ncol;
+        lii = lvalid ? c : 0;
+        lblk = 0;
+        if (p.ncol_blk < p.ncol) {
+            lblk = lii / p.ncol_blk;
+            lii -= lblk * p.ncol_blk;
+        }
+    };
+    auto load_in = [&](float (&raw)[16], int c) {  // chunk c: groups 4c + 2s + hh, 8 levels each
+        sfor<2>([&](auto sc) {
+            constexpr int s = decltype(sc)::value;
+            const int m0 = p.gmeta[4 * c + 2 * s], m1 = p.gmeta[4 * c + 2 * s + 1];
+            const int v0 = m0 & 15, v1 = m1 & 15;
+            const float* b0 = p.in[v0].ptr + (int64_t)((m0 >> 4) & 0xfffff) * p.in[v0].ld;
+            const float* b1 = p.in[v1].ptr + (int64_t)((m1 >> 4) & 0xfffff) * p.in[v1].ld;
+            const int64_t ld = hh ? p.in[v1].ld : p.in[v0].ld;
+            const int64_t bs = hh ? p.in[v1].bs : p.in[v0].bs;
+            const int nv = lvalid ? ((hh ? m1 : m0) >> 24) : 0;
+            const float* ptr = (hh ? b1 : b0) + lblk * bs + lii;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)  // read once: keep them from evicting the weight stream in L2
+#ifdef FV3_B3_EXP_NOINPUT
+                raw[8 * s + j] = (float)(j < nv);
+#else
+                raw[8 * s + j] = j < nv ? __builtin_nontemporal_load(ptr + j * ld) : 0.0f;
+#endif
+        });
+    };
+    auto stage_in = [&](const float (&raw)[16], int c, bf16x8 (&bh)[2], bf16x8 (&bl)[2]) {
+        sfor<2>([&](auto sc) {
+            constexpr int s = decltype(sc)::value;
+            const int f0 = 32 * c + 16 * s + 8 * hh;
+            const b3f4 mu0 = *reinterpret_cast<const b3f4*>(s_mean + f0);
+            const b3f4 mu1 = *reinterpret_cast<const b3f4*>(s_mean + f0 + 4);
+            const b3f4 rs0 = *reinterpret_cast<const b3f4*>(s_rs + f0);
+            const b3f4 rs1 = *reinterpret_cast<const b3f4*>(s_rs + f0 + 4);
+            float leps = 0.0f;
+            if (p.any_log) {
+                const float l0 = p.in[p.gmeta[4 * c + 2 * s] & 15].leps;
+                const float l1 = p.in[p.gmeta[4 * c + 2 * s + 1] & 15].leps;
+                leps = hh ? l1 : l0;
+            }
+            float y[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float x = raw[8 * s + j];
+                if (leps > 0.0f) x = b3_log(x, leps);  // LogTransform.forward (transforms.py:123-124)
+                y[j] = (x - (j < 4 ? mu0[j] : mu1[j - 4])) * (j < 4 ? rs0[j] : rs1[j - 4]);
+            }
+            split8(y, bh[s], bl[s]);
+        });
+    };
+
+    // ---- activations: B fragments of the next layer (unit 32t + 16s + 8(j>>2) + (j&3) + 4hh) ----
+    bf16x8 Bh[HT][2], Bl[HT][2];
+    auto hidden_epi = [&](int l) {  // relu(acc + bias_l) -> Bh/Bl
+        sfor<HT>([&](auto tc) {
+            constexpr int t = decltype(tc)::value;
+            sfor<2>([&](auto sc) {
+                constexpr int s = decltype(sc)::value;
+                float y[8];
+#pragma unroll
+                for (int g2 = 0; g2 < 2; ++g2) {
+                    const int g = 2 * s + g2;  // register group: registers 4g .. 4g+3
+                    const b3f4 b = *reinterpret_cast<const b3f4*>(s_bias + l * HP + 32 * t + 8 * g + 4 * hh);
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const float v = acc[t][4 * g + rr] + b[rr];
+                        y[4 * g2 + rr] = v > 0.0f ? v : 0.0f;
+                    }
+                }
+                split8(y, Bh[t][s], Bl[t][s]);
+            });
+        });
+    };
+    int64_t oblk = 0, oii = 0;
+    bool ovalid = false;
+    auto out_epi = [&](int pp, int nact) {
+        sfor<HT>([&](auto tc) {
+            constexpr int t = decltype(tc)::value;
+            if (t < nact) {
+                const int T = pp * HT + t;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    int R0 = 32 * T + 8 * g + 4 * hh;
+                    asm volatile("" : "+v"(R0));  // keep the constant reads next to their use
+                    const b3f4 bo = *reinterpret_cast<const b3f4*>(s_oc + R0);
+                    const b3f4 sg = *reinterpret_cast<const b3f4*>(s_oc + kop + R0);
+                    const b3f4 mu = *reinterpret_cast<const b3f4*>(s_oc + 2 * kop + R0);
+                    const b3f4 lo = *reinterpret_cast<const b3f4*>(s_oc + 3 * kop + R0);
+                    const b3f4 hi = *reinterpret_cast<const b3f4*>(s_oc + 4 * kop + R0);
+                    const b3f4 mk = *reinterpret_cast<const b3f4*>(s_oc + 5 * kop + R0);
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int R = R0 + rr;
+                        float y = acc[t][4 * g + rr] + bo[rr];
+                        y = y * sg[rr];
+                        y = y + mu[rr];
+                        if (y < lo[rr]) y = lo[rr];
+                        if (y >= hi[rr]) y = hi[rr];
+                        y = y * mk[rr];
+                        const long long oa = s_row[R];
+                        if (ovalid && oa) {
+                            const long long ra = s_row[2 * kop + R];
+                            if (ra)
+                                y = __builtin_nontemporal_load(reinterpret_cast<const float*>(ra) + oblk * s_row[3 * kop + R] +
+                                                               oii) + y;
+                            __builtin_nontemporal_store(y, reinterpret_cast<float*>(oa) + oblk * s_row[kop + R] + oii);
+                        }
+                    }
+                }
+            }
+        });
+    };
+
+    float rawA[16], rawB[16];
+    int64_t tile = blockIdx.x;
+    set_load_tile(tile);
+    if (tile < p.ntiles) {
+        load_in(rawA, 0);
+        if (p.n1 > 1) load_in(rawB, 1);
+    }
+    b3_barrier();  // constants, row table and chunk 0 visible
+
+    for (; tile < p.ntiles; tile += gridDim.x) {
+        oblk = lblk;
+        oii = lii;
+        ovalid = lvalid;
+        // ---- layer 1 over the padded input features ----
+        zero_acc();
+        for (int c = 0; c < p.n1; c += 2) {
+            bf16x8 xh[2], xl[2];
+            stage_in(rawA, c, xh, xl);
+            if (c + 2 < p.n1) load_in(rawA, c + 2);
+            step(xh, xl, HT);
+            if (c + 1 < p.n1) {
+                stage_in(rawB, c + 1, xh, xl);
+                if (c + 3 < p.n1) load_in(rawB, c + 3);
+                step(xh, xl, HT);
+            }
+        }
+        hidden_epi(0);
+        // ---- further hidden layers ----
+        for (int l = 0; l < p.nhx; ++l) {
+            zero_acc();
+            sfor<HT>([&](auto cc) {
+                constexpr int c = decltype(cc)::value;
+                step(Bh[c], Bl[c], HT);
+            });
+            hidden_epi(l + 1);
+        }
+        // ---- output layer in passes of HT tiles; the next tile's inputs start loading ----
+        const int64_t nt = tile + gridDim.x;
+        if (nt < p.ntiles) {
+            set_load_tile(nt);
+            load_in(rawA, 0);
+            if (p.n1 > 1) load_in(rawB, 1);
+        }
+        for (int pp = 0; pp < p.npass; ++pp) {
+            zero_acc();
+            const int nact = min(HT, p.n_otile - pp * HT);
+            sfor<HT>([&](auto cc) {
+                constexpr int c = decltype(cc)::value;
+                step(Bh[c], Bl[c], nact);
+            });
+            out_epi(pp, nact);
+        }
+    }
+}
+
+uint16_t bf16_rne(float f)
+{
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+float bf16_f(uint16_t h)
+{
+    const uint32_t u = (uint32_t)h << 16;
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------
+// host: pack the model once (fv3_dense_create) into the bf16x3 chunk stream
+// ------------------------------------------------------------------------------------
+int b3_pack(fv3_dense_model* m, const fv3_dense_desc* d)
+{
+    auto b = new B3Pack();
+    std::unique_ptr<B3Pack> guard(b);
+    const int W = d->width;
+    b->ht = W <= 64 ? 2 : (W <= 128 ? 4 : 8);
+    b->hp = 32 * b->ht;
+    const int HT = b->ht, HP = b->hp;
+
+    // input feature groups of 8 levels of one variable (chunk = 4 groups = 32 features)
+    std::vector<int> fsrc;  // padded feature -> kept feature index or -1
+    int kbase = 0;
+    for (int v = 0; v < m->n_in; ++v) {
+        const int nkeep = m->in_nkeep[v], z0 = m->in_z0[v];
+        FV3_REQUIRE(z0 + nkeep < (1 << 20), "dense_create: too many levels for the bf16x3 path");
+        for (int g0 = 0; g0 < nkeep; g0 += 8) {
+            const int nv = std::min(8, nkeep - g0);
+            b->gmeta.push_back(v | ((z0 + g0) << 4) | (nv << 24));
+            for (int j = 0; j < 8; ++j) fsrc.push_back(j < nv ? kbase + g0 + j : -1);
+        }
+        b->any_log |= m->in_log_eps[v] > 0.0f;
+        kbase += nkeep;
+    }
+    while (b->gmeta.size() % 4) {
+        b->gmeta.push_back(0);
+        for (int j = 0; j < 8; ++j) fsrc.push_back(-1);
+    }
+    FV3_REQUIRE((int)b->gmeta.size() <= kB3Groups, "dense_create: %d input features are too many for bf16x3",
+                (int)fsrc.size());
+    b->kp1 = (int)fsrc.size();
+    b->n1 = b->kp1 / 32;
+    b->nhx = d->n_hidden - 1;
+    b->n_otile = (m->k_out + 31) / 32;
+    b->kop = 32 * b->n_otile;
+    b->npass = (b->n_otile + HT - 1) / HT;
+    const int per_layer = HP / 32;
+    b->nch = b->n1 + b->nhx * per_layer + b->npass * per_layer;
+    const size_t cbe = (size_t)2048 * HT;  // bf16 elements per chunk
+    FV3_REQUIRE((size_t)b->nch * cbe * 2 < (1u << 31), "dense_create: model too large for the bf16x3 stream");
+
+    std::vector<uint16_t> ws((size_t)b->nch * cbe, 0);
+    auto put = [&](int chunk, int s, int t, int lane, int j, float v) {
+        const uint16_t hi = bf16_rne(v);
+        const uint16_t lo = bf16_rne(v - bf16_f(hi));
+        const size_t at = (size_t)chunk * cbe + ((size_t)((s * HT + t) * 2) * 64 + lane) * 8 + j;
+        ws[at] = hi;
+        ws[at + 512] = lo;
+    };
+    // layer 1: natural feature order, k = 32c + 16s + 8h + j
+    const float* K0 = d->hidden_kernel[0];
+    for (int c = 0; c < b->n1; ++c)
+        for (int s = 0; s < 2; ++s)
+            for (int t = 0; t < HT; ++t)
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int j = 0; j < 8; ++j) {
+                        const int f = 32 * c + 16 * s + 8 * (lane >> 5) + j;
+                        const int unit = 32 * t + (lane & 31);
+                        const int src = fsrc[f];
+                        put(c, s, t, lane, j, (src >= 0 && unit < W) ? K0[(size_t)src * W + unit] : 0.0f);
+                    }
+    // hidden and output layers: k-step (c, s), element j of lane half h contracts over the
+    // previous layer's unit 32c + 16s + 8(j>>2) + (j&3) + 4h (its accumulator layout)
+    auto in_unit = [](int c, int s, int lane, int j) { return 32 * c + 16 * s + 8 * (j >> 2) + (j & 3) + 4 * (lane >> 5); };
+    for (int li = 0; li < b->nhx; ++li) {
+        const float* K = d->hidden_kernel[li + 1];
+        for (int c = 0; c < per_layer; ++c)
+            for (int s = 0; s < 2; ++s)
+                for (int t = 0; t < HT; ++t)
+                    for (int lane = 0; lane < 64; ++lane)
+                        for (int j = 0; j < 8; ++j) {
+                            const int in = in_unit(c, s, lane, j), unit = 32 * t + (lane & 31);
+                            put(b->n1 + li * per_layer + c, s, t, lane, j,
+                                (in < W && unit < W) ? K[(size_t)in * W + unit] : 0.0f);
+                        }
+    }
+    std::vector<int> ocol_var(m->k_out), ocol_z(m->k_out);
+    for (int v = 0, o = 0; v < m->n_out; ++v)
+        for (int z = 0; z < m->out_nz[v]; ++z, ++o) {
+            ocol_var[o] = v;
+            ocol_z[o] = z;
+        }
+    for (int pp = 0; pp < b->npass; ++pp)
+        for (int c = 0; c < per_layer; ++c)
+            for (int s = 0; s < 2; ++s)
+                for (int t = 0; t < HT; ++t)
+                    for (int lane = 0; lane < 64; ++lane)
+                        for (int j = 0; j < 8; ++j) {
+                            const int in = in_unit(c, s, lane, j);
+                            const int R = 32 * (pp * HT + t) + (lane & 31);
+                            float v = 0.0f;
+                            if (in < W && R < m->k_out) {
+                                const int ov = ocol_var[R], oz = ocol_z[R];
+                                v = d->out_kernel[ov][(size_t)in * m->out_nz[ov] + oz];
+                            }
+                            put(b->n1 + b->nhx * per_layer + pp * per_layer + c, s, t, lane, j, v);
+                        }
+
+    // constants: [kp1] mean | [kp1] 1/(sigma+eps) | [nh][HP] bias | [6][kop] | [kop] int var|z<<8
+    const int nh = 1 + b->nhx, kop = b->kop;
+    b->nconst = 2 * b->kp1 + nh * HP + 6 * kop;
+    std::vector<float> cst((size_t)b->nconst + kop, 0.0f);
+    for (int f = 0; f < b->kp1; ++f) {
+        const int src = fsrc[f];
+        if (src < 0) continue;
+        cst[f] = d->in_mean[src];
+        volatile float den = d->in_sigma[src] + d->epsilon;  // StandardNormLayer: f32(sigma + eps)
+        cst[b->kp1 + f] = 1.0f / den;
+    }
+    for (int l = 0; l < nh; ++l)
+        for (int u = 0; u < W; ++u) cst[2 * b->kp1 + l * HP + u] = d->hidden_bias[l][u];
+    float* oc = cst.data() + 2 * b->kp1 + nh * HP;
+    int* vz = reinterpret_cast<int*>(cst.data() + b->nconst);
+    for (int R = 0; R < kop; ++R) {
+        float v[6] = {0.0f, 1.0f, 0.0f, -INFINITY, INFINITY, 1.0f};
+        int e = 255;
+        if (R < m->k_out) {
+            const int ov = ocol_var[R], oz = ocol_z[R];
+            v[0] = d->out_bias[ov][oz];
+            v[1] = d->out_sigma[R];
+            v[2] = d->out_mean[R];
+            if (d->out_min) v[3] = d->out_min[R];
+            if (d->out_max) v[4] = d->out_max[R];
+            if (d->out_mask) v[5] = d->out_mask[R];
+            e = ov | (oz << 8);
+        }
+        for (int k = 0; k < 6; ++k) oc[(size_t)k * kop + R] = v[k];
+        vz[R] = e;
+    }
+
+    b->wbytes = (int)(ws.size() * 2);
+    b->consts_off = ((size_t)b->wbytes + 255) / 256 * 256;
+    FV3_HIP(hipMalloc(&b->dbuf, b->consts_off + cst.size() * 4));
+    FV3_HIP(hipMemcpy(b->dbuf, ws.data(), ws.size() * 2, hipMemcpyHostToDevice));
+    FV3_HIP(hipMemcpy((char*)b->dbuf + b->consts_off, cst.data(), cst.size() * 4, hipMemcpyHostToDevice));
+    m->b3 = guard.release();
+    return FV3_OK;
+}
+
+void b3_free(fv3_dense_model* m)
+{
+    if (!m || !m->b3) return;
+    if (m->b3->dbuf) (void)hipFree(m->b3->dbuf);
+    delete m->b3;
+    m->b3 = nullptr;
+}
+
+}  // namespace fv3
+
+extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const* inputs, const fv3_layout* in_l,
+                                    float* const* outputs, const fv3_layout* out_l, int64_t ncol, int precision,
+                                    void* stream)
+{
+    using namespace fv3;
+    if (precision == FV3_DENSE_F32) return fv3_dense_forward(m, inputs, in_l, outputs, out_l, ncol, stream);
+    clear_error();
+    FV3_REQUIRE(precision == FV3_DENSE_BF16X3, "dense_forward_ex: unknown precision %d", precision);
+    FV3_REQUIRE(m && m->b3, "dense_forward_ex: NULL model");
+    FV3_REQUIRE(ncol >= 0, "dense_forward_ex: ncol < 0");
+    if (ncol == 0) return FV3_OK;
+    FV3_REQUIRE(inputs && in_l && outputs && out_l, "dense_forward_ex: NULL argument");
+    const B3Pack& b = *m->b3;
+    B3Args a{};
+    const int64_t nb = in_l[0].ncol_blk;
+    for (int v = 0; v < m->n_in; ++v) {
+        FV3_REQUIRE(inputs[v], "dense_forward_ex: input %d is NULL", v);
+        FV3_REQUIRE(layout_ok(in_l[v], ncol) && in_l[v].ncol_blk == nb,
+                    "dense_forward_ex: input %d layout invalid or ncol_blk differs", v);
+        a.in[v] = B3InVar{inputs[v], in_l[v].ld, in_l[v].blk_stride, m->in_log_eps[v], 0};
+    }
+    for (int v = 0; v < m->n_out; ++v) {
+        FV3_REQUIRE(outputs[v], "dense_forward_ex: output %d is NULL", v);
+        FV3_REQUIRE(layout_ok(out_l[v], ncol) && out_l[v].ncol_blk == nb,
+                    "dense_forward_ex: output %d layout invalid or ncol_blk differs", v);
+        a.out_ptr[v] = outputs[v];
+        a.out_ld[v] = out_l[v].ld;
+        a.out_bs[v] = out_l[v].blk_stride;
+        const int r = m->out_residual[v];
+        a.res_ptr[v] = r >= 0 ? inputs[r] : nullptr;
+        a.res_ld[v] = r >= 0 ? in_l[r].ld : 0;
+        a.res_bs[v] = r >= 0 ? in_l[r].blk_stride : 0;
+    }
+    a.wstream = b.dbuf;
+    a.consts = reinterpret_cast<const float*>((const char*)b.dbuf + b.consts_off);
+    a.wbytes = b.wbytes;
+    a.nch = b.nch;
+    a.n1 = b.n1;
+    a.nhx = b.nhx;
+    a.npass = b.npass;
+    a.n_otile = b.n_otile;
+    a.kp1 = b.kp1;
+    a.kop = b.kop;
+    a.nconst = b.nconst;
+    a.any_log = b.any_log;
+    a.ncol = ncol;
+    a.ncol_blk = nb;
+    a.ntiles = (ncol + kB3Cols - 1) / kB3Cols;
+    for (size_t g = 0; g < b.gmeta.size(); ++g) a.gmeta[g] = b.gmeta[g];
+
+    const void* kfn = b.ht == 2 ? (const void*)dense_b3_kernel<2>
+                      : b.ht == 4 ? (const void*)dense_b3_kernel<4>
+                                  : (const void*)dense_b3_kernel<8>;
+    const size_t lds = (size_t)2 * 4096 * b.ht + (size_t)4 * b.nconst + (size_t)8 * 4 * b.kop;
+    FV3_REQUIRE(lds <= 160 * 1024, "dense_forward_ex: model needs %zu bytes of LDS", lds);
+    static std::mutex mu;
+    static int n_cu = 0;
+    static std::vector<std::pair<std::pair<const void*, size_t>, int>> resident;
+    int res = 0;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        if (!n_cu) {
+            int dev = 0;
+            FV3_HIP(hipGetDevice(&dev));
+            FV3_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+        }
+        for (auto& r : resident)
+            if (r.first.first == kfn && r.first.second == lds) res = r.second;
+        if (!res) {
+            FV3_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&res, kfn, 256, lds));
+            res = std::max(1, res);
+            resident.push_back({{kfn, lds}, res});
+        }
+    }
+    int64_t grid = std::min<int64_t>(a.ntiles, (int64_t)res * n_cu);
+    if (const char* e = getenv("FV3_B3_GRID")) grid = std::min<int64_t>(a.ntiles, std::max(1, atoi(e)));
+    void* kargs[] = {&a};
+    FV3_HIP(hipLaunchKernel(kfn, dim3((unsigned)grid), dim3(256), kargs, lds, (hipStream_t)stream));
+    FV3_LAUNCH_CHECK();
+    return FV3_OK;
+}

@@ -89,14 +89,33 @@ def _glorot(rng, fan_in, fan_out):
     return rng.uniform(-lim, lim, size=(fan_in, fan_out)).astype(np.float32)
 
 
-class DenseColumnModel:
-    """Weights + normalisation of a DenseModel, plus its device handle."""
+PRECISIONS = {"f32": _native.DENSE_F32, "bf16x3": _native.DENSE_BF16X3}
 
-    def __init__(self, config: DenseModelConfig, params: Mapping[str, object]):
+
+class DenseColumnModel:
+    """Weights + normalisation of a DenseModel, plus its device handle.
+
+    ``precision`` selects the fused kernel's arithmetic: ``"f32"`` (exact f32 products on
+    v_mfma_f32_16x16x4_f32, the Keras precision) or ``"bf16x3"`` (each f32 operand split
+    into bf16 hi + lo, three bf16 MFMAs per product; ~1e-5 rel, BASELINE config #5's
+    bf16-MFMA path)."""
+
+    def __init__(self, config: DenseModelConfig, params: Mapping[str, object], precision: str = "f32"):
         self.config = config
         self.params = dict(params)
         self._handles: Dict[int, int] = {}
+        self.precision = precision
         self._validate()
+
+    @property
+    def precision(self) -> str:
+        return self._precision
+
+    @precision.setter
+    def precision(self, value: str):
+        if value not in PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {value!r}")
+        self._precision = value
 
     # ---- construction ----------------------------------------------------------
     @classmethod
@@ -260,7 +279,8 @@ class DenseColumnModel:
 
     # ---- forward -----------------------------------------------------------------
     def forward(self, inputs: Sequence, level_axes: Optional[Sequence[int]] = None,
-                outputs: Optional[Sequence] = None, out_level_axis: int = 0, stream=None):
+                outputs: Optional[Sequence] = None, out_level_axis: int = 0, stream=None,
+                precision: Optional[str] = None):
         """Predict on device.  ``inputs[v]``: CUDA tensor whose axis ``level_axes[v]``
         (default 0) holds that variable's levels and whose other axes are columns
         (any leading axes are blocks, e.g. tiles).  A 2-D input may omit the level
@@ -303,16 +323,17 @@ class DenseColumnModel:
             olays.append(lay)
         if any(l.ncol_blk != lays[0].ncol_blk for l in lays + olays):
             raise ValueError("all inputs/outputs must share the horizontal layout")
-        bound = BoundForward(self, ts, lays, outputs, olays, ncol)
+        bound = BoundForward(self, ts, lays, outputs, olays, ncol, precision or self.precision)
         bound(stream)
         return outputs
 
     def bind(self, inputs: Sequence, level_axes: Optional[Sequence[int]] = None,
-             outputs: Optional[Sequence] = None, out_level_axis: int = 0) -> "BoundForward":
+             outputs: Optional[Sequence] = None, out_level_axis: int = 0,
+             precision: Optional[str] = None) -> "BoundForward":
         """Validate once and return a callable that re-launches the fused kernel on the
         same device buffers with no per-call argument marshalling (the prognostic loop
         calls predict on the same state arrays every timestep)."""
-        self.forward(inputs, level_axes, outputs, out_level_axis)
+        self.forward(inputs, level_axes, outputs, out_level_axis, precision=precision)
         return self._last_bound
 
     # ---- persistence -------------------------------------------------------------
@@ -359,7 +380,12 @@ class DenseColumnModel:
 class BoundForward:
     """A validated dense forward over fixed device buffers (see DenseColumnModel.bind)."""
 
-    def __init__(self, model: "DenseColumnModel", inputs, in_layouts, outputs, out_layouts, ncol: int):
+    def __init__(self, model: "DenseColumnModel", inputs, in_layouts, outputs, out_layouts, ncol: int,
+                 precision: str = "f32"):
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {precision!r}")
+        self.precision = precision
+        self._prec = PRECISIONS[precision]
         self.model = model
         self.inputs = list(inputs)  # keep the tensors alive
         self.outputs = list(outputs)
@@ -369,12 +395,12 @@ class BoundForward:
         self._out_l = (_native.Layout * len(out_layouts))(*out_layouts)
         self._ncol = int(ncol)
         self._handle = model.handle()
-        self._fn = _native.load().fv3_dense_forward
+        self._fn = _native.load().fv3_dense_forward_ex
         model._last_bound = self
 
     def __call__(self, stream=None):
         st = self._fn(self._handle, self._in_ptrs, self._in_l, self._out_ptrs, self._out_l, self._ncol,
-                      _device.stream_handle(stream))
+                      self._prec, _device.stream_handle(stream))
         if st:
             _native.check(st, "dense_forward")
         return self.outputs

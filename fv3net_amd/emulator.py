@@ -97,12 +97,18 @@ class MicrophysicsEmulator:
     ``__call__(state)``: state maps raw input names to [nz, ncol] (Fortran
     [feature, sample]) arrays; returns the after-states and direct outputs as
     [nz, ncol] / [ncol] float32 device tensors.
+
+    ``precision`` (None keeps the model's): "bf16x3" runs the MLP on bf16 MFMA with a
+    3-term split (BASELINE config #5: bf16 MFMA, 1e-3 rel), "f32" on exact f32 MFMA.
     """
 
-    def __init__(self, features: List[EmulatorFeature], outputs: List[EmulatorOutput], model: DenseColumnModel):
+    def __init__(self, features: List[EmulatorFeature], outputs: List[EmulatorOutput], model: DenseColumnModel,
+                 precision: Optional[str] = None):
         self.features = list(features)
         self.outputs = list(outputs)
         self.model = model
+        if precision is not None:
+            model.precision = precision
 
     @property
     def raw_inputs(self) -> List[str]:
@@ -131,7 +137,8 @@ class MicrophysicsEmulator:
     @classmethod
     def random(cls, sample_raw: Mapping[str, np.ndarray], sample_out: Mapping[str, np.ndarray],
                features: Optional[List[EmulatorFeature]] = None, outputs: Optional[List[EmulatorOutput]] = None,
-               width: int = 256, depth: int = 2, seed: int = 0) -> "MicrophysicsEmulator":
+               width: int = 256, depth: int = 2, seed: int = 0,
+               precision: str = "bf16x3") -> "MicrophysicsEmulator":
         """Glorot-initialised weights, normalisation fitted like MicrophysicsConfig.build
         on a sample: raw inputs [ncol, nz] per name, model outputs (differences and
         direct outputs) [ncol, nz] per output name."""
@@ -163,7 +170,7 @@ class MicrophysicsEmulator:
                       out_kernels=[_glorot(rng, width, o.nz) for o in outputs],
                       out_biases=[np.zeros(o.nz, np.float32) for o in outputs],
                       out_mean=out_mean, out_sigma=out_sigma, in_mean=in_mean, in_sigma=in_sigma)
-        return cls(features, outputs, DenseColumnModel(cfg, params))
+        return cls(features, outputs, DenseColumnModel(cfg, params), precision=precision)
 
     def params_by_name(self) -> dict:
         """Weights/normalisations keyed like the oracle (tests)."""

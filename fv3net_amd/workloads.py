@@ -59,7 +59,8 @@ class DenseWorkload:
             self._bound()
 
 
-def make_dense_workload(res: int, seed: int = 0, device=None, model: Optional[DenseColumnModel] = None):
+def make_dense_workload(res: int, seed: int = 0, device=None, model: Optional[DenseColumnModel] = None,
+                        precision: Optional[str] = None):
     device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
     T, q = synthetic_state(res, seed, device)
     if model is None:
@@ -67,6 +68,8 @@ def make_dense_workload(res: int, seed: int = 0, device=None, model: Optional[De
         sample_T = T[0, :, :8, :8].reshape(NZ, -1).T.cpu().numpy()
         sample_q = q[0, :, :8, :8].reshape(NZ, -1).T.cpu().numpy()
         model = DenseColumnModel.random(dense_2x256_config(), seed=1, sample_inputs=[sample_T, sample_q])
+    if precision is not None:
+        model.precision = precision
     outs = [torch.empty_like(T), torch.empty_like(T)]
     cfg = model.config
     return DenseWorkload(model, [T, q], outs, c_columns(res), cfg.flops_per_column(),
@@ -215,7 +218,7 @@ class EmulatorWorkload:
         return self.emulator(self.state, out=self.out)
 
 
-def make_emulator_workload(res: int = 384, seed: int = 0, device=None):
+def make_emulator_workload(res: int = 384, seed: int = 0, device=None, precision: str = "bf16x3"):
     from .emulator import MicrophysicsEmulator, zhao_carr_outputs
 
     device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -239,7 +242,7 @@ def make_emulator_workload(res: int = 384, seed: int = 0, device=None):
     for o in zhao_carr_outputs(NZ):
         sc = 1e-3 if o.name == "total_precipitation" else (1e-5 if ("humid" in o.name or "cloud" in o.name) else 0.5)
         sample_out[o.name] = rng.normal(0, sc, (4096, o.nz)).astype(np.float32)
-    emu = MicrophysicsEmulator.random(sample, sample_out, seed=seed)
+    emu = MicrophysicsEmulator.random(sample, sample_out, seed=seed, precision=precision)
     out = {(o.after or o.name): torch.empty((o.nz, ncol), device=device) for o in emu.outputs}
     cfg = emu.model.config
     return EmulatorWorkload(emu, state, out, ncol, cfg.flops_per_column(),

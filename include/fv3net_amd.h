@@ -11,7 +11,7 @@
  *   fv3_mappm*            external/mappm/mappm/mappm.f90:10  (f2py `mappm.mappm(pe1, q1,
  *                         pe2, i1, i2, iv, kord, ptop)`, bound at
  *                         external/vcm/vcm/cubedsphere/regridz.py:273)
- *   fv3_dense_*           the Keras predict of a DenseModel:
+ *   fv3_dense_*           the Keras predict of a DenseModel (and of the emulator MLP):
  *                         external/fv3fit/fv3fit/keras/_models/shared/pure_keras.py:112
  *                         (graph built in external/fv3fit/fv3fit/keras/_models/dense.py:234-305)
  *   fv3_regrid_coarsen    external/vcm/vcm/cubedsphere/regridz.py:25-55 + 115-161 fused with
@@ -47,7 +47,8 @@ extern "C" {
 #define FV3_ERR_UNSUPPORTED 3 /* valid request this build does not implement */
 
 const char* fv3_last_error(void);
-int fv3_abi_version(void); /* bumped on any signature change (2: emulator fields in fv3_dense_desc) */
+int fv3_abi_version(void); /* bumped on any signature change (2: emulator fields in fv3_dense_desc,
+                              3: fv3_dense_forward_ex) */
 
 /*
  * Column layout of a [level, column] field.  Element (column c, level k) lives at
@@ -127,6 +128,19 @@ int fv3_dense_set_trace(fv3_dense_model* model, long long* trace);
 int fv3_dense_forward(const fv3_dense_model* model, const float* const* inputs,
                       const fv3_layout* in_l, float* const* outputs, const fv3_layout* out_l,
                       int64_t ncol, void* stream);
+
+/* Forward with an explicit arithmetic:
+ *   FV3_DENSE_F32     exact f32 products on v_mfma_f32_16x16x4_f32 (= fv3_dense_forward);
+ *   FV3_DENSE_BF16X3  every f32 operand split into bf16 hi + lo, products as
+ *                     hi*hi + lo*hi + hi*lo on v_mfma_f32_32x32x16_bf16 with f32
+ *                     accumulation (~16 mantissa bits per operand: ~1e-5 rel on the
+ *                     reference graphs; BASELINE config #5, bf16 MFMA at 1e-3 rel).
+ * Same graph, layouts and in-place semantics as fv3_dense_forward. */
+#define FV3_DENSE_F32 0
+#define FV3_DENSE_BF16X3 1
+int fv3_dense_forward_ex(const fv3_dense_model* model, const float* const* inputs,
+                         const fv3_layout* in_l, float* const* outputs, const fv3_layout* out_l,
+                         int64_t ncol, int precision, void* stream);
 
 /* ---- fused pressure-level coarse-graining (config #3) ----------------------------
  * For every coarse cell (factor x factor fine columns of a tile):

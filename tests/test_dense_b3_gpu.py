@@ -1,0 +1,151 @@
+"""GPU parity of the bf16x3 fused dense kernel (csrc/dense_b3.hip: each f32 operand split
+into bf16 hi + lo, products hi*hi + lo*hi + hi*lo on v_mfma_f32_32x32x16_bf16) against
+the float64 evaluation of the reference graph (oracle/dense.py; reference
+external/fv3fit/fv3fit/keras/_models/dense.py:234-305).
+
+Tolerance: max |gpu - ref64| <= 5e-5 * max |ref64| per output variable.  The split
+keeps ~16 mantissa bits per operand; the CPU model of it (tools/bf16_study.py) gives
+8e-6 on the 2x256 model, so 5e-5 has margin while any fragment-layout or permutation
+error (O(1)) fails.  BASELINE config #5's contract for this path is 1e-3 rel
+(test_emulator.py); config #2's 1e-5 headline runs the exact-f32 kernel.
+"""
+import numpy as np
+import pytest
+
+from oracle.dense import dense_predict
+
+pytestmark = pytest.mark.gpu
+
+RTOL_B3 = 5e-5
+
+
+def _to_samples(a):
+    t, z, y, x = a.shape
+    return a.transpose(0, 2, 3, 1).reshape(t * y * x, z)
+
+
+def _check(gpu_out, ref64, rtol=RTOL_B3):
+    for g, r in zip(gpu_out, ref64):
+        scale = max(np.abs(r).max(), 1e-30)
+        err = np.abs(g.astype(np.float64) - r).max() / scale
+        assert err <= rtol, f"max rel err {err:.3e} > {rtol}"
+
+
+def _model(cfg_kwargs, seed=1, bias_scale=0.1, samples=None):
+    from fv3net_amd.dense import DenseColumnModel, DenseModelConfig
+
+    cfg = DenseModelConfig(**cfg_kwargs)
+    m = DenseColumnModel.random(cfg, seed=seed, sample_inputs=samples, bias_scale=bias_scale)
+    m.precision = "bf16x3"
+    return m
+
+
+def test_c48_2x256_tile_layout(gpu):
+    import torch
+
+    rng = np.random.default_rng(0)
+    T = rng.normal(260.0, 15.0, (6, 79, 48, 48)).astype(np.float32)
+    q = rng.uniform(0.0, 0.02, (6, 79, 48, 48)).astype(np.float32)
+    samples = [_to_samples(T), _to_samples(q)]
+    m = _model(dict(input_variables=["air_temperature", "specific_humidity"],
+                    output_variables=["dQ1", "dQ2"], in_nz=[79, 79], out_nz=[79, 79],
+                    width=256, depth=3), samples=samples)
+    outs = m.forward([torch.from_numpy(T).cuda(), torch.from_numpy(q).cuda()], level_axes=[1, 1])
+    torch.cuda.synchronize()
+    got = [_to_samples(o.cpu().numpy()) for o in outs]
+    _check(got, dense_predict(samples, m.oracle_params(), np.float64))
+    # the same model on the exact-f32 kernel agrees to the split's precision
+    f32 = m.forward([torch.from_numpy(T).cuda(), torch.from_numpy(q).cuda()], level_axes=[1, 1], precision="f32")
+    for a, b in zip(outs, f32):
+        assert (a - b).abs().max().item() <= RTOL_B3 * b.abs().max().item()
+
+
+@pytest.mark.parametrize("width,depth", [(64, 2), (128, 3), (100, 4), (256, 2), (37, 3), (256, 4)])
+def test_widths_depths_plain_layout(gpu, width, depth):
+    import torch
+
+    rng = np.random.default_rng(width + depth)
+    n = 1000  # ragged: not a multiple of 32 or 128
+    x1 = rng.normal(0, 3, (n, 20)).astype(np.float32)
+    x2 = rng.normal(5, 1, (n, 7)).astype(np.float32)
+    m = _model(dict(input_variables=["a", "b"], output_variables=["y1", "y2", "y3"], in_nz=[20, 7],
+                    out_nz=[5, 33, 1], width=width, depth=depth), samples=[x1, x2])
+    outs = m.forward([torch.from_numpy(x1.T.copy()).cuda(), torch.from_numpy(x2.T.copy()).cuda()])
+    got = [o.cpu().numpy().T for o in outs]
+    _check(got, dense_predict([x1, x2], m.oracle_params(), np.float64))
+
+
+def test_many_outputs_two_passes(gpu):
+    """> 256 output rows: the output layer runs in two passes of 8 tiles; 9 inputs
+    (the emulator's 736-feature staging)."""
+    import torch
+
+    rng = np.random.default_rng(11)
+    n = 700
+    xs = [rng.normal(i, 1 + i, (n, 79)).astype(np.float32) for i in range(9)]
+    m = _model(dict(input_variables=[f"x{i}" for i in range(9)], output_variables=["a", "b", "c", "d", "e", "f"],
+                    in_nz=[79] * 9, out_nz=[1, 79, 79, 79, 79, 79], width=256, depth=3), samples=xs)
+    outs = m.forward([torch.from_numpy(x.T.copy()).cuda() for x in xs])
+    got = [o.cpu().numpy().reshape(o.shape[0], n).T for o in outs]
+    _check(got, dense_predict(xs, m.oracle_params(), np.float64))
+
+
+def test_clip_limits_mask_and_scalar_input(gpu):
+    import torch
+
+    rng = np.random.default_rng(3)
+    n = 777
+    T = rng.normal(260, 15, (n, 79)).astype(np.float32)
+    ps = rng.normal(1e5, 500, (n, 1)).astype(np.float32)
+    cfg = dict(input_variables=["T", "ps"], output_variables=["dQ1", "dQ2"], in_nz=[79, 1],
+               out_nz=[79, 79], width=128, depth=3,
+               clip={"T": (10, 70), "dQ2": (5, 60)},
+               output_limits={"dQ1": (-0.5, 0.5), "dQ2": (None, 0.1)})
+    m = _model(cfg, samples=[T, ps], bias_scale=0.5)
+    outs = m.forward([torch.from_numpy(T.T.copy()).cuda(), torch.from_numpy(ps[:, 0].copy()).cuda()],
+                     level_axes=[0, None])
+    got = [o.cpu().numpy().reshape(79, n).T for o in outs]
+    _check(got, dense_predict([T, ps], m.oracle_params(), np.float64))
+    assert (got[1][:, :5] == 0).all() and (got[1][:, 60:] == 0).all()
+    assert got[0].max() <= 0.5 and got[0].min() >= -0.5 and got[1].max() <= 0.1
+
+
+@pytest.mark.parametrize("n", [1, 31, 32, 33, 127, 128, 129, 300])
+def test_tiny_and_ragged(gpu, n):
+    import torch
+
+    rng = np.random.default_rng(n)
+    x = rng.normal(0, 1, (n, 79)).astype(np.float32)
+    m = _model(dict(input_variables=["x"], output_variables=["y"], in_nz=[79], out_nz=[79],
+                    width=256, depth=3))
+    # outputs pre-filled with a sentinel: columns past n must not be touched
+    out = torch.full((79, n + 5), 7.0, device="cuda")
+    m.forward([torch.from_numpy(x.T.copy()).cuda()], outputs=[out[:, :n]])
+    o = out.cpu().numpy()
+    assert (o[:, n:] == 7.0).all()
+    _check([o[:, :n].T], dense_predict([x], m.oracle_params(), np.float64))
+
+
+def test_c384_persistent_tiles_and_determinism(gpu):
+    """884,736 columns = 6,912 tiles of 128 over one block per CU (27 tiles per block):
+    the weight-stream ring and input prefetch carry across tiles."""
+    import torch
+
+    rng = np.random.default_rng(384)
+    ntile, nz, n = 6, 79, 384
+    T = torch.from_numpy(rng.normal(260, 15, (ntile, nz, n, n)).astype(np.float32)).cuda()
+    q = torch.from_numpy(rng.uniform(0, 0.02, (ntile, nz, n, n)).astype(np.float32)).cuda()
+    m = _model(dict(input_variables=["T", "q"], output_variables=["dQ1", "dQ2"], in_nz=[79, 79],
+                    out_nz=[79, 79], width=256, depth=3),
+               samples=[_to_samples(T[:, :, :8, :8].cpu().numpy()), _to_samples(q[:, :, :8, :8].cpu().numpy())])
+    a = m.forward([T, q], level_axes=[1, 1])
+    b = m.forward([T, q], level_axes=[1, 1])
+    torch.cuda.synchronize()
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+        assert torch.isfinite(x).all()
+    # columns from the first, a middle and the last tiles
+    for ys, xs in [(slice(0, 8), slice(0, 8)), (slice(200, 206), slice(100, 140)), (slice(376, 384), slice(344, 384))]:
+        sub = [_to_samples(T[:, :, ys, xs].cpu().numpy()), _to_samples(q[:, :, ys, xs].cpu().numpy())]
+        got = [_to_samples(o[:, :, ys, xs].cpu().numpy()) for o in a]
+        _check(got, dense_predict(sub, m.oracle_params(), np.float64))

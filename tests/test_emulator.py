@@ -1,6 +1,7 @@
 """Zhao-Carr microphysics emulator (BASELINE config #5): the fused
 kernel vs the numpy restatement of the inference graph (oracle/emulator.py).
-Contract: 1e-3 rel (north_star); the float32 MFMA path is held to 1e-5."""
+Contract: 1e-3 rel (north_star, bf16 MFMA); the bf16x3 path (the config's default) is
+held to 1e-4 on every output, the exact-f32 MFMA path to 1e-5."""
 import numpy as np
 import pytest
 
@@ -36,7 +37,7 @@ def test_oracle_bf16_rounding():
     assert r[4] == -3.140625 and np.isnan(r[5])
 
 
-def _emulator(ncol=2048, seed=1):
+def _emulator(ncol=2048, seed=1, precision="bf16x3"):
     from fv3net_amd.emulator import MicrophysicsEmulator, zhao_carr_outputs
 
     raw = OE.synthetic_raw(ncol, seed=seed)
@@ -45,15 +46,16 @@ def _emulator(ncol=2048, seed=1):
     for o in zhao_carr_outputs():
         s = 1e-3 if o.name == "total_precipitation" else (1e-5 if ("humid" in o.name or "cloud" in o.name) else 0.5)
         sample_out[o.name] = rng.normal(0, s, (4096, o.nz)).astype(np.float32)
-    emu = MicrophysicsEmulator.random(raw, sample_out, seed=seed)
+    emu = MicrophysicsEmulator.random(raw, sample_out, seed=seed, precision=precision)
     return emu, raw
 
 
 @pytest.mark.gpu
-def test_emulator_matches_oracle(gpu):
+@pytest.mark.parametrize("precision,rtol", [("bf16x3", 1e-4), ("f32", 1e-5)])
+def test_emulator_matches_oracle(gpu, precision, rtol):
     import torch
 
-    emu, raw = _emulator()
+    emu, raw = _emulator(precision=precision)
     ref = OE.forward(raw, OE.zhao_carr_spec(), emu.params_by_name(), np.float64)
     state = {k: torch.from_numpy(np.ascontiguousarray(v.T)).cuda() for k, v in raw.items()}  # [feature, sample]
     got = emu(state)
@@ -63,7 +65,7 @@ def test_emulator_matches_oracle(gpu):
         r = ref[name]
         r = r[:, 0] if o["nz"] == 1 else r.T
         err = np.abs(g - r).max() / np.abs(r).max()
-        assert err <= 1e-5, (name, err)
+        assert err <= rtol, (name, err)
         if o.get("residual_of"):  # the difference itself, recovered from the after-state
             d = g.astype(np.float64) - raw[o["residual_of"]].T.astype(np.float64)
             derr = np.abs(d - ref[o["name"]].T).max() / np.abs(ref[o["name"]]).max()
