@@ -15,6 +15,7 @@ except ImportError:  # pragma: no cover
 
 NZ = 79
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, dense f32 MFMA (= vector) peak
+BF16_MFMA_PEAK_TFLOPS = 2516.6  # MI355X_MICROARCH.md, dense bf16 MFMA peak
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
 
 
