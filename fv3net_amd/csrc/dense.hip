@@ -107,6 +107,25 @@ __device__ __forceinline__ float frag_at(const typename Frag<T4>::type& a, int j
         return a[j];
 }
 
+// every f32 MFMA of the kernel (FV3_EXP_NOMFMA, experiment only: operands consumed, no MFMA)
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c)
+{
+#ifdef FV3_EXP_NOMFMA
+    asm volatile("" ::"v"(a), "v"(b));
+    return c;
+#else
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+#endif
+}
+
+// the tile loop's workgroup barriers (FV3_EXP_NOBARRIER, experiment only: none)
+__device__ __forceinline__ void tile_sync()
+{
+#ifndef FV3_EXP_NOBARRIER
+    __syncthreads();
+#endif
+}
+
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.0f, 0.0f, 0.0f, 0.0f}; }
 
 // log(max(x, eps)) with tf.maximum's NaN propagation and a correctly rounded-class log
@@ -151,6 +170,19 @@ __device__ __forceinline__ FT bload(Rsrc r, int voff, int soff)
 {
 #ifdef FV3_EXP_L1_WEIGHTS  // experiment only: every weight fragment from one 4 KiB window (L1 hits)
     soff &= 0xfff;
+#endif
+#ifdef FV3_EXP_NOWLOAD  // experiment only (results invalid): no weight loads at all
+    FT v;
+    if constexpr (sizeof(FT) == 16) {
+        asm volatile("v_mov_b32 %0, %1" : "=v"(v[0]) : "s"(soff));
+        v[1] = v[0]; v[2] = v[0]; v[3] = v[0];
+    } else if constexpr (sizeof(FT) == 8) {
+        asm volatile("v_mov_b32 %0, %1" : "=v"(v[0]) : "s"(soff));
+        v[1] = v[0];
+    } else {
+        asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(soff));
+    }
+    return v;
 #endif
     if constexpr (sizeof(FT) == 16)
         return __builtin_bit_cast(FT, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
@@ -204,8 +236,7 @@ __device__ __forceinline__ void gemm_hidden(f32x4 (&acc)[NC][T4], const f32x4* _
             for (int j = 0; j < T4; ++j)
 #pragma unroll
                 for (int c = 0; c < NC; ++c)
-                    acc[c][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(frag_at<T4>(g[t % RD][r], j), bq[t % 2][c][r],
-                                                                     acc[c][j], 0, 0, 0);
+                    acc[c][j] = mfma4(frag_at<T4>(g[t % RD][r], j), bq[t % 2][c][r], acc[c][j]);
     });
 }
 
@@ -248,7 +279,7 @@ __device__ __forceinline__ void gemm_out(f32x4 (&o)[kMaxUnits], const f32x4* __r
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int i = 0; i < N; ++i)
-                o[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(g[t % RD][i][r], bq[t % 2][r], o[i], 0, 0, 0);
+                o[i] = mfma4(g[t % RD][i][r], bq[t % 2][r], o[i]);
     });
 }
 
@@ -430,11 +461,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         // ~100 loop-invariant scalars spilled into VGPRs for the whole loop
         KArgs* pt = &p;
         asm volatile("" : "+s"(pt));
+#ifndef FV3_EXP_NOSTAGE  // experiment only (results invalid): no input staging
         if (p.has_log)
             store_x(*pt, tile, fq, std::true_type{});
         else
             store_x(*pt, tile, fq, std::false_type{});
-        __syncthreads();
+#endif
+        tile_sync();
         trace_mark(p, tile, 1);
 
         // ---- layer 1: Dense(width) over the padded input features ----
@@ -473,8 +506,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
                             for (int j = 0; j < T4; ++j)
 #pragma unroll
                                 for (int c = 0; c < NC; ++c)
-                                    acc[c][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(frag_at<T4>(g1[h][r], j),
-                                                                                     xb[h][c][r], acc[c][j], 0, 0, 0);
+                                    acc[c][j] = mfma4(frag_at<T4>(g1[h][r], j), xb[h][c][r], acc[c][j]);
                     }
                 });
             }
@@ -486,9 +518,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
             load_raw(*pn, tile + gridDim.x, fq);
         }
         prime_after(-1);
-        __syncthreads();  // every wave is done with the staged inputs
+        tile_sync();  // every wave is done with the staged inputs
         bias_relu_store<T4, NC>(acc, p.b1, wave, lane, kr, hbuf);
-        __syncthreads();
+        tile_sync();
         trace_mark(p, tile, 2);
 
         // ---- further hidden layers, in place ----
@@ -499,9 +531,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
                 for (int j = 0; j < T4; ++j) acc[c][j] = zero4();
             gemm_hidden<T4, NC, RD>(acc, hbuf, rw, voff, p.wh_off + l * (HP / 4) * KS, gh, lane);
             prime_after(l);
-            __syncthreads();  // every wave is done reading this layer's input
+            tile_sync();  // every wave is done reading this layer's input
             bias_relu_store<T4, NC>(acc, p.bh + (size_t)l * HP, wave, lane, kr, hbuf);
-            __syncthreads();
+            tile_sync();
         }
         trace_mark(p, tile, 3);
 
@@ -552,14 +584,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
                     y = y * mk[r];
                     if (cvalid && row < onrow) {  // padding rows of the last tile: no reads either
                         if (rsrc) y = rsrc[(int64_t)(oz0 + row) * rld] + y;  // after = before + to
+#ifdef FV3_EXP_NOSTORE  // experiment only (results invalid): keep the value, skip the store
+                        asm volatile("" ::"v"(y));
+#else
                         dst[(int64_t)(oz0 + row) * ld] = y;
+#endif
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
         prime_ring<RD, FT>(g1, rw, voff, p.w1_off);  // the next tile's layer 1
-        __syncthreads();         // the activations are free for the next tile's inputs
+        tile_sync();         // the activations are free for the next tile's inputs
         trace_mark(p, tile, 4);
     }
 }

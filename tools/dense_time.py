@@ -11,7 +11,9 @@ from fv3net_amd import workloads as W  # noqa: E402
 
 def time_res(res, n):
     wl = W.make_dense_workload(res, seed=1, device=torch.device("cuda", 0))
-    for _ in range(5):
+    import time
+    t0 = time.time()
+    while time.time() - t0 < 0.3:  # settle clocks (bench.py does the same)
         wl.step()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
