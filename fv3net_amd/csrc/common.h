@@ -23,6 +23,14 @@ void clear_error();
         }                                          \
     } while (0)
 
+#define FV3_REQUIRE_CODE(code, cond, ...)          \
+    do {                                           \
+        if (!(cond)) {                             \
+            ::fv3::set_error(__VA_ARGS__);         \
+            return (code);                         \
+        }                                          \
+    } while (0)
+
 #define FV3_HIP(call)                                                                  \
     do {                                                                               \
         hipError_t e_ = (call);                                                        \

@@ -119,10 +119,40 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c)
 }
 
 // the tile loop's workgroup barriers (FV3_EXP_NOBARRIER, experiment only: none)
+// Only LDS traffic is ordered by these barriers (staged inputs, activations, constants):
+// wait for this wave's LDS operations, then s_barrier.  Global loads in flight (the next
+// tile's inputs, the weight rings) are NOT drained, as __syncthreads() would (vmcnt(0)).
 __device__ __forceinline__ void tile_sync()
 {
-#ifndef FV3_EXP_NOBARRIER
+#if defined(FV3_EXP_NOBARRIER)
+#elif defined(FV3_EXP_OLDBAR)
     __syncthreads();
+#else
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
+}
+
+// column data is touched once per launch: streamed past L2 so the weights (re-read by
+// every tile) stay resident there across launches
+__device__ __forceinline__ float in_load(const float* p)
+{
+#ifdef FV3_EXP_NOINLOAD  // experiment only (results invalid): no input loads
+    float v;
+    asm volatile("v_mov_b32 %0, 1.0" : "=v"(v));
+    return v;
+#endif
+#ifdef FV3_EXP_TEMPORAL
+    return *p;
+#else
+    return __builtin_nontemporal_load(p);
+#endif
+}
+__device__ __forceinline__ void out_store(float* p, float v)
+{
+#ifdef FV3_EXP_TEMPORAL
+    *p = v;
+#else
+    __builtin_nontemporal_store(v, p);
 #endif
 }
 
@@ -333,15 +363,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     // scalar reads of all slot descriptors can be in flight together.
     auto slot_load = [&](KArgs& pk, int q, int meta, bool valid, int64_t blk, int64_t ii, int fq) {
         return (valid && fq < ((meta >> 8) & 0xff))
-                   ? pk.slot_base[q][blk * pk.slot_bs[q] + ii + (int64_t)fq * pk.slot_ld[q]]
+                   ? in_load(pk.slot_base[q] + blk * pk.slot_bs[q] + ii + (int64_t)fq * pk.slot_ld[q])
                    : 0.0f;
     };
+    // the register-prefetched slots: 32-bit element offsets (the host checks every
+    // slot's span fits), one branch-free load per slot (a lane that must not read
+    // loads a constant instead and keeps 0)
     auto load_raw = [&](KArgs& pk, int64_t tile, int fq) {
         int64_t blk, ii;
         const bool valid = col_of(tile, blk, ii);
+        const unsigned b32 = (unsigned)blk, i32 = (unsigned)ii;
         static_for<kRawSlots>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
-            raw[q] = slot_load(pk, q, pk.slot_meta[q], valid, blk, ii, fq);
+            const int meta = pk.slot_meta[q];
+            const bool on = valid && fq < ((meta >> 8) & 0xff);
+            const unsigned off = b32 * (unsigned)pk.slot_bs[q] + i32 + (unsigned)fq * (unsigned)pk.slot_ld[q];
+            const float v = in_load(on ? pk.slot_base[q] + off : pk.in_mean);
+            raw[q] = on ? v : 0.0f;
         });
     };
     // normalise and write the staged inputs in B-operand order: for column tile c,
@@ -353,21 +391,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     float* s_dummy = s_ep + 6 * 16 * p.n_otiles;  // write-only sink
     // branch-free: lanes past the slot's rows store to s_dummy, so the slots of a batch
     // schedule together (no divergent region between them)
-    // (x - mean) / denom as x' * rcp + one residual correction (within an ulp of the
-    // IEEE quotient; the 1e-5 contract does not need the exact division sequence)
+    // (x - mean) / denom as (x - mean) * (1 / denom), the reciprocal packed at create time
+    // (within 1.5 ulp of the IEEE quotient; the contract is 1e-5)
     auto put = [&](int meta, float x, float leps, float mu, float dn, bool valid, int fq, auto logc) {
         const int f = min(((meta >> 16) & 0x7ff) + fq, p.kp - 1);
         if constexpr (decltype(logc)::value)
             if (leps > 0.0f) x = __logf_exact(x, leps);  // LogTransform.forward (transforms.py:123-124)
-        const float a = x - mu;
-        const float r = __builtin_amdgcn_rcpf(dn);
-        const float q0 = a * r;
-        float y = __builtin_fmaf(__builtin_fmaf(-q0, dn, a), r, q0);
+        float y = (x - mu) * dn;  // dn = 1 / (sigma + eps)
         asm volatile("" : "+v"(y));  // computed by every lane, then selected: no divergent branch
         y = (valid && fq < ((meta >> 8) & 0xff)) ? y : 0.0f;
         *(fq < (meta & 0xff) ? xc + xidx(f) : s_dummy) = y;
     };
     auto feat = [&](int meta, int fq) { return min(((meta >> 16) & 0x7ff) + fq, p.kp - 1); };
+    // ---- the short staging path (p.fast_stage: slots FPS-aligned, all in registers, no
+    // LogTransform): the staging address splits into a per-slot scalar part and a
+    // per-thread part: with fdst a multiple of FPS,
+    //   xidx(fdst + fq) = (fdst >> 4) * 256 + ((fdst >> 2) & 3) + [(fq & 3) * 64 + cl16 * 4 + (fq >> 2)]
+    auto store_x_fast = [&](KArgs& pk, int64_t tile, int fq) {
+        int64_t blk, ii;
+        const bool valid = col_of(tile, blk, ii);
+        const int tpart = (fq & 3) * 64 + cl16 * 4 + (fq >> 2);
+        static_for<kRawSlots>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            const int meta = pk.slot_meta[q];
+            const int fdst = (meta >> 16) & 0x7ff;
+            const int f = min(fdst + fq, p.kp - 1);
+            float y = (raw[q] - s_mean[f]) * s_denom[f];
+            y = (valid && fq < ((meta >> 8) & 0xff)) ? y : 0.0f;
+            *(fq < (meta & 0xff) ? xc + ((fdst >> 4) * 256 + ((fdst >> 2) & 3)) + tpart : s_dummy) = y;
+        });
+        for (int f = 4 * p.in_steps_total + fq; f < p.kp; f += FPS) xc[xidx(f)] = 0.0f;
+    };
     auto store_x = [&](KArgs& pk, int64_t tile, int fq, auto logc) {
         int64_t blk, ii;
         const bool valid = col_of(tile, blk, ii);
@@ -413,18 +467,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     // ---- prologue: this tile's inputs and the layer-1 ring in flight, constants to LDS ----
     int64_t tile = blockIdx.x;
     trace_mark(p, tile, 0);
-    if (tile < p.ntiles) load_raw(p, tile, fq0);
     const Rsrc rw = make_rsrc(p.wbase, p.wbytes);
     const int voff = (wave * 64 + lane) * (int)sizeof(FT);  // hidden-layer fragments
     const int voff_o = lane * 16;                           // output-layer fragments
     constexpr int KS = 256 * sizeof(FT);
     FT g1[RD][4];
+#ifdef FV3_EXP_OLDPROLOG
+    if (tile < p.ntiles) load_raw(p, tile, fq0);
     prime_ring<RD, FT>(g1, rw, voff, p.w1_off);
     for (int i = threadIdx.x; i < p.kp; i += 256) {
         s_mean[i] = p.in_mean[i];
         s_denom[i] = p.in_denom[i];
     }
     for (int i = threadIdx.x; i < 6 * kop; i += 256) s_ep[i] = p.oep[i];
+#else
+    // loads complete in issue order (one vmcnt counter): the constants and the layer-1
+    // ring go first, so writing the constants to LDS and the first MFMAs do not wait
+    // for the tile's inputs (HBM), which are issued last
+    {
+        constexpr int NM = 4, NE = 12;  // constants held in registers: kp <= 1024, 6*kop <= 3072
+        float cm[NM], cd[NM], ce[NE];
+#pragma unroll
+        for (int j = 0; j < NM; ++j) {
+            const int i = threadIdx.x + 256 * j;
+            cm[j] = i < p.kp ? p.in_mean[i] : 0.0f;
+            cd[j] = i < p.kp ? p.in_denom[i] : 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < NE; ++j) {
+            const int i = threadIdx.x + 256 * j;
+            ce[j] = i < 6 * kop ? p.oep[i] : 0.0f;
+        }
+        prime_ring<RD, FT>(g1, rw, voff, p.w1_off);
+        if (tile < p.ntiles) load_raw(p, tile, fq0);
+#pragma unroll
+        for (int j = 0; j < NM; ++j) {
+            const int i = threadIdx.x + 256 * j;
+            if (i < p.kp) {
+                s_mean[i] = cm[j];
+                s_denom[i] = cd[j];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NE; ++j) {
+            const int i = threadIdx.x + 256 * j;
+            if (i < 6 * kop) s_ep[i] = ce[j];
+        }
+        for (int i = threadIdx.x + 256 * NM; i < p.kp; i += 256) {
+            s_mean[i] = p.in_mean[i];
+            s_denom[i] = p.in_denom[i];
+        }
+        for (int i = threadIdx.x + 256 * NE; i < 6 * kop; i += 256) s_ep[i] = p.oep[i];
+    }
+#endif
 
     // output plan of this wave
     const int nunits = p.n_otiles * NC;
@@ -449,7 +544,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
             prime_out<RD>(go, rw, voff_o, plan(0));
         }
     };
-    __syncthreads();
+    tile_sync();
 
     for (; tile < p.ntiles; tile += gridDim.x) {  // persistent over column tiles
         trace_mark(p, tile, 5);
@@ -462,7 +557,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         KArgs* pt = &p;
         asm volatile("" : "+s"(pt));
 #ifndef FV3_EXP_NOSTAGE  // experiment only (results invalid): no input staging
-        if (p.has_log)
+        if (p.fast_stage)
+            store_x_fast(*pt, tile, fq);
+        else if (p.has_log)
             store_x(*pt, tile, fq, std::true_type{});
         else
             store_x(*pt, tile, fq, std::false_type{});
@@ -583,11 +680,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
                     if (y >= hi[r]) y = hi[r];
                     y = y * mk[r];
                     if (cvalid && row < onrow) {  // padding rows of the last tile: no reads either
-                        if (rsrc) y = rsrc[(int64_t)(oz0 + row) * rld] + y;  // after = before + to
+                        if (rsrc) y = in_load(rsrc + (int64_t)(oz0 + row) * rld) + y;  // after = before + to
 #ifdef FV3_EXP_NOSTORE  // experiment only (results invalid): keep the value, skip the store
                         asm volatile("" ::"v"(y));
 #else
-                        dst[(int64_t)(oz0 + row) * ld] = y;
+                        out_store(dst + (int64_t)(oz0 + row) * ld, y);
 #endif
                     }
                 }
@@ -701,7 +798,8 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
         if (src < 0) continue;
         in_mean[f] = d->in_mean[src];
         volatile float s = d->in_sigma[src];
-        in_denom[f] = s + d->epsilon;  // StandardNormLayer computes sigma + epsilon in f32
+        volatile float den = s + d->epsilon;  // StandardNormLayer computes sigma + epsilon in f32
+        in_denom[f] = 1.0f / den;             // the kernel multiplies: <= 1.5 ulp from the quotient
     }
     const int T4 = HT / 4;
     // layer 1: W1[k_in][W] -> [KP/4][wave][64][T4]; tile m = wave*T4 + j
@@ -913,6 +1011,21 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
             a.slot_leps[q] = m->in_log_eps[v];
             a.has_log |= m->in_log_eps[v] > 0.0f;
         }
+    }
+    {
+        bool fast = !a.has_log && a.nslots <= kRawSlots;
+        const int64_t nblk = (ncol + nb - 1) / nb;
+        for (int q = 0; q < a.nslots; ++q) {
+            const int fdst = (a.slot_meta[q] >> 16) & 0x7ff;
+            const int64_t bs = nblk > 1 ? (int64_t)a.slot_bs[q] : 0;
+            const int64_t span = (nblk - 1) * bs + (std::min<int64_t>(nb, ncol) - 1) + (int64_t)(fps - 1) * a.slot_ld[q];
+            // the kernel addresses a slot's rows with 32-bit unsigned element offsets
+            FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, bs >= 0 && a.slot_ld[q] >= 0 && span < ((int64_t)1 << 32),
+                             "dense_forward: input %d spans more than 2^32 elements", a.slot_meta[q] >> 27);
+            fast = fast && fdst % fps == 0;
+        }
+        if (getenv("FV3_DENSE_SLOWSTAGE")) fast = false;  // A/B
+        a.fast_stage = fast;
     }
     hipStream_t s = (hipStream_t)stream;
     // LDS: activations (NC x HT tiles x 64 lanes x 16 B) or the staged inputs

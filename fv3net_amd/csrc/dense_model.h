@@ -31,7 +31,7 @@ struct DenseOutTile {
 
 struct DenseArgs {
     const float* in_mean;   // [KP] padded feature order
-    const float* in_denom;  // [KP] f32(sigma + eps)
+    const float* in_denom;  // [KP] 1 / f32(sigma + eps) (StandardNormLayer's divisor, inverted)
     const float* w1;        // [KP/4][4 waves][64][T4]
     const float* b1;        // [HP]
     const float* wh;        // [n_hidden-1][HP/4][4 waves][64][T4]
@@ -66,6 +66,8 @@ struct DenseArgs {
     int in_steps_total, nslots;
     int lds_x;              // f32x4 offset of the constants area (after activations / inputs)
     int has_log;            // any slot with a LogTransform (selects the staging variant)
+    int fast_stage;         // every slot FPS-aligned, <= kRawSlots slots, no log, 32-bit
+                            // element offsets: the short staging path (buffer loads)
     long long* trace;       // profiling hook (fv3_dense_set_trace): [tiles][8] timestamps, or NULL
 };
 static_assert(sizeof(DenseArgs) <= 4096, "kernel arguments are limited to 4 KiB");
