@@ -10,10 +10,11 @@
 // tendencies are written straight into [level][column] outputs (the unstack).
 //
 // Mapping (CDNA4, wave64, v_mfma_f32_16x16x4_f32 — exact f32, no xf32 on gfx950):
-//  * a 256-thread block (4 waves, one per SIMD) owns a tile of NC x 16 columns for
-//    the whole network; wave w owns hidden-unit tiles [w*T4, (w+1)*T4) of every
-//    hidden layer (T4 = width/64 tiles of 16 units); lane l holds column (l & 15)
-//    and k-slot (l >> 4) of every B operand;
+//  * a block of NW waves (4: one per SIMD; 8: two per SIMD, used when there are few
+//    tiles per CU, e.g. C48) owns a tile of NC x 16 columns for the whole network;
+//    wave w owns hidden-unit tiles [w*T4, (w+1)*T4) of every hidden layer
+//    (T4 = width/(16 NW) tiles of 16 units); lane l holds column (l & 15) and k-slot
+//    (l >> 4) of every B operand;
 //  * a layer's output is written to LDS in the MFMA accumulator layout
 //    ([tile][lane] x 4 regs, register r of tile t = unit 16t + 4(l>>4) + r) and the
 //    next layer reads it back with one ds_read_b128 per 4 k-steps: k-step s = 4t + r
@@ -21,7 +22,7 @@
 //    permuted and the packed weights carry the same permutation (no shuffles);
 //  * ONE activation buffer is updated in place (read, barrier, write, barrier) and
 //    the staged inputs alias it: ~37 KB of LDS per block -> 3 blocks per CU;
-//  * inputs are loaded by "slots" (256 threads x one feature row each, the
+//  * inputs are loaded by "slots" (64 NW threads x one feature row each, the
 //    variable uniform per slot), all slots of a tile in flight at once; blocks are
 //    persistent over column tiles and load the NEXT tile's inputs into registers
 //    while the current tile runs its hidden and output layers;
@@ -162,11 +163,11 @@ __device__ __forceinline__ f32x4 zero4() { return f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 __device__ __forceinline__ float __logf_exact(float x, float eps) { return x != x ? x : logf(x > eps ? x : eps); }
 
 // relu(acc + bias) for this wave's T4 tiles (x NC column tiles), stored in accumulator layout
-template <int T4, int NC>
+template <int T4, int NC, int NW>
 __device__ __forceinline__ void bias_relu_store(f32x4 (&acc)[NC][T4], const float* __restrict__ b, int wave,
                                                 int lane, int kr, f32x4* __restrict__ dst)
 {
-    constexpr int HT = 4 * T4;
+    constexpr int HT = NW * T4;
 #pragma unroll
     for (int j = 0; j < T4; ++j) {
         const int m = wave * T4 + j;
@@ -225,10 +226,10 @@ __device__ __forceinline__ FT bload(Rsrc r, int voff, int soff)
 // first RD-1 groups (4 k-steps each) of a [k-step][wave][lane] fragment stream
 // starting at byte offset soff (voff = this lane's (wave * 64 + lane) * sizeof(FT)).
 // RD = ring depth: a ring of RD groups is refilled RD-1 groups ahead of use.
-template <int RD, typename FT>
+template <int RD, int NW, typename FT>
 __device__ __forceinline__ void prime_ring(FT (&g)[RD][4], Rsrc r, int voff, int soff)
 {
-    constexpr int KS = 256 * sizeof(FT);  // bytes per k-step
+    constexpr int KS = 64 * NW * sizeof(FT);  // bytes per k-step
 #pragma unroll
     for (int d = 0; d + 1 < RD; ++d)
 #pragma unroll
@@ -238,13 +239,13 @@ __device__ __forceinline__ void prime_ring(FT (&g)[RD][4], Rsrc r, int voff, int
 // acc[c][j] += W^T h over all HT*4 k-steps, h read from LDS in accumulator layout.
 // Weight fragments stream through the RD-group ring g (groups 0..RD-2 primed by the
 // caller), RD-1 groups (4*T4*NC MFMAs each) ahead of use.
-template <int T4, int NC, int RD>
+template <int T4, int NC, int RD, int NW>
 __device__ __forceinline__ void gemm_hidden(f32x4 (&acc)[NC][T4], const f32x4* __restrict__ src, Rsrc rw,
                                             int voff, int soff, typename Frag<T4>::type (&g)[RD][4], int lane)
 {
-    constexpr int HT = 4 * T4;
+    constexpr int HT = NW * T4;
     typedef typename Frag<T4>::type FT;
-    constexpr int KS = 256 * sizeof(FT);
+    constexpr int KS = 64 * NW * sizeof(FT);
     f32x4 bq[2][NC];  // B operands, one group ahead
 #pragma unroll
     for (int c = 0; c < NC; ++c) bq[0][c] = src[(c * HT) * 64 + lane];
@@ -270,7 +271,7 @@ __device__ __forceinline__ void gemm_hidden(f32x4 (&acc)[NC][T4], const f32x4* _
     });
 }
 
-// output units of this wave: unit i = wave + 4 * (i0 + i), otile m = unit / NC;
+// output units of this wave: unit i = wave + NW * (i0 + i), otile m = unit / NC;
 // soff[i] = byte offset of unit i's weights (group 0) in the model allocation
 struct OutPlan {
     int soff[kMaxUnits];
@@ -289,11 +290,10 @@ __device__ __forceinline__ void prime_out(f32x4 (&g)[RD][kMaxUnits], Rsrc rw, in
 }
 
 // o[i] = W_m^T h for N units over all HT*4 k-steps; B operands of column tile cw
-template <int T4, int N, int RD>
+template <int HT, int N, int RD>
 __device__ __forceinline__ void gemm_out(f32x4 (&o)[kMaxUnits], const f32x4* __restrict__ src, Rsrc rw, int voff,
                                          const OutPlan& pl, f32x4 (&g)[RD][kMaxUnits])
 {
-    constexpr int HT = 4 * T4;
     f32x4 bq[2];
     bq[0] = src[0];
     static_for<HT>([&](auto tc) {
@@ -318,17 +318,20 @@ typedef __attribute__((address_space(4))) const DenseArgs KArgs;
 // WPE: waves per SIMD the register allocation targets (2: no limit below 256 VGPRs;
 // 3: <= 168, letting three blocks share a CU)
 // RD: weight ring depth (groups of 4 k-steps held; refilled RD-1 groups ahead)
-template <int T4, int NC, int WPE, int RD>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void dense_forward_kernel(DenseArgs pa)
+// NW: waves per block (4: one per SIMD; 8: two per SIMD sharing a tile, T4 halved)
+template <int T4, int NC, int WPE, int RD, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void dense_forward_kernel(DenseArgs pa)
 {
     // read the arguments in place in the kernarg segment (constant address space):
     // capturing a by-value kernel parameter by reference would copy it to scratch
     (void)pa;
     KArgs& p = *(KArgs*)(__builtin_amdgcn_kernarg_segment_ptr());
-    constexpr int HT = 4 * T4;   // hidden tiles of 16 units
+    constexpr int NT = 64 * NW;  // threads per block
+    constexpr int HT = NW * T4;  // hidden tiles of 16 units
     constexpr int HP = 16 * HT;  // padded width
     constexpr int NCOL = 16 * NC;
-    constexpr int FPS = 256 / NCOL;  // feature rows per slot
+    constexpr int FPS = NT / NCOL;  // feature rows per slot
+    static_assert(FPS == 8 || FPS == 16, "the staging address split assumes 8 or 16 rows per slot");
     typedef typename Frag<T4>::type FT;
     extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
     f32x4* hbuf = lds;  // activations [NC][HT][64]; the staged inputs [NC][kp/16][64] alias it
@@ -470,39 +473,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     const Rsrc rw = make_rsrc(p.wbase, p.wbytes);
     const int voff = (wave * 64 + lane) * (int)sizeof(FT);  // hidden-layer fragments
     const int voff_o = lane * 16;                           // output-layer fragments
-    constexpr int KS = 256 * sizeof(FT);
+    constexpr int KS = NT * sizeof(FT);
     FT g1[RD][4];
 #ifdef FV3_EXP_OLDPROLOG
     if (tile < p.ntiles) load_raw(p, tile, fq0);
-    prime_ring<RD, FT>(g1, rw, voff, p.w1_off);
-    for (int i = threadIdx.x; i < p.kp; i += 256) {
+    prime_ring<RD, NW, FT>(g1, rw, voff, p.w1_off);
+    for (int i = threadIdx.x; i < p.kp; i += NT) {
         s_mean[i] = p.in_mean[i];
         s_denom[i] = p.in_denom[i];
     }
-    for (int i = threadIdx.x; i < 6 * kop; i += 256) s_ep[i] = p.oep[i];
+    for (int i = threadIdx.x; i < 6 * kop; i += NT) s_ep[i] = p.oep[i];
 #else
     // loads complete in issue order (one vmcnt counter): the constants and the layer-1
     // ring go first, so writing the constants to LDS and the first MFMAs do not wait
     // for the tile's inputs (HBM), which are issued last
     {
-        constexpr int NM = 4, NE = 12;  // constants held in registers: kp <= 1024, 6*kop <= 3072
+        constexpr int NM = 1024 / NT, NE = 3072 / NT;  // constants held in registers: kp <= 1024, 6*kop <= 3072
         float cm[NM], cd[NM], ce[NE];
 #pragma unroll
         for (int j = 0; j < NM; ++j) {
-            const int i = threadIdx.x + 256 * j;
+            const int i = threadIdx.x + NT * j;
             cm[j] = i < p.kp ? p.in_mean[i] : 0.0f;
             cd[j] = i < p.kp ? p.in_denom[i] : 0.0f;
         }
 #pragma unroll
         for (int j = 0; j < NE; ++j) {
-            const int i = threadIdx.x + 256 * j;
+            const int i = threadIdx.x + NT * j;
             ce[j] = i < 6 * kop ? p.oep[i] : 0.0f;
         }
-        prime_ring<RD, FT>(g1, rw, voff, p.w1_off);
+        prime_ring<RD, NW, FT>(g1, rw, voff, p.w1_off);
         if (tile < p.ntiles) load_raw(p, tile, fq0);
 #pragma unroll
         for (int j = 0; j < NM; ++j) {
-            const int i = threadIdx.x + 256 * j;
+            const int i = threadIdx.x + NT * j;
             if (i < p.kp) {
                 s_mean[i] = cm[j];
                 s_denom[i] = cd[j];
@@ -510,27 +513,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         }
 #pragma unroll
         for (int j = 0; j < NE; ++j) {
-            const int i = threadIdx.x + 256 * j;
+            const int i = threadIdx.x + NT * j;
             if (i < 6 * kop) s_ep[i] = ce[j];
         }
-        for (int i = threadIdx.x + 256 * NM; i < p.kp; i += 256) {
+        for (int i = threadIdx.x + NT * NM; i < p.kp; i += NT) {
             s_mean[i] = p.in_mean[i];
             s_denom[i] = p.in_denom[i];
         }
-        for (int i = threadIdx.x + 256 * NE; i < 6 * kop; i += 256) s_ep[i] = p.oep[i];
+        for (int i = threadIdx.x + NT * NE; i < 6 * kop; i += NT) s_ep[i] = p.oep[i];
     }
 #endif
 
     // output plan of this wave
     const int nunits = p.n_otiles * NC;
-    const int cw = wave % NC;  // (wave + 4i) % NC: one column tile per wave
-    const int ucnt = nunits > wave ? (nunits - wave + 3) / 4 : 0;
+    const int cw = wave % NC;  // (wave + NW i) % NC: one column tile per wave
+    const int ucnt = nunits > wave ? (nunits - wave + NW - 1) / NW : 0;
     auto plan = [&](int i0) {
         OutPlan pl;
         pl.n = min(kMaxUnits, ucnt - i0);
 #pragma unroll
         for (int i = 0; i < kMaxUnits; ++i) {
-            const int u = wave + 4 * (i0 + min(i, pl.n - 1));
+            const int u = wave + NW * (i0 + min(i, pl.n - 1));
             pl.soff[i] = p.wo_off + (u / NC) * (HP / 16) * 1024;
         }
         return pl;
@@ -539,7 +542,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     FT gh[RD][4];
     auto prime_after = [&](int l) {  // prime the ring of the layer that follows hidden layer l
         if (l + 1 < p.n_hidden_extra) {
-            prime_ring<RD, FT>(gh, rw, voff, p.wh_off + (l + 1) * (HP / 4) * KS);
+            prime_ring<RD, NW, FT>(gh, rw, voff, p.wh_off + (l + 1) * (HP / 4) * KS);
         } else if (ucnt > 0) {
             prime_out<RD>(go, rw, voff_o, plan(0));
         }
@@ -616,7 +619,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
         }
         prime_after(-1);
         tile_sync();  // every wave is done with the staged inputs
-        bias_relu_store<T4, NC>(acc, p.b1, wave, lane, kr, hbuf);
+        bias_relu_store<T4, NC, NW>(acc, p.b1, wave, lane, kr, hbuf);
         tile_sync();
         trace_mark(p, tile, 2);
 
@@ -626,10 +629,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
             for (int c = 0; c < NC; ++c)
 #pragma unroll
                 for (int j = 0; j < T4; ++j) acc[c][j] = zero4();
-            gemm_hidden<T4, NC, RD>(acc, hbuf, rw, voff, p.wh_off + l * (HP / 4) * KS, gh, lane);
+            gemm_hidden<T4, NC, RD, NW>(acc, hbuf, rw, voff, p.wh_off + l * (HP / 4) * KS, gh, lane);
             prime_after(l);
             tile_sync();  // every wave is done reading this layer's input
-            bias_relu_store<T4, NC>(acc, p.bh + (size_t)l * HP, wave, lane, kr, hbuf);
+            bias_relu_store<T4, NC, NW>(acc, p.bh + (size_t)l * HP, wave, lane, kr, hbuf);
             tile_sync();
         }
         trace_mark(p, tile, 3);
@@ -648,14 +651,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 #pragma unroll
             for (int i = 0; i < kMaxUnits; ++i) o[i] = zero4();
             switch (pl.n) {
-                case 1: gemm_out<T4, 1, RD>(o, src, rw, voff_o, pl, go); break;
-                case 2: gemm_out<T4, 2, RD>(o, src, rw, voff_o, pl, go); break;
-                default: gemm_out<T4, kMaxUnits, RD>(o, src, rw, voff_o, pl, go); break;
+                case 1: gemm_out<HT, 1, RD>(o, src, rw, voff_o, pl, go); break;
+                case 2: gemm_out<HT, 2, RD>(o, src, rw, voff_o, pl, go); break;
+                default: gemm_out<HT, kMaxUnits, RD>(o, src, rw, voff_o, pl, go); break;
             }
 #pragma unroll
             for (int i = 0; i < kMaxUnits; ++i) {
                 if (i >= pl.n) break;
-                const int m = (wave + 4 * (i0 + i)) / NC;
+                const int m = (wave + NW * (i0 + i)) / NC;
                 const int ovar = p.otile[m].var, oz0 = p.otile[m].z0, onrow = p.otile[m].nrow;
                 if (ovar < 0) continue;
                 float* dst = p.out_ptr[ovar] + oblk * p.out_bs[ovar] + oii;
@@ -691,7 +694,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
-        prime_ring<RD, FT>(g1, rw, voff, p.w1_off);  // the next tile's layer 1
+        prime_ring<RD, NW, FT>(g1, rw, voff, p.w1_off);  // the next tile's layer 1
         tile_sync();         // the activations are free for the next tile's inputs
         trace_mark(p, tile, 4);
     }
@@ -801,42 +804,59 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
         volatile float den = s + d->epsilon;  // StandardNormLayer computes sigma + epsilon in f32
         in_denom[f] = 1.0f / den;             // the kernel multiplies: <= 1.5 ulp from the quotient
     }
-    const int T4 = HT / 4;
-    // layer 1: W1[k_in][W] -> [KP/4][wave][64][T4]; tile m = wave*T4 + j
-    std::vector<float> w1((size_t)m->kp * HP, 0.0f);
-    for (int s = 0; s < m->kp / 4; ++s)
-        for (int wv = 0; wv < 4; ++wv)
-            for (int l = 0; l < 64; ++l)
-                for (int j = 0; j < T4; ++j) {
-                    const int f = 4 * s + (l >> 4);
-                    const int unit = 16 * (wv * T4 + j) + (l & 15);
-                    const int src = feat_src[f];
-                    float v = 0.0f;
-                    if (src >= 0 && unit < W) v = d->hidden_kernel[0][(size_t)src * W + unit];
-                    w1[(((size_t)s * 4 + wv) * 64 + l) * T4 + j] = v;
-                }
-    std::vector<float> b1(HP, 0.0f);
-    for (int u = 0; u < W; ++u) b1[u] = d->hidden_bias[0][u];
-    // hidden layers 2..n: W[W][W] -> [HP/4][wave][64][T4]; k-step s = 4t + r reads
-    // input unit 16t + 4(l>>4) + r (the accumulator-layout permutation)
+    // layer 1: W1[k_in][W] -> [KP/4][wave][64][T4]; tile m = wave*T4 + j, T4 = HT / NW
+    // (packed for NW = 4 waves per block, and for NW = 8 when HT >= 8)
     const int nhx = d->n_hidden - 1;
-    std::vector<float> wh((size_t)std::max(nhx, 1) * HP * HP, 0.0f), bh((size_t)std::max(nhx, 1) * HP, 0.0f);
-    for (int li = 0; li < nhx; ++li) {
-        const float* K = d->hidden_kernel[li + 1];
-        for (int s = 0; s < HP / 4; ++s) {
-            const int t = s / 4, r = s % 4;
-            for (int wv = 0; wv < 4; ++wv)
+    auto pack_w1 = [&](int NW) {
+        const int T4 = HT / NW;
+        std::vector<float> w1((size_t)m->kp * HP, 0.0f);
+        for (int s = 0; s < m->kp / 4; ++s)
+            for (int wv = 0; wv < NW; ++wv)
                 for (int l = 0; l < 64; ++l)
                     for (int j = 0; j < T4; ++j) {
-                        const int in = 16 * t + 4 * (l >> 4) + r;
+                        const int f = 4 * s + (l >> 4);
                         const int unit = 16 * (wv * T4 + j) + (l & 15);
+                        const int src = feat_src[f];
                         float v = 0.0f;
-                        if (in < W && unit < W) v = K[(size_t)in * W + unit];
-                        wh[(size_t)li * HP * HP + (((size_t)s * 4 + wv) * 64 + l) * T4 + j] = v;
+                        if (src >= 0 && unit < W) v = d->hidden_kernel[0][(size_t)src * W + unit];
+                        w1[(((size_t)s * NW + wv) * 64 + l) * T4 + j] = v;
                     }
+        return w1;
+    };
+    // hidden layers 2..n: W[W][W] -> [HP/4][wave][64][T4]; k-step s = 4t + r reads
+    // input unit 16t + 4(l>>4) + r (the accumulator-layout permutation)
+    auto pack_wh = [&](int NW) {
+        const int T4 = HT / NW;
+        std::vector<float> wh((size_t)std::max(nhx, 1) * HP * HP, 0.0f);
+        for (int li = 0; li < nhx; ++li) {
+            const float* K = d->hidden_kernel[li + 1];
+            for (int s = 0; s < HP / 4; ++s) {
+                const int t = s / 4, r = s % 4;
+                for (int wv = 0; wv < NW; ++wv)
+                    for (int l = 0; l < 64; ++l)
+                        for (int j = 0; j < T4; ++j) {
+                            const int in = 16 * t + 4 * (l >> 4) + r;
+                            const int unit = 16 * (wv * T4 + j) + (l & 15);
+                            float v = 0.0f;
+                            if (in < W && unit < W) v = K[(size_t)in * W + unit];
+                            wh[(size_t)li * HP * HP + (((size_t)s * NW + wv) * 64 + l) * T4 + j] = v;
+                        }
+            }
         }
-        for (int u = 0; u < W; ++u) bh[(size_t)li * HP + u] = d->hidden_bias[li + 1][u];
+        return wh;
+    };
+    const bool nw8 = HT >= 8;
+    std::vector<float> w1 = pack_w1(4), wh = pack_wh(4);
+    std::vector<float> w1_8, wh_8;
+    if (nw8) {
+        w1_8 = pack_w1(8);
+        wh_8 = pack_wh(8);
     }
+    std::vector<float> b1(HP, 0.0f);
+    for (int u = 0; u < W; ++u) b1[u] = d->hidden_bias[0][u];
+    std::vector<float> bh((size_t)std::max(nhx, 1) * HP, 0.0f);
+    for (int li = 0; li < nhx; ++li)
+        for (int u = 0; u < W; ++u) bh[(size_t)li * HP + u] = d->hidden_bias[li + 1][u];
     // output layer: concat of out kernels [W][out_nz] -> [otile][HP/16][64][4 k-steps]
     std::vector<int> ocol_var(k_out), ocol_z(k_out);
     {
@@ -891,6 +911,7 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
         {w1.data(), w1.size() * 4, 0},           {b1.data(), b1.size() * 4, 0},
         {wh.data(), wh.size() * 4, 0},           {bh.data(), bh.size() * 4, 0},
         {wo.data(), wo.size() * 4, 0},           {oep.data(), oep.size() * 4, 0},
+        {w1_8.data(), w1_8.size() * 4, 0},       {wh_8.data(), wh_8.size() * 4, 0},
     };
     size_t total = 0;
     for (auto& p : pcs) {
@@ -900,7 +921,8 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
     size_t alloc = total;
     if (const char* e = getenv("FV3_DENSE_PAD_MB")) alloc = std::max(alloc, (size_t)atoi(e) << 20);
     FV3_HIP(hipMalloc(&m->dbuf, alloc));
-    for (auto& p : pcs) FV3_HIP(hipMemcpy((char*)m->dbuf + p.off, p.src, p.bytes, hipMemcpyHostToDevice));
+    for (auto& p : pcs)
+        if (p.bytes) FV3_HIP(hipMemcpy((char*)m->dbuf + p.off, p.src, p.bytes, hipMemcpyHostToDevice));
     auto at = [&](int i) { return (char*)m->dbuf + pcs[i].off; };
     DenseArgs& a = m->tmpl;
     a.in_mean = (const float*)at(0);
@@ -917,6 +939,8 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
     a.wh_off = (int)pcs[4].off;
     a.wo_off = (int)pcs[6].off;
     a.wbytes = (int)total;
+    m->w1_off8 = nw8 ? (int)pcs[8].off : -1;
+    m->wh_off8 = nw8 ? (int)pcs[9].off : -1;
     for (int t = 0; t < m->n_otiles; ++t) a.otile[t] = m->otiles[t];
     a.n_in = m->n_in;
     a.n_hidden_extra = nhx;
@@ -991,10 +1015,32 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
     // columns in > 64 KiB of LDS, i.e. one block per CU: use 16-column tiles there
     int nc = (size_t)2 * 16 * 4 * m->kp > 64 * 1024 ? 1 : 2;
     if (const char* e = getenv("FV3_DENSE_NC")) nc = atoi(e) == 1 ? 1 : 2;
+    // waves per block: with few tiles per CU (C48: 1.7) 8 waves, two per SIMD on one
+    // tile and each wave half the hidden units (C48 47.7 -> 46.7 us); with many, 4
+    // (C384: 2.32 vs 2.36 ms).  Needs 32-column tiles and width >= 128.
+    // FV3_DENSE_NW=4|8 for A/B
+    static std::mutex mu;
+    static int n_cu = 0;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        if (!n_cu) {
+            int dev = 0;
+            FV3_HIP(hipGetDevice(&dev));
+            FV3_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+        }
+    }
+    int nw = (ncol + 31) / 32 < 4 * (int64_t)n_cu ? 8 : 4;
+    if (const char* e = getenv("FV3_DENSE_NW")) nw = atoi(e) == 8 ? 8 : 4;
+    if (nc != 2 || m->w1_off8 < 0) nw = 4;
+    const int nt = 64 * nw;
+    if (nw == 8) {
+        a.w1_off = m->w1_off8;
+        a.wh_off = m->wh_off8;
+    }
     const int ncol_tile = 16 * nc;
     a.ntiles = (ncol + ncol_tile - 1) / ncol_tile;
-    // input slots: 256 threads read 256 / ncol_tile feature rows of one variable
-    const int fps = 256 / ncol_tile;
+    // input slots: nt threads read nt / ncol_tile feature rows of one variable
+    const int fps = nt / ncol_tile;
     a.nslots = 0;
     for (int v = 0; v < m->n_in; ++v) {
         const int nf_v = 4 * m->in_nsteps[v], nk_v = m->in_nkeep[v];
@@ -1045,7 +1091,8 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
         else if (!strcmp(e, "4,2")) wpe = 4, rd = 2;
     }
     auto kernel_of = [&](int t4) -> const void* {
-#define FV3_K(T4, NC, W, R) (const void*)dense_forward_kernel<T4, NC, W, R>
+#define FV3_K(T4, NC, W, R) (const void*)dense_forward_kernel<T4, NC, W, R, 4>
+        if (nw == 8) return t4 == 1 ? (const void*)dense_forward_kernel<1, 2, 4, 2, 8> : (const void*)dense_forward_kernel<2, 2, 4, 2, 8>;
         if (nc == 1) {
             if (wpe == 3) return t4 == 1 ? FV3_K(1, 1, 3, 2) : t4 == 2 ? FV3_K(2, 1, 3, 2) : FV3_K(4, 1, 3, 2);
             if (wpe == 4) return t4 == 1 ? FV3_K(1, 1, 4, 2) : t4 == 2 ? FV3_K(2, 1, 4, 2) : FV3_K(4, 1, 4, 2);
@@ -1056,11 +1103,9 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
         return t4 == 1 ? FV3_K(1, 2, 2, 3) : t4 == 2 ? FV3_K(2, 2, 2, 3) : FV3_K(4, 2, 2, 3);
 #undef FV3_K
     };
-    const void* kfn = kernel_of(m->ht / 4);
+    const void* kfn = kernel_of(m->ht / nw);
     // persistent blocks: resident blocks per CU x CUs (queried once per kernel);
     // FV3_DENSE_GRID overrides (A/B)
-    static std::mutex mu;
-    static int n_cu = 0;
     struct Resident {
         const void* fn;
         size_t lds;
@@ -1068,23 +1113,18 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
     };
     static std::vector<Resident> resident;  // keyed by kernel and LDS size (models differ in LDS)
     std::lock_guard<std::mutex> lock(mu);
-    if (!n_cu) {
-        int dev = 0;
-        FV3_HIP(hipGetDevice(&dev));
-        FV3_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-    }
     int res = 0;
     for (auto& r : resident)
         if (r.fn == kfn && r.lds == lds) res = r.blocks;
     if (!res) {
-        FV3_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&res, kfn, 256, lds));
+        FV3_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&res, kfn, nt, lds));
         res = std::max(1, res);
         resident.push_back({kfn, lds, res});
     }
     int64_t grid = std::min<int64_t>(a.ntiles, (int64_t)res * n_cu);
     if (const char* e = getenv("FV3_DENSE_GRID")) grid = std::min<int64_t>(a.ntiles, std::max(1, atoi(e)));
     void* kargs[] = {&a};
-    FV3_HIP(hipLaunchKernel(kfn, dim3((unsigned)grid), dim3(256), kargs, lds, s));
+    FV3_HIP(hipLaunchKernel(kfn, dim3((unsigned)grid), dim3(nt), kargs, lds, s));
     FV3_LAUNCH_CHECK();
     return FV3_OK;
 }

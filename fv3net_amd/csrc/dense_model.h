@@ -79,6 +79,7 @@ struct B3Pack;  // dense_b3.hip: the bf16x3 weight stream and its constants
 struct fv3_dense_model {
     int n_in = 0, n_out = 0, k_in = 0, k_out = 0, width = 0, ht = 0, hp = 0, n_hidden = 0;
     int kp = 0, n_otiles = 0, steps_total = 0;
+    int w1_off8 = -1, wh_off8 = -1;  // layer-1 / hidden streams packed for 8-wave blocks (-1: none)
     std::vector<int> in_nz, out_nz, in_z0, in_nkeep, in_step0, in_nsteps, out_residual;
     std::vector<float> in_log_eps;
     std::vector<fv3::DenseOutTile> otiles;
