@@ -133,8 +133,9 @@ __device__ __forceinline__ void tile_sync()
 #endif
 }
 
-// column data is touched once per launch: streamed past L2 so the weights (re-read by
-// every tile) stay resident there across launches
+// column data: plain loads / stores.  Measured (tools/et_ab.sh): nontemporal input
+// loads cost the emulator 4% (its residual outputs re-read the inputs), nontemporal
+// stores cost the stepper 8% (its next kernel reads the tendencies); C48 gains < 1%
 __device__ __forceinline__ float in_load(const float* p)
 {
 #ifdef FV3_EXP_NOINLOAD  // experiment only (results invalid): no input loads
@@ -142,20 +143,9 @@ __device__ __forceinline__ float in_load(const float* p)
     asm volatile("v_mov_b32 %0, 1.0" : "=v"(v));
     return v;
 #endif
-#ifdef FV3_EXP_TEMPORAL
     return *p;
-#else
-    return __builtin_nontemporal_load(p);
-#endif
 }
-__device__ __forceinline__ void out_store(float* p, float v)
-{
-#ifdef FV3_EXP_TEMPORAL
-    *p = v;
-#else
-    __builtin_nontemporal_store(v, p);
-#endif
-}
+__device__ __forceinline__ void out_store(float* p, float v) { *p = v; }
 
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.0f, 0.0f, 0.0f, 0.0f}; }
 
