@@ -361,7 +361,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
     };
     // the register-prefetched slots: 32-bit element offsets (the host checks every
     // slot's span fits), one branch-free load per slot (a lane that must not read
-    // loads a constant instead and keeps 0)
+    // loads the slot's first element instead; unused slots point at a valid array)
     auto load_raw = [&](KArgs& pk, int64_t tile, int fq) {
         int64_t blk, ii;
         const bool valid = col_of(tile, blk, ii);
@@ -371,8 +371,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
             const int meta = pk.slot_meta[q];
             const bool on = valid && fq < ((meta >> 8) & 0xff);
             const unsigned off = b32 * (unsigned)pk.slot_bs[q] + i32 + (unsigned)fq * (unsigned)pk.slot_ld[q];
-            const float v = in_load(on ? pk.slot_base[q] + off : pk.in_mean);
-            raw[q] = on ? v : 0.0f;
+            // mask, not a select of pointers: the compiler turns that into a branch per
+            // slot, with the descriptor reads and an lgkmcnt(0) wait inside each
+            // no select here: consuming the value right away makes the compiler wait for
+            // each load in turn; staging zeroes the lanes past a slot's rows anyway
+            raw[q] = in_load(pk.slot_base[q] + (off & (0u - (unsigned)on)));
         });
     };
     // normalise and write the staged inputs in B-operand order: for column tile c,
@@ -403,15 +406,33 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
     auto store_x_fast = [&](KArgs& pk, int64_t tile, int fq) {
         int64_t blk, ii;
         const bool valid = col_of(tile, blk, ii);
-        const int tpart = (fq & 3) * 64 + cl16 * 4 + (fq >> 2);
+        // branch-free in three batches (descriptors, constants, values) so the scalar and
+        // LDS reads of all slots are in flight together; lanes past a slot's rows are
+        // zeroed with a bit mask and write to the dummy word (index select, not pointer
+        // select: the compiler turns either of those into a branch per slot)
+        float* const L = reinterpret_cast<float*>(lds);
+        const int tidx = (int)(xc - L) + (fq & 3) * 64 + cl16 * 4 + (fq >> 2);
+        const int didx = (int)(s_dummy - L);
+        int mt[kRawSlots];
+        float mu[kRawSlots], rv[kRawSlots];
         static_for<kRawSlots>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
-            const int meta = pk.slot_meta[q];
+            mt[q] = pk.slot_meta[q];
+        });
+        static_for<kRawSlots>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            const int f = min(((mt[q] >> 16) & 0x7ff) + fq, p.kp - 1);
+            mu[q] = s_mean[f];
+            rv[q] = s_denom[f];
+        });
+        static_for<kRawSlots>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            const int meta = mt[q];
             const int fdst = (meta >> 16) & 0x7ff;
-            const int f = min(fdst + fq, p.kp - 1);
-            float y = (raw[q] - s_mean[f]) * s_denom[f];
-            y = (valid && fq < ((meta >> 8) & 0xff)) ? y : 0.0f;
-            *(fq < (meta & 0xff) ? xc + ((fdst >> 4) * 256 + ((fdst >> 2) & 3)) + tpart : s_dummy) = y;
+            const float y = (raw[q] - mu[q]) * rv[q];
+            const unsigned keep = 0u - (unsigned)(valid && fq < ((meta >> 8) & 0xff));
+            L[fq < (meta & 0xff) ? tidx + ((fdst >> 4) * 256 + ((fdst >> 2) & 3)) : didx] =
+                __builtin_bit_cast(float, __builtin_bit_cast(unsigned, y) & keep);
         });
         for (int f = 4 * p.in_steps_total + fq; f < p.kp; f += FPS) xc[xidx(f)] = 0.0f;
     };
@@ -1047,6 +1068,11 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
             a.slot_leps[q] = m->in_log_eps[v];
             a.has_log |= m->in_log_eps[v] > 0.0f;
         }
+    }
+    for (int q = a.nslots; q < kMaxSlots; ++q) {  // unused slots: meta 0 (no rows), a valid base
+        a.slot_base[q] = inputs[0];
+        a.slot_bs[q] = a.slot_ld[q] = a.slot_meta[q] = 0;
+        a.slot_leps[q] = 0.0f;
     }
     {
         bool fast = !a.has_log && a.nslots <= kRawSlots;
