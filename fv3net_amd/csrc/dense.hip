@@ -337,7 +337,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
     const int fq0 = threadIdx.x / NCOL;  // feature row of this thread within a slot
 
     // ---- input slots: issue every load of a tile at once ----
-    float raw[kRawSlots];
+    // slots prefetched into registers: kRawSlots x 8 feature rows (160) whatever FPS
+    constexpr int RS = kRawSlots * 8 / FPS;
+    float raw[RS];
     auto col_of = [&](int64_t tile, int64_t& blk, int64_t& ii) {
         const int64_t col = tile * NCOL + cb;
         const bool valid = col < p.ncol;
@@ -366,7 +368,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         int64_t blk, ii;
         const bool valid = col_of(tile, blk, ii);
         const unsigned b32 = (unsigned)blk, i32 = (unsigned)ii;
-        static_for<kRawSlots>([&](auto qc) {
+        static_for<RS>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
             const int meta = pk.slot_meta[q];
             const bool on = valid && fq < ((meta >> 8) & 0xff);
@@ -413,19 +415,19 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         float* const L = reinterpret_cast<float*>(lds);
         const int tidx = (int)(xc - L) + (fq & 3) * 64 + cl16 * 4 + (fq >> 2);
         const int didx = (int)(s_dummy - L);
-        int mt[kRawSlots];
-        float mu[kRawSlots], rv[kRawSlots];
-        static_for<kRawSlots>([&](auto qc) {
+        int mt[RS];
+        float mu[RS], rv[RS];
+        static_for<RS>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
             mt[q] = pk.slot_meta[q];
         });
-        static_for<kRawSlots>([&](auto qc) {
+        static_for<RS>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
             const int f = min(((mt[q] >> 16) & 0x7ff) + fq, p.kp - 1);
             mu[q] = s_mean[f];
             rv[q] = s_denom[f];
         });
-        static_for<kRawSlots>([&](auto qc) {
+        static_for<RS>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
             const int meta = mt[q];
             const int fdst = (meta >> 16) & 0x7ff;
@@ -440,8 +442,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         int64_t blk, ii;
         const bool valid = col_of(tile, blk, ii);
         constexpr int B = 5;  // slots per batch: descriptors and constants read before any use
-        static_assert(kRawSlots % B == 0, "");
-        static_for<kRawSlots / B>([&](auto bc) {
+        static_assert(RS % B == 0, "");
+        static_for<RS / B>([&](auto bc) {
             constexpr int b = decltype(bc)::value;
             int mt[B];
             float le[B], mu[B], dn[B];
@@ -461,7 +463,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
             });
         });
         // inputs wider than the register prefetch: batches of 8 loads in flight
-        for (int q0 = kRawSlots; q0 < pk.nslots; q0 += 8) {
+        for (int q0 = RS; q0 < pk.nslots; q0 += 8) {
             float xt[8];
             int mt[8];
             static_for<8>([&](auto ic) {
@@ -1075,7 +1077,7 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
         a.slot_leps[q] = 0.0f;
     }
     {
-        bool fast = !a.has_log && a.nslots <= kRawSlots;
+        bool fast = !a.has_log && a.nslots <= kRawSlots * 8 / fps;  // the kernel's register slots
         const int64_t nblk = (ncol + nb - 1) / nb;
         for (int q = 0; q < a.nslots; ++q) {
             const int fdst = (a.slot_meta[q] >> 16) & 0x7ff;

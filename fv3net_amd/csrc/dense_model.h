@@ -11,7 +11,7 @@ namespace fv3 {
 constexpr int kMaxVars = 16;
 constexpr int kMaxOutTiles = 64;
 constexpr int kMaxSlots = 96;   // input feature rows per tile / (256 / columns per tile)
-constexpr int kRawSlots = 20;   // slots prefetched into registers across tiles
+constexpr int kRawSlots = 20;   // slots prefetched into registers across tiles at 8 rows per slot
 constexpr int kMaxUnits = 3;    // output units per wave per pass (register budget: 3 waves/SIMD)
 
 struct DenseInVar {
@@ -66,7 +66,7 @@ struct DenseArgs {
     int in_steps_total, nslots;
     int lds_x;              // f32x4 offset of the constants area (after activations / inputs)
     int has_log;            // any slot with a LogTransform (selects the staging variant)
-    int fast_stage;         // every slot FPS-aligned, <= kRawSlots slots, no log, 32-bit
+    int fast_stage;         // every slot FPS-aligned, all in registers, no log, 32-bit
                             // element offsets: the short staging path (buffer loads)
     long long* trace;       // profiling hook (fv3_dense_set_trace): [tiles][8] timestamps, or NULL
 };
