@@ -145,7 +145,6 @@ __device__ __forceinline__ float in_load(const float* p)
 #endif
     return *p;
 }
-__device__ __forceinline__ void out_store(float* p, float v) { *p = v; }
 
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.0f, 0.0f, 0.0f, 0.0f}; }
 
@@ -674,10 +673,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
                 const int m = (wave + NW * (i0 + i)) / NC;
                 const int ovar = p.otile[m].var, oz0 = p.otile[m].z0, onrow = p.otile[m].nrow;
                 if (ovar < 0) continue;
-                float* dst = p.out_ptr[ovar] + oblk * p.out_bs[ovar] + oii;
-                const int64_t ld = p.out_ld[ovar];
-                const float* rsrc = p.res_ptr[ovar] ? p.res_ptr[ovar] + oblk * p.res_bs[ovar] + oii : nullptr;
-                const int64_t rld = p.res_ld[ovar];
+                // buffer stores at 32-bit byte offsets (the host checks the spans): a lane
+                // that must not store (padding rows, columns past the end) gets an offset
+                // past the range and its store is dropped, so no branch per row
+                const Rsrc ro = make_rsrc(p.out_ptr[ovar], 0x7ffffffc);
+                const unsigned ob = (unsigned)oblk * (unsigned)p.out_bs[ovar] + (unsigned)oii;
+                const unsigned old_ = (unsigned)p.out_ld[ovar];
+                const bool has_res = p.res_ptr[ovar] != nullptr;  // uniform
+                const Rsrc rres = make_rsrc(has_res ? p.res_ptr[ovar] : p.out_ptr[ovar], 0x7ffffffc);
+                const unsigned rb = (unsigned)oblk * (unsigned)p.res_bs[ovar] + (unsigned)oii;
+                const unsigned rld = (unsigned)p.res_ld[ovar];
                 int fo = 16 * m + 4 * kr;
                 asm volatile("" : "+v"(fo));  // keep this unit's constant reads here, not hoisted above the GEMM
                 const f32x4 bo = *reinterpret_cast<const f32x4*>(s_ep + fo);
@@ -695,14 +700,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
                     if (y < lo[r]) y = lo[r];
                     if (y >= hi[r]) y = hi[r];
                     y = y * mk[r];
-                    if (cvalid && row < onrow) {  // padding rows of the last tile: no reads either
-                        if (rsrc) y = in_load(rsrc + (int64_t)(oz0 + row) * rld) + y;  // after = before + to
-#ifdef FV3_EXP_NOSTORE  // experiment only (results invalid): keep the value, skip the store
-                        asm volatile("" ::"v"(y));
-#else
-                        out_store(dst + (int64_t)(oz0 + row) * ld, y);
-#endif
+                    const bool ok = cvalid && row < onrow;  // padding rows of the last tile: no reads either
+                    if (has_res) {  // after = before + to (Difference.backward)
+                        const unsigned roff = ok ? (rb + (unsigned)(oz0 + row) * rld) * 4u : 0x80000000u;
+                        y = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rres, (int)roff, 0, 0)) + y;
                     }
+                    const unsigned off = ok ? (ob + (unsigned)(oz0 + row) * old_) * 4u : 0x80000000u;
+#ifdef FV3_EXP_NOSTORE  // experiment only (results invalid): keep the value, skip the store
+                    asm volatile("" ::"v"(y), "v"(off));
+#else
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, (int)off, 0, 0);
+#endif
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -1012,6 +1020,18 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
         FV3_REQUIRE(outputs[v], "dense_forward: output %d is NULL", v);
         FV3_REQUIRE(layout_ok(out_l[v], ncol) && out_l[v].ncol_blk == nb,
                     "dense_forward: output %d layout invalid or ncol_blk differs", v);
+        {  // the epilogue stores (and residual reads) at 32-bit byte offsets below 2^31
+            const int64_t nblk = (ncol + nb - 1) / nb;
+            auto span = [&](const fv3_layout& l, int nz) {
+                return (nblk > 1 ? (nblk - 1) * l.blk_stride : 0) + (std::min<int64_t>(nb, ncol) - 1) +
+                       (int64_t)(nz - 1) * l.ld;
+            };
+            const int r = m->out_residual[v];
+            FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED,
+                             span(out_l[v], m->out_nz[v]) < ((int64_t)1 << 29) &&
+                                 (r < 0 || span(in_l[r], m->out_nz[v]) < ((int64_t)1 << 29)),
+                             "dense_forward: output %d spans more than 2^29 elements", v);
+        }
         a.out_ptr[v] = outputs[v];
         a.out_ld[v] = out_l[v].ld;
         a.out_bs[v] = out_l[v].blk_stride;

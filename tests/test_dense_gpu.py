@@ -149,3 +149,28 @@ def test_c384_throughput_shape_and_determinism(gpu):
         assert torch.isfinite(x).all()
     got = [_to_samples(o[:, :, :8, :8].cpu().numpy()) for o in a]
     _check(got, dense_predict(sub, m.oracle_params(), np.float64))
+
+
+@pytest.mark.parametrize("res,precision", [(7, "f32"), (48, "f32"), (7, "bf16x3"), (48, "bf16x3")])
+def test_writes_stay_inside_outputs(gpu, res, precision):
+    """Outputs as level slices of larger (tile, z, y, x) buffers pre-filled with NaN:
+    the kernels write exactly the model's rows of the real columns (the f32 epilogue
+    drops padding rows and columns past the end with range-checked buffer stores).
+    C7: 294 columns, a ragged last tile for both kernels' tile widths."""
+    import torch
+
+    rng = np.random.default_rng(res)
+    T, q = _c48_state(rng, n=res)
+    samples = [_to_samples(T), _to_samples(q)]
+    m = _model(dict(input_variables=["air_temperature", "specific_humidity"],
+                    output_variables=["dQ1", "dQ2"], in_nz=[79, 79], out_nz=[79, 79],
+                    width=256, depth=3), samples=samples)
+    bigs = [torch.full((6, 90, res, res), float("nan"), device="cuda") for _ in range(2)]
+    outs = [b[:, 5:84] for b in bigs]
+    m.forward([torch.from_numpy(T).cuda(), torch.from_numpy(q).cuda()], level_axes=[1, 1],
+              outputs=outs, out_level_axis=1, precision=precision)
+    torch.cuda.synchronize()
+    for b in bigs:
+        assert torch.isnan(b[:, :5]).all() and torch.isnan(b[:, 84:]).all()
+    got = [_to_samples(o.cpu().numpy()) for o in outs]
+    _check(got, dense_predict(samples, m.oracle_params(), np.float64), rtol=RTOL if precision == "f32" else 5e-5)
