@@ -400,20 +400,30 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         *(fq < (meta & 0xff) ? xc + xidx(f) : s_dummy) = y;
     };
     auto feat = [&](int meta, int fq) { return min(((meta >> 16) & 0x7ff) + fq, p.kp - 1); };
-    // ---- the short staging path (p.fast_stage: slots FPS-aligned, all in registers, no
-    // LogTransform): the staging address splits into a per-slot scalar part and a
-    // per-thread part: with fdst a multiple of FPS,
+    // ---- the short staging path (p.fast_stage: every slot FPS-aligned; log inputs and
+    // slots past the register prefetch included): the staging address splits into a
+    // per-slot scalar part and a per-thread part: with fdst a multiple of FPS,
     //   xidx(fdst + fq) = (fdst >> 4) * 256 + ((fdst >> 2) & 3) + [(fq & 3) * 64 + cl16 * 4 + (fq >> 2)]
-    auto store_x_fast = [&](KArgs& pk, int64_t tile, int fq) {
+    // the short staging path's per-slot store (fdst a multiple of FPS); lanes past a
+    // slot's rows are zeroed with a bit mask and write to the dummy word (an index
+    // select, not a pointer select: the compiler turns that into a branch per slot)
+    float* const L = reinterpret_cast<float*>(lds);
+    const int didx = (int)(s_dummy - L);
+    auto put_fast = [&](int meta, float x, float le, float mu, float rv, bool valid, int tidx, int fq, auto logc) {
+        const int fdst = (meta >> 16) & 0x7ff;
+        if constexpr (decltype(logc)::value)
+            if (le > 0.0f) x = __logf_exact(x, le);  // LogTransform.forward (transforms.py:123-124); uniform
+        const float y = (x - mu) * rv;
+        const unsigned keep = 0u - (unsigned)(valid && fq < ((meta >> 8) & 0xff));
+        L[fq < (meta & 0xff) ? tidx + ((fdst >> 4) * 256 + ((fdst >> 2) & 3)) : didx] =
+            __builtin_bit_cast(float, __builtin_bit_cast(unsigned, y) & keep);
+    };
+    auto store_x_fast = [&](KArgs& pk, int64_t tile, int fq, auto logc) {
         int64_t blk, ii;
         const bool valid = col_of(tile, blk, ii);
-        // branch-free in three batches (descriptors, constants, values) so the scalar and
-        // LDS reads of all slots are in flight together; lanes past a slot's rows are
-        // zeroed with a bit mask and write to the dummy word (index select, not pointer
-        // select: the compiler turns either of those into a branch per slot)
-        float* const L = reinterpret_cast<float*>(lds);
+        // in batches (descriptors, constants, values) so the scalar and LDS reads of all
+        // slots are in flight together
         const int tidx = (int)(xc - L) + (fq & 3) * 64 + cl16 * 4 + (fq >> 2);
-        const int didx = (int)(s_dummy - L);
         int mt[RS];
         float mu[RS], rv[RS];
         static_for<RS>([&](auto qc) {
@@ -428,13 +438,38 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         });
         static_for<RS>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
-            const int meta = mt[q];
-            const int fdst = (meta >> 16) & 0x7ff;
-            const float y = (raw[q] - mu[q]) * rv[q];
-            const unsigned keep = 0u - (unsigned)(valid && fq < ((meta >> 8) & 0xff));
-            L[fq < (meta & 0xff) ? tidx + ((fdst >> 4) * 256 + ((fdst >> 2) & 3)) : didx] =
-                __builtin_bit_cast(float, __builtin_bit_cast(unsigned, y) & keep);
+            put_fast(mt[q], raw[q], decltype(logc)::value ? pk.slot_leps[q] : 0.0f, mu[q], rv[q], valid, tidx, fq,
+                     logc);
         });
+        // slots past the register prefetch (wide inputs, e.g. the emulator's 736
+        // features): batches of 8, every load of a batch in flight before any use
+        const unsigned b32 = (unsigned)blk, i32 = (unsigned)ii;
+        for (int q0 = RS; q0 < pk.nslots; q0 += 8) {
+            int mw[8];
+            float xw[8], mw_mu[8], mw_rv[8];
+            static_for<8>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                mw[i] = q0 + i < pk.nslots ? pk.slot_meta[q0 + i] : 0;  // uniform
+            });
+            static_for<8>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                const int q = min(q0 + i, kMaxSlots - 1);  // past nslots: meta 0, any valid base
+                const bool on = valid && fq < ((mw[i] >> 8) & 0xff);
+                const unsigned off = b32 * (unsigned)pk.slot_bs[q] + i32 + (unsigned)fq * (unsigned)pk.slot_ld[q];
+                xw[i] = in_load(pk.slot_base[q] + (off & (0u - (unsigned)on)));
+            });
+            static_for<8>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                const int f = min(((mw[i] >> 16) & 0x7ff) + fq, p.kp - 1);
+                mw_mu[i] = s_mean[f];
+                mw_rv[i] = s_denom[f];
+            });
+            static_for<8>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                put_fast(mw[i], xw[i], decltype(logc)::value ? pk.slot_leps[min(q0 + i, kMaxSlots - 1)] : 0.0f, mw_mu[i], mw_rv[i],
+                         valid, tidx, fq, logc);
+            });
+        }
         for (int f = 4 * p.in_steps_total + fq; f < p.kp; f += FPS) xc[xidx(f)] = 0.0f;
     };
     auto store_x = [&](KArgs& pk, int64_t tile, int fq, auto logc) {
@@ -572,8 +607,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         KArgs* pt = &p;
         asm volatile("" : "+s"(pt));
 #ifndef FV3_EXP_NOSTAGE  // experiment only (results invalid): no input staging
-        if (p.fast_stage)
-            store_x_fast(*pt, tile, fq);
+        if (p.fast_stage && p.has_log)
+            store_x_fast(*pt, tile, fq, std::true_type{});
+        else if (p.fast_stage)
+            store_x_fast(*pt, tile, fq, std::false_type{});
         else if (p.has_log)
             store_x(*pt, tile, fq, std::true_type{});
         else
@@ -1097,7 +1134,7 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
         a.slot_leps[q] = 0.0f;
     }
     {
-        bool fast = !a.has_log && a.nslots <= kRawSlots * 8 / fps;  // the kernel's register slots
+        bool fast = true;
         const int64_t nblk = (ncol + nb - 1) / nb;
         for (int q = 0; q < a.nslots; ++q) {
             const int fdst = (a.slot_meta[q] >> 16) & 0x7ff;

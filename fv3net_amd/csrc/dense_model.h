@@ -66,8 +66,7 @@ struct DenseArgs {
     int in_steps_total, nslots;
     int lds_x;              // f32x4 offset of the constants area (after activations / inputs)
     int has_log;            // any slot with a LogTransform (selects the staging variant)
-    int fast_stage;         // every slot FPS-aligned, all in registers, no log, 32-bit
-                            // element offsets: the short staging path (buffer loads)
+    int fast_stage;         // every slot FPS-aligned: the short staging path
     long long* trace;       // profiling hook (fv3_dense_set_trace): [tiles][8] timestamps, or NULL
 };
 static_assert(sizeof(DenseArgs) <= 4096, "kernel arguments are limited to 4 KiB");
