@@ -1083,7 +1083,17 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
     // fastest at C48 and C384); FV3_DENSE_NC=1 for A/B
     // wide-input models (the microphysics emulator: 736 padded features) stage 32
     // columns in > 64 KiB of LDS, i.e. one block per CU: use 16-column tiles there
-    int nc = (size_t)2 * 16 * 4 * m->kp > 64 * 1024 ? 1 : 2;
+    // (with 8-wave blocks, wide inputs keep 32-column tiles at one block per CU: the
+    // emulator 7.12 -> 6.66 ms; 16-column tiles remain for widths < 128)
+    const bool wide = (size_t)2 * 16 * 4 * m->kp > 64 * 1024;
+    // LDS of a block: activations (NC x HT tiles x 64 lanes x 16 B) or the staged inputs
+    // (NC x kp features x 16 columns), whichever is larger, then the constants and one
+    // dummy f32x4 (the staging stores of lanes past a slot's rows land there)
+    auto lds_of = [&](int c) {
+        const size_t hb = (size_t)c * 16 * 64 * (size_t)m->ht, xb = (size_t)c * sizeof(float) * 16 * (size_t)m->kp;
+        return std::max(hb, xb) + sizeof(float) * (2 * (size_t)m->kp + 6 * 16 * (size_t)m->n_otiles) + 16;
+    };
+    int nc = wide && (m->w1_off8 < 0 || lds_of(2) > 160 * 1024) ? 1 : 2;
     if (const char* e = getenv("FV3_DENSE_NC")) nc = atoi(e) == 1 ? 1 : 2;
     // waves per block: with few tiles per CU (C48: 1.7) 8 waves, two per SIMD on one
     // tile and each wave half the hidden units (C48 47.7 -> 46.7 us); with many, 4
@@ -1099,7 +1109,7 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
             FV3_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
         }
     }
-    int nw = (ncol + 31) / 32 < 4 * (int64_t)n_cu ? 8 : 4;
+    int nw = (wide || (ncol + 31) / 32 < 4 * (int64_t)n_cu) ? 8 : 4;
     if (const char* e = getenv("FV3_DENSE_NW")) nw = atoi(e) == 8 ? 8 : 4;
     if (nc != 2 || m->w1_off8 < 0) nw = 4;
     const int nt = 64 * nw;
@@ -1149,14 +1159,9 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
         a.fast_stage = fast;
     }
     hipStream_t s = (hipStream_t)stream;
-    // LDS: activations (NC x HT tiles x 64 lanes x 16 B) or the staged inputs
-    // (NC x kp features x 16 columns), whichever is larger, then the constants
-    const size_t hbytes = (size_t)nc * 16 * 64 * (size_t)m->ht;
-    const size_t xbytes = (size_t)nc * sizeof(float) * 16 * (size_t)m->kp;
-    const size_t abytes = std::max(hbytes, xbytes);
+    const size_t abytes = std::max((size_t)nc * 16 * 64 * (size_t)m->ht, (size_t)nc * sizeof(float) * 16 * (size_t)m->kp);
     a.lds_x = (int)(abytes / 16);
-    // + one dummy f32x4: the staging stores of lanes past a slot's rows land there
-    const size_t lds = abytes + sizeof(float) * (2 * (size_t)m->kp + 6 * 16 * (size_t)m->n_otiles) + 16;
+    const size_t lds = lds_of(nc);
     FV3_REQUIRE(lds <= 160 * 1024, "dense_forward: %d input features need too much LDS", m->kp);
     // (waves per SIMD targeted by register allocation, weight ring depth):
     // FV3_DENSE_CFG = "3,2" (default) | "2,3" | "4,2" (A/B)
