@@ -1095,9 +1095,9 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
     };
     int nc = wide && (m->w1_off8 < 0 || lds_of(2) > 160 * 1024) ? 1 : 2;
     if (const char* e = getenv("FV3_DENSE_NC")) nc = atoi(e) == 1 ? 1 : 2;
-    // waves per block: with few tiles per CU (C48: 1.7) 8 waves, two per SIMD on one
-    // tile and each wave half the hidden units (C48 47.7 -> 46.7 us); with many, 4
-    // (C384: 2.32 vs 2.36 ms).  Needs 32-column tiles and width >= 128.
+    // waves per block: 8, two per SIMD on one tile and each wave half the hidden units,
+    // measured faster than 4 at every size after the staging work (C48 42.8 vs 47.9 us,
+    // C96 141 vs 147 us, C384 2.15 vs 2.18 ms).  Needs 32-column tiles and width >= 128.
     // FV3_DENSE_NW=4|8 for A/B
     static std::mutex mu;
     static int n_cu = 0;
@@ -1109,7 +1109,7 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
             FV3_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
         }
     }
-    int nw = (wide || (ncol + 31) / 32 < 4 * (int64_t)n_cu) ? 8 : 4;
+    int nw = 8;
     if (const char* e = getenv("FV3_DENSE_NW")) nw = atoi(e) == 8 ? 8 : 4;
     if (nc != 2 || m->w1_off8 < 0) nw = 4;
     const int nt = 64 * nw;
