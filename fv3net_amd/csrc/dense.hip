@@ -30,9 +30,10 @@
 //    order (every A-operand fetch is one coalesced T4*4 B/lane load) and stream
 //    through 3-deep compile-time register rings; each layer's first two groups are
 //    loaded before the barrier that precedes it, so no layer starts on a cold ring;
-//  * the output layer: unit (otile m, column tile c) with c = wave % NC fixed per
-//    wave; every wave runs all its units in one pass (up to kMaxUnits accumulators)
-//    and the bias/denorm/limit/mask epilogue reads its constants from LDS;
+//  * the output layer: whole 16-row output tiles dealt to the waves (one weight fetch
+//    feeds both column tiles), the remainder split into (tile, column tile) units so
+//    every SIMD gets the same work; the bias/denorm/limit/mask epilogue reads its
+//    constants from LDS and writes with range-checked buffer stores;
 //  * each input variable's features and each output tile are padded so a k-step
 //    (4 features) never straddles two variables.
 // Roofline: fp32 MFMA-bound.  2*(k_in*w + (n_hidden-1)*w*w + w*k_out) FLOP per
@@ -260,46 +261,48 @@ __device__ __forceinline__ void gemm_hidden(f32x4 (&acc)[NC][T4], const f32x4* _
     });
 }
 
-// output units of this wave: unit i = wave + NW * (i0 + i), otile m = unit / NC;
-// soff[i] = byte offset of unit i's weights (group 0) in the model allocation
-struct OutPlan {
-    int soff[kMaxUnits];
-    int n;  // units in this pass
-};
-
-template <int RD>
-__device__ __forceinline__ void prime_out(f32x4 (&g)[RD][kMaxUnits], Rsrc rw, int voff, const OutPlan& pl)
+// o[i][c] = W_{m_i}^T h_c for N output tiles over all HT*4 k-steps and NCC column
+// tiles: one weight fragment feeds NCC MFMAs (src = column tile c0's activations; the
+// next column tile is HT*64 f32x4 further); soff[i] = byte offset of tile i's weights
+constexpr int kOutTiles = 2;  // output tiles per wave per pass
+template <int HT, int N, int NCC, int RD>
+__device__ __forceinline__ void gemm_out_tiles(f32x4 (&o)[kOutTiles][2], const f32x4* __restrict__ src, Rsrc rw,
+                                               int voff, const int (&soff)[kOutTiles],
+                                               f32x4 (&g)[RD][kOutTiles])
 {
+    f32x4 bq[2][NCC];
 #pragma unroll
-    for (int i = 0; i < kMaxUnits; ++i)
-        if (i < pl.n) {
-#pragma unroll
-            for (int d = 0; d + 1 < RD; ++d) g[d][i] = bload<f32x4>(rw, voff, pl.soff[i] + d * 1024);
-        }
-}
-
-// o[i] = W_m^T h for N units over all HT*4 k-steps; B operands of column tile cw
-template <int HT, int N, int RD>
-__device__ __forceinline__ void gemm_out(f32x4 (&o)[kMaxUnits], const f32x4* __restrict__ src, Rsrc rw, int voff,
-                                         const OutPlan& pl, f32x4 (&g)[RD][kMaxUnits])
-{
-    f32x4 bq[2];
-    bq[0] = src[0];
+    for (int c = 0; c < NCC; ++c) bq[0][c] = src[(c * HT) * 64];
     static_for<HT>([&](auto tc) {
         constexpr int t = decltype(tc)::value;
         if constexpr (t + RD - 1 < HT) {
 #pragma unroll
-            for (int i = 0; i < N; ++i)
-                g[(t + RD - 1) % RD][i] = bload<f32x4>(rw, voff, pl.soff[i] + (t + RD - 1) * 1024);
+            for (int i = 0; i < N; ++i) g[(t + RD - 1) % RD][i] = bload<f32x4>(rw, voff, soff[i] + (t + RD - 1) * 1024);
         }
-        if constexpr (t + 1 < HT) bq[(t + 1) % 2] = src[(t + 1) * 64];
+        if constexpr (t + 1 < HT) {
+#pragma unroll
+            for (int c = 0; c < NCC; ++c) bq[(t + 1) % 2][c] = src[(c * HT + t + 1) * 64];
+        }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int i = 0; i < N; ++i)
-                o[i] = mfma4(g[t % RD][i][r], bq[t % 2][r], o[i]);
+#pragma unroll
+                for (int c = 0; c < NCC; ++c) o[i][c] = mfma4(g[t % RD][i][r], bq[t % 2][c][r], o[i][c]);
     });
+}
+
+template <int RD>
+__device__ __forceinline__ void prime_out_tiles(f32x4 (&g)[RD][kOutTiles], Rsrc rw, int voff, const int (&soff)[kOutTiles],
+                                                int n)
+{
+#pragma unroll
+    for (int i = 0; i < kOutTiles; ++i)
+        if (i < n) {
+#pragma unroll
+            for (int d = 0; d + 1 < RD; ++d) g[d][i] = bload<f32x4>(rw, voff, soff[i] + d * 1024);
+        }
 }
 
 typedef __attribute__((address_space(4))) const DenseArgs KArgs;
@@ -571,27 +574,40 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
     }
 #endif
 
-    // output plan of this wave
-    const int nunits = p.n_otiles * NC;
-    const int cw = wave % NC;  // (wave + NW i) % NC: one column tile per wave
-    const int ucnt = nunits > wave ? (nunits - wave + NW - 1) / NW : 0;
-    auto plan = [&](int i0) {
-        OutPlan pl;
-        pl.n = min(kMaxUnits, ucnt - i0);
+    // output plan of this wave.  The first (n_otiles / NW) * NW output tiles go whole to
+    // the waves (tile m to wave m % NW): one weight fetch feeds both column tiles.  The
+    // rest are split into (tile, column tile) units dealt round-robin, so every SIMD
+    // still gets the same number of units (C48's 10 tiles on 8 waves: one whole tile
+    // per wave plus one unit on waves 0-3)
+    const int n_whole = p.n_otiles / NW;           // whole tiles per wave (every wave the same)
+    const int m_split = n_whole * NW;              // first split tile
+    const int n_units = (p.n_otiles - m_split) * NC;
+    const int n_split = n_units > wave ? (n_units - wave + NW - 1) / NW : 0;  // split units of this wave
+    auto whole_soff = [&](int j0, int (&so)[kOutTiles]) {  // tiles wave + NW*(j0+i); returns how many
+        const int n = min(kOutTiles, n_whole - j0);
 #pragma unroll
-        for (int i = 0; i < kMaxUnits; ++i) {
-            const int u = wave + NW * (i0 + min(i, pl.n - 1));
-            pl.soff[i] = p.wo_off + (u / NC) * (HP / 16) * 1024;
-        }
-        return pl;
+        for (int i = 0; i < kOutTiles; ++i) so[i] = p.wo_off + (wave + NW * (j0 + min(i, n - 1))) * (HP / 16) * 1024;
+        return n;
     };
-    f32x4 go[RD][kMaxUnits];
+    auto split_unit = [&](int k, int& m, int& c) {
+        const int u = wave + NW * k;
+        m = m_split + u / NC;
+        c = u % NC;
+    };
+    f32x4 go[RD][kOutTiles];
     FT gh[RD][4];
     auto prime_after = [&](int l) {  // prime the ring of the layer that follows hidden layer l
         if (l + 1 < p.n_hidden_extra) {
             prime_ring<RD, NW, FT>(gh, rw, voff, p.wh_off + (l + 1) * (HP / 4) * KS);
-        } else if (ucnt > 0) {
-            prime_out<RD>(go, rw, voff_o, plan(0));
+        } else if (n_whole > 0) {
+            int so[kOutTiles];
+            const int n = whole_soff(0, so);
+            prime_out_tiles<RD>(go, rw, voff_o, so, n);
+        } else if (n_split > 0) {
+            int m, c;
+            split_unit(0, m, c);
+            const int so[kOutTiles] = {p.wo_off + m * (HP / 16) * 1024, p.wo_off + m * (HP / 16) * 1024};
+            prime_out_tiles<RD>(go, rw, voff_o, so, 1);
         }
     };
     tile_sync();
@@ -687,70 +703,91 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         trace_mark(p, tile, 3);
 
         // ---- output Dense layers + bias/denorm/limit/mask epilogue ----
-        const f32x4* src = hbuf + (cw * HT) * 64 + lane;
-        const int64_t colw = tile * NCOL + 16 * cw + (lane & 15);
-        const bool cvalid = colw < p.ncol;
-        const int64_t cc = cvalid ? colw : 0;
-        const int64_t oblk = p.ncol_blk >= p.ncol ? 0 : cc / p.ncol_blk;
-        const int64_t oii = cc - oblk * p.ncol_blk;
-        for (int i0 = 0; i0 < ucnt; i0 += kMaxUnits) {
-            const OutPlan pl = plan(i0);
-            if (i0 > 0) prime_out<RD>(go, rw, voff_o, pl);
-            f32x4 o[kMaxUnits];
+        unsigned ob_c[NC], oi_c[NC];  // per column tile: block and in-block index of this lane's column
+        bool cv_c[NC];
 #pragma unroll
-            for (int i = 0; i < kMaxUnits; ++i) o[i] = zero4();
-            switch (pl.n) {
-                case 1: gemm_out<HT, 1, RD>(o, src, rw, voff_o, pl, go); break;
-                case 2: gemm_out<HT, 2, RD>(o, src, rw, voff_o, pl, go); break;
-                default: gemm_out<HT, kMaxUnits, RD>(o, src, rw, voff_o, pl, go); break;
-            }
+        for (int c = 0; c < NC; ++c) {
+            const int64_t colw = tile * NCOL + 16 * c + (lane & 15);
+            cv_c[c] = colw < p.ncol;
+            const int64_t cc = cv_c[c] ? colw : 0;
+            const int64_t oblk = p.ncol_blk >= p.ncol ? 0 : cc / p.ncol_blk;
+            ob_c[c] = (unsigned)oblk;
+            oi_c[c] = (unsigned)(cc - oblk * p.ncol_blk);
+        }
+        // bias / denorm / OutputLimit / mask of output tile m, column tile c, then the store
+        auto epilogue = [&](int m, int c, const f32x4& acc) {
+            const int ovar = p.otile[m].var, oz0 = p.otile[m].z0, onrow = p.otile[m].nrow;
+            if (ovar < 0) return;
+            // buffer stores at 32-bit byte offsets (the host checks the spans): a lane that
+            // must not store (padding rows, columns past the end) gets an offset past the
+            // range and its store is dropped, so no branch per row
+            const Rsrc ro = make_rsrc(p.out_ptr[ovar], 0x7ffffffc);
+            const unsigned ob = ob_c[c] * (unsigned)p.out_bs[ovar] + oi_c[c];
+            const unsigned old_ = (unsigned)p.out_ld[ovar];
+            const bool has_res = p.res_ptr[ovar] != nullptr;  // uniform
+            const Rsrc rres = make_rsrc(has_res ? p.res_ptr[ovar] : p.out_ptr[ovar], 0x7ffffffc);
+            const unsigned rb = ob_c[c] * (unsigned)p.res_bs[ovar] + oi_c[c];
+            const unsigned rld = (unsigned)p.res_ld[ovar];
+            int fo = 16 * m + 4 * kr;
+            asm volatile("" : "+v"(fo));  // keep this tile's constant reads here, not hoisted above the GEMM
+            const f32x4 bo = *reinterpret_cast<const f32x4*>(s_ep + fo);
+            const f32x4 sg = *reinterpret_cast<const f32x4*>(s_ep + kop + fo);
+            const f32x4 mu = *reinterpret_cast<const f32x4*>(s_ep + 2 * kop + fo);
+            const f32x4 lo = *reinterpret_cast<const f32x4*>(s_ep + 3 * kop + fo);
+            const f32x4 hi = *reinterpret_cast<const f32x4*>(s_ep + 4 * kop + fo);
+            const f32x4 mk = *reinterpret_cast<const f32x4*>(s_ep + 5 * kop + fo);
 #pragma unroll
-            for (int i = 0; i < kMaxUnits; ++i) {
-                if (i >= pl.n) break;
-                const int m = (wave + NW * (i0 + i)) / NC;
-                const int ovar = p.otile[m].var, oz0 = p.otile[m].z0, onrow = p.otile[m].nrow;
-                if (ovar < 0) continue;
-                // buffer stores at 32-bit byte offsets (the host checks the spans): a lane
-                // that must not store (padding rows, columns past the end) gets an offset
-                // past the range and its store is dropped, so no branch per row
-                const Rsrc ro = make_rsrc(p.out_ptr[ovar], 0x7ffffffc);
-                const unsigned ob = (unsigned)oblk * (unsigned)p.out_bs[ovar] + (unsigned)oii;
-                const unsigned old_ = (unsigned)p.out_ld[ovar];
-                const bool has_res = p.res_ptr[ovar] != nullptr;  // uniform
-                const Rsrc rres = make_rsrc(has_res ? p.res_ptr[ovar] : p.out_ptr[ovar], 0x7ffffffc);
-                const unsigned rb = (unsigned)oblk * (unsigned)p.res_bs[ovar] + (unsigned)oii;
-                const unsigned rld = (unsigned)p.res_ld[ovar];
-                int fo = 16 * m + 4 * kr;
-                asm volatile("" : "+v"(fo));  // keep this unit's constant reads here, not hoisted above the GEMM
-                const f32x4 bo = *reinterpret_cast<const f32x4*>(s_ep + fo);
-                const f32x4 sg = *reinterpret_cast<const f32x4*>(s_ep + kop + fo);
-                const f32x4 mu = *reinterpret_cast<const f32x4*>(s_ep + 2 * kop + fo);
-                const f32x4 lo = *reinterpret_cast<const f32x4*>(s_ep + 3 * kop + fo);
-                const f32x4 hi = *reinterpret_cast<const f32x4*>(s_ep + 4 * kop + fo);
-                const f32x4 mk = *reinterpret_cast<const f32x4*>(s_ep + 5 * kop + fo);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = 4 * kr + r;
-                    float y = o[i][r] + bo[r];
-                    y = y * sg[r];
-                    y = y + mu[r];
-                    if (y < lo[r]) y = lo[r];
-                    if (y >= hi[r]) y = hi[r];
-                    y = y * mk[r];
-                    const bool ok = cvalid && row < onrow;  // padding rows of the last tile: no reads either
-                    if (has_res) {  // after = before + to (Difference.backward)
-                        const unsigned roff = ok ? (rb + (unsigned)(oz0 + row) * rld) * 4u : 0x80000000u;
-                        y = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rres, (int)roff, 0, 0)) + y;
-                    }
-                    const unsigned off = ok ? (ob + (unsigned)(oz0 + row) * old_) * 4u : 0x80000000u;
-#ifdef FV3_EXP_NOSTORE  // experiment only (results invalid): keep the value, skip the store
-                    asm volatile("" ::"v"(y), "v"(off));
-#else
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, (int)off, 0, 0);
-#endif
+            for (int r = 0; r < 4; ++r) {
+                const int row = 4 * kr + r;
+                float y = acc[r] + bo[r];
+                y = y * sg[r];
+                y = y + mu[r];
+                if (y < lo[r]) y = lo[r];
+                if (y >= hi[r]) y = hi[r];
+                y = y * mk[r];
+                const bool ok = cv_c[c] && row < onrow;  // padding rows of the last tile: no reads either
+                if (has_res) {  // after = before + to (Difference.backward)
+                    const unsigned roff = ok ? (rb + (unsigned)(oz0 + row) * rld) * 4u : 0x80000000u;
+                    y = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rres, (int)roff, 0, 0)) + y;
                 }
-                __builtin_amdgcn_sched_barrier(0);
+                const unsigned off = ok ? (ob + (unsigned)(oz0 + row) * old_) * 4u : 0x80000000u;
+#ifdef FV3_EXP_NOSTORE  // experiment only (results invalid): keep the value, skip the store
+                asm volatile("" ::"v"(y), "v"(off));
+#else
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, (int)off, 0, 0);
+#endif
             }
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        // whole output tiles: both column tiles per weight fetch
+        for (int j0 = 0; j0 < n_whole; j0 += kOutTiles) {
+            int so[kOutTiles];
+            const int n = whole_soff(j0, so);
+            if (j0 > 0) prime_out_tiles<RD>(go, rw, voff_o, so, n);
+            f32x4 o[kOutTiles][2];
+#pragma unroll
+            for (int i = 0; i < kOutTiles; ++i) o[i][0] = o[i][1] = zero4();
+            if (n == 1)
+                gemm_out_tiles<HT, 1, NC, RD>(o, hbuf + lane, rw, voff_o, so, go);
+            else
+                gemm_out_tiles<HT, kOutTiles, NC, RD>(o, hbuf + lane, rw, voff_o, so, go);
+#pragma unroll
+            for (int i = 0; i < kOutTiles; ++i) {
+                if (i >= n) break;
+#pragma unroll
+                for (int c = 0; c < NC; ++c) epilogue(wave + NW * (j0 + i), c, o[i][c]);
+            }
+        }
+        // the remaining tiles, split into (tile, column tile) units
+        for (int k = 0; k < n_split; ++k) {
+            int m, c;
+            split_unit(k, m, c);
+            const int so[kOutTiles] = {p.wo_off + m * (HP / 16) * 1024, p.wo_off + m * (HP / 16) * 1024};
+            if (k > 0 || n_whole > 0) prime_out_tiles<RD>(go, rw, voff_o, so, 1);
+            f32x4 o[kOutTiles][2];
+            o[0][0] = zero4();
+            gemm_out_tiles<HT, 1, 1, RD>(o, hbuf + c * HT * 64 + lane, rw, voff_o, so, go);
+            epilogue(m, c, o[0][0]);
         }
         prime_ring<RD, NW, FT>(g1, rw, voff, p.w1_off);  // the next tile's layer 1
         tile_sync();         // the activations are free for the next tile's inputs

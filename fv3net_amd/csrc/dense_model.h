@@ -12,7 +12,6 @@ constexpr int kMaxVars = 16;
 constexpr int kMaxOutTiles = 64;
 constexpr int kMaxSlots = 96;   // input feature rows per tile / (256 / columns per tile)
 constexpr int kRawSlots = 20;   // slots prefetched into registers across tiles at 8 rows per slot
-constexpr int kMaxUnits = 3;    // output units per wave per pass (register budget: 3 waves/SIMD)
 
 struct DenseInVar {
     const float* ptr;
