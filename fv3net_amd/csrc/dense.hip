@@ -51,6 +51,15 @@
 #include "common.h"
 #include "dense_model.h"
 
+// output tiles per wave per pass and output-weight ring depth (A/B: OUT_TILES=2,
+// OUT_RING=2 was 0.5% slower at C96-C384, equal at C48)
+#ifndef OUT_TILES
+#define OUT_TILES 1
+#endif
+#ifndef OUT_RING
+#define OUT_RING 3
+#endif
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -264,7 +273,8 @@ __device__ __forceinline__ void gemm_hidden(f32x4 (&acc)[NC][T4], const f32x4* _
 // o[i][c] = W_{m_i}^T h_c for N output tiles over all HT*4 k-steps and NCC column
 // tiles: one weight fragment feeds NCC MFMAs (src = column tile c0's activations; the
 // next column tile is HT*64 f32x4 further); soff[i] = byte offset of tile i's weights
-constexpr int kOutTiles = 2;  // output tiles per wave per pass
+constexpr int kOutTiles = OUT_TILES;  // output tiles per wave per pass
+constexpr int kOutRing = OUT_RING;    // output-weight ring depth (groups held; refilled kOutRing-1 ahead)
 template <int HT, int N, int NCC, int RD>
 __device__ __forceinline__ void gemm_out_tiles(f32x4 (&o)[kOutTiles][2], const f32x4* __restrict__ src, Rsrc rw,
                                                int voff, const int (&soff)[kOutTiles],
@@ -594,7 +604,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         m = m_split + u / NC;
         c = u % NC;
     };
-    f32x4 go[RD][kOutTiles];
+    f32x4 go[kOutRing][kOutTiles];
     FT gh[RD][4];
     auto prime_after = [&](int l) {  // prime the ring of the layer that follows hidden layer l
         if (l + 1 < p.n_hidden_extra) {
@@ -602,12 +612,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         } else if (n_whole > 0) {
             int so[kOutTiles];
             const int n = whole_soff(0, so);
-            prime_out_tiles<RD>(go, rw, voff_o, so, n);
+            prime_out_tiles<kOutRing>(go, rw, voff_o, so, n);
         } else if (n_split > 0) {
             int m, c;
             split_unit(0, m, c);
-            const int so[kOutTiles] = {p.wo_off + m * (HP / 16) * 1024, p.wo_off + m * (HP / 16) * 1024};
-            prime_out_tiles<RD>(go, rw, voff_o, so, 1);
+            int so[kOutTiles];
+#pragma unroll
+            for (int i = 0; i < kOutTiles; ++i) so[i] = p.wo_off + m * (HP / 16) * 1024;
+            prime_out_tiles<kOutRing>(go, rw, voff_o, so, 1);
         }
     };
     tile_sync();
@@ -763,14 +775,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         for (int j0 = 0; j0 < n_whole; j0 += kOutTiles) {
             int so[kOutTiles];
             const int n = whole_soff(j0, so);
-            if (j0 > 0) prime_out_tiles<RD>(go, rw, voff_o, so, n);
+            if (j0 > 0) prime_out_tiles<kOutRing>(go, rw, voff_o, so, n);
             f32x4 o[kOutTiles][2];
 #pragma unroll
             for (int i = 0; i < kOutTiles; ++i) o[i][0] = o[i][1] = zero4();
             if (n == 1)
-                gemm_out_tiles<HT, 1, NC, RD>(o, hbuf + lane, rw, voff_o, so, go);
+                gemm_out_tiles<HT, 1, NC, kOutRing>(o, hbuf + lane, rw, voff_o, so, go);
             else
-                gemm_out_tiles<HT, kOutTiles, NC, RD>(o, hbuf + lane, rw, voff_o, so, go);
+                gemm_out_tiles<HT, kOutTiles, NC, kOutRing>(o, hbuf + lane, rw, voff_o, so, go);
 #pragma unroll
             for (int i = 0; i < kOutTiles; ++i) {
                 if (i >= n) break;
@@ -782,11 +794,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         for (int k = 0; k < n_split; ++k) {
             int m, c;
             split_unit(k, m, c);
-            const int so[kOutTiles] = {p.wo_off + m * (HP / 16) * 1024, p.wo_off + m * (HP / 16) * 1024};
-            if (k > 0 || n_whole > 0) prime_out_tiles<RD>(go, rw, voff_o, so, 1);
+            int so[kOutTiles];
+#pragma unroll
+            for (int i = 0; i < kOutTiles; ++i) so[i] = p.wo_off + m * (HP / 16) * 1024;
+            if (k > 0 || n_whole > 0) prime_out_tiles<kOutRing>(go, rw, voff_o, so, 1);
             f32x4 o[kOutTiles][2];
             o[0][0] = zero4();
-            gemm_out_tiles<HT, 1, 1, RD>(o, hbuf + c * HT * 64 + lane, rw, voff_o, so, go);
+            gemm_out_tiles<HT, 1, 1, kOutRing>(o, hbuf + c * HT * 64 + lane, rw, voff_o, so, go);
             epilogue(m, c, o[0][0]);
         }
         prime_ring<RD, NW, FT>(g1, rw, voff, p.w1_off);  // the next tile's layer 1
