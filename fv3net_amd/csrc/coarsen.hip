@@ -212,9 +212,15 @@ __global__ __launch_bounds__(512) void regrid_coarsen_kernel(CoarsenArgs<DT> a)
         col.next = 0;
         col.km = km;
         col.kn = km;
+#ifndef FV3_EXP_NOPPM
         PpmCursor<FineCol<DT>> cur(col, km, km, a.iv, a.kord);
+#endif
         for (int k = 0; k < km; ++k) {
+#ifdef FV3_EXP_NOPPM  // experiment only (results invalid): no remap, the field's own level
+            const float q2 = col.q1(k + 1);
+#else
             const float q2 = cur.next();
+#endif
             // _mask_weights (regridz.py:150-161): area where phalf_c_on_f[k+1] < phalf_f[-1]
             // (compared in delp's dtype); the masked area stays float32 (coarsen.py:213-215)
             const float w = (pcc[k + 1] < pbot) ? area : 0.0f;
