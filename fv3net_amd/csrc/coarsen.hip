@@ -35,6 +35,8 @@
 // Measured VALU-bound like the standalone mappm (the PPM arithmetic with its IEEE
 // divisions dominates).
 #define FV3_HD __host__ __device__
+#include <cstdlib>
+
 #include "common.h"
 #include "mappm_core.h"
 
@@ -53,6 +55,7 @@ struct CoarsenArgs {
     float* delp_out;
     int n_fields, ntile, km, ny, nx, f, iv, kord;
     double ptop;
+    float* scratch;   // [km][gridDim * blockDim]: each lane's remapped column (input-driven path), or NULL
 };
 
 constexpr int kChunk = 16;  // delp*area levels staged per pass-1 round
@@ -120,8 +123,13 @@ struct FineCol {
         return (float)run;
     }
     __device__ __forceinline__ float pe2(int k) const { return (float)pc[k - 1]; }
-    __device__ __forceinline__ void emit(int, float) {}
+    __device__ __forceinline__ void emit(int k, float v)
+    {
+        if (out) out[(int64_t)(k - 1) * ostride] = v;
+    }
     __device__ __forceinline__ float next_edge(int k) const { return (k + 1 <= kn + 1) ? pe2(k + 1) : 0.0f; }
+    float* out = nullptr;  // this lane's remapped column in the scratch (stride ostride), or NULL
+    int64_t ostride = 0;
 };
 
 template <typename DT>
@@ -212,21 +220,32 @@ __global__ __launch_bounds__(512) void regrid_coarsen_kernel(CoarsenArgs<DT> a)
         col.next = 0;
         col.km = km;
         col.kn = km;
-#ifndef FV3_EXP_NOPPM
-        PpmCursor<FineCol<DT>> cur(col, km, km, a.iv, a.kord);
-#endif
-        for (int k = 0; k < km; ++k) {
-#ifdef FV3_EXP_NOPPM  // experiment only (results invalid): no remap, the field's own level
-            const float q2 = col.q1(k + 1);
-#else
-            const float q2 = cur.next();
-#endif
-            // _mask_weights (regridz.py:150-161): area where phalf_c_on_f[k+1] < phalf_f[-1]
-            // (compared in delp's dtype); the masked area stays float32 (coarsen.py:213-215)
+        // _mask_weights (regridz.py:150-161): area where phalf_c_on_f[k+1] < phalf_f[-1]
+        // (compared in delp's dtype); the masked area stays float32 (coarsen.py:213-215)
+        auto level_sum = [&](int k, float q2) {
             const float w = (pcc[k + 1] < pbot) ? area : 0.0f;
             const float r = row_sum<float>(nan0(q2 * w), f, base);
             if (active && dx == 0) rs[(k * f + dy) * C + cell] = r;
+        };
+#ifdef FV3_EXP_NOPPM  // experiment only (results invalid): no remap, the field's own level
+        for (int k = 0; k < km; ++k) level_sum(k, col.q1(k + 1));
+#else
+        if (a.scratch) {
+            // input-driven remap (the streaming mappm, uniform over input layers: every
+            // lane ingests layer L together) into this lane's scratch column, then the
+            // per-level masked row sums read it back (each lane only its own values)
+            const int64_t sstride = (int64_t)gridDim.x * blockDim.x;
+            float* const mine = a.scratch + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+            col.out = mine;
+            col.ostride = sstride;
+            mappm_ppm_column(col, km, km, a.iv, a.kord);
+            for (int k = 0; k < km; ++k) level_sum(k, mine[(int64_t)k * sstride]);
+        } else {
+            // output-driven cursor: no scratch, but the per-lane layer loops diverge
+            PpmCursor<FineCol<DT>> cur(col, km, km, a.iv, a.kord);
+            for (int k = 0; k < km; ++k) level_sum(k, cur.next());
         }
+#endif
         __syncthreads();
         float* o = a.out[v] + (int64_t)tile * km * cplane + crow;
         for (int i = threadIdx.x; i < km * C; i += blockDim.x) {
@@ -486,8 +505,16 @@ int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* f
                        std::max(sizeof(float) * (size_t)km * 64, sizeof(DT) * kChunk * 64);
     FV3_REQUIRE(lds <= 160 * 1024, "regrid_coarsen: %zu B of LDS needed", lds);
     FV3_REQUIRE(blocks < (int64_t)0x7fffffff, "regrid_coarsen: grid too large");
+    // per-lane remapped columns for the input-driven path: km x (blocks x 64 f) floats from
+    // the stream-ordered pool (C384 79 levels: ~285 MB, reused by every field of the call;
+    // FV3_COARSEN_CURSOR=1 selects the scratch-free output-driven path for A/B)
+    void* scratch = nullptr;
+    if (n_fields > 0 && !getenv("FV3_COARSEN_CURSOR"))
+        FV3_HIP(hipMallocAsync(&scratch, sizeof(float) * (size_t)km * (size_t)blocks * 64 * factor, s));
+    a.scratch = (float*)scratch;
     hipLaunchKernelGGL(regrid_coarsen_kernel<DT>, dim3((unsigned)blocks), dim3(64 * factor), lds, s, a);
     FV3_LAUNCH_CHECK();
+    if (scratch) FV3_HIP(hipFreeAsync(scratch, s));
     return FV3_OK;
 }
 
