@@ -105,12 +105,18 @@ def _smooth_state(rng, nt, km, ny, nx):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("path", ["scratch", "cursor"])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("factor,n", [(1, 4), (2, 16), (3, 12), (4, 24), (8, 48)])
-def test_kernel_vs_oracle_random(gpu, factor, n, dtype):
+def test_kernel_vs_oracle_random(gpu, factor, n, dtype, path, monkeypatch):
     """Bit-identical to the oracle for every factor (numpy's block-sum order) and
-    both delp dtypes (the arithmetic follows delp's dtype, as the reference does)."""
+    both delp dtypes (the arithmetic follows delp's dtype, as the reference does), on
+    both remap paths: the input-driven streaming remap through a per-lane scratch
+    column (default) and the scratch-free output-driven cursor (FV3_COARSEN_CURSOR)."""
     from fv3net_amd.coarsen import coarsen_on_pressure
+
+    if path == "cursor":
+        monkeypatch.setenv("FV3_COARSEN_CURSOR", "1")
 
     rng = np.random.default_rng(factor * 100 + n)
     delp, area, T, q = _smooth_state(rng, 6, 79, n, n)
