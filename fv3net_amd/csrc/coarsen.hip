@@ -132,7 +132,10 @@ struct FineCol {
     int64_t ostride = 0;
 };
 
-template <typename DT>
+// SCR: the input-driven remap through the per-lane scratch (default); !SCR: the
+// scratch-free output-driven cursor.  Separate builds, so the default's register
+// allocation does not carry the cursor's.
+template <typename DT, bool SCR>
 __global__ __launch_bounds__(512) void regrid_coarsen_kernel(CoarsenArgs<DT> a)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -230,7 +233,7 @@ __global__ __launch_bounds__(512) void regrid_coarsen_kernel(CoarsenArgs<DT> a)
 #ifdef FV3_EXP_NOPPM  // experiment only (results invalid): no remap, the field's own level
         for (int k = 0; k < km; ++k) level_sum(k, col.q1(k + 1));
 #else
-        if (a.scratch) {
+        if constexpr (SCR) {
             // input-driven remap (the streaming mappm, uniform over input layers: every
             // lane ingests layer L together) into this lane's scratch column, then the
             // per-level masked row sums read it back (each lane only its own values)
@@ -512,7 +515,10 @@ int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* f
     if (n_fields > 0 && !getenv("FV3_COARSEN_CURSOR"))
         FV3_HIP(hipMallocAsync(&scratch, sizeof(float) * (size_t)km * (size_t)blocks * 64 * factor, s));
     a.scratch = (float*)scratch;
-    hipLaunchKernelGGL(regrid_coarsen_kernel<DT>, dim3((unsigned)blocks), dim3(64 * factor), lds, s, a);
+    if (scratch)
+        hipLaunchKernelGGL((regrid_coarsen_kernel<DT, true>), dim3((unsigned)blocks), dim3(64 * factor), lds, s, a);
+    else
+        hipLaunchKernelGGL((regrid_coarsen_kernel<DT, false>), dim3((unsigned)blocks), dim3(64 * factor), lds, s, a);
     FV3_LAUNCH_CHECK();
     if (scratch) FV3_HIP(hipFreeAsync(scratch, s));
     return FV3_OK;
