@@ -307,6 +307,7 @@ struct EdgeArgs {
     float* out[kMaxFields];  // (6, km, nyc_e, nxc_e)
     int n_fields, km, n, f, iv, kord, edge;  // edge 0: "x" (u), 1: "y" (v)
     double ptop;
+    float* scratch;  // [km][gridDim * 64]: each lane's remapped column (input-driven path)
 };
 
 // element offset (level 0) of delp cell (tile t, row r, col c), r/c possibly one past
@@ -362,11 +363,17 @@ struct EdgeCol {
         return (float)run;
     }
     __device__ __forceinline__ float pe2(int k) const { return (float)pc[k - 1]; }
-    __device__ __forceinline__ void emit(int, float) {}
+    __device__ __forceinline__ void emit(int k, float v)
+    {
+        if (out) out[(int64_t)(k - 1) * ostride] = v;
+    }
     __device__ __forceinline__ float next_edge(int k) const { return (k + 1 <= kn + 1) ? pe2(k + 1) : 0.0f; }
+    float* out = nullptr;  // this lane's remapped column in the scratch (stride ostride), or NULL
+    int64_t ostride = 0;
 };
 
-template <typename DT>
+// SCR: input-driven remap through the per-lane scratch (default); !SCR: the cursor
+template <typename DT, bool SCR>
 __global__ __launch_bounds__(64) void regrid_coarsen_edge_kernel(EdgeArgs<DT> a)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -446,14 +453,23 @@ __global__ __launch_bounds__(64) void regrid_coarsen_edge_kernel(EdgeArgs<DT> a)
         col.next = 0;
         col.km = km;
         col.kn = km;
-        PpmCursor<EdgeCol<DT>> cur(col, km, km, a.iv, a.kord);
         float* o = a.out[v] + (int64_t)tile * km * cplane + (int64_t)Y * ncol_out + Xa;
-        for (int k = 0; k < km; ++k) {
-            const float q2 = cur.next();
+        auto level_sum = [&](int k, float q2) {
             const float w = (pcc[k + 1] < pbot) ? sp : 0.0f;  // _mask_weights (compared in delp's dtype)
             const float num = edge_sum<float>(nan0(q2 * w), f, base, pw);
             const float den = edge_sum<float>(nan0(w), f, base, pw);
             if (active && j == 0) o[(int64_t)k * cplane] = num / den;
+        };
+        if constexpr (SCR) {  // as in regrid_coarsen_kernel: uniform over input layers
+            const int64_t sstride = (int64_t)gridDim.x * 64;
+            float* const mine = a.scratch + (int64_t)blockIdx.x * 64 + threadIdx.x;
+            col.out = mine;
+            col.ostride = sstride;
+            mappm_ppm_column(col, km, km, a.iv, a.kord);
+            for (int k = 0; k < km; ++k) level_sum(k, mine[(int64_t)k * sstride]);
+        } else {
+            PpmCursor<EdgeCol<DT>> cur(col, km, km, a.iv, a.kord);
+            for (int k = 0; k < km; ++k) level_sum(k, cur.next());
         }
     }
 }
@@ -574,9 +590,17 @@ int regrid_coarsen_edge_impl(const DT* delp, const float* spacing, const float* 
     const int ncx = edge == 0 ? nc : nc + 1, ncy = edge == 0 ? nc + 1 : nc;
     const int64_t blocks = (int64_t)6 * ncy * ((ncx + C - 1) / C);
     const size_t lds = sizeof(DT) * (size_t)C * (km + 1);
-    hipLaunchKernelGGL(regrid_coarsen_edge_kernel<DT>, dim3((unsigned)blocks), dim3(64), lds, (hipStream_t)stream,
-                       a);
+    hipStream_t s = (hipStream_t)stream;
+    void* scratch = nullptr;  // per-lane remapped columns (see regrid_coarsen_impl)
+    if (n_fields > 0 && !getenv("FV3_COARSEN_CURSOR"))
+        FV3_HIP(hipMallocAsync(&scratch, sizeof(float) * (size_t)km * (size_t)blocks * 64, s));
+    a.scratch = (float*)scratch;
+    if (scratch)
+        hipLaunchKernelGGL((regrid_coarsen_edge_kernel<DT, true>), dim3((unsigned)blocks), dim3(64), lds, s, a);
+    else
+        hipLaunchKernelGGL((regrid_coarsen_edge_kernel<DT, false>), dim3((unsigned)blocks), dim3(64), lds, s, a);
     FV3_LAUNCH_CHECK();
+    if (scratch) FV3_HIP(hipFreeAsync(scratch, s));
     return FV3_OK;
 }
 

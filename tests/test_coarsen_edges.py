@@ -153,10 +153,15 @@ def _winds_state(rng, km, n, dtype):
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("factor,n", [(1, 4), (2, 16), (3, 12), (4, 24), (8, 48)])
-def test_kernel_vs_oracle_random(gpu, factor, n, dtype):
+@pytest.mark.parametrize("path", ["scratch", "cursor"])
+def test_kernel_vs_oracle_random(gpu, factor, n, dtype, path, monkeypatch):
     """Bit-identical to the oracle for both edges, every factor (numpy's order:
-    pairwise along x, sequential along y) and both delp dtypes."""
+    pairwise along x, sequential along y), both delp dtypes and both remap paths
+    (input-driven through the scratch column, and the output-driven cursor)."""
     from fv3net_amd.coarsen import coarsen_edges_on_pressure
+
+    if path == "cursor":
+        monkeypatch.setenv("FV3_COARSEN_CURSOR", "1")
 
     rng = np.random.default_rng(factor * 10 + n)
     delp, u, v, dx, dy = _winds_state(rng, 40, n, dtype)
