@@ -15,6 +15,8 @@
 #include "common.h"
 #include "mappm_core.h"
 
+#include <cstdlib>
+
 namespace fv3 {
 namespace {
 
@@ -43,6 +45,17 @@ struct LdsScr {
     __device__ __forceinline__ float& g(int k) { return base[plane + k * stride]; }
 };
 
+// The same [2][km+3][column] scratch in global memory (stream-ordered allocation):
+// coalesced like the column arrays, and unlike LDS (42 KB per 64 columns at km = 79,
+// i.e. 3 waves per CU) it leaves occupancy to the VGPR budget.
+struct GlobalScr {
+    float* base;     // scratch + column
+    int64_t stride;  // padded column count
+    int64_t plane;   // (km+3) * stride
+    __device__ __forceinline__ float& e(int k) { return base[k * stride]; }
+    __device__ __forceinline__ float& g(int k) { return base[plane + k * stride]; }
+};
+
 struct MappmArgs {
     const float* pe1;
     const float* q1;
@@ -51,6 +64,7 @@ struct MappmArgs {
     fv3_layout l_pe1, l_q1, l_pe2, l_q2;
     int64_t ncol;
     int km, kn, iv, kord;
+    float* scratch;  // kord > 7: [2][km+3][grid * block] (NULL: the LDS path)
 };
 
 __device__ __forceinline__ DevCol make_col(const MappmArgs& a, int64_t c)
@@ -86,11 +100,31 @@ __global__ __launch_bounds__(64) void mappm_cs_kernel(MappmArgs a)
     mappm_cs_column(col, scr, a.km, a.kn, a.iv, a.kord);
 }
 
+__global__ __launch_bounds__(256) void mappm_cs_global_kernel(MappmArgs a)
+{
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.ncol) return;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    GlobalScr scr{a.scratch + c, stride, (int64_t)(a.km + 3) * stride};
+    DevCol col = make_col(a, c);
+    mappm_cs_column(col, scr, a.km, a.kn, a.iv, a.kord);
+}
+
 }  // namespace
 
-int launch_mappm(const MappmArgs& a, hipStream_t stream)
+int launch_mappm(MappmArgs a, hipStream_t stream)
 {
     if (a.ncol == 0) return FV3_OK;
+    if (a.kord > 7 && !getenv("FV3_MAPPM_LDS")) {
+        const int block = 256;
+        const int64_t grid = (a.ncol + block - 1) / block;
+        FV3_HIP(hipMallocAsync((void**)&a.scratch, sizeof(float) * 2 * (size_t)(a.km + 3) * (size_t)grid * block,
+                               stream));
+        hipLaunchKernelGGL(mappm_cs_global_kernel, dim3((unsigned)grid), dim3(block), 0, stream, a);
+        FV3_LAUNCH_CHECK();
+        FV3_HIP(hipFreeAsync(a.scratch, stream));
+        return FV3_OK;
+    }
     if (a.kord > 7) {
         const int block = 64;
         const size_t lds = sizeof(float) * 2 * (size_t)(a.km + 3) * block;
@@ -125,7 +159,7 @@ extern "C" int fv3_mappm_ex(const float* pe1, fv3_layout pe1_l, const float* q1,
                               fv3::layout_ok(pe2_l, ncol) && fv3::layout_ok(q2_l, ncol)),
                 "mappm: invalid column layout");
     FV3_REQUIRE(ncol / 256 < (int64_t)0x7fffffff, "mappm: ncol too large");
-    MappmArgs a{pe1, q1, pe2, q2, pe1_l, q1_l, pe2_l, q2_l, ncol, km, kn, iv, kord};
+    MappmArgs a{pe1, q1, pe2, q2, pe1_l, q1_l, pe2_l, q2_l, ncol, km, kn, iv, kord, nullptr};
     return fv3::launch_mappm(a, (hipStream_t)stream);
 }
 

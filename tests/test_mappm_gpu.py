@@ -81,6 +81,21 @@ def test_random_vs_oracle_bit_exact(gpu, km, kn, ncol):
             assert _bits_equal(res, oracle_mappm(pe1, q, pe2, iv, kord)), (kord, iv)
 
 
+@pytest.mark.parametrize("km,kn,ncol", [(5, 9, 257), (79, 79, 777), (127, 40, 300)])
+def test_cs_lds_path_vs_oracle_bit_exact(gpu, km, kn, ncol, monkeypatch):
+    """kord > 7 with the edge-solve scratch in LDS (FV3_MAPPM_LDS=1) instead of the
+    default global scratch: the same arithmetic, bit-identical."""
+    from fv3net_amd.mappm import mappm_device
+
+    monkeypatch.setenv("FV3_MAPPM_LDS", "1")
+    rng = np.random.default_rng(km * kn + ncol)
+    pe1, q, pe2 = _columns(rng, km, kn, ncol)
+    for kord in (8, 10, 13, 17):
+        for iv in (0, 1, -1, 2):
+            res = mappm_device(pe1, q, pe2, iv, kord).cpu().numpy()
+            assert _bits_equal(res, oracle_mappm(pe1, q, pe2, iv, kord)), (kord, iv)
+
+
 def test_tile_layout_in_place(gpu):
     """(tile, z, y, x) restart-shaped arrays remapped in place via fv3_mappm_ex."""
     import torch
