@@ -20,6 +20,9 @@
 namespace fv3 {
 namespace {
 
+// The remap consumer emits q2(k) for k = 1, 2, ... and asks for next_edge(k) for
+// k = 2, 3, ... strictly in order, so both walk running pointers: no per-lane 64-bit
+// index multiply per output level.
 struct DevCol {
     const float* pe1_;
     const float* q1_;
@@ -27,13 +30,21 @@ struct DevCol {
     float* q2_;
     int64_t ld_pe1, ld_q1, ld_pe2, ld_q2;
     int kn;
+    const float* pe2_next;  // pe2(k + 1) for the next next_edge(k)
     __device__ __forceinline__ float q1(int k) const { return q1_[(int64_t)(k - 1) * ld_q1]; }
     __device__ __forceinline__ float pe1(int k) const { return pe1_[(int64_t)(k - 1) * ld_pe1]; }
     __device__ __forceinline__ float pe2(int k) const { return pe2_[(int64_t)(k - 1) * ld_pe2]; }
-    __device__ __forceinline__ void emit(int k, float v) { q2_[(int64_t)(k - 1) * ld_q2] = v; }
-    __device__ __forceinline__ float next_edge(int k) const
+    __device__ __forceinline__ void emit(int, float v)
     {
-        return (k + 1 <= kn + 1) ? pe2(k + 1) : 0.0f;
+        *q2_ = v;
+        q2_ += ld_q2;
+    }
+    __device__ __forceinline__ float next_edge(int k)
+    {
+        if (k + 1 > kn + 1) return 0.0f;
+        const float r = *pe2_next;
+        pe2_next += ld_pe2;
+        return r;
     }
 };
 
@@ -79,6 +90,7 @@ __device__ __forceinline__ DevCol make_col(const MappmArgs& a, int64_t c)
     d.ld_pe2 = a.l_pe2.ld;
     d.ld_q2 = a.l_q2.ld;
     d.kn = a.kn;
+    d.pe2_next = d.pe2_ + 2 * d.ld_pe2;
     return d;
 }
 
