@@ -6,9 +6,10 @@
 // One thread per column; the column-fastest [level][column] layout (Fortran's
 // pe1(i,k)) makes every per-level load a coalesced 256 B wave access.  The
 // per-column algorithm is the one-pass streaming formulation in mappm_core.h:
-// kord <= 7 runs entirely in registers (no LDS, no scratch); kord > 7 solves
-// cs_profile's tridiagonal edge system into LDS (2 x (km+2) floats per column,
-// [level][lane] so every access is bank-conflict free), then streams.
+// kord <= 7 runs entirely in registers (no LDS, no scratch) -- or, below
+// kLevelsMaxCols columns, one block per column with a lane per level; kord > 7 solves
+// cs_profile's tridiagonal edge system into a [2][km+3][column] scratch in global
+// memory (coalesced; LDS kept behind FV3_MAPPM_LDS), then streams.
 // Roofline: HBM-bound at (km+1 + km + kn+1 + kn) * 4 B per column, with ~150
 // VALU ops per input level (including ~7 IEEE divides) close behind.
 #define FV3_HD __host__ __device__
@@ -102,6 +103,175 @@ __global__ __launch_bounds__(256) void mappm_ppm_kernel(MappmArgs a)
     mappm_ppm_column(col, a.km, a.kn, a.iv, a.kord);
 }
 
+// tools/mappm_small_time.py, kord 1 79->79: C48 (13,824 columns) 142 -> 38 us, C96
+// (55,296) 168 -> 118 us; at C384 the serial kernel (0.70 ms) wins.
+constexpr int64_t kLevelsMaxCols = 65536;
+
+// No-op edge source for remap_one (the level-parallel kernel finishes one output
+// layer per lane, so the next edge is never read).
+struct NoEdge {
+    __device__ __forceinline__ float next_edge(int) const { return 0.0f; }
+};
+
+// kord <= 7 with one BLOCK per column and one lane per level: the latency-bound
+// case (config #1: 864 columns = 14 waves of the one-lane-per-column kernel, each
+// walking 79 levels serially).  ppm_profile is a local stencil, so each phase below
+// evaluates one of mappm_ppm_column's per-level expressions for every level at once,
+// with the same helpers and operands, into LDS; the remap then gives each output
+// layer its own lane, which replays remap_one over the input layers it overlaps
+// (mappm.f90:58-124 for one k).  The streaming code starts output k's layer search
+// where output k-1 ended; with non-decreasing pe1 and pe2 that is the first L with
+// pe2(k) <= pe1(L+1), found here by bisection.  A column whose edges are not
+// non-decreasing (or hold NaNs) runs the serial streaming code on lane 0 instead, so
+// every input gives the serial kernel's (bit-exact) result.
+//
+// LDS: 9 (km+2) + (kn+2) floats, 1-based levels.
+__global__ __launch_bounds__(128) void mappm_ppm_levels_kernel(MappmArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int km = a.km, kn = a.kn, n = km + 2;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    float* const q = lds;
+    float* const pe = lds + n;
+    float* const dp = lds + 2 * n;
+    float* const dc = lds + 3 * n;
+    float* const al = lds + 4 * n;  // AL(k); al[km+1] holds ar_km
+    float* const h2 = lds + 5 * n;
+    float* const pal = lds + 6 * n;  // final layer coefficients
+    float* const par = lds + 7 * n;
+    float* const pa6 = lds + 8 * n;
+    float* const pe2 = lds + 9 * n;
+    const int64_t c = blockIdx.x;
+    DevCol col = make_col(a, c);
+
+    for (int k = tid + 1; k <= km + 1; k += nt) {
+        pe[k] = col.pe1(k);
+        if (k <= km) q[k] = col.q1(k);
+    }
+    for (int k = tid + 1; k <= kn + 1; k += nt) pe2[k] = col.pe2(k);
+    __syncthreads();
+    int sorted = 1;
+    for (int k = tid + 1; k <= km; k += nt) {
+        dp[k] = pe[k + 1] - pe[k];
+        sorted &= pe[k] <= pe[k + 1];
+    }
+    for (int k = tid + 1; k <= kn; k += nt) sorted &= pe2[k] <= pe2[k + 1];
+    if (!__syncthreads_and(sorted)) {
+        if (tid == 0) mappm_ppm_column(col, km, kn, a.iv, a.kord);
+        return;
+    }
+    const int iv = a.iv, kord = a.kord;
+    const bool huynh = kord >= 7;
+    // dc(k), k = 2..km-1 (mappm.f90:658-668)
+    for (int k = tid + 2; k <= km - 1; k += nt) dc[k] = ppm_dc(q[k - 1], q[k], q[k + 1], dp[k - 1], dp[k], dp[k + 1]);
+    __syncthreads();
+    // ALraw(m), m = 3..km-1 (mappm.f90:674-683)
+    for (int m = tid + 3; m <= km - 1; m += nt)
+        al[m] = ppm_al(dp[m - 2], dp[m - 1], dp[m], dp[m + 1], q[m - 1], q[m], dc[m - 1], dc[m]);
+    __syncthreads();
+    if (tid == 0) {  // top: area-preserving cubic (mappm.f90:689-725), as in mappm_ppm_column
+        const float d1 = dp[1], d2 = dp[2];
+        const float q1 = q[1], q2 = q[2];
+        const float qm = (d2 * q1 + d1 * q2) / (d1 + d2);
+        const float dq = 2.0f * (q2 - q1) / (d1 + d2);
+        const float c1 = 4.0f * (al[3] - qm - d2 * dq) / (d2 * (2.0f * d2 * d2 + d1 * (d2 + 3.0f * d1)));
+        const float c3 = dq - 0.5f * c1 * (d2 * (5.0f * d1 + d2) - 3.0f * d1 * d1);
+        float al2 = qm - 0.25f * c1 * d1 * d2 * (d2 + 3.0f * d1);
+        float al1 = d1 * (2.0f * c1 * (d1 * d1) - c3) + al2;
+        al2 = fmax2(al2, fmin2(q1, q2));
+        al2 = fmin2(al2, fmax2(q1, q2));
+        dc[1] = 0.5f * (al2 - q1);
+        if (iv == 0) {
+            al1 = fmax2(0.0f, al1);
+            al2 = fmax2(0.0f, al2);
+        } else if (iv == -1) {
+            if (al1 * q1 <= 0.0f) al1 = 0.0f;
+        } else if (iv == 2 || iv == -2) {
+            al1 = q1;
+        }
+        al[1] = al1;
+        al[2] = al2;
+    }
+    if (tid == (1 % nt)) {  // bottom: area-preserving cubic (mappm.f90:729-761)
+        const float d1 = dp[km], d2 = dp[km - 1];
+        const float qk = q[km], qk1 = q[km - 1];
+        const float qm = (d2 * qk + d1 * qk1) / (d1 + d2);
+        const float dq = 2.0f * (qk1 - qk) / (d1 + d2);
+        const float c1 = (al[km - 1] - qm - d2 * dq) / (d2 * (2.0f * d2 * d2 + d1 * (d2 + 3.0f * d1)));
+        const float c3 = dq - 2.0f * c1 * (d2 * (5.0f * d1 + d2) - 3.0f * d1 * d1);
+        float alm = qm - c1 * d1 * d2 * (d2 + 3.0f * d1);
+        float ar = d1 * (8.0f * c1 * (d1 * d1) - c3) + alm;
+        alm = fmax2(alm, fmin2(qk, qk1));
+        alm = fmin2(alm, fmax2(qk, qk1));
+        dc[km] = 0.5f * (qk - alm);
+        if (iv == 0) {
+            alm = fmax2(0.0f, alm);
+            ar = fmax2(0.0f, ar);
+        } else if (iv < 0) {
+            if (qk * ar <= 0.0f) ar = 0.0f;
+        }
+        al[km] = alm;
+        al[km + 1] = ar;
+    }
+    __syncthreads();
+    if (huynh) {  // h2(k), k = 2..km-1 (mappm.f90:784-795)
+        for (int k = tid + 2; k <= km - 1; k += nt) h2[k] = ppm_h2(dc[k - 1], dc[k + 1], dp[k - 1], dp[k], dp[k + 1]);
+        __syncthreads();
+    }
+    int lmt = kord - 3;
+    lmt = lmt > 0 ? lmt : 0;
+    if (iv == 0) lmt = lmt < 2 ? lmt : 2;
+    // final coefficients of every layer (the top of mappm_ppm_column's L loop)
+    for (int L = tid + 1; L <= km; L += nt) {
+        Ppm p{q[L], al[L], al[L + 1], 0.0f};  // al[km+1] = ar_km
+        const float dcL = dc[L];
+        if (L <= 2 || L >= km - 1) {
+            p.a6 = a6_of(p);
+            ppm_limit(dcL, p, 0);
+        } else if (huynh) {
+            ppm_huynh(p, dcL, h2[L - 1], h2[L + 1]);
+            if (iv == 0) ppm_limit(dcL, p, 2);
+        } else {
+            if (kord != 4) p.a6 = a6_of(p);
+            if (kord != 6) ppm_limit(dcL, p, lmt);
+        }
+        pal[L] = p.al;
+        par[L] = p.ar;
+        pa6[L] = p.a6;
+    }
+    __syncthreads();
+    // one output layer per lane
+    const ColumnEnds ends{pe[1], pe[km + 1], q[1], q[km]};
+    NoEdge none;
+    for (int k = tid + 1; k <= kn; k += nt) {
+        RemapState s{k, false, 0.0f, 0.0f, pe2[k], pe2[k + 1]};
+        float val = 0.0f;
+        bool done = false;
+        if (!(s.t <= ends.pe_top) && !(s.t >= ends.pe_bot)) {
+            int lo = 1, hi = km;  // first L in [1, km] with t <= pe1(L+1); exists since t < pe_bot
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (s.t <= pe[mid + 1]) hi = mid; else lo = mid + 1;
+            }
+            for (int L = lo; L <= km && !done; ++L) {
+                const LayerView v{pe[L], pe[L + 1], dp[L], q[L], Ppm{q[L], pal[L], par[L], pa6[L]}};
+                done = remap_one(s, v, ends, none, val);
+            }
+            if (!done) {  // below the last input layer (mappm.f90:115-121); s.accum is set here
+                const float delp = s.b - ends.pe_bot;
+                if (delp > 0.0f) {
+                    s.qsum = s.qsum + delp * ends.q_bot;
+                    s.dpsum = s.dpsum + delp;
+                }
+                val = s.qsum / s.dpsum;
+            }
+        } else {
+            val = (s.t <= ends.pe_top) ? ends.q_top : ends.q_bot;
+        }
+        col.q2_[(int64_t)(k - 1) * col.ld_q2] = val;
+    }
+}
+
 __global__ __launch_bounds__(64) void mappm_cs_kernel(MappmArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -124,6 +294,17 @@ __global__ __launch_bounds__(256) void mappm_cs_global_kernel(MappmArgs a)
 
 }  // namespace
 
+// kord <= 7: the level-parallel kernel while one lane per column leaves the chip
+// mostly idle (FV3_MAPPM_PATH=serial|levels overrides, for tests and A/B).
+bool use_levels_kernel(const MappmArgs& a)
+{
+    const char* p = getenv("FV3_MAPPM_PATH");
+    if (p && p[0] == 's') return false;
+    if (a.km > 1000 || a.kn > 1000) return false;
+    if (p && p[0] == 'l') return true;
+    return a.ncol < kLevelsMaxCols;
+}
+
 int launch_mappm(MappmArgs a, hipStream_t stream)
 {
     if (a.ncol == 0) return FV3_OK;
@@ -143,6 +324,12 @@ int launch_mappm(MappmArgs a, hipStream_t stream)
         FV3_REQUIRE(lds <= 160 * 1024, "mappm: km=%d too large for the kord>7 LDS path", a.km);
         const int64_t grid = (a.ncol + block - 1) / block;
         hipLaunchKernelGGL(mappm_cs_kernel, dim3((unsigned)grid), dim3(block), lds, stream, a);
+    } else if (use_levels_kernel(a)) {
+        const int block = a.km + 1 > 64 ? 128 : 64;
+        const size_t lds = sizeof(float) * (9 * (size_t)(a.km + 2) + (size_t)(a.kn + 2));
+        FV3_REQUIRE(lds <= 64 * 1024, "mappm: km=%d kn=%d too large for the level-parallel path", a.km, a.kn);
+        FV3_REQUIRE(a.ncol <= 0x7fffffff, "mappm: ncol too large for the level-parallel path");
+        hipLaunchKernelGGL(mappm_ppm_levels_kernel, dim3((unsigned)a.ncol), dim3(block), lds, stream, a);
     } else {
         const int block = 256;
         const int64_t grid = (a.ncol + block - 1) / block;

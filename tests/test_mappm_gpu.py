@@ -14,6 +14,14 @@ from oracle.mappm import oracle_mappm
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["serial", "levels"])
+def mappm_path(request, monkeypatch):
+    """Every test runs on both kord <= 7 kernels: one lane per column (`serial`) and
+    one block per column, one lane per level (`levels`, the small-ncol default)."""
+    monkeypatch.setenv("FV3_MAPPM_PATH", request.param)
+    return request.param
+
+
 def _bits_equal(a, b):
     a = np.asarray(a, np.float32)
     b = np.asarray(b, np.float32)
@@ -158,3 +166,33 @@ def test_c384_scale_sampled_bit_exact(gpu):
     idx = np.sort(rng.choice(ncol, 4096, replace=False))
     ref = oracle_mappm(pe1[:, idx], q[:, idx], pe2[:, idx], 1, 1)
     assert _bits_equal(res[:, idx], ref)
+
+
+def test_unsorted_edges_fall_back_per_column(gpu):
+    """Columns whose pe1 or pe2 are not non-decreasing (or hold NaN) take the serial
+    streaming code inside the level-parallel kernel; sorted neighbours in the same launch
+    do not.  Both kernels agree bit for bit.  A negative layer thickness with sorted pe2
+    also matches the oracle; out-of-order or NaN pe2 hits the reference's failed search
+    (mappm.f90:58-124 leaves q2 undefined), where the product writes NaN, so there only
+    the two kernels are compared."""
+    import os as _os
+
+    from fv3net_amd.mappm import mappm_device
+
+    rng = np.random.default_rng(5)
+    km, kn, ncol = 79, 50, 300
+    pe1, q, pe2 = _columns(rng, km, kn, ncol)
+    pe1[40, 1::7] = pe1[39, 1::7] - 5  # a negative layer thickness
+    bad2 = pe2.copy()
+    bad2[10, ::3] = bad2[20, ::3]      # pe2 out of order in every third column
+    bad2[5, 2::11] = np.nan
+    for kord in (1, 4, 6, 7):
+        for iv in (0, 1, -1):
+            for p2, vs_oracle in ((pe2, True), (bad2, False)):
+                _os.environ["FV3_MAPPM_PATH"] = "levels"
+                a = mappm_device(pe1, q, p2, iv, kord).cpu().numpy()
+                _os.environ["FV3_MAPPM_PATH"] = "serial"
+                b = mappm_device(pe1, q, p2, iv, kord).cpu().numpy()
+                assert _bits_equal(a, b), (kord, iv, vs_oracle)
+                if vs_oracle:
+                    assert _bits_equal(a, oracle_mappm(pe1, q, p2, iv, kord)), (kord, iv)
