@@ -64,13 +64,32 @@ __global__ __launch_bounds__(64) void ml_epilogue_kernel(EpilogueArgs<DT> a)
     const DT cv = (DT)(kCp - kRdgas), lv = (DT)kLv, g = (DT)kGravity;
     DT s_h = 0, s_m = 0, s_nm = 0, s_ch = 0;
     int n1 = 0, n2 = 0;
-    // unrolled so several levels' loads are in flight per thread (one wave per 64
-    // columns leaves few waves per CU: C96 = 864 waves); the z sums stay in order
-#pragma unroll 4
-    for (int k = 0; k < a.nz; ++k) {
+    // Levels are fetched in batches of U, the next batch issued before the current one
+    // is processed: with at most one wave per SIMD (C96 = 864 waves) the loads in
+    // flight per thread set the HBM rate.  The explicit batches also keep the loads
+    // ahead of the stores, which the compiler may not reorder itself since temp_out /
+    // sphum_out may alias temp / sphum.  The z sums stay in level order.
+#ifndef FV3_EXP_EPI_U
+#define FV3_EXP_EPI_U 8
+#endif
+    constexpr int U = FV3_EXP_EPI_U;
+    float b_q1[2][U], b_q2[2][U];
+    DT b_sp[2][U], b_dp[2][U], b_t[2][U];
+    const bool want_t = a.temp_out != nullptr;
+    auto fetch = [&](int buf, int k0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = k0 + u < a.nz ? k0 + u : a.nz - 1;  // clamped: re-reads the last level
+            const int64_t i = off + (int64_t)k * a.lay.ld;
+            b_q1[buf][u] = a.dq1[i];
+            b_q2[buf][u] = a.dq2[i];
+            b_sp[buf][u] = a.sphum[i];
+            b_dp[buf][u] = a.delp[i];
+            b_t[buf][u] = want_t ? a.temp[i] : (DT)0;
+        }
+    };
+    auto level = [&](int k, float q1, float q2, DT sp, DT dp, DT t) {
         const int64_t i = off + (int64_t)k * a.lay.ld;
-        const float q1 = a.dq1[i], q2 = a.dq2[i];
-        const DT sp = a.sphum[i], dp = a.delp[i];
         DT q1n, q2n;
         if (a.mse) {
             // update_moisture_tendency_to_ensure_non_negative_humidity (machine_learning.py:77-80)
@@ -101,8 +120,21 @@ __global__ __launch_bounds__(64) void ml_epilogue_kernel(EpilogueArgs<DT> a)
         const bool nan1 = q1n != q1n, nan2 = q2n != q2n;
         n1 += nan1;
         n2 += nan2;
-        if (a.temp_out) a.temp_out[i] = a.temp[i] + (nan1 ? (DT)0 : q1n) * dtd;
+        if (want_t) a.temp_out[i] = t + (nan1 ? (DT)0 : q1n) * dtd;
         if (a.sphum_out) a.sphum_out[i] = sp + (nan2 ? (DT)0 : q2n) * dtd;
+    };
+    fetch(0, 0);
+    for (int k0 = 0; k0 < a.nz; k0 += 2 * U) {
+        if (k0 + U < a.nz) fetch(1, k0 + U);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (k0 + u < a.nz) level(k0 + u, b_q1[0][u], b_q2[0][u], b_sp[0][u], b_dp[0][u], b_t[0][u]);
+        if (k0 + U >= a.nz) break;
+        if (k0 + 2 * U < a.nz) fetch(0, k0 + 2 * U);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (k0 + U + u < a.nz)
+                level(k0 + U + u, b_q1[1][u], b_q2[1][u], b_sp[1][u], b_dp[1][u], b_t[1][u]);
     }
     if (a.col) {
         const DT ch = a.hydrostatic ? (DT)kCp : cv;

@@ -68,6 +68,30 @@ def test_epilogue_bit_identical_to_oracle(gpu, dtype, mse, hydrostatic):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nz", [1, 3, 8, 9, 16, 17, 24, 33])
+def test_epilogue_level_batches(gpu, nz):
+    """The kernel fetches levels in double-buffered batches of 8: every remainder of nz
+    (fewer levels than one batch, exact multiples, one past) stays bit-identical."""
+    import torch
+
+    from fv3net_amd.stepper import ml_epilogue
+
+    rng = np.random.default_rng(nz)
+    dq1, dq2, q, delp, T, precip = _state(rng, nz=nz, ncol=130)
+    dq2[nz - 1, 5] = -1.0  # limiter active at the last level
+    dq1[0, 7] = np.nan
+    ref = OS.epilogue(dq1, dq2, q, delp, T, precip, 900.0, True, False)
+    got = ml_epilogue(*(torch.from_numpy(a).cuda() for a in (dq1, dq2, q, delp, T)), 900.0,
+                      torch.from_numpy(precip).cuda(), True, False, label="ml")
+    names = {"net_moistening": "net_moistening_due_to_ml", "column_heating": "column_heating_due_to_ml"}
+    for k, r in ref.items():
+        g = got[names.get(k, k)].cpu().numpy()
+        if k.endswith("filled_frac"):
+            r = r.astype(np.float64)
+        _bits(g, r)
+
+
+@pytest.mark.gpu
 def test_epilogue_in_place_on_tile_state(gpu):
     """(tile, z, y, x) state updated in place; columns = (tile, y, x)."""
     import torch
