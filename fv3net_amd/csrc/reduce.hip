@@ -12,8 +12,9 @@
 //
 // Both are HBM-bound streams.  Column integral: one thread per column, levels
 // walked in order (coalesced [level][column] rows), float64 accumulation.
-// Area sums: fixed-shape two-level tree (per-block partials in a fixed order,
-// then one block folds them) so the result is bitwise reproducible run to run.
+// Area sums: fixed-shape two-level tree (per-block partials from wave butterflies in a
+// fixed order, then one block folds them) so the result is bitwise reproducible run to
+// run for a given column count.
 #include "common.h"
 
 namespace fv3 {
@@ -52,39 +53,75 @@ __device__ __forceinline__ double block_sum(double v, double* sh)
     return r;
 }
 
-// partials[blk][2*n_diag]: block-level partial sums over a grid-stride range.
-__global__ __launch_bounds__(kSumBlock) void area_sums_stage1(const float* const* __restrict__ diags,
-                                                              int n_diag, const float* __restrict__ area,
-                                                              int64_t ncol, double* __restrict__ partials)
+// The diagnostic fields, passed by value in the kernel arguments (no pointer-table
+// upload per call).
+struct DiagPtrs {
+    const float* p[64];
+};
+
+// Sum over the 64 lanes of a wave by a fixed xor-butterfly (bitwise reproducible).
+__device__ __forceinline__ double wave_sum(double v)
 {
-    __shared__ double sh[kSumBlock];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+constexpr int kDiagChunk = 8;
+
+// partials[blk][2*n_diag]: block-level partial sums over a grid-stride range, diags
+// taken kDiagChunk at a time: each thread accumulates area and area*x for the chunk,
+// then one butterfly per wave and a fixed-order fold of the 4 waves.
+__global__ __launch_bounds__(kSumBlock) void area_sums_stage1(DiagPtrs diags, int n_diag,
+                                                              const float* __restrict__ area, int64_t ncol,
+                                                              double* __restrict__ partials)
+{
+    __shared__ double sh[kSumBlock / 64][kDiagChunk + 1];
     const int64_t stride = (int64_t)gridDim.x * kSumBlock;
-    double asum = 0.0;
-    for (int64_t c = (int64_t)blockIdx.x * kSumBlock + threadIdx.x; c < ncol; c += stride)
-        asum += (double)area[c];
-    const double atot = block_sum(asum, sh);
-    for (int d = 0; d < n_diag; ++d) {
-        const float* x = diags[d];
-        double s = 0.0;
-        for (int64_t c = (int64_t)blockIdx.x * kSumBlock + threadIdx.x; c < ncol; c += stride)
-            s += (double)area[c] * (double)x[c];
-        const double tot = block_sum(s, sh);
-        if (threadIdx.x == 0) {
-            partials[(int64_t)blockIdx.x * 2 * n_diag + 2 * d] = tot;
-            partials[(int64_t)blockIdx.x * 2 * n_diag + 2 * d + 1] = atot;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int d0 = 0; d0 < n_diag; d0 += kDiagChunk) {
+        double s[kDiagChunk + 1];
+#pragma unroll
+        for (int j = 0; j <= kDiagChunk; ++j) s[j] = 0.0;
+        for (int64_t c = (int64_t)blockIdx.x * kSumBlock + threadIdx.x; c < ncol; c += stride) {
+            const double a = (double)area[c];
+            s[kDiagChunk] += a;
+#pragma unroll
+            for (int j = 0; j < kDiagChunk; ++j)
+                if (d0 + j < n_diag) s[j] += a * (double)diags.p[d0 + j][c];
         }
+#pragma unroll
+        for (int j = 0; j <= kDiagChunk; ++j) s[j] = wave_sum(s[j]);
+        if (lane == 0) {
+#pragma unroll
+            for (int j = 0; j <= kDiagChunk; ++j) sh[w][j] = s[j];
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < kDiagChunk && d0 + (int)threadIdx.x < n_diag) {
+            const int j = threadIdx.x;
+            double tot = sh[0][j], atot = sh[0][kDiagChunk];
+            for (int v = 1; v < kSumBlock / 64; ++v) {
+                tot += sh[v][j];
+                atot += sh[v][kDiagChunk];
+            }
+            partials[(int64_t)blockIdx.x * 2 * n_diag + 2 * (d0 + j)] = tot;
+            partials[(int64_t)blockIdx.x * 2 * n_diag + 2 * (d0 + j) + 1] = atot;
+        }
+        __syncthreads();
     }
 }
 
+// out[j] = sum over blocks of partials[b][j]: one wave per value, lanes stride over
+// the blocks in a fixed order, then the butterfly.
 __global__ __launch_bounds__(kSumBlock) void area_sums_stage2(const double* __restrict__ partials, int nblk,
                                                               int n_diag, double* __restrict__ out)
 {
-    __shared__ double sh[kSumBlock];
-    for (int j = 0; j < 2 * n_diag; ++j) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int j = w; j < 2 * n_diag; j += kSumBlock / 64) {
         double s = 0.0;
-        for (int b = threadIdx.x; b < nblk; b += kSumBlock) s += partials[(int64_t)b * 2 * n_diag + j];
-        const double tot = block_sum(s, sh);
-        if (threadIdx.x == 0) out[j] = tot;
+        for (int b = lane; b < nblk; b += 64) s += partials[(int64_t)b * 2 * n_diag + j];
+        s = wave_sum(s);
+        if (lane == 0) out[j] = s;
     }
 }
 
@@ -142,18 +179,20 @@ extern "C" int fv3_area_weighted_sums(const float* const* diags, int n_diag, con
     if (n_diag == 0) return FV3_OK;
     FV3_REQUIRE(diags && area && partial, "area_weighted_sums: NULL array");
     hipStream_t s = (hipStream_t)stream;
-    // device copy of the pointer table + partial slabs, carved from one scratch allocation
-    // owned by this call's stream (hipMallocAsync keeps it capture-safe).
-    const int nblk = (int)std::min<int64_t>(fv3::kSumMaxBlocks, std::max<int64_t>(1, (ncol + 4095) / 4096));
-    const size_t tab_bytes = sizeof(float*) * (size_t)n_diag;
-    const size_t part_bytes = sizeof(double) * 2 * (size_t)n_diag * nblk;
+    // one column per thread up to kSumMaxBlocks blocks; partial slabs from a
+    // stream-ordered scratch allocation (capture-safe)
+    const int nblk = (int)std::min<int64_t>(fv3::kSumMaxBlocks,
+                                            std::max<int64_t>(1, (ncol + fv3::kSumBlock - 1) / fv3::kSumBlock));
+    fv3::DiagPtrs dp{};
+    for (int d = 0; d < n_diag; ++d) {
+        FV3_REQUIRE(diags[d], "area_weighted_sums: NULL diagnostic %d", d);
+        dp.p[d] = diags[d];
+    }
     void* scratch = nullptr;
-    FV3_HIP(hipMallocAsync(&scratch, tab_bytes + part_bytes + 16, s));
-    const float** dtab = (const float**)scratch;
-    double* parts = (double*)((char*)scratch + ((tab_bytes + 15) / 16) * 16);
-    FV3_HIP(hipMemcpyAsync((void*)dtab, diags, tab_bytes, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(fv3::area_sums_stage1, dim3(nblk), dim3(fv3::kSumBlock), 0, s, dtab, n_diag, area,
-                       ncol, parts);
+    FV3_HIP(hipMallocAsync(&scratch, sizeof(double) * 2 * (size_t)n_diag * nblk, s));
+    double* parts = (double*)scratch;
+    hipLaunchKernelGGL(fv3::area_sums_stage1, dim3(nblk), dim3(fv3::kSumBlock), 0, s, dp, n_diag, area, ncol,
+                       parts);
     FV3_LAUNCH_CHECK();
     hipLaunchKernelGGL(fv3::area_sums_stage2, dim3(1), dim3(fv3::kSumBlock), 0, s, parts, nblk, n_diag,
                        partial);
