@@ -37,6 +37,7 @@ EXPORTED_SYMBOLS = (
     "fv3_pressure_midpoint_log",
     "fv3_column_integral",
     "fv3_area_weighted_sums",
+    "fv3_area_weighted_sums_f64",
     "fv3_level_sums",
     "fv3_ml_epilogue",
 )
@@ -135,6 +136,7 @@ _SIGNATURES = {
     "fv3_pressure_midpoint_log": (_I, [_P, _I, _I64, _P, _I64, _I64, _I, _D, _P]),
     "fv3_column_integral": (_I, [_P, Layout, _P, Layout, _P, _I64, _I, _D, _P]),
     "fv3_area_weighted_sums": (_I, [ctypes.POINTER(_P), _I, _P, _I64, _P, _P]),
+    "fv3_area_weighted_sums_f64": (_I, [ctypes.POINTER(_P), _I, _P, _I64, _P, _P]),
     "fv3_level_sums": (_I, [_P, Layout, _I64, _I, _P, _P]),
     "fv3_ml_epilogue": (_I, [ctypes.POINTER(EpilogueIO), Layout, _I64, _I, _I, _D, _I, _I, _P]),
 }

@@ -55,8 +55,9 @@ __device__ __forceinline__ double block_sum(double v, double* sh)
 
 // The diagnostic fields, passed by value in the kernel arguments (no pointer-table
 // upload per call).
+template <typename T>
 struct DiagPtrs {
-    const float* p[64];
+    const T* p[64];
 };
 
 // Sum over the 64 lanes of a wave by a fixed xor-butterfly (bitwise reproducible).
@@ -72,8 +73,9 @@ constexpr int kDiagChunk = 8;
 // partials[blk][2*n_diag]: block-level partial sums over a grid-stride range, diags
 // taken kDiagChunk at a time: each thread accumulates area and area*x for the chunk,
 // then one butterfly per wave and a fixed-order fold of the 4 waves.
-__global__ __launch_bounds__(kSumBlock) void area_sums_stage1(DiagPtrs diags, int n_diag,
-                                                              const float* __restrict__ area, int64_t ncol,
+template <typename T>
+__global__ __launch_bounds__(kSumBlock) void area_sums_stage1(DiagPtrs<T> diags, int n_diag,
+                                                              const T* __restrict__ area, int64_t ncol,
                                                               double* __restrict__ partials)
 {
     __shared__ double sh[kSumBlock / 64][kDiagChunk + 1];
@@ -170,10 +172,14 @@ extern "C" int fv3_column_integral(const float* field, fv3_layout field_l, const
     return FV3_OK;
 }
 
-extern "C" int fv3_area_weighted_sums(const float* const* diags, int n_diag, const float* area,
-                                      int64_t ncol, double* partial, void* stream)
+namespace fv3 {
+namespace {
+
+template <typename T>
+int area_weighted_sums_impl(const T* const* diags, int n_diag, const T* area, int64_t ncol, double* partial,
+                            void* stream)
 {
-    fv3::clear_error();
+    clear_error();
     FV3_REQUIRE(n_diag >= 0 && n_diag <= 64, "area_weighted_sums: n_diag must be in [0, 64]");
     FV3_REQUIRE(ncol >= 0, "area_weighted_sums: ncol < 0");
     if (n_diag == 0) return FV3_OK;
@@ -181,9 +187,8 @@ extern "C" int fv3_area_weighted_sums(const float* const* diags, int n_diag, con
     hipStream_t s = (hipStream_t)stream;
     // one column per thread up to kSumMaxBlocks blocks; partial slabs from a
     // stream-ordered scratch allocation (capture-safe)
-    const int nblk = (int)std::min<int64_t>(fv3::kSumMaxBlocks,
-                                            std::max<int64_t>(1, (ncol + fv3::kSumBlock - 1) / fv3::kSumBlock));
-    fv3::DiagPtrs dp{};
+    const int nblk = (int)std::min<int64_t>(kSumMaxBlocks, std::max<int64_t>(1, (ncol + kSumBlock - 1) / kSumBlock));
+    DiagPtrs<T> dp{};
     for (int d = 0; d < n_diag; ++d) {
         FV3_REQUIRE(diags[d], "area_weighted_sums: NULL diagnostic %d", d);
         dp.p[d] = diags[d];
@@ -191,12 +196,25 @@ extern "C" int fv3_area_weighted_sums(const float* const* diags, int n_diag, con
     void* scratch = nullptr;
     FV3_HIP(hipMallocAsync(&scratch, sizeof(double) * 2 * (size_t)n_diag * nblk, s));
     double* parts = (double*)scratch;
-    hipLaunchKernelGGL(fv3::area_sums_stage1, dim3(nblk), dim3(fv3::kSumBlock), 0, s, dp, n_diag, area, ncol,
-                       parts);
+    hipLaunchKernelGGL(area_sums_stage1<T>, dim3(nblk), dim3(kSumBlock), 0, s, dp, n_diag, area, ncol, parts);
     FV3_LAUNCH_CHECK();
-    hipLaunchKernelGGL(fv3::area_sums_stage2, dim3(1), dim3(fv3::kSumBlock), 0, s, parts, nblk, n_diag,
-                       partial);
+    hipLaunchKernelGGL(area_sums_stage2, dim3(1), dim3(kSumBlock), 0, s, parts, nblk, n_diag, partial);
     FV3_LAUNCH_CHECK();
     FV3_HIP(hipFreeAsync(scratch, s));
     return FV3_OK;
+}
+
+}  // namespace
+}  // namespace fv3
+
+extern "C" int fv3_area_weighted_sums(const float* const* diags, int n_diag, const float* area,
+                                      int64_t ncol, double* partial, void* stream)
+{
+    return fv3::area_weighted_sums_impl<float>(diags, n_diag, area, ncol, partial, stream);
+}
+
+extern "C" int fv3_area_weighted_sums_f64(const double* const* diags, int n_diag, const double* area,
+                                          int64_t ncol, double* partial, void* stream)
+{
+    return fv3::area_weighted_sums_impl<double>(diags, n_diag, area, ncol, partial, stream);
 }

@@ -75,10 +75,17 @@ def segment_view(arr, seg: Segment):
 def area_weighted_partials(diags: Sequence, area, stream=None):
     """Device float64 partials [n_diag, 2] = (sum(area * x_d), sum(area)) over this
     rank's columns, computed by the deterministic two-stage HIP reduction
-    (csrc/reduce.hip).  ``diags``: float32 CUDA tensors shaped like ``area``."""
+    (csrc/reduce.hip).  ``diags``: CUDA tensors shaped like ``area``.  As numpy's
+    ``area * ds`` promotes, any float64 operand puts the whole reduction on the float64
+    kernel (float32 operands widened exactly); all-float32 inputs use the float32 one."""
     _device.require_gpu()
-    area = _device.to_device_f32(area).contiguous()
-    xs = [_device.to_device_f32(d).contiguous() for d in diags]
+    wide = any(torch.is_tensor(t) and t.dtype == torch.float64 for t in [area, *diags])
+    if wide:
+        conv = lambda t: torch.as_tensor(t, device="cuda").to(torch.float64).contiguous()  # noqa: E731
+    else:
+        conv = lambda t: _device.to_device_f32(t).contiguous()  # noqa: E731
+    area = conv(area)
+    xs = [conv(d) for d in diags]
     for d in xs:
         if d.shape != area.shape:
             raise ValueError(f"diagnostic shape {tuple(d.shape)} != area shape {tuple(area.shape)}")
@@ -86,8 +93,9 @@ def area_weighted_partials(diags: Sequence, area, stream=None):
     if not xs:
         return out
     tab = (ctypes.c_void_p * len(xs))(*[d.data_ptr() for d in xs])
-    st = _native.load().fv3_area_weighted_sums(tab, len(xs), area.data_ptr(), area.numel(), out.data_ptr(),
-                                               _device.stream_handle(stream))
+    lib = _native.load()
+    fn = lib.fv3_area_weighted_sums_f64 if wide else lib.fv3_area_weighted_sums
+    st = fn(tab, len(xs), area.data_ptr(), area.numel(), out.data_ptr(), _device.stream_handle(stream))
     _native.check(st, "area_weighted_sums")
     return out
 

@@ -182,7 +182,7 @@ class StepperWorkload:
         self.state["total_precipitation"] = res["total_precipitation"]
         diags = [res["net_moistening_due_to_machine_learning"], res["column_heating_due_to_machine_learning"],
                  res["total_precipitation"]]
-        part = area_weighted_partials([d.to(torch.float32) for d in diags], self.area)
+        part = area_weighted_partials(diags, self.area)  # float64 diagnostics: the f64 reduction
         return combine_partials(part, self.group)
 
 
@@ -199,7 +199,7 @@ def make_stepper_workload(res: int = 96, seed: int = 0, device=None, group=None)
             base * (0.99 + 0.02 * torch.rand(shape, generator=g, device=device, dtype=torch.float64)),
         "total_precipitation": 1e-3 * torch.rand((6, res, res), generator=g, device=device, dtype=torch.float64),
     }
-    area = 0.5 + 0.5 * torch.rand((6, res, res), generator=g, device=device)
+    area = 0.5 + 0.5 * torch.rand((6, res, res), generator=g, device=device, dtype=torch.float64)
     wl = make_dense_workload(min(res, 48), seed=seed, device=device)
     return StepperWorkload(wl.model, state, area, 900.0, 6 * res * res, group)
 

@@ -206,6 +206,10 @@ int fv3_column_integral(const float* field, fv3_layout field_l, const float* del
  * Deterministic (fixed reduction tree).  metrics.py:18-24 partials. */
 int fv3_area_weighted_sums(const float* const* diags, int n_diag, const float* area,
                            int64_t ncol, double* partial, void* stream);
+/* The same over float64 diagnostics and area (the reference's dtype: numpy's
+ * area * ds on float64 grid data); same reduction tree. */
+int fv3_area_weighted_sums_f64(const double* const* diags, int n_diag, const double* area,
+                               int64_t ncol, double* partial, void* stream);
 
 /* Per-level horizontal sums out[k] = sum_c x[k][c] in float64 (fixed reduction tree):
  * the per-rank part of metrics.py:27-32 global_horizontal_sum. */

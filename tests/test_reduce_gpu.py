@@ -29,6 +29,29 @@ def test_area_weighted_partials(gpu, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 300, 55296])
+@pytest.mark.parametrize("n_diag", [1, 9, 17])
+def test_area_weighted_partials_f64(gpu, n, n_diag):
+    """float64 diagnostics (the stepper's dtype) run the float64 kernel, with an float32
+    area widened exactly, as numpy's area * ds promotes; diags in chunks of 8."""
+    import torch
+
+    from fv3net_amd import distributed as D
+
+    rng = np.random.default_rng(n + n_diag)
+    x = rng.normal(0, 1, (n_diag, n)) * 10.0 ** rng.integers(-8, 3, (n_diag, 1))
+    a = rng.uniform(0.5, 1, n).astype(np.float32)
+    xt = [torch.from_numpy(v).cuda() for v in x]
+    p1 = D.area_weighted_partials(xt, torch.from_numpy(a).cuda()).cpu().numpy()
+    p2 = D.area_weighted_partials(xt, torch.from_numpy(a.astype(np.float64)).cuda()).cpu().numpy()
+    assert (p1.view(np.uint64) == p2.view(np.uint64)).all()
+    a64 = a.astype(np.float64)
+    for d in range(n_diag):
+        np.testing.assert_allclose(p1[d, 0], np.sum(a64 * x[d]), rtol=1e-12, atol=1e-300)
+        np.testing.assert_allclose(p1[d, 1], np.sum(a64), rtol=1e-13)
+
+
+@pytest.mark.gpu
 def test_level_sums_on_views(gpu):
     import torch
 
