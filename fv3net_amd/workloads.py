@@ -93,10 +93,15 @@ class MappmWorkload:
     def bytes_per_column(self) -> int:
         return 4 * ((self.km + 1) + self.km + (self.kn + 1) + self.kn)
 
-    def step(self):
-        from .mappm import mappm_device
+    plan: object = None
 
-        mappm_device(self.pe1, self.q1, self.pe2, self.iv, self.kord, out=self.q2)
+    def step(self):
+        from .mappm import MappmPlan
+
+        if self.plan is None:  # prepared once: each step is one C-ABI call
+            self.plan = MappmPlan(self.pe1, self.q1, self.pe2, self.iv, self.kord, out=self.q2)
+        else:
+            self.plan()
 
 
 def make_mappm_workload(ncol: int, km: int = NZ, kn: int = NZ, kord: int = 1, seed: int = 0, device=None):

@@ -196,3 +196,21 @@ def test_unsorted_edges_fall_back_per_column(gpu):
                 assert _bits_equal(a, b), (kord, iv, vs_oracle)
                 if vs_oracle:
                     assert _bits_equal(a, oracle_mappm(pe1, q, p2, iv, kord)), (kord, iv)
+
+
+def test_prepared_plan_matches_and_tracks_contents(gpu):
+    """MappmPlan re-issues the same call on the same buffers: bit-identical to
+    mappm_device, and it sees in-place updates of the inputs."""
+    import torch
+
+    from fv3net_amd.mappm import MappmPlan, mappm_device
+
+    rng = np.random.default_rng(21)
+    pe1, q, pe2 = _columns(rng, 79, 50, 864)
+    d = [torch.from_numpy(a).cuda() for a in (pe1, q, pe2)]
+    plan = MappmPlan(*d, 1, 4)
+    assert _bits_equal(plan().cpu().numpy(), oracle_mappm(pe1, q, pe2, 1, 4))
+    d[1].mul_(2.0)
+    got = plan().cpu().numpy()
+    assert _bits_equal(got, mappm_device(*d, 1, 4).cpu().numpy())
+    assert _bits_equal(got, oracle_mappm(pe1, q * 2, pe2, 1, 4))
