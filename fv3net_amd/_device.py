@@ -35,11 +35,15 @@ def to_device_f32(x, device=None, contiguous: bool = True):
     return t.contiguous() if contiguous else t
 
 
-def column_view(x, level_axis: int):
+def column_view(x, level_axis: int, keep_f64: bool = False):
     """(tensor, fv3_layout, ncol, nz) for ``x`` with levels on ``level_axis``: strided
     CUDA views the layout can express are used in place, anything else is copied to a
-    contiguous device tensor first."""
-    t = to_device_f32(x, contiguous=False)
+    contiguous device tensor first.  float32 unless ``keep_f64`` and ``x`` is a float64
+    CUDA tensor (kernels that read float64 in place)."""
+    if keep_f64 and torch.is_tensor(x) and x.is_cuda and x.dtype == torch.float64:
+        t = x
+    else:
+        t = to_device_f32(x, contiguous=False)
     try:
         lay, ncol, nz = level_layout(t, level_axis)
     except ValueError:

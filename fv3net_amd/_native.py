@@ -26,6 +26,7 @@ EXPORTED_SYMBOLS = (
     "fv3_dense_k_in",
     "fv3_dense_k_out",
     "fv3_dense_forward",
+    "fv3_dense_forward_f64in",
     "fv3_dense_forward_ex",
     "fv3_dense_set_trace",
     "fv3_regrid_coarsen",
@@ -120,6 +121,8 @@ _SIGNATURES = {
     "fv3_dense_k_in": (_I, [_P]),
     "fv3_dense_k_out": (_I, [_P]),
     "fv3_dense_forward": (_I, [_P, ctypes.POINTER(_P), ctypes.POINTER(Layout), ctypes.POINTER(_P),
+                               ctypes.POINTER(Layout), _I64, _P]),
+    "fv3_dense_forward_f64in": (_I, [_P, ctypes.POINTER(_P), ctypes.POINTER(Layout), ctypes.POINTER(_P),
                                ctypes.POINTER(Layout), _I64, _P]),
     "fv3_dense_forward_ex": (_I, [_P, ctypes.POINTER(_P), ctypes.POINTER(Layout), ctypes.POINTER(_P),
                                   ctypes.POINTER(Layout), _I64, _I, _P]),

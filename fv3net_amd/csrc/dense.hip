@@ -156,6 +156,16 @@ __device__ __forceinline__ float in_load(const float* p)
     return *p;
 }
 
+// element `off` of an input slot whose base is stored as const float*: IT = double for
+// float64 state read in place (the f32 model input is the round-to-nearest cast, as
+// Keras's own cast); IT = float is the plain load above
+template <typename IT>
+__device__ __forceinline__ IT in_at(const float* base, int64_t off)
+{
+    if constexpr (std::is_same<IT, float>::value) return in_load(base + off);
+    else return reinterpret_cast<const IT*>(base)[off];
+}
+
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.0f, 0.0f, 0.0f, 0.0f}; }
 
 // log(max(x, eps)) with tf.maximum's NaN propagation and a correctly rounded-class log
@@ -321,7 +331,7 @@ typedef __attribute__((address_space(4))) const DenseArgs KArgs;
 // 3: <= 168, letting three blocks share a CU)
 // RD: weight ring depth (groups of 4 k-steps held; refilled RD-1 groups ahead)
 // NW: waves per block (4: one per SIMD; 8: two per SIMD sharing a tile, T4 halved)
-template <int T4, int NC, int WPE, int RD, int NW>
+template <int T4, int NC, int WPE, int RD, int NW, typename IT = float>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void dense_forward_kernel(DenseArgs pa)
 {
     // read the arguments in place in the kernarg segment (constant address space):
@@ -351,7 +361,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
     // ---- input slots: issue every load of a tile at once ----
     // slots prefetched into registers: kRawSlots x 8 feature rows (160) whatever FPS
     constexpr int RS = kRawSlots * 8 / FPS;
-    float raw[RS];
+    IT raw[RS];  // converted to f32 at staging, after every load of the tile is issued
     auto col_of = [&](int64_t tile, int64_t& blk, int64_t& ii) {
         const int64_t col = tile * NCOL + cb;
         const bool valid = col < p.ncol;
@@ -370,7 +380,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
     // scalar reads of all slot descriptors can be in flight together.
     auto slot_load = [&](KArgs& pk, int q, int meta, bool valid, int64_t blk, int64_t ii, int fq) {
         return (valid && fq < ((meta >> 8) & 0xff))
-                   ? in_load(pk.slot_base[q] + blk * pk.slot_bs[q] + ii + (int64_t)fq * pk.slot_ld[q])
+                   ? (float)in_at<IT>(pk.slot_base[q], blk * pk.slot_bs[q] + ii + (int64_t)fq * pk.slot_ld[q])
                    : 0.0f;
     };
     // the register-prefetched slots: 32-bit element offsets (the host checks every
@@ -389,7 +399,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
             // slot, with the descriptor reads and an lgkmcnt(0) wait inside each
             // no select here: consuming the value right away makes the compiler wait for
             // each load in turn; staging zeroes the lanes past a slot's rows anyway
-            raw[q] = in_load(pk.slot_base[q] + (off & (0u - (unsigned)on)));
+            raw[q] = in_at<IT>(pk.slot_base[q], off & (0u - (unsigned)on));
         });
     };
     // normalise and write the staged inputs in B-operand order: for column tile c,
@@ -459,7 +469,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         const unsigned b32 = (unsigned)blk, i32 = (unsigned)ii;
         for (int q0 = RS; q0 < pk.nslots; q0 += 8) {
             int mw[8];
-            float xw[8], mw_mu[8], mw_rv[8];
+            IT xw[8];
+            float mw_mu[8], mw_rv[8];
             static_for<8>([&](auto ic) {
                 constexpr int i = decltype(ic)::value;
                 mw[i] = q0 + i < pk.nslots ? pk.slot_meta[q0 + i] : 0;  // uniform
@@ -469,7 +480,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
                 const int q = min(q0 + i, kMaxSlots - 1);  // past nslots: meta 0, any valid base
                 const bool on = valid && fq < ((mw[i] >> 8) & 0xff);
                 const unsigned off = b32 * (unsigned)pk.slot_bs[q] + i32 + (unsigned)fq * (unsigned)pk.slot_ld[q];
-                xw[i] = in_load(pk.slot_base[q] + (off & (0u - (unsigned)on)));
+                xw[i] = in_at<IT>(pk.slot_base[q], off & (0u - (unsigned)on));
             });
             static_for<8>([&](auto ic) {
                 constexpr int i = decltype(ic)::value;
@@ -1086,11 +1097,17 @@ extern "C" int fv3_dense_destroy(fv3_dense_model* m)
 extern "C" int fv3_dense_k_in(const fv3_dense_model* m) { return m ? m->k_in : -1; }
 extern "C" int fv3_dense_k_out(const fv3_dense_model* m) { return m ? m->k_out : -1; }
 
-extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* inputs, const fv3_layout* in_l,
-                                 float* const* outputs, const fv3_layout* out_l, int64_t ncol, void* stream)
+// in64: inputs are float64 (read in place, cast to f32 in the staging)
+static int dense_forward_impl(const fv3_dense_model* m, const void* const* inputs, bool in64, const fv3_layout* in_l,
+                              float* const* outputs, const fv3_layout* out_l, int64_t ncol, void* stream)
 {
     using namespace fv3;
     clear_error();
+    // element `off` of input v, as the const float* the slot descriptors carry
+    auto in_ptr = [&](int v, int64_t off) -> const float* {
+        return in64 ? reinterpret_cast<const float*>(static_cast<const double*>(inputs[v]) + off)
+                    : static_cast<const float*>(inputs[v]) + off;
+    };
     FV3_REQUIRE(m, "dense_forward: NULL model");
     FV3_REQUIRE(ncol >= 0, "dense_forward: ncol < 0");
     if (ncol == 0) return FV3_OK;
@@ -1124,7 +1141,9 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
         a.out_ld[v] = out_l[v].ld;
         a.out_bs[v] = out_l[v].blk_stride;
         const int r = m->out_residual[v];
-        a.res_ptr[v] = r >= 0 ? inputs[r] : nullptr;
+        FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, !in64 || r < 0,
+                         "dense_forward: residual outputs need float32 inputs");
+        a.res_ptr[v] = r >= 0 ? in_ptr(r, 0) : nullptr;
         a.res_ld[v] = r >= 0 ? (int)in_l[r].ld : 0;
         a.res_bs[v] = r >= 0 ? (int)in_l[r].blk_stride : 0;
     }
@@ -1179,7 +1198,7 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
             FV3_REQUIRE(a.nslots < kMaxSlots, "dense_forward: %d input features are too many", m->kp);
             const int q = a.nslots++;
             const int zf = std::min(m->in_z0[v] + f0, m->in_nz[v] - 1);  // never dereferenced past nk
-            a.slot_base[q] = inputs[v] + (int64_t)zf * in_l[v].ld;
+            a.slot_base[q] = in_ptr(v, (int64_t)zf * in_l[v].ld);
             a.slot_bs[q] = (int)in_l[v].blk_stride;
             a.slot_ld[q] = (int)in_l[v].ld;
             const int nk = std::max(0, std::min(nk_v - f0, 255));
@@ -1190,7 +1209,7 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
         }
     }
     for (int q = a.nslots; q < kMaxSlots; ++q) {  // unused slots: meta 0 (no rows), a valid base
-        a.slot_base[q] = inputs[0];
+        a.slot_base[q] = in_ptr(0, 0);
         a.slot_bs[q] = a.slot_ld[q] = a.slot_meta[q] = 0;
         a.slot_leps[q] = 0.0f;
     }
@@ -1234,7 +1253,11 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
         return t4 == 1 ? FV3_K(1, 2, 2, 3) : t4 == 2 ? FV3_K(2, 2, 2, 3) : FV3_K(4, 2, 2, 3);
 #undef FV3_K
     };
-    const void* kfn = kernel_of(m->ht / nw);
+    FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, !in64 || nw == 8,
+                     "dense_forward: float64 inputs need the 8-wave kernel (32-column tiles, width >= 128)");
+    const void* kfn = in64 ? (m->ht / nw == 1 ? (const void*)dense_forward_kernel<1, 2, 4, 2, 8, double>
+                                              : (const void*)dense_forward_kernel<2, 2, 4, 2, 8, double>)
+                           : kernel_of(m->ht / nw);
     // persistent blocks: resident blocks per CU x CUs (queried once per kernel);
     // FV3_DENSE_GRID overrides (A/B)
     struct Resident {
@@ -1258,4 +1281,18 @@ extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* i
     FV3_HIP(hipLaunchKernel(kfn, dim3((unsigned)grid), dim3(nt), kargs, lds, s));
     FV3_LAUNCH_CHECK();
     return FV3_OK;
+}
+
+extern "C" int fv3_dense_forward(const fv3_dense_model* m, const float* const* inputs, const fv3_layout* in_l,
+                                 float* const* outputs, const fv3_layout* out_l, int64_t ncol, void* stream)
+{
+    return dense_forward_impl(m, reinterpret_cast<const void* const*>(inputs), false, in_l, outputs, out_l, ncol,
+                              stream);
+}
+
+extern "C" int fv3_dense_forward_f64in(const fv3_dense_model* m, const double* const* inputs, const fv3_layout* in_l,
+                                       float* const* outputs, const fv3_layout* out_l, int64_t ncol, void* stream)
+{
+    return dense_forward_impl(m, reinterpret_cast<const void* const*>(inputs), true, in_l, outputs, out_l, ncol,
+                              stream);
 }

@@ -290,13 +290,18 @@ class DenseColumnModel:
         if len(inputs) != len(c.input_variables):
             raise ValueError(f"expected {len(c.input_variables)} inputs")
         level_axes = list(level_axes) if level_axes is not None else [0] * len(inputs)
+        prec = precision or self.precision
+        outputs_arg = outputs
+        # a float64 state (the stepper's) is read in place and cast in the kernel's staging
+        in64 = (prec == "f32" and len(inputs) > 0 and all(ax is not None for ax in level_axes)
+                and all(torch.is_tensor(t) and t.is_cuda and t.dtype == torch.float64 for t in inputs))
         ts, lays = [], []
         ncol = None
         for v, (t, ax) in enumerate(zip(inputs, level_axes)):
             if ax is None:
                 t = _device.to_device_f32(t, contiguous=False).unsqueeze(0)
                 ax = 0
-            t, lay, n, nz = _device.column_view(t, ax)  # strided views read in place
+            t, lay, n, nz = _device.column_view(t, ax, keep_f64=in64)  # strided views read in place
             if nz != c.in_nz[v]:
                 raise ValueError(f"input {c.input_variables[v]} has {nz} levels, model expects {c.in_nz[v]}")
             if ncol is not None and n != ncol:
@@ -323,8 +328,18 @@ class DenseColumnModel:
             olays.append(lay)
         if any(l.ncol_blk != lays[0].ncol_blk for l in lays + olays):
             raise ValueError("all inputs/outputs must share the horizontal layout")
-        bound = BoundForward(self, ts, lays, outputs, olays, ncol, precision or self.precision)
-        bound(stream)
+        bound = BoundForward(self, ts, lays, outputs, olays, ncol, prec, in64=in64)
+        self._last_cast_copy = False
+        try:
+            bound(stream)
+        except NotImplementedError:
+            if not in64:
+                raise
+            self._last_cast_copy = True  # the bound call below reads a float32 copy
+            # models the float64 kernel does not cover (residual outputs, narrow widths):
+            # cast first, as before
+            return self.forward([t.to(torch.float32) for t in inputs], level_axes, outputs_arg, out_level_axis,
+                                stream, precision)
         return outputs
 
     def bind(self, inputs: Sequence, level_axes: Optional[Sequence[int]] = None,
@@ -334,6 +349,10 @@ class DenseColumnModel:
         same device buffers with no per-call argument marshalling (the prognostic loop
         calls predict on the same state arrays every timestep)."""
         self.forward(inputs, level_axes, outputs, out_level_axis, precision=precision)
+        if getattr(self, "_last_cast_copy", False):
+            raise NotImplementedError("this model reads float64 inputs through a float32 copy made per call "
+                                      "(no 8-wave kernel or residual outputs): call forward() each step, "
+                                      "or bind float32 buffers")
         return self._last_bound
 
     # ---- persistence -------------------------------------------------------------
@@ -381,7 +400,7 @@ class BoundForward:
     """A validated dense forward over fixed device buffers (see DenseColumnModel.bind)."""
 
     def __init__(self, model: "DenseColumnModel", inputs, in_layouts, outputs, out_layouts, ncol: int,
-                 precision: str = "f32"):
+                 precision: str = "f32", in64: bool = False):
         if precision not in PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {precision!r}")
         self.precision = precision
@@ -395,12 +414,18 @@ class BoundForward:
         self._out_l = (_native.Layout * len(out_layouts))(*out_layouts)
         self._ncol = int(ncol)
         self._handle = model.handle()
-        self._fn = _native.load().fv3_dense_forward_ex
+        self._in64 = bool(in64)  # float64 inputs: fv3_dense_forward_f64in (exact f32 only)
+        lib = _native.load()
+        self._fn = lib.fv3_dense_forward_f64in if self._in64 else lib.fv3_dense_forward_ex
         model._last_bound = self
 
     def __call__(self, stream=None):
-        st = self._fn(self._handle, self._in_ptrs, self._in_l, self._out_ptrs, self._out_l, self._ncol,
-                      self._prec, _device.stream_handle(stream))
+        if self._in64:
+            st = self._fn(self._handle, self._in_ptrs, self._in_l, self._out_ptrs, self._out_l, self._ncol,
+                          _device.stream_handle(stream))
+        else:
+            st = self._fn(self._handle, self._in_ptrs, self._in_l, self._out_ptrs, self._out_l, self._ncol,
+                          self._prec, _device.stream_handle(stream))
         if st:
             _native.check(st, "dense_forward")
         return self.outputs

@@ -174,14 +174,16 @@ class StepperWorkload:
     dt: float
     ncol: int
     group: object = None
+    bound: object = None
 
     def step(self):
         from .distributed import area_weighted_partials, combine_partials
         from .stepper import ml_epilogue
 
         T, q = self.state["air_temperature"], self.state["specific_humidity"]
-        t32, q32 = T.to(torch.float32), q.to(torch.float32)
-        dq1, dq2 = self.model.forward([t32, q32], level_axes=[1, 1])
+        if self.bound is None:  # validated once; float64 state read in place every step
+            self.bound = self.model.bind([T, q], level_axes=[1, 1])
+        dq1, dq2 = self.bound()
         res = ml_epilogue(dq1, dq2, q, self.state["pressure_thickness_of_atmospheric_layer"], T, self.dt,
                           self.state["total_precipitation"], in_place=True, level_axis=1)
         self.state["total_precipitation"] = res["total_precipitation"]

@@ -129,6 +129,15 @@ int fv3_dense_forward(const fv3_dense_model* model, const float* const* inputs,
                       const fv3_layout* in_l, float* const* outputs, const fv3_layout* out_l,
                       int64_t ncol, void* stream);
 
+/* fv3_dense_forward over float64 inputs read in place: each value is cast to float32
+ * (round to nearest) in the kernel's input staging, as the Keras model's input cast
+ * does (pure_keras.py:98-118 on a float64 state), so the outputs are bit-identical to
+ * casting first.  Exact-f32 arithmetic only; FV3_ERR_UNSUPPORTED for models with
+ * residual outputs or without the 8-wave kernel (width < 128, 16-column tiles). */
+int fv3_dense_forward_f64in(const fv3_dense_model* model, const double* const* inputs,
+                            const fv3_layout* in_l, float* const* outputs, const fv3_layout* out_l,
+                            int64_t ncol, void* stream);
+
 /* Forward with an explicit arithmetic:
  *   FV3_DENSE_F32     exact f32 products on v_mfma_f32_16x16x4_f32 (= fv3_dense_forward);
  *   FV3_DENSE_BF16X3  every f32 operand split into bf16 hi + lo, products as

@@ -174,3 +174,47 @@ def test_writes_stay_inside_outputs(gpu, res, precision):
         assert torch.isnan(b[:, :5]).all() and torch.isnan(b[:, 84:]).all()
     got = [_to_samples(o.cpu().numpy()) for o in outs]
     _check(got, dense_predict(samples, m.oracle_params(), np.float64), rtol=RTOL if precision == "f32" else 5e-5)
+
+
+@pytest.mark.parametrize("res,width,ragged", [(12, 256, False), (48, 256, False), (7, 128, True), (12, 64, False)])
+def test_float64_inputs_read_in_place(gpu, res, width, ragged):
+    """A float64 state goes to fv3_dense_forward_f64in (cast in the kernel's staging):
+    bit-identical to casting to float32 first, on the (tile, z, y, x) layout and on a
+    strided row-band view, for widths 64-256."""
+    import torch
+
+    rng = np.random.default_rng(res + width)
+    T = rng.normal(260.0, 15.0, (6, 79, res, res))
+    q = rng.uniform(0.0, 0.02, (6, 79, res, res))
+    m = _model(dict(input_variables=["air_temperature", "specific_humidity"],
+                    output_variables=["dQ1", "dQ2"], in_nz=[79, 79], out_nz=[79, 79],
+                    width=width, depth=3),
+               samples=[_to_samples(T.astype(np.float32)), _to_samples(q.astype(np.float32))])
+    Td, qd = torch.from_numpy(T).cuda(), torch.from_numpy(q).cuda()
+    if ragged:  # a row band of every tile: strided columns
+        Td, qd = Td[:, :, 1:6], qd[:, :, 1:6]
+    a = m.forward([Td, qd], level_axes=[1, 1])
+    b = m.forward([Td.to(torch.float32), qd.to(torch.float32)], level_axes=[1, 1])
+    torch.cuda.synchronize()
+    for x, y in zip(a, b):
+        assert x.dtype == torch.float32
+        assert torch.equal(x, y)
+
+
+def test_bind_float64_state_sees_updates(gpu):
+    """bind() on a float64 state reads it in place: an in-place state update (the
+    stepper's add_tendency) is seen by the next call."""
+    import torch
+
+    rng = np.random.default_rng(4)
+    T = torch.from_numpy(rng.normal(260.0, 15.0, (6, 79, 8, 8))).cuda()
+    q = torch.from_numpy(rng.uniform(0.0, 0.02, (6, 79, 8, 8))).cuda()
+    cfg = dict(input_variables=["T", "q"], output_variables=["dQ1", "dQ2"], in_nz=[79, 79], out_nz=[79, 79],
+               width=256, depth=3)
+    m = _model(cfg)
+    b = m.bind([T, q], level_axes=[1, 1])
+    T.add_(1.5)
+    got = [o.clone() for o in b()]
+    ref = m.forward([T.to(torch.float32), q.to(torch.float32)], level_axes=[1, 1])
+    for x, y in zip(got, ref):
+        assert torch.equal(x, y)
