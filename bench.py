@@ -262,7 +262,7 @@ def main():
             "parallelism": f"columns sharded, 1 process/GPU x {world}",
         },
         "roofline": {
-            "kernel": "fv3::dense_forward_kernel<2,2,4,2,8> (csrc/dense.hip: 8-wave blocks, 32-column tiles)",
+            "kernel": "fv3::dense_forward_kernel<2,2,4,2,8,float> (csrc/dense.hip: 8-wave blocks, 32-column tiles, f32 inputs)",
             "bound": "mfma",
             "achieved": achieved,
             "peak": W.FP32_MFMA_PEAK_TFLOPS,
