@@ -94,15 +94,39 @@ def timed_steps(step, steps, warmup, dist=None, settle_ms=0.0):
     return wall, e0.elapsed_time(e1) * 1e-3 / steps
 
 
-def pmc_traffic(kernel_key):
-    """HBM bytes per launch from the committed PMC pass (tools/profile.sh), or None."""
+def pmc_record(leg):
+    """The committed PMC record of a bench leg (profiles/pmc_traffic.json, written by
+    tools/pmc_all.sh + tools/pmc_publish.py), or {}."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d.get(kernel_key, {}).get("hbm_bytes_per_launch")
+            return json.load(f).get(leg, {})
     except (OSError, ValueError):
-        return None
+        return {}
+
+
+def pmc_traffic(leg):
+    """HBM bytes per launch of the leg's dominant kernel from the committed PMC passes
+    (FETCH_SIZE x calibrated read factor + WRITE_SIZE), or None."""
+    return pmc_record(leg).get("hbm_bytes_per_launch")
+
+
+def with_counters(leg, rec, alg_bytes=None):
+    """Attach the committed counter evidence of ``leg`` to its bench record: HBM traffic
+    per launch (and its ratio to the algorithmic bytes), MFMA busy fraction, VALU busy /
+    utilisation, and which profile they come from."""
+    r = pmc_record(leg)
+    if not r:
+        rec["traffic"] = None
+        return rec
+    rec["traffic"] = r.get("hbm_bytes_per_launch")
+    if alg_bytes and rec["traffic"]:
+        rec["traffic_over_algorithmic"] = rec["traffic"] / alg_bytes
+    for k in ("kernel", "mfma_busy_frac", "valu_busy_pct", "valu_utilization_pct"):
+        if r.get(k) is not None:
+            rec[k if k != "kernel" else "pmc_kernel"] = r[k]
+    rec["pmc_profile"] = r.get("profile")
+    return rec
 
 
 def cpu_baseline(wl, seconds):
@@ -150,11 +174,11 @@ def extra_measurements(dev, settle_ms=150.0):
     # config #2 at C384 (one GPU, 884,736 columns): MFMA-bound predict
     wl = W.make_dense_workload(384, seed=3, device=dev)
     wall, t = timed_steps(wl.step, 10, 3, settle_ms=settle_ms)
-    out["dense_c384"] = {
+    out["dense_c384"] = with_counters("dense_c384", {
         "columns_per_s": wl.ncol / t, "ms_per_step": t * 1e3,
         "tflops": wl.ncol * wl.flops_per_column / t / 1e12,
         "frac_f32_mfma_peak": wl.ncol * wl.flops_per_column / t / 1e12 / W.FP32_MFMA_PEAK_TFLOPS,
-    }
+    }, wl.ncol * wl.bytes_per_column)
     del wl
     # mappm: config #3 fine columns (C384 79->79) and config #1 (C12 79->50)
     for name, ncol, kn, kord in (("mappm_c384_79to79_kord1", W.c_columns(384), 79, 1),
@@ -163,15 +187,16 @@ def extra_measurements(dev, settle_ms=150.0):
         wl = W.make_mappm_workload(ncol, 79, kn, kord, seed=5, device=dev)
         wall, t = timed_steps(wl.step, 10, 3, settle_ms=settle_ms)
         gbs = wl.bytes_per_column * ncol / t / 1e9
-        out[name] = {"columns_per_s": ncol / t, "ms_per_step": t * 1e3, "hbm_gbs": gbs,
-                     "frac_hbm_peak": gbs / W.HBM_PEAK_GBS}
+        out[name] = with_counters(name, {"columns_per_s": ncol / t, "ms_per_step": t * 1e3, "hbm_gbs": gbs,
+                                         "frac_hbm_peak": gbs / W.HBM_PEAK_GBS}, wl.bytes_per_column * ncol)
         del wl
     # config #4: one ML-stepper step (predict + fused limiter/diagnostics/apply + global
     # means) on a float64 C96 state, one GPU
     wl = W.make_stepper_workload(96, seed=11, device=dev)
     wall, t = timed_steps(wl.step, 20, 3, settle_ms=settle_ms)
-    out["stepper_c96"] = {"columns_per_s": wl.ncol / (wall / 20), "ms_per_step": wall / 20 * 1e3,
-                          "note": "wall clock per step (several kernels + host glue)"}
+    out["stepper_c96"] = with_counters("stepper_c96", {
+        "columns_per_s": wl.ncol / (wall / 20), "ms_per_step": wall / 20 * 1e3,
+        "note": "wall clock per step (several kernels + host glue); counters: the fused epilogue kernel"})
     del wl
     # config #5: Zhao-Carr microphysics emulator on a C384 state.  Its arithmetic is bf16
     # MFMA (1e-3 rel): the bf16x3 kernel (csrc/dense_b3.hip, 3 bf16 MFMAs per f32
@@ -187,23 +212,26 @@ def extra_measurements(dev, settle_ms=150.0):
             rec["frac_f32_mfma_peak"] = tf / W.FP32_MFMA_PEAK_TFLOPS
         else:
             rec["frac_bf16_mfma_peak"] = 3 * tf / W.BF16_MFMA_PEAK_TFLOPS
-        out["emulator_c384" if prec == "bf16x3" else "emulator_c384_f32"] = rec
+        leg = "emulator_c384" if prec == "bf16x3" else "emulator_c384_f32"
+        out[leg] = with_counters(leg, rec, wl.ncol * wl.bytes_per_column)
         del wl
     # config #2's model on the bf16x3 kernel (8e-6 rel: not the headline's exact-f32 path)
     wl = W.make_dense_workload(384, seed=3, device=dev, precision="bf16x3")
     wall, t = timed_steps(wl.step, 10, 3, settle_ms=settle_ms)
     tf = wl.ncol * wl.flops_per_column / t / 1e12
-    out["dense_c384_bf16x3"] = {"columns_per_s": wl.ncol / t, "ms_per_step": t * 1e3, "tflops_f32_equiv": tf,
-                                "frac_bf16_mfma_peak": 3 * tf / W.BF16_MFMA_PEAK_TFLOPS}
+    out["dense_c384_bf16x3"] = with_counters("dense_c384_bf16x3", {
+        "columns_per_s": wl.ncol / t, "ms_per_step": t * 1e3, "tflops_f32_equiv": tf,
+        "frac_bf16_mfma_peak": 3 * tf / W.BF16_MFMA_PEAK_TFLOPS}, wl.ncol * wl.bytes_per_column)
     del wl
     # config #3: fused C384 -> C48 pressure-level coarsen (1 and 4 fields), fine columns/s
     for nf in (1, 4):
         wl = W.make_coarsen_workload(384, 8, nf, seed=7, device=dev)
         wall, t = timed_steps(wl.step, 10, 3, settle_ms=settle_ms)
         gbs = wl.bytes_per_column * wl.ncol_fine / t / 1e9
-        out[f"coarsen_c384_to_c48_{nf}field"] = {
+        leg = f"coarsen_c384_to_c48_{nf}field"
+        out[leg] = with_counters(leg, {
             "fine_columns_per_s": wl.ncol_fine / t, "ms_per_step": t * 1e3, "hbm_gbs": gbs,
-            "frac_hbm_peak": gbs / W.HBM_PEAK_GBS}
+            "frac_hbm_peak": gbs / W.HBM_PEAK_GBS}, wl.bytes_per_column * wl.ncol_fine)
         del wl
     torch.cuda.empty_cache()
     return out

@@ -40,7 +40,11 @@ EXPORTED_SYMBOLS = (
     "fv3_area_weighted_sums",
     "fv3_area_weighted_sums_f64",
     "fv3_level_sums",
+    "fv3_level_sums_f64",
+    "fv3_level_sums_u8",
     "fv3_ml_epilogue",
+    "fv3_standard_normalize",
+    "fv3_standard_denormalize",
 )
 ABI_VERSION = 3
 
@@ -141,6 +145,10 @@ _SIGNATURES = {
     "fv3_area_weighted_sums": (_I, [ctypes.POINTER(_P), _I, _P, _I64, _P, _P]),
     "fv3_area_weighted_sums_f64": (_I, [ctypes.POINTER(_P), _I, _P, _I64, _P, _P]),
     "fv3_level_sums": (_I, [_P, Layout, _I64, _I, _P, _P]),
+    "fv3_level_sums_f64": (_I, [_P, Layout, _I64, _I, _P, _P]),
+    "fv3_level_sums_u8": (_I, [_P, Layout, _I64, _I, _P, _P]),
+    "fv3_standard_normalize": (_I, [_P, _I, Layout, _P, _P, _I, _P, Layout, _I64, _I, _P]),
+    "fv3_standard_denormalize": (_I, [_P, Layout, _P, _P, _I, _P, Layout, _I64, _I, _P]),
     "fv3_ml_epilogue": (_I, [ctypes.POINTER(EpilogueIO), Layout, _I64, _I, _I, _D, _I, _I, _P]),
 }
 

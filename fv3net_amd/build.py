@@ -1,9 +1,11 @@
 """Build the in-tree HIP extension ``fv3net_amd/_lib/libfv3net_amd.so`` for gfx950.
 
-Plain ``hipcc --offload-arch=gfx950 -shared`` over ``csrc/*.hip`` + ``csrc/*.cpp``;
-no torch extension machinery (the C ABI has no torch types), no JIT cache: the
-built ``.so`` sits in the tree so it travels to the GPU box with the snapshot.
+Plain ``hipcc --offload-arch=gfx950``: each ``csrc/*.hip`` / ``csrc/*.cpp`` compiles to
+its own object (in parallel, cached by content hash under ``_lib/obj``), then one
+``-shared`` link.  No torch extension machinery (the C ABI has no torch types), no JIT
+cache: the built ``.so`` sits in the tree so it travels to the GPU box with the snapshot.
 """
+import concurrent.futures
 import glob
 import hashlib
 import os
@@ -13,43 +15,82 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "_lib")
+OBJ_DIR = os.path.join(LIB_DIR, "obj")
 LIB = os.path.join(LIB_DIR, "libfv3net_amd.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("FV3_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: one rounding per operation, required for bit parity of the
 # mappm / coarsen paths with the x86 reference build (no FMA there).
-FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", f"--offload-arch={ARCH}"]
+CFLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", f"--offload-arch={ARCH}"]
+FLAGS = CFLAGS + ["-shared"]
 
 
 def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
 
 
+def _headers():
+    return sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(ROOT, "include", "fv3net_amd.h")]
+
+
+def _read(p):
+    with open(p, "rb") as f:
+        return f.read()
+
+
+def _obj_digest(src, hdr_blob):
+    h = hashlib.sha256()
+    h.update(_read(src) + hdr_blob + " ".join(CFLAGS).encode())
+    return h.hexdigest()[:20]
+
+
 def _digest():
     h = hashlib.sha256()
-    for p in sources() + sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [
-        os.path.join(ROOT, "include", "fv3net_amd.h")
-    ]:
-        with open(p, "rb") as f:
-            h.update(p.encode() + f.read())
+    for p in sources() + _headers():
+        h.update(p.encode() + _read(p))
     h.update(" ".join(FLAGS).encode())
     return h.hexdigest()
 
 
+def _compile(src, obj, verbose):
+    cmd = [HIPCC] + CFLAGS + ["-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(obj + ".tmp", obj)
+    return obj
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     """Compile the extension if sources changed; returns the library path."""
-    os.makedirs(LIB_DIR, exist_ok=True)
+    os.makedirs(OBJ_DIR, exist_ok=True)
     stamp = LIB + ".sha256"
     digest = _digest()
     if not force and os.path.exists(LIB) and os.path.exists(stamp):
         with open(stamp) as f:
             if f.read().strip() == digest:
                 return LIB
+    hdr_blob = b"".join(_read(p) for p in _headers())
+    objs, todo = [], []
+    for src in sources():
+        base = os.path.splitext(os.path.basename(src))[0]
+        obj = os.path.join(OBJ_DIR, f"{base}.{_obj_digest(src, hdr_blob)}.o")
+        objs.append(obj)
+        if force or not os.path.exists(obj):
+            todo.append((src, obj))
+    jobs = max(1, min(len(todo), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 8))
+    with concurrent.futures.ThreadPoolExecutor(jobs) as ex:
+        for f in [ex.submit(_compile, s, o, verbose) for s, o in todo]:
+            f.result()
+    keep = set(objs)
+    for stale in glob.glob(os.path.join(OBJ_DIR, "*.o")):
+        if stale not in keep:
+            os.remove(stale)
     tmp = LIB + ".tmp"
-    cmd = [HIPCC] + FLAGS + ["-I", os.path.join(ROOT, "include"), "-o", tmp] + sources()
+    cmd = [HIPCC] + FLAGS + ["-o", tmp] + objs
     if verbose:
-        print(" ".join(cmd))
+        print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
     with open(stamp, "w") as f:

@@ -129,7 +129,8 @@ __global__ __launch_bounds__(kSumBlock) void area_sums_stage2(const double* __re
 
 // out[k] = sum over columns of x[k][c]: one block per level, grid-stride lanes then
 // the fixed LDS tree (bitwise reproducible)
-__global__ __launch_bounds__(kSumBlock) void level_sums_kernel(const float* __restrict__ x, fv3_layout xl,
+template <typename T>
+__global__ __launch_bounds__(kSumBlock) void level_sums_kernel(const T* __restrict__ x, fv3_layout xl,
                                                                int64_t ncol, double* __restrict__ out)
 {
     __shared__ double sh[kSumBlock];
@@ -143,16 +144,35 @@ __global__ __launch_bounds__(kSumBlock) void level_sums_kernel(const float* __re
 }  // namespace
 }  // namespace fv3
 
-extern "C" int fv3_level_sums(const float* x, fv3_layout x_l, int64_t ncol, int nz, double* out, void* stream)
+namespace fv3 {
+namespace {
+template <typename T>
+int level_sums_impl(const T* x, fv3_layout x_l, int64_t ncol, int nz, double* out, void* stream)
 {
-    fv3::clear_error();
+    clear_error();
     FV3_REQUIRE(ncol >= 0 && nz >= 1, "level_sums: bad sizes ncol=%lld nz=%d", (long long)ncol, nz);
     FV3_REQUIRE(x && out, "level_sums: NULL array");
-    FV3_REQUIRE(ncol == 0 || fv3::layout_ok(x_l, ncol), "level_sums: bad layout");
-    hipLaunchKernelGGL(fv3::level_sums_kernel, dim3(nz), dim3(fv3::kSumBlock), 0, (hipStream_t)stream, x, x_l,
-                       ncol, out);
+    FV3_REQUIRE(ncol == 0 || layout_ok(x_l, ncol), "level_sums: bad layout");
+    hipLaunchKernelGGL(level_sums_kernel<T>, dim3(nz), dim3(kSumBlock), 0, (hipStream_t)stream, x, x_l, ncol, out);
     FV3_LAUNCH_CHECK();
     return FV3_OK;
+}
+}  // namespace
+}  // namespace fv3
+
+extern "C" int fv3_level_sums(const float* x, fv3_layout x_l, int64_t ncol, int nz, double* out, void* stream)
+{
+    return fv3::level_sums_impl(x, x_l, ncol, nz, out, stream);
+}
+
+extern "C" int fv3_level_sums_f64(const double* x, fv3_layout x_l, int64_t ncol, int nz, double* out, void* stream)
+{
+    return fv3::level_sums_impl(x, x_l, ncol, nz, out, stream);
+}
+
+extern "C" int fv3_level_sums_u8(const uint8_t* x, fv3_layout x_l, int64_t ncol, int nz, double* out, void* stream)
+{
+    return fv3::level_sums_impl(x, x_l, ncol, nz, out, stream);
 }
 
 extern "C" int fv3_column_integral(const float* field, fv3_layout field_l, const float* delp,

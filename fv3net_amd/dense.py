@@ -297,7 +297,9 @@ class DenseColumnModel:
                 and all(torch.is_tensor(t) and t.is_cuda and t.dtype == torch.float64 for t in inputs))
         ts, lays = [], []
         ncol = None
+        copied = []  # inputs the kernel reads through a copy (not the caller's buffer)
         for v, (t, ax) in enumerate(zip(inputs, level_axes)):
+            orig = t
             if ax is None:
                 t = _device.to_device_f32(t, contiguous=False).unsqueeze(0)
                 ax = 0
@@ -307,6 +309,8 @@ class DenseColumnModel:
             if ncol is not None and n != ncol:
                 raise ValueError("inputs disagree on the number of columns")
             ncol = n
+            if not (torch.is_tensor(orig) and orig.is_cuda and t.data_ptr() == orig.data_ptr()):
+                copied.append(c.input_variables[v])
             ts.append(t)
             lays.append(lay)
         ref = ts[0]
@@ -329,6 +333,7 @@ class DenseColumnModel:
         if any(l.ncol_blk != lays[0].ncol_blk for l in lays + olays):
             raise ValueError("all inputs/outputs must share the horizontal layout")
         bound = BoundForward(self, ts, lays, outputs, olays, ncol, prec, in64=in64)
+        self._last_copied = copied
         self._last_cast_copy = False
         try:
             bound(stream)
@@ -353,6 +358,11 @@ class DenseColumnModel:
             raise NotImplementedError("this model reads float64 inputs through a float32 copy made per call "
                                       "(no 8-wave kernel or residual outputs): call forward() each step, "
                                       "or bind float32 buffers")
+        if self._last_copied:
+            # a bound call on a snapshot would never see the caller's in-place updates
+            raise ValueError(f"bind: inputs {self._last_copied} are read through a copy (host/numpy, another "
+                             "dtype than the kernel reads, or a layout the kernel cannot address); bind "
+                             "device buffers the kernel reads in place, or call forward() each step")
         return self._last_bound
 
     # ---- persistence -------------------------------------------------------------

@@ -161,10 +161,22 @@ def level_sums(field, stream=None):
     """Device float64 per-level horizontal sums of a (z, ...) field (deterministic
     fixed-tree HIP reduction): the per-rank part of metrics.py:27-32."""
     _device.require_gpu()
-    t = _device.to_device_f32(field)
-    lay, ncol, nz = _device.level_layout(t, 0)
+    lib = _native.load()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    src = field if torch.is_tensor(field) else torch.from_numpy(np.ascontiguousarray(field))
+    if src.dtype in (torch.float64, torch.uint8):  # read in the field's own dtype (no f32 rounding)
+        t = src.to(dev)
+        fn = lib.fv3_level_sums_f64 if t.dtype == torch.float64 else lib.fv3_level_sums_u8
+    else:  # float32, or integer/bool flags that float32 holds exactly
+        t = _device.to_device_f32(src)
+        fn = lib.fv3_level_sums
+    try:
+        lay, ncol, nz = _device.level_layout(t, 0)
+    except ValueError:
+        t = t.contiguous()
+        lay, ncol, nz = _device.level_layout(t, 0)
     out = torch.empty(nz, dtype=torch.float64, device=t.device)
-    st = _native.load().fv3_level_sums(t.data_ptr(), lay, ncol, nz, out.data_ptr(), _device.stream_handle(stream))
+    st = fn(t.data_ptr(), lay, ncol, nz, out.data_ptr(), _device.stream_handle(stream))
     _native.check(st, "level_sums")
     return out
 

@@ -54,9 +54,13 @@ class MappmPlan:
 
     def __init__(self, pe1, q1, pe2, iv: int = 1, kord: int = 1, out=None, stream=None):
         self.out = mappm_device(pe1, q1, pe2, iv, kord, out=out, stream=stream)  # validates, first run
-        pe1, l1, _, _ = _device.column_view(pe1, 0)
-        q1, lq, ncol, km = _device.column_view(q1, 0)
-        pe2, l2, _, kp2 = _device.column_view(pe2, 0)
+        views = [_device.column_view(a, 0) for a in (pe1, q1, pe2)]
+        for name, a, v in zip(("pe1", "q1", "pe2"), (pe1, q1, pe2), views):
+            if not (torch.is_tensor(a) and a.is_cuda and v[0].data_ptr() == a.data_ptr()):
+                # a plan over a copy would keep remapping the stale snapshot
+                raise ValueError(f"MappmPlan: {name} is read through a copy (host, float64 or an unaddressable "
+                                 "layout); pass float32 CUDA buffers, or call mappm_device each time")
+        (pe1, l1, _, _), (q1, lq, ncol, km), (pe2, l2, _, kp2) = views
         lo, _, _ = _device.level_layout(self.out, 0)
         self._keep = (pe1, q1, pe2)
         self._fn = _native.load().fv3_mappm_ex
@@ -71,8 +75,10 @@ class MappmPlan:
 def mappm(pe1, q1, pe2, i1, i2, iv, kord, ptop):
     """f2py-compatible signature of ``mappm.mappm`` (mappm.f90:10).
 
-    ``pe1 (ncol, km+1)``, ``q1 (ncol, km)``, ``pe2 (ncol, kn+1)`` host arrays; columns
-    ``i1..i2`` (1-based, inclusive) are remapped; returns float32 ``(i2-i1+1, kn)``.
+    ``pe1 (ncol, km+1)``, ``q1 (ncol, km)``, ``pe2 (ncol, kn+1)`` host arrays.  As in the
+    f2py signature (``pe1(i1:i2, km+1)``), the arrays hold exactly the columns
+    ``i1..i2`` (1-based, inclusive): ``ncol == i2 - i1 + 1``; returns float32
+    ``(ncol, kn)``.
     """
     i1 = int(i1)
     i2 = int(i2)
@@ -81,6 +87,7 @@ def mappm(pe1, q1, pe2, i1, i2, iv, kord, ptop):
     pe2 = np.asarray(pe2, dtype=np.float32)
     if pe1.ndim != 2 or q1.ndim != 2 or pe2.ndim != 2:
         raise ValueError("mappm expects 2-D (column, level) arrays")
-    sl = slice(i1 - 1, i2)
-    res = mappm_device(pe1[sl].T, q1[sl].T, pe2[sl].T, iv=int(iv), kord=int(kord))
+    if not (pe1.shape[0] == q1.shape[0] == pe2.shape[0] == i2 - i1 + 1):
+        raise ValueError(f"mappm: arrays hold {pe1.shape[0]} columns, i1..i2 = {i1}..{i2} names {i2 - i1 + 1}")
+    res = mappm_device(pe1.T, q1.T, pe2.T, iv=int(iv), kord=int(kord))
     return res.T.contiguous().cpu().numpy()

@@ -55,7 +55,12 @@ def ml_epilogue(dq1, dq2, sphum, delp, temperature, dt: float, physics_precip=No
         t = torch.as_tensor(x).to(device=dev, dtype=state_dtype)
         return t if t.is_contiguous() else t.contiguous()
 
+    sphum_in, temperature_in = sphum, temperature
     sphum, delp, temperature = st(sphum), st(delp), st(temperature)
+    if in_place and (sphum is not sphum_in or temperature is not temperature_in):
+        # the kernel would update a copy and leave the caller's state unchanged
+        raise ValueError("ml_epilogue(in_place=True) needs the specific humidity and air temperature as "
+                         "contiguous CUDA tensors of one dtype (float32 or float64)")
     dq1 = _device.to_device_f32(dq1)
     dq2 = _device.to_device_f32(dq2)
     for name, t in (("dQ1", dq1), ("dQ2", dq2), (DELP, delp), (TEMP, temperature)):

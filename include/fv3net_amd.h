@@ -223,6 +223,24 @@ int fv3_area_weighted_sums_f64(const double* const* diags, int n_diag, const dou
 /* Per-level horizontal sums out[k] = sum_c x[k][c] in float64 (fixed reduction tree):
  * the per-rank part of metrics.py:27-32 global_horizontal_sum. */
 int fv3_level_sums(const float* x, fv3_layout x_l, int64_t ncol, int nz, double* out, void* stream);
+/* The same over a float64 field (summed without a float32 rounding, as numpy sums a
+ * float64 DataArray) and over a uint8 flag field (the stepper's
+ * specific_humidity_limiter_active, machine_learning.py:301-303, read in place). */
+int fv3_level_sums_f64(const double* x, fv3_layout x_l, int64_t ncol, int nz, double* out, void* stream);
+int fv3_level_sums_u8(const unsigned char* x, fv3_layout x_l, int64_t ncol, int nz, double* out, void* stream);
+
+/* ---- StandardScaler (external/fv3fit/fv3fit/_shared/scaler.py:36-100) -------------
+ * As the PytorchPredictor applies it around its model (fv3fit/pytorch/predict.py:
+ * 299-399):  out = float32((x - mean) / std) computed in float64 (x float32, or float64
+ * when x_f64), and out = y * std + mean in float64 from the model's float32 y.
+ * mean/std are DEVICE float64 arrays of n_params = nz values (per level) or 1 (a 2-D
+ * variable).  Bit-identical to numpy's float64 arithmetic. */
+int fv3_standard_normalize(const void* x, int x_f64, fv3_layout x_l, const double* mean,
+                           const double* std_, int n_params, float* out, fv3_layout out_l,
+                           int64_t ncol, int nz, void* stream);
+int fv3_standard_denormalize(const float* y, fv3_layout y_l, const double* mean, const double* std_,
+                             int n_params, double* out, fv3_layout out_l, int64_t ncol, int nz,
+                             void* stream);
 
 /* ---- ML stepper epilogue: limiter + diagnostics + apply (config #4) --------------
  * One pass per column over everything the prognostic loop does with a (dQ1, dQ2)

@@ -3,20 +3,23 @@ into bf16 hi + lo, products hi*hi + lo*hi + hi*lo on v_mfma_f32_32x32x16_bf16) a
 the float64 evaluation of the reference graph (oracle/dense.py; reference
 external/fv3fit/fv3fit/keras/_models/dense.py:234-305).
 
-Tolerance: max |gpu - ref64| <= 5e-5 * max |ref64| per output variable.  The split
-keeps ~16 mantissa bits per operand; the CPU model of it (tools/bf16_study.py) gives
-8e-6 on the 2x256 model, so 5e-5 has margin while any fragment-layout or permutation
-error (O(1)) fails.  BASELINE config #5's contract for this path is 1e-3 rel
-(test_emulator.py); config #2's 1e-5 headline runs the exact-f32 kernel.
+Tolerance: max |gpu - ref64| <= 1e-4 * max |ref64| for EVERY output level (tests/parity.py;
+the emulator's bf16x3 bound).  The split keeps ~16 mantissa bits per operand; the CPU
+model of it (tools/bf16_study.py) gives 8e-6 over a whole variable on the 2x256 model and
+up to ~5e-5 on its worst single level (round 2, GPU), so 1e-4 has margin while any
+fragment-layout or permutation error (O(1)) fails.  BASELINE config #5's contract for
+this path is 1e-3 rel (test_emulator.py); config #2's 1e-5 headline runs the exact-f32
+kernel.
 """
 import numpy as np
 import pytest
 
 from oracle.dense import dense_predict
+from tests.parity import assert_per_level
 
 pytestmark = pytest.mark.gpu
 
-RTOL_B3 = 5e-5
+RTOL_B3 = 1e-4
 
 
 def _to_samples(a):
@@ -25,10 +28,8 @@ def _to_samples(a):
 
 
 def _check(gpu_out, ref64, rtol=RTOL_B3):
-    for g, r in zip(gpu_out, ref64):
-        scale = max(np.abs(r).max(), 1e-30)
-        err = np.abs(g.astype(np.float64) - r).max() / scale
-        assert err <= rtol, f"max rel err {err:.3e} > {rtol}"
+    for o, (g, r) in enumerate(zip(gpu_out, ref64)):
+        assert_per_level(g, r, rtol, f"output {o}")
 
 
 def _model(cfg_kwargs, seed=1, bias_scale=0.1, samples=None):
@@ -123,7 +124,10 @@ def test_tiny_and_ragged(gpu, n):
     m.forward([torch.from_numpy(x.T.copy()).cuda()], outputs=[out[:, :n]])
     o = out.cpu().numpy()
     assert (o[:, n:] == 7.0).all()
-    _check([o[:, :n].T], dense_predict([x], m.oracle_params(), np.float64))
+    # level magnitudes from 512 columns of the same model (tests/parity.py)
+    wide = rng.normal(0, 1, (512, 79)).astype(np.float32)
+    scale = np.abs(dense_predict([wide], m.oracle_params(), np.float64)[0]).max(axis=0)
+    assert_per_level(o[:, :n].T, dense_predict([x], m.oracle_params(), np.float64)[0], RTOL_B3, "y", scale=scale)
 
 
 def test_c384_persistent_tiles_and_determinism(gpu):

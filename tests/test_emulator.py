@@ -1,11 +1,13 @@
 """Zhao-Carr microphysics emulator (BASELINE config #5): the fused
 kernel vs the numpy restatement of the inference graph (oracle/emulator.py).
 Contract: 1e-3 rel (north_star, bf16 MFMA); the bf16x3 path (the config's default) is
-held to 1e-4 on every output, the exact-f32 MFMA path to 1e-5."""
+held to 1e-4 on every output level, the exact-f32 MFMA path to 1e-5 (tests/parity.py:
+max over columns / max |ref| of each level)."""
 import numpy as np
 import pytest
 
 from oracle import emulator as OE
+from tests.parity import assert_per_level
 
 
 def test_product_spec_matches_the_reference_restatement():
@@ -64,8 +66,7 @@ def test_emulator_matches_oracle(gpu, precision, rtol):
         g = got[name].cpu().numpy()
         r = ref[name]
         r = r[:, 0] if o["nz"] == 1 else r.T
-        err = np.abs(g - r).max() / np.abs(r).max()
-        assert err <= rtol, (name, err)
+        assert_per_level(g.T if g.ndim == 2 else g, r.T if r.ndim == 2 else r, rtol, name)
         if o.get("residual_of"):  # the difference itself, recovered from the after-state
             d = g.astype(np.float64) - raw[o["residual_of"]].T.astype(np.float64)
             derr = np.abs(d - ref[o["name"]].T).max() / np.abs(ref[o["name"]]).max()

@@ -214,3 +214,33 @@ def test_prepared_plan_matches_and_tracks_contents(gpu):
     got = plan().cpu().numpy()
     assert _bits_equal(got, mappm_device(*d, 1, 4).cpu().numpy())
     assert _bits_equal(got, oracle_mappm(pe1, q * 2, pe2, 1, 4))
+
+
+def test_prepared_plan_refuses_copies(gpu):
+    """A plan bound to a copy (float64 input, host array) would keep remapping a stale
+    snapshot: MappmPlan refuses it."""
+    import torch
+
+    from fv3net_amd.mappm import MappmPlan
+
+    rng = np.random.default_rng(22)
+    pe1, q, pe2 = _columns(rng, 79, 50, 64)
+    d = [torch.from_numpy(a).cuda() for a in (pe1, q, pe2)]
+    with pytest.raises(ValueError, match="copy"):
+        MappmPlan(d[0], d[1].double(), d[2], 1, 1)
+    with pytest.raises(ValueError, match="copy"):
+        MappmPlan(d[0], q, d[2], 1, 1)
+
+
+def test_f2py_signature_column_count(gpu):
+    """pe1(i1:i2, km+1): the arrays hold exactly columns i1..i2 (f2py), so any
+    i1 > 1 call passes i2-i1+1 columns; a mismatch is an error, not a silent slice."""
+    from fv3net_amd import mappm as mappm_mod
+
+    rng = np.random.default_rng(23)
+    pe1, q, pe2 = _columns(rng, 79, 50, 10)
+    full = mappm_mod.mappm(pe1.T, q.T, pe2.T, 1, 10, 1, 1, 0.0)
+    part = mappm_mod.mappm(pe1.T[3:7], q.T[3:7], pe2.T[3:7], 4, 7, 1, 1, 0.0)
+    assert _bits_equal(part, full[3:7])
+    with pytest.raises(ValueError, match="columns"):
+        mappm_mod.mappm(pe1.T, q.T, pe2.T, 4, 7, 1, 1, 0.0)

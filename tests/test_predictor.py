@@ -9,6 +9,8 @@ import os
 import numpy as np
 import pytest
 
+from tests.parity import assert_per_level
+
 from fv3net_amd import dataset as D
 from fv3net_amd import predictor as P
 from fv3net_amd.predictor import SAMPLE_DIM_NAME, Z_DIM_NAMES, stack
@@ -151,7 +153,7 @@ def test_dense_predictor_end_to_end(gpu):
     got1 = out["dQ1"].values.transpose(1, 2, 0).reshape(-1, nz)
     got3 = out["total_precip"].values.reshape(-1, 1)
     for g, r in ((got1, ref[0]), (got3, ref[2])):
-        assert np.abs(g - r).max() / np.abs(r).max() <= 1e-5
+        assert_per_level(g, r, 1e-5)
     np.testing.assert_array_equal(out.coords["x"], np.arange(nx))
     # device-resident input stays on device
     Xd = D.Dataset({k: D.DataArray(torch.from_numpy(X[k].values.astype(np.float32)).cuda(), X[k].dims)
@@ -202,4 +204,4 @@ def test_dense_predictor_level_axis_anywhere(gpu, dims):
     g1 = cols(out["dQ1"].data.cpu().numpy())
     g2 = out["pr"].data.cpu().numpy().reshape(-1, 1)
     for g, r in ((g1, ref[0]), (g2, ref[1])):
-        assert np.abs(g - r).max() / np.abs(r).max() <= 1e-5
+        assert_per_level(g, r, 1e-5)

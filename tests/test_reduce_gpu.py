@@ -111,3 +111,20 @@ def test_metrics_mirrors_single_rank(gpu):
     sums = D.globally_sum_3d_diagnostics(diags, include=["T"])
     np.testing.assert_allclose(sums["T_global_sum"], t3.astype(np.float64).sum(axis=(1, 2)), rtol=1e-12,
                                atol=1e-10)
+
+
+@pytest.mark.gpu
+def test_level_sums_keep_dtype(gpu):
+    """float64 fields are summed without a float32 rounding and the uint8
+    limiter flag is read in place; the sums equal numpy's in float64."""
+    import torch
+
+    from fv3net_amd import distributed as D
+
+    rng = np.random.default_rng(9)
+    f = rng.normal(0, 1, (79, 24, 24)) * (1 + 1e-9 * rng.normal(size=(79, 24, 24)))
+    got = D.level_sums(torch.from_numpy(f).cuda()).cpu().numpy()
+    np.testing.assert_allclose(got, f.sum(axis=(1, 2)), rtol=1e-13, atol=1e-12)
+    flag = (rng.uniform(size=(79, 24, 24)) < 0.3).astype(np.uint8)
+    got = D.level_sums(torch.from_numpy(flag).cuda()).cpu().numpy()
+    np.testing.assert_array_equal(got, flag.sum(axis=(1, 2)).astype(np.float64))

@@ -170,3 +170,20 @@ def test_pure_ml_stepper_mirror(gpu):
     updated, fracs = stepper.apply()
     _bits(updated["specific_humidity"].cpu().numpy().reshape(nz, -1), ref["specific_humidity"])
     _bits(updated["total_precipitation"].cpu().numpy().reshape(-1), ref["total_precipitation"])
+
+
+@pytest.mark.gpu
+def test_in_place_refuses_copies(gpu):
+    """in_place=True with a state the kernel would read through a copy (mixed dtypes,
+    host arrays) would leave the caller's state unchanged: refused."""
+    import torch
+
+    from fv3net_amd.stepper import ml_epilogue
+
+    rng = np.random.default_rng(4)
+    dq1, dq2, q, delp, T, _ = _state(rng, ncol=64)
+    qd = torch.from_numpy(q).cuda()
+    with pytest.raises(ValueError, match="in_place"):
+        ml_epilogue(dq1, dq2, qd, delp, torch.from_numpy(T).cuda().float(), 450.0, in_place=True)
+    with pytest.raises(ValueError, match="in_place"):
+        ml_epilogue(dq1, dq2, qd, delp, T, 450.0, in_place=True)

@@ -1,0 +1,31 @@
+#!/usr/bin/env bash
+# Per-kernel PMC passes over every bench leg:  tools/pmc_all.sh <tag> [legs...]
+# Each (leg, counter set) is its own rocprofv3 --pmc run (no tracing domains), under its own
+# time limit; a failed pass is recorded and the next one runs (a pass that exceeds the
+# hardware's counter slots is killed by its timeout).  Summary: tools/pmc_collect.py.
+set -uo pipefail
+TAG=$1; shift
+LEGS=("$@")
+if [ ${#LEGS[@]} -eq 0 ]; then
+  LEGS=(calib dense_c48 dense_c384 dense_c384_bf16x3 emulator_c384 emulator_c384_f32 mappm_c384_k1 mappm_c384_k10 mappm_c12 coarsen_1f coarsen_4f stepper_c96)
+fi
+OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out/pmc_${TAG}
+mkdir -p "$OUT"; export TMPDIR=/tmp
+SETS=("FETCH_SIZE"
+      "WRITE_SIZE"
+      "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE"
+      "VALUBusy VALUUtilization")
+for leg in "${LEGS[@]}"; do
+  mkdir -p "$OUT/$leg"
+  i=0
+  for set in "${SETS[@]}"; do
+    i=$((i+1))
+    timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d "$OUT/$leg/p$i" -o run -- \
+        python3 tools/pmc_drive.py "$leg" 5 > "$OUT/$leg/p$i.log" 2>&1
+    rc=$?
+    echo "$leg pass $i rc=$rc" | tee -a "$OUT/status.txt"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping: $leg pass $i rc=$rc"; exit $rc; fi
+  done
+done
+python3 tools/pmc_collect.py "$OUT" > "$OUT/summary.json"
+echo "pmc done: $OUT"

@@ -1,0 +1,95 @@
+"""Summarise tools/pmc_all.sh passes: per leg and kernel, mean counter values over the
+last N dispatches, plus HBM bytes per launch with per-width FETCH/WRITE calibration.
+
+    python3 tools/pmc_collect.py gpurun_out/pmc_<tag>  > summary.json
+
+Calibration (leg `calib`, tools/calib.hip): 1 GiB read/written with 4/8/16 B per lane;
+factor_w = true bytes / counted bytes.  A kernel's reads are scaled by the factor of the
+width it uses (`WIDTH` below; MI355X_MICROARCH.md §HBM documents only the 16 B/lane
+read factor, 2.0), writes likewise.
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+N_LAST = 5
+# read width (bytes per lane) of each kernel's dominant streams
+WIDTH = {"dense_forward_kernel": 4, "dense_b3_kernel": 4, "mappm": 4, "regrid_coarsen": 4,
+         "ml_epilogue_kernel": 8, "area_sums": 8, "level_sums": 4}
+
+
+def short(name):
+    m = re.search(r"(\w*kernel\w*|calib_\w+<[^>]*>|\w+_stage\d)", name)
+    return (m.group(1) if m else name.split("(")[0])[:60]
+
+
+def load_pass(d):
+    """-> {kernel: [ {counter: value} per dispatch in order ]}"""
+    per = defaultdict(lambda: defaultdict(dict))
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                k = short(row.get("Kernel_Name", ""))
+                did = int(row.get("Dispatch_Id", row.get("Correlation_Id", 0)))
+                c = row["Counter_Name"]
+                per[k][did][c] = per[k][did].get(c, 0.0) + float(row["Counter_Value"])
+    return {k: [v[i] for i in sorted(v)] for k, v in per.items()}
+
+
+def width_of(k):
+    for key, w in WIDTH.items():
+        if key in k:
+            return w
+    return 16
+
+
+def main(root):
+    legs = {}
+    for leg_dir in sorted(glob.glob(os.path.join(root, "*"))):
+        if not os.path.isdir(leg_dir):
+            continue
+        leg = os.path.basename(leg_dir)
+        merged = defaultdict(dict)
+        for pdir in sorted(glob.glob(os.path.join(leg_dir, "p*"))):
+            if not os.path.isdir(pdir):
+                continue
+            for k, disp in load_pass(pdir).items():
+                last = disp[-N_LAST:] if leg != "calib" else disp[-1:]
+                keys = set().union(*[set(x) for x in last]) if last else set()
+                for c in keys:
+                    vals = [x[c] for x in last if c in x]
+                    merged[k][c] = sum(vals) / len(vals)
+                merged[k]["_dispatches"] = len(disp)
+        legs[leg] = merged
+    factors = {}
+    cal = legs.get("calib", {})
+    for w, tname in ((4, "float"), (8, "B8"), (16, "B16")):
+        r = cal.get(f"calib_read<{tname}>", {}).get("FETCH_SIZE")
+        wr = cal.get(f"calib_write<{tname}>", {}).get("WRITE_SIZE")
+        factors[w] = {"read": (2 ** 30 / (r * 1024)) if r else None, "write": (2 ** 30 / (wr * 1024)) if wr else None}
+    out = {"calibration": factors, "legs": {}}
+    for leg, ks in legs.items():
+        if leg == "calib":
+            continue
+        rec = {}
+        for k, c in ks.items():
+            w = width_of(k)
+            fr = factors.get(w, {}).get("read") or 2.0
+            fw = factors.get(w, {}).get("write") or 1.0
+            e = dict(c)
+            if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+                e["hbm_bytes_per_launch"] = (fr * c["FETCH_SIZE"] + fw * c["WRITE_SIZE"]) * 1024
+                e["read_factor"], e["write_factor"] = fr, fw
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in c and c.get("SQ_BUSY_CU_CYCLES"):
+                e["mfma_busy_frac"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (4 * c["SQ_BUSY_CU_CYCLES"])
+            rec[k] = e
+        out["legs"][leg] = rec
+    json.dump(out, sys.stdout, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
