@@ -1068,9 +1068,12 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
     a.kp = m->kp;
     a.in_steps_total = m->steps_total;
     if (const int st = b3_pack(m, d)) {  // the bf16x3 weight stream (fv3_dense_forward_ex)
-        (void)hipFree(m->dbuf);
         b3_free(m);
-        return st;
+        if (st != FV3_ERR_UNSUPPORTED) {
+            (void)hipFree(m->dbuf);
+            return st;
+        }
+        clear_error();  // a model the bf16x3 kernel cannot pack still runs in exact f32
     }
     *out = guard.release();
     return FV3_OK;

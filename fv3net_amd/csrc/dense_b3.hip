@@ -50,14 +50,16 @@ typedef float b3f4 __attribute__((ext_vector_type(4)));
 
 namespace fv3 {
 
-constexpr int kB3Groups = 128;  // 8-feature input groups (<= 1024 padded input features)
-constexpr int kB3Cols = 128;    // columns per block tile: 4 waves x 32
+constexpr int kB3Groups = 128;    // 8-feature input groups (<= 1024 padded input features)
+constexpr int kB3Cols = 128;      // columns per block tile: 4 waves x 32
+constexpr int kB3OutGroups = 64;  // 8-row output groups (<= 512 padded output rows)
 
 struct B3Pack {
     void* dbuf = nullptr;
     int ht = 0, hp = 0, kp1 = 0, n1 = 0, nhx = 0, npass = 0, n_otile = 0, kop = 0, nch = 0;
     int nconst = 0, wbytes = 0, any_log = 0;
     std::vector<int> gmeta;  // per 8-feature group: var | zstart << 4 | nvalid << 24
+    std::vector<int> ogrp;   // per 8-row output group: var | z0 << 8 | nrow << 24 (var 255: padding)
     size_t consts_off = 0;
 };
 
@@ -72,12 +74,15 @@ struct B3InVar {
 
 struct B3Args {
     const void* wstream;  // [nch][CB]: the packed weight chunks of one column tile
-    const float* consts;  // [kp1] mean | [kp1] 1/(sigma+eps) | [nh][HP] bias | [6][kop] | [kop] int var|z<<8
+    const float* consts;  // [kp1] mean | [kp1] 1/(sigma+eps) | [nh][HP] bias | [6][kop]
     int wbytes;
     int nch, n1, nhx, npass, n_otile, kp1, kop, nconst, any_log;
     int64_t ncol, ncol_blk, ntiles;
     B3InVar in[kMaxVars];
     int gmeta[kB3Groups];
+    // output rows in 8-row groups, each of ONE variable (every variable is padded to a
+    // multiple of 8 rows): group G = var | z0 << 8 | nrow << 24 (var 255: padding)
+    int ogrp[kB3OutGroups];
     float* out_ptr[kMaxVars];
     int64_t out_ld[kMaxVars], out_bs[kMaxVars];
     const float* res_ptr[kMaxVars];
@@ -139,7 +144,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     float* s_rs = s_mean + p.kp1;
     float* s_bias = s_rs + p.kp1;             // [nh][HP]
     float* s_oc = s_bias + (1 + p.nhx) * HP;  // [6][kop]: bias, sigma, mean, lo, hi, mask
-    long long* s_row = reinterpret_cast<long long*>(s_oc + 6 * p.kop);  // [4][kop]
     const int kop = p.kop;
 
     const int tid = threadIdx.x;
@@ -150,26 +154,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
     // ---- constants and per-row destinations to LDS ----
     for (int i = tid; i < p.nconst; i += 256) s_mean[i] = p.consts[i];
-    {
-        const int* vz = reinterpret_cast<const int*>(p.consts + p.nconst);
-        for (int R = tid; R < kop; R += 256) {
-            const int e = vz[R];
-            const int v = e & 0xff, z = e >> 8;
-            long long oa = 0, ob = 0, ra = 0, rb = 0;
-            if (v < kMaxVars) {
-                oa = (long long)(p.out_ptr[v] + (int64_t)z * p.out_ld[v]);
-                ob = p.out_bs[v];
-                if (p.res_ptr[v]) {
-                    ra = (long long)(p.res_ptr[v] + (int64_t)z * p.res_ld[v]);
-                    rb = p.res_bs[v];
-                }
-            }
-            s_row[R] = oa;
-            s_row[kop + R] = ob;
-            s_row[2 * kop + R] = ra;
-            s_row[3 * kop + R] = rb;
-        }
-    }
 
     // ---- weight stream: LDS ring of 2 chunks, the chunk after next in registers ----
     const Rsrc3 rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.wstream), 0, p.wbytes, 0x00020000);
@@ -232,17 +216,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     };
 
     // ---- layer-1 inputs: B fragments straight from the [level][column] arrays ----
-    int64_t lblk = 0, lii = 0;  // column address of the tile being loaded
+    unsigned lblk = 0, lii = 0;  // column address of the tile being loaded (block, index in block)
     bool lvalid = false;
     auto set_load_tile = [&](int64_t tile) {
         const int64_t c = tile * kB3Cols + wave * 32 + cl;
         lvalid = c < p.ncol;
-        lii = lvalid ? c : 0;
-        lblk = 0;
-        if (p.ncol_blk < p.ncol) {
-            lblk = lii / p.ncol_blk;
-            lii -= lblk * p.ncol_blk;
-        }
+        const int64_t cc = lvalid ? c : 0;
+        const int64_t b = p.ncol_blk < p.ncol ? cc / p.ncol_blk : 0;
+        lblk = (unsigned)b;
+        lii = (unsigned)(cc - b * p.ncol_blk);
     };
     auto load_in = [&](float (&raw)[16], int c) {  // chunk c: groups 4c + 2s + hh, 8 levels each
         sfor<2>([&](auto sc) {
@@ -254,7 +236,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             const int64_t ld = hh ? p.in[v1].ld : p.in[v0].ld;
             const int64_t bs = hh ? p.in[v1].bs : p.in[v0].bs;
             const int nv = lvalid ? ((hh ? m1 : m0) >> 24) : 0;
-            const float* ptr = (hh ? b1 : b0) + lblk * bs + lii;
+            const float* ptr = (hh ? b1 : b0) + (int64_t)lblk * bs + lii;
 #pragma unroll
             for (int j = 0; j < 8; ++j)  // read once: keep them from evicting the weight stream in L2
 #ifdef FV3_B3_EXP_NOINPUT
@@ -292,6 +274,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // ---- activations: B fragments of the next layer (unit 32t + 16s + 8(j>>2) + (j&3) + 4hh) ----
     bf16x8 Bh[HT][2], Bl[HT][2];
     auto hidden_epi = [&](int l) {  // relu(acc + bias_l) -> Bh/Bl
+#ifdef FV3_B3_EXP_NOHIDEPI  // experiment: plain cast, no bias/relu/lo split, results invalid
+        sfor<HT>([&](auto tc) {
+            constexpr int t = decltype(tc)::value;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                Bh[t][0][j] = (__bf16)acc[t][j];
+                Bh[t][1][j] = (__bf16)acc[t][8 + j];
+                Bl[t][0][j] = Bh[t][0][j];
+                Bl[t][1][j] = Bh[t][1][j];
+            }
+        });
+        return;
+#endif
         sfor<HT>([&](auto tc) {
             constexpr int t = decltype(tc)::value;
             sfor<2>([&](auto sc) {
@@ -311,42 +306,87 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             });
         });
     };
-    int64_t oblk = 0, oii = 0;
+    // ---- output epilogue ----------------------------------------------------------
+    // Output tile T's accumulator register 4g + rr of lane (hh, cl) is row 32T + 8g + 4hh + rr
+    // of column cl: each 8-row group g belongs to ONE output variable (ogrp), so its
+    // destination is one buffer resource plus a 32-bit element offset per lane
+    // (the host checks every span < 2^29 elements); lanes that must not store (padding
+    // rows, columns past the end) get an offset past the range, so no branch per row.
+    // Residual inputs (Difference.backward: after = before + to) are read one tile ahead
+    // of their use, so the loads of tile t+1 travel while tile t is finished and stored.
+    unsigned oblk = 0, oii = 0;
     bool ovalid = false;
+    float resv[2][16];  // residual values of the tile being finished / the next one
+    auto res_load = [&](int T, float (&r)[16]) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int e = p.ogrp[4 * T + g];
+            const int v = e & 0xff, z0 = (e >> 8) & 0xffff, nrow = e >> 24;
+            if (v < kMaxVars && p.res_ptr[v]) {  // uniform
+                const Rsrc3 rr_ = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.res_ptr[v]), 0, 0x7ffffffc,
+                                                                    0x00020000);
+                const unsigned rb = oblk * (unsigned)p.res_bs[v] + oii;
+                const unsigned rld = (unsigned)p.res_ld[v];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int row = 4 * hh + q;
+                    const unsigned off = (ovalid && row < nrow) ? (rb + (unsigned)(z0 + row) * rld) * 4u : 0x80000000u;
+                    r[4 * g + q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr_, (int)off, 0, 0));
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) r[4 * g + q] = 0.0f;
+            }
+        }
+    };
+    auto out_tile = [&](const b3f16& a, int T, const float (&r)[16]) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int e = p.ogrp[4 * T + g];
+            const int v = e & 0xff, z0 = (e >> 8) & 0xffff, nrow = e >> 24;
+            if (v >= kMaxVars) continue;  // padding group (uniform)
+            int R0 = 32 * T + 8 * g + 4 * hh;
+            asm volatile("" : "+v"(R0));  // keep the constant reads next to their use
+            const b3f4 bo = *reinterpret_cast<const b3f4*>(s_oc + R0);
+            const b3f4 sg = *reinterpret_cast<const b3f4*>(s_oc + kop + R0);
+            const b3f4 mu = *reinterpret_cast<const b3f4*>(s_oc + 2 * kop + R0);
+            const b3f4 lo = *reinterpret_cast<const b3f4*>(s_oc + 3 * kop + R0);
+            const b3f4 hi = *reinterpret_cast<const b3f4*>(s_oc + 4 * kop + R0);
+            const b3f4 mk = *reinterpret_cast<const b3f4*>(s_oc + 5 * kop + R0);
+            const Rsrc3 ro = __builtin_amdgcn_make_buffer_rsrc(p.out_ptr[v], 0, 0x7ffffffc, 0x00020000);
+            const unsigned ob = oblk * (unsigned)p.out_bs[v] + oii;
+            const unsigned old_ = (unsigned)p.out_ld[v];
+            const bool has_res = p.res_ptr[v] != nullptr;  // uniform
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = 4 * hh + q;
+                float y = a[4 * g + q] + bo[q];
+                y = y * sg[q];
+                y = y + mu[q];
+                if (y < lo[q]) y = lo[q];
+                if (y >= hi[q]) y = hi[q];
+                y = y * mk[q];
+                if (has_res) y = r[4 * g + q] + y;
+                const unsigned off = (ovalid && row < nrow) ? (ob + (unsigned)(z0 + row) * old_) * 4u : 0x80000000u;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, (int)off, 0, 0);
+            }
+        }
+    };
     auto out_epi = [&](int pp, int nact) {
+#ifdef FV3_B3_EXP_NOOUTEPI  // experiment: no output epilogue (one store per tile), results invalid
+        float sink = 0.0f;
+        sfor<HT>([&](auto tc) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sink += acc[decltype(tc)::value][r];
+        });
+        if (sink == 1234.5f) p.out_ptr[0][0] = sink;
+        return;
+#endif
         sfor<HT>([&](auto tc) {
             constexpr int t = decltype(tc)::value;
             if (t < nact) {
-                const int T = pp * HT + t;
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    int R0 = 32 * T + 8 * g + 4 * hh;
-                    asm volatile("" : "+v"(R0));  // keep the constant reads next to their use
-                    const b3f4 bo = *reinterpret_cast<const b3f4*>(s_oc + R0);
-                    const b3f4 sg = *reinterpret_cast<const b3f4*>(s_oc + kop + R0);
-                    const b3f4 mu = *reinterpret_cast<const b3f4*>(s_oc + 2 * kop + R0);
-                    const b3f4 lo = *reinterpret_cast<const b3f4*>(s_oc + 3 * kop + R0);
-                    const b3f4 hi = *reinterpret_cast<const b3f4*>(s_oc + 4 * kop + R0);
-                    const b3f4 mk = *reinterpret_cast<const b3f4*>(s_oc + 5 * kop + R0);
-#pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) {
-                        const int R = R0 + rr;
-                        float y = acc[t][4 * g + rr] + bo[rr];
-                        y = y * sg[rr];
-                        y = y + mu[rr];
-                        if (y < lo[rr]) y = lo[rr];
-                        if (y >= hi[rr]) y = hi[rr];
-                        y = y * mk[rr];
-                        const long long oa = s_row[R];
-                        if (ovalid && oa) {
-                            const long long ra = s_row[2 * kop + R];
-                            if (ra)
-                                y = __builtin_nontemporal_load(reinterpret_cast<const float*>(ra) + oblk * s_row[3 * kop + R] +
-                                                               oii) + y;
-                            __builtin_nontemporal_store(y, reinterpret_cast<float*>(oa) + oblk * s_row[kop + R] + oii);
-                        }
-                    }
-                }
+                if (t + 1 < nact) res_load(pp * HT + t + 1, resv[(t + 1) & 1]);
+                out_tile(acc[t], pp * HT + t, resv[t & 1]);
             }
         });
     };
@@ -397,6 +437,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int pp = 0; pp < p.npass; ++pp) {
             zero_acc();
             const int nact = min(HT, p.n_otile - pp * HT);
+            res_load(pp * HT, resv[0]);  // lands while the pass runs its MFMAs
             sfor<HT>([&](auto cc) {
                 constexpr int c = decltype(cc)::value;
                 step(Bh[c], Bl[c], nact);
@@ -460,7 +501,34 @@ int b3_pack(fv3_dense_model* m, const fv3_dense_desc* d)
     b->kp1 = (int)fsrc.size();
     b->n1 = b->kp1 / 32;
     b->nhx = d->n_hidden - 1;
-    b->n_otile = (m->k_out + 31) / 32;
+    // output rows: each variable padded to a multiple of 8 rows (one variable per 8-row
+    // accumulator group, see the kernel's epilogue); row R -> (variable, level) or -1
+    std::vector<int> ocol_var, ocol_z, okeep;  // okeep: row's index in the model's k_out order
+    for (int v = 0, o = 0; v < m->n_out; ++v) {
+        const int nz = m->out_nz[v];
+        for (int z0 = 0; z0 < nz; z0 += 8) {
+            const int nrow = std::min(8, nz - z0);
+            b->ogrp.push_back(v | (z0 << 8) | (nrow << 24));
+            for (int j = 0; j < 8; ++j) {
+                ocol_var.push_back(j < nrow ? v : -1);
+                ocol_z.push_back(j < nrow ? z0 + j : 0);
+                okeep.push_back(j < nrow ? o + z0 + j : -1);
+            }
+        }
+        FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, nz < (1 << 16), "dense_create: output levels too many for bf16x3");
+        o += nz;
+    }
+    while (b->ogrp.size() % 4) {
+        b->ogrp.push_back(255);
+        for (int j = 0; j < 8; ++j) {
+            ocol_var.push_back(-1);
+            ocol_z.push_back(0);
+            okeep.push_back(-1);
+        }
+    }
+    FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, (int)b->ogrp.size() <= kB3OutGroups,
+                     "dense_create: %d padded output rows are too many for bf16x3", (int)ocol_var.size());
+    b->n_otile = (int)b->ogrp.size() / 4;
     b->kop = 32 * b->n_otile;
     b->npass = (b->n_otile + HT - 1) / HT;
     const int per_layer = HP / 32;
@@ -503,12 +571,6 @@ int b3_pack(fv3_dense_model* m, const fv3_dense_desc* d)
                                 (in < W && unit < W) ? K[(size_t)in * W + unit] : 0.0f);
                         }
     }
-    std::vector<int> ocol_var(m->k_out), ocol_z(m->k_out);
-    for (int v = 0, o = 0; v < m->n_out; ++v)
-        for (int z = 0; z < m->out_nz[v]; ++z, ++o) {
-            ocol_var[o] = v;
-            ocol_z[o] = z;
-        }
     for (int pp = 0; pp < b->npass; ++pp)
         for (int c = 0; c < per_layer; ++c)
             for (int s = 0; s < 2; ++s)
@@ -518,17 +580,17 @@ int b3_pack(fv3_dense_model* m, const fv3_dense_desc* d)
                             const int in = in_unit(c, s, lane, j);
                             const int R = 32 * (pp * HT + t) + (lane & 31);
                             float v = 0.0f;
-                            if (in < W && R < m->k_out) {
+                            if (in < W && R < b->kop && ocol_var[R] >= 0) {
                                 const int ov = ocol_var[R], oz = ocol_z[R];
                                 v = d->out_kernel[ov][(size_t)in * m->out_nz[ov] + oz];
                             }
                             put(b->n1 + b->nhx * per_layer + pp * per_layer + c, s, t, lane, j, v);
                         }
 
-    // constants: [kp1] mean | [kp1] 1/(sigma+eps) | [nh][HP] bias | [6][kop] | [kop] int var|z<<8
+    // constants: [kp1] mean | [kp1] 1/(sigma+eps) | [nh][HP] bias | [6][kop]
     const int nh = 1 + b->nhx, kop = b->kop;
     b->nconst = 2 * b->kp1 + nh * HP + 6 * kop;
-    std::vector<float> cst((size_t)b->nconst + kop, 0.0f);
+    std::vector<float> cst((size_t)b->nconst, 0.0f);
     for (int f = 0; f < b->kp1; ++f) {
         const int src = fsrc[f];
         if (src < 0) continue;
@@ -539,22 +601,18 @@ int b3_pack(fv3_dense_model* m, const fv3_dense_desc* d)
     for (int l = 0; l < nh; ++l)
         for (int u = 0; u < W; ++u) cst[2 * b->kp1 + l * HP + u] = d->hidden_bias[l][u];
     float* oc = cst.data() + 2 * b->kp1 + nh * HP;
-    int* vz = reinterpret_cast<int*>(cst.data() + b->nconst);
     for (int R = 0; R < kop; ++R) {
         float v[6] = {0.0f, 1.0f, 0.0f, -INFINITY, INFINITY, 1.0f};
-        int e = 255;
-        if (R < m->k_out) {
-            const int ov = ocol_var[R], oz = ocol_z[R];
+        if (ocol_var[R] >= 0) {
+            const int ov = ocol_var[R], oz = ocol_z[R], K = okeep[R];
             v[0] = d->out_bias[ov][oz];
-            v[1] = d->out_sigma[R];
-            v[2] = d->out_mean[R];
-            if (d->out_min) v[3] = d->out_min[R];
-            if (d->out_max) v[4] = d->out_max[R];
-            if (d->out_mask) v[5] = d->out_mask[R];
-            e = ov | (oz << 8);
+            v[1] = d->out_sigma[K];
+            v[2] = d->out_mean[K];
+            if (d->out_min) v[3] = d->out_min[K];
+            if (d->out_max) v[4] = d->out_max[K];
+            if (d->out_mask) v[5] = d->out_mask[K];
         }
         for (int k = 0; k < 6; ++k) oc[(size_t)k * kop + R] = v[k];
-        vz[R] = e;
     }
 
     b->wbytes = (int)(ws.size() * 2);
@@ -584,7 +642,9 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
     if (precision == FV3_DENSE_F32) return fv3_dense_forward(m, inputs, in_l, outputs, out_l, ncol, stream);
     clear_error();
     FV3_REQUIRE(precision == FV3_DENSE_BF16X3, "dense_forward_ex: unknown precision %d", precision);
-    FV3_REQUIRE(m && m->b3, "dense_forward_ex: NULL model");
+    FV3_REQUIRE(m, "dense_forward_ex: NULL model");
+    FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, m->b3, "dense_forward_ex: this model has no bf16x3 pack "
+                     "(too many input features or output rows); use FV3_DENSE_F32");
     FV3_REQUIRE(ncol >= 0, "dense_forward_ex: ncol < 0");
     if (ncol == 0) return FV3_OK;
     FV3_REQUIRE(inputs && in_l && outputs && out_l, "dense_forward_ex: NULL argument");
@@ -625,11 +685,27 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
     a.ncol_blk = nb;
     a.ntiles = (ncol + kB3Cols - 1) / kB3Cols;
     for (size_t g = 0; g < b.gmeta.size(); ++g) a.gmeta[g] = b.gmeta[g];
+    for (size_t g = 0; g < b.ogrp.size(); ++g) a.ogrp[g] = b.ogrp[g];
+    // the epilogue addresses outputs / residual inputs with 32-bit byte offsets
+    // ((block * bs + index + z * ld) * 4 < 2^31) and 32-bit block / index values
+    FV3_REQUIRE(ncol < (int64_t)1 << 31, "dense_forward_ex: too many columns for bf16x3");
+    auto span = [&](const fv3_layout& l, int nz) {
+        const int64_t nblk = (ncol + l.ncol_blk - 1) / l.ncol_blk;
+        return (nblk - 1) * l.blk_stride + (int64_t)(nz - 1) * l.ld + l.ncol_blk;
+    };
+    for (int v = 0; v < m->n_out; ++v) {
+        FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, span(out_l[v], m->out_nz[v]) < ((int64_t)1 << 29),
+                         "dense_forward_ex: output %d spans too many elements for bf16x3", v);
+        const int r = m->out_residual[v];
+        if (r >= 0)
+            FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, span(in_l[r], m->in_nz[r]) < ((int64_t)1 << 29),
+                             "dense_forward_ex: residual input %d spans too many elements for bf16x3", r);
+    }
 
     const void* kfn = b.ht == 2 ? (const void*)dense_b3_kernel<2>
                       : b.ht == 4 ? (const void*)dense_b3_kernel<4>
                                   : (const void*)dense_b3_kernel<8>;
-    const size_t lds = (size_t)2 * 4096 * b.ht + (size_t)4 * b.nconst + (size_t)8 * 4 * b.kop;
+    const size_t lds = (size_t)2 * 4096 * b.ht + (size_t)4 * b.nconst;
     FV3_REQUIRE(lds <= 160 * 1024, "dense_forward_ex: model needs %zu bytes of LDS", lds);
     static std::mutex mu;
     static int n_cu = 0;
