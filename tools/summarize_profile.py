@@ -6,8 +6,6 @@
 Writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --stats summary (copied verbatim)
   profiles/<tag>_summary.md         per (kernel, grid) mean duration + PMC traffic
-  profiles/pmc_traffic.json         HBM bytes per launch of the bench's dominant kernel
-                                    (read by bench.py for roofline.traffic)
 
 HBM bytes per dispatch = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes), applying the
 gfx950 correction of MI355X_MICROARCH.md §HBM (FETCH_SIZE counts half of the bytes
@@ -105,14 +103,10 @@ def main():
     for k, v in summary.items():
         if k.startswith("dense_forward_kernel") and any(k.endswith(f"@{g}") for g in c48_grids):
             dom = v
-    traffic = {}
-    tpath = os.path.join(prof, "pmc_traffic.json")
-    if dom and dom["hbm_bytes_per_launch"] is not None:
-        traffic["dense_c48"] = {"hbm_bytes_per_launch": dom["hbm_bytes_per_launch"],
-                                               "fetch_kib": dom["fetch_kib"], "write_kib": dom["write_kib"],
-                                               "workload": "C48 bench step", "profile": tag}
-    with open(tpath, "w") as fh:
-        json.dump(traffic, fh, indent=1)
+    # profiles/pmc_traffic.json (read by bench.py) is written by tools/pmc_publish.py from the
+    # calibrated per-leg PMC passes (tools/pmc_all.sh); this summary only reports the trace's
+    # own FETCH/WRITE passes beside the durations, and never overwrites that file.
+    del dom
     print("\n".join(lines))
 
 
