@@ -31,6 +31,10 @@ EXPORTED_SYMBOLS = (
     "fv3_dense_set_trace",
     "fv3_regrid_coarsen",
     "fv3_regrid_coarsen_f64",
+    "fv3_regrid_coarsen_f64d",
+    "fv3_weighted_block_average",
+    "fv3_weighted_block_average_f64",
+    "fv3_hydrostatic_balance",
     "fv3_regrid_coarsen_edge",
     "fv3_regrid_coarsen_edge_f64",
     "fv3_interpolate_2d",
@@ -43,6 +47,8 @@ EXPORTED_SYMBOLS = (
     "fv3_level_sums_f64",
     "fv3_level_sums_u8",
     "fv3_ml_epilogue",
+    "fv3_ml_epilogue_ex",
+    "fv3_tendency_columns",
     "fv3_standard_normalize",
     "fv3_standard_denormalize",
 )
@@ -51,6 +57,12 @@ ABI_VERSION = 3
 # fv3_dense_forward_ex precisions
 DENSE_F32 = 0
 DENSE_BF16X3 = 1
+
+# fv3_ml_epilogue_ex flags, fv3_tendency_columns modes
+EPI_HAS_DQ1 = 1
+EPI_HAS_DQ2 = 2
+TEND_WIND = 0
+TEND_MASS = 1
 
 
 class NativeLibraryError(RuntimeError):
@@ -134,6 +146,12 @@ _SIGNATURES = {
                                 _I, _I, _I, _I, _D, _P]),
     "fv3_regrid_coarsen_f64": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _P, _I, _I, _I,
                                     _I, _I, _I, _I, _D, _P]),
+    "fv3_regrid_coarsen_f64d": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _P, _I, _I, _I,
+                                     _I, _I, _I, _I, _D, _P]),
+    "fv3_weighted_block_average": (_I, [ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _P, _I, _I, _I, _I, _I, _P]),
+    "fv3_weighted_block_average_f64": (_I, [ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _P, _I, _I, _I, _I, _I,
+                                            _P]),
+    "fv3_hydrostatic_balance": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _D, _P]),
     "fv3_regrid_coarsen_edge": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _I, _I, _I, _I,
                                      _I, _I, _I, _I, _D, _P]),
     "fv3_regrid_coarsen_edge_f64": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _I, _I, _I, _I,
@@ -150,6 +168,8 @@ _SIGNATURES = {
     "fv3_standard_normalize": (_I, [_P, _I, Layout, _P, _P, _I, _P, Layout, _I64, _I, _P]),
     "fv3_standard_denormalize": (_I, [_P, Layout, _P, _P, _I, _P, Layout, _I64, _I, _P]),
     "fv3_ml_epilogue": (_I, [ctypes.POINTER(EpilogueIO), Layout, _I64, _I, _I, _D, _I, _I, _P]),
+    "fv3_ml_epilogue_ex": (_I, [ctypes.POINTER(EpilogueIO), Layout, _I64, _I, _I, _D, _I, _I, _I, _P]),
+    "fv3_tendency_columns": (_I, [_P, _P, _P, _P, _P, _P, Layout, _I64, _I, _I, _I, _D, _P]),
 }
 
 

@@ -22,9 +22,12 @@ TOA_PRESSURE = 300.0  # external/vcm/vcm/calc/thermo/constants.py:17
 
 
 def coarsen_on_pressure(delp, area, fields: Mapping[str, object], factor: int, iv: int = 1, kord: int = 1,
-                        ptop: float = TOA_PRESSURE, stream=None):
+                        ptop: float = TOA_PRESSURE, stream=None, coarse_delp_f64: bool = False):
     """delp and fields (tile, z, y, x), area (tile, y, x) -> dict of coarse fields
-    (tile, z, y/f, x/f) and the area-weighted coarse delp.  Device tensors in and out."""
+    (tile, z, y/f, x/f) and the area-weighted coarse delp (float32, or float64 when
+    ``coarse_delp_f64`` and delp is float64: the restart-precision
+    weighted_block_average(delp, area) of coarsen_restarts.py:480-486).  Device tensors
+    in and out."""
     _device.require_gpu()
     delp64 = (isinstance(delp, np.ndarray) and delp.dtype == np.float64) or (
         torch is not None and isinstance(delp, torch.Tensor) and delp.dtype == torch.float64)
@@ -50,11 +53,12 @@ def coarsen_on_pressure(delp, area, fields: Mapping[str, object], factor: int, i
         raise ValueError(f"grid {ny}x{nx} is not divisible by the coarsening factor {factor}")
     cshape = (nt, km, ny // factor, nx // factor)
     outs = [torch.empty(cshape, dtype=torch.float32, device=delp.device) for _ in names]
-    delp_c = torch.empty(cshape, dtype=torch.float32, device=delp.device)
+    want64 = delp64 and coarse_delp_f64
+    delp_c = torch.empty(cshape, dtype=torch.float64 if want64 else torch.float32, device=delp.device)
     fptr = (ctypes.c_void_p * max(1, len(tens)))(*[t.data_ptr() for t in tens])
     optr = (ctypes.c_void_p * max(1, len(outs)))(*[t.data_ptr() for t in outs])
     lib = _native.load()
-    fn = lib.fv3_regrid_coarsen_f64 if delp64 else lib.fv3_regrid_coarsen
+    fn = lib.fv3_regrid_coarsen_f64d if want64 else (lib.fv3_regrid_coarsen_f64 if delp64 else lib.fv3_regrid_coarsen)
     st = fn(delp.data_ptr(), area.data_ptr(), fptr, optr, len(tens), delp_c.data_ptr(), nt, km, ny, nx,
             int(factor), int(iv), int(kord), float(ptop), _device.stream_handle(stream))
     _native.check(st, "regrid_coarsen")

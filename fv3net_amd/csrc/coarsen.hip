@@ -37,6 +37,7 @@
 #define FV3_HD __host__ __device__
 #include <cstdlib>
 
+#include "blocks.h"
 #include "common.h"
 #include "mappm_core.h"
 
@@ -53,36 +54,13 @@ struct CoarsenArgs {
     const float* fields[kMaxFields];
     float* out[kMaxFields];
     float* delp_out;
+    double* delp_out64;  // the coarse delp in float64 (restart precision), or NULL
     int n_fields, ntile, km, ny, nx, f, iv, kord;
     double ptop;
     float* scratch;   // [km][gridDim * blockDim]: each lane's remapped column (input-driven path), or NULL
 };
 
 constexpr int kChunk = 16;  // delp*area levels staged per pass-1 round
-
-template <typename T>
-__device__ __forceinline__ T nan0(T x) { return x != x ? T(0) : x; }  // nansum: NaN terms count as 0
-
-// numpy's np.sum over the two f axes of a C-order (.., Y, f, X, f) block: val(j) is
-// element j = dy*f + dx.  A reduced contiguous row goes through pairwise_sum
-// (n < 8: sequential; n == 8: eight partials combined as a fixed tree) and is added
-// to the running sum.
-template <typename T, typename V>
-__device__ __forceinline__ T block_sum(int f, V val)
-{
-    auto row = [&](int r) -> T {
-        const int b = r * f;
-        if (f == 8)
-            return ((val(b) + val(b + 1)) + (val(b + 2) + val(b + 3))) +
-                   ((val(b + 4) + val(b + 5)) + (val(b + 6) + val(b + 7)));
-        T s = val(b);
-        for (int c = 1; c < f; ++c) s = s + val(b + c);
-        return s;
-    };
-    T acc = row(0);
-    for (int r = 1; r < f; ++r) acc = acc + row(r);
-    return acc;
-}
 
 // the same row sum across the f lanes of this lane's cell (every lane of the cell
 // gets the identical value): f == 8 pairwise == xor tree over aligned 8-lane groups
@@ -196,6 +174,7 @@ __global__ __launch_bounds__(512) void regrid_coarsen_kernel(CoarsenArgs<DT> a)
                 const DT dc = acc / (DT)asum[c];  // weighted_block_average (coarsen.py:213-215)
                 pc[c * (km + 1) + k0 + kk + 1] = dc;
                 if (a.delp_out) a.delp_out[((int64_t)tile * km + k0 + kk) * cplane + crow + c] = (float)dc;
+                if (a.delp_out64) a.delp_out64[((int64_t)tile * km + k0 + kk) * cplane + crow + c] = (double)dc;
             }
         }
         __syncthreads();
@@ -478,8 +457,8 @@ __global__ __launch_bounds__(64) void regrid_coarsen_edge_kernel(EdgeArgs<DT> a)
 
 template <typename DT>
 int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* fields, float* const* out,
-                        int n_fields, float* delp_out, int ntile, int km, int ny, int nx, int factor, int iv,
-                        int kord, double ptop_toa, void* stream)
+                        int n_fields, float* delp_out, double* delp_out64, int ntile, int km, int ny, int nx,
+                        int factor, int iv, int kord, double ptop_toa, void* stream)
 {
     using namespace fv3;
     clear_error();
@@ -506,6 +485,7 @@ int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* f
     a.delp = delp;
     a.area = area;
     a.delp_out = delp_out;
+    a.delp_out64 = delp_out64;
     a.n_fields = n_fields;
     a.ntile = ntile;
     a.km = km;
@@ -626,14 +606,22 @@ extern "C" int fv3_regrid_coarsen(const float* delp, const float* area, const fl
                                   float* const* out, int n_fields, float* delp_out, int ntile, int km, int ny,
                                   int nx, int factor, int iv, int kord, double ptop_toa, void* stream)
 {
-    return fv3::regrid_coarsen_impl<float>(delp, area, fields, out, n_fields, delp_out, ntile, km, ny, nx, factor,
-                                           iv, kord, ptop_toa, stream);
+    return fv3::regrid_coarsen_impl<float>(delp, area, fields, out, n_fields, delp_out, nullptr, ntile, km, ny, nx,
+                                           factor, iv, kord, ptop_toa, stream);
 }
 
 extern "C" int fv3_regrid_coarsen_f64(const double* delp, const float* area, const float* const* fields,
                                       float* const* out, int n_fields, float* delp_out, int ntile, int km, int ny,
                                       int nx, int factor, int iv, int kord, double ptop_toa, void* stream)
 {
-    return fv3::regrid_coarsen_impl<double>(delp, area, fields, out, n_fields, delp_out, ntile, km, ny, nx,
+    return fv3::regrid_coarsen_impl<double>(delp, area, fields, out, n_fields, delp_out, nullptr, ntile, km, ny, nx,
+                                            factor, iv, kord, ptop_toa, stream);
+}
+
+extern "C" int fv3_regrid_coarsen_f64d(const double* delp, const float* area, const float* const* fields,
+                                       float* const* out, int n_fields, double* delp_out, int ntile, int km, int ny,
+                                       int nx, int factor, int iv, int kord, double ptop_toa, void* stream)
+{
+    return fv3::regrid_coarsen_impl<double>(delp, area, fields, out, n_fields, nullptr, delp_out, ntile, km, ny, nx,
                                             factor, iv, kord, ptop_toa, stream);
 }

@@ -46,6 +46,7 @@ struct EpilogueArgs {
     fv3_layout lay;        // every [z][col] array
     int64_t ncol, col_ld;  // column diagnostics: row stride
     int nz, mse, hydrostatic;
+    int has_dq1, has_dq2;  // the prediction holds dQ1 / dQ2 (else the inputs are zeros, machine_learning.py:258-259)
     double dt;
 };
 
@@ -109,19 +110,21 @@ __global__ __launch_bounds__(64) void ml_epilogue_kernel(EpilogueArgs<DT> a)
         // mass_integrate terms: (x * delp) / g, NaN-skipping sum from +0.0
         s_h = s_h + nan0((q1n - (DT)q1) * dp / g);
         s_m = s_m + nan0((q2n - (DT)q2) * dp / g);
-        s_nm = s_nm + nan0(q2n * dp / g);
-        s_ch = s_ch + nan0(q1n * dp / g);
+        // compute_diagnostics reads the tendency dict: zeros for a tendency the model lacks
+        if (a.has_dq2) s_nm = s_nm + nan0(q2n * dp / g);
+        if (a.has_dq1) s_ch = s_ch + nan0(q1n * dp / g);
         if (a.dq1_out) {
             a.dq1_out[i] = q1n;
             a.dq2_out[i] = q2n;
         }
         if (a.active) a.active[i] = ((DT)q2 != q2n) ? 1 : 0;
         // fillna_tendency + add_tendency
+        // (only the tendencies the model predicts are applied, loop.py:202-219)
         const bool nan1 = q1n != q1n, nan2 = q2n != q2n;
         n1 += nan1;
         n2 += nan2;
-        if (want_t) a.temp_out[i] = t + (nan1 ? (DT)0 : q1n) * dtd;
-        if (a.sphum_out) a.sphum_out[i] = sp + (nan2 ? (DT)0 : q2n) * dtd;
+        if (want_t) a.temp_out[i] = a.has_dq1 ? t + (nan1 ? (DT)0 : q1n) * dtd : t;
+        if (a.sphum_out) a.sphum_out[i] = a.has_dq2 ? sp + (nan2 ? (DT)0 : q2n) * dtd : sp;
     };
     fetch(0, 0);
     for (int k0 = 0; k0 < a.nz; k0 += 2 * U) {
@@ -154,7 +157,7 @@ __global__ __launch_bounds__(64) void ml_epilogue_kernel(EpilogueArgs<DT> a)
 
 template <typename DT>
 int epilogue_impl(const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, int nz, double dt, int mse_conserving,
-                  int hydrostatic, void* stream)
+                  int hydrostatic, int flags, void* stream)
 {
     clear_error();
     FV3_REQUIRE(io, "ml_epilogue: NULL io");
@@ -183,10 +186,86 @@ int epilogue_impl(const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, int n
     a.nz = nz;
     a.mse = mse_conserving != 0;
     a.hydrostatic = hydrostatic != 0;
+    a.has_dq1 = (flags & FV3_EPI_HAS_DQ1) != 0;
+    a.has_dq2 = (flags & FV3_EPI_HAS_DQ2) != 0;
     a.dt = dt;
     const int block = 64;  // one wave: C96's 864 waves spread over every CU (256-thread blocks left 40 idle)
     const int64_t grid = (ncol + block - 1) / block;
     hipLaunchKernelGGL(ml_epilogue_kernel<DT>, dim3((unsigned)grid), dim3(block), 0, (hipStream_t)stream, a);
+    FV3_LAUNCH_CHECK();
+    return FV3_OK;
+}
+
+// The prediction's other tendencies (runtime/names.py:31-50), one pass per column:
+//   TEND_WIND (dQu, dQv): compute_ml_momentum_diagnostics (diagnostics/compute.py:140-161)
+//       column_integrated_dQ{u,v}_stress = mass_integrate(dQ, delp) = sum (dQ delp) / g
+//       (float32 * state dtype -> DT), fillna + filled fraction (loop.py:103-123), and the
+//       filled tendency cast to float64 as prepare_agrid_wind_tendencies does
+//       (loop.py:126-145; the A->D-grid transform after it belongs to the fv3gfs wrapper)
+//   TEND_MASS (dQp): net_mass_tendency = mass_integrate(ones_like(dQp), dQp)
+//       (compute.py:107-115) = sum (1 * dQp) / g in float32 (all-float32 operands),
+//       fillna + filled fraction, add_tendency delp + fill(dQp) dt (loop.py:202-219)
+// Column sums over z in order from +0.0 skipping NaN; HBM-bound.
+template <typename DT>
+struct TendArgs {
+    const float* t;
+    const DT* delp;   // TEND_WIND: the integral's weights; TEND_MASS: the state updated
+    double* filled;   // TEND_WIND: [z][col] float64 filled tendency, or NULL
+    DT* state_out;    // TEND_MASS: [z][col] delp + fill(dQp) dt, or NULL (may alias delp)
+    void* integral;   // [col]: DT (TEND_WIND) or float (TEND_MASS), or NULL
+    DT* frac;         // [col] filled fraction, or NULL
+    fv3_layout lay;
+    int64_t ncol;
+    int nz, mode;
+    double dt;
+};
+
+template <typename DT>
+__global__ __launch_bounds__(64) void tendency_columns_kernel(TendArgs<DT> a)
+{
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.ncol) return;
+    const int64_t off = col_offset(a.lay, c);
+    const DT g = (DT)kGravity;
+    const float gf = (float)kGravity, dtf = (float)a.dt;
+    DT sd = 0;
+    float sf = 0.0f;
+    int n = 0;
+    for (int k = 0; k < a.nz; ++k) {
+        const int64_t i = off + (int64_t)k * a.lay.ld;
+        const float t = a.t[i];
+        const DT dp = a.delp[i];
+        const bool isnan_ = t != t;
+        n += isnan_;
+        const float tf = isnan_ ? 0.0f : t;
+        if (a.mode == FV3_TEND_WIND) {
+            sd = sd + nan0((DT)t * dp / g);
+            if (a.filled) a.filled[i] = (double)tf;
+        } else {
+            sf = sf + nan0(1.0f * t / gf);
+            if (a.state_out) a.state_out[i] = dp + (DT)(tf * dtf);
+        }
+    }
+    if (a.integral) {
+        if (a.mode == FV3_TEND_WIND) static_cast<DT*>(a.integral)[c] = sd;
+        else static_cast<float*>(a.integral)[c] = sf;
+    }
+    if (a.frac) a.frac[c] = (DT)((double)n / a.nz);
+}
+
+template <typename DT>
+int tendency_impl(const float* t, const void* delp, double* filled, void* state_out, void* integral, void* frac,
+                  fv3_layout lay, int64_t ncol, int nz, int mode, double dt, void* stream)
+{
+    clear_error();
+    FV3_REQUIRE(ncol >= 0 && nz >= 1, "tendency_columns: bad sizes ncol=%lld nz=%d", (long long)ncol, nz);
+    FV3_REQUIRE(mode == FV3_TEND_WIND || mode == FV3_TEND_MASS, "tendency_columns: unknown mode %d", mode);
+    if (ncol == 0) return FV3_OK;
+    FV3_REQUIRE(t && delp, "tendency_columns: the tendency and delp are required");
+    FV3_REQUIRE(layout_ok(lay, ncol), "tendency_columns: bad layout");
+    TendArgs<DT> a{t, (const DT*)delp, filled, (DT*)state_out, integral, (DT*)frac, lay, ncol, nz, mode, dt};
+    const int64_t grid = (ncol + 63) / 64;
+    hipLaunchKernelGGL(tendency_columns_kernel<DT>, dim3((unsigned)grid), dim3(64), 0, (hipStream_t)stream, a);
     FV3_LAUNCH_CHECK();
     return FV3_OK;
 }
@@ -197,6 +276,23 @@ int epilogue_impl(const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, int n
 extern "C" int fv3_ml_epilogue(const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, int nz, int state_f64,
                                double dt, int mse_conserving, int hydrostatic, void* stream)
 {
-    return state_f64 ? fv3::epilogue_impl<double>(io, lay, ncol, nz, dt, mse_conserving, hydrostatic, stream)
-                     : fv3::epilogue_impl<float>(io, lay, ncol, nz, dt, mse_conserving, hydrostatic, stream);
+    return fv3_ml_epilogue_ex(io, lay, ncol, nz, state_f64, dt, mse_conserving, hydrostatic,
+                              FV3_EPI_HAS_DQ1 | FV3_EPI_HAS_DQ2, stream);
+}
+
+extern "C" int fv3_ml_epilogue_ex(const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, int nz, int state_f64,
+                                  double dt, int mse_conserving, int hydrostatic, int flags, void* stream)
+{
+    return state_f64 ? fv3::epilogue_impl<double>(io, lay, ncol, nz, dt, mse_conserving, hydrostatic, flags, stream)
+                     : fv3::epilogue_impl<float>(io, lay, ncol, nz, dt, mse_conserving, hydrostatic, flags, stream);
+}
+
+extern "C" int fv3_tendency_columns(const float* tendency, const void* delp, double* filled_out, void* state_out,
+                                    void* integral, void* filled_frac, fv3_layout lay, int64_t ncol, int nz,
+                                    int state_f64, int mode, double dt, void* stream)
+{
+    return state_f64 ? fv3::tendency_impl<double>(tendency, delp, filled_out, state_out, integral, filled_frac, lay,
+                                                  ncol, nz, mode, dt, stream)
+                     : fv3::tendency_impl<float>(tendency, delp, filled_out, state_out, integral, filled_frac, lay,
+                                                 ncol, nz, mode, dt, stream);
 }

@@ -17,6 +17,9 @@
  *   fv3_regrid_coarsen    external/vcm/vcm/cubedsphere/regridz.py:25-55 + 115-161 fused with
  *                         external/vcm/vcm/cubedsphere/coarsen.py:183-218
  *                         (as orchestrated by coarsen_restarts.py:411-516, 840-887)
+ *   fv3_weighted_block_average*, fv3_hydrostatic_balance  the plain area-weighted averages
+ *                         and _impose_hydrostatic_balance of coarsen_restarts_on_pressure
+ *                         (external/vcm/vcm/cubedsphere/coarsen_restarts.py:152-225, 916-938)
  *   fv3_regrid_coarsen_edge  external/vcm/vcm/cubedsphere/regridz.py:58-112 + 115-161 fused with
  *                         external/vcm/vcm/cubedsphere/coarsen.py:221-271 (D-grid u/v of
  *                         coarsen_restarts.py:460-509)
@@ -177,6 +180,34 @@ int fv3_regrid_coarsen_f64(const double* delp, const float* area, const float* c
                            int ny, int nx, int factor, int iv, int kord, double ptop_toa,
                            void* stream);
 
+/* Same, with the coarse delp returned in float64 (restart precision, as
+ * weighted_block_average(delp, area) gives it in coarsen_restarts.py:480-486). */
+int fv3_regrid_coarsen_f64d(const double* delp, const float* area, const float* const* fields,
+                            float* const* out, int n_fields, double* delp_out, int ntile, int km,
+                            int ny, int nx, int factor, int iv, int kord, double ptop_toa,
+                            void* stream);
+
+/* ---- the rest of coarsen_restarts_on_pressure (coarsen_restarts.py:152-225) -------
+ * fv3_weighted_block_average[_f64]: sum(obj * w) / sum(w) over factor x factor blocks
+ *   (cubedsphere/coarsen.py:183-218) of n_fields (<= 16) arrays (ntile, nz, ny, nx) with
+ *   weights (ntile, ny, nx) float32 -> (ntile, nz, ny/f, nx/f) in the field's dtype;
+ *   NaN-skipping sums in numpy's order.  Replaces the plain area-weighted averages of
+ *   phis/delp/DZ (coarsen_restarts.py:439, 480-486) and u_srf/v_srf (:890-913).
+ * fv3_hydrostatic_balance: _impose_hydrostatic_balance (coarsen_restarts.py:916-938) on
+ *   the coarse grid: dz_out = hydrostatic_dz(T, sphum, delp) (vertically_dependent.py:
+ *   211-228), phis_out = g * (top height of height_at_interface(dz, phis) + sum dz_out)
+ *   (:69-100, 182-186).  T/sphum float32 (tile, km, ny, nx), delp/dz float64, phis
+ *   (tile, ny, nx) float64.  dz_out may alias dz. */
+int fv3_weighted_block_average(const float* const* fields, float* const* out, int n_fields,
+                               const float* weights, int ntile, int nz, int ny, int nx, int factor,
+                               void* stream);
+int fv3_weighted_block_average_f64(const double* const* fields, double* const* out, int n_fields,
+                                   const float* weights, int ntile, int nz, int ny, int nx,
+                                   int factor, void* stream);
+int fv3_hydrostatic_balance(const float* temperature, const float* sphum, const double* delp,
+                            const double* dz, const double* phis, double* dz_out, double* phis_out,
+                            int ntile, int km, int ny, int nx, double ptop_toa, void* stream);
+
 /* ---- edge-weighted (D-grid wind) pressure-level coarse-graining ------------------
  * edge 0 ("x", u): fields and spacing (dx) on (y outer = ny+1, x center = nx); coarse
  *   output (tile, km, ny/f + 1, nx/f), coarsened along x, every f-th outer row kept.
@@ -275,6 +306,35 @@ typedef struct {
 
 int fv3_ml_epilogue(const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, int nz, int state_f64,
                     double dt, int mse_conserving, int hydrostatic, void* stream);
+
+/* Same, for a prediction that lacks dQ1 or dQ2 (machine_learning.py:258-259 limits
+ * zeros in its place): `flags` holds FV3_EPI_HAS_DQ1 / FV3_EPI_HAS_DQ2 for the tendencies
+ * the model predicts; for a missing one pass zeros as dq1/dq2, and the kernel leaves its
+ * state variable unchanged and its net moistening / column heating at zero, as
+ * compute_diagnostics and add_tendency do (diagnostics/compute.py:84-85, loop.py:202-219).
+ * fv3_ml_epilogue is this with both flags. */
+#define FV3_EPI_HAS_DQ1 1
+#define FV3_EPI_HAS_DQ2 2
+int fv3_ml_epilogue_ex(const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, int nz, int state_f64,
+                       double dt, int mse_conserving, int hydrostatic, int flags, void* stream);
+
+/* The prediction's other tendencies (runtime/names.py:31-50), one pass per column, every
+ * [z][col] array under `lay`; delp / state_out / filled_frac in the state's dtype
+ * (state_f64), the tendency float32 (model output):
+ *   FV3_TEND_WIND (dQu, dQv): integral[col] (state dtype) = sum_z dQ * delp / g, the
+ *     column_integrated_dQ{u,v}_stress of compute_ml_momentum_diagnostics
+ *     (diagnostics/compute.py:140-161); filled_out (float64, or NULL) = fillna(dQ) as
+ *     prepare_agrid_wind_tendencies hands it on (loop.py:126-145).
+ *   FV3_TEND_MASS (dQp): integral[col] (float32) = sum_z 1 * dQp / g, the
+ *     net_mass_tendency_due_to_<label> (compute.py:107-115); state_out = delp +
+ *     fillna(dQp) * dt (add_tendency, loop.py:202-219), may alias delp.
+ * filled_frac[col] = NaN count / nz (loop.py:103-110).  Sums run over z in order, NaN
+ * skipped.  Any output may be NULL. */
+#define FV3_TEND_WIND 0
+#define FV3_TEND_MASS 1
+int fv3_tendency_columns(const float* tendency, const void* delp, double* filled_out, void* state_out,
+                         void* integral, void* filled_frac, fv3_layout lay, int64_t ncol, int nz,
+                         int state_f64, int mode, double dt, void* stream);
 
 /* ---- vertical interpolation to new levels ------------------------------------------
  * Every array is level-major: element (level k, column c) at [k * ld + c].  One thread

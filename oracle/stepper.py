@@ -97,3 +97,73 @@ def epilogue(dq1, dq2, sphum, delp, temperature, physics_precip, dt, mse_conserv
     total = physics_precip + (-out["net_moistening"] * dt * m_per_mm)
     out["total_precipitation"] = np.where(total >= 0, total, 0)
     return out
+
+
+# ---------------------------------------------------------------------------------
+# The whole PureMLStepper step for an arbitrary prediction (machine_learning.py:239-309,
+# runtime/names.py:31-65), its get_diagnostics (diagnostics/compute.py:77-161) and the
+# loop's apply (loop.py:103-145, 202-219, 615-628).  Arrays are [z, column].
+# ---------------------------------------------------------------------------------
+TENDENCY_TO_STATE_NAME = {"dQ1": "air_temperature", "dQ2": "specific_humidity", "dQu": "eastward_wind",
+                          "dQv": "northward_wind", "dQx_wind": "x_wind", "dQy_wind": "y_wind",
+                          "dQp": "pressure_thickness_of_atmospheric_layer"}
+TENDENCY_NAMES = set(TENDENCY_TO_STATE_NAME) | {"dQu", "dQv"}
+TOTAL_PRECIP_RATE = "total_precipitation_rate"
+
+
+def is_state_update_variable(key, state):
+    return (key in state and key not in TENDENCY_NAMES) or key == TOTAL_PRECIP_RATE
+
+
+def pure_ml_step(prediction, state, dt, mse_conserving=True, hydrostatic=False, label="machine_learning"):
+    """-> (tendency, diagnostics, state_updates, stepper_diags, applied) where
+    stepper_diags is get_diagnostics' dict and applied the loop's updated state +
+    filled fractions + the float64 A-grid wind tendencies handed to the wrapper."""
+    dt = float(dt)
+    sphum, delp = state["specific_humidity"], state["pressure_thickness_of_atmospheric_layer"]
+    tendency, updates, diags = {}, {}, {}
+    for k, v in prediction.items():
+        if is_state_update_variable(k, state):
+            updates[k] = v
+        elif k in TENDENCY_NAMES:
+            tendency[k] = v
+        else:
+            diags[k] = v
+    diags.update(updates)
+    zeros = np.zeros_like(sphum)
+    dq1 = tendency.get("dQ1", zeros)
+    dq2 = tendency.get("dQ2", zeros)
+    q1n, q2n = limiter(sphum, dq1, dq2, dt, mse_conserving)
+    if "dQ1" in tendency:
+        diags["column_integrated_dQ1_change_non_neg_sphum_constraint"] = heating(q1n - tendency["dQ1"], delp,
+                                                                                  hydrostatic)
+        tendency["dQ1"] = q1n
+    if "dQ2" in tendency:
+        diags["column_integrated_dQ2_change_non_neg_sphum_constraint"] = mass_integrate(q2n - tendency["dQ2"], delp)
+        tendency["dQ2"] = q2n
+    diags["specific_humidity_limiter_active"] = np.where(dq2 != q2n, 1, 0).astype(np.uint8)
+    # get_diagnostics: compute_diagnostics + compute_ml_momentum_diagnostics
+    zd = np.zeros_like(delp)
+    sd = {f"net_moistening_due_to_{label}": mass_integrate(tendency.get("dQ2", zd), delp),
+          f"column_heating_due_to_{label}": heating(tendency.get("dQ1", zd), delp, hydrostatic)}
+    if "dQp" in tendency:
+        sd[f"net_mass_tendency_due_to_{label}"] = mass_integrate(np.ones_like(tendency["dQp"]), tendency["dQp"])
+    sd["dQ1"] = tendency.get("dQ1", zd)
+    sd["dQ2"] = tendency.get("dQ2", zd)
+    for w in ("dQu", "dQv"):
+        sd[w] = tendency.get(w, zd)
+        sd[f"column_integrated_{w}_stress"] = mass_integrate(sd[w], delp)
+    # apply: fillna, add_tendency (A-grid winds go to the wrapper as float64), precipitation_sum
+    applied, fracs = {}, {}
+    for name, t in tendency.items():
+        filled, fracs[f"{name}_filled_frac"] = fillna(t)
+        if name in ("dQu", "dQv"):
+            applied[name] = filled.astype(np.float64)
+        else:
+            sname = TENDENCY_TO_STATE_NAME[name]
+            applied[sname] = state[sname] + filled * dt
+    if "total_precipitation" in state:
+        net = sd[f"net_moistening_due_to_{label}"]
+        total = state["total_precipitation"] + (-net * dt * (1 / 1000))
+        applied["total_precipitation"] = np.where(total >= 0, total, 0)
+    return tendency, diags, updates, sd, (applied, fracs)

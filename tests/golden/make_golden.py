@@ -11,11 +11,14 @@ container, where /root/reference exists; the GPU box only reads the .npz files).
   values, not the files), for the masked-area-weighted pressure-level variables.
 * coarsen_edge_kat.npz — the same data's coarse D-grid winds u and v (the
   edge-weighted pressure-level path, regridz.py:58-112).
+* restarts_kat.npz — EVERY variable of the same data's fv_core.res, fv_tracer.res and
+  fv_srf_wnd.res categories, for both pressure-level tags (with and without A-grid
+  winds): the whole coarsen_restarts_on_pressure output except sfc_data.
   Inputs are regenerated in the tests exactly as external/synth does
   (np.random.seed(0); uniform(lo, hi, shape) per single-chunk variable,
   synth/core.py:63-67), so only the expected values are stored.
 
-Usage:  python tests/golden/make_golden.py [--edge-kat]
+Usage:  python tests/golden/make_golden.py [--edge-kat | --restarts-kat]
 """
 import json
 import os
@@ -116,9 +119,24 @@ def make_coarsen_edge_kat():
     np.savez_compressed(os.path.join(HERE, "coarsen_edge_kat.npz"), **out)
 
 
+def make_restarts_kat():
+    out = {}
+    for tag in ("pressure-level-without-agrid-winds", "pressure-level-with-agrid-winds"):
+        for cat in ("fv_core.res", "fv_tracer.res", "fv_srf_wnd.res"):
+            with open(os.path.join(REF_JSON, f"{tag}-{cat}.json")) as f:
+                d = json.load(f)
+            for name, var in d["data_vars"].items():
+                out[f"{tag}/{cat}/{name}"] = np.asarray(var["data"], dtype=np.float64)
+                out[f"{tag}/{cat}/{name}/dims"] = np.array(var["dims"])
+    np.savez_compressed(os.path.join(HERE, "restarts_kat.npz"), **out)
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["--edge-kat"]:  # JSON values only; no reference build needed
         make_coarsen_edge_kat()
+        raise SystemExit(0)
+    if sys.argv[1:] == ["--restarts-kat"]:  # JSON values only; no reference build needed
+        make_restarts_kat()
         raise SystemExit(0)
     build()
     if not reference_available():
@@ -126,4 +144,5 @@ if __name__ == "__main__":
     make_mappm_golden()
     make_coarsen_kat()
     make_coarsen_edge_kat()
+    make_restarts_kat()
     print("golden fixtures written to", HERE)
