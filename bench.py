@@ -165,6 +165,123 @@ def cpu_baseline(wl, seconds):
     }
 
 
+def max_over_ranks(x, dist, dev):
+    import torch
+
+    if dist is None:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def scaling_legs(dev, dist, rank, world, settle_ms=150.0):
+    """Strong-scaling legs run at EVERY world size (all ranks): one global problem
+    sharded by row bands of the flattened (tile, y) rows; value = the
+    global columns / the max-over-ranks wall time per step.
+      stepper_c96_sharded: config #4, the ML-stepper step on a C96 float64 state with
+        the per-step exchange of the global-mean / limiter-profile row partials
+        (all-gather over RCCL, folded in global row order: the same bits at any N);
+      predict_mappm_c384_sharded: north_star's fused predict + mappm at C384 x 79L."""
+    import torch
+
+    from fv3net_amd import workloads as W
+
+    out = {}
+    wl = W.make_sharded_stepper_workload(96, rank, world, seed=11, device=dev)
+    steps = 30
+    wall, t = timed_steps(wl.step, steps, 3, dist, settle_ms=settle_ms)
+    wall = max_over_ranks(wall, dist, dev)
+    del wl
+    wl = W.make_sharded_stepper_workload(96, rank, world, seed=11, device=dev)  # fresh state: exactly 1 step
+    means, profile = W.ShardedStepperWorkload.means(wl.step())
+    out["stepper_c96_sharded"] = {
+        "columns_per_s": wl.ncol_global / (wall / steps), "ms_per_step": wall / steps * 1e3,
+        "scaling": "strong", "columns_global": wl.ncol_global, "columns_per_rank_max": wl.ncol,
+        "global_means": [float(x) for x in means.cpu()],
+        "limiter_profile_sum": float(profile.sum().item()),
+        "note": "wall clock per step incl. the per-step all-gather; global_means / limiter_profile_sum after "
+                "one step from the seeded state carry the same bits at any N"}
+    del wl
+    wl = W.make_predict_mappm_workload(384, rank, world, seed=21, device=dev)
+    steps = 10
+    wall, t = timed_steps(wl.step, steps, 2, dist, settle_ms=settle_ms)
+    wall = max_over_ranks(wall, dist, dev)
+    out["predict_mappm_c384_sharded"] = {
+        "columns_per_s": wl.ncol_global / (wall / steps), "ms_per_step": wall / steps * 1e3,
+        "scaling": "strong", "columns_global": wl.ncol_global, "columns_per_rank_max": wl.ncol,
+        "gpu_ms_per_step_rank0": t * 1e3,
+        "bytes_per_column_kernels": wl.bytes_per_column,
+        "hbm_gbs_per_gpu_kernels": wl.ncol * wl.bytes_per_column / t / 1e9,
+        "tflops_per_gpu_dense": wl.ncol * wl.flops_per_column / t / 1e12}
+    del wl
+    torch.cuda.empty_cache()
+    return out
+
+
+def host_to_host(dev, res, steps=10):
+    """The reference's boundary crossing: float64 host (numpy) T/q in, pageable H2D
+    copies, the fused predict reading float64 in place, float32 dQ1/dQ2 copied back to
+    host numpy (pure_keras.py:98-118 runs on host arrays).  Wall time per step."""
+    import torch
+
+    from fv3net_amd import workloads as W
+
+    wl = W.make_dense_workload(res, seed=3, device=dev)
+    T = wl.inputs[0].double().cpu().numpy()
+    q = wl.inputs[1].double().cpu().numpy()
+    dT = torch.empty(T.shape, dtype=torch.float64, device=dev)
+    dq = torch.empty(q.shape, dtype=torch.float64, device=dev)
+    bound = wl.model.bind([dT, dq], level_axes=[1, 1])
+    host_out = [np.empty(T.shape, np.float32), np.empty(T.shape, np.float32)]
+
+    def step():
+        dT.copy_(torch.from_numpy(T))
+        dq.copy_(torch.from_numpy(q))
+        outs = bound()
+        for h, o in zip(host_out, outs):
+            h[...] = o.cpu().numpy()
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    wall = (time.perf_counter() - t0) / steps
+    nbytes = T.nbytes + q.nbytes + sum(h.nbytes for h in host_out)
+    return {"columns_per_s": wl.ncol / wall, "ms_per_step": wall * 1e3, "host_bytes_per_step": nbytes,
+            "pcie_inclusive_gbs": nbytes / wall / 1e9,
+            "note": "float64 numpy in -> pageable H2D -> fused predict (f64 read in place) -> D2H float32 numpy"}
+
+
+def reference_mappm_cpu(seconds=5.0):
+    """The reference's own Fortran mappm (flang build in oracle/_ref)
+    timed on one host core in 512-column chunks on config #3 columns (79 -> 79, kord 1).
+    A reported baseline only."""
+    from oracle import mappm as OM
+
+    if not OM.reference_available():
+        return None
+    rng = np.random.default_rng(0)
+    n = 8192
+    base = np.linspace(200.0, 1800.0, 79)[:, None]
+    delp = (base * rng.uniform(0.99, 1.01, (79, n))).astype(np.float32)
+    pe1 = np.concatenate([np.full((1, n), 300.0, np.float32), 300.0 + np.cumsum(delp, 0, dtype=np.float32)])
+    d2 = (base * rng.uniform(0.99, 1.01, (79, n))).astype(np.float32)
+    pe2 = np.concatenate([np.full((1, n), 300.0, np.float32), 300.0 + np.cumsum(d2, 0, dtype=np.float32)])
+    q = rng.normal(250.0, 10.0, (79, n)).astype(np.float32)
+    cols = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        OM.reference_mappm(pe1, q, pe2, 1, 1)
+        cols += n
+    dt = time.perf_counter() - t0
+    return {"value": cols / dt, "unit": "columns/s", "cores": 1, "kind": "reference",
+            "sample": f"{cols} config #3 columns (79 -> 79, kord 1, iv 1) through the reference mappm.f90 "
+                      f"(flang -O2, oracle/_ref) in 512-column chunks via ctypes, {dt:.1f} s, 1 core"}
+
+
 def extra_measurements(dev, settle_ms=150.0):
     import torch
 
@@ -190,6 +307,10 @@ def extra_measurements(dev, settle_ms=150.0):
         out[name] = with_counters(name, {"columns_per_s": ncol / t, "ms_per_step": t * 1e3, "hbm_gbs": gbs,
                                          "frac_hbm_peak": gbs / W.HBM_PEAK_GBS}, wl.bytes_per_column * ncol)
         del wl
+    try:
+        out["mappm_c384_79to79_kord1"]["cpu_baseline"] = reference_mappm_cpu()
+    except Exception as e:  # a report, never fatal
+        log("reference mappm cpu baseline failed:", repr(e))
     # config #4: one ML-stepper step (predict + fused limiter/diagnostics/apply + global
     # means) on a float64 C96 state, one GPU
     wl = W.make_stepper_workload(96, seed=11, device=dev)
@@ -233,6 +354,9 @@ def extra_measurements(dev, settle_ms=150.0):
             "fine_columns_per_s": wl.ncol_fine / t, "ms_per_step": t * 1e3, "hbm_gbs": gbs,
             "frac_hbm_peak": gbs / W.HBM_PEAK_GBS}, wl.bytes_per_column * wl.ncol_fine)
         del wl
+    # host -> host (numpy float64 in, numpy float32 out) beside the device-resident legs
+    for res in (48, 384):
+        out[f"dense_c{res}_host_to_host"] = host_to_host(dev, res)
     torch.cuda.empty_cache()
     return out
 
@@ -308,9 +432,14 @@ def main():
             result["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds)
         except Exception as e:  # the baseline is a report, never fatal
             log("cpu_baseline failed:", repr(e))
-    if rank == 0 and world == 1 and not args.no_extra:
+    if not args.no_extra:
         del wl
         torch.cuda.empty_cache()
+        try:  # every rank takes part: one global problem sharded over the ranks
+            result["extra_scaling"] = scaling_legs(dev, dist, rank, world, settle_ms=min(args.settle_ms, 150.0))
+        except Exception as e:
+            log("scaling legs failed:", repr(e))
+    if rank == 0 and world == 1 and not args.no_extra:
         try:
             result["extra"] = extra_measurements(dev, settle_ms=min(args.settle_ms, 150.0))
         except Exception as e:

@@ -46,9 +46,23 @@ EXPORTED_SYMBOLS = (
     "fv3_level_sums",
     "fv3_level_sums_f64",
     "fv3_level_sums_u8",
+    "fv3_area_weighted_row_sums",
+    "fv3_area_weighted_row_sums_f64",
+    "fv3_level_row_sums_u8",
+    "fv3_level_row_sums_f64",
+    "fv3_fold_rows",
     "fv3_ml_epilogue",
     "fv3_ml_epilogue_ex",
     "fv3_tendency_columns",
+    "fv3_range_mask",
+    "fv3_classify_one_hot",
+    "fv3_zc_infer_gscond_cloud",
+    "fv3_zc_squash",
+    "fv3_zc_zero_where",
+    "fv3_zc_gscond_update",
+    "fv3_zc_ice_water_flag",
+    "fv3_zc_precpd_conservative",
+    "fv3_zc_precip_simple",
     "fv3_standard_normalize",
     "fv3_standard_denormalize",
 )
@@ -63,6 +77,14 @@ EPI_HAS_DQ1 = 1
 EPI_HAS_DQ2 = 2
 TEND_WIND = 0
 TEND_MASS = 1
+
+# fv3_zc_gscond_update modes
+ZC_CLOUD_EMULATOR = 0
+ZC_CLOUD_IDENTICAL = 1
+ZC_CLOUD_VANISHES = 2
+ZC_CLOUD_CLASS_ZERO = 3
+ZC_CLOUD_CLASS_NOTEND = 4
+ZC_PHASE_DEPENDENT = 5
 
 
 class NativeLibraryError(RuntimeError):
@@ -165,6 +187,20 @@ _SIGNATURES = {
     "fv3_level_sums": (_I, [_P, Layout, _I64, _I, _P, _P]),
     "fv3_level_sums_f64": (_I, [_P, Layout, _I64, _I, _P, _P]),
     "fv3_level_sums_u8": (_I, [_P, Layout, _I64, _I, _P, _P]),
+    "fv3_area_weighted_row_sums": (_I, [ctypes.POINTER(_P), _I, _P, _I64, _I, _P, _I64, _P]),
+    "fv3_area_weighted_row_sums_f64": (_I, [ctypes.POINTER(_P), _I, _P, _I64, _I, _P, _I64, _P]),
+    "fv3_level_row_sums_u8": (_I, [_P, _I, _I64, _I, _I64, _P, _I64, _P]),
+    "fv3_level_row_sums_f64": (_I, [_P, _I, _I64, _I, _I64, _P, _I64, _P]),
+    "fv3_fold_rows": (_I, [_P, _I64, _I, _P, _P]),
+    "fv3_range_mask": (_I, [_P, _P, _I64, _D, _D, _I, _I, _I, _P]),
+    "fv3_classify_one_hot": (_I, [_P, _I, _I64, _P, _I, _I, _I, _P]),
+    "fv3_zc_infer_gscond_cloud": (_I, [_P, _P, _P, _P, _I64, _I, _P]),
+    "fv3_zc_squash": (_I, [_P, _P, _D, _P, _P, _I64, _I, _P]),
+    "fv3_zc_zero_where": (_I, [_P, _P, _P, _I64, _I, _P]),
+    "fv3_zc_gscond_update": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I, _P]),
+    "fv3_zc_ice_water_flag": (_I, [_P, _P, _D, _P, _I64, _I64, _I, _P]),
+    "fv3_zc_precpd_conservative": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I64, _I, _P]),
+    "fv3_zc_precip_simple": (_I, [_P, _P, _P, _P, _P, _P, _I, _I64, _I, _P]),
     "fv3_standard_normalize": (_I, [_P, _I, Layout, _P, _P, _I, _P, Layout, _I64, _I, _P]),
     "fv3_standard_denormalize": (_I, [_P, Layout, _P, _P, _I, _P, Layout, _I64, _I, _P]),
     "fv3_ml_epilogue": (_I, [ctypes.POINTER(EpilogueIO), Layout, _I64, _I, _I, _D, _I, _I, _P]),

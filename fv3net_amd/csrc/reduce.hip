@@ -238,3 +238,168 @@ extern "C" int fv3_area_weighted_sums_f64(const double* const* diags, int n_diag
 {
     return fv3::area_weighted_sums_impl<double>(diags, n_diag, area, ncol, partial, stream);
 }
+
+// ====================================================================================
+// World-size-invariant global sums.  The partials are taken per grid ROW (one (tile, y)
+// row of row_len columns: what a rank's contiguous band of the flattened (tile, y) rows
+// is made of, distributed.column_segments) and folded in global row order, so the
+// global sums have the same bits whatever the number of ranks the rows are spread
+// over (distributed.global_row_sums).  One wave per row: each lane sums its columns
+// c = lane, lane + 64, ... in order, then a fixed xor butterfly.
+// ====================================================================================
+namespace fv3 {
+namespace {
+
+template <typename T>
+__global__ __launch_bounds__(64) void area_row_sums_kernel(DiagPtrs<T> d, int n_diag, const T* __restrict__ area,
+                                                           int row_len, double* __restrict__ out, int64_t out_ld)
+{
+    const int64_t r = blockIdx.x;
+    const int lane = threadIdx.x;
+    const T* a = area + r * row_len;
+    double sa = 0.0;
+    for (int c = lane; c < row_len; c += 64) sa += (double)a[c];
+    sa = wave_sum(sa);
+    double* o = out + r * out_ld;
+    for (int j = 0; j < n_diag; ++j) {
+        const T* x = d.p[j] + r * row_len;
+        double s = 0.0;
+        for (int c = lane; c < row_len; c += 64) s += (double)(a[c] * x[c]);  // area * x in T (numpy's product)
+        s = wave_sum(s);
+        if (lane == 0) {
+            o[2 * j] = s;
+            o[2 * j + 1] = sa;
+        }
+    }
+}
+
+// per (row, level) sums of a (nz, nrows, row_len) float64 field: out[r][k], one wave each
+__global__ __launch_bounds__(64) void level_row_sums_f64_kernel(const double* __restrict__ x, int nz, int row_len,
+                                                                int64_t level_stride, double* __restrict__ out,
+                                                                int64_t out_ld)
+{
+    const int64_t r = blockIdx.x;
+    const int k = blockIdx.y;
+    const double* p = x + (int64_t)k * level_stride + r * row_len;
+    double s = 0.0;
+    for (int c = threadIdx.x; c < row_len; c += 64) s += p[c];
+    s = wave_sum(s);
+    if (threadIdx.x == 0) out[r * out_ld + k] = s;
+}
+
+// the same for a uint8 flag field: the counts are integers, exact in any order, so one
+// thread per (row, level) counts its row run (adjacent threads: adjacent rows)
+__global__ __launch_bounds__(256) void level_row_sums_u8_kernel(const unsigned char* __restrict__ x, int nz,
+                                                                int64_t nrows, int row_len, int64_t level_stride,
+                                                                double* __restrict__ out, int64_t out_ld)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nrows * nz) return;
+    const int k = (int)(i / nrows);
+    const int64_t r = i - (int64_t)k * nrows;
+    const unsigned char* p = x + (int64_t)k * level_stride + r * row_len;
+    unsigned n = 0;
+    for (int c = 0; c < row_len; ++c) n += p[c];
+    out[r * out_ld + k] = (double)n;
+}
+
+// out[j] = sum_r rows[r][j]: one wave per j, lane l sums rows l, l + 64, ... in order,
+// then the fixed xor butterfly (the order depends only on the global row index)
+__global__ __launch_bounds__(64) void fold_rows_kernel(const double* __restrict__ rows, int64_t nrows, int width,
+                                                       double* __restrict__ out)
+{
+    const int j = blockIdx.x;
+    double s = 0.0;
+    for (int64_t r = threadIdx.x; r < nrows; r += 64) s += rows[r * width + j];
+    s = wave_sum(s);
+    if (threadIdx.x == 0) out[j] = s;
+}
+
+template <typename T>
+int area_row_sums_impl(const T* const* diags, int n_diag, const T* area, int64_t nrows, int row_len, double* partial,
+                       int64_t partial_ld, void* stream)
+{
+    clear_error();
+    FV3_REQUIRE(n_diag >= 0 && n_diag <= 64, "area_weighted_row_sums: n_diag must be in [0, 64]");
+    FV3_REQUIRE(nrows >= 0 && row_len >= 1, "area_weighted_row_sums: bad sizes nrows=%lld row_len=%d",
+                (long long)nrows, row_len);
+    FV3_REQUIRE(nrows < 0x7fffffff, "area_weighted_row_sums: too many rows");
+    FV3_REQUIRE(partial_ld >= 2 * n_diag, "area_weighted_row_sums: row stride %lld < 2 * n_diag",
+                (long long)partial_ld);
+    if (n_diag == 0 || nrows == 0) return FV3_OK;
+    FV3_REQUIRE(diags && area && partial, "area_weighted_row_sums: NULL array");
+    DiagPtrs<T> dp{};
+    for (int j = 0; j < n_diag; ++j) {
+        FV3_REQUIRE(diags[j], "area_weighted_row_sums: NULL diagnostic %d", j);
+        dp.p[j] = diags[j];
+    }
+    hipLaunchKernelGGL(area_row_sums_kernel<T>, dim3((unsigned)nrows), dim3(64), 0, (hipStream_t)stream, dp, n_diag,
+                       area, row_len, partial, partial_ld);
+    FV3_LAUNCH_CHECK();
+    return FV3_OK;
+}
+
+template <typename T>
+int level_row_sums_impl(const T* x, int nz, int64_t nrows, int row_len, int64_t level_stride, double* out,
+                        int64_t out_ld, void* stream)
+{
+    clear_error();
+    FV3_REQUIRE(nz >= 1 && nz <= 65535 && nrows >= 0 && nrows < 0x7fffffff && row_len >= 1,
+                "level_row_sums: bad sizes nz=%d nrows=%lld row_len=%d", nz, (long long)nrows, row_len);
+    FV3_REQUIRE(nz == 1 || level_stride >= nrows * row_len, "level_row_sums: level stride %lld < %lld",
+                (long long)level_stride, (long long)(nrows * row_len));
+    FV3_REQUIRE(out_ld >= nz, "level_row_sums: row stride %lld < nz", (long long)out_ld);
+    if (nrows == 0) return FV3_OK;
+    FV3_REQUIRE(x && out, "level_row_sums: NULL array");
+    hipStream_t s = (hipStream_t)stream;
+    if constexpr (sizeof(T) == 1) {
+        const int64_t n = nrows * nz;
+        hipLaunchKernelGGL(level_row_sums_u8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, nz, nrows,
+                           row_len, level_stride, out, out_ld);
+    } else {
+        hipLaunchKernelGGL(level_row_sums_f64_kernel, dim3((unsigned)nrows, (unsigned)nz), dim3(64), 0, s, x, nz,
+                           row_len, level_stride, out, out_ld);
+    }
+    FV3_LAUNCH_CHECK();
+    return FV3_OK;
+}
+
+}  // namespace
+}  // namespace fv3
+
+extern "C" int fv3_area_weighted_row_sums_f64(const double* const* diags, int n_diag, const double* area,
+                                              int64_t nrows, int row_len, double* partial, int64_t partial_ld,
+                                              void* stream)
+{
+    return fv3::area_row_sums_impl<double>(diags, n_diag, area, nrows, row_len, partial, partial_ld, stream);
+}
+
+extern "C" int fv3_area_weighted_row_sums(const float* const* diags, int n_diag, const float* area, int64_t nrows,
+                                          int row_len, double* partial, int64_t partial_ld, void* stream)
+{
+    return fv3::area_row_sums_impl<float>(diags, n_diag, area, nrows, row_len, partial, partial_ld, stream);
+}
+
+extern "C" int fv3_level_row_sums_u8(const unsigned char* x, int nz, int64_t nrows, int row_len,
+                                     int64_t level_stride, double* out, int64_t out_ld, void* stream)
+{
+    return fv3::level_row_sums_impl<unsigned char>(x, nz, nrows, row_len, level_stride, out, out_ld, stream);
+}
+
+extern "C" int fv3_level_row_sums_f64(const double* x, int nz, int64_t nrows, int row_len, int64_t level_stride,
+                                      double* out, int64_t out_ld, void* stream)
+{
+    return fv3::level_row_sums_impl<double>(x, nz, nrows, row_len, level_stride, out, out_ld, stream);
+}
+
+extern "C" int fv3_fold_rows(const double* rows, int64_t nrows, int width, double* out, void* stream)
+{
+    fv3::clear_error();
+    FV3_REQUIRE(nrows >= 0 && width >= 0, "fold_rows: bad sizes nrows=%lld width=%d", (long long)nrows, width);
+    if (width == 0) return FV3_OK;
+    FV3_REQUIRE(rows && out, "fold_rows: NULL array");
+    hipLaunchKernelGGL(fv3::fold_rows_kernel, dim3((unsigned)width), dim3(64), 0, (hipStream_t)stream, rows, nrows,
+                       width, out);
+    FV3_LAUNCH_CHECK();
+    return FV3_OK;
+}

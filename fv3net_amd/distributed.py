@@ -14,7 +14,7 @@ the CPU tests.
 """
 import ctypes
 from dataclasses import dataclass
-from typing import List, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -196,3 +196,124 @@ def globally_sum_3d_diagnostics(diagnostics: dict, include: Sequence[str], group
             total = combine_partials(part, group)[:, 0]
             sums[f"{k}_global_sum"] = [float(x) for x in total.cpu().numpy()]
     return sums
+
+
+# --------------------------------------------------------------------------------
+# World-size-invariant global sums: partials per grid ROW, gathered in global row
+# order and folded row by row (csrc/reduce.hip).  A rank owns a contiguous band of the
+# flattened (tile, y) rows (row_band), so the gathered rows are the global rows in
+# order and the folded sums carry the same bits for 1, 2, 4 or 8 ranks.
+# --------------------------------------------------------------------------------
+def area_row_partials(diags: Sequence, area, stream=None, out=None):
+    """Device float64 [nrows, n_diag, 2]: per row of (rows, row_len) fields,
+    (sum area*x_d, sum area).  float64 if any operand is (numpy's promotion).  ``out``:
+    a [nrows, W >= 2 n_diag] float64 buffer whose leading columns receive them."""
+    _device.require_gpu()
+    wide = any(torch.is_tensor(t) and t.dtype == torch.float64 for t in [area, *diags])
+    dev = torch.device("cuda", torch.cuda.current_device())
+    conv = (lambda t: torch.as_tensor(t).to(dev, torch.float64).contiguous()) if wide else \
+        (lambda t: _device.to_device_f32(t).contiguous())  # noqa: E731
+    area = conv(area)
+    xs = [conv(d) for d in diags]
+    if area.dim() < 1:
+        raise ValueError("area must have a row axis")
+    row_len = int(area.shape[-1])
+    nrows = area.numel() // max(row_len, 1)
+    for d in xs:
+        if d.shape != area.shape:
+            raise ValueError(f"diagnostic shape {tuple(d.shape)} != area shape {tuple(area.shape)}")
+    if out is None:
+        out = torch.empty((nrows, len(xs), 2), dtype=torch.float64, device=dev)
+    elif not (out.dtype == torch.float64 and out.dim() == 2 and out.shape[0] == nrows and out.stride(1) == 1
+              and out.shape[1] >= 2 * len(xs)):
+        raise ValueError(f"out must be a row-major [{nrows}, >= {2 * len(xs)}] float64 buffer")
+    if not xs or nrows == 0:
+        return out
+    tab = (ctypes.c_void_p * len(xs))(*[d.data_ptr() for d in xs])
+    lib = _native.load()
+    fn = lib.fv3_area_weighted_row_sums_f64 if wide else lib.fv3_area_weighted_row_sums
+    ld = out.stride(0) if out.dim() == 2 else 2 * len(xs)
+    st = fn(tab, len(xs), area.data_ptr(), nrows, row_len, out.data_ptr(), ld, _device.stream_handle(stream))
+    _native.check(st, "area_weighted_row_sums")
+    return out
+
+
+def level_row_partials(field, stream=None, out=None):
+    """Device float64 [nrows, nz] per-row level sums of a (nz, rows, row_len) field
+    (uint8 flags such as specific_humidity_limiter_active, or float64) read in place.
+    ``out``: a [nrows, >= nz] float64 view (e.g. columns of a wider buffer)."""
+    _device.require_gpu()
+    t = field if torch.is_tensor(field) else torch.from_numpy(np.ascontiguousarray(field))
+    t = t.to(torch.device("cuda", torch.cuda.current_device()))
+    if t.dtype not in (torch.uint8, torch.float64):
+        t = t.to(torch.float64)
+    if t.dim() != 3:
+        raise ValueError("field must be (z, rows, row_len)")
+    if not (t.stride(2) == 1 and t.stride(1) == t.shape[2]):
+        t = t.contiguous()
+    nz, nrows, row_len = (int(n) for n in t.shape)
+    if out is None:
+        out = torch.empty((nrows, nz), dtype=torch.float64, device=t.device)
+    elif not (out.dtype == torch.float64 and out.dim() == 2 and out.shape[0] == nrows and out.stride(1) == 1
+              and out.shape[1] >= nz):
+        raise ValueError(f"out must be a row-major [{nrows}, >= {nz}] float64 view")
+    lib = _native.load()
+    fn = lib.fv3_level_row_sums_u8 if t.dtype == torch.uint8 else lib.fv3_level_row_sums_f64
+    st = fn(t.data_ptr(), nz, nrows, row_len, int(t.stride(0)) if nz > 1 else nrows * row_len, out.data_ptr(),
+            int(out.stride(0)), _device.stream_handle(stream))
+    _native.check(st, "level_row_sums")
+    return out
+
+
+def _distributed() -> bool:
+    return dist is not None and dist.is_available() and dist.is_initialized()
+
+
+def row_counts(nrows: int, group=None) -> List[int]:
+    """Every rank's row count (one small all-gather; fixed for a run, so callers keep it)."""
+    if not _distributed():
+        return [int(nrows)]
+    dev = _backend_device(group)
+    n = torch.tensor([int(nrows)], dtype=torch.int64, device=dev)
+    counts = [torch.empty_like(n) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(counts, n, group=group)
+    return [int(c.item()) for c in counts]
+
+
+def gather_rows(local, group=None, counts: Optional[Sequence[int]] = None):
+    """All ranks' [nrows_r, W] row partials concatenated in rank order (= global row
+    order for row bands): one all-gather of the rows padded to the largest band
+    (``counts`` from row_counts, gathered here when not given).  Without a process
+    group: ``local`` itself."""
+    if not _distributed():
+        return local
+    dev = _backend_device(group)
+    world = dist.get_world_size(group)
+    x = local.to(dev).contiguous()
+    counts = list(counts) if counts is not None else row_counts(x.shape[0], group)
+    if len(counts) != world or counts[dist.get_rank(group)] != x.shape[0]:
+        raise ValueError(f"row counts {counts} do not match this rank's {x.shape[0]} rows")
+    cap = max(counts)
+    pad = torch.zeros((cap,) + tuple(x.shape[1:]), dtype=x.dtype, device=dev)
+    pad[: x.shape[0]] = x
+    bufs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad, group=group)
+    return torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
+
+
+def fold_rows(rows, stream=None):
+    """Device float64 sums over the rows of [nrows, ...] partials, in row order (HIP)."""
+    _device.require_gpu()
+    r = rows.to(torch.device("cuda", torch.cuda.current_device()), torch.float64).contiguous()
+    nrows = int(r.shape[0])
+    width = int(r[0].numel()) if nrows else int(np.prod(r.shape[1:], dtype=np.int64))
+    out = torch.empty(tuple(r.shape[1:]), dtype=torch.float64, device=r.device)
+    st = _native.load().fv3_fold_rows(r.data_ptr(), nrows, width, out.data_ptr(), _device.stream_handle(stream))
+    _native.check(st, "fold_rows")
+    return out
+
+
+def global_row_sums(local_rows, group=None, counts: Optional[Sequence[int]] = None):
+    """fold_rows(gather_rows(local_rows)): the same bits on every rank and for every
+    world size."""
+    return fold_rows(gather_rows(local_rows, group, counts))

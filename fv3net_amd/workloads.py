@@ -207,8 +207,142 @@ def make_stepper_workload(res: int = 96, seed: int = 0, device=None, group=None)
         "total_precipitation": 1e-3 * torch.rand((6, res, res), generator=g, device=device, dtype=torch.float64),
     }
     area = 0.5 + 0.5 * torch.rand((6, res, res), generator=g, device=device, dtype=torch.float64)
-    wl = make_dense_workload(min(res, 48), seed=seed, device=device)
-    return StepperWorkload(wl.model, state, area, 900.0, 6 * res * res, group)
+    # the model's output normalisation fitted on tendencies of physical size (dQ1 ~ 1e-4 K/s,
+    # dQ2 ~ 3e-8 kg/kg/s), so the state stays physical over many steps
+    T, q = synthetic_state(8, seed, device, ntile=1)
+    sample_T = T[0].reshape(NZ, -1).T.cpu().numpy()
+    sample_q = q[0].reshape(NZ, -1).T.cpu().numpy()
+    rng = np.random.default_rng(seed)
+    sample_out = [rng.normal(0.0, 1e-4, sample_T.shape).astype(np.float32),
+                  rng.normal(0.0, 3e-8, sample_T.shape).astype(np.float32)]
+    model = DenseColumnModel.random(dense_2x256_config(), seed=1, sample_inputs=[sample_T, sample_q],
+                                    sample_outputs=sample_out)
+    return StepperWorkload(model, state, area, 900.0, 6 * res * res, group)
+
+
+@dataclasses.dataclass
+class ShardedStepperWorkload:
+    """BASELINE config #4 sharded as SURVEY.md 8(e) lays it out: this rank owns the rows
+    [r0, r1) of the flattened (tile, y) rows of one global C<res> state, stored as a
+    (z, rows, x) band, and per step runs the predict, the fused epilogue (in place) and
+    the step's one exchange: the global-mean partials of the 2-D diagnostics (net
+    moistening, column heating, total precipitation) and the 3-D limiter profile
+    (main.py:55-60), taken per grid row, all-gathered (RCCL on the GPU box) and folded in
+    global row order, so the result has the same bits for any number of ranks."""
+    model: DenseColumnModel
+    state: dict
+    area: object
+    dt: float
+    rows: tuple
+    ncol: int          # this rank's columns
+    ncol_global: int
+    group: object = None
+    bound: object = None
+    counts: object = None
+    partials: object = None
+
+    def step(self):
+        from .distributed import area_row_partials, global_row_sums, level_row_partials, row_counts
+        from .stepper import ml_epilogue
+
+        T, q = self.state["air_temperature"], self.state["specific_humidity"]
+        if self.bound is None:
+            self.bound = self.model.bind([T, q], level_axes=[0, 0])
+        dq1, dq2 = self.bound()
+        res = ml_epilogue(dq1, dq2, q, self.state["pressure_thickness_of_atmospheric_layer"], T, self.dt,
+                          self.state["total_precipitation"], in_place=True, level_axis=0)
+        self.state["total_precipitation"] = res["total_precipitation"]
+        if self.partials is None:  # [rows][3 (sum area*x, sum area) pairs + nz limiter counts]
+            self.partials = torch.empty((self.area.shape[0], 6 + q.shape[0]), dtype=torch.float64, device=q.device)
+        local = self.partials
+        area_row_partials([res["net_moistening_due_to_machine_learning"],
+                           res["column_heating_due_to_machine_learning"], res["total_precipitation"]],
+                          self.area, out=local)
+        level_row_partials(res["specific_humidity_limiter_active"], out=local[:, 6:])
+        if self.counts is None:  # the bands are fixed: their sizes are exchanged once
+            self.counts = row_counts(local.shape[0], self.group)
+        return global_row_sums(local, self.group, self.counts)
+
+    @staticmethod
+    def means(total):
+        """(global means of the three 2-D diagnostics, limiter global-sum profile)."""
+        return total[0:6:2] / total[1:6:2], total[6:]
+
+
+def make_sharded_stepper_workload(res: int = 96, rank: int = 0, world: int = 1, seed: int = 0, device=None,
+                                  group=None):
+    """Every rank generates the same global state (seeded) and keeps its row band."""
+    from .distributed import row_band
+
+    wl = make_stepper_workload(res, seed=seed, device=device)
+    r0, r1 = row_band(6 * res, rank, world)
+    band3 = lambda a: a.permute(1, 0, 2, 3).reshape(NZ, 6 * res, res)[:, r0:r1].contiguous()  # noqa: E731
+    band2 = lambda a: a.reshape(6 * res, res)[r0:r1].contiguous()  # noqa: E731
+    state = {k: (band3(v) if v.dim() == 4 else band2(v)) for k, v in wl.state.items()}
+    return ShardedStepperWorkload(wl.model, state, band2(wl.area), wl.dt, (r0, r1), (r1 - r0) * res,
+                                  6 * res * res, group)
+
+
+@dataclasses.dataclass
+class PredictMappmWorkload:
+    """north_star's "fused predict + mappm at C384 x 79L": on this rank's band of the
+    flattened (tile, y) rows of a C<res> state (z, rows, x), the config #2 predict of
+    dQ1/dQ2 from T/q, then both tendencies remapped (mappm, kord 1, iv 1) from the state's
+    edge pressures pe1 = 300 Pa + cumsum(delp) to 79 layers evenly spaced between the
+    same top and surface (a per-column pressure-level regrid of the ML tendencies), all
+    device-resident: one dense kernel and two mappm kernels per step."""
+    model: DenseColumnModel
+    inputs: List
+    outputs: List
+    pe1: object
+    pe2: object
+    remapped: List
+    ncol: int
+    ncol_global: int
+    flops_per_column: int
+    bytes_per_column: int
+    _bound: object = None
+    _plans: object = None
+
+    def step(self):
+        from .mappm import MappmPlan
+
+        if self._bound is None:
+            self._bound = self.model.bind(self.inputs, level_axes=[0, 0], outputs=self.outputs, out_level_axis=0)
+            self._plans = [MappmPlan(self.pe1, o.view(o.shape[0], -1), self.pe2, 1, 1, out=r)
+                           for o, r in zip(self.outputs, self.remapped)]
+        else:
+            self._bound()
+            for p in self._plans:
+                p()
+
+
+def make_predict_mappm_workload(res: int = 384, rank: int = 0, world: int = 1, seed: int = 0, device=None):
+    from .distributed import row_band
+
+    device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    r0, r1 = row_band(6 * res, rank, world)
+    band = lambda a: a.permute(1, 0, 2, 3).reshape(NZ, 6 * res, res)[:, r0:r1].contiguous()  # noqa: E731
+    T, q = synthetic_state(res, seed, device)
+    sample_T = T[0, :, :8, :8].reshape(NZ, -1).T.cpu().numpy()
+    sample_q = q[0, :, :8, :8].reshape(NZ, -1).T.cpu().numpy()
+    model = DenseColumnModel.random(dense_2x256_config(), seed=1, sample_inputs=[sample_T, sample_q])
+    T, q = band(T), band(q)
+    ncol = (r1 - r0) * res
+    g = torch.Generator(device=device)
+    g.manual_seed(seed + 17)
+    base = torch.linspace(200.0, 1800.0, NZ, device=device)[:, None]
+    delp = base * (0.99 + 0.02 * torch.rand((NZ, ncol), generator=g, device=device))
+    top = torch.full((1, ncol), 300.0, device=device)
+    pe1 = torch.cat([top, 300.0 + torch.cumsum(delp, 0)]).contiguous()
+    frac = torch.linspace(0.0, 1.0, NZ + 1, device=device)[:, None]
+    pe2 = (pe1[:1] + frac * (pe1[-1:] - pe1[:1])).contiguous()
+    outs = [torch.empty_like(T), torch.empty_like(T)]
+    remapped = [torch.empty((NZ, ncol), device=device), torch.empty((NZ, ncol), device=device)]
+    cfg = model.config
+    mappm_bytes = 4 * ((NZ + 1) + NZ + (NZ + 1) + NZ)
+    return PredictMappmWorkload(model, [T, q], outs, pe1, pe2, remapped, ncol, 6 * res * res,
+                                cfg.flops_per_column(), 4 * (cfg.k_in + cfg.k_out) + 2 * mappm_bytes)
 
 
 @dataclasses.dataclass

@@ -260,6 +260,81 @@ int fv3_level_sums(const float* x, fv3_layout x_l, int64_t ncol, int nz, double*
 int fv3_level_sums_f64(const double* x, fv3_layout x_l, int64_t ncol, int nz, double* out, void* stream);
 int fv3_level_sums_u8(const unsigned char* x, fv3_layout x_l, int64_t ncol, int nz, double* out, void* stream);
 
+/* World-size-invariant global sums (distributed.global_row_sums): partials per grid ROW
+ * (row_len contiguous columns; a rank's band of the flattened (tile, y) rows is a run
+ * of rows), folded in global row order, so the global result has the same bits for any
+ * number of ranks.
+ *   fv3_area_weighted_row_sums[_f64]: partial[r*partial_ld + 2d + {0,1}] = (sum_c area*x_d,
+ *     sum_c area) over row r of n_diag (rows, row_len) diagnostics, float64;
+ *   fv3_level_row_sums_{u8,f64}: out[r*out_ld + k] = sum_c x[k][r][c] of a (nz, rows,
+ *     row_len) field whose levels are level_stride elements apart, float64 (the u8 flag
+ *     counts are integers, exact in any order);
+ *   (the strides let both write into one [nrows][W] buffer for a single exchange)
+ *   fv3_fold_rows: out[j] = sum_r rows[r][j].
+ * Every sum: lane-strided sequential sums over 64 lanes (column c or row r on lane
+ * c % 64, r % 64) then a fixed 64-lane xor butterfly. */
+int fv3_area_weighted_row_sums(const float* const* diags, int n_diag, const float* area, int64_t nrows,
+                               int row_len, double* partial, int64_t partial_ld, void* stream);
+int fv3_area_weighted_row_sums_f64(const double* const* diags, int n_diag, const double* area,
+                                   int64_t nrows, int row_len, double* partial, int64_t partial_ld,
+                                   void* stream);
+int fv3_level_row_sums_u8(const unsigned char* x, int nz, int64_t nrows, int row_len, int64_t level_stride,
+                          double* out, int64_t out_ld, void* stream);
+int fv3_level_row_sums_f64(const double* x, int nz, int64_t nrows, int row_len, int64_t level_stride,
+                           double* out, int64_t out_ld, void* stream);
+int fv3_fold_rows(const double* rows, int64_t nrows, int width, double* out, void* stream);
+
+/* ---- microphysics emulator hook post-processing (external/emulation) ------------------
+ * On the hook's [feature, sample] arrays, contiguous, n elements (or nz x ncol), every
+ * array of one dtype (f64 != 0: double, else float); numpy semantics (NaN-propagating
+ * maximum/minimum, Python-float constants in the arrays' dtype).
+ *   fv3_range_mask            RangeMask (masks.py:23-39)
+ *   fv3_classify_one_hot      _get_classify_output (zhao_carr.py:214-219): logits
+ *                             [n_class][inner] -> masks [n_class + 1][inner] (uint8), the
+ *                             last = masks[positive] | masks[negative]
+ *   fv3_zc_infer_gscond_cloud infer_gscond_cloud_from_conservation (zhao_carr.py:72-76)
+ *   fv3_zc_squash             squash_water_water_conserving (zhao_carr.py:57-69)
+ *   fv3_zc_zero_where         out = class_mask ? 0 : cloud (mask_zero_cloud_classifier_precpd,
+ *                             zhao_carr.py:240-247)
+ *   fv3_zc_gscond_update      mode FV3_ZC_CLOUD_*: the gscond cloud choice then
+ *                             _update_with_net_condensation (zhao_carr.py:79-105, 164-245);
+ *                             FV3_ZC_PHASE_DEPENDENT: enforce_conservative_phase_dependent
+ *                             with ice_flag from fv3_zc_ice_water_flag (:143-146, 242-245)
+ *   fv3_zc_ice_water_flag     ice_water_flag (zhao_carr.py:108-133) of T - offset over
+ *                             the last axis of (nrows, z) arrays
+ *   fv3_zc_precpd_conservative enforce_conservative_precpd (zhao_carr.py:277-352); precip
+ *                             [ncol] float64 in m
+ *   fv3_zc_precip_simple      conservative_precip_simple (zhao_carr.py:355-371), precip [ncol] */
+#define FV3_ZC_CLOUD_EMULATOR 0     /* enforce_conservative_gscond */
+#define FV3_ZC_CLOUD_IDENTICAL 1    /* mask_where_fortran_cloud_identical */
+#define FV3_ZC_CLOUD_VANISHES 2     /* mask_where_fortran_cloud_vanishes_gscond */
+#define FV3_ZC_CLOUD_CLASS_ZERO 3   /* mask_zero_cloud_classifier (class_mask = zero_cloud) */
+#define FV3_ZC_CLOUD_CLASS_NOTEND 4 /* mask_zero_tend_classifier (class_mask = zero_tendency) */
+#define FV3_ZC_PHASE_DEPENDENT 5    /* enforce_conservative_phase_dependent */
+int fv3_range_mask(const void* x, void* out, int64_t n, double lo, double hi, int has_lo, int has_hi, int f64,
+                   void* stream);
+int fv3_classify_one_hot(const void* logits, int n_class, int64_t inner, unsigned char* masks, int positive,
+                         int negative, int f64, void* stream);
+int fv3_zc_infer_gscond_cloud(const void* qc_in, const void* qv_in, const void* qv_gscond, void* qc_out,
+                              int64_t n, int f64, void* stream);
+int fv3_zc_squash(const void* cloud, const void* humidity, double bound, void* cloud_out, void* humidity_out,
+                  int64_t n, int f64, void* stream);
+int fv3_zc_zero_where(const unsigned char* class_mask, const void* cloud, void* out, int64_t n, int f64,
+                      void* stream);
+int fv3_zc_gscond_update(int mode, const void* qc_in, const void* qv_in, const void* t_in,
+                         const void* qc_fortran_gscond, const void* qc_emulator, const unsigned char* class_mask,
+                         const unsigned char* ice_flag, void* qc_out, void* qv_out, void* t_out, int64_t n,
+                         int f64, void* stream);
+int fv3_zc_ice_water_flag(const void* temperature, const void* cloud, double offset, void* iw, int64_t nrows,
+                          int64_t z, int f64, void* stream);
+int fv3_zc_precpd_conservative(const void* qc_gscond, const void* qv_gscond, const void* t_gscond,
+                               const void* qc_emulator, const void* qv_emulator, const void* delp, void* qc_out,
+                               void* qv_out, void* t_out, double* precip, int nz, int64_t ncol, int f64,
+                               void* stream);
+int fv3_zc_precip_simple(const void* qv_gscond, const void* qc_gscond, const void* qv_emulator,
+                         const void* qc_emulator, const void* delp, void* precip, int nz, int64_t ncol, int f64,
+                         void* stream);
+
 /* ---- StandardScaler (external/fv3fit/fv3fit/_shared/scaler.py:36-100) -------------
  * As the PytorchPredictor applies it around its model (fv3fit/pytorch/predict.py:
  * 299-399):  out = float32((x - mean) / std) computed in float64 (x float32, or float64

@@ -58,3 +58,67 @@ def rank_order_worker(rank, world, port, out_dir):
     np.save(os.path.join(out_dir, f"rank{rank}.npy"), total.numpy())
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _lane_sum(v):
+    """The kernels' order: lane-strided sequential sums over 64 lanes, then the xor
+    butterfly (offsets 32, 16, ..., 1); v is summed along axis 0."""
+    lanes = np.zeros((64,) + v.shape[1:])
+    for c in range(v.shape[0]):
+        lanes[c % 64] = lanes[c % 64] + v[c]
+    for o in (32, 16, 8, 4, 2, 1):
+        lanes = lanes + lanes[np.arange(64) ^ o]
+    return lanes[0]
+
+
+def fold_rows_np(rows):
+    """fv3_fold_rows restated."""
+    return _lane_sum(np.asarray(rows))
+
+
+def _rows_partials_np(x, area):
+    """numpy restatement of fv3_area_weighted_row_sums for (rows, row_len) float64
+    fields: per row, lane-strided sequential sums over 64 lanes, then the kernel's
+    xor butterfly (offsets 32, 16, ..., 1)."""
+    return np.array([[_lane_sum(area[r] * x[r]), _lane_sum(area[r])] for r in range(x.shape[0])])
+
+
+def gather_rows_worker(rank, world, port, out_dir):
+    """Each rank owns a row band of a (rows, x) field: its row partials, gathered in
+    global row order and folded row by row, must give the world-1 bits."""
+    import torch
+
+    from fv3net_amd import distributed as D
+
+    dist = init_gloo(rank, world, port)
+    rng = np.random.default_rng(1)
+    nrows, nx = 6 * 12, 12
+    x = rng.normal(280, 20, (nrows, nx))
+    area = rng.uniform(0.5, 1.0, (nrows, nx))
+    r0, r1 = D.row_band(nrows, rank, world)
+    local = torch.from_numpy(_rows_partials_np(x[r0:r1], area[r0:r1]))
+    rows = D.gather_rows(local).numpy()
+    total = fold_rows_np(rows)
+    np.save(os.path.join(out_dir, f"rank{rank}.npy"), np.concatenate([total, rows.reshape(-1)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def sharded_stepper_worker(rank, world, port, out_dir, res, steps):
+    """The config #4 sharded stepper (workloads.ShardedStepperWorkload) on one GPU per
+    rank process (gloo for the exchange): global sums and this rank's state band."""
+    import torch
+
+    from fv3net_amd import workloads as W
+
+    dist = init_gloo(rank, world, port)
+    torch.cuda.set_device(0)
+    wl = W.make_sharded_stepper_workload(res, rank, world, seed=5)
+    for _ in range(steps):
+        total = wl.step()
+    torch.cuda.synchronize()
+    np.save(os.path.join(out_dir, f"total{rank}.npy"), total.cpu().numpy())
+    np.save(os.path.join(out_dir, f"q{rank}.npy"), wl.state["specific_humidity"].cpu().numpy())
+    np.save(os.path.join(out_dir, f"rows{rank}.npy"), np.array(wl.rows))
+    dist.barrier()
+    dist.destroy_process_group()

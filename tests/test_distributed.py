@@ -96,3 +96,68 @@ def test_gpu_global_average_two_ranks(gpu, tmp_path):
     expect = np.array([np.sum(area * x), np.sum(area * x * 2)]) / np.sum(area)
     assert (res[0].view(np.uint64) == res[1].view(np.uint64)).all()
     np.testing.assert_allclose(res[0], expect, rtol=1e-12)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_row_partials_are_world_size_invariant(tmp_path, world):
+    """Row partials gathered in global row order and folded row by row: every rank of
+    every world size gets the world-1 bits (distributed.gather_rows + fv3_fold_rows order)."""
+    _spawn(H.gather_rows_worker, world, str(tmp_path))
+    res = [np.load(tmp_path / f"rank{r}.npy") for r in range(world)]
+    rng = np.random.default_rng(1)
+    x = rng.normal(280, 20, (72, 12))
+    area = rng.uniform(0.5, 1.0, (72, 12))
+    rows = H._rows_partials_np(x, area)
+    total = H.fold_rows_np(rows)
+    expect = np.concatenate([total, rows.reshape(-1)])
+    for r in res:
+        assert (r.view(np.uint64) == expect.view(np.uint64)).all()
+    np.testing.assert_allclose(total, [np.sum(area * x), np.sum(area)], rtol=1e-13)
+
+
+def test_gather_rows_without_process_group_is_identity():
+    import torch
+
+    x = torch.arange(6.0).reshape(3, 2)
+    assert D.gather_rows(x) is x
+
+
+@pytest.mark.gpu
+def test_gpu_row_partials_match_restatement(gpu):
+    """fv3_area_weighted_row_sums_f64 / fv3_level_row_sums_u8 / fv3_fold_rows vs the
+    numpy restatement of their order, bit for bit."""
+    import torch
+
+    rng = np.random.default_rng(2)
+    x = rng.normal(280, 20, (40, 96))
+    area = rng.uniform(0.5, 1.0, (40, 96))
+    got = D.area_row_partials([torch.from_numpy(x).cuda()], torch.from_numpy(area).cuda()).cpu().numpy()
+    ref = H._rows_partials_np(x, area)
+    assert (got[:, 0].view(np.uint64) == ref.view(np.uint64)).all()
+    flag = (rng.uniform(size=(7, 40, 96)) < 0.2).astype(np.uint8)
+    lev = D.level_row_partials(torch.from_numpy(flag).cuda()).cpu().numpy()
+    assert (lev == flag.sum(axis=2).T).all()
+    big = rng.normal(0, 1e6, (700, 5))  # more rows than lanes: lane-strided partial sums
+    for rows in (ref, big):
+        tot = D.fold_rows(torch.from_numpy(rows).cuda()).cpu().numpy()
+        expect = H.fold_rows_np(rows)
+        assert (tot.view(np.uint64) == expect.view(np.uint64)).all()
+
+
+@pytest.mark.gpu
+def test_sharded_stepper_two_ranks_bit_identical_to_one(gpu, tmp_path):
+    """Config #4 sharded over 2 ranks (2 processes on one GPU, gloo exchange): after two
+    steps the global means / limiter profile have the world-1 bits on both ranks, and
+    each rank's state band equals the world-1 state's rows."""
+    for world in (1, 2):
+        (tmp_path / f"w{world}").mkdir()
+        _spawn(H.sharded_stepper_worker, world, str(tmp_path / f"w{world}"), 12, 2)
+    one = np.load(tmp_path / "w1" / "total0.npy")
+    q1 = np.load(tmp_path / "w1" / "q0.npy")
+    for r in range(2):
+        t = np.load(tmp_path / "w2" / f"total{r}.npy")
+        assert (t.view(np.uint64) == one.view(np.uint64)).all()
+        r0, r1 = np.load(tmp_path / "w2" / f"rows{r}.npy")
+        q = np.load(tmp_path / "w2" / f"q{r}.npy")
+        assert (q.view(np.uint64) == q1[:, r0:r1].view(np.uint64)).all()
+    assert np.isfinite(one).all() and one[6:].sum() > 0  # the limiter engaged somewhere
