@@ -65,6 +65,8 @@ EXPORTED_SYMBOLS = (
     "fv3_zc_precip_simple",
     "fv3_standard_normalize",
     "fv3_standard_denormalize",
+    "fv3_standard_normalize_f64",
+    "fv3_standard_denormalize_f64",
 )
 ABI_VERSION = 3
 
@@ -203,6 +205,8 @@ _SIGNATURES = {
     "fv3_zc_precip_simple": (_I, [_P, _P, _P, _P, _P, _P, _I, _I64, _I, _P]),
     "fv3_standard_normalize": (_I, [_P, _I, Layout, _P, _P, _I, _P, Layout, _I64, _I, _P]),
     "fv3_standard_denormalize": (_I, [_P, Layout, _P, _P, _I, _P, Layout, _I64, _I, _P]),
+    "fv3_standard_normalize_f64": (_I, [_P, _I, Layout, _P, _P, _I, _P, Layout, _I64, _I, _P]),
+    "fv3_standard_denormalize_f64": (_I, [_P, Layout, _P, _P, _I, _P, Layout, _I64, _I, _P]),
     "fv3_ml_epilogue": (_I, [ctypes.POINTER(EpilogueIO), Layout, _I64, _I, _I, _D, _I, _I, _P]),
     "fv3_ml_epilogue_ex": (_I, [ctypes.POINTER(EpilogueIO), Layout, _I64, _I, _I, _D, _I, _I, _I, _P]),
     "fv3_tendency_columns": (_I, [_P, _P, _P, _P, _P, _P, Layout, _I64, _I, _I, _I, _D, _P]),

@@ -23,11 +23,11 @@ namespace {
 
 constexpr int kScaleBlock = 256;
 
-template <typename T>
+template <typename T, typename TO>
 __global__ __launch_bounds__(kScaleBlock) void standard_normalize_kernel(const T* __restrict__ x, fv3_layout xl,
                                                                          const double* __restrict__ mean,
                                                                          const double* __restrict__ std_,
-                                                                         int per_level, float* __restrict__ out,
+                                                                         int per_level, TO* __restrict__ out,
                                                                          fv3_layout ol, int64_t ncol)
 {
     const int64_t c = (int64_t)blockIdx.x * kScaleBlock + threadIdx.x;
@@ -36,10 +36,11 @@ __global__ __launch_bounds__(kScaleBlock) void standard_normalize_kernel(const T
     const int p = per_level ? k : 0;
     const double v = (double)x[col_offset(xl, c) + (int64_t)k * xl.ld];
     const double n = (v - mean[p]) / std_[p];
-    out[col_offset(ol, c) + (int64_t)k * ol.ld] = (float)n;
+    out[col_offset(ol, c) + (int64_t)k * ol.ld] = (TO)n;
 }
 
-__global__ __launch_bounds__(kScaleBlock) void standard_denormalize_kernel(const float* __restrict__ y,
+template <typename T>
+__global__ __launch_bounds__(kScaleBlock) void standard_denormalize_kernel(const T* __restrict__ y,
                                                                            fv3_layout yl,
                                                                            const double* __restrict__ mean,
                                                                            const double* __restrict__ std_,
@@ -66,6 +67,39 @@ int check_scale_args(const void* x, fv3_layout xl, const double* mean, const dou
     return FV3_OK;
 }
 
+template <typename TO>
+int normalize_impl(const void* x, int x_f64, fv3_layout x_l, const double* mean, const double* std_, int n_params,
+                   TO* out, fv3_layout out_l, int64_t ncol, int nz, void* stream)
+{
+    clear_error();
+    if (int st = check_scale_args(x, x_l, mean, std_, n_params, out, out_l, ncol, nz, "standard_normalize")) return st;
+    if (ncol == 0) return FV3_OK;
+    const dim3 grid((unsigned)((ncol + kScaleBlock - 1) / kScaleBlock), (unsigned)nz);
+    if (x_f64)
+        hipLaunchKernelGGL((standard_normalize_kernel<double, TO>), grid, dim3(kScaleBlock), 0, (hipStream_t)stream,
+                           (const double*)x, x_l, mean, std_, n_params == nz ? 1 : 0, out, out_l, ncol);
+    else
+        hipLaunchKernelGGL((standard_normalize_kernel<float, TO>), grid, dim3(kScaleBlock), 0, (hipStream_t)stream,
+                           (const float*)x, x_l, mean, std_, n_params == nz ? 1 : 0, out, out_l, ncol);
+    FV3_LAUNCH_CHECK();
+    return FV3_OK;
+}
+
+template <typename T>
+int denormalize_impl(const T* y, fv3_layout y_l, const double* mean, const double* std_, int n_params, double* out,
+                     fv3_layout out_l, int64_t ncol, int nz, void* stream)
+{
+    clear_error();
+    if (int st = check_scale_args(y, y_l, mean, std_, n_params, out, out_l, ncol, nz, "standard_denormalize"))
+        return st;
+    if (ncol == 0) return FV3_OK;
+    const dim3 grid((unsigned)((ncol + kScaleBlock - 1) / kScaleBlock), (unsigned)nz);
+    hipLaunchKernelGGL(standard_denormalize_kernel<T>, grid, dim3(kScaleBlock), 0, (hipStream_t)stream, y, y_l, mean,
+                       std_, n_params == nz ? 1 : 0, out, out_l, ncol);
+    FV3_LAUNCH_CHECK();
+    return FV3_OK;
+}
+
 }  // namespace
 }  // namespace fv3
 
@@ -73,33 +107,26 @@ extern "C" int fv3_standard_normalize(const void* x, int x_f64, fv3_layout x_l, 
                                       const double* std_, int n_params, float* out, fv3_layout out_l, int64_t ncol,
                                       int nz, void* stream)
 {
-    using namespace fv3;
-    clear_error();
-    if (int st = check_scale_args(x, x_l, mean, std_, n_params, out, out_l, ncol, nz, "standard_normalize")) return st;
-    if (ncol == 0) return FV3_OK;
-    const dim3 grid((unsigned)((ncol + kScaleBlock - 1) / kScaleBlock), (unsigned)nz);
-    if (x_f64)
-        hipLaunchKernelGGL(standard_normalize_kernel<double>, grid, dim3(kScaleBlock), 0, (hipStream_t)stream,
-                           (const double*)x, x_l, mean, std_, n_params == nz ? 1 : 0, out, out_l, ncol);
-    else
-        hipLaunchKernelGGL(standard_normalize_kernel<float>, grid, dim3(kScaleBlock), 0, (hipStream_t)stream,
-                           (const float*)x, x_l, mean, std_, n_params == nz ? 1 : 0, out, out_l, ncol);
-    FV3_LAUNCH_CHECK();
-    return FV3_OK;
+    return fv3::normalize_impl<float>(x, x_f64, x_l, mean, std_, n_params, out, out_l, ncol, nz, stream);
+}
+
+extern "C" int fv3_standard_normalize_f64(const void* x, int x_f64, fv3_layout x_l, const double* mean,
+                                          const double* std_, int n_params, double* out, fv3_layout out_l,
+                                          int64_t ncol, int nz, void* stream)
+{
+    return fv3::normalize_impl<double>(x, x_f64, x_l, mean, std_, n_params, out, out_l, ncol, nz, stream);
 }
 
 extern "C" int fv3_standard_denormalize(const float* y, fv3_layout y_l, const double* mean, const double* std_,
                                         int n_params, double* out, fv3_layout out_l, int64_t ncol, int nz,
                                         void* stream)
 {
-    using namespace fv3;
-    clear_error();
-    if (int st = check_scale_args(y, y_l, mean, std_, n_params, out, out_l, ncol, nz, "standard_denormalize"))
-        return st;
-    if (ncol == 0) return FV3_OK;
-    const dim3 grid((unsigned)((ncol + kScaleBlock - 1) / kScaleBlock), (unsigned)nz);
-    hipLaunchKernelGGL(standard_denormalize_kernel, grid, dim3(kScaleBlock), 0, (hipStream_t)stream, y, y_l, mean,
-                       std_, n_params == nz ? 1 : 0, out, out_l, ncol);
-    FV3_LAUNCH_CHECK();
-    return FV3_OK;
+    return fv3::denormalize_impl<float>(y, y_l, mean, std_, n_params, out, out_l, ncol, nz, stream);
+}
+
+extern "C" int fv3_standard_denormalize_f64(const double* y, fv3_layout y_l, const double* mean, const double* std_,
+                                            int n_params, double* out, fv3_layout out_l, int64_t ncol, int nz,
+                                            void* stream)
+{
+    return fv3::denormalize_impl<double>(y, y_l, mean, std_, n_params, out, out_l, ncol, nz, stream);
 }

@@ -96,6 +96,8 @@ class _Register:
         return return_name
 
     def load(self, path: str):
+        from . import pytorch_predictor  # noqa: F401  registers "pytorch_predictor"
+
         name_file = os.path.join(path, _NAME_PATH)
         if not os.path.exists(name_file):
             warnings.warn(f"Model type is not located at {name_file}. Trying all known models one-by-one.",

@@ -347,6 +347,14 @@ int fv3_standard_normalize(const void* x, int x_f64, fv3_layout x_l, const doubl
 int fv3_standard_denormalize(const float* y, fv3_layout y_l, const double* mean, const double* std_,
                              int n_params, double* out, fv3_layout out_l, int64_t ncol, int nz,
                              void* stream);
+/* The same with a float64 result (StandardScaler.normalize's own float64 output,
+ * scaler.py:65-68) / from a float64 input (StandardScaler.denormalize, :70-73). */
+int fv3_standard_normalize_f64(const void* x, int x_f64, fv3_layout x_l, const double* mean,
+                               const double* std_, int n_params, double* out, fv3_layout out_l,
+                               int64_t ncol, int nz, void* stream);
+int fv3_standard_denormalize_f64(const double* y, fv3_layout y_l, const double* mean, const double* std_,
+                                 int n_params, double* out, fv3_layout out_l, int64_t ncol, int nz,
+                                 void* stream);
 
 /* ---- ML stepper epilogue: limiter + diagnostics + apply (config #4) --------------
  * One pass per column over everything the prognostic loop does with a (dQ1, dQ2)
