@@ -8,28 +8,30 @@
 //
 // Arithmetic: every f32 operand x is split into bf16 hi = rne(x) and lo = rne(x - hi),
 // and a product a*b is taken as hi_a*hi_b + lo_a*hi_b + hi_a*lo_b on
-// v_mfma_f32_32x32x16_bf16 (f32 accumulate).  That keeps ~16 mantissa bits of each
-// operand: measured 8e-6 rel on the 2x256 DenseModel and 9e-6 on the Zhao-Carr emulator
-// against the float64 graph (plain bf16: 4.7e-3, outside BASELINE config #5's 1e-3).
-// Three bf16 MFMAs cost 48 cycles per 16x32x32 block against 512 for exact f32
-// (v_mfma_f32_32x32x2_f32), i.e. ~5.3x the f32 MFMA rate.
+// v_mfma_f32_16x16x32_bf16 (f32 accumulate).  That keeps ~16 mantissa bits of each
+// operand: ~1e-5 rel against the float64 graph on the 2x256 DenseModel and the Zhao-Carr
+// emulator (plain bf16: 4.7e-3, outside BASELINE config #5's 1e-3).  Three bf16 MFMAs
+// cost 48 cycles per 16x16x32 block against 256 for exact f32, ~5.3x the f32 MFMA rate.
 //
-// Mapping (one 256-thread block per CU, 1 wave per SIMD, persistent over column tiles):
-//  * a block tile is 128 columns; wave w owns columns [32w, 32w+32) for the WHOLE network,
-//    so activations never leave registers: the 32x32 accumulator of a layer (units on
-//    the 16 registers, column on the lane) is, after bias + relu + split, exactly the
-//    B operand of the next layer's 32x32x16 MFMA (k order permuted; the packed weights
-//    carry the permutation);
-//  * weights stream through LDS in 32 KiB chunks (2 k-steps x all unit tiles x hi/lo,
-//    MFMA A-fragment order, one ds_read_b128 per fragment), double-buffered: the chunk
-//    after next is loaded into registers while the current one runs (one barrier per
-//    chunk); the 4 waves share every chunk, so L2 traffic is 1/128 of a weight per column;
-//  * layer-1 inputs are loaded straight into the B-fragment layout (lane = column,
-//    8 consecutive levels per lane: 128-B coalesced rows), two chunks ahead, then
-//    log / normalised / split in registers: no LDS staging of inputs at all;
-//  * the output layer runs in passes of HT 32-row tiles over the packed output rows;
-//    the epilogue (bias, denorm, limits, mask, residual) reads per-row constants and
-//    destination addresses from LDS.
+// Mapping (one 512-thread block per CU, 2 waves per SIMD, persistent over column tiles):
+//  * a block tile is 128 columns; wave w owns columns [16w, 16w+16) for the WHOLE network,
+//    so activations never leave registers: a layer's 16x16 accumulators (units 4q..4q+3 of
+//    each 16-unit tile on lane quarter q, column on lane & 15) are, after bias + relu +
+//    split, exactly the B operands of the next layer's 16x16x32 MFMAs (two unit tiles per
+//    32-deep k-step, k order permuted; the packed weights carry the permutation);
+//  * two waves per SIMD: one wave's epilogue and LDS reads run while the other's MFMAs
+//    do; the per-wave state that allows it (<= 256 registers) is what sets 16 columns;
+//  * weights stream through LDS in chunks of one 32-deep k-step x all unit tiles x hi/lo
+//    (32 KiB at width 256, A-fragment order, one ds_read_b128 per fragment), double-
+//    buffered: the chunk after next is loaded into registers while the current one runs
+//    (one barrier per chunk); the 8 waves share every chunk, so L2 traffic is 1/128 of a
+//    weight per column;
+//  * layer-1 inputs are loaded straight into the B-fragment layout (lane = column, 8
+//    consecutive levels per lane quarter), two chunks ahead, then log / normalised / split
+//    in registers: no LDS staging of inputs;
+//  * the output layer runs in chunks of two 16-row tiles (every output variable is padded
+//    to 16 rows, so a tile has ONE destination); the epilogue of a chunk (bias, denorm,
+//    limits, mask, residual) runs after the next chunk's MFMAs are issued.
 // Roofline: bf16 MFMA (3 products per f32 product) — see DESIGN.md §3.5.
 #include <algorithm>
 #include <cmath>
@@ -45,21 +47,21 @@
 #include "dense_model.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float b3f16 __attribute__((ext_vector_type(16)));
 typedef float b3f4 __attribute__((ext_vector_type(4)));
 
 namespace fv3 {
 
-constexpr int kB3Groups = 128;    // 8-feature input groups (<= 1024 padded input features)
-constexpr int kB3Cols = 128;      // columns per block tile: 4 waves x 32
-constexpr int kB3OutGroups = 64;  // 8-row output groups (<= 512 padded output rows)
+constexpr int kB3Groups = 128;   // 8-feature input groups (<= 1024 padded input features)
+constexpr int kB3Cols = 128;     // columns per block tile: 8 waves x 16
+constexpr int kB3OutTiles = 32;  // 16-row output tiles (<= 512 padded output rows)
+constexpr int kB3Threads = 512;
 
 struct B3Pack {
     void* dbuf = nullptr;
-    int ht = 0, hp = 0, kp1 = 0, n1 = 0, nhx = 0, npass = 0, n_otile = 0, kop = 0, nch = 0;
+    int hu = 0, hp = 0, kp1 = 0, n1 = 0, nhx = 0, n_oc = 0, kop = 0, nch = 0;
     int nconst = 0, wbytes = 0, any_log = 0;
     std::vector<int> gmeta;  // per 8-feature group: var | zstart << 4 | nvalid << 24
-    std::vector<int> ogrp;   // per 8-row output group: var | z0 << 8 | nrow << 24 (var 255: padding)
+    std::vector<int> otile;  // per 16-row output tile: var | z0 << 8 | nrow << 24 (var 255: padding)
     size_t consts_off = 0;
 };
 
@@ -76,13 +78,13 @@ struct B3Args {
     const void* wstream;  // [nch][CB]: the packed weight chunks of one column tile
     const float* consts;  // [kp1] mean | [kp1] 1/(sigma+eps) | [nh][HP] bias | [6][kop]
     int wbytes;
-    int nch, n1, nhx, npass, n_otile, kp1, kop, nconst, any_log;
+    int nch, n1, nhx, n_oc, kp1, kop, nconst, any_log;
     int64_t ncol, ncol_blk, ntiles;
     B3InVar in[kMaxVars];
     int gmeta[kB3Groups];
-    // output rows in 8-row groups, each of ONE variable (every variable is padded to a
-    // multiple of 8 rows): group G = var | z0 << 8 | nrow << 24 (var 255: padding)
-    int ogrp[kB3OutGroups];
+    // output rows in 16-row tiles, each of ONE variable (every variable is padded to a
+    // multiple of 16 rows): tile T = var | z0 << 8 | nrow << 24 (var 255: padding)
+    int otile[kB3OutTiles];
     float* out_ptr[kMaxVars];
     int64_t out_ld[kMaxVars], out_bs[kMaxVars];
     const float* res_ptr[kMaxVars];
@@ -122,22 +124,33 @@ __device__ __forceinline__ void split8(const float (&y)[8], bf16x8& hi, bf16x8& 
     }
 }
 
-__device__ __forceinline__ b3f16 mma3(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl,
-                                      b3f16 c)
+__device__ __forceinline__ b3f4 mma3(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl, b3f4 c)
 {
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
     return c;
 }
 
-template <int HT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void dense_b3_kernel(B3Args pa)
+// value of lane quarter q from 4 wave-uniform candidates
+template <typename T>
+__device__ __forceinline__ T sel4(int q, T a0, T a1, T a2, T a3)
+{
+    const T lo = (q & 1) ? a1 : a0;
+    const T hi = (q & 1) ? a3 : a2;
+    return (q & 2) ? hi : lo;
+}
+
+template <int HU>
+__global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2))) void dense_b3_kernel(B3Args pa)
 {
     (void)pa;
     KB3& p = *(KB3*)(__builtin_amdgcn_kernarg_segment_ptr());
-    constexpr int HP = 32 * HT;
-    constexpr int CB = 4096 * HT;  // chunk: 2 k-steps x HT tiles x {hi, lo} x 64 lanes x 16 B
+    constexpr int HP = 16 * HU;      // padded units
+    constexpr int KS = HU / 2;       // 32-deep k-steps over HP units
+    constexpr int CB = 2048 * HU;    // chunk: HU A fragments x {hi, lo} x 64 lanes x 16 B
+    constexpr int NST = CB / (16 * kB3Threads);  // 16-B loads per thread per chunk
+    static_assert(HU % 4 == 0 && NST >= 1, "unit tiles per layer must be a multiple of 4");
     extern __shared__ __attribute__((aligned(16))) b3f4 lds3[];
     char* ring = reinterpret_cast<char*>(lds3);
     float* s_mean = reinterpret_cast<float*>(ring + 2 * CB);
@@ -149,256 +162,213 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int hh = lane >> 5;  // lane half: k offset 8*hh inside a 16-deep k-step
-    const int cl = lane & 31;  // column of this lane inside the wave's 32
+    const int hq = lane >> 4;  // lane quarter: k offset 8*hq of a k-step, rows 4*hq of a tile
+    const int cl = lane & 15;  // column of this lane inside the wave's 16
 
-    // ---- constants and per-row destinations to LDS ----
-    for (int i = tid; i < p.nconst; i += 256) s_mean[i] = p.consts[i];
+    for (int i = tid; i < p.nconst; i += kB3Threads) s_mean[i] = p.consts[i];
 
     // ---- weight stream: LDS ring of 2 chunks, the chunk after next in registers ----
     const Rsrc3 rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.wstream), 0, p.wbytes, 0x00020000);
-    b3f4 stg[HT];
+    b3f4 stg[NST];
     auto load_stage = [&](int j) {
 #pragma unroll
-        for (int q = 0; q < HT; ++q)
-            stg[q] = __builtin_bit_cast(b3f4, __builtin_amdgcn_raw_buffer_load_b128(rw, tid * 16, j * CB + q * 4096, 0));
+        for (int q = 0; q < NST; ++q)
+            stg[q] = __builtin_bit_cast(
+                b3f4, __builtin_amdgcn_raw_buffer_load_b128(rw, tid * 16, j * CB + q * 16 * kB3Threads, 0));
     };
     auto write_stage = [&](int slot) {
 #pragma unroll
-        for (int q = 0; q < HT; ++q) *reinterpret_cast<b3f4*>(ring + slot * CB + q * 4096 + tid * 16) = stg[q];
+        for (int q = 0; q < NST; ++q)
+            *reinterpret_cast<b3f4*>(ring + slot * CB + q * 16 * kB3Threads + tid * 16) = stg[q];
     };
-    int slot = 0;                             // ring slot of the chunk computed next
-    int jn2 = p.nch > 2 ? 2 : 2 % p.nch;      // stream index of the chunk after next
+    int slot = 0;                         // ring slot of the chunk computed next
+    int jn2 = p.nch > 2 ? 2 : 2 % p.nch;  // stream index of the chunk after next
     load_stage(0);
     write_stage(0);
     load_stage(p.nch > 1 ? 1 : 0);
 
-    b3f16 acc[HT];
+    b3f4 acc[HU];
     auto zero_acc = [&]() {
 #pragma unroll
-        for (int t = 0; t < HT; ++t)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+        for (int t = 0; t < HU; ++t) acc[t] = b3f4{0.0f, 0.0f, 0.0f, 0.0f};
     };
-    // one chunk: 2 k-steps x (tiles < nact) x 3 MFMAs, A fragments from the ring; the
-    // fragments of the next tile are read while this tile's MFMAs run (1 wave per SIMD:
-    // nothing else hides the LDS latency)
-    auto mma_chunk = [&](int sl, const bf16x8 (&bh)[2], const bf16x8 (&bl)[2], int nact) {
-        const char* base = ring + sl * CB + lane * 16;
-        bf16x8 fa[2][2];  // [buffer][hi, lo]
-        fa[0][0] = *reinterpret_cast<const bf16x8*>(base);
-        fa[0][1] = *reinterpret_cast<const bf16x8*>(base + 1024);
-        sfor<2 * HT>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;  // i = s * HT + t
-            constexpr int s = i / HT, t = i % HT;
-            if constexpr (i + 1 < 2 * HT) {
-                fa[(i + 1) & 1][0] = *reinterpret_cast<const bf16x8*>(base + (i + 1) * 2048);
-                fa[(i + 1) & 1][1] = *reinterpret_cast<const bf16x8*>(base + (i + 1) * 2048 + 1024);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            if (t < nact) acc[t] = mma3(fa[i & 1][0], fa[i & 1][1], bh[s], bl[s], acc[t]);
-            __builtin_amdgcn_sched_barrier(0);
+    // A fragment i of the chunk in slot sl: hi at i*2048, lo at i*2048 + 1024
+    auto frag = [&](int sl, int i, bf16x8 (&f)[2]) {
+        const char* a = ring + sl * CB + i * 2048 + lane * 16;
+        f[0] = *reinterpret_cast<const bf16x8*>(a);
+        f[1] = *reinterpret_cast<const bf16x8*>(a + 1024);
+    };
+    // fragment i -> (accumulator, B operand) by MAP; fragments are read two ahead
+    auto mma_chunk = [&](int sl, auto map) {
+        bf16x8 fa[3][2];
+        frag(sl, 0, fa[0]);
+        frag(sl, 1, fa[1]);
+        sfor<HU>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            if constexpr (i + 2 < HU) frag(sl, i + 2, fa[(i + 2) % 3]);
+            map(ic, fa[i % 3]);
         });
     };
-    auto step = [&](const bf16x8 (&bh)[2], const bf16x8 (&bl)[2], int nact) {
-#ifndef FV3_B3_EXP_NOSTAGE  // experiment switches (tools/b3_ab.sh): timing only, results invalid
+    auto stage_next = [&]() {
         write_stage(slot ^ 1);  // chunk +1 (its slot held chunk -1, released by the last barrier)
         load_stage(jn2);        // chunk +2
-#endif
-#ifndef FV3_B3_EXP_NOMFMA
-        mma_chunk(slot, bh, bl, nact);
-#endif
-#ifndef FV3_B3_EXP_NOBARRIER
+    };
+    auto advance = [&]() {
         b3_barrier();
-#endif
         slot ^= 1;
         jn2 = jn2 + 1 == p.nch ? 0 : jn2 + 1;
+    };
+    // layer chunk: unit tile t accumulates A_t x B (one 32-deep k-step)
+    auto step_layer = [&](const bf16x8& bh, const bf16x8& bl) {
+        stage_next();
+        mma_chunk(slot, [&](auto ic, const bf16x8 (&f)[2]) {
+            constexpr int t = decltype(ic)::value;
+            acc[t] = mma3(f[0], f[1], bh, bl, acc[t]);
+        });
+        advance();
     };
 
     // ---- layer-1 inputs: B fragments straight from the [level][column] arrays ----
     unsigned lblk = 0, lii = 0;  // column address of the tile being loaded (block, index in block)
     bool lvalid = false;
     auto set_load_tile = [&](int64_t tile) {
-        const int64_t c = tile * kB3Cols + wave * 32 + cl;
+        const int64_t c = tile * kB3Cols + wave * 16 + cl;
         lvalid = c < p.ncol;
         const int64_t cc = lvalid ? c : 0;
         const int64_t b = p.ncol_blk < p.ncol ? cc / p.ncol_blk : 0;
         lblk = (unsigned)b;
         lii = (unsigned)(cc - b * p.ncol_blk);
     };
-    auto load_in = [&](float (&raw)[16], int c) {  // chunk c: groups 4c + 2s + hh, 8 levels each
-        sfor<2>([&](auto sc) {
-            constexpr int s = decltype(sc)::value;
-            const int m0 = p.gmeta[4 * c + 2 * s], m1 = p.gmeta[4 * c + 2 * s + 1];
-            const int v0 = m0 & 15, v1 = m1 & 15;
-            const float* b0 = p.in[v0].ptr + (int64_t)((m0 >> 4) & 0xfffff) * p.in[v0].ld;
-            const float* b1 = p.in[v1].ptr + (int64_t)((m1 >> 4) & 0xfffff) * p.in[v1].ld;
-            const int64_t ld = hh ? p.in[v1].ld : p.in[v0].ld;
-            const int64_t bs = hh ? p.in[v1].bs : p.in[v0].bs;
-            const int nv = lvalid ? ((hh ? m1 : m0) >> 24) : 0;
-            const float* ptr = (hh ? b1 : b0) + (int64_t)lblk * bs + lii;
+    auto load_in = [&](float (&raw)[8], int c) {  // chunk c: group 4c + hq, 8 levels
+        const int m0 = p.gmeta[4 * c], m1 = p.gmeta[4 * c + 1], m2 = p.gmeta[4 * c + 2], m3 = p.gmeta[4 * c + 3];
+        const int m = sel4(hq, m0, m1, m2, m3);
+        auto base = [&](int mg) {
+            const int v = mg & 15;
+            return p.in[v].ptr + (int64_t)((mg >> 4) & 0xfffff) * p.in[v].ld;
+        };
+        const float* b = sel4(hq, base(m0), base(m1), base(m2), base(m3));
+        const int64_t ld = sel4(hq, p.in[m0 & 15].ld, p.in[m1 & 15].ld, p.in[m2 & 15].ld, p.in[m3 & 15].ld);
+        const int64_t bs = sel4(hq, p.in[m0 & 15].bs, p.in[m1 & 15].bs, p.in[m2 & 15].bs, p.in[m3 & 15].bs);
+        const int nv = lvalid ? (m >> 24) : 0;
+        const float* ptr = b + (int64_t)lblk * bs + lii;
 #pragma unroll
-            for (int j = 0; j < 8; ++j)  // read once: keep them from evicting the weight stream in L2
-#ifdef FV3_B3_EXP_NOINPUT
-                raw[8 * s + j] = (float)(j < nv);
-#else
-                raw[8 * s + j] = j < nv ? __builtin_nontemporal_load(ptr + j * ld) : 0.0f;
-#endif
-        });
+        for (int j = 0; j < 8; ++j)  // read once: keep them from evicting the weight stream in L2
+            raw[j] = j < nv ? __builtin_nontemporal_load(ptr + j * ld) : 0.0f;
     };
-    auto stage_in = [&](const float (&raw)[16], int c, bf16x8 (&bh)[2], bf16x8 (&bl)[2]) {
-        sfor<2>([&](auto sc) {
-            constexpr int s = decltype(sc)::value;
-            const int f0 = 32 * c + 16 * s + 8 * hh;
-            const b3f4 mu0 = *reinterpret_cast<const b3f4*>(s_mean + f0);
-            const b3f4 mu1 = *reinterpret_cast<const b3f4*>(s_mean + f0 + 4);
-            const b3f4 rs0 = *reinterpret_cast<const b3f4*>(s_rs + f0);
-            const b3f4 rs1 = *reinterpret_cast<const b3f4*>(s_rs + f0 + 4);
-            float leps = 0.0f;
-            if (p.any_log) {
-                const float l0 = p.in[p.gmeta[4 * c + 2 * s] & 15].leps;
-                const float l1 = p.in[p.gmeta[4 * c + 2 * s + 1] & 15].leps;
-                leps = hh ? l1 : l0;
-            }
+    auto stage_in = [&](const float (&raw)[8], int c, bf16x8& bh, bf16x8& bl) {
+        const int f0 = 32 * c + 8 * hq;
+        const b3f4 mu0 = *reinterpret_cast<const b3f4*>(s_mean + f0);
+        const b3f4 mu1 = *reinterpret_cast<const b3f4*>(s_mean + f0 + 4);
+        const b3f4 rs0 = *reinterpret_cast<const b3f4*>(s_rs + f0);
+        const b3f4 rs1 = *reinterpret_cast<const b3f4*>(s_rs + f0 + 4);
+        float leps = 0.0f;
+        if (p.any_log)
+            leps = sel4(hq, p.in[p.gmeta[4 * c] & 15].leps, p.in[p.gmeta[4 * c + 1] & 15].leps,
+                        p.in[p.gmeta[4 * c + 2] & 15].leps, p.in[p.gmeta[4 * c + 3] & 15].leps);
+        float y[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float x = raw[j];
+            if (leps > 0.0f) x = b3_log(x, leps);  // LogTransform.forward (transforms.py:123-124)
+            y[j] = (x - (j < 4 ? mu0[j] : mu1[j - 4])) * (j < 4 ? rs0[j] : rs1[j - 4]);
+        }
+        split8(y, bh, bl);
+    };
+
+    // ---- activations: B fragments of the next layer (k-step c, element j of quarter q is
+    //      unit 32c + 16(j>>2) + 4q + (j&3): registers of unit tiles 2c and 2c+1) ----
+    bf16x8 Bh[KS], Bl[KS];
+    auto hidden_epi = [&](int l) {  // relu(acc + bias_l) -> Bh/Bl
+        sfor<KS>([&](auto cc) {
+            constexpr int c = decltype(cc)::value;
+            const b3f4 b0 = *reinterpret_cast<const b3f4*>(s_bias + l * HP + 32 * c + 4 * hq);
+            const b3f4 b1 = *reinterpret_cast<const b3f4*>(s_bias + l * HP + 32 * c + 16 + 4 * hq);
             float y[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                float x = raw[8 * s + j];
-                if (leps > 0.0f) x = b3_log(x, leps);  // LogTransform.forward (transforms.py:123-124)
-                y[j] = (x - (j < 4 ? mu0[j] : mu1[j - 4])) * (j < 4 ? rs0[j] : rs1[j - 4]);
+            for (int r = 0; r < 4; ++r) {
+                const float v0 = acc[2 * c][r] + b0[r];
+                const float v1 = acc[2 * c + 1][r] + b1[r];
+                y[r] = v0 > 0.0f ? v0 : 0.0f;
+                y[4 + r] = v1 > 0.0f ? v1 : 0.0f;
             }
-            split8(y, bh[s], bl[s]);
+            split8(y, Bh[c], Bl[c]);
+        });
+    };
+    // output chunk: fragment i = 2q + ts accumulates tile ts of the chunk over k-step q
+    auto step_out = [&]() {
+        mma_chunk(slot, [&](auto ic, const bf16x8 (&f)[2]) {
+            constexpr int i = decltype(ic)::value;
+            acc[i & 1] = mma3(f[0], f[1], Bh[i >> 1], Bl[i >> 1], acc[i & 1]);
         });
     };
 
-    // ---- activations: B fragments of the next layer (unit 32t + 16s + 8(j>>2) + (j&3) + 4hh) ----
-    bf16x8 Bh[HT][2], Bl[HT][2];
-    auto hidden_epi = [&](int l) {  // relu(acc + bias_l) -> Bh/Bl
-#ifdef FV3_B3_EXP_NOHIDEPI  // experiment: plain cast, no bias/relu/lo split, results invalid
-        sfor<HT>([&](auto tc) {
-            constexpr int t = decltype(tc)::value;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                Bh[t][0][j] = (__bf16)acc[t][j];
-                Bh[t][1][j] = (__bf16)acc[t][8 + j];
-                Bl[t][0][j] = Bh[t][0][j];
-                Bl[t][1][j] = Bh[t][1][j];
-            }
-        });
-        return;
-#endif
-        sfor<HT>([&](auto tc) {
-            constexpr int t = decltype(tc)::value;
-            sfor<2>([&](auto sc) {
-                constexpr int s = decltype(sc)::value;
-                float y[8];
-#pragma unroll
-                for (int g2 = 0; g2 < 2; ++g2) {
-                    const int g = 2 * s + g2;  // register group: registers 4g .. 4g+3
-                    const b3f4 b = *reinterpret_cast<const b3f4*>(s_bias + l * HP + 32 * t + 8 * g + 4 * hh);
-#pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) {
-                        const float v = acc[t][4 * g + rr] + b[rr];
-                        y[4 * g2 + rr] = v > 0.0f ? v : 0.0f;
-                    }
-                }
-                split8(y, Bh[t][s], Bl[t][s]);
-            });
-        });
-    };
     // ---- output epilogue ----------------------------------------------------------
-    // Output tile T's accumulator register 4g + rr of lane (hh, cl) is row 32T + 8g + 4hh + rr
-    // of column cl: each 8-row group g belongs to ONE output variable (ogrp), so its
-    // destination is one buffer resource plus a 32-bit element offset per lane
-    // (the host checks every span < 2^29 elements); lanes that must not store (padding
-    // rows, columns past the end) get an offset past the range, so no branch per row.
-    // Residual inputs (Difference.backward: after = before + to) are read one tile ahead
-    // of their use, so the loads of tile t+1 travel while tile t is finished and stored.
+    // Output tile T's accumulator register r of lane (q, cl) is row 16T + 4q + r of column
+    // cl; a tile belongs to ONE output variable (otile), so its destination is one buffer
+    // resource plus a 32-bit element offset per lane (the host checks every span < 2^29
+    // elements); lanes that must not store (padding rows, columns past the end) get an
+    // offset past the range, so no branch per row.  Residual inputs (Difference.backward:
+    // after = before + to) are loaded one chunk ahead of their use.
     unsigned oblk = 0, oii = 0;
     bool ovalid = false;
-    float resv[2][16];  // residual values of the tile being finished / the next one
-    auto res_load = [&](int T, float (&r)[16]) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int e = p.ogrp[4 * T + g];
-            const int v = e & 0xff, z0 = (e >> 8) & 0xffff, nrow = e >> 24;
-            if (v < kMaxVars && p.res_ptr[v]) {  // uniform
-                const Rsrc3 rr_ = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.res_ptr[v]), 0, 0x7ffffffc,
-                                                                    0x00020000);
-                const unsigned rb = oblk * (unsigned)p.res_bs[v] + oii;
-                const unsigned rld = (unsigned)p.res_ld[v];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int row = 4 * hh + q;
-                    const unsigned off = (ovalid && row < nrow) ? (rb + (unsigned)(z0 + row) * rld) * 4u : 0x80000000u;
-                    r[4 * g + q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr_, (int)off, 0, 0));
-                }
-            } else {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) r[4 * g + q] = 0.0f;
-            }
-        }
-    };
-    auto out_tile = [&](const b3f16& a, int T, const float (&r)[16]) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int e = p.ogrp[4 * T + g];
-            const int v = e & 0xff, z0 = (e >> 8) & 0xffff, nrow = e >> 24;
-            if (v >= kMaxVars) continue;  // padding group (uniform)
-            int R0 = 32 * T + 8 * g + 4 * hh;
-            asm volatile("" : "+v"(R0));  // keep the constant reads next to their use
-            const b3f4 bo = *reinterpret_cast<const b3f4*>(s_oc + R0);
-            const b3f4 sg = *reinterpret_cast<const b3f4*>(s_oc + kop + R0);
-            const b3f4 mu = *reinterpret_cast<const b3f4*>(s_oc + 2 * kop + R0);
-            const b3f4 lo = *reinterpret_cast<const b3f4*>(s_oc + 3 * kop + R0);
-            const b3f4 hi = *reinterpret_cast<const b3f4*>(s_oc + 4 * kop + R0);
-            const b3f4 mk = *reinterpret_cast<const b3f4*>(s_oc + 5 * kop + R0);
-            const Rsrc3 ro = __builtin_amdgcn_make_buffer_rsrc(p.out_ptr[v], 0, 0x7ffffffc, 0x00020000);
-            const unsigned ob = oblk * (unsigned)p.out_bs[v] + oii;
-            const unsigned old_ = (unsigned)p.out_ld[v];
-            const bool has_res = p.res_ptr[v] != nullptr;  // uniform
+    auto res_load = [&](int T, float (&r)[4]) {
+        const int e = p.otile[T];
+        const int v = e & 0xff, z0 = (e >> 8) & 0xffff, nrow = e >> 24;
+        if (v < kMaxVars && p.res_ptr[v]) {  // uniform
+            const Rsrc3 rr_ = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.res_ptr[v]), 0, 0x7ffffffc,
+                                                                0x00020000);
+            const unsigned rb = oblk * (unsigned)p.res_bs[v] + oii;
+            const unsigned rld = (unsigned)p.res_ld[v];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int row = 4 * hh + q;
-                float y = a[4 * g + q] + bo[q];
-                y = y * sg[q];
-                y = y + mu[q];
-                if (y < lo[q]) y = lo[q];
-                if (y >= hi[q]) y = hi[q];
-                y = y * mk[q];
-                if (has_res) y = r[4 * g + q] + y;
-                const unsigned off = (ovalid && row < nrow) ? (ob + (unsigned)(z0 + row) * old_) * 4u : 0x80000000u;
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, (int)off, 0, 0);
+                const int row = 4 * hq + q;
+                const unsigned off = (ovalid && row < nrow) ? (rb + (unsigned)(z0 + row) * rld) * 4u : 0x80000000u;
+                r[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr_, (int)off, 0, 0));
             }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) r[q] = 0.0f;
         }
     };
-    auto out_epi = [&](int pp, int nact) {
-#ifdef FV3_B3_EXP_NOOUTEPI  // experiment: no output epilogue (one store per tile), results invalid
-        float sink = 0.0f;
-        sfor<HT>([&](auto tc) {
+    auto out_tile = [&](const b3f4& a, int T, const float (&r)[4]) {
+        const int e = p.otile[T];
+        const int v = e & 0xff, z0 = (e >> 8) & 0xffff, nrow = e >> 24;
+        if (v >= kMaxVars) return;  // padding tile (uniform)
+        int R0 = 16 * T + 4 * hq;
+        asm volatile("" : "+v"(R0));  // keep the constant reads next to their use
+        const b3f4 bo = *reinterpret_cast<const b3f4*>(s_oc + R0);
+        const b3f4 sg = *reinterpret_cast<const b3f4*>(s_oc + kop + R0);
+        const b3f4 mu = *reinterpret_cast<const b3f4*>(s_oc + 2 * kop + R0);
+        const b3f4 lo = *reinterpret_cast<const b3f4*>(s_oc + 3 * kop + R0);
+        const b3f4 hi = *reinterpret_cast<const b3f4*>(s_oc + 4 * kop + R0);
+        const b3f4 mk = *reinterpret_cast<const b3f4*>(s_oc + 5 * kop + R0);
+        const Rsrc3 ro = __builtin_amdgcn_make_buffer_rsrc(p.out_ptr[v], 0, 0x7ffffffc, 0x00020000);
+        const unsigned ob = oblk * (unsigned)p.out_bs[v] + oii;
+        const unsigned old_ = (unsigned)p.out_ld[v];
+        const bool has_res = p.res_ptr[v] != nullptr;  // uniform
 #pragma unroll
-            for (int r = 0; r < 16; ++r) sink += acc[decltype(tc)::value][r];
-        });
-        if (sink == 1234.5f) p.out_ptr[0][0] = sink;
-        return;
-#endif
-        sfor<HT>([&](auto tc) {
-            constexpr int t = decltype(tc)::value;
-            if (t < nact) {
-                if (t + 1 < nact) res_load(pp * HT + t + 1, resv[(t + 1) & 1]);
-                out_tile(acc[t], pp * HT + t, resv[t & 1]);
-            }
-        });
+        for (int q = 0; q < 4; ++q) {
+            const int row = 4 * hq + q;
+            float y = a[q] + bo[q];
+            y = y * sg[q];
+            y = y + mu[q];
+            if (y < lo[q]) y = lo[q];
+            if (y >= hi[q]) y = hi[q];
+            y = y * mk[q];
+            if (has_res) y = r[q] + y;
+            const unsigned off = (ovalid && row < nrow) ? (ob + (unsigned)(z0 + row) * old_) * 4u : 0x80000000u;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, (int)off, 0, 0);
+        }
     };
 
-    float rawA[16], rawB[16];
+    float rawA[8], rawB[8];
     int64_t tile = blockIdx.x;
     set_load_tile(tile);
     if (tile < p.ntiles) {
         load_in(rawA, 0);
         if (p.n1 > 1) load_in(rawB, 1);
     }
-    b3_barrier();  // constants, row table and chunk 0 visible
+    b3_barrier();  // constants and chunk 0 visible
 
     for (; tile < p.ntiles; tile += gridDim.x) {
         oblk = lblk;
@@ -407,43 +377,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         // ---- layer 1 over the padded input features ----
         zero_acc();
         for (int c = 0; c < p.n1; c += 2) {
-            bf16x8 xh[2], xl[2];
+            bf16x8 xh, xl;
             stage_in(rawA, c, xh, xl);
             if (c + 2 < p.n1) load_in(rawA, c + 2);
-            step(xh, xl, HT);
+            step_layer(xh, xl);
             if (c + 1 < p.n1) {
                 stage_in(rawB, c + 1, xh, xl);
                 if (c + 3 < p.n1) load_in(rawB, c + 3);
-                step(xh, xl, HT);
+                step_layer(xh, xl);
             }
         }
         hidden_epi(0);
         // ---- further hidden layers ----
         for (int l = 0; l < p.nhx; ++l) {
             zero_acc();
-            sfor<HT>([&](auto cc) {
+            sfor<KS>([&](auto cc) {
                 constexpr int c = decltype(cc)::value;
-                step(Bh[c], Bl[c], HT);
+                step_layer(Bh[c], Bl[c]);
             });
             hidden_epi(l + 1);
         }
-        // ---- output layer in passes of HT tiles; the next tile's inputs start loading ----
+        // ---- output layer, two 16-row tiles per chunk; the next tile's inputs start loading ----
         const int64_t nt = tile + gridDim.x;
         if (nt < p.ntiles) {
             set_load_tile(nt);
             load_in(rawA, 0);
             if (p.n1 > 1) load_in(rawB, 1);
         }
-        for (int pp = 0; pp < p.npass; ++pp) {
-            zero_acc();
-            const int nact = min(HT, p.n_otile - pp * HT);
-            res_load(pp * HT, resv[0]);  // lands while the pass runs its MFMAs
-            sfor<HT>([&](auto cc) {
-                constexpr int c = decltype(cc)::value;
-                step(Bh[c], Bl[c], nact);
-            });
-            out_epi(pp, nact);
+        b3f4 accP[2];
+        float resN[2][4], resP[2][4];
+        for (int oc = 0; oc < p.n_oc; ++oc) {
+            res_load(2 * oc, resN[0]);  // lands while this chunk and the next run their MFMAs
+            res_load(2 * oc + 1, resN[1]);
+            acc[0] = acc[1] = b3f4{0.0f, 0.0f, 0.0f, 0.0f};
+            stage_next();
+            step_out();
+            if (oc > 0) {  // finish the previous chunk while these MFMAs run
+                out_tile(accP[0], 2 * oc - 2, resP[0]);
+                out_tile(accP[1], 2 * oc - 1, resP[1]);
+            }
+            advance();
+            accP[0] = acc[0];
+            accP[1] = acc[1];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                resP[0][q] = resN[0][q];
+                resP[1][q] = resN[1][q];
+            }
         }
+        out_tile(accP[0], 2 * p.n_oc - 2, resP[0]);
+        out_tile(accP[1], 2 * p.n_oc - 1, resP[1]);
     }
 }
 
@@ -474,9 +457,9 @@ int b3_pack(fv3_dense_model* m, const fv3_dense_desc* d)
     auto b = new B3Pack();
     std::unique_ptr<B3Pack> guard(b);
     const int W = d->width;
-    b->ht = W <= 64 ? 2 : (W <= 128 ? 4 : 8);
-    b->hp = 32 * b->ht;
-    const int HT = b->ht, HP = b->hp;
+    b->hu = W <= 64 ? 4 : (W <= 128 ? 8 : 16);
+    b->hp = 16 * b->hu;
+    const int HU = b->hu, KS = HU / 2;
 
     // input feature groups of 8 levels of one variable (chunk = 4 groups = 32 features)
     std::vector<int> fsrc;  // padded feature -> kept feature index or -1
@@ -501,94 +484,92 @@ int b3_pack(fv3_dense_model* m, const fv3_dense_desc* d)
     b->kp1 = (int)fsrc.size();
     b->n1 = b->kp1 / 32;
     b->nhx = d->n_hidden - 1;
-    // output rows: each variable padded to a multiple of 8 rows (one variable per 8-row
-    // accumulator group, see the kernel's epilogue); row R -> (variable, level) or -1
+    // output rows: each variable padded to a multiple of 16 rows (one variable per 16-row
+    // accumulator tile, see the kernel's epilogue), tiles padded to an even count (two per
+    // chunk); row R -> (variable, level) or -1
     std::vector<int> ocol_var, ocol_z, okeep;  // okeep: row's index in the model's k_out order
+    auto pad_tile = [&]() {
+        b->otile.push_back(255);
+        for (int j = 0; j < 16; ++j) {
+            ocol_var.push_back(-1);
+            ocol_z.push_back(0);
+            okeep.push_back(-1);
+        }
+    };
     for (int v = 0, o = 0; v < m->n_out; ++v) {
         const int nz = m->out_nz[v];
-        for (int z0 = 0; z0 < nz; z0 += 8) {
-            const int nrow = std::min(8, nz - z0);
-            b->ogrp.push_back(v | (z0 << 8) | (nrow << 24));
-            for (int j = 0; j < 8; ++j) {
+        FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, nz < (1 << 16), "dense_create: output levels too many for bf16x3");
+        for (int z0 = 0; z0 < nz; z0 += 16) {
+            const int nrow = std::min(16, nz - z0);
+            b->otile.push_back(v | (z0 << 8) | (nrow << 24));
+            for (int j = 0; j < 16; ++j) {
                 ocol_var.push_back(j < nrow ? v : -1);
                 ocol_z.push_back(j < nrow ? z0 + j : 0);
                 okeep.push_back(j < nrow ? o + z0 + j : -1);
             }
         }
-        FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, nz < (1 << 16), "dense_create: output levels too many for bf16x3");
         o += nz;
     }
-    while (b->ogrp.size() % 4) {
-        b->ogrp.push_back(255);
-        for (int j = 0; j < 8; ++j) {
-            ocol_var.push_back(-1);
-            ocol_z.push_back(0);
-            okeep.push_back(-1);
-        }
-    }
-    FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, (int)b->ogrp.size() <= kB3OutGroups,
+    if (b->otile.size() % 2) pad_tile();
+    FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, (int)b->otile.size() <= kB3OutTiles,
                      "dense_create: %d padded output rows are too many for bf16x3", (int)ocol_var.size());
-    b->n_otile = (int)b->ogrp.size() / 4;
-    b->kop = 32 * b->n_otile;
-    b->npass = (b->n_otile + HT - 1) / HT;
-    const int per_layer = HP / 32;
-    b->nch = b->n1 + b->nhx * per_layer + b->npass * per_layer;
-    const size_t cbe = (size_t)2048 * HT;  // bf16 elements per chunk
+    b->n_oc = (int)b->otile.size() / 2;
+    b->kop = 16 * (int)b->otile.size();
+    b->nch = b->n1 + b->nhx * KS + b->n_oc;
+    const size_t cbe = (size_t)1024 * HU;  // bf16 elements per chunk
     FV3_REQUIRE((size_t)b->nch * cbe * 2 < (1u << 31), "dense_create: model too large for the bf16x3 stream");
 
     std::vector<uint16_t> ws((size_t)b->nch * cbe, 0);
-    auto put = [&](int chunk, int s, int t, int lane, int j, float v) {
+    // fragment i of a chunk: lane (q = lane >> 4, r = lane & 15) element j is A[row r][k 8q + j]
+    auto put = [&](int chunk, int i, int lane, int j, float v) {
         const uint16_t hi = bf16_rne(v);
         const uint16_t lo = bf16_rne(v - bf16_f(hi));
-        const size_t at = (size_t)chunk * cbe + ((size_t)((s * HT + t) * 2) * 64 + lane) * 8 + j;
+        const size_t at = (size_t)chunk * cbe + ((size_t)(2 * i) * 64 + lane) * 8 + j;
         ws[at] = hi;
         ws[at + 512] = lo;
     };
-    // layer 1: natural feature order, k = 32c + 16s + 8h + j
+    // layer 1: natural feature order, k = 32c + 8q + j; fragment t = unit tile t
     const float* K0 = d->hidden_kernel[0];
     for (int c = 0; c < b->n1; ++c)
-        for (int s = 0; s < 2; ++s)
-            for (int t = 0; t < HT; ++t)
-                for (int lane = 0; lane < 64; ++lane)
-                    for (int j = 0; j < 8; ++j) {
-                        const int f = 32 * c + 16 * s + 8 * (lane >> 5) + j;
-                        const int unit = 32 * t + (lane & 31);
-                        const int src = fsrc[f];
-                        put(c, s, t, lane, j, (src >= 0 && unit < W) ? K0[(size_t)src * W + unit] : 0.0f);
-                    }
-    // hidden and output layers: k-step (c, s), element j of lane half h contracts over the
-    // previous layer's unit 32c + 16s + 8(j>>2) + (j&3) + 4h (its accumulator layout)
-    auto in_unit = [](int c, int s, int lane, int j) { return 32 * c + 16 * s + 8 * (j >> 2) + (j & 3) + 4 * (lane >> 5); };
+        for (int t = 0; t < HU; ++t)
+            for (int lane = 0; lane < 64; ++lane)
+                for (int j = 0; j < 8; ++j) {
+                    const int f = 32 * c + 8 * (lane >> 4) + j;
+                    const int unit = 16 * t + (lane & 15);
+                    const int src = fsrc[f];
+                    put(c, t, lane, j, (src >= 0 && unit < W) ? K0[(size_t)src * W + unit] : 0.0f);
+                }
+    // hidden and output layers: k-step c, element j of lane quarter q contracts over the
+    // previous layer's unit 32c + 16(j>>2) + 4q + (j&3) (its accumulator layout)
+    auto in_unit = [](int c, int lane, int j) { return 32 * c + 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3); };
     for (int li = 0; li < b->nhx; ++li) {
         const float* K = d->hidden_kernel[li + 1];
-        for (int c = 0; c < per_layer; ++c)
-            for (int s = 0; s < 2; ++s)
-                for (int t = 0; t < HT; ++t)
-                    for (int lane = 0; lane < 64; ++lane)
-                        for (int j = 0; j < 8; ++j) {
-                            const int in = in_unit(c, s, lane, j), unit = 32 * t + (lane & 31);
-                            put(b->n1 + li * per_layer + c, s, t, lane, j,
-                                (in < W && unit < W) ? K[(size_t)in * W + unit] : 0.0f);
-                        }
+        for (int c = 0; c < KS; ++c)
+            for (int t = 0; t < HU; ++t)
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int j = 0; j < 8; ++j) {
+                        const int in = in_unit(c, lane, j), unit = 16 * t + (lane & 15);
+                        put(b->n1 + li * KS + c, t, lane, j, (in < W && unit < W) ? K[(size_t)in * W + unit] : 0.0f);
+                    }
     }
-    for (int pp = 0; pp < b->npass; ++pp)
-        for (int c = 0; c < per_layer; ++c)
-            for (int s = 0; s < 2; ++s)
-                for (int t = 0; t < HT; ++t)
-                    for (int lane = 0; lane < 64; ++lane)
-                        for (int j = 0; j < 8; ++j) {
-                            const int in = in_unit(c, s, lane, j);
-                            const int R = 32 * (pp * HT + t) + (lane & 31);
-                            float v = 0.0f;
-                            if (in < W && R < b->kop && ocol_var[R] >= 0) {
-                                const int ov = ocol_var[R], oz = ocol_z[R];
-                                v = d->out_kernel[ov][(size_t)in * m->out_nz[ov] + oz];
-                            }
-                            put(b->n1 + b->nhx * per_layer + pp * per_layer + c, s, t, lane, j, v);
-                        }
+    // output chunk oc, fragment i = 2q + ts: tile 2oc + ts over k-step q
+    for (int oc = 0; oc < b->n_oc; ++oc)
+        for (int i = 0; i < HU; ++i)
+            for (int lane = 0; lane < 64; ++lane)
+                for (int j = 0; j < 8; ++j) {
+                    const int q = i >> 1, ts = i & 1;
+                    const int in = in_unit(q, lane, j);
+                    const int R = 16 * (2 * oc + ts) + (lane & 15);
+                    float v = 0.0f;
+                    if (in < W && ocol_var[R] >= 0) {
+                        const int ov = ocol_var[R], oz = ocol_z[R];
+                        v = d->out_kernel[ov][(size_t)in * m->out_nz[ov] + oz];
+                    }
+                    put(b->n1 + b->nhx * KS + oc, i, lane, j, v);
+                }
 
     // constants: [kp1] mean | [kp1] 1/(sigma+eps) | [nh][HP] bias | [6][kop]
-    const int nh = 1 + b->nhx, kop = b->kop;
+    const int nh = 1 + b->nhx, kop = b->kop, HP = b->hp;
     b->nconst = 2 * b->kp1 + nh * HP + 6 * kop;
     std::vector<float> cst((size_t)b->nconst, 0.0f);
     for (int f = 0; f < b->kp1; ++f) {
@@ -675,8 +656,7 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
     a.nch = b.nch;
     a.n1 = b.n1;
     a.nhx = b.nhx;
-    a.npass = b.npass;
-    a.n_otile = b.n_otile;
+    a.n_oc = b.n_oc;
     a.kp1 = b.kp1;
     a.kop = b.kop;
     a.nconst = b.nconst;
@@ -685,7 +665,7 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
     a.ncol_blk = nb;
     a.ntiles = (ncol + kB3Cols - 1) / kB3Cols;
     for (size_t g = 0; g < b.gmeta.size(); ++g) a.gmeta[g] = b.gmeta[g];
-    for (size_t g = 0; g < b.ogrp.size(); ++g) a.ogrp[g] = b.ogrp[g];
+    for (size_t g = 0; g < b.otile.size(); ++g) a.otile[g] = b.otile[g];
     // the epilogue addresses outputs / residual inputs with 32-bit byte offsets
     // ((block * bs + index + z * ld) * 4 < 2^31) and 32-bit block / index values
     FV3_REQUIRE(ncol < (int64_t)1 << 31, "dense_forward_ex: too many columns for bf16x3");
@@ -702,10 +682,10 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
                              "dense_forward_ex: residual input %d spans too many elements for bf16x3", r);
     }
 
-    const void* kfn = b.ht == 2 ? (const void*)dense_b3_kernel<2>
-                      : b.ht == 4 ? (const void*)dense_b3_kernel<4>
-                                  : (const void*)dense_b3_kernel<8>;
-    const size_t lds = (size_t)2 * 4096 * b.ht + (size_t)4 * b.nconst;
+    const void* kfn = b.hu == 4 ? (const void*)dense_b3_kernel<4>
+                      : b.hu == 8 ? (const void*)dense_b3_kernel<8>
+                                  : (const void*)dense_b3_kernel<16>;
+    const size_t lds = (size_t)2 * 2048 * b.hu + (size_t)4 * b.nconst;
     FV3_REQUIRE(lds <= 160 * 1024, "dense_forward_ex: model needs %zu bytes of LDS", lds);
     static std::mutex mu;
     static int n_cu = 0;
@@ -721,7 +701,7 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
         for (auto& r : resident)
             if (r.first.first == kfn && r.first.second == lds) res = r.second;
         if (!res) {
-            FV3_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&res, kfn, 256, lds));
+            FV3_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&res, kfn, kB3Threads, lds));
             res = std::max(1, res);
             resident.push_back({{kfn, lds}, res});
         }
@@ -729,7 +709,7 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
     int64_t grid = std::min<int64_t>(a.ntiles, (int64_t)res * n_cu);
     if (const char* e = getenv("FV3_B3_GRID")) grid = std::min<int64_t>(a.ntiles, std::max(1, atoi(e)));
     void* kargs[] = {&a};
-    FV3_HIP(hipLaunchKernel(kfn, dim3((unsigned)grid), dim3(256), kargs, lds, (hipStream_t)stream));
+    FV3_HIP(hipLaunchKernel(kfn, dim3((unsigned)grid), dim3(kB3Threads), kargs, lds, (hipStream_t)stream));
     FV3_LAUNCH_CHECK();
     return FV3_OK;
 }
