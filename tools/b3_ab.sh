@@ -5,5 +5,5 @@ set -o pipefail
 for v in "$@"; do
     echo "== $v"
     if [ "$v" = base ]; then lib=fv3net_amd/_lib/libfv3net_amd.so; else lib=tools/variants/lib$v.so; fi
-    FV3NET_AMD_LIB=$lib timeout -k 10 120 python tools/b3_time.py dense emulator 2>&1 | grep bf16x3 || exit 1
+    B3_PRECS=bf16x3 FV3NET_AMD_LIB=$lib timeout -k 10 120 python tools/b3_time.py dense emulator 2>&1 | grep bf16x3 || exit 1
 done

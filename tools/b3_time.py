@@ -38,7 +38,7 @@ def report(name, wl, t, prec):
 if __name__ == "__main__":
     dev = torch.device("cuda", 0)
     which = sys.argv[1:] or ["dense", "emulator"]
-    for prec in ("bf16x3", "f32"):
+    for prec in os.environ.get("B3_PRECS", "bf16x3,f32").split(","):
         if "dense" in which:
             for res, n in ((48, 200), (384, 10)):
                 wl = W.make_dense_workload(res, seed=1, device=dev, precision=prec)
