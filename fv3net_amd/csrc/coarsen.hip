@@ -88,6 +88,15 @@ struct FineCol {
     DT ptop, pbot, run;
     int next;         // next fine interface index (0-based) the running sum will produce
     int km, kn;
+    const DT* dnx;    // &delp[next]
+    DT dl;            // delp[next], loaded one call ahead (its latency overlaps a layer)
+    __device__ __forceinline__ void start()
+    {
+        run = ptop;
+        next = 0;
+        dnx = dp;
+        dl = dp[0];
+    }
     __device__ __forceinline__ float q1(int k) const { return q[(int64_t)(k - 1) * plane]; }
     __device__ __forceinline__ float pe1(int k)
     {
@@ -95,8 +104,10 @@ struct FineCol {
         if (k == 1) return (float)ptop;
         if (k == km + 1) return (float)pbot;
         while (next < k - 1) {  // interface k-1 (0-based) = ptop + sum delp[0..k-2]
-            run = run + dp[(int64_t)next * plane];
+            run = run + dl;
             ++next;
+            dnx += plane;
+            if (next < km) dl = *dnx;
         }
         return (float)run;
     }
@@ -198,9 +209,8 @@ __global__ __launch_bounds__(512) void regrid_coarsen_kernel(CoarsenArgs<DT> a)
         col.pc = pcc;
         col.ptop = ptop;
         col.pbot = pbot;
-        col.run = ptop;
-        col.next = 0;
         col.km = km;
+        col.start();
         col.kn = km;
         // _mask_weights (regridz.py:150-161): area where phalf_c_on_f[k+1] < phalf_f[-1]
         // (compared in delp's dtype); the masked area stays float32 (coarsen.py:213-215)
@@ -244,6 +254,274 @@ __global__ __launch_bounds__(512) void regrid_coarsen_kernel(CoarsenArgs<DT> a)
             }
         }
         __syncthreads();
+    }
+}
+
+// ====================================================================================
+// Cell-per-wave mapping (default for f >= 2): one 64-lane block holds G = 64 / f^2 whole
+// coarse cells (f = 8: one cell, lane = dy * 8 + dx), so every f x f block sum is a
+// wave-local reduction and the coarse pressure edges of a cell (its remap targets)
+// live in LDS per wave.  No cross-wave barrier anywhere.
+//   pass 1: delp streamed once; delp*area of CH levels staged in LDS, then the
+//           numpy-order cell sums (rows, then rows in y order) of all CH levels at
+//           once (lane = row of (cell, level)), coarse delp and its cumsum;
+//           the masked-area denominators of every level (field-independent) once.
+//   per field: each lane runs the streaming mappm (remap_layer_fast) on its column;
+//           emit(k) applies the level's mask weight and drops nan0(q * w) into a
+//           per-wave ring of kRing levels; after every input layer, once all lanes
+//           have emitted kcons + NB levels, those NB levels are summed per cell in
+//           numpy order (lane = row of (cell, level)) and written.  A lane that runs
+//           kRing levels ahead of the slowest (e.g. a much shallower column in a
+//           steep cell) writes from then on into a per-lane global column instead
+//           (sticky, recorded in LDS); the sums read those entries from there.
+// Same arithmetic and order as regrid_coarsen_kernel, so the same bits.
+// ====================================================================================
+
+constexpr int kRing = 16;     // output levels held per wave
+constexpr int kRingLd = 65;   // ring row stride (floats): rows of one cell read bank-free
+
+// per-level cell sums in numpy's order for nb consecutive levels of G cells:
+// val(g, kk, j) = element j = dy * f + dx of cell g at level kk; res(g, kk, sum)
+template <typename T, typename Val, typename Res>
+__device__ __forceinline__ void cell_sums(int lane, int G, int f, int nb, T* rowbuf, Val val, Res res)
+{
+    const int nrow = G * nb * f;
+    for (int i = lane; i < nrow; i += 64) {
+        const int dy = i % f, kk = (i / f) % nb, g = i / (f * nb);
+        const int b = dy * f;
+        T r;
+        if (f == 8) {
+            r = ((val(g, kk, b) + val(g, kk, b + 1)) + (val(g, kk, b + 2) + val(g, kk, b + 3))) +
+                ((val(g, kk, b + 4) + val(g, kk, b + 5)) + (val(g, kk, b + 6) + val(g, kk, b + 7)));
+        } else {
+            r = val(g, kk, b);
+            for (int c = 1; c < f; ++c) r = r + val(g, kk, b + c);
+        }
+        rowbuf[i] = r;
+    }
+    __syncthreads();
+    for (int i = lane; i < G * nb; i += 64) {
+        const T* rr = rowbuf + i * f;  // rows of (cell, level) i = g * nb + kk
+        T acc = rr[0];
+        for (int dy = 1; dy < f; ++dy) acc = acc + rr[dy];
+        res(i / nb, i % nb, acc);
+    }
+    __syncthreads();
+}
+
+template <typename DT, int FF>
+struct CellCtx {
+    const CoarsenArgs<DT>* a;
+    int lane, G, f, ff, nb, km, tile, Y, X0, nxc;
+    int64_t cplane;
+    const DT* pc;       // [G][km+1] coarse phalf
+    const float* den;   // [G][km] masked-area sums
+    float* ring;        // [kRing][kRingLd]
+    const int* ovf;     // [64] first level a lane wrote to its global column (km: none)
+    float* rowbuf;      // [64]
+    float* scr;         // global columns [km][gridDim * 64], or NULL
+    int64_t sstride;
+    float* out;         // this field's output
+
+    // sum and write levels [k0, k0 + nb) of every cell of the block
+    __device__ void consume(int k0, int nb_) const
+    {
+        const int gl0 = blockIdx.x * 64;
+        const int f = FF ? FF : this->f, ff = f * f, G = 64 / ff;
+        cell_sums<float>(
+            lane, G, f, nb_, rowbuf,
+            [&](int g, int kk, int j) {
+                const int l = g * ff + j, k = k0 + kk;
+                if (k >= ovf[l]) return scr[(int64_t)k * sstride + gl0 + l];
+                return ring[(k % kRing) * kRingLd + l];
+            },
+            [&](int g, int kk, float num) {
+                const int k = k0 + kk, X = X0 + g;
+                if (X < nxc) out[((int64_t)tile * km + k) * cplane + (int64_t)Y * nxc + X] = num / den[g * km + k];
+            });
+    }
+};
+
+template <typename DT, int FF>
+struct CellCol : FineCol<DT> {
+    const CellCtx<DT, FF>* ctx;
+    float area;
+    bool active;
+    int nemit;   // output levels emitted so far by this lane
+    int kcons;   // levels [0, kcons) summed and written (wave-uniform)
+    int ovf_k;   // first level this lane sent to its global column (km: none)
+    int* ovf_lds;
+    float* mine;  // this lane's global column (level 0), or NULL
+
+    __device__ __forceinline__ void emit(int k, float v)
+    {
+        const int k0 = k - 1;
+        nemit = k;
+        if (!active) return;
+        // _mask_weights (regridz.py:150-161): area where phalf_c[k0+1] < phalf_f[-1]
+        const float w = (this->pc[k] < this->pbot) ? area : 0.0f;
+        const float x = nan0(v * w);
+        if (k0 >= ovf_k || k0 - kcons >= kRing) {
+            if (ovf_k > k0) {
+                ovf_k = k0;
+                ovf_lds[ctx->lane] = k0;
+            }
+            mine[(int64_t)k0 * ctx->sstride] = x;
+        } else {
+            ctx->ring[(k0 % kRing) * kRingLd + ctx->lane] = x;
+        }
+    }
+
+    // after every input layer: sum the next NB levels once every lane has emitted them
+    __device__ __forceinline__ void layer_done()
+    {
+        const int nb = FF ? std::min(8, 64 / ((64 / (FF * FF)) * FF)) : ctx->nb;
+        if (__all(nemit >= kcons + nb)) {
+            __syncthreads();
+            ctx->consume(kcons, nb);
+            kcons += nb;
+        }
+    }
+};
+
+// FF: the coarsening factor at compile time (8, config #3: all index arithmetic folds),
+// or 0 (runtime a.f)
+template <typename DT, int FF>
+__global__ __launch_bounds__(64) void regrid_coarsen_cells_kernel(CoarsenArgs<DT> a)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int f = FF ? FF : a.f, km = a.km, ff = f * f;
+    const int G = 64 / ff;
+    const int CH = min(8, 64 / (G * f));  // levels per cell-sum batch (G * CH * f <= 64)
+    const int lane = threadIdx.x;
+    const int g = lane / ff, j = lane - (lane / ff) * ff;
+    const int dy = j / f, dx = j - (j / f) * f;
+    const int nxc = a.nx / f, nyc = a.ny / f;
+    const int ngrp = (nxc + G - 1) / G;
+    // neighbouring cells share delp / field cache lines (f = 8: 32 B of each 128 B row
+    // line): give them to the same XCD
+    int64_t bi = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int grp = (int)(bi % ngrp);
+    bi /= ngrp;
+    const int Y = (int)(bi % nyc);
+    const int tile = (int)(bi / nyc);
+    const int X0 = grp * G;
+    const int X = X0 + min(g, G - 1);
+    const bool active = g < G && X < nxc;
+    const int64_t plane = (int64_t)a.ny * a.nx;
+    const int64_t fine = (int64_t)(Y * f + (active ? dy : 0)) * a.nx + (int64_t)min(X, nxc - 1) * f + (active ? dx : 0);
+    const int64_t cplane = (int64_t)nyc * nxc;
+    const int gg = min(g, G - 1);
+
+    DT* pc = reinterpret_cast<DT*>(smem);                   // [G][km+1]
+    DT* lpb = pc + G * (km + 1);                              // [64] fine surface phalf
+    DT* buf = lpb + 64;                                       // [CH][kRingLd] pass-1 staging ...
+    float* ring = reinterpret_cast<float*>(buf);              // ... aliased by the ring [kRing][kRingLd]
+    char* after = reinterpret_cast<char*>(buf) + std::max(sizeof(DT) * CH * kRingLd, sizeof(float) * kRing * kRingLd);
+    DT* rowd = reinterpret_cast<DT*>(after);                  // [64] row sums (DT)
+    float* rowf = reinterpret_cast<float*>(rowd + 64);        // [64] row sums (f32)
+    float* lar = rowf + 64;                                   // [64] fine area
+    float* asum = lar + 64;                                   // [64]
+    float* den = asum + 64;                                   // [G][km]
+    int* ovf = reinterpret_cast<int*>(den + G * km);          // [64]
+
+    // ---- pass 1: fine phalf (per lane), area-weighted coarse delp and phalf ----
+    const float area = active ? a.area[(int64_t)tile * plane + fine] : 0.0f;
+    lar[lane] = area;
+    __syncthreads();
+    if (lane < G)  // weights.coarsen().sum(): float32 (area's dtype)
+        asum[lane] = block_sum<float>(f, [&](int jj) { return nan0(lar[lane * ff + jj]); });
+    const DT* dp = a.delp + (int64_t)tile * km * plane + fine;
+    const DT ptop = (DT)a.ptop;
+    DT run = ptop;  // fine phalf = cumsum([ptop, delp]) (vertically_dependent.py:62-63)
+    DT crun = ptop;  // lanes < G: coarse phalf = cumsum([ptop, delp_c]), sequential like np.cumsum
+    if (lane < G) pc[lane * (km + 1)] = ptop;
+    // the chunk after the current one is loaded before the current one is reduced
+    constexpr int kCH = 8;
+    DT dcur[kCH], dnxt[kCH];
+    auto load_chunk = [&](DT* dst, int k0) {
+#pragma unroll
+        for (int kk = 0; kk < kCH; ++kk)
+            if (kk < CH && k0 + kk < km) dst[kk] = dp[(int64_t)(k0 + kk) * plane];
+    };
+    load_chunk(dcur, 0);
+    for (int k0 = 0; k0 < km; k0 += CH) {
+        const int nk = min(CH, km - k0);
+        if (k0 + CH < km) load_chunk(dnxt, k0 + CH);
+#pragma unroll
+        for (int kk = 0; kk < kCH; ++kk) {
+            if (kk < nk) {
+                const DT d = active ? dcur[kk] : (DT)0;
+                run = run + d;
+                buf[kk * kRingLd + lane] = nan0(d * (DT)area);  // (delp * area) in delp's dtype
+            }
+        }
+        __syncthreads();
+        cell_sums<DT>(
+            lane, G, f, nk, rowd, [&](int gi, int kk, int jj) { return buf[kk * kRingLd + gi * ff + jj]; },
+            [&](int gi, int kk, DT acc) {
+                const int k = k0 + kk, Xg = X0 + gi;
+                const DT dc = acc / (DT)asum[gi];  // weighted_block_average (coarsen.py:213-215)
+                pc[gi * (km + 1) + k + 1] = dc;
+                if (Xg < nxc) {
+                    const int64_t o = ((int64_t)tile * km + k) * cplane + (int64_t)Y * nxc + Xg;
+                    if (a.delp_out) a.delp_out[o] = (float)dc;
+                    if (a.delp_out64) a.delp_out64[o] = (double)dc;
+                }
+            });
+        if (lane < G) {
+            DT* p = pc + lane * (km + 1) + k0 + 1;
+            for (int kk = 0; kk < nk; ++kk) {
+                crun = crun + p[kk];
+                p[kk] = crun;
+            }
+        }
+#pragma unroll
+        for (int kk = 0; kk < kCH; ++kk) dcur[kk] = dnxt[kk];
+    }
+    const DT pbot = run;  // phalf_fine[-1] of this fine column
+    lpb[lane] = pbot;
+    __syncthreads();
+    // masked-area denominators of every level (the same for every field)
+    for (int k0 = 0; k0 < km; k0 += CH) {
+        const int nk = min(CH, km - k0);
+        cell_sums<float>(
+            lane, G, f, nk, rowf,
+            [&](int gi, int kk, int jj) {
+                const int l = gi * ff + jj;
+                return (pc[gi * (km + 1) + k0 + kk + 1] < lpb[l]) ? nan0(lar[l]) : 0.0f;
+            },
+            [&](int gi, int kk, float s) { den[gi * km + k0 + kk] = s; });
+    }
+
+    // ---- per field: stream the remap, sum finished levels per cell ----
+    const int64_t sstride = (int64_t)gridDim.x * 64;
+    for (int v = 0; v < a.n_fields; ++v) {
+        ovf[lane] = km;
+        __syncthreads();
+        CellCtx<DT, FF> ctx{&a, lane, G, f, ff, CH, km, tile, Y, X0, nxc, cplane, pc, den, ring, ovf, rowf,
+                        a.scratch, sstride, a.out[v]};
+        CellCol<DT, FF> col;
+        col.q = a.fields[v] + (int64_t)tile * km * plane + fine;
+        col.dp = dp;
+        col.plane = plane;
+        col.pc = pc + gg * (km + 1);
+        col.ptop = ptop;
+        col.pbot = pbot;
+        col.km = km;
+        col.start();
+        col.kn = km;
+        col.ctx = &ctx;
+        col.area = area;
+        col.active = active;
+        col.nemit = 0;
+        col.kcons = 0;
+        col.ovf_k = km;
+        col.ovf_lds = ovf;
+        col.mine = a.scratch + (int64_t)blockIdx.x * 64 + lane;
+        mappm_ppm_column(col, km, km, a.iv, a.kord);
+        __syncthreads();
+        for (int k0 = col.kcons; k0 < km; k0 += CH) ctx.consume(k0, min(CH, km - k0));
     }
 }
 
@@ -507,8 +785,33 @@ int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* f
     // per-lane remapped columns for the input-driven path: km x (blocks x 64 f) floats from
     // the stream-ordered pool (C384 79 levels: ~285 MB, reused by every field of the call;
     // FV3_COARSEN_CURSOR=1 selects the scratch-free output-driven path for A/B)
+    // FV3_COARSEN_PATH = cells (default for f >= 2) | rows (the f-wave row-segment
+    // blocks with a per-lane scratch column) | cursor (rows, scratch-free cursor remap)
+    const char* path = getenv("FV3_COARSEN_PATH");
+    const bool cursor = (path && path[0] == 'c' && path[1] == 'u') || getenv("FV3_COARSEN_CURSOR");
+    const bool cells = !cursor && factor >= 2 && !(path && path[0] == 'r');
     void* scratch = nullptr;
-    if (n_fields > 0 && !getenv("FV3_COARSEN_CURSOR"))
+    if (cells) {
+        const int ff = factor * factor, G = 64 / ff;
+        const int CH = std::min(8, 64 / (G * factor));
+        const int64_t cblocks = (int64_t)ntile * (ny / factor) * ((nxc + G - 1) / G);
+        const size_t lds_c = sizeof(DT) * ((size_t)G * (km + 1) + 64 + 64) +
+                             std::max(sizeof(DT) * CH * kRingLd, sizeof(float) * kRing * kRingLd) +
+                             sizeof(float) * (64 * 3 + (size_t)G * km) + sizeof(int) * 64;
+        FV3_REQUIRE(lds_c <= 64 * 1024, "regrid_coarsen: %zu B of LDS needed", lds_c);
+        FV3_REQUIRE(cblocks < (int64_t)0x7fffffff, "regrid_coarsen: grid too large");
+        // per-lane overflow columns: only written by lanes that run kRing levels ahead
+        if (n_fields > 0) FV3_HIP(hipMallocAsync(&scratch, sizeof(float) * (size_t)km * (size_t)cblocks * 64, s));
+        a.scratch = (float*)scratch;
+        if (factor == 8)
+            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 8>), dim3((unsigned)cblocks), dim3(64), lds_c, s, a);
+        else
+            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 0>), dim3((unsigned)cblocks), dim3(64), lds_c, s, a);
+        FV3_LAUNCH_CHECK();
+        if (scratch) FV3_HIP(hipFreeAsync(scratch, s));
+        return FV3_OK;
+    }
+    if (n_fields > 0 && !cursor)
         FV3_HIP(hipMallocAsync(&scratch, sizeof(float) * (size_t)km * (size_t)blocks * 64 * factor, s));
     a.scratch = (float*)scratch;
     if (scratch)

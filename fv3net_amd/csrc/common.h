@@ -66,4 +66,15 @@ inline bool layout_ok(const fv3_layout& l, int64_t ncol)
 
 inline fv3_layout plain_layout(int64_t ncol) { return fv3_layout{ncol, ncol, 0}; }
 
+// Workgroups are dealt round-robin over the 8 XCDs (each with its own L2): block b runs
+// on XCD b % 8.  This bijection of [0, nblocks) gives the blocks of one XCD consecutive
+// logical ids, so neighbouring tiles that share cache lines land in the same L2.
+constexpr unsigned kNumXcd = 8;
+__device__ __forceinline__ unsigned xcd_swizzle(unsigned b, unsigned nblocks)
+{
+    const unsigned r = b % kNumXcd, q = b / kNumXcd;
+    const unsigned per = nblocks / kNumXcd, rem = nblocks % kNumXcd;
+    return r * per + (r < rem ? r : rem) + q;
+}
+
 }  // namespace fv3

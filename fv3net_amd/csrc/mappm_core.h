@@ -190,6 +190,8 @@ struct RemapState {
     bool accum;     // true: accumulating whole layers below the top edge (label 111 loop)
     float qsum, dpsum;
     float t, b;     // pe2(k), pe2(k+1)
+    float xt = 0.0f;  // remap_layer_fast: (t - pe1(L)) / dp1(L) of the current layer L, valid if xv
+    bool xv = false;
 };
 
 // The column's input layer L as the consumer sees it.
@@ -256,6 +258,79 @@ FV3_HD inline void remap_layer(RemapState& s, const LayerView& v, const ColumnEn
     }
 }
 
+// remap_layer with the same events, values and bits, arranged for a wave of columns
+// whose lanes sit at different points of the event sequence (mappm.f90:58-124):
+//  * an accumulating output meets at most one event per layer and only as the layer's
+//    first (whole layer, or the bottom piece that ends it), so it runs once up front;
+//  * every edge's normalised position (pe2(e) - pe1(L)) / dp1(L) is the same
+//    expression whether the edge is the bottom of one output (ESL, PR) or the top of
+//    the next (PL), so it is divided once and carried in xt;
+//  * the inside-layer value (mappm.f90:76-83) and the fractional top piece
+//    (mappm.f90:85-92) share one operand tree: with PR := 1 the top piece's
+//    (1+PL) is PR+PL bit for bit, and TT = r3*(u + PL*w) with (u, w) = (PR*(PR+PL), PL)
+//    inside or (1, 1+PL) for the top piece, so both run as one branch-free body.
+// Holds for every input (no ordering assumption): each value is computed by the
+// reference's expression on the same operands.
+template <class Out>
+FV3_HD inline void remap_layer_fast(RemapState& s, const LayerView& v, const ColumnEnds& e, int kn, Out& out)
+{
+    const float r3 = 1.0f / 3.0f, r23 = 2.0f / 3.0f;
+    s.xv = false;
+    if (s.k > kn) return;
+    if (s.accum) {
+        if (s.b > v.pl1) {
+            // whole layer (mappm.f90:99-104)
+            s.qsum = s.qsum + v.dp * v.q1;
+            s.dpsum = s.dpsum + v.dp;
+            return;
+        }
+        // bottom piece (mappm.f90:105-112)
+        const float delp = s.b - v.pl0;
+        const float esl = delp / v.dp;
+        s.qsum = s.qsum + delp * (v.a.al + 0.5f * esl * (v.a.ar - v.a.al + v.a.a6 * (1.0f - r23 * esl)));
+        s.dpsum = s.dpsum + delp;
+        out.emit(s.k, s.qsum / s.dpsum);
+        s.accum = false;
+        s.k += 1;
+        s.t = s.b;
+        s.b = out.next_edge(s.k);
+        s.xt = esl;  // = (t - pe1(L)) / dp1(L) for the new top edge
+        s.xv = true;
+    }
+    while (s.k <= kn) {
+        // one body for every event kind: boundary emit, inside-layer emit, top piece
+        const bool above = s.t <= e.pe_top;
+        const bool bnd = above || s.t >= e.pe_bot;
+        const bool inl = !bnd && s.t >= v.pl0 && s.t <= v.pl1;
+        if (!bnd && !inl) return;  // top edge further down: next layer
+        if (inl && !s.xv) s.xt = (s.t - v.pl0) / v.dp;
+        const bool inside = s.b <= v.pl1;
+        float pr = 1.0f;
+        if (inl && inside) pr = (s.b - v.pl0) / v.dp;
+        const float pl = s.xt;
+        const float x = pr + pl;
+        const float u = inside ? pr * x : 1.0f;
+        const float w = inside ? pl : 1.0f + pl;
+        const float tt = r3 * (u + pl * w);
+        const float val = v.a.al + 0.5f * (v.a.a6 + v.a.ar - v.a.al) * x - v.a.a6 * tt;
+        if (inl && !inside) {
+            // fractional top piece; continue in the layers below
+            const float delp = v.pl1 - s.t;
+            s.qsum = delp * val;
+            s.dpsum = delp;
+            s.accum = true;
+            return;
+        }
+        // boundary value, or the entire new layer inside input layer L
+        out.emit(s.k, bnd ? (above ? e.q_top : e.q_bot) : val);
+        s.xt = pr;
+        s.xv = inl;
+        s.k += 1;
+        s.t = s.b;
+        s.b = out.next_edge(s.k);
+    }
+}
+
 // After the last input layer: extension below the old surface and the
 // boundary branches for what is left (mappm.f90:115-121, 62-67).
 template <class Out>
@@ -283,13 +358,24 @@ FV3_HD inline void remap_finish(RemapState& s, const ColumnEnds& e, int kn, Out&
     }
 }
 
+// Optional per-layer hook: a `Col` with layer_done() has it called after every input
+// layer's outputs (lockstep over L, so a wave can act on its lanes' emits together).
+template <class C>
+FV3_HD inline auto layer_hook(C& c, int) -> decltype(c.layer_done(), void())
+{
+    c.layer_done();
+}
+template <class C>
+FV3_HD inline void layer_hook(C&, long) {}
+
 // ---- one column, kord <= 7 (ppm_profile path), fully streaming ----
 //
 // `Col` provides (1-based levels):
 //   float q1(int k)   k = 1..km          float pe1(int k)  k = 1..km+1
 //   float pe2(int k)  k = 1..kn+1        void emit(int k, float v)
 //   float next_edge(int k) -> pe2(k+1) or 0 when k+1 > kn+1
-template <class Col>
+// FAST selects remap_layer_fast (default) or the reference-shaped remap_layer (host A/B).
+template <class Col, bool FAST = true>
 FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
 {
     // window state E_L: q(L..L+3), dp(L..L+3), pe1(L..L+4), dc(L..L+2), ALraw(L..L+2), h2(L-1..L+1)
@@ -340,6 +426,14 @@ FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
 
     RemapState s{1, false, 0.0f, 0.0f, c.pe2(1), c.pe2(2)};
 
+    // level j = L + 4 is ingested at the end of iteration L; its q1 / pe1 are read one
+    // iteration earlier, so each load has a whole layer of arithmetic to arrive
+    float q_pf = 0.0f, pe_pf = 0.0f;
+    if (5 <= km) {
+        q_pf = c.q1(5);
+        pe_pf = c.pe1(6);
+    }
+
     for (int L = 1; L <= km; ++L) {
         // ---- emit the final coefficients of layer L ----
         Ppm a{qv[0], alv[0], (L < km) ? alv[1] : ar_km, 0.0f};
@@ -355,22 +449,39 @@ FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
             if (kord != 6) ppm_limit(dcL, a, lmt);
         }
         const LayerView v{pev[0], pev[1], dpv[0], qv[0], a};
-        remap_layer(s, v, ends, kn, c);
+#ifdef FV3_EXP_NOREMAP  // experiment only (results invalid): profile cost without the consumer
+        if (L <= kn) c.emit(L, v.a.al + v.a.ar + v.a.a6);
+#else
+        if constexpr (FAST)
+            remap_layer_fast(s, v, ends, kn, c);
+        else
+            remap_layer(s, v, ends, kn, c);
+#endif
+        layer_hook(c, 0);
 
         if (L == km) break;
         // ---- advance the window E_L -> E_{L+1} ----
         const int j = L + 4;  // level to ingest
         float qn = 0.0f, pen = 0.0f, dpn = 0.0f;
         if (j <= km) {
-            qn = c.q1(j);
-            pen = c.pe1(j + 1);
+            qn = q_pf;
+            pen = pe_pf;
             dpn = pen - pev[4];
+        }
+        if (j + 1 <= km) {  // prefetch level j + 1
+            q_pf = c.q1(j + 1);
+            pe_pf = c.pe1(j + 2);
         }
         const int m = L + 3;  // dc(m), ALraw(m)
         float dcm = 0.0f, alm = 0.0f;
         if (m <= km - 1) {
+#ifdef FV3_EXP_NOPROFILE  // experiment only (results invalid): consumer cost without dc/al
+            dcm = qn - qv[3];
+            alm = 0.5f * (qv[2] + qv[3]);
+#else
             dcm = ppm_dc(qv[2], qv[3], qn, dpv[2], dpv[3], dpn);
             alm = ppm_al(dpv[1], dpv[2], dpv[3], dpn, qv[2], qv[3], dcv[2], dcm);
+#endif
         } else if (m == km) {
             // bottom: area-preserving cubic (mappm.f90:729-761)
             const float d1 = dpv[3], d2 = dpv[2];
@@ -402,7 +513,9 @@ FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
         alv[0] = alv[1]; alv[1] = alv[2]; alv[2] = alm;
         h2v[0] = h2v[1]; h2v[1] = h2v[2]; h2v[2] = h2n;
     }
+#ifndef FV3_EXP_NOREMAP
     remap_finish(s, ends, kn, c);
+#endif
 }
 
 // ---- resumable PPM column (kord <= 7): one OUTPUT level per call ----
@@ -864,7 +977,7 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
             }
         }
         const LayerView v{pl0, pl1, pl1 - pl0, qw[2], a};
-        remap_layer(s, v, ends, kn, c);
+        remap_layer_fast(s, v, ends, kn, c);
         if (L == km) break;
         for (int i = 0; i < 5; ++i) qw[i] = qw[i + 1];
         qw[5] = q1_or0(L + 4);

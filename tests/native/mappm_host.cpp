@@ -50,3 +50,16 @@ extern "C" int host_mappm_cursor(int km, const float* pe1, const float* q1, int 
     }
     return 0;
 }
+
+// the streaming column with the reference-shaped event loop (remap_layer) instead of
+// remap_layer_fast: the two must agree bit for bit on every input, sorted or not
+extern "C" int host_mappm_generic(int km, const float* pe1, const float* q1, int kn, const float* pe2,
+                                  float* q2, int64_t ncol, int iv, int kord)
+{
+    if (km < 4 || kn < 1 || kord > 7) return -1;
+    for (int64_t i = 0; i < ncol; ++i) {
+        Col c{pe1, q1, pe2, q2, ncol, i, kn};
+        fv3::mappm_ppm_column<Col, false>(c, km, kn, iv, kord);
+    }
+    return 0;
+}

@@ -105,18 +105,18 @@ def _smooth_state(rng, nt, km, ny, nx):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["scratch", "cursor"])
+@pytest.mark.parametrize("path", ["cells", "rows", "cursor"])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("factor,n", [(1, 4), (2, 16), (3, 12), (4, 24), (8, 48)])
 def test_kernel_vs_oracle_random(gpu, factor, n, dtype, path, monkeypatch):
     """Bit-identical to the oracle for every factor (numpy's block-sum order) and
     both delp dtypes (the arithmetic follows delp's dtype, as the reference does), on
-    both remap paths: the input-driven streaming remap through a per-lane scratch
-    column (default) and the scratch-free output-driven cursor (FV3_COARSEN_CURSOR)."""
+    every kernel path (FV3_COARSEN_PATH): whole cells per wave with the per-wave output
+    ring (default, f >= 2), f-wave row segments with a per-lane scratch column, and
+    the row segments with the scratch-free output-driven cursor."""
     from fv3net_amd.coarsen import coarsen_on_pressure
 
-    if path == "cursor":
-        monkeypatch.setenv("FV3_COARSEN_CURSOR", "1")
+    monkeypatch.setenv("FV3_COARSEN_PATH", path)
 
     rng = np.random.default_rng(factor * 100 + n)
     delp, area, T, q = _smooth_state(rng, 6, 79, n, n)
@@ -126,6 +126,30 @@ def test_kernel_vs_oracle_random(gpu, factor, n, dtype, path, monkeypatch):
     for name, r in zip(("T", "q"), ref):
         _bits_equal(out[name].cpu().numpy(), r)
     _bits_equal(delp_c.cpu().numpy(), ref_dc)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["cells", "rows"])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_kernel_steep_cells_overflow_columns(gpu, path, dtype, monkeypatch):
+    """Fine columns of one coarse cell with very different surface pressures (steep
+    terrain: the lowest 40 of 79 layers scaled by 0.05 .. 4 per column), so within a
+    cell some columns emit their remapped levels dozens of levels ahead of others: the
+    cells path's per-wave ring (16 levels) overflows into the per-lane global columns.
+    Still bit-identical to the oracle, on both paths."""
+    from fv3net_amd.coarsen import coarsen_on_pressure
+
+    monkeypatch.setenv("FV3_COARSEN_PATH", path)
+    rng = np.random.default_rng(11)
+    delp, area, T, q = _smooth_state(rng, 6, 79, 16, 16)
+    delp[:, -40:] *= rng.uniform(0.05, 4.0, (6, 1, 16, 16)).astype(np.float32)
+    delp = delp.astype(dtype)
+    for f in (8, 4):
+        out, delp_c = coarsen_on_pressure(delp, area, {"T": T, "q": q}, f)
+        ref, ref_dc = OC.coarsen_on_pressure(delp, area, [T, q], f)
+        for name, r in zip(("T", "q"), ref):
+            _bits_equal(out[name].cpu().numpy(), r)
+        _bits_equal(delp_c.cpu().numpy(), ref_dc)
 
 
 @pytest.mark.gpu

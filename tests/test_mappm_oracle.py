@@ -83,7 +83,7 @@ def host_lib():
     subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
                     "-o", HOST_SO, HOST_SRC], check=True)
     lib = ctypes.CDLL(HOST_SO)
-    for fn in (lib.host_mappm, lib.host_mappm_cursor):
+    for fn in (lib.host_mappm, lib.host_mappm_cursor, lib.host_mappm_generic):
         fn.restype = ctypes.c_int
         fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                        ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
@@ -93,7 +93,7 @@ def host_lib():
 def _host(lib, pe1, q, pe2, iv, kord, cursor=False):
     pe1, q, pe2 = (np.ascontiguousarray(a, np.float32) for a in (pe1, q, pe2))
     out = np.empty((pe2.shape[0] - 1, q.shape[1]), np.float32)
-    fn = lib.host_mappm_cursor if cursor else lib.host_mappm
+    fn = {True: lib.host_mappm_cursor, False: lib.host_mappm, "generic": lib.host_mappm_generic}[cursor]
     rc = fn(q.shape[0], pe1.ctypes.data, q.ctypes.data, pe2.shape[0] - 1, pe2.ctypes.data, out.ctypes.data,
             q.shape[1], iv, kord)
     assert rc == 0
@@ -170,3 +170,57 @@ def test_output_driven_cursor_golden(host_lib):
                 for qn in ("qs", "qr"):
                     res = _host(host_lib, pe1, g[f"c{ci}_{qn}"], pe2, int(iv), int(kord), cursor=True)
                     assert _bits_equal(res, g[f"c{ci}_{qn}_k{kord}_iv{iv}"]), (ci, qn, kord, iv)
+
+
+@pytest.mark.parametrize("km,kn", [(4, 40), (79, 79), (79, 300), (20, 5)])
+def test_streaming_degenerate_edges(host_lib, km, kn):
+    """remap_layer_fast (the streaming consumer) == oracle bit for bit where the
+    event mix per layer is extreme: zero-thickness input layers (repeated pe1),
+    runs of repeated output edges, output grids much finer than the input (many
+    inside-layer outputs per layer, each reusing the previous edge's position),
+    output edges above the old top and below the old surface."""
+    rng = np.random.default_rng(km * 31 + kn)
+    for kord in (1, 4, 5, 6, 7, 10):
+        for iv in (0, 1, -1):
+            ncol = 64
+            delp = rng.uniform(1, 3000, (km, ncol)).astype(np.float32)
+            delp[rng.random((km, ncol)) < 0.1] = 0.0  # zero-thickness layers
+            delp[:2] = np.maximum(delp[:2], 1.0)       # keep the end cubics finite
+            delp[-2:] = np.maximum(delp[-2:], 1.0)
+            pe1 = np.concatenate([np.full((1, ncol), 300, np.float32),
+                                  300 + np.cumsum(delp, 0, dtype=np.float32)])
+            pe2 = rng.uniform(pe1[0] * 0.7, pe1[-1] * 1.2, (kn + 1, ncol)).astype(np.float32)
+            rep = rng.random((kn + 1, ncol)) < 0.2
+            pe2[1:][rep[1:]] = pe2[:-1][rep[1:]]       # repeated output edges
+            snap = rng.random((kn + 1, ncol)) < 0.2    # output edges on input edges
+            idx = rng.integers(0, km + 1, (kn + 1, ncol))
+            pe2[snap] = np.take_along_axis(pe1, idx, 0)[snap]
+            pe2 = np.sort(pe2, 0)
+            q = (rng.normal(0, 1, (km, ncol)) * rng.choice([1e-4, 1, 300], (km, ncol))).astype(np.float32)
+            with np.errstate(all="ignore"):
+                exp = oracle_mappm(pe1, q, pe2, iv, kord)
+            assert _bits_equal(_host(host_lib, pe1, q, pe2, iv, kord), exp), (kord, iv)
+
+
+@pytest.mark.parametrize("km,kn", [(4, 40), (79, 79), (79, 300), (20, 5)])
+def test_fast_consumer_equals_reference_loop_unsorted(host_lib, km, kn):
+    """remap_layer_fast == remap_layer bit for bit on UNSORTED output edges too
+    (outputs that step back above the current layer, leave and re-enter the column):
+    the rearrangement assumes no ordering."""
+    rng = np.random.default_rng(km * 17 + kn)
+    for kord in (1, 4, 5, 6, 7):
+        for iv in (0, 1, -1):
+            ncol = 64
+            # some input layers of negative thickness too (non-monotone pe1)
+            delp = rng.uniform(-300 if iv else 1, 3000, (km, ncol)).astype(np.float32)
+            pe1 = np.concatenate([np.full((1, ncol), 300, np.float32),
+                                  300 + np.cumsum(delp, 0, dtype=np.float32)])
+            pe2 = np.sort(rng.uniform(pe1.min() * 0.7, pe1.max() * 1.2, (kn + 1, ncol)), 0).astype(np.float32)
+            swap = rng.random((kn, ncol)) < 0.15  # local inversions
+            a, b = pe2[:-1].copy(), pe2[1:].copy()
+            pe2[:-1][swap], pe2[1:][swap] = b[swap], a[swap]
+            q = (rng.normal(0, 1, (km, ncol)) * rng.choice([1e-4, 1, 300], (km, ncol))).astype(np.float32)
+            with np.errstate(all="ignore"):
+                fast = _host(host_lib, pe1, q, pe2, iv, kord)
+                ref = _host(host_lib, pe1, q, pe2, iv, kord, cursor="generic")
+            assert _bits_equal(fast, ref), (kord, iv)

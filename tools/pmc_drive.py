@@ -35,6 +35,8 @@ def make(leg, dev):
         return W.make_mappm_workload(W.c_columns(384), 79, 79, 10, seed=5, device=dev)
     if leg == "mappm_c12":
         return W.make_mappm_workload(W.c_columns(12), 79, 50, 1, seed=5, device=dev)
+    if leg == "coarsen_0f":  # pass 1 only (coarse delp / phalf, denominators)
+        return W.make_coarsen_workload(384, 8, 0, seed=7, device=dev)
     if leg == "coarsen_1f":
         return W.make_coarsen_workload(384, 8, 1, seed=7, device=dev)
     if leg == "coarsen_4f":
