@@ -265,10 +265,9 @@ FV3_HD inline void remap_layer(RemapState& s, const LayerView& v, const ColumnEn
 //  * every edge's normalised position (pe2(e) - pe1(L)) / dp1(L) is the same
 //    expression whether the edge is the bottom of one output (ESL, PR) or the top of
 //    the next (PL), so it is divided once and carried in xt;
-//  * the inside-layer value (mappm.f90:76-83) and the fractional top piece
-//    (mappm.f90:85-92) share one operand tree: with PR := 1 the top piece's
-//    (1+PL) is PR+PL bit for bit, and TT = r3*(u + PL*w) with (u, w) = (PR*(PR+PL), PL)
-//    inside or (1, 1+PL) for the top piece, so both run as one branch-free body.
+//  * an inside-layer output (mappm.f90:76-83) is followed, in the same pass, by the
+//    next output's fractional top piece (mappm.f90:85-92) when that is the next event,
+//    so a wave needs one pass per layer unless a lane has several inside outputs.
 // Holds for every input (no ordering assumption): each value is computed by the
 // reference's expression on the same operands.
 template <class Out>
@@ -298,36 +297,46 @@ FV3_HD inline void remap_layer_fast(RemapState& s, const LayerView& v, const Col
         s.xv = true;
     }
     while (s.k <= kn) {
-        // one body for every event kind: boundary emit, inside-layer emit, top piece
-        const bool above = s.t <= e.pe_top;
-        const bool bnd = above || s.t >= e.pe_bot;
-        const bool inl = !bnd && s.t >= v.pl0 && s.t <= v.pl1;
+        bool above = s.t <= e.pe_top;
+        bool bnd = above || s.t >= e.pe_bot;
+        bool inl = !bnd && s.t >= v.pl0 && s.t <= v.pl1;
         if (!bnd && !inl) return;  // top edge further down: next layer
-        if (inl && !s.xv) s.xt = (s.t - v.pl0) / v.dp;
-        const bool inside = s.b <= v.pl1;
-        float pr = 1.0f;
-        if (inl && inside) pr = (s.b - v.pl0) / v.dp;
-        const float pl = s.xt;
-        const float x = pr + pl;
-        const float u = inside ? pr * x : 1.0f;
-        const float w = inside ? pl : 1.0f + pl;
-        const float tt = r3 * (u + pl * w);
-        const float val = v.a.al + 0.5f * (v.a.a6 + v.a.ar - v.a.al) * x - v.a.a6 * tt;
-        if (inl && !inside) {
-            // fractional top piece; continue in the layers below
-            const float delp = v.pl1 - s.t;
-            s.qsum = delp * val;
-            s.dpsum = delp;
-            s.accum = true;
-            return;
+        if (bnd) {
+            out.emit(s.k, above ? e.q_top : e.q_bot);
+            s.k += 1;
+            s.t = s.b;
+            s.b = out.next_edge(s.k);
+            s.xv = false;
+            continue;
         }
-        // boundary value, or the entire new layer inside input layer L
-        out.emit(s.k, bnd ? (above ? e.q_top : e.q_bot) : val);
-        s.xt = pr;
-        s.xv = inl;
-        s.k += 1;
-        s.t = s.b;
-        s.b = out.next_edge(s.k);
+        if (!s.xv) s.xt = (s.t - v.pl0) / v.dp;
+        if (s.b <= v.pl1) {
+            // entire new layer inside input layer L (mappm.f90:76-83)
+            const float pl = s.xt;
+            const float pr = (s.b - v.pl0) / v.dp;
+            const float tt = r3 * (pr * (pr + pl) + pl * pl);
+            out.emit(s.k, v.a.al + 0.5f * (v.a.a6 + v.a.ar - v.a.al) * (pr + pl) - v.a.a6 * tt);
+            s.k += 1;
+            s.t = s.b;
+            s.b = out.next_edge(s.k);
+            s.xt = pr;
+            s.xv = true;
+            if (s.k > kn) return;
+            // the usual next event is this output's top piece in the same layer: run it
+            // here rather than in another pass of the loop
+            above = s.t <= e.pe_top;
+            bnd = above || s.t >= e.pe_bot;
+            inl = !bnd && s.t >= v.pl0 && s.t <= v.pl1;
+            if (!inl || s.b <= v.pl1) continue;  // anything else: the loop head
+        }
+        // fractional top piece (mappm.f90:85-92); continue in the layers below
+        const float pl = s.xt;
+        const float tt = r3 * (1.0f + pl * (1.0f + pl));
+        const float delp = v.pl1 - s.t;
+        s.qsum = delp * (v.a.al + 0.5f * (v.a.a6 + v.a.ar - v.a.al) * (1.0f + pl) - v.a.a6 * tt);
+        s.dpsum = delp;
+        s.accum = true;
+        return;
     }
 }
 
