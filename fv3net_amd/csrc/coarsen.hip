@@ -40,6 +40,7 @@
 #include "blocks.h"
 #include "common.h"
 #include "mappm_core.h"
+#include "mappm_multi.h"
 
 namespace fv3 {
 namespace {
@@ -309,51 +310,61 @@ __device__ __forceinline__ void cell_sums(int lane, int G, int f, int nb, T* row
     __syncthreads();
 }
 
-template <typename DT, int FF>
+template <typename DT, int FF, int NF>
 struct CellCtx {
-    const CoarsenArgs<DT>* a;
-    int lane, G, f, ff, nb, km, tile, Y, X0, nxc;
+    int lane, f, nb, km, tile, Y, X0, nxc;
     int64_t cplane;
     const DT* pc;       // [G][km+1] coarse phalf
     const float* den;   // [G][km] masked-area sums
-    float* ring;        // [kRing][kRingLd]
-    const int* ovf;     // [64] first level a lane wrote to its global column (km: none)
+    float* ring;        // [NF][kRing][kRingLd]
+    const int* ovf;     // [NF][64] first level a lane wrote to its global column (km: none)
     float* rowbuf;      // [64]
-    float* scr;         // global columns [km][gridDim * 64], or NULL
-    int64_t sstride;
-    float* out;         // this field's output
+    float* scr;         // global columns [NF][km][gridDim * 64], or NULL
+    int64_t sstride;    // gridDim * 64
+    float* out[NF];     // the fields' outputs
 
-    // sum and write levels [k0, k0 + nb) of every cell of the block
+    // sum and write levels [k0, k0 + nb) of every cell of the block, for every field
     __device__ void consume(int k0, int nb_) const
     {
         const int gl0 = blockIdx.x * 64;
         const int f = FF ? FF : this->f, ff = f * f, G = 64 / ff;
-        cell_sums<float>(
-            lane, G, f, nb_, rowbuf,
-            [&](int g, int kk, int j) {
-                const int l = g * ff + j, k = k0 + kk;
-                if (k >= ovf[l]) return scr[(int64_t)k * sstride + gl0 + l];
-                return ring[(k % kRing) * kRingLd + l];
-            },
-            [&](int g, int kk, float num) {
-                const int k = k0 + kk, X = X0 + g;
-                if (X < nxc) out[((int64_t)tile * km + k) * cplane + (int64_t)Y * nxc + X] = num / den[g * km + k];
-            });
+        for (int fi = 0; fi < NF; ++fi) {
+            const float* rg = ring + fi * (kRing * kRingLd);
+            const int* ov = ovf + fi * 64;
+            const float* sc = scr + (int64_t)fi * km * sstride;
+            float* o = out[fi];
+            cell_sums<float>(
+                lane, G, f, nb_, rowbuf,
+                [&](int g, int kk, int j) {
+                    const int l = g * ff + j, k = k0 + kk;
+                    if (k >= ov[l]) return sc[(int64_t)k * sstride + gl0 + l];
+                    return rg[(k % kRing) * kRingLd + l];
+                },
+                [&](int g, int kk, float num) {
+                    const int k = k0 + kk, X = X0 + g;
+                    if (X < nxc) o[((int64_t)tile * km + k) * cplane + (int64_t)Y * nxc + X] = num / den[g * km + k];
+                });
+        }
     }
 };
 
-template <typename DT, int FF>
+// NF fields of one fine column, for mappm_ppm_columns<NF>: pressure edges from the
+// running delp sum (FineCol), q from the NF field arrays at the same element offset
+template <typename DT, int FF, int NF>
 struct CellCol : FineCol<DT> {
-    const CellCtx<DT, FF>* ctx;
+    const CellCtx<DT, FF, NF>* ctx;
+    const float* const* fields;  // NF field bases (level 0 of tile 0)
+    int64_t off;                 // this lane's element offset (tile, level 0, fine column)
     float area;
     bool active;
-    int nemit;   // output levels emitted so far by this lane
+    int nemit;   // output levels emitted so far by this lane (every field alike)
     int kcons;   // levels [0, kcons) summed and written (wave-uniform)
-    int ovf_k;   // first level this lane sent to its global column (km: none)
+    int ovf_k[NF];  // first level this lane sent to its global column (km: none)
     int* ovf_lds;
-    float* mine;  // this lane's global column (level 0), or NULL
+    float* mine;  // this lane's global column (field 0, level 0)
 
-    __device__ __forceinline__ void emit(int k, float v)
+    __device__ __forceinline__ float q1(int f, int k) const { return fields[f][off + (int64_t)(k - 1) * this->plane]; }
+    __device__ __forceinline__ void emit(int fi, int k, float v)
     {
         const int k0 = k - 1;
         nemit = k;
@@ -361,14 +372,14 @@ struct CellCol : FineCol<DT> {
         // _mask_weights (regridz.py:150-161): area where phalf_c[k0+1] < phalf_f[-1]
         const float w = (this->pc[k] < this->pbot) ? area : 0.0f;
         const float x = nan0(v * w);
-        if (k0 >= ovf_k || k0 - kcons >= kRing) {
-            if (ovf_k > k0) {
-                ovf_k = k0;
-                ovf_lds[ctx->lane] = k0;
+        if (k0 >= ovf_k[fi] || k0 - kcons >= kRing) {
+            if (ovf_k[fi] > k0) {
+                ovf_k[fi] = k0;
+                ovf_lds[fi * 64 + ctx->lane] = k0;
             }
-            mine[(int64_t)k0 * ctx->sstride] = x;
+            mine[((int64_t)fi * ctx->km + k0) * ctx->sstride] = x;
         } else {
-            ctx->ring[(k0 % kRing) * kRingLd + ctx->lane] = x;
+            ctx->ring[fi * (kRing * kRingLd) + (k0 % kRing) * kRingLd + ctx->lane] = x;
         }
     }
 
@@ -384,9 +395,53 @@ struct CellCol : FineCol<DT> {
     }
 };
 
+// one pass of the streaming remap for fields [v0, v0 + NF), then the last levels' sums
+template <int NF, typename DT, int FF>
+__device__ __forceinline__ void cells_field_group(const CoarsenArgs<DT>& a, int v0, int lane, int f, int nb, int tile,
+                                                  int Y, int X0, int nxc, int64_t cplane, const DT* pc,
+                                                  const DT* pcg, const float* den, float* ring, int* ovf,
+                                                  float* rowf, int64_t off, const DT* dp, int64_t plane, DT ptop,
+                                                  DT pbot, float area, bool active)
+{
+    const int km = a.km;
+    const int64_t sstride = (int64_t)gridDim.x * 64;
+    for (int fi = 0; fi < NF; ++fi) ovf[fi * 64 + lane] = km;
+    __syncthreads();
+    CellCtx<DT, FF, NF> ctx{lane, f, nb, km, tile, Y, X0, nxc, cplane, pc, den, ring, ovf, rowf, a.scratch, sstride, {}};
+    for (int fi = 0; fi < NF; ++fi) ctx.out[fi] = a.out[v0 + fi];
+    CellCol<DT, FF, NF> col;
+    col.q = nullptr;
+    col.dp = dp;
+    col.plane = plane;
+    col.pc = pcg;
+    col.ptop = ptop;
+    col.pbot = pbot;
+    col.km = km;
+    col.kn = km;
+    col.start();
+    col.ctx = &ctx;
+    col.fields = a.fields + v0;
+    col.off = off;
+    col.area = area;
+    col.active = active;
+    col.nemit = 0;
+    col.kcons = 0;
+    for (int fi = 0; fi < NF; ++fi) col.ovf_k[fi] = km;
+    col.ovf_lds = ovf;
+    col.mine = a.scratch + (int64_t)blockIdx.x * 64 + lane;
+    if constexpr (NF == 1) {
+        FirstField<CellCol<DT, FF, NF>> one{col};
+        mappm_ppm_column(one, km, km, a.iv, a.kord);
+    } else {
+        mappm_ppm_columns<NF>(col, km, km, a.iv, a.kord);
+    }
+    __syncthreads();
+    for (int k0 = col.kcons; k0 < km; k0 += nb) ctx.consume(k0, min(nb, km - k0));
+}
+
 // FF: the coarsening factor at compile time (8, config #3: all index arithmetic folds),
 // or 0 (runtime a.f)
-template <typename DT, int FF>
+template <typename DT, int FF, int NF>
 __global__ __launch_bounds__(64) void regrid_coarsen_cells_kernel(CoarsenArgs<DT> a)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -416,14 +471,14 @@ __global__ __launch_bounds__(64) void regrid_coarsen_cells_kernel(CoarsenArgs<DT
     DT* pc = reinterpret_cast<DT*>(smem);                   // [G][km+1]
     DT* lpb = pc + G * (km + 1);                              // [64] fine surface phalf
     DT* buf = lpb + 64;                                       // [CH][kRingLd] pass-1 staging ...
-    float* ring = reinterpret_cast<float*>(buf);              // ... aliased by the ring [kRing][kRingLd]
-    char* after = reinterpret_cast<char*>(buf) + std::max(sizeof(DT) * CH * kRingLd, sizeof(float) * kRing * kRingLd);
+    float* ring = reinterpret_cast<float*>(buf);              // ... aliased by the rings [NF][kRing][kRingLd]
+    char* after = reinterpret_cast<char*>(buf) + std::max(sizeof(DT) * CH * kRingLd, sizeof(float) * NF * kRing * kRingLd);
     DT* rowd = reinterpret_cast<DT*>(after);                  // [64] row sums (DT)
     float* rowf = reinterpret_cast<float*>(rowd + 64);        // [64] row sums (f32)
     float* lar = rowf + 64;                                   // [64] fine area
     float* asum = lar + 64;                                   // [64]
     float* den = asum + 64;                                   // [G][km]
-    int* ovf = reinterpret_cast<int*>(den + G * km);          // [64]
+    int* ovf = reinterpret_cast<int*>(den + G * km);          // [NF][64]
 
     // ---- pass 1: fine phalf (per lane), area-weighted coarse delp and phalf ----
     const float area = active ? a.area[(int64_t)tile * plane + fine] : 0.0f;
@@ -494,34 +549,16 @@ __global__ __launch_bounds__(64) void regrid_coarsen_cells_kernel(CoarsenArgs<DT
             [&](int gi, int kk, float s) { den[gi * km + k0 + kk] = s; });
     }
 
-    // ---- per field: stream the remap, sum finished levels per cell ----
-    const int64_t sstride = (int64_t)gridDim.x * 64;
-    for (int v = 0; v < a.n_fields; ++v) {
-        ovf[lane] = km;
-        __syncthreads();
-        CellCtx<DT, FF> ctx{&a, lane, G, f, ff, CH, km, tile, Y, X0, nxc, cplane, pc, den, ring, ovf, rowf,
-                        a.scratch, sstride, a.out[v]};
-        CellCol<DT, FF> col;
-        col.q = a.fields[v] + (int64_t)tile * km * plane + fine;
-        col.dp = dp;
-        col.plane = plane;
-        col.pc = pc + gg * (km + 1);
-        col.ptop = ptop;
-        col.pbot = pbot;
-        col.km = km;
-        col.start();
-        col.kn = km;
-        col.ctx = &ctx;
-        col.area = area;
-        col.active = active;
-        col.nemit = 0;
-        col.kcons = 0;
-        col.ovf_k = km;
-        col.ovf_lds = ovf;
-        col.mine = a.scratch + (int64_t)blockIdx.x * 64 + lane;
-        mappm_ppm_column(col, km, km, a.iv, a.kord);
-        __syncthreads();
-        for (int k0 = col.kcons; k0 < km; k0 += CH) ctx.consume(k0, min(CH, km - k0));
+    // ---- per group of NF fields: stream the remap, sum finished levels per cell ----
+    const int64_t off = (int64_t)tile * km * plane + fine;
+    int v0 = 0;
+    for (; v0 + NF <= a.n_fields; v0 += NF)
+        cells_field_group<NF, DT, FF>(a, v0, lane, f, CH, tile, Y, X0, nxc, cplane, pc, pc + gg * (km + 1), den,
+                                      ring, ovf, rowf, off, dp, plane, ptop, pbot, area, active);
+    if constexpr (NF > 1) {
+        for (; v0 < a.n_fields; ++v0)
+            cells_field_group<1, DT, FF>(a, v0, lane, f, CH, tile, Y, X0, nxc, cplane, pc, pc + gg * (km + 1), den,
+                                         ring, ovf, rowf, off, dp, plane, ptop, pbot, area, active);
     }
 }
 
@@ -792,21 +829,31 @@ int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* f
     const bool cells = !cursor && factor >= 2 && !(path && path[0] == 'r');
     void* scratch = nullptr;
     if (cells) {
+        // fields remapped NF = 2 at a time (one streaming pass shares the pressure work;
+        // FV3_COARSEN_NF=1 for A/B)
+        const char* nfe = getenv("FV3_COARSEN_NF");
+        const int NF = (n_fields >= 2 && !(nfe && nfe[0] == '1')) ? 2 : 1;
         const int ff = factor * factor, G = 64 / ff;
         const int CH = std::min(8, 64 / (G * factor));
         const int64_t cblocks = (int64_t)ntile * (ny / factor) * ((nxc + G - 1) / G);
         const size_t lds_c = sizeof(DT) * ((size_t)G * (km + 1) + 64 + 64) +
-                             std::max(sizeof(DT) * CH * kRingLd, sizeof(float) * kRing * kRingLd) +
-                             sizeof(float) * (64 * 3 + (size_t)G * km) + sizeof(int) * 64;
+                             std::max(sizeof(DT) * CH * kRingLd, sizeof(float) * NF * kRing * kRingLd) +
+                             sizeof(float) * (64 * 3 + (size_t)G * km) + sizeof(int) * 64 * NF;
         FV3_REQUIRE(lds_c <= 64 * 1024, "regrid_coarsen: %zu B of LDS needed", lds_c);
         FV3_REQUIRE(cblocks < (int64_t)0x7fffffff, "regrid_coarsen: grid too large");
         // per-lane overflow columns: only written by lanes that run kRing levels ahead
-        if (n_fields > 0) FV3_HIP(hipMallocAsync(&scratch, sizeof(float) * (size_t)km * (size_t)cblocks * 64, s));
+        if (n_fields > 0)
+            FV3_HIP(hipMallocAsync(&scratch, sizeof(float) * NF * (size_t)km * (size_t)cblocks * 64, s));
         a.scratch = (float*)scratch;
-        if (factor == 8)
-            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 8>), dim3((unsigned)cblocks), dim3(64), lds_c, s, a);
+        const dim3 grid((unsigned)cblocks), block(64);
+        if (factor == 8 && NF == 2)
+            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 8, 2>), grid, block, lds_c, s, a);
+        else if (factor == 8)
+            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 8, 1>), grid, block, lds_c, s, a);
+        else if (NF == 2)
+            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 0, 2>), grid, block, lds_c, s, a);
         else
-            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 0>), dim3((unsigned)cblocks), dim3(64), lds_c, s, a);
+            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 0, 1>), grid, block, lds_c, s, a);
         FV3_LAUNCH_CHECK();
         if (scratch) FV3_HIP(hipFreeAsync(scratch, s));
         return FV3_OK;

@@ -1,0 +1,397 @@
+// fv3net_amd — the streaming PPM remap (mappm_core.h, kord <= 7) for NF fields that
+// share one column's pressure edges, in ONE pass.
+//
+// coarsen_restarts_on_pressure remaps every masked variable of a restart file onto the
+// same coarse pressure edges (external/vcm/vcm/cubedsphere/coarsen_restarts.py:411-516,
+// 840-887; one regrid_vertical -> mappm call per variable, regridz.py:164-279).  In
+// mappm (external/mappm/mappm/mappm.f90:10-126, ppm_profile :614-851) a large part of
+// the work depends on the pressures alone:
+//   * ppm_profile: of the 7 divisions per level in dc(k) and the provisional edge
+//     a4(2,k), 5 divide pressure thicknesses only (c1, c2 of dc; a1, a2 and
+//     2/(d4(k-1)+d4(k+1)) of the edge), the 6th denominator (d4(k)+delp(k+1)) too;
+//   * the remap: every decision (which output edge falls in which input layer) and
+//     every position PL / PR / ESL, and dpsum.
+// Here those are computed once per column and level, and only the field-dependent
+// parts (differences of q, the limiters, the pieces' values, qsum / dpsum) per field.
+// Each shared value is the same expression on the same operands as in the
+// single-field code, so every field's result carries exactly the bits of
+// mappm_ppm_column (and of the reference) for that field alone.
+//
+// `Col` provides (1-based levels, f = 0..NF-1):
+//   float q1(int f, int k)      float pe1(int k)      float pe2(int k)
+//   void emit(int f, int k, float v)                  float next_edge(int k)
+//   optionally void layer_done() (called after every input layer, as layer_hook)
+#pragma once
+
+#include "mappm_core.h"
+
+namespace fv3 {
+
+// ---- pressure-only / field parts of ppm_dc, ppm_al, ppm_h2 (mappm.f90:658-683, 784-795) ----
+
+struct DcShared {
+    float c1, c2, den;
+};
+FV3_HD inline DcShared ppm_dc_shared(float dm1, float d0, float dp1)
+{
+    const float d4k = dm1 + d0;    // d4(k)
+    const float d4kp = d0 + dp1;   // d4(k+1)
+    return DcShared{(dm1 + 0.5f * d0) / d4kp, (dp1 + 0.5f * d0) / d4k, d4k + dp1};
+}
+FV3_HD inline float ppm_dc_field(const DcShared& p, float qm1, float q0, float qp1, float d0)
+{
+    const float delq_k = qp1 - q0;
+    const float delq_km = q0 - qm1;
+    const float df2 = d0 * (p.c1 * delq_k + p.c2 * delq_km) / p.den;
+    return fsign(fmin3(fabsf(df2), fmax3(qm1, q0, qp1) - q0, q0 - fmin3(qm1, q0, qp1)), df2);
+}
+
+struct AlShared {
+    float d4k, s2, amd, a2, dm1a1;
+};
+FV3_HD inline AlShared ppm_al_shared(float dm2, float dm1, float d0, float dp1)
+{
+    const float d4km = dm2 + dm1;  // d4(k-1)
+    const float d4k = dm1 + d0;    // d4(k)
+    const float d4kp = d0 + dp1;   // d4(k+1)
+    const float a1 = d4km / (d4k + dm1);
+    const float a2 = d4kp / (d4k + d0);
+    return AlShared{d4k, 2.0f / (d4km + d4kp), a1 - a2, a2, dm1 * a1};
+}
+FV3_HD inline float ppm_al_field(const AlShared& p, float dm1, float d0, float qm1, float q0, float dcm1, float dc0)
+{
+    const float c1 = (q0 - qm1) * dm1 / p.d4k;
+    return qm1 + c1 + p.s2 * (d0 * (c1 * p.amd + p.a2 * dcm1) - p.dm1a1 * dc0);
+}
+
+// ---- the area-preserving end cubics, one field (mappm.f90:689-725, 729-761) ----
+
+FV3_HD inline void ppm_top_cubic(float q1, float q2, float d1, float d2, float al3, int iv, float& al1,
+                                 float& al2, float& dc1)
+{
+    const float qm = (d2 * q1 + d1 * q2) / (d1 + d2);
+    const float dq = 2.0f * (q2 - q1) / (d1 + d2);
+    const float c1 = 4.0f * (al3 - qm - d2 * dq) / (d2 * (2.0f * d2 * d2 + d1 * (d2 + 3.0f * d1)));
+    const float c3 = dq - 0.5f * c1 * (d2 * (5.0f * d1 + d2) - 3.0f * d1 * d1);
+    al2 = qm - 0.25f * c1 * d1 * d2 * (d2 + 3.0f * d1);
+    al1 = d1 * (2.0f * c1 * (d1 * d1) - c3) + al2;
+    al2 = fmax2(al2, fmin2(q1, q2));
+    al2 = fmin2(al2, fmax2(q1, q2));
+    dc1 = 0.5f * (al2 - q1);
+    if (iv == 0) {
+        al1 = fmax2(0.0f, al1);
+        al2 = fmax2(0.0f, al2);
+    } else if (iv == -1) {
+        if (al1 * q1 <= 0.0f) al1 = 0.0f;
+    } else if (iv == 2 || iv == -2) {
+        al1 = q1;
+    }
+}
+
+// d1 = dp(km), d2 = dp(km-1), qk = q(km), qk1 = q(km-1), alk1 = ALraw(km-1)
+FV3_HD inline void ppm_bottom_cubic(float qk, float qk1, float d1, float d2, float alk1, int iv, float& alm,
+                                    float& ar, float& dcm)
+{
+    const float qm = (d2 * qk + d1 * qk1) / (d1 + d2);
+    const float dq = 2.0f * (qk1 - qk) / (d1 + d2);
+    const float c1 = (alk1 - qm - d2 * dq) / (d2 * (2.0f * d2 * d2 + d1 * (d2 + 3.0f * d1)));
+    const float c3 = dq - 2.0f * c1 * (d2 * (5.0f * d1 + d2) - 3.0f * d1 * d1);
+    alm = qm - c1 * d1 * d2 * (d2 + 3.0f * d1);
+    ar = d1 * (8.0f * c1 * (d1 * d1) - c3) + alm;
+    alm = fmax2(alm, fmin2(qk, qk1));
+    alm = fmin2(alm, fmax2(qk, qk1));
+    dcm = 0.5f * (qk - alm);
+    if (iv == 0) {
+        alm = fmax2(0.0f, alm);
+        ar = fmax2(0.0f, ar);
+    } else if (iv < 0) {
+        if (qk * ar <= 0.0f) ar = 0.0f;
+    }
+}
+
+// ---- remap consumer for NF fields (remap_layer_fast / remap_finish semantics) ----
+
+template <int NF>
+struct RemapStateN {
+    int k;
+    bool accum;
+    float dpsum, t, b, xt;
+    bool xv;
+    float qsum[NF];
+};
+
+template <int NF>
+struct LayerViewN {
+    float pl0, pl1, dp;
+    float q1[NF], al[NF], ar[NF], a6[NF];
+};
+
+template <int NF>
+struct ColumnEndsN {
+    float pe_top, pe_bot;
+    float q_top[NF], q_bot[NF];
+};
+
+template <int NF, class Out>
+FV3_HD inline void remap_layer_n(RemapStateN<NF>& s, const LayerViewN<NF>& v, const ColumnEndsN<NF>& e, int kn,
+                                 Out& out)
+{
+    const float r3 = 1.0f / 3.0f, r23 = 2.0f / 3.0f;
+    s.xv = false;
+    if (s.k > kn) return;
+    if (s.accum) {
+        if (s.b > v.pl1) {
+            // whole layer (mappm.f90:99-104)
+            for (int f = 0; f < NF; ++f) s.qsum[f] = s.qsum[f] + v.dp * v.q1[f];
+            s.dpsum = s.dpsum + v.dp;
+            return;
+        }
+        // bottom piece (mappm.f90:105-112)
+        const float delp = s.b - v.pl0;
+        const float esl = delp / v.dp;
+        const float h = 0.5f * esl;
+        const float w = 1.0f - r23 * esl;
+        for (int f = 0; f < NF; ++f)
+            s.qsum[f] = s.qsum[f] + delp * (v.al[f] + h * (v.ar[f] - v.al[f] + v.a6[f] * w));
+        s.dpsum = s.dpsum + delp;
+        for (int f = 0; f < NF; ++f) out.emit(f, s.k, s.qsum[f] / s.dpsum);
+        s.accum = false;
+        s.k += 1;
+        s.t = s.b;
+        s.b = out.next_edge(s.k);
+        s.xt = esl;
+        s.xv = true;
+    }
+    while (s.k <= kn) {
+        bool above = s.t <= e.pe_top;
+        bool bnd = above || s.t >= e.pe_bot;
+        bool inl = !bnd && s.t >= v.pl0 && s.t <= v.pl1;
+        if (!bnd && !inl) return;
+        if (bnd) {
+            for (int f = 0; f < NF; ++f) out.emit(f, s.k, above ? e.q_top[f] : e.q_bot[f]);
+            s.k += 1;
+            s.t = s.b;
+            s.b = out.next_edge(s.k);
+            s.xv = false;
+            continue;
+        }
+        if (!s.xv) s.xt = (s.t - v.pl0) / v.dp;
+        if (s.b <= v.pl1) {
+            // entire new layer inside input layer L (mappm.f90:76-83)
+            const float pl = s.xt;
+            const float pr = (s.b - v.pl0) / v.dp;
+            const float tt = r3 * (pr * (pr + pl) + pl * pl);
+            const float x = pr + pl;
+            for (int f = 0; f < NF; ++f)
+                out.emit(f, s.k, v.al[f] + 0.5f * (v.a6[f] + v.ar[f] - v.al[f]) * x - v.a6[f] * tt);
+            s.k += 1;
+            s.t = s.b;
+            s.b = out.next_edge(s.k);
+            s.xt = pr;
+            s.xv = true;
+            if (s.k > kn) return;
+            above = s.t <= e.pe_top;
+            bnd = above || s.t >= e.pe_bot;
+            inl = !bnd && s.t >= v.pl0 && s.t <= v.pl1;
+            if (!inl || s.b <= v.pl1) continue;
+        }
+        // fractional top piece (mappm.f90:85-92)
+        const float pl = s.xt;
+        const float tt = r3 * (1.0f + pl * (1.0f + pl));
+        const float x = 1.0f + pl;
+        const float delp = v.pl1 - s.t;
+        for (int f = 0; f < NF; ++f)
+            s.qsum[f] = delp * (v.al[f] + 0.5f * (v.a6[f] + v.ar[f] - v.al[f]) * x - v.a6[f] * tt);
+        s.dpsum = delp;
+        s.accum = true;
+        return;
+    }
+}
+
+template <int NF, class Out>
+FV3_HD inline void remap_finish_n(RemapStateN<NF>& s, const ColumnEndsN<NF>& e, int kn, Out& out)
+{
+    while (s.k <= kn) {
+        if (s.accum) {
+            const float delp = s.b - e.pe_bot;
+            if (delp > 0.0f) {
+                for (int f = 0; f < NF; ++f) s.qsum[f] = s.qsum[f] + delp * e.q_bot[f];
+                s.dpsum = s.dpsum + delp;
+            }
+            for (int f = 0; f < NF; ++f) out.emit(f, s.k, s.qsum[f] / s.dpsum);
+            s.accum = false;
+        } else if (s.t <= e.pe_top) {
+            for (int f = 0; f < NF; ++f) out.emit(f, s.k, e.q_top[f]);
+        } else if (s.t >= e.pe_bot) {
+            for (int f = 0; f < NF; ++f) out.emit(f, s.k, e.q_bot[f]);
+        } else {
+            for (int f = 0; f < NF; ++f) out.emit(f, s.k, __builtin_nanf(""));  // search failed: reference UB
+        }
+        s.k += 1;
+        s.t = s.b;
+        s.b = out.next_edge(s.k);
+    }
+}
+
+// ---- NF columns on one pressure column, kord <= 7, fully streaming ----
+template <int NF, class Col>
+FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord)
+{
+    // window state E_L as in mappm_ppm_column, the q-dependent parts per field
+    float qv[NF][4], dcv[NF][3], alv[NF][3], h2v[NF][3], ar_km[NF], q_pf[NF];
+    float dpv[4], pev[5];
+    const bool huynh = kord >= 7;
+
+    for (int f = 0; f < NF; ++f)
+        for (int i = 0; i < 4; ++i) qv[f][i] = c.q1(f, 1 + i);
+    for (int i = 0; i < 5; ++i) pev[i] = c.pe1(1 + i);
+    for (int i = 0; i < 4; ++i) dpv[i] = pev[i + 1] - pev[i];
+
+    ColumnEndsN<NF> ends;
+    ends.pe_top = pev[0];
+    ends.pe_bot = c.pe1(km + 1);
+    for (int f = 0; f < NF; ++f) {
+        ends.q_top[f] = qv[f][0];
+        ends.q_bot[f] = c.q1(f, km);
+    }
+
+    {
+        const DcShared p2 = ppm_dc_shared(dpv[0], dpv[1], dpv[2]);
+        const DcShared p3 = ppm_dc_shared(dpv[1], dpv[2], dpv[3]);
+        const AlShared a3 = ppm_al_shared(dpv[0], dpv[1], dpv[2], dpv[3]);
+        const float hden = dpv[1] + 0.5f * (dpv[0] + dpv[2]);
+        const float d0sq = dpv[1] * dpv[1];
+        for (int f = 0; f < NF; ++f) {
+            const float dc2 = ppm_dc_field(p2, qv[f][0], qv[f][1], qv[f][2], dpv[1]);
+            const float dc3 = ppm_dc_field(p3, qv[f][1], qv[f][2], qv[f][3], dpv[2]);  // 3 <= km-1
+            const float al3 = ppm_al_field(a3, dpv[1], dpv[2], qv[f][1], qv[f][2], dc2, dc3);
+            float al1, al2, dc1;
+            ppm_top_cubic(qv[f][0], qv[f][1], dpv[0], dpv[1], al3, iv, al1, al2, dc1);
+            dcv[f][0] = dc1; dcv[f][1] = dc2; dcv[f][2] = dc3;
+            alv[f][0] = al1; alv[f][1] = al2; alv[f][2] = al3;
+            h2v[f][0] = 0.0f; h2v[f][1] = 0.0f;
+            // h2(2) = ppm_h2(dc1, dc3, dp(1), dp(2), dp(3))
+            h2v[f][2] = huynh ? 2.0f * (dc3 / dpv[2] - dc1 / dpv[0]) / hden * d0sq : 0.0f;
+            ar_km[f] = 0.0f;
+            q_pf[f] = 0.0f;
+        }
+    }
+
+    int lmt = kord - 3;
+    lmt = lmt > 0 ? lmt : 0;
+    if (iv == 0) lmt = lmt < 2 ? lmt : 2;
+
+    RemapStateN<NF> s;
+    s.k = 1;
+    s.accum = false;
+    s.dpsum = 0.0f;
+    s.t = c.pe2(1);
+    s.b = c.pe2(2);
+    s.xt = 0.0f;
+    s.xv = false;
+    for (int f = 0; f < NF; ++f) s.qsum[f] = 0.0f;
+
+    float pe_pf = 0.0f;
+    if (5 <= km) {
+        for (int f = 0; f < NF; ++f) q_pf[f] = c.q1(f, 5);
+        pe_pf = c.pe1(6);
+    }
+
+    for (int L = 1; L <= km; ++L) {
+        // ---- the final coefficients of layer L, per field ----
+        LayerViewN<NF> v;
+        v.pl0 = pev[0];
+        v.pl1 = pev[1];
+        v.dp = dpv[0];
+        for (int f = 0; f < NF; ++f) {
+            Ppm a{qv[f][0], alv[f][0], (L < km) ? alv[f][1] : ar_km[f], 0.0f};
+            const float dcL = dcv[f][0];
+            if (L <= 2 || L >= km - 1) {
+                a.a6 = a6_of(a);
+                ppm_limit(dcL, a, 0);
+            } else if (huynh) {
+                ppm_huynh(a, dcL, h2v[f][0], h2v[f][2]);
+                if (iv == 0) ppm_limit(dcL, a, 2);
+            } else {
+                if (kord != 4) a.a6 = a6_of(a);
+                if (kord != 6) ppm_limit(dcL, a, lmt);
+            }
+            v.q1[f] = qv[f][0];
+            v.al[f] = a.al;
+            v.ar[f] = a.ar;
+            v.a6[f] = a.a6;
+        }
+        remap_layer_n<NF>(s, v, ends, kn, c);
+        layer_hook(c, 0);
+
+        if (L == km) break;
+        // ---- advance the window E_L -> E_{L+1} ----
+        const int j = L + 4;
+        float qn[NF], pen = 0.0f, dpn = 0.0f;
+        for (int f = 0; f < NF; ++f) qn[f] = 0.0f;
+        if (j <= km) {
+            for (int f = 0; f < NF; ++f) qn[f] = q_pf[f];
+            pen = pe_pf;
+            dpn = pen - pev[4];
+        }
+        if (j + 1 <= km) {
+            for (int f = 0; f < NF; ++f) q_pf[f] = c.q1(f, j + 1);
+            pe_pf = c.pe1(j + 2);
+        }
+        const int m = L + 3;
+        float dcm[NF], alm[NF];
+        for (int f = 0; f < NF; ++f) {
+            dcm[f] = 0.0f;
+            alm[f] = 0.0f;
+        }
+        if (m <= km - 1) {
+            const DcShared pd = ppm_dc_shared(dpv[2], dpv[3], dpn);
+            const AlShared pa = ppm_al_shared(dpv[1], dpv[2], dpv[3], dpn);
+            for (int f = 0; f < NF; ++f) {
+                dcm[f] = ppm_dc_field(pd, qv[f][2], qv[f][3], qn[f], dpv[3]);
+                alm[f] = ppm_al_field(pa, dpv[2], dpv[3], qv[f][2], qv[f][3], dcv[f][2], dcm[f]);
+            }
+        } else if (m == km) {
+            for (int f = 0; f < NF; ++f) {
+                float ar;
+                ppm_bottom_cubic(qv[f][3], qv[f][2], dpv[3], dpv[2], alv[f][2], iv, alm[f], ar, dcm[f]);
+                ar_km[f] = ar;
+            }
+        }
+        if (huynh && L + 2 <= km - 1) {  // h2(L+2) = ppm_h2(dc(L+1), dc(L+3), dp(L+1..L+3))
+            const float hden = dpv[2] + 0.5f * (dpv[1] + dpv[3]);
+            const float d0sq = dpv[2] * dpv[2];
+            for (int f = 0; f < NF; ++f) {
+                const float h2n = 2.0f * (dcm[f] / dpv[3] - dcv[f][1] / dpv[1]) / hden * d0sq;
+                h2v[f][0] = h2v[f][1]; h2v[f][1] = h2v[f][2]; h2v[f][2] = h2n;
+            }
+        } else {
+            for (int f = 0; f < NF; ++f) {
+                h2v[f][0] = h2v[f][1]; h2v[f][1] = h2v[f][2]; h2v[f][2] = 0.0f;
+            }
+        }
+        for (int f = 0; f < NF; ++f) {
+            qv[f][0] = qv[f][1]; qv[f][1] = qv[f][2]; qv[f][2] = qv[f][3]; qv[f][3] = qn[f];
+            dcv[f][0] = dcv[f][1]; dcv[f][1] = dcv[f][2]; dcv[f][2] = dcm[f];
+            alv[f][0] = alv[f][1]; alv[f][1] = alv[f][2]; alv[f][2] = alm[f];
+        }
+        dpv[0] = dpv[1]; dpv[1] = dpv[2]; dpv[2] = dpv[3]; dpv[3] = dpn;
+        pev[0] = pev[1]; pev[1] = pev[2]; pev[2] = pev[3]; pev[3] = pev[4]; pev[4] = pen;
+    }
+    remap_finish_n<NF>(s, ends, kn, c);
+}
+
+// A one-field view of an NF-interface column, so NF = 1 runs the single-field
+// streaming code (mappm_ppm_column) on it.
+template <class Col>
+struct FirstField {
+    Col& c;
+    FV3_HD float q1(int k) { return c.q1(0, k); }
+    FV3_HD float pe1(int k) { return c.pe1(k); }
+    FV3_HD float pe2(int k) { return c.pe2(k); }
+    FV3_HD void emit(int k, float v) { c.emit(0, k, v); }
+    FV3_HD float next_edge(int k) { return c.next_edge(k); }
+    FV3_HD void layer_done() { layer_hook(c, 0); }
+};
+
+}  // namespace fv3

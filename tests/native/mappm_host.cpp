@@ -63,3 +63,42 @@ extern "C" int host_mappm_generic(int km, const float* pe1, const float* q1, int
     }
     return 0;
 }
+
+// NF fields on one pressure column in one pass (mappm_multi.h), as the fused coarsen
+// kernel runs them: q1 / q2 hold NF arrays [km][ncol] / [kn][ncol] back to back
+#include "../../fv3net_amd/csrc/mappm_multi.h"
+namespace {
+struct ColN {
+    const float *pe1_, *q1_, *pe2_;
+    float* q2_;
+    int64_t ncol, i;
+    int km, kn;
+    float q1(int f, int k) const { return q1_[((int64_t)f * km + (k - 1)) * ncol + i]; }
+    float pe1(int k) const { return pe1_[(int64_t)(k - 1) * ncol + i]; }
+    float pe2(int k) const { return pe2_[(int64_t)(k - 1) * ncol + i]; }
+    void emit(int f, int k, float v) { q2_[((int64_t)f * kn + (k - 1)) * ncol + i] = v; }
+    float next_edge(int k) const { return (k + 1 <= kn + 1) ? pe2(k + 1) : 0.0f; }
+};
+template <int NF>
+void run_n(int km, const float* pe1, const float* q1, int kn, const float* pe2, float* q2, int64_t ncol, int iv,
+           int kord)
+{
+    for (int64_t i = 0; i < ncol; ++i) {
+        ColN c{pe1, q1, pe2, q2, ncol, i, km, kn};
+        fv3::mappm_ppm_columns<NF>(c, km, kn, iv, kord);
+    }
+}
+}  // namespace
+
+extern "C" int host_mappm_multi(int nf, int km, const float* pe1, const float* q1, int kn, const float* pe2,
+                                float* q2, int64_t ncol, int iv, int kord)
+{
+    if (km < 4 || kn < 1 || kord > 7) return -1;
+    switch (nf) {
+        case 1: run_n<1>(km, pe1, q1, kn, pe2, q2, ncol, iv, kord); return 0;
+        case 2: run_n<2>(km, pe1, q1, kn, pe2, q2, ncol, iv, kord); return 0;
+        case 3: run_n<3>(km, pe1, q1, kn, pe2, q2, ncol, iv, kord); return 0;
+        case 4: run_n<4>(km, pe1, q1, kn, pe2, q2, ncol, iv, kord); return 0;
+    }
+    return -1;
+}

@@ -224,3 +224,38 @@ def test_fast_consumer_equals_reference_loop_unsorted(host_lib, km, kn):
                 fast = _host(host_lib, pe1, q, pe2, iv, kord)
                 ref = _host(host_lib, pe1, q, pe2, iv, kord, cursor="generic")
             assert _bits_equal(fast, ref), (kord, iv)
+
+
+@pytest.mark.parametrize("nf", [1, 2, 3, 4])
+@pytest.mark.parametrize("km,kn", [(4, 40), (79, 79), (79, 50), (20, 5)])
+def test_multi_field_streaming_bit_identical(host_lib, nf, km, kn):
+    """mappm_ppm_columns<NF> (NF fields on one pressure column, the pressure-only
+    divisions, positions and decisions shared) == the single-field streaming column
+    for each field, bit for bit, for every PPM kord and iv, incl. degenerate edges."""
+    import ctypes
+
+    fn = host_lib.host_mappm_multi
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
+    rng = np.random.default_rng(km * 13 + kn * 7 + nf)
+    ncol = 48
+    for kord in (0, 1, 2, 3, 4, 5, 6, 7):
+        for iv in (0, 1, -1, 2, -2):
+            delp = rng.uniform(1, 3000, (km, ncol)).astype(np.float32)
+            delp[rng.random((km, ncol)) < 0.05] = 0.0
+            delp[:2] = np.maximum(delp[:2], 1.0)
+            delp[-2:] = np.maximum(delp[-2:], 1.0)
+            pe1 = np.concatenate([np.full((1, ncol), 300, np.float32),
+                                  300 + np.cumsum(delp, 0, dtype=np.float32)])
+            pe2 = np.sort(rng.uniform(pe1[0] * 0.8, pe1[-1] * 1.1, (kn + 1, ncol)), 0).astype(np.float32)
+            m = min(km, kn) + 1
+            pe2[: m // 3] = pe1[: m // 3]
+            pe2 = np.sort(pe2, 0)
+            q = (rng.normal(0, 1, (nf, km, ncol)) * rng.choice([1e-4, 1, 300], (nf, km, ncol))).astype(np.float32)
+            out = np.empty((nf, kn, ncol), np.float32)
+            with np.errstate(all="ignore"):
+                assert fn(nf, km, pe1.ctypes.data, q.ctypes.data, kn, pe2.ctypes.data, out.ctypes.data, ncol,
+                          iv, kord) == 0
+                for f in range(nf):
+                    assert _bits_equal(out[f], _host(host_lib, pe1, q[f], pe2, iv, kord)), (nf, f, kord, iv)
