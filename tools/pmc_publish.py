@@ -29,8 +29,8 @@ LEGS = {
     "mappm_c384_79to79_kord1": ("mappm_c384_k1", "mappm_ppm_kernel"),
     "mappm_c384_79to79_kord10": ("mappm_c384_k10", "mappm_cs_global_kernel"),
     "mappm_c12_79to50_kord1": ("mappm_c12", "mappm_ppm_levels_kernel"),
-    "coarsen_c384_to_c48_1field": ("coarsen_1f", "regrid_coarsen_kernel"),
-    "coarsen_c384_to_c48_4field": ("coarsen_4f", "regrid_coarsen_kernel"),
+    "coarsen_c384_to_c48_1field": ("coarsen_1f", "regrid_coarsen_cells_kernel"),
+    "coarsen_c384_to_c48_4field": ("coarsen_4f", "regrid_coarsen_cells_kernel"),
     "stepper_c96": ("stepper_c96", "ml_epilogue_kernel"),
     "stepper_c96_predict": ("stepper_c96", "dense_forward_kernel"),
     "predict_mappm_c384": ("predict_mappm_c384", "dense_forward_kernel"),
