@@ -10,6 +10,11 @@ if [ ${#LEGS[@]} -eq 0 ]; then
   LEGS=(calib dense_c48 dense_c384 dense_c384_bf16x3 emulator_c384 emulator_c384_f32 mappm_c384_k1 mappm_c384_k10 mappm_c12 coarsen_1f coarsen_4f stepper_c96)
 fi
 OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out/pmc_${TAG}
+# the calibration kernels of the "calib" leg (tools only; git-ignored build)
+if [ ! -f tools/variants/libcalib.so ]; then
+  mkdir -p tools/variants
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 -o tools/variants/libcalib.so tools/calib.hip
+fi
 mkdir -p "$OUT"; export TMPDIR=/tmp
 SETS=("FETCH_SIZE"
       "WRITE_SIZE"
