@@ -109,7 +109,11 @@ __device__ __forceinline__ void sfor(F&& f)
 // this wave's LDS writes done, then the workgroup barrier; global loads in flight (the
 // next weight chunk, the next inputs) are NOT drained (a __syncthreads() fence would
 // wait vmcnt(0) on gfx9, where loads and stores share the counter)
+#ifdef FV3_B3_EXP_NOBAR  // experiment only (results invalid): no chunk barriers
+__device__ __forceinline__ void b3_barrier() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+#else
 __device__ __forceinline__ void b3_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+#endif
 
 __device__ __forceinline__ float b3_log(float x, float eps) { return x != x ? x : logf(x > eps ? x : eps); }
 
@@ -126,9 +130,13 @@ __device__ __forceinline__ void split8(const float (&y)[8], bf16x8& hi, bf16x8& 
 
 __device__ __forceinline__ b3f4 mma3(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl, b3f4 c)
 {
+#ifdef FV3_B3_EXP_NOMFMA  // experiment only (results invalid): everything but the MFMAs
+    c[0] += (float)ah[0] + (float)al[1] + (float)bh[2] + (float)bl[3];
+#else
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
+#endif
     return c;
 }
 
@@ -192,11 +200,22 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
 #pragma unroll
         for (int t = 0; t < HU; ++t) acc[t] = b3f4{0.0f, 0.0f, 0.0f, 0.0f};
     };
+#ifdef FV3_B3_EXP_NOFRAG
+    bf16x8 fconst[2][2];
+    for (int i = 0; i < 2; ++i)
+        for (int h = 0; h < 2; ++h) fconst[i][h] = *reinterpret_cast<const bf16x8*>(ring + i * 2048 + h * 1024 + lane * 16);
+#endif
     // A fragment i of the chunk in slot sl: hi at i*2048, lo at i*2048 + 1024
     auto frag = [&](int sl, int i, bf16x8 (&f)[2]) {
+#ifdef FV3_B3_EXP_NOFRAG  // experiment only (results invalid): one fragment, no LDS reads per step
+        (void)sl;
+        f[0] = fconst[i & 1][0];
+        f[1] = fconst[i & 1][1];
+#else
         const char* a = ring + sl * CB + i * 2048 + lane * 16;
         f[0] = *reinterpret_cast<const bf16x8*>(a);
         f[1] = *reinterpret_cast<const bf16x8*>(a + 1024);
+#endif
     };
     // fragment i -> (accumulator, B operand) by MAP; fragments are read two ahead
     auto mma_chunk = [&](int sl, auto map) {
@@ -210,8 +229,10 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
         });
     };
     auto stage_next = [&]() {
+#ifndef FV3_B3_EXP_NOSTAGE  // experiment only (results invalid): no weight streaming
         write_stage(slot ^ 1);  // chunk +1 (its slot held chunk -1, released by the last barrier)
         load_stage(jn2);        // chunk +2
+#endif
     };
     auto advance = [&]() {
         b3_barrier();
@@ -253,7 +274,11 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
         const float* ptr = b + (int64_t)lblk * bs + lii;
 #pragma unroll
         for (int j = 0; j < 8; ++j)  // read once: keep them from evicting the weight stream in L2
+#ifdef FV3_B3_EXP_NOIN  // experiment only (results invalid): no input loads
+            raw[j] = j < nv ? 1.0f + (float)(uintptr_t)(ptr + j * ld) * 0.0f : 0.0f;
+#else
             raw[j] = j < nv ? __builtin_nontemporal_load(ptr + j * ld) : 0.0f;
+#endif
     };
     auto stage_in = [&](const float (&raw)[8], int c, bf16x8& bh, bf16x8& bl) {
         const int f0 = 32 * c + 8 * hq;
@@ -357,6 +382,9 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
             y = y * mk[q];
             if (has_res) y = r[q] + y;
             const unsigned off = (ovalid && row < nrow) ? (ob + (unsigned)(z0 + row) * old_) * 4u : 0x80000000u;
+#ifdef FV3_B3_EXP_NOOUT  // experiment only (results invalid): store only a value that is never true
+            if (y == 1234.5f)
+#endif
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, (int)off, 0, 0);
         }
     };
