@@ -104,14 +104,23 @@ def gather_rows_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def sharded_stepper_worker(rank, world, port, out_dir, res, steps):
+def sharded_stepper_worker(rank, world, port, out_dir, res, steps, backend="gloo"):
     """The config #4 sharded stepper (workloads.ShardedStepperWorkload) on one GPU per
-    rank process (gloo for the exchange): global sums and this rank's state band."""
+    rank process (gloo, or nccl = RCCL for a single rank on the box's one GPU, for the
+    exchange): global sums and this rank's state band."""
     import torch
+    import torch.distributed as tdist
 
     from fv3net_amd import workloads as W
 
-    dist = init_gloo(rank, world, port)
+    if backend == "gloo":
+        dist = init_gloo(rank, world, port)
+    else:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        torch.cuda.set_device(0)
+        tdist.init_process_group(backend, rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+        dist = tdist
     torch.cuda.set_device(0)
     wl = W.make_sharded_stepper_workload(res, rank, world, seed=5)
     for _ in range(steps):

@@ -161,3 +161,19 @@ def test_sharded_stepper_two_ranks_bit_identical_to_one(gpu, tmp_path):
         q = np.load(tmp_path / "w2" / f"q{r}.npy")
         assert (q.view(np.uint64) == q1[:, r0:r1].view(np.uint64)).all()
     assert np.isfinite(one).all() and one[6:].sum() > 0  # the limiter engaged somewhere
+
+
+@pytest.mark.gpu
+def test_sharded_stepper_rccl_exchange_matches_gloo(gpu, tmp_path):
+    """The RCCL (nccl backend) branch of the per-step exchange (device tensors in the
+    all-gather) on the box's one GPU (world 1: RCCL runs one rank per device): the same
+    bits as the gloo exchange."""
+    for be in ("gloo", "nccl"):
+        (tmp_path / be).mkdir()
+        _spawn(H.sharded_stepper_worker, 1, str(tmp_path / be), 12, 2, be)
+    a = np.load(tmp_path / "gloo" / "total0.npy")
+    b = np.load(tmp_path / "nccl" / "total0.npy")
+    assert (a.view(np.uint64) == b.view(np.uint64)).all()
+    qa = np.load(tmp_path / "gloo" / "q0.npy")
+    qb = np.load(tmp_path / "nccl" / "q0.npy")
+    assert (qa.view(np.uint64) == qb.view(np.uint64)).all()
