@@ -93,6 +93,20 @@ struct B3Args {
 static_assert(sizeof(B3Args) <= 4096, "kernel arguments are limited to 4 KiB");
 
 typedef __attribute__((address_space(4))) const B3Args KB3;
+
+// layer-1 input group g (8 levels of one variable), resolved once per block into LDS:
+// the lane quarter that reads group g of a k-step takes its address, strides, valid
+// level count and LogTransform epsilon with two LDS reads instead of re-deriving them
+// from gmeta / in[] (per-lane selects of four 64-bit candidates) every k-step
+struct B3Grp {
+    const float* ptr;  // level z0 of the group's variable (column 0)
+    int64_t bs;        // column-block stride
+    int ld;            // level stride (elements)
+    int nv;            // valid levels (0..8)
+    float leps;        // > 0: LogTransform
+    int klog;          // some group of this group's k-step (4 groups) has a LogTransform
+};
+static_assert(sizeof(B3Grp) == 32, "B3Grp is read as two 16-byte words");
 typedef __amdgpu_buffer_rsrc_t Rsrc3;
 
 template <typename F, int... I>
@@ -141,6 +155,25 @@ __device__ __forceinline__ b3f4 mma3(const bf16x8& ah, const bf16x8& al, const b
 }
 
 // value of lane quarter q from 4 wave-uniform candidates
+// two independent accumulations interleaved (c0 <- a0 x b0, c1 <- a1 x b1, each in the
+// hi*hi, lo*hi, hi*lo order of mma3): no MFMA waits on the one just issued
+__device__ __forceinline__ void mma3x2(const bf16x8& ah0, const bf16x8& al0, const bf16x8& bh0, const bf16x8& bl0,
+                                       b3f4& c0, const bf16x8& ah1, const bf16x8& al1, const bf16x8& bh1,
+                                       const bf16x8& bl1, b3f4& c1)
+{
+#ifdef FV3_B3_EXP_NOMFMA
+    c0 = mma3(ah0, al0, bh0, bl0, c0);
+    c1 = mma3(ah1, al1, bh1, bl1, c1);
+#else
+    c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah0, bh0, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah1, bh1, c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al0, bh0, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al1, bh1, c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah0, bl0, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah1, bl1, c1, 0, 0, 0);
+#endif
+}
+
 template <typename T>
 __device__ __forceinline__ T sel4(int q, T a0, T a1, T a2, T a3)
 {
@@ -165,6 +198,7 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
     float* s_rs = s_mean + p.kp1;
     float* s_bias = s_rs + p.kp1;             // [nh][HP]
     float* s_oc = s_bias + (1 + p.nhx) * HP;  // [6][kop]: bias, sigma, mean, lo, hi, mask
+    B3Grp* s_grp = reinterpret_cast<B3Grp*>(ring + 2 * CB + 4 * ((p.nconst + 7) & ~7));  // [4 n1]
     const int kop = p.kop;
 
     const int tid = threadIdx.x;
@@ -174,6 +208,20 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
     const int cl = lane & 15;  // column of this lane inside the wave's 16
 
     for (int i = tid; i < p.nconst; i += kB3Threads) s_mean[i] = p.consts[i];
+    for (int g = tid; g < 4 * p.n1; g += kB3Threads) {
+        const int m = p.gmeta[g], v = m & 15;
+        B3Grp e;
+        e.ptr = p.in[v].ptr + (int64_t)((m >> 4) & 0xfffff) * p.in[v].ld;
+        e.bs = p.in[v].bs;
+        e.ld = (int)p.in[v].ld;
+        e.nv = m >> 24;
+        e.leps = p.in[v].leps;
+        e.klog = 0;
+        for (int i = 4 * (g / 4); i < 4 * (g / 4) + 4; ++i)
+            e.klog |= (p.gmeta[i] >> 24) > 0 && p.in[p.gmeta[i] & 15].leps > 0.0f;
+        s_grp[g] = e;
+    }
+    b3_barrier();  // the group table is read by the first tile's input loads below
 
     // ---- weight stream: LDS ring of 2 chunks, the chunk after next in registers ----
     const Rsrc3 rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.wstream), 0, p.wbytes, 0x00020000);
@@ -217,17 +265,6 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
         f[1] = *reinterpret_cast<const bf16x8*>(a + 1024);
 #endif
     };
-    // fragment i -> (accumulator, B operand) by MAP; fragments are read two ahead
-    auto mma_chunk = [&](int sl, auto map) {
-        bf16x8 fa[3][2];
-        frag(sl, 0, fa[0]);
-        frag(sl, 1, fa[1]);
-        sfor<HU>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            if constexpr (i + 2 < HU) frag(sl, i + 2, fa[(i + 2) % 3]);
-            map(ic, fa[i % 3]);
-        });
-    };
     auto stage_next = [&]() {
 #ifndef FV3_B3_EXP_NOSTAGE  // experiment only (results invalid): no weight streaming
         write_stage(slot ^ 1);  // chunk +1 (its slot held chunk -1, released by the last barrier)
@@ -239,12 +276,20 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
         slot ^= 1;
         jn2 = jn2 + 1 == p.nch ? 0 : jn2 + 1;
     };
-    // layer chunk: unit tile t accumulates A_t x B (one 32-deep k-step)
+    // layer chunk: unit tile t accumulates A_t x B (one 32-deep k-step); tiles in pairs,
+    // their MFMAs interleaved, fragments read one pair ahead
     auto step_layer = [&](const bf16x8& bh, const bf16x8& bl) {
         stage_next();
-        mma_chunk(slot, [&](auto ic, const bf16x8 (&f)[2]) {
-            constexpr int t = decltype(ic)::value;
-            acc[t] = mma3(f[0], f[1], bh, bl, acc[t]);
+        bf16x8 fa[4][2];
+        frag(slot, 0, fa[0]);
+        frag(slot, 1, fa[1]);
+        sfor<HU / 2>([&](auto pc) {
+            constexpr int t0 = 2 * decltype(pc)::value, t1 = t0 + 1;
+            if constexpr (t0 + 2 < HU) {
+                frag(slot, t0 + 2, fa[(t0 + 2) % 4]);
+                frag(slot, t1 + 2, fa[(t1 + 2) % 4]);
+            }
+            mma3x2(fa[t0 % 4][0], fa[t0 % 4][1], bh, bl, acc[t0], fa[t1 % 4][0], fa[t1 % 4][1], bh, bl, acc[t1]);
         });
         advance();
     };
@@ -261,24 +306,22 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
         lii = (unsigned)(cc - b * p.ncol_blk);
     };
     auto load_in = [&](float (&raw)[8], int c) {  // chunk c: group 4c + hq, 8 levels
-        const int m0 = p.gmeta[4 * c], m1 = p.gmeta[4 * c + 1], m2 = p.gmeta[4 * c + 2], m3 = p.gmeta[4 * c + 3];
-        const int m = sel4(hq, m0, m1, m2, m3);
-        auto base = [&](int mg) {
-            const int v = mg & 15;
-            return p.in[v].ptr + (int64_t)((mg >> 4) & 0xfffff) * p.in[v].ld;
-        };
-        const float* b = sel4(hq, base(m0), base(m1), base(m2), base(m3));
-        const int64_t ld = sel4(hq, p.in[m0 & 15].ld, p.in[m1 & 15].ld, p.in[m2 & 15].ld, p.in[m3 & 15].ld);
-        const int64_t bs = sel4(hq, p.in[m0 & 15].bs, p.in[m1 & 15].bs, p.in[m2 & 15].bs, p.in[m3 & 15].bs);
-        const int nv = lvalid ? (m >> 24) : 0;
-        const float* ptr = b + (int64_t)lblk * bs + lii;
+        const B3Grp& g = s_grp[4 * c + hq];
+        const int ld = g.ld;  // the host checks 8 * ld < 2^31
+        const int nv = lvalid ? g.nv : 0;
+        typedef const __attribute__((address_space(1))) float* GPtr;
+        const GPtr ptr = (GPtr)(g.ptr + (int64_t)lblk * g.bs + lii);
+        // all 8 loads issued unconditionally (levels past nv read the group's first level,
+        // always in range, and are zeroed after), so none waits behind a branch
 #pragma unroll
-        for (int j = 0; j < 8; ++j)  // read once: keep them from evicting the weight stream in L2
+        for (int j = 0; j < 8; ++j) {  // read once: keep them from evicting the weight stream in L2
 #ifdef FV3_B3_EXP_NOIN  // experiment only (results invalid): no input loads
-            raw[j] = j < nv ? 1.0f + (float)(uintptr_t)(ptr + j * ld) * 0.0f : 0.0f;
+            const float x = 1.0f + (float)(uintptr_t)(ptr + (j < nv ? j * ld : 0)) * 0.0f;
 #else
-            raw[j] = j < nv ? __builtin_nontemporal_load(ptr + j * ld) : 0.0f;
+            const float x = __builtin_nontemporal_load(ptr + (j < nv ? j * ld : 0));
 #endif
+            raw[j] = j < nv ? x : 0.0f;
+        }
     };
     auto stage_in = [&](const float (&raw)[8], int c, bf16x8& bh, bf16x8& bl) {
         const int f0 = 32 * c + 8 * hq;
@@ -286,17 +329,18 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
         const b3f4 mu1 = *reinterpret_cast<const b3f4*>(s_mean + f0 + 4);
         const b3f4 rs0 = *reinterpret_cast<const b3f4*>(s_rs + f0);
         const b3f4 rs1 = *reinterpret_cast<const b3f4*>(s_rs + f0 + 4);
-        float leps = 0.0f;
-        if (p.any_log)
-            leps = sel4(hq, p.in[p.gmeta[4 * c] & 15].leps, p.in[p.gmeta[4 * c + 1] & 15].leps,
-                        p.in[p.gmeta[4 * c + 2] & 15].leps, p.in[p.gmeta[4 * c + 3] & 15].leps);
         float y[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            float x = raw[j];
-            if (leps > 0.0f) x = b3_log(x, leps);  // LogTransform.forward (transforms.py:123-124)
-            y[j] = (x - (j < 4 ? mu0[j] : mu1[j - 4])) * (j < 4 ? rs0[j] : rs1[j - 4]);
+        for (int j = 0; j < 8; ++j) y[j] = raw[j];
+        // the log path only for k-steps that hold a LogTransform group (uniform branch)
+        if (p.any_log && __builtin_amdgcn_readfirstlane(s_grp[4 * c].klog)) {
+            const float leps = s_grp[4 * c + hq].leps;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)  // LogTransform.forward (transforms.py:123-124)
+                if (leps > 0.0f) y[j] = b3_log(y[j], leps);
         }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = (y[j] - (j < 4 ? mu0[j] : mu1[j - 4])) * (j < 4 ? rs0[j] : rs1[j - 4]);
         split8(y, bh, bl);
     };
 
@@ -320,10 +364,18 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
         });
     };
     // output chunk: fragment i = 2q + ts accumulates tile ts of the chunk over k-step q
-    auto step_out = [&]() {
-        mma_chunk(slot, [&](auto ic, const bf16x8 (&f)[2]) {
-            constexpr int i = decltype(ic)::value;
-            acc[i & 1] = mma3(f[0], f[1], Bh[i >> 1], Bl[i >> 1], acc[i & 1]);
+    auto step_out = [&]() {  // fragments 2q, 2q+1: k-step q of tiles 0 and 1, interleaved
+        bf16x8 fa[4][2];
+        frag(slot, 0, fa[0]);
+        frag(slot, 1, fa[1]);
+        sfor<HU / 2>([&](auto qc) {
+            constexpr int q = decltype(qc)::value, i0 = 2 * q, i1 = i0 + 1;
+            if constexpr (i0 + 2 < HU) {
+                frag(slot, i0 + 2, fa[(i0 + 2) % 4]);
+                frag(slot, i1 + 2, fa[(i1 + 2) % 4]);
+            }
+            mma3x2(fa[i0 % 4][0], fa[i0 % 4][1], Bh[q], Bl[q], acc[0], fa[i1 % 4][0], fa[i1 % 4][1], Bh[q], Bl[q],
+                   acc[1]);
         });
     };
 
@@ -664,6 +716,8 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
         FV3_REQUIRE(inputs[v], "dense_forward_ex: input %d is NULL", v);
         FV3_REQUIRE(layout_ok(in_l[v], ncol) && in_l[v].ncol_blk == nb,
                     "dense_forward_ex: input %d layout invalid or ncol_blk differs", v);
+        FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, in_l[v].ld < ((int64_t)1 << 28),
+                         "dense_forward_ex: input %d level stride >= 2^28 elements (bf16x3 path)", v);
         a.in[v] = B3InVar{inputs[v], in_l[v].ld, in_l[v].blk_stride, m->in_log_eps[v], 0};
     }
     for (int v = 0; v < m->n_out; ++v) {
@@ -713,7 +767,7 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
     const void* kfn = b.hu == 4 ? (const void*)dense_b3_kernel<4>
                       : b.hu == 8 ? (const void*)dense_b3_kernel<8>
                                   : (const void*)dense_b3_kernel<16>;
-    const size_t lds = (size_t)2 * 2048 * b.hu + (size_t)4 * b.nconst;
+    const size_t lds = (size_t)2 * 2048 * b.hu + (size_t)4 * ((b.nconst + 7) & ~7) + sizeof(B3Grp) * 4 * b.n1;
     FV3_REQUIRE(lds <= 160 * 1024, "dense_forward_ex: model needs %zu bytes of LDS", lds);
     static std::mutex mu;
     static int n_cu = 0;
