@@ -220,9 +220,10 @@ def scaling_legs(dev, dist, rank, world, settle_ms=150.0):
 
 
 def host_to_host(dev, res, steps=10):
-    """The reference's boundary crossing: float64 host (numpy) T/q in, pageable H2D
-    copies, the fused predict reading float64 in place, float32 dQ1/dQ2 copied back to
-    host numpy (pure_keras.py:98-118 runs on host arrays).  Wall time per step."""
+    """The reference's boundary crossing: float64 host (numpy) T/q in, H2D through the
+    product's pinned double-buffered staging (fv3net_amd/transfer.py), the fused
+    predict reading float64 in place, float32 dQ1/dQ2 copied back to host numpy the same
+    way (pure_keras.py:98-118 runs on host arrays).  Wall time per step."""
     import torch
 
     from fv3net_amd import workloads as W
@@ -235,12 +236,14 @@ def host_to_host(dev, res, steps=10):
     bound = wl.model.bind([dT, dq], level_axes=[1, 1])
     host_out = [np.empty(T.shape, np.float32), np.empty(T.shape, np.float32)]
 
-    def step():
-        dT.copy_(torch.from_numpy(T))
-        dq.copy_(torch.from_numpy(q))
+    from fv3net_amd import transfer
+
+    def step():  # the product's host boundary: pinned, double-buffered staging both ways
+        transfer.h2d(T, out=dT)
+        transfer.h2d(q, out=dq)
         outs = bound()
         for h, o in zip(host_out, outs):
-            h[...] = o.cpu().numpy()
+            transfer.d2h(o, out=h)
 
     for _ in range(2):
         step()
@@ -252,7 +255,7 @@ def host_to_host(dev, res, steps=10):
     nbytes = T.nbytes + q.nbytes + sum(h.nbytes for h in host_out)
     return {"columns_per_s": wl.ncol / wall, "ms_per_step": wall * 1e3, "host_bytes_per_step": nbytes,
             "pcie_inclusive_gbs": nbytes / wall / 1e9,
-            "note": "float64 numpy in -> pageable H2D -> fused predict (f64 read in place) -> D2H float32 numpy"}
+            "note": "float64 numpy in -> pinned double-buffered H2D -> fused predict (f64 read in place) -> pinned D2H -> float32 numpy"}
 
 
 def reference_mappm_cpu(seconds=5.0):

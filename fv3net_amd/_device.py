@@ -31,7 +31,17 @@ def to_device_f32(x, device=None, contiguous: bool = True):
     if isinstance(x, torch.Tensor):
         t = x.to(device=dev, dtype=torch.float32)
     else:
-        t = torch.from_numpy(np.ascontiguousarray(np.asarray(x, dtype=np.float32))).to(dev)
+        a = np.asarray(x)
+        if a.dtype in (np.float32, np.float64):
+            # pinned, double-buffered H2D of the array's own bytes; a float64 host array
+            # is cast on the device (round to nearest, as numpy's astype)
+            from . import transfer
+
+            t = transfer.h2d(a, device=dev)
+            if t.dtype != torch.float32:
+                t = t.to(torch.float32)
+        else:
+            t = torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.float32))).to(dev)
     return t.contiguous() if contiguous else t
 
 

@@ -313,6 +313,15 @@ def _as_contig(t):
     return np.ascontiguousarray(t)
 
 
+def _to_host(t) -> np.ndarray:
+    """A device output back to numpy (pinned, double-buffered D2H), or a host tensor's view."""
+    if t.is_cuda:
+        from .transfer import d2h
+
+        return d2h(t)
+    return t.detach().numpy()
+
+
 def _make_output(X, result: Dict, xr_in: bool):
     """Build the output dataset of the input's kind; coords copied from the input."""
     coords = getattr(X, "coords", {})
@@ -321,7 +330,7 @@ def _make_output(X, result: Dict, xr_in: bool):
 
         data_vars = {}
         for name, (dims, t) in result.items():
-            arr = t.detach().cpu().numpy() if hasattr(t, "detach") else np.asarray(t)
+            arr = _to_host(t) if hasattr(t, "detach") else np.asarray(t)
             data_vars[name] = xr.DataArray(arr, dims=dims, coords={d: coords[d] for d in dims if d in coords})
         return xr.Dataset(data_vars)
     out = dsmod.Dataset()
@@ -330,7 +339,7 @@ def _make_output(X, result: Dict, xr_in: bool):
         src_is_torch = any(torch is not None and isinstance(dsmod.variable_data(X, n), torch.Tensor)
                            for n in X)
         if not src_is_torch and hasattr(t, "detach"):
-            data = t.detach().cpu().numpy()
+            data = _to_host(t)
         out[name] = dsmod.DataArray(data, dims, {d: coords[d] for d in dims if d in coords})
     return out
 

@@ -1,0 +1,43 @@
+"""Host <-> device staging (fv3net_amd/transfer.py): bytes unchanged for every size
+(empty, below / at / across the chunk size), dtype and shape; the predictor's numpy
+path through it equals its device path."""
+import numpy as np
+import pytest
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [np.float32, np.float64, np.uint8, np.int64])
+def test_round_trip_bit_exact(gpu, dtype):
+    import torch
+
+    from fv3net_amd import transfer
+
+    st = transfer.PinnedStager(torch.device("cuda", 0), chunk_bytes=1 << 16, threads=4, min_staged=1 << 12)
+    rng = np.random.default_rng(3)
+    for n in (0, 1, 1000, (1 << 16) // np.dtype(dtype).itemsize, 3 * (1 << 16) + 17, 1 << 20):
+        a = (rng.normal(0, 1e3, n) if np.dtype(dtype).kind == "f" else rng.integers(0, 200, n)).astype(dtype)
+        a = a.reshape(-1, 1) if n else a
+        t = st.h2d(a)
+        assert t.is_cuda and tuple(t.shape) == a.shape
+        ref = torch.from_numpy(np.ascontiguousarray(a)).cuda()
+        assert torch.equal(t, ref)
+        t2 = t * 1 if np.dtype(dtype).kind != "u" else t.clone()  # produced on the current stream
+        back = st.d2h(t2)
+        assert back.dtype == a.dtype and back.shape == a.shape
+        assert (back.view(np.uint8) == a.view(np.uint8)).all()
+        out = np.empty_like(a)
+        st.d2h(t2, out=out)
+        assert (out.view(np.uint8) == a.view(np.uint8)).all()
+    with pytest.raises(ValueError):
+        st.h2d(np.zeros(10, dtype), out=torch.empty(11, dtype=torch.from_numpy(np.zeros(1, dtype)).dtype,
+                                                     device="cuda"))
+
+
+@pytest.mark.gpu
+def test_float64_host_inputs_cast_on_device(gpu):
+    """to_device_f32 on float64 numpy: the device cast equals numpy's astype."""
+    from fv3net_amd import _device
+
+    a = np.random.default_rng(0).normal(0, 1, (79, 3000)) * 10.0 ** np.random.default_rng(1).integers(-30, 30, (79, 1))
+    t = _device.to_device_f32(a)
+    assert (t.cpu().numpy().view(np.uint32) == a.astype(np.float32).view(np.uint32)).all()
