@@ -21,6 +21,7 @@ EXPORTED_SYMBOLS = (
     "fv3_abi_version",
     "fv3_mappm",
     "fv3_mappm_ex",
+    "fv3_mappm_multi",
     "fv3_dense_create",
     "fv3_dense_destroy",
     "fv3_dense_k_in",
@@ -155,6 +156,8 @@ _SIGNATURES = {
     "fv3_abi_version": (_I, []),
     "fv3_mappm": (_I, [_P, _P, _P, _P, _I64, _I, _I, _I, _I, _F, _P]),
     "fv3_mappm_ex": (_I, [_P, Layout, _P, Layout, _P, Layout, _P, Layout, _I64, _I, _I, _I, _I, _F, _P]),
+    "fv3_mappm_multi": (_I, [_P, Layout, ctypes.POINTER(_P), ctypes.POINTER(Layout), _P, Layout, ctypes.POINTER(_P),
+                             ctypes.POINTER(Layout), _I, _I64, _I, _I, _I, _I, _F, _P]),
     "fv3_dense_create": (_I, [ctypes.POINTER(DenseDesc), ctypes.POINTER(_P)]),
     "fv3_dense_destroy": (_I, [_P]),
     "fv3_dense_set_trace": (_I, [_P, _P]),

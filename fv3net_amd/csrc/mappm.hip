@@ -15,6 +15,7 @@
 #define FV3_HD __host__ __device__
 #include "common.h"
 #include "mappm_core.h"
+#include "mappm_multi.h"
 
 #include <cstdlib>
 
@@ -339,6 +340,67 @@ int launch_mappm(MappmArgs a, hipStream_t stream)
     return FV3_OK;
 }
 
+// ---- two fields on one column's edges (fv3_mappm_multi) ----
+
+struct MappmPairArgs {
+    const float* pe1;
+    const float* pe2;
+    fv3_layout l_pe1, l_pe2;
+    const float* q1[2];
+    float* q2[2];
+    fv3_layout l_q1[2], l_q2[2];
+    int64_t ncol;
+    int km, kn, iv, kord;
+};
+
+// DevCol for mappm_ppm_columns<2>: fields f = 0, 1 emit output k in turn, so each keeps
+// its own running output pointer
+struct DevColPair {
+    const float* pe1_;
+    const float* pe2_;
+    const float* q1_[2];
+    float* q2_[2];
+    int64_t ld_pe1, ld_pe2, ld_q1[2], ld_q2[2];
+    int kn;
+    const float* pe2_next;
+    __device__ __forceinline__ float q1(int f, int k) const { return q1_[f][(int64_t)(k - 1) * ld_q1[f]]; }
+    __device__ __forceinline__ float pe1(int k) const { return pe1_[(int64_t)(k - 1) * ld_pe1]; }
+    __device__ __forceinline__ float pe2(int k) const { return pe2_[(int64_t)(k - 1) * ld_pe2]; }
+    __device__ __forceinline__ void emit(int f, int, float v)
+    {
+        *q2_[f] = v;
+        q2_[f] += ld_q2[f];
+    }
+    __device__ __forceinline__ float next_edge(int k)
+    {
+        if (k + 1 > kn + 1) return 0.0f;
+        const float r = *pe2_next;
+        pe2_next += ld_pe2;
+        return r;
+    }
+};
+
+__global__ __launch_bounds__(256) void mappm_ppm_pair_kernel(MappmPairArgs a)
+{
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.ncol) return;
+    DevColPair d;
+    d.pe1_ = a.pe1 + col_offset(a.l_pe1, c);
+    d.pe2_ = a.pe2 + col_offset(a.l_pe2, c);
+    d.ld_pe1 = a.l_pe1.ld;
+    d.ld_pe2 = a.l_pe2.ld;
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+        d.q1_[f] = a.q1[f] + col_offset(a.l_q1[f], c);
+        d.q2_[f] = a.q2[f] + col_offset(a.l_q2[f], c);
+        d.ld_q1[f] = a.l_q1[f].ld;
+        d.ld_q2[f] = a.l_q2[f].ld;
+    }
+    d.kn = a.kn;
+    d.pe2_next = d.pe2_ + 2 * d.ld_pe2;
+    mappm_ppm_columns<2>(d, a.km, a.kn, a.iv, a.kord);
+}
+
 }  // namespace fv3
 
 using fv3::MappmArgs;
@@ -367,4 +429,47 @@ extern "C" int fv3_mappm(const float* pe1, const float* q1, const float* pe2, fl
 {
     const fv3_layout l = fv3::plain_layout(ncol > 0 ? ncol : 1);
     return fv3_mappm_ex(pe1, l, q1, l, pe2, l, q2, l, ncol, km, kn, iv, kord, ptop, stream);
+}
+
+extern "C" int fv3_mappm_multi(const float* pe1, fv3_layout pe1_l, const float* const* q1, const fv3_layout* q1_l,
+                               const float* pe2, fv3_layout pe2_l, float* const* q2, const fv3_layout* q2_l,
+                               int n_fields, int64_t ncol, int km, int kn, int iv, int kord, float ptop,
+                               void* stream)
+{
+    fv3::clear_error();
+    FV3_REQUIRE(n_fields >= 1 && n_fields <= 64, "mappm_multi: n_fields must be in 1..64 (got %d)", n_fields);
+    FV3_REQUIRE(q1 && q1_l && q2 && q2_l, "mappm_multi: NULL field array");
+    FV3_REQUIRE(ncol >= 0, "mappm: ncol must be >= 0 (got %lld)", (long long)ncol);
+    FV3_REQUIRE(km >= 4, "mappm: km must be >= 4 (got %d)", km);
+    FV3_REQUIRE(kn >= 1, "mappm: kn must be >= 1 (got %d)", kn);
+    if (ncol == 0) return FV3_OK;
+    FV3_REQUIRE(pe1 && pe2, "mappm: NULL array");
+    FV3_REQUIRE(fv3::layout_ok(pe1_l, ncol) && fv3::layout_ok(pe2_l, ncol), "mappm: invalid column layout");
+    for (int f = 0; f < n_fields; ++f) {
+        FV3_REQUIRE(q1[f] && q2[f], "mappm_multi: NULL field %d", f);
+        FV3_REQUIRE(fv3::layout_ok(q1_l[f], ncol) && fv3::layout_ok(q2_l[f], ncol),
+                    "mappm_multi: invalid column layout of field %d", f);
+    }
+    FV3_REQUIRE(ncol / 256 < (int64_t)0x7fffffff, "mappm: ncol too large");
+    const hipStream_t s = (hipStream_t)stream;
+    int f = 0;
+    // pairs on the streaming kord <= 7 kernel; the level-parallel (small grids) and
+    // cs_profile (kord > 7) paths, and an odd last field, one field per launch
+    MappmArgs one{pe1, nullptr, pe2, nullptr, pe1_l, {}, pe2_l, {}, ncol, km, kn, iv, kord, nullptr};
+    if (kord <= 7 && !fv3::use_levels_kernel(one)) {
+        for (; f + 2 <= n_fields; f += 2) {
+            fv3::MappmPairArgs a{pe1, pe2, pe1_l, pe2_l, {q1[f], q1[f + 1]}, {q2[f], q2[f + 1]},
+                                 {q1_l[f], q1_l[f + 1]}, {q2_l[f], q2_l[f + 1]}, ncol, km, kn, iv, kord};
+            const int block = 256;
+            const int64_t grid = (ncol + block - 1) / block;
+            hipLaunchKernelGGL(fv3::mappm_ppm_pair_kernel, dim3((unsigned)grid), dim3(block), 0, s, a);
+            FV3_LAUNCH_CHECK();
+        }
+    }
+    for (; f < n_fields; ++f) {
+        const int st = fv3_mappm_ex(pe1, pe1_l, q1[f], q1_l[f], pe2, pe2_l, q2[f], q2_l[f], ncol, km, kn, iv, kord,
+                                    ptop, stream);
+        if (st != FV3_OK) return st;
+    }
+    return FV3_OK;
 }

@@ -6,6 +6,8 @@ calls ``mappm.mappm(p_in, f_in, p_out, 1, n_columns, iv, kord, dummy_ptop)``
 with C-ordered ``(ncol, nlev)`` float64 arrays and gets ``(ncol, kn)`` float32
 back (``regridz.py:268-275``, dtype pinned by ``tests/test_mappm.py:14,28,42``).
 """
+import ctypes
+
 import numpy as np
 
 from . import _device, _native
@@ -66,6 +68,77 @@ class MappmPlan:
         self._fn = _native.load().fv3_mappm_ex
         self._args = (_device.ptr(pe1), l1, _device.ptr(q1), lq, _device.ptr(pe2), l2, _device.ptr(self.out), lo,
                       ncol, km, kp2 - 1, int(iv), int(kord), 0.0, _device.stream_handle(stream))
+
+    def __call__(self):
+        _native.check(self._fn(*self._args), "mappm")
+        return self.out
+
+
+def _multi_args(pe1, q1s, pe2, iv, kord, outs, stream):
+    """Validated argument tuple of fv3_mappm_multi (+ the outputs and the tensors read)."""
+    _device.require_gpu()
+    q1s = list(q1s)
+    if not 1 <= len(q1s) <= 64:
+        raise ValueError("mappm_multi: 1..64 fields")
+    for a in [pe1, pe2] + q1s:
+        if len(getattr(a, "shape", ())) != 2:
+            raise ValueError("pe1, q1, pe2 must be 2-D [level, column]")
+    pe1, l1, n1, kp1 = _device.column_view(pe1, 0)
+    pe2, l2, n2, kp2 = _device.column_view(pe2, 0)
+    kn = kp2 - 1
+    views = [_device.column_view(q, 0) for q in q1s]
+    for _, _, ncol, km in views:
+        if kp1 != km + 1:
+            raise ValueError("f_in must have a vertical dimension one shorter than p_in")
+        if ncol != n1 or n2 != n1:
+            raise ValueError("All dimensions except vertical must be same size for p_in, f_in and p_out")
+    ncol = n1
+    if outs is None:
+        outs = [torch.empty((kn, ncol), dtype=torch.float32, device=pe1.device) for _ in q1s]
+    outs = list(outs)
+    if len(outs) != len(q1s):
+        raise ValueError("mappm_multi: one output per field")
+    for o in outs:
+        if tuple(o.shape) != (kn, ncol) or o.dtype != torch.float32:
+            raise ValueError(f"out must be float32 ({kn}, {ncol})")
+    lo = [_device.level_layout(o, 0)[0] for o in outs]
+    nf = len(q1s)
+    qp = (ctypes.c_void_p * nf)(*[_device.ptr(v[0]) for v in views])
+    ql = (_native.Layout * nf)(*[v[1] for v in views])
+    op = (ctypes.c_void_p * nf)(*[_device.ptr(o) for o in outs])
+    ol = (_native.Layout * nf)(*lo)
+    args = (_device.ptr(pe1), l1, qp, ql, _device.ptr(pe2), l2, op, ol, nf, ncol, views[0][3], kn, int(iv),
+            int(kord), 0.0, _device.stream_handle(stream))
+    return args, outs, [pe1, pe2] + [v[0] for v in views]
+
+
+def mappm_device_multi(pe1, q1s, pe2, iv: int = 1, kord: int = 1, out=None, stream=None):
+    """``mappm_device`` for several fields on the same ``pe1`` / ``pe2`` (one reference
+    ``mappm.mappm`` call per field, as ``coarsen_restarts_on_pressure`` issues them,
+    coarsen_restarts.py:411-516): for kord <= 7 the fields go two per streaming pass,
+    sharing the pressure-only arithmetic; each result is bit-identical to
+    ``mappm_device`` on that field.  Returns the list of ``[kn, ncol]`` outputs."""
+    args, outs, keep = _multi_args(pe1, q1s, pe2, iv, kord, out, stream)
+    _native.check(_native.load().fv3_mappm_multi(*args), "mappm")
+    del keep
+    return outs
+
+
+class MappmMultiPlan:
+    """``MappmPlan`` for ``mappm_device_multi``: one C-ABI call per step on fixed
+    float32 CUDA buffers (read in place; a copy would go stale, so it is refused)."""
+
+    def __init__(self, pe1, q1s, pe2, iv: int = 1, kord: int = 1, out=None, stream=None):
+        q1s = list(q1s)
+        args, self.out, keep = _multi_args(pe1, q1s, pe2, iv, kord, out, stream)
+        for name, a, v in zip(["pe1", "pe2"] + [f"q1[{i}]" for i in range(len(q1s))], [pe1, pe2] + q1s, keep):
+            if not (torch.is_tensor(a) and a.is_cuda and v.data_ptr() == a.data_ptr()):
+                raise ValueError(f"MappmMultiPlan: {name} is read through a copy (host, float64 or an "
+                                 "unaddressable layout); pass float32 CUDA buffers")
+        self._keep = keep
+        self._fn = _native.load().fv3_mappm_multi
+        self._args = args
+        self()
 
     def __call__(self):
         _native.check(self._fn(*self._args), "mappm")

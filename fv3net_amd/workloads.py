@@ -290,7 +290,7 @@ class PredictMappmWorkload:
     dQ1/dQ2 from T/q, then both tendencies remapped (mappm, kord 1, iv 1) from the state's
     edge pressures pe1 = 300 Pa + cumsum(delp) to 79 layers evenly spaced between the
     same top and surface (a per-column pressure-level regrid of the ML tendencies), all
-    device-resident: one dense kernel and two mappm kernels per step."""
+    device-resident: one dense kernel and one two-field mappm kernel per step."""
     model: DenseColumnModel
     inputs: List
     outputs: List
@@ -305,16 +305,16 @@ class PredictMappmWorkload:
     _plans: object = None
 
     def step(self):
-        from .mappm import MappmPlan
+        from .mappm import MappmMultiPlan
 
         if self._bound is None:
             self._bound = self.model.bind(self.inputs, level_axes=[0, 0], outputs=self.outputs, out_level_axis=0)
-            self._plans = [MappmPlan(self.pe1, o.view(o.shape[0], -1), self.pe2, 1, 1, out=r)
-                           for o, r in zip(self.outputs, self.remapped)]
+            # both tendencies in one streaming pass over the shared edges
+            self._plans = MappmMultiPlan(self.pe1, [o.view(o.shape[0], -1) for o in self.outputs], self.pe2, 1, 1,
+                                         out=self.remapped)
         else:
             self._bound()
-            for p in self._plans:
-                p()
+            self._plans()
 
 
 def make_predict_mappm_workload(res: int = 384, rank: int = 0, world: int = 1, seed: int = 0, device=None):

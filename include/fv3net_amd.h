@@ -79,6 +79,17 @@ int fv3_mappm_ex(const float* pe1, fv3_layout pe1_l, const float* q1, fv3_layout
                  const float* pe2, fv3_layout pe2_l, float* q2, fv3_layout q2_l, int64_t ncol,
                  int km, int kn, int iv, int kord, float ptop, void* stream);
 
+/* n_fields fields remapped onto the same edges: one mappm.mappm call per variable on a
+ * shared p_in / p_out, as regrid_vertical is used by coarsen_restarts_on_pressure
+ * (external/vcm/vcm/cubedsphere/coarsen_restarts.py:411-516, regridz.py:164-279).
+ * q1[f] / q2[f] with layouts q1_l[f] / q2_l[f] (host arrays of n_fields device
+ * pointers / layouts).  For kord <= 7 fields go two per streaming pass, sharing the
+ * pressure-only arithmetic (csrc/mappm_multi.h); every field's result carries exactly
+ * the bits of fv3_mappm_ex on that field alone.  1 <= n_fields <= 64. */
+int fv3_mappm_multi(const float* pe1, fv3_layout pe1_l, const float* const* q1, const fv3_layout* q1_l,
+                    const float* pe2, fv3_layout pe2_l, float* const* q2, const fv3_layout* q2_l,
+                    int n_fields, int64_t ncol, int km, int kn, int iv, int kord, float ptop, void* stream);
+
 /* ---- dense column model: DenseModel predict graph (dense.py:234-305) ----------
  * inputs -> per-input clip (clip.py:65-83) -> StandardNormLayer (x-mean)/(sigma+eps)
  * (emulation/layers/normalization.py:121-139) -> concat (utils.py:65-86) ->
