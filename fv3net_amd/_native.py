@@ -56,6 +56,7 @@ EXPORTED_SYMBOLS = (
     "fv3_ml_epilogue_ex",
     "fv3_tendency_columns",
     "fv3_range_mask",
+    "fv3_time_blend",
     "fv3_classify_one_hot",
     "fv3_zc_infer_gscond_cloud",
     "fv3_zc_squash",
@@ -197,6 +198,7 @@ _SIGNATURES = {
     "fv3_level_row_sums_u8": (_I, [_P, _I, _I64, _I, _I64, _P, _I64, _P]),
     "fv3_level_row_sums_f64": (_I, [_P, _I, _I64, _I, _I64, _P, _I64, _P]),
     "fv3_fold_rows": (_I, [_P, _I64, _I, _P, _P]),
+    "fv3_time_blend": (_I, [_P, _I, _P, _I, _P, _I64, _D, _P]),
     "fv3_range_mask": (_I, [_P, _P, _I64, _D, _D, _I, _I, _I, _P]),
     "fv3_classify_one_hot": (_I, [_P, _I, _I64, _P, _I, _I, _I, _P]),
     "fv3_zc_infer_gscond_cloud": (_I, [_P, _P, _P, _P, _I64, _I, _P]),

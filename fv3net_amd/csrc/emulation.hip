@@ -3,6 +3,8 @@
 // What external/emulation does to the emulator's prediction before it goes back to the
 // Fortran state, on the hook's [feature, sample] arrays (_emulate/microphysics.py:83-101):
 //   fv3_range_mask            RangeMask: np.maximum / np.minimum clamps      masks.py:23-39
+//   fv3_time_blend            TimeMask: state * alpha + emulator * (1 - alpha)
+//                                                         _emulate/microphysics.py:37-47
 //   fv3_classify_one_hot      _get_classify_output: one-hot of the class logits where
 //                             they equal their max over the class axis, plus
 //                             nontrivial = positive | negative                 zhao_carr.py:214-219
@@ -308,6 +310,42 @@ inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 
 using namespace fv3;
 
 #define FV3_DISPATCH(f64, CALL) ((f64) ? CALL(double) : CALL(float))
+
+// TimeMask's blend with numpy's dtype flow: each product in its array's dtype (the
+// Python-float weight cast to it, NumPy's weak scalars), the sum in the promoted dtype
+template <typename TS, typename TE, typename TO>
+__global__ __launch_bounds__(256) void time_blend_kernel(const TS* __restrict__ s, const TE* __restrict__ e,
+                                                         TO* __restrict__ out, int64_t n, TS alpha, TE beta)
+{
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const TS a = s[i] * alpha;
+        const TE b = e[i] * beta;
+        out[i] = (TO)a + (TO)b;
+    }
+}
+
+template <typename TS, typename TE, typename TO>
+static void launch_blend(const void* s, const void* e, void* out, int64_t n, double alpha, hipStream_t st)
+{
+    hipLaunchKernelGGL((time_blend_kernel<TS, TE, TO>), dim3(grid_for(n, 256)), dim3(256), 0, st, (const TS*)s,
+                       (const TE*)e, (TO*)out, n, (TS)alpha, (TE)(1.0 - alpha));
+}
+
+extern "C" int fv3_time_blend(const void* state, int state_f64, const void* emulator, int emulator_f64, void* out,
+                              int64_t n, double alpha, void* stream)
+{
+    clear_error();
+    FV3_REQUIRE(n >= 0, "time_blend: n must be >= 0");
+    if (n == 0) return FV3_OK;
+    FV3_REQUIRE(state && emulator && out, "time_blend: NULL array");
+    hipStream_t st = (hipStream_t)stream;
+    if (state_f64 && emulator_f64) launch_blend<double, double, double>(state, emulator, out, n, alpha, st);
+    else if (state_f64) launch_blend<double, float, double>(state, emulator, out, n, alpha, st);
+    else if (emulator_f64) launch_blend<float, double, double>(state, emulator, out, n, alpha, st);
+    else launch_blend<float, float, float>(state, emulator, out, n, alpha, st);
+    FV3_LAUNCH_CHECK();
+    return FV3_OK;
+}
 
 extern "C" int fv3_range_mask(const void* x, void* out, int64_t n, double lo, double hi, int has_lo, int has_hi,
                               int f64, void* stream)

@@ -19,6 +19,7 @@ share a dtype, e.g. the all-float32 and all-float64 hooks).  Not mirrored: the
 transforms around a loaded TF model (the MicrophysicsEmulator graph has its own).
 """
 import dataclasses
+import datetime
 from typing import Callable, Dict, Iterable, Mapping, Optional, Sequence, Union
 
 from . import _device, _native
@@ -97,6 +98,75 @@ def compose_masks(funcs: Iterable[Mask]) -> Mask:
         return out
 
     return composed
+
+
+# ------------------------------------------------------------ _emulate/microphysics.py
+@dataclasses.dataclass(frozen=True)
+class JulianTime:
+    """A date on the Julian calendar (what cftime.DatetimeJulian holds for the schedule,
+    _time.py:6-13; cftime is not a dependency here): subtraction gives the exact
+    ``datetime.timedelta`` between two such dates."""
+    year: int
+    month: int
+    day: int
+    hour: int = 0
+    minute: int = 0
+    second: int = 0
+
+    def _seconds(self) -> int:
+        a = (14 - self.month) // 12
+        y = self.year + 4800 - a
+        m = self.month + 12 * a - 3
+        jdn = self.day + (153 * m + 2) // 5 + 365 * y + y // 4 - 32083  # Julian-calendar day number
+        return ((jdn * 24 + self.hour) * 60 + self.minute) * 60 + self.second
+
+    def __sub__(self, other: "JulianTime") -> datetime.timedelta:
+        return datetime.timedelta(seconds=self._seconds() - other._seconds())
+
+
+def translate_time(time) -> JulianTime:
+    """_time.py:6-13: the Fortran model_time array; index 3 is skipped, as there."""
+    return JulianTime(int(time[0]), int(time[1]), int(time[2]), int(time[4]), int(time[5]))
+
+
+@dataclasses.dataclass
+class IntervalSchedule:
+    """_emulate/microphysics.py:23-34: 1.0 in the first half of every ``period`` after
+    ``initial_time``, else 0.0."""
+    period: datetime.timedelta
+    initial_time: JulianTime
+
+    def __call__(self, time: JulianTime) -> float:
+        fraction_of_interval = ((time - self.initial_time) / self.period) % 1
+        return 1.0 if fraction_of_interval < 0.5 else 0.0
+
+
+class TimeMask:
+    """_emulate/microphysics.py:37-47: ``state * alpha + emulator * (1 - alpha)`` for the
+    keys both hold, alpha = ``schedule(model time)``; arrays blend on the device
+    (fv3_time_blend, numpy's dtype flow), Python numbers as Python does."""
+
+    def __init__(self, schedule: Callable):
+        self.schedule = schedule
+
+    def __call__(self, state, emulator):
+        alpha = float(self.schedule(translate_time(state["model_time"])))
+        out = {}
+        for key in set(state) & set(emulator):
+            a, b = state[key], emulator[key]
+            if isinstance(a, (int, float)) and isinstance(b, (int, float)):
+                out[key] = a * alpha + b * (1 - alpha)
+                continue
+            ta, tb = _dev(a), _dev(b)
+            if ta.numel() != tb.numel():
+                raise ValueError(f"TimeMask: {key} sizes differ: {tuple(ta.shape)} vs {tuple(tb.shape)}")
+            a64, b64 = ta.dtype == torch.float64, tb.dtype == torch.float64
+            res = torch.empty(ta.shape, dtype=torch.float64 if (a64 or b64) else torch.float32, device=ta.device)
+            st = _native.load().fv3_time_blend(ta.data_ptr(), int(a64), tb.data_ptr(), int(b64), res.data_ptr(),
+                                               res.numel(), alpha, _s())
+            _native.check(st, "time_blend")
+            out[key] = res
+        return out
 
 
 class RangeMask:
@@ -395,6 +465,7 @@ class MaskConfig:
     mask_precpd_zero_cloud_classifier: bool = False
     enforce_strict_precpd_conservative: bool = False
     simple_precip_conservative: bool = False
+    online_schedule: Optional[Callable] = None  # e.g. IntervalSchedule: TimeMask first
 
     def __post_init__(self):
         if self.enforce_conservative and self.enforce_conservative_phase_dependent:
@@ -406,6 +477,8 @@ class MaskConfig:
         return compose_masks(self.build_masks())
 
     def build_masks(self) -> Iterable[Mask]:
+        if self.online_schedule:
+            yield TimeMask(self.online_schedule)
         for key, r in self.ranges.items():
             yield RangeMask(key, min=r.min, max=r.max)
         if self.gscond_cloud_conservative:

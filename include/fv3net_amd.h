@@ -295,6 +295,13 @@ int fv3_level_row_sums_f64(const double* x, int nz, int64_t nrows, int row_len, 
                            double* out, int64_t out_ld, void* stream);
 int fv3_fold_rows(const double* rows, int64_t nrows, int width, double* out, void* stream);
 
+/* TimeMask (external/emulation/emulation/_emulate/microphysics.py:37-47): out =
+ * state * alpha + emulator * (1 - alpha) over n elements, each product in its array's
+ * dtype (float64 when *_f64, else float32) and the sum in the promoted dtype (float64 if
+ * either is), as numpy computes it.  out may alias either input. */
+int fv3_time_blend(const void* state, int state_f64, const void* emulator, int emulator_f64, void* out,
+                   int64_t n, double alpha, void* stream);
+
 /* ---- microphysics emulator hook post-processing (external/emulation) ------------------
  * On the hook's [feature, sample] arrays, contiguous, n elements (or nz x ncol), every
  * array of one dtype (f64 != 0: double, else float); numpy semantics (NaN-propagating

@@ -257,3 +257,81 @@ def test_model_with_classifier(gpu):
         _bits(out[k], r.astype(np.uint8))
     plain = E.ModelWithClassifier(regressor, classifier=None)({"a": torch.from_numpy(a).cuda()})
     assert set(plain) == {"air_temperature_output"}
+
+
+# ---- TimeMask / IntervalSchedule (_emulate/microphysics.py:23-47) ----------------------
+def test_interval_schedule_reference_kats():
+    """test_microphysics.py:47-56, on the Julian calendar the reference's cftime uses."""
+    import datetime
+
+    from fv3net_amd.emulation import IntervalSchedule, JulianTime
+
+    scheduler = IntervalSchedule(datetime.timedelta(hours=3), JulianTime(2000, 1, 1))
+    assert scheduler(JulianTime(2000, 1, 1)) == 1
+    assert scheduler(JulianTime(2000, 1, 1, 1)) == 1
+    assert scheduler(JulianTime(2000, 1, 1, 1, 30)) == 0
+    assert scheduler(JulianTime(2000, 1, 1, 2)) == 0
+    assert scheduler(JulianTime(2000, 1, 20)) == 1
+    # Julian-calendar day counts: 1900 is a leap year there (not in the Gregorian one)
+    assert JulianTime(1900, 3, 1) - JulianTime(1900, 2, 28) == datetime.timedelta(days=2)
+    assert JulianTime(2001, 1, 1) - JulianTime(2000, 1, 1) == datetime.timedelta(days=366)
+
+
+@pytest.mark.parametrize("weight", [0.0, 0.5, 1.0])
+def test_time_mask_reference_kat(weight):
+    """test_microphysics.py:58-64: Python numbers blend as Python does; only the keys
+    both dicts hold are returned; model_time[3] is skipped (_time.py:6-13)."""
+    from fv3net_amd.emulation import TimeMask
+
+    mask = TimeMask(schedule=lambda time: weight)
+    left = {"a": 0.0, "model_time": [2021, 1, 1, 0, 0, 0]}
+    right = {"a": 1.0}
+    assert mask(left, right) == {"a": 1 - weight}
+
+
+def test_mask_config_time_mask_first():
+    """config.py:176-177: the online schedule's TimeMask is the first mask."""
+    from fv3net_amd.emulation import MaskConfig, Range, RangeMask, TimeMask
+
+    def schedule(time):
+        return 1.0
+
+    masks = list(MaskConfig(ranges={"x": Range(min=0.0)}, online_schedule=schedule).build_masks())
+    assert isinstance(masks[0], TimeMask) and masks[0].schedule is schedule
+    assert isinstance(masks[1], RangeMask)
+    assert not any(isinstance(m, TimeMask) for m in MaskConfig().build_masks())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ds,de", [(np.float64, np.float64), (np.float64, np.float32), (np.float32, np.float64),
+                                   (np.float32, np.float32)])
+def test_time_mask_blend_matches_numpy(gpu, ds, de):
+    """fv3_time_blend: bitwise numpy's `state * alpha + emulator * (1 - alpha)` (NumPy 2
+    weak scalars: each product in its array's dtype, the sum promoted), NaN / inf
+    included; keys only one side holds are left out, as in the reference."""
+    import datetime
+
+    import torch
+
+    from fv3net_amd.emulation import IntervalSchedule, JulianTime, TimeMask
+
+    rng = np.random.default_rng(11)
+    s = rng.normal(0, 1, (79, 1000)).astype(ds)
+    e = rng.normal(0, 1, (79, 1000)).astype(de)
+    s[0, :3] = [np.nan, np.inf, -0.0]
+    e[1, :3] = [np.inf, np.nan, 0.0]
+    for alpha in (0.0, 1.0, 0.5, 0.3):
+        mask = TimeMask(schedule=lambda t, a=alpha: a)
+        out = mask({"x": torch.from_numpy(s).cuda(), "model_time": [2021, 1, 1, 0, 0, 0], "only_state": 1.0},
+                   {"x": torch.from_numpy(e).cuda(), "only_emulator": 2.0})
+        assert set(out) == {"x"}
+        ref = s * alpha + e * (1 - alpha)
+        got = out["x"].cpu().numpy()
+        assert got.dtype == ref.dtype
+        assert ((got.view(np.uint8) == ref.view(np.uint8)).all()), alpha
+    # the interval schedule picks the state in the first half of each period
+    sched = IntervalSchedule(datetime.timedelta(hours=3), JulianTime(2021, 1, 1))
+    st = {"x": torch.from_numpy(s).cuda(), "model_time": [2021, 1, 1, 0, 2, 0]}  # hour 2: second half
+    got = TimeMask(sched)(st, {"x": torch.from_numpy(e).cuda()})["x"].cpu().numpy()
+    ref = s * 0.0 + e * 1.0
+    assert (got.view(np.uint8) == ref.view(np.uint8)).all()
