@@ -149,3 +149,22 @@ def test_multi_errors(gpu):
     with pytest.raises(ValueError, match="one output per field"):
         mappm_device_multi(z(80, 3), [z(79, 3), z(79, 3)], z(51, 3), out=[z(50, 3)])
     torch.cuda.synchronize()
+
+
+def test_multi_on_a_side_stream(gpu, path):
+    """A call on another stream waits for the current stream (host inputs are copied
+    there) and keeps its temporaries alive until that stream is done: same bits."""
+    import torch
+
+    from fv3net_amd.mappm import mappm_device, mappm_device_multi
+
+    rng = np.random.default_rng(31)
+    pe1, q0, pe2 = _columns(rng, 79, 50, 3000)
+    q1 = _fields(rng, 79, 3000, 1)[0]
+    side = torch.cuda.Stream()
+    outs = mappm_device_multi(pe1, [q0, q1], pe2, 1, 1, stream=side)
+    one = mappm_device(pe1, q1, pe2, 1, 1, stream=side)
+    side.synchronize()
+    for q, o in zip((q0, q1), outs):
+        assert _bits_equal(o.cpu().numpy(), oracle_mappm(pe1, q, pe2, 1, 1))
+    assert _bits_equal(one.cpu().numpy(), oracle_mappm(pe1, q1, pe2, 1, 1))
