@@ -19,8 +19,15 @@ def require_gpu():
 
 
 def stream_handle(stream=None) -> int:
-    s = torch.cuda.current_stream() if stream is None else stream
-    return int(s.cuda_stream)
+    """The hipStream_t of ``stream`` (default: the current stream).  A launch on another
+    stream is ordered after the current stream's work so far, where the caller's inputs
+    (or their device copies) were produced."""
+    if stream is None:
+        return int(torch.cuda.current_stream().cuda_stream)
+    cur = torch.cuda.current_stream()
+    if stream != cur:
+        stream.wait_stream(cur)
+    return int(stream.cuda_stream)
 
 
 def to_device_f32(x, device=None, contiguous: bool = True):

@@ -41,19 +41,11 @@ def mappm_device(pe1, q1, pe2, iv: int = 1, kord: int = 1, out=None, stream=None
         raise ValueError(f"out must be float32 ({kn}, {ncol})")
     lo, _, _ = _device.level_layout(out, 0)
     lib = _native.load()
-    _order_on(stream)
     st = lib.fv3_mappm_ex(_device.ptr(pe1), l1, _device.ptr(q1), lq, _device.ptr(pe2), l2, _device.ptr(out), lo,
                           ncol, km, kn, int(iv), int(kord), 0.0, _device.stream_handle(stream))
     _native.check(st, "mappm")
     _keep_for(stream, [pe1, q1, pe2, out])
     return out
-
-
-def _order_on(stream):
-    """A call on another stream than the current one runs after the current stream's
-    work (the inputs, or their device copies, were produced there)."""
-    if stream is not None:
-        stream.wait_stream(torch.cuda.current_stream())
 
 
 def _keep_for(stream, tensors):
@@ -136,7 +128,6 @@ def mappm_device_multi(pe1, q1s, pe2, iv: int = 1, kord: int = 1, out=None, stre
     sharing the pressure-only arithmetic; each result is bit-identical to
     ``mappm_device`` on that field.  Returns the list of ``[kn, ncol]`` outputs."""
     args, outs, keep = _multi_args(pe1, q1s, pe2, iv, kord, out, stream)
-    _order_on(stream)
     _native.check(_native.load().fv3_mappm_multi(*args), "mappm")
     _keep_for(stream, keep + outs)
     return outs
