@@ -393,7 +393,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         static_for<RS>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
             const int meta = pk.slot_meta[q];
-            const bool on = valid && fq < ((meta >> 8) & 0xff);
+            // bitwise, not &&: a short-circuit makes the per-lane `valid` an exec-masked
+            // region around the slot's descriptor read, one scalar round trip per slot
+            const bool on = valid & (fq < ((meta >> 8) & 0xff));
             const unsigned off = b32 * (unsigned)pk.slot_bs[q] + i32 + (unsigned)fq * (unsigned)pk.slot_ld[q];
             // mask, not a select of pointers: the compiler turns that into a branch per
             // slot, with the descriptor reads and an lgkmcnt(0) wait inside each
@@ -437,7 +439,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         if constexpr (decltype(logc)::value)
             if (le > 0.0f) x = __logf_exact(x, le);  // LogTransform.forward (transforms.py:123-124); uniform
         const float y = (x - mu) * rv;
-        const unsigned keep = 0u - (unsigned)(valid && fq < ((meta >> 8) & 0xff));
+        const unsigned keep = 0u - (unsigned)(valid & (fq < ((meta >> 8) & 0xff)));
         L[fq < (meta & 0xff) ? tidx + ((fdst >> 4) * 256 + ((fdst >> 2) & 3)) : didx] =
             __builtin_bit_cast(float, __builtin_bit_cast(unsigned, y) & keep);
     };
@@ -478,7 +480,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
             static_for<8>([&](auto ic) {
                 constexpr int i = decltype(ic)::value;
                 const int q = min(q0 + i, kMaxSlots - 1);  // past nslots: meta 0, any valid base
-                const bool on = valid && fq < ((mw[i] >> 8) & 0xff);
+                const bool on = valid & (fq < ((mw[i] >> 8) & 0xff));
                 const unsigned off = b32 * (unsigned)pk.slot_bs[q] + i32 + (unsigned)fq * (unsigned)pk.slot_ld[q];
                 xw[i] = in_at<IT>(pk.slot_base[q], off & (0u - (unsigned)on));
             });
