@@ -379,7 +379,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
     // past the last column, and in unused slots: meta 0).  No branch per slot, so the
     // scalar reads of all slot descriptors can be in flight together.
     auto slot_load = [&](KArgs& pk, int q, int meta, bool valid, int64_t blk, int64_t ii, int fq) {
-        return (valid && fq < ((meta >> 8) & 0xff))
+        return (valid & (fq < ((meta >> 8) & 0xff)))
                    ? (float)in_at<IT>(pk.slot_base[q], blk * pk.slot_bs[q] + ii + (int64_t)fq * pk.slot_ld[q])
                    : 0.0f;
     };
@@ -421,7 +421,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
             if (leps > 0.0f) x = __logf_exact(x, leps);  // LogTransform.forward (transforms.py:123-124)
         float y = (x - mu) * dn;  // dn = 1 / (sigma + eps)
         asm volatile("" : "+v"(y));  // computed by every lane, then selected: no divergent branch
-        y = (valid && fq < ((meta >> 8) & 0xff)) ? y : 0.0f;
+        y = (valid & (fq < ((meta >> 8) & 0xff))) ? y : 0.0f;
         *(fq < (meta & 0xff) ? xc + xidx(f) : s_dummy) = y;
     };
     auto feat = [&](int meta, int fq) { return min(((meta >> 16) & 0x7ff) + fq, p.kp - 1); };

@@ -399,7 +399,7 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int row = 4 * hq + q;
-                const unsigned off = (ovalid && row < nrow) ? (rb + (unsigned)(z0 + row) * rld) * 4u : 0x80000000u;
+                const unsigned off = (ovalid & (row < nrow)) ? (rb + (unsigned)(z0 + row) * rld) * 4u : 0x80000000u;
                 r[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr_, (int)off, 0, 0));
             }
         } else {
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
             if (y >= hi[q]) y = hi[q];
             y = y * mk[q];
             if (has_res) y = r[q] + y;
-            const unsigned off = (ovalid && row < nrow) ? (ob + (unsigned)(z0 + row) * old_) * 4u : 0x80000000u;
+            const unsigned off = (ovalid & (row < nrow)) ? (ob + (unsigned)(z0 + row) * old_) * 4u : 0x80000000u;
 #ifdef FV3_B3_EXP_NOOUT  // experiment only (results invalid): store only a value that is never true
             if (y == 1234.5f)
 #endif
