@@ -34,7 +34,7 @@ LEGS = {
     "stepper_c96": ("stepper_c96", "ml_epilogue_kernel"),
     "stepper_c96_predict": ("stepper_c96", "dense_forward_kernel"),
     "predict_mappm_c384": ("predict_mappm_c384", "dense_forward_kernel"),
-    "predict_mappm_c384_mappm": ("predict_mappm_c384", "mappm_ppm_kernel"),
+    "predict_mappm_c384_mappm": ("predict_mappm_c384", "mappm_ppm_pair_kernel"),
 }
 KEEP = ("fv3::", "calib_")
 
