@@ -18,16 +18,30 @@ def require_gpu():
     _native.load()
 
 
-def stream_handle(stream=None) -> int:
+def stream_handle(stream=None, keep=()) -> int:
     """The hipStream_t of ``stream`` (default: the current stream).  A launch on another
     stream is ordered after the current stream's work so far, where the caller's inputs
-    (or their device copies) were produced."""
+    (or their device copies) were produced, and every tensor in ``keep`` (the temporaries
+    and outputs the kernel touches, allocated on the current stream) stays allocated
+    until the side stream's work is done (``record_stream``): without it the caching
+    allocator could hand a returned-and-dropped buffer to new current-stream work while
+    the side-stream kernel still reads or writes it."""
     if stream is None:
         return int(torch.cuda.current_stream().cuda_stream)
     cur = torch.cuda.current_stream()
     if stream != cur:
         stream.wait_stream(cur)
+        keep_for(stream, keep)
     return int(stream.cuda_stream)
+
+
+def keep_for(stream, tensors):
+    """Tensors allocated on the current stream but used on ``stream`` stay allocated
+    until that stream's work is done."""
+    if stream is not None:
+        for t in tensors:
+            if torch.is_tensor(t) and t.is_cuda:
+                t.record_stream(stream)
 
 
 def to_device_f32(x, device=None, contiguous: bool = True):

@@ -69,8 +69,11 @@ EXPORTED_SYMBOLS = (
     "fv3_standard_denormalize",
     "fv3_standard_normalize_f64",
     "fv3_standard_denormalize_f64",
+    "fv3_member_reduce",
+    "fv3_scale_levels",
+    "fv3_adapter_apply",
 )
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # fv3_dense_forward_ex precisions
 DENSE_F32 = 0
@@ -81,6 +84,12 @@ EPI_HAS_DQ1 = 1
 EPI_HAS_DQ2 = 2
 TEND_WIND = 0
 TEND_MASS = 1
+
+# fv3_member_reduce reductions; fv3_adapter_apply limits
+REDUCE_MEAN = 0
+REDUCE_MEDIAN = 1
+ADAPTER_MAX_PREDS = 8
+ADAPTER_MAX_TARGETS = 16
 
 # fv3_zc_gscond_update modes
 ZC_CLOUD_EMULATOR = 0
@@ -140,6 +149,15 @@ class EpilogueIO(ctypes.Structure):
         ("sphum_out", ctypes.c_void_p),
         ("column", ctypes.c_void_p),
         ("column_ld", ctypes.c_int64),
+    ]
+
+
+class AdapterTarget(ctypes.Structure):
+    _fields_ = [
+        ("preds", ctypes.c_void_p * 8),
+        ("n_preds", ctypes.c_int),
+        ("state", ctypes.c_void_p),
+        ("out", ctypes.c_void_p),
     ]
 
 
@@ -215,6 +233,9 @@ _SIGNATURES = {
     "fv3_ml_epilogue": (_I, [ctypes.POINTER(EpilogueIO), Layout, _I64, _I, _I, _D, _I, _I, _P]),
     "fv3_ml_epilogue_ex": (_I, [ctypes.POINTER(EpilogueIO), Layout, _I64, _I, _I, _D, _I, _I, _I, _P]),
     "fv3_tendency_columns": (_I, [_P, _P, _P, _P, _P, _P, Layout, _I64, _I, _I, _I, _D, _P]),
+    "fv3_member_reduce": (_I, [ctypes.POINTER(_P), _I, _I64, _I, _I, _P, _P]),
+    "fv3_scale_levels": (_I, [_P, _I, Layout, _P, _I64, _I, _P, _P]),
+    "fv3_adapter_apply": (_I, [ctypes.POINTER(AdapterTarget), _I, _I64, _I, _D, _I, _I, _I, _P]),
 }
 
 

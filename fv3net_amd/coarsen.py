@@ -60,7 +60,8 @@ def coarsen_on_pressure(delp, area, fields: Mapping[str, object], factor: int, i
     lib = _native.load()
     fn = lib.fv3_regrid_coarsen_f64d if want64 else (lib.fv3_regrid_coarsen_f64 if delp64 else lib.fv3_regrid_coarsen)
     st = fn(delp.data_ptr(), area.data_ptr(), fptr, optr, len(tens), delp_c.data_ptr(), nt, km, ny, nx,
-            int(factor), int(iv), int(kord), float(ptop), _device.stream_handle(stream))
+            int(factor), int(iv), int(kord), float(ptop),
+            _device.stream_handle(stream, [delp, area, delp_c] + tens + outs))
     _native.check(st, "regrid_coarsen")
     return dict(zip(names, outs)), delp_c
 
@@ -113,7 +114,8 @@ def coarsen_edges_on_pressure(delp, spacing, fields: Mapping[str, object], facto
     lib = _native.load()
     fn = lib.fv3_regrid_coarsen_edge_f64 if delp64 else lib.fv3_regrid_coarsen_edge
     st = fn(delp.data_ptr(), spacing.data_ptr(), fptr, optr, len(tens), nt, km, ny, nx, int(factor),
-            0 if edge == "x" else 1, int(iv), int(kord), float(ptop), _device.stream_handle(stream))
+            0 if edge == "x" else 1, int(iv), int(kord), float(ptop),
+            _device.stream_handle(stream, [delp, spacing] + tens + outs))
     _native.check(st, "regrid_coarsen_edge")
     return dict(zip(names, outs))
 

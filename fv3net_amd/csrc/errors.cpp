@@ -20,4 +20,4 @@ void clear_error() { g_err[0] = 0; }
 }  // namespace fv3
 
 extern "C" const char* fv3_last_error(void) { return g_err; }
-extern "C" int fv3_abi_version(void) { return 3; }
+extern "C" int fv3_abi_version(void) { return 4; }

@@ -432,10 +432,10 @@ class BoundForward:
     def __call__(self, stream=None):
         if self._in64:
             st = self._fn(self._handle, self._in_ptrs, self._in_l, self._out_ptrs, self._out_l, self._ncol,
-                          _device.stream_handle(stream))
+                          _device.stream_handle(stream, self.inputs + self.outputs))
         else:
             st = self._fn(self._handle, self._in_ptrs, self._in_l, self._out_ptrs, self._out_l, self._ncol,
-                          self._prec, _device.stream_handle(stream))
+                          self._prec, _device.stream_handle(stream, self.inputs + self.outputs))
         if st:
             _native.check(st, "dense_forward")
         return self.outputs

@@ -79,9 +79,9 @@ def area_weighted_partials(diags: Sequence, area, stream=None):
     ``area * ds`` promotes, any float64 operand puts the whole reduction on the float64
     kernel (float32 operands widened exactly); all-float32 inputs use the float32 one."""
     _device.require_gpu()
-    wide = any(torch.is_tensor(t) and t.dtype == torch.float64 for t in [area, *diags])
+    wide = any(_is_f64(t) for t in [area, *diags])
     if wide:
-        conv = lambda t: torch.as_tensor(t, device="cuda").to(torch.float64).contiguous()  # noqa: E731
+        conv = lambda t: _f64_on_device(t, torch.device("cuda", torch.cuda.current_device()))  # noqa: E731
     else:
         conv = lambda t: _device.to_device_f32(t).contiguous()  # noqa: E731
     area = conv(area)
@@ -95,7 +95,7 @@ def area_weighted_partials(diags: Sequence, area, stream=None):
     tab = (ctypes.c_void_p * len(xs))(*[d.data_ptr() for d in xs])
     lib = _native.load()
     fn = lib.fv3_area_weighted_sums_f64 if wide else lib.fv3_area_weighted_sums
-    st = fn(tab, len(xs), area.data_ptr(), area.numel(), out.data_ptr(), _device.stream_handle(stream))
+    st = fn(tab, len(xs), area.data_ptr(), area.numel(), out.data_ptr(), _device.stream_handle(stream, [area, out] + xs))
     _native.check(st, "area_weighted_sums")
     return out
 
@@ -176,7 +176,7 @@ def level_sums(field, stream=None):
         t = t.contiguous()
         lay, ncol, nz = _device.level_layout(t, 0)
     out = torch.empty(nz, dtype=torch.float64, device=t.device)
-    st = fn(t.data_ptr(), lay, ncol, nz, out.data_ptr(), _device.stream_handle(stream))
+    st = fn(t.data_ptr(), lay, ncol, nz, out.data_ptr(), _device.stream_handle(stream, [t, out]))
     _native.check(st, "level_sums")
     return out
 
@@ -204,14 +204,27 @@ def globally_sum_3d_diagnostics(diagnostics: dict, include: Sequence[str], group
 # flattened (tile, y) rows (row_band), so the gathered rows are the global rows in
 # order and the folded sums carry the same bits for 1, 2, 4 or 8 ranks.
 # --------------------------------------------------------------------------------
+def _is_f64(t) -> bool:
+    """float64 operand, torch or numpy (numpy's promotion decides the arithmetic)."""
+    if torch.is_tensor(t):
+        return t.dtype == torch.float64
+    return np.asarray(t).dtype == np.float64
+
+
+def _f64_on_device(t, dev):
+    if not torch.is_tensor(t):
+        t = torch.from_numpy(np.ascontiguousarray(np.asarray(t)))
+    return t.to(dev, torch.float64).contiguous()
+
+
 def area_row_partials(diags: Sequence, area, stream=None, out=None):
     """Device float64 [nrows, n_diag, 2]: per row of (rows, row_len) fields,
     (sum area*x_d, sum area).  float64 if any operand is (numpy's promotion).  ``out``:
     a [nrows, W >= 2 n_diag] float64 buffer whose leading columns receive them."""
     _device.require_gpu()
-    wide = any(torch.is_tensor(t) and t.dtype == torch.float64 for t in [area, *diags])
+    wide = any(_is_f64(t) for t in [area, *diags])
     dev = torch.device("cuda", torch.cuda.current_device())
-    conv = (lambda t: torch.as_tensor(t).to(dev, torch.float64).contiguous()) if wide else \
+    conv = (lambda t: _f64_on_device(t, dev)) if wide else \
         (lambda t: _device.to_device_f32(t).contiguous())  # noqa: E731
     area = conv(area)
     xs = [conv(d) for d in diags]
@@ -233,7 +246,8 @@ def area_row_partials(diags: Sequence, area, stream=None, out=None):
     lib = _native.load()
     fn = lib.fv3_area_weighted_row_sums_f64 if wide else lib.fv3_area_weighted_row_sums
     ld = out.stride(0) if out.dim() == 2 else 2 * len(xs)
-    st = fn(tab, len(xs), area.data_ptr(), nrows, row_len, out.data_ptr(), ld, _device.stream_handle(stream))
+    st = fn(tab, len(xs), area.data_ptr(), nrows, row_len, out.data_ptr(), ld,
+            _device.stream_handle(stream, [area, out] + xs))
     _native.check(st, "area_weighted_row_sums")
     return out
 
@@ -260,7 +274,7 @@ def level_row_partials(field, stream=None, out=None):
     lib = _native.load()
     fn = lib.fv3_level_row_sums_u8 if t.dtype == torch.uint8 else lib.fv3_level_row_sums_f64
     st = fn(t.data_ptr(), nz, nrows, row_len, int(t.stride(0)) if nz > 1 else nrows * row_len, out.data_ptr(),
-            int(out.stride(0)), _device.stream_handle(stream))
+            int(out.stride(0)), _device.stream_handle(stream, [t, out]))
     _native.check(st, "level_row_sums")
     return out
 
@@ -308,7 +322,8 @@ def fold_rows(rows, stream=None):
     nrows = int(r.shape[0])
     width = int(r[0].numel()) if nrows else int(np.prod(r.shape[1:], dtype=np.int64))
     out = torch.empty(tuple(r.shape[1:]), dtype=torch.float64, device=r.device)
-    st = _native.load().fv3_fold_rows(r.data_ptr(), nrows, width, out.data_ptr(), _device.stream_handle(stream))
+    st = _native.load().fv3_fold_rows(r.data_ptr(), nrows, width, out.data_ptr(),
+                                      _device.stream_handle(stream, [r, out]))
     _native.check(st, "fold_rows")
     return out
 
@@ -317,3 +332,17 @@ def global_row_sums(local_rows, group=None, counts: Optional[Sequence[int]] = No
     """fold_rows(gather_rows(local_rows)): the same bits on every rank and for every
     world size."""
     return fold_rows(gather_rows(local_rows, group, counts))
+
+
+def global_count_sums(local_counts, group=None):
+    """Global sums of integer-valued float64 counts (e.g. the per-level number of
+    columns where the humidity limiter fired, metrics.py:27-32 on a 0/1 field): one
+    all-reduce.  Integers below 2**53 add exactly in float64 in any order, so unlike
+    the float partials they need no row granularity to be world-size invariant."""
+    x = torch.as_tensor(local_counts, dtype=torch.float64)
+    if not _distributed():
+        return x.clone()
+    dev = _backend_device(group)
+    y = x.to(dev).contiguous().clone()
+    dist.all_reduce(y, op=dist.ReduceOp.SUM, group=group)
+    return y.to(x.device)

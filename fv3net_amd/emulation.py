@@ -14,8 +14,9 @@ the updated emulator dict, as in the reference.
 dtype: the kernels compute in one dtype per call, numpy's for same-dtype operands; a
 float32 emulator output meeting a float64 state is promoted to float64 first (numpy
 promotes at the first mixed operation instead; identical whenever state and emulator
-share a dtype, e.g. the all-float32 and all-float64 hooks).  Not mirrored: the
-``online_schedule`` TimeMask (it needs the Fortran model clock) and the Keras tensor
+share a dtype, e.g. the all-float32 and all-float64 hooks).  The ``online_schedule``
+TimeMask is mirrored by ``IntervalSchedule`` / ``TimeMask`` below on a Julian-calendar
+model time (cftime is absent; config.py:78-175).  Not mirrored: the Keras tensor
 transforms around a loaded TF model (the MicrophysicsEmulator graph has its own).
 """
 import dataclasses

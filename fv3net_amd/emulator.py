@@ -16,8 +16,10 @@ Inputs are read in place from the Fortran state layout [feature, sample] (the
 hook's state dict, _emulate/microphysics.py:83-101), which is the kernel's
 [level][column] layout: no transposes.
 
-Precision: float32 MFMA (exact f32 products) — tolerance 1e-3 rel is met with
-~1e-6; the bf16 3-term split path is future work.
+Precision: ``"bf16x3"`` (the default, csrc/dense_b3.hip) runs every product on bf16
+MFMA with each f32 operand split into hi + lo (3 MFMAs per product, ~1e-5 against the
+float64 graph); ``"f32"`` runs exact-f32 MFMA (csrc/dense.hip, ~1e-6).  Config #5's
+contract is 1e-3 rel; the tests hold bf16x3 to 1e-4 and f32 to 1e-5 per level.
 """
 import dataclasses
 from typing import Callable, Dict, List, Mapping, Optional

@@ -80,7 +80,7 @@ def _interp_columns(xp, x, y, fill_value, stream):
     out = torch.empty((n_out, ncol), dtype=torch.float64, device=x.device)
     st = _native.load().fv3_interpolate_2d(xp.data_ptr(), ncol, x.data_ptr(), ncol, y.data_ptr(), ncol,
                                             out.data_ptr(), ncol, ncol, n_in, n_out, float(fill_value),
-                                            _device.stream_handle(stream))
+                                            _device.stream_handle(stream, [xp, x, y, out]))
     _native.check(st, "interpolate_2d")
     return out
 
@@ -97,7 +97,7 @@ def _interp_levels(levels, xp, var, fill_value, stream):
     dtypes = int(xp.dtype == torch.float64) | (int(var.dtype == torch.float64) << 1)
     st = _native.load().fv3_interpolate_levels(xp.data_ptr(), ncol, var.data_ptr(), ncol, dtypes, dl.data_ptr(),
                                                 lv.size, reverse, out.data_ptr(), ncol, ncol, n_in,
-                                                float(fill_value), _device.stream_handle(stream))
+                                                float(fill_value), _device.stream_handle(stream, [xp, var, dl, out]))
     _native.check(st, "interpolate_levels")
     return out
 
@@ -134,7 +134,7 @@ def pressure_at_midpoint_log(delp, axis: int = 0, toa_pressure: float = TOA_PRES
     out = torch.empty_like(dl)
     st = _native.load().fv3_pressure_midpoint_log(dl.data_ptr(), int(dl.dtype == torch.float64), ncol,
                                                    out.data_ptr(), ncol, ncol, nz, float(toa_pressure),
-                                                   _device.stream_handle(stream))
+                                                   _device.stream_handle(stream, [dl, out]))
     _native.check(st, "pressure_midpoint_log")
     return out.reshape((nz,) + cols).movedim(0, axis % d.dim())
 

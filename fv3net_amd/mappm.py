@@ -42,18 +42,9 @@ def mappm_device(pe1, q1, pe2, iv: int = 1, kord: int = 1, out=None, stream=None
     lo, _, _ = _device.level_layout(out, 0)
     lib = _native.load()
     st = lib.fv3_mappm_ex(_device.ptr(pe1), l1, _device.ptr(q1), lq, _device.ptr(pe2), l2, _device.ptr(out), lo,
-                          ncol, km, kn, int(iv), int(kord), 0.0, _device.stream_handle(stream))
+                          ncol, km, kn, int(iv), int(kord), 0.0, _device.stream_handle(stream, [pe1, q1, pe2, out]))
     _native.check(st, "mappm")
-    _keep_for(stream, [pe1, q1, pe2, out])
     return out
-
-
-def _keep_for(stream, tensors):
-    """Tensors allocated on the current stream but used on ``stream`` stay allocated
-    until that stream's work is done."""
-    if stream is not None:
-        for t in tensors:
-            t.record_stream(stream)
 
 
 class MappmPlan:
@@ -74,11 +65,16 @@ class MappmPlan:
         (pe1, l1, _, _), (q1, lq, ncol, km), (pe2, l2, _, kp2) = views
         lo, _, _ = _device.level_layout(self.out, 0)
         self._keep = (pe1, q1, pe2)
+        self._stream = stream
         self._fn = _native.load().fv3_mappm_ex
         self._args = (_device.ptr(pe1), l1, _device.ptr(q1), lq, _device.ptr(pe2), l2, _device.ptr(self.out), lo,
                       ncol, km, kp2 - 1, int(iv), int(kord), 0.0, _device.stream_handle(stream))
 
     def __call__(self):
+        if self._stream is not None:
+            # a side-stream plan is ordered after the current stream's writes to the
+            # bound buffers on EVERY call, not only when it was built
+            _device.stream_handle(self._stream)
         _native.check(self._fn(*self._args), "mappm")
         return self.out
 
@@ -129,7 +125,7 @@ def mappm_device_multi(pe1, q1s, pe2, iv: int = 1, kord: int = 1, out=None, stre
     ``mappm_device`` on that field.  Returns the list of ``[kn, ncol]`` outputs."""
     args, outs, keep = _multi_args(pe1, q1s, pe2, iv, kord, out, stream)
     _native.check(_native.load().fv3_mappm_multi(*args), "mappm")
-    _keep_for(stream, keep + outs)
+    _device.keep_for(stream, keep + outs)
     return outs
 
 
@@ -145,11 +141,14 @@ class MappmMultiPlan:
                 raise ValueError(f"MappmMultiPlan: {name} is read through a copy (host, float64 or an "
                                  "unaddressable layout); pass float32 CUDA buffers")
         self._keep = keep
+        self._stream = stream
         self._fn = _native.load().fv3_mappm_multi
         self._args = args
         self()
 
     def __call__(self):
+        if self._stream is not None:  # ordered after current-stream writes, every call
+            _device.stream_handle(self._stream)
         _native.check(self._fn(*self._args), "mappm")
         return self.out
 

@@ -54,12 +54,18 @@ class StandardScaler:
         return np.asarray(self.mean, np.float64), np.asarray(self.std, np.float64)
 
     def _on_device(self, dev):
-        key = str(dev)
-        if key not in self._device_stats:
-            m, s = self._stats("use")
-            self._device_stats[key] = (torch.as_tensor(np.ascontiguousarray(m.ravel()), device=dev),
-                                       torch.as_tensor(np.ascontiguousarray(s.ravel()), device=dev))
-        return self._device_stats[key]
+        """Device copies of mean / std, keyed on their current values: the reference's
+        load assigns the attributes directly (scaler.py:86-100), and a reassigned or
+        edited statistic must never be served from a stale copy (a few hundred bytes
+        compared per call)."""
+        m, s = self._stats("use")
+        key = (m.shape, s.shape, m.tobytes(), s.tobytes())
+        hit = self._device_stats.get(str(dev))
+        if hit is None or hit[0] != key:
+            hit = (key, torch.as_tensor(np.ascontiguousarray(m.ravel()), device=dev),
+                   torch.as_tensor(np.ascontiguousarray(s.ravel()), device=dev))
+            self._device_stats[str(dev)] = hit
+        return hit[1], hit[2]
 
     # -- device arithmetic ----------------------------------------------------------------
     def _apply(self, data, forward: bool, feature_axis: Optional[int], out_f32: bool = False, out=None):

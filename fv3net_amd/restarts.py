@@ -77,7 +77,8 @@ def weighted_block_average(fields: Mapping[str, object], weights, factor: int, s
             chunk = items[i:i + 16]
             fp = (ctypes.c_void_p * len(chunk))(*[a.data_ptr() for a, _ in chunk])
             op = (ctypes.c_void_p * len(chunk))(*[r.data_ptr() for _, r in chunk])
-            st = fn(fp, op, len(chunk), w.data_ptr(), nt, nz, ny, nx, int(factor), _device.stream_handle(stream))
+            st = fn(fp, op, len(chunk), w.data_ptr(), nt, nz, ny, nx, int(factor),
+                    _device.stream_handle(stream, [w] + [a for a, _ in chunk] + [r for _, r in chunk]))
             _native.check(st, "weighted_block_average")
     return out
 
@@ -97,7 +98,8 @@ def impose_hydrostatic_balance(temperature, sphum, delp, dz, phis, ptop: float =
     phis_out = torch.empty_like(phis)
     st = _native.load().fv3_hydrostatic_balance(T.data_ptr(), q.data_ptr(), delp.data_ptr(), dz.data_ptr(),
                                                  phis.data_ptr(), dz_out.data_ptr(), phis_out.data_ptr(), nt, km,
-                                                 ny, nx, float(ptop), _device.stream_handle(stream))
+                                                 ny, nx, float(ptop),
+                                                 _device.stream_handle(stream, [T, q, delp, dz, phis, dz_out, phis_out]))
     _native.check(st, "hydrostatic_balance")
     return dz_out, phis_out
 
@@ -126,13 +128,20 @@ def coarsen_restarts_on_pressure(coarsening_factor: int, grid_spec: Mapping[str,
     delp = _dev(strip(core["delp"]))
     # one fused pass: masked core fields and every tracer share delp and area
     fused = {("c", n): strip(core[n]) for n in masked}
-    fused.update({("t", n): strip(tracer[n]) for n in tracer})
+    # only the listed tracers are coarsened and returned, cld_amt first (xr.merge order of
+    # _coarse_grain_fv_tracer_on_pressure, coarsen_restarts.py:859-887); a missing one is
+    # the reference's KeyError on ds_regridded[...]
+    tracer_names = FRACTION_TRACERS + NON_FRACTION_TRACERS
+    missing = [n for n in tracer_names if n not in tracer]
+    if missing:
+        raise KeyError(f"fv_tracer.res lacks {missing}")
+    fused.update({("t", n): strip(tracer[n]) for n in tracer_names})
     keys = list(fused)
     names = [f"{c}:{n}" for c, n in keys]
     res, delp_c = coarsen_on_pressure(delp, area, dict(zip(names, (fused[k] for k in keys))), f, iv, kord,
                                       stream=stream, coarse_delp_f64=True)
     out_core = {n: res[f"c:{n}"] for n in masked}
-    out_tracer = {n: res[f"t:{n}"] for n in tracer}
+    out_tracer = {n: res[f"t:{n}"] for n in tracer_names}
     out_core["delp"] = delp_c
     out_core["u"] = coarsen_edges_on_pressure(delp, grid_spec["dx"], {"u": strip(core["u"])}, f, "x", iv, kord,
                                               stream=stream)["u"]

@@ -121,7 +121,8 @@ def ml_epilogue(dq1, dq2, sphum, delp, temperature, dt: float, physics_precip=No
     flags = (_native.EPI_HAS_DQ1 if has_dq1 else 0) | (_native.EPI_HAS_DQ2 if has_dq2 else 0)
     st_ = _native.load().fv3_ml_epilogue_ex(ctypes_byref(io), lay, ncol, nz, int(state_dtype == torch.float64),
                                             float(dt), int(bool(mse_conserving)), int(bool(hydrostatic)), flags,
-                                            _device.stream_handle(stream))
+                                            _device.stream_handle(stream, [dq1, dq2, sphum, delp, temperature, precip,
+                                                                           column] + list(out.values())))
     _native.check(st_, "ml_epilogue")
     for i, name in enumerate(COLUMN_DIAGNOSTICS):
         if name == TOTAL_PRECIP and precip is None:
@@ -162,7 +163,7 @@ def tendency_columns(tendency, delp, dt: float, mode: str, level_axis: int = 0, 
     st_ = _native.load().fv3_tendency_columns(t.data_ptr(), delp.data_ptr(), filled, state_out,
                                               out["integral"].data_ptr(), out["filled_frac"].data_ptr(), lay, ncol,
                                               nz, int(state_dtype == torch.float64), m, float(dt),
-                                              _device.stream_handle(stream))
+                                              _device.stream_handle(stream, [t, delp] + list(out.values())))
     _native.check(st_, "tendency_columns")
     out["integral"] = out["integral"].reshape(col_shape)
     out["filled_frac"] = out["filled_frac"].reshape(col_shape)

@@ -225,10 +225,13 @@ class ShardedStepperWorkload:
     """BASELINE config #4 sharded as SURVEY.md 8(e) lays it out: this rank owns the rows
     [r0, r1) of the flattened (tile, y) rows of one global C<res> state, stored as a
     (z, rows, x) band, and per step runs the predict, the fused epilogue (in place) and
-    the step's one exchange: the global-mean partials of the 2-D diagnostics (net
-    moistening, column heating, total precipitation) and the 3-D limiter profile
-    (main.py:55-60), taken per grid row, all-gathered (RCCL on the GPU box) and folded in
-    global row order, so the result has the same bits for any number of ranks."""
+    the step's exchange: the global-mean partials of the 2-D diagnostics (net
+    moistening, column heating, total precipitation), taken per grid row (6 doubles),
+    all-gathered (RCCL on the GPU box) and folded in global row order, so the means have
+    the same bits for any number of ranks; and the 3-D limiter profile (main.py:55-60),
+    whose per-level counts are integers, summed on the rank and all-reduced (exact in
+    float64 in any order: nz doubles per rank).  ``exchange_bytes``: this rank's bytes
+    sent per step."""
     model: DenseColumnModel
     state: dict
     area: object
@@ -240,9 +243,10 @@ class ShardedStepperWorkload:
     bound: object = None
     counts: object = None
     partials: object = None
+    exchange_bytes: int = 0
 
     def step(self):
-        from .distributed import area_row_partials, global_row_sums, level_row_partials, row_counts
+        from .distributed import area_row_partials, global_count_sums, global_row_sums, level_sums, row_counts
         from .stepper import ml_epilogue
 
         T, q = self.state["air_temperature"], self.state["specific_humidity"]
@@ -252,16 +256,18 @@ class ShardedStepperWorkload:
         res = ml_epilogue(dq1, dq2, q, self.state["pressure_thickness_of_atmospheric_layer"], T, self.dt,
                           self.state["total_precipitation"], in_place=True, level_axis=0)
         self.state["total_precipitation"] = res["total_precipitation"]
-        if self.partials is None:  # [rows][3 (sum area*x, sum area) pairs + nz limiter counts]
-            self.partials = torch.empty((self.area.shape[0], 6 + q.shape[0]), dtype=torch.float64, device=q.device)
+        if self.partials is None:  # [rows][3 (sum area*x, sum area) pairs]
+            self.partials = torch.empty((self.area.shape[0], 6), dtype=torch.float64, device=q.device)
         local = self.partials
         area_row_partials([res["net_moistening_due_to_machine_learning"],
                            res["column_heating_due_to_machine_learning"], res["total_precipitation"]],
                           self.area, out=local)
-        level_row_partials(res["specific_humidity_limiter_active"], out=local[:, 6:])
+        limited = level_sums(res["specific_humidity_limiter_active"])  # [nz] exact column counts
         if self.counts is None:  # the bands are fixed: their sizes are exchanged once
             self.counts = row_counts(local.shape[0], self.group)
-        return global_row_sums(local, self.group, self.counts)
+            self.exchange_bytes = 8 * (max(self.counts) * 6 + limited.numel())
+        means = global_row_sums(local, self.group, self.counts)
+        return torch.cat([means, global_count_sums(limited, self.group).to(means.device)])
 
     @staticmethod
     def means(total):
@@ -332,7 +338,10 @@ def make_predict_mappm_workload(res: int = 384, rank: int = 0, world: int = 1, s
     g = torch.Generator(device=device)
     g.manual_seed(seed + 17)
     base = torch.linspace(200.0, 1800.0, NZ, device=device)[:, None]
-    delp = base * (0.99 + 0.02 * torch.rand((NZ, ncol), generator=g, device=device))
+    # the global state's delp (columns in flattened (tile, y, x) order), this rank's band
+    # of rows: every rank count sees the same columns
+    delp = base * (0.99 + 0.02 * torch.rand((NZ, 6 * res * res), generator=g, device=device))
+    delp = delp[:, r0 * res:r1 * res].contiguous()
     top = torch.full((1, ncol), 300.0, device=device)
     pe1 = torch.cat([top, 300.0 + torch.cumsum(delp, 0)]).contiguous()
     frac = torch.linspace(0.0, 1.0, NZ + 1, device=device)[:, None]

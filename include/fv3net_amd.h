@@ -51,7 +51,7 @@ extern "C" {
 
 const char* fv3_last_error(void);
 int fv3_abi_version(void); /* bumped on any signature change (2: emulator fields in fv3_dense_desc,
-                              3: fv3_dense_forward_ex) */
+                              3: fv3_dense_forward_ex, 4: composites + Adapter) */
 
 /*
  * Column layout of a [level, column] field.  Element (column c, level k) lives at
@@ -464,6 +464,46 @@ int fv3_interpolate_levels(const void* xp, int64_t ld_xp, const void* var, int64
  * delp's dtype (0 float32, 1 float64). */
 int fv3_pressure_midpoint_log(const void* delp, int dtype, int64_t ld_in, void* out, int64_t ld_out,
                               int64_t ncol, int nz, double ptop, void* stream);
+
+/* ---- composite predictors and the online transformer Adapter ------------------------
+ * The arithmetic of the fv3fit composites that nest the build's predictor as a
+ * base_model (external/fv3fit/fv3fit/_shared/models.py) and of the prognostic run's
+ * second Predictor caller (workflows/prognostic_c48_run/runtime/transformers/fv3fit.py).
+ *
+ * fv3_member_reduce replaces EnsembleModel.predict's xr.concat(outputs, "member") then
+ * .mean / .median(dim="member") (models.py:253-260): n_members contiguous arrays of n
+ * elements (float32, or float64 with dtype_f64), NaN-skipping as numpy's nanmean /
+ * nanmedian (member order, (low + high) / 2 for the median, NaN where every member is
+ * NaN); out may alias nothing.  1..32 members. */
+#define FV3_REDUCE_MEAN 0
+#define FV3_REDUCE_MEDIAN 1
+int fv3_member_reduce(const void* const* members, int n_members, int64_t n, int dtype_f64, int op,
+                      void* out, void* stream);
+
+/* fv3_scale_levels replaces TaperConfig.apply (_shared/config.py:21-29, TaperedModel
+ * models.py:95-100): out[k][c] (float64, contiguous [nz][ncol]) = scale[k] * x(c, k),
+ * x float32 or float64 under `lay` with its levels on the taper dimension. */
+int fv3_scale_levels(const void* x, int x_f64, fv3_layout lay, const double* scale, int64_t ncol, int nz,
+                     double* out, void* stream);
+
+/* fv3_adapter_apply replaces Adapter.predict's arithmetic (transformers/fv3fit.py:66-83) for
+ * every state variable updated by tendency predictions: tendency = 0 + p_0 + p_1 + ...
+ * (float32 model outputs), out = state + tendency * dt in the state's dtype; with `limit`
+ * the specific-humidity target (index sphum_target) and, if temp_target >= 0, the
+ * air-temperature target go through non_negative_sphum_mse_conserving
+ * (steppers/machine_learning.py:77-99) first.  Every array holds n contiguous elements;
+ * out may alias state.  limit without a humidity target: FV3_ERR_UNSUPPORTED (the
+ * reference's NotImplementedError). */
+#define FV3_ADAPTER_MAX_PREDS 8
+#define FV3_ADAPTER_MAX_TARGETS 16
+typedef struct fv3_adapter_target {
+    const float* preds[FV3_ADAPTER_MAX_PREDS];
+    int n_preds;
+    const void* state; /* float64 (state_f64) or float32 */
+    void* out;
+} fv3_adapter_target;
+int fv3_adapter_apply(const fv3_adapter_target* targets, int n_targets, int64_t n, int state_f64, double dt,
+                      int limit, int sphum_target, int temp_target, void* stream);
 
 #ifdef __cplusplus
 }

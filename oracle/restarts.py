@@ -85,7 +85,12 @@ def coarsen_restarts_on_pressure(factor, grid_spec, restarts, coarsen_agrid_wind
     out_core.update(zip(masked, regridded))
     (out_core["u"],) = OC.coarsen_edges_on_pressure(delp, dx, [core["u"]], factor, "x", iv, kord)
     (out_core["v"],) = OC.coarsen_edges_on_pressure(delp, dy, [core["v"]], factor, "y", iv, kord)
-    names = [n for n in tracer]
+    # only the listed tracers come out (cld_amt first: xr.merge order, :859-887); a
+    # missing one is the reference's KeyError on ds_regridded[...]
+    names = FRACTION_TRACERS + NON_FRACTION_TRACERS
+    missing = [n for n in names if n not in tracer]
+    if missing:
+        raise KeyError(f"fv_tracer.res lacks {missing}")
     regridded, _ = OC.coarsen_on_pressure(delp, area, [tracer[n] for n in names], factor, iv, kord)
     out_tracer = dict(zip(names, regridded))
     out_core["DZ"], out_core["phis"] = impose_hydrostatic_balance(out_core, out_tracer["sphum"])

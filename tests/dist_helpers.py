@@ -131,3 +131,41 @@ def sharded_stepper_worker(rank, world, port, out_dir, res, steps, backend="gloo
     np.save(os.path.join(out_dir, f"rows{rank}.npy"), np.array(wl.rows))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def count_sums_worker(rank, world, port, out_dir):
+    """Integer-valued float64 level counts summed over ranks by one all-reduce
+    (distributed.global_count_sums): exact, so every rank and world size agree."""
+    import torch
+
+    from fv3net_amd import distributed as D
+
+    dist = init_gloo(rank, world, port)
+    counts = np.random.default_rng(7).integers(0, 2 ** 40, (world, 79)).astype(np.float64)
+    total = D.global_count_sums(torch.from_numpy(counts[rank]))
+    np.save(os.path.join(out_dir, f"rank{rank}.npy"), total.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def predict_mappm_worker(rank, world, port, out_dir, res, steps):
+    """north_star's predict + mappm (workloads.PredictMappmWorkload) on this rank's row
+    band of one global C<res> state (gloo; ranks share the box's one GPU): the band's
+    tendencies and remapped tendencies after ``steps`` steps."""
+    import torch
+
+    from fv3net_amd import distributed as D
+    from fv3net_amd import workloads as W
+
+    dist = init_gloo(rank, world, port)
+    torch.cuda.set_device(0)
+    wl = W.make_predict_mappm_workload(res, rank, world, seed=3)
+    for _ in range(steps):
+        wl.step()
+    torch.cuda.synchronize()
+    out = np.stack([o.reshape(o.shape[0], -1).cpu().numpy() for o in wl.outputs] +
+                   [r.cpu().numpy() for r in wl.remapped])
+    np.save(os.path.join(out_dir, f"out{rank}.npy"), out)
+    np.save(os.path.join(out_dir, f"rows{rank}.npy"), np.array(D.row_band(6 * res, rank, world)))
+    dist.barrier()
+    dist.destroy_process_group()

@@ -211,3 +211,33 @@ def test_regrid_vertical_device_matches_oracle(gpu):
         regrid_vertical(p_in, f_in[..., :3], p_out)
     with pytest.raises(ValueError, match="same size"):
         regrid_vertical(p_in, f_in[:3], p_out)
+
+
+@pytest.mark.gpu
+def test_side_stream_host_and_float64_inputs(gpu):
+    """``stream=`` with host float64 inputs: the device copies and the outputs are
+    allocated on the current stream and used on the side stream, so they must be kept
+    alive for it (record_stream).  Churning the allocator on the current stream while
+    the side stream still runs must not change a bit of the results."""
+    import torch
+
+    from fv3net_amd.coarsen import coarsen_on_pressure
+    from fv3net_amd.restarts import weighted_block_average
+
+    rng = np.random.default_rng(21)
+    delp, area, T, q = _smooth_state(rng, 6, 79, 96, 96)
+    ref, ref_dc = coarsen_on_pressure(delp.astype(np.float64), area, {"T": T.astype(np.float64), "q": q}, 8)
+    wref = weighted_block_average({"T": T.astype(np.float64)}, area, 8)["T"]
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    for _ in range(3):
+        out, dc = coarsen_on_pressure(delp.astype(np.float64), area, {"T": T.astype(np.float64), "q": q}, 8,
+                                      stream=side)
+        w = weighted_block_average({"T": T.astype(np.float64)}, area, 8, stream=side)["T"]
+        # reuse whatever the caching allocator frees on the current stream
+        junk = [torch.full((6, 79, 96, 96), float("nan"), device="cuda") for _ in range(4)]
+        del junk
+        side.synchronize()
+        for k in ref:
+            assert torch.equal(out[k], ref[k]), k
+        assert torch.equal(dc, ref_dc) and torch.equal(w, wref)

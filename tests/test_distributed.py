@@ -134,6 +134,10 @@ def test_gpu_row_partials_match_restatement(gpu):
     got = D.area_row_partials([torch.from_numpy(x).cuda()], torch.from_numpy(area).cuda()).cpu().numpy()
     ref = H._rows_partials_np(x, area)
     assert (got[:, 0].view(np.uint64) == ref.view(np.uint64)).all()
+    # numpy float64 operands take the float64 kernel too (numpy's promotion), not a
+    # float32 rounding of the host arrays
+    host = D.area_row_partials([x], area).cpu().numpy()
+    assert (host[:, 0].view(np.uint64) == ref.view(np.uint64)).all()
     flag = (rng.uniform(size=(7, 40, 96)) < 0.2).astype(np.uint8)
     lev = D.level_row_partials(torch.from_numpy(flag).cuda()).cpu().numpy()
     assert (lev == flag.sum(axis=2).T).all()
@@ -177,3 +181,36 @@ def test_sharded_stepper_rccl_exchange_matches_gloo(gpu, tmp_path):
     qa = np.load(tmp_path / "gloo" / "q0.npy")
     qb = np.load(tmp_path / "nccl" / "q0.npy")
     assert (qa.view(np.uint64) == qb.view(np.uint64)).all()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_count_sums_are_exact(tmp_path, world):
+    """The limiter-profile exchange: per-rank integer counts (float64), one all-reduce;
+    exact in any order, so equal to the serial sum on every rank."""
+    _spawn(H.count_sums_worker, world, str(tmp_path))
+    counts = np.random.default_rng(7).integers(0, 2 ** 40, (world, 79)).astype(np.float64)
+    expect = counts.sum(axis=0)
+    for r in range(world):
+        assert (np.load(tmp_path / f"rank{r}.npy") == expect).all()
+
+
+@pytest.mark.gpu
+def test_sharded_predict_mappm_bit_identical_across_world_sizes(gpu, tmp_path):
+    """north_star's predict + mappm sharded as 8(e) lays it out (row bands of one global
+    state, no data-path exchange): at world 2 and 3 (gloo, processes sharing the GPU)
+    each rank's band of tendencies and remapped tendencies equals the world-1 columns
+    bit for bit (C24 stands in for C384: the same code with 144 rows)."""
+    res = 24
+    for world in (1, 2, 3):
+        (tmp_path / f"w{world}").mkdir()
+        _spawn(H.predict_mappm_worker, world, str(tmp_path / f"w{world}"), res, 2)
+    one = np.load(tmp_path / "w1" / "out0.npy")
+    assert np.isfinite(one).all()
+    for world in (2, 3):
+        cols = 0
+        for r in range(world):
+            r0, r1 = np.load(tmp_path / f"w{world}" / f"rows{r}.npy")
+            got = np.load(tmp_path / f"w{world}" / f"out{r}.npy")
+            assert (got.view(np.uint32) == one[:, :, r0 * res:r1 * res].view(np.uint32)).all(), (world, r)
+            cols += got.shape[-1]
+        assert cols == one.shape[-1]

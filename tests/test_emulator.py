@@ -73,6 +73,107 @@ def test_emulator_matches_oracle(gpu, precision, rtol):
             assert derr <= 1e-3, (o["name"], derr)
 
 
+def _check_columns(got, raw, emu, cols, rtol, scale=None):
+    """got: the emulator's outputs ([nz, ncol] / [ncol] device tensors) over the whole
+    grid; cols: column indices checked against the float64 oracle (per level)."""
+    import torch
+
+    idx = torch.as_tensor(cols, device="cuda")
+    sub = {k: v[:, idx].T.cpu().numpy() if torch.is_tensor(v) else v[cols] for k, v in raw.items()}
+    ref = OE.forward(sub, OE.zhao_carr_spec(), emu.params_by_name(), np.float64)
+    for o in OE.zhao_carr_spec()["outputs"]:
+        name = o.get("after") or o["name"]
+        g = got[name]
+        g = (g[idx] if g.ndim == 1 else g[:, idx].T).cpu().numpy()
+        r = ref[name][:, 0] if o["nz"] == 1 else ref[name]
+        sc = None if scale is None else scale.get(name)
+        assert_per_level(g, r, rtol, f"{name} columns {cols[0]}..{cols[-1]}", scale=sc)
+        if o.get("residual_of"):  # the difference, recovered from the after-state
+            d = g.astype(np.float64) - sub[o["residual_of"]].astype(np.float64)
+            derr = np.abs(d - ref[o["name"]]).max() / np.abs(ref[o["name"]]).max()
+            assert derr <= 1e-3, (o["name"], derr)
+    return ref
+
+
+def _device_raw(ncol, nz=79, seed=5):
+    """oracle.emulator.synthetic_raw's distributions, drawn on the device ([nz, ncol],
+    the hook's Fortran [feature, sample] layout) so a C384 state is cheap to make."""
+    import torch
+
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    dev = "cuda"
+    shape = (nz, ncol)
+
+    def u(lo, hi):
+        return torch.rand(shape, generator=g, device=dev) * (hi - lo) + lo
+
+    prof = torch.linspace(200.0, 300.0, nz, device=dev)[:, None]
+    T = prof + 5 * torch.randn(shape, generator=g, device=dev)
+    q = 0.02 * torch.exp(-torch.linspace(0, 6, nz, device=dev))[:, None] * u(0.2, 1.0)
+    qc = torch.where(torch.rand(shape, generator=g, device=dev) < 0.3, u(0, 1e-4), torch.zeros((), device=dev))
+    delp = torch.linspace(200, 1800, nz, device=dev)[:, None] * u(0.98, 1.02)
+    return {
+        "air_temperature_input": T.contiguous(),
+        "specific_humidity_input": q.contiguous(),
+        "cloud_water_mixing_ratio_input": qc.contiguous(),
+        "pressure_thickness_of_atmospheric_layer": delp.contiguous(),
+        "air_temperature_after_last_gscond": (T + 0.1 * torch.randn(shape, generator=g, device=dev)).contiguous(),
+        "specific_humidity_after_last_gscond": (q * u(0.95, 1.05)).contiguous(),
+    }
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision,rtol", [("bf16x3", 1e-4), ("f32", 1e-5)])
+def test_emulator_c384_full_grid(gpu, precision, rtol):
+    """BASELINE config #5 at its real size: 884,736 columns, so every persistent block
+    walks many tiles (bf16x3: 6,912 tiles of 128 on one block per CU; f32: 27,648 tiles
+    of 32).  Columns from the first, a middle and the last tile, plus a stride through
+    every block's tiles, are checked per level against the float64 oracle; the whole
+    grid must be finite and reproducible launch to launch."""
+    import torch
+
+    ncol = 6 * 384 * 384
+    emu, _ = _emulator(precision=precision)
+    raw = _device_raw(ncol)
+    a = emu(raw)
+    b = emu(raw)
+    torch.cuda.synchronize()
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+        assert torch.isfinite(a[k]).all(), k
+    # level magnitudes from the strided sample, applied to the contiguous blocks too
+    strided = np.arange(7, ncol, 97)
+    ref = _check_columns(a, raw, emu, strided, rtol)
+    scale = {}
+    for o in OE.zhao_carr_spec()["outputs"]:
+        name = o.get("after") or o["name"]
+        r = ref[name][:, 0] if o["nz"] == 1 else ref[name]
+        scale[name] = np.abs(r).max(axis=0)
+    for c0 in (0, ncol // 2 - 1024, ncol - 2048):
+        _check_columns(a, raw, emu, np.arange(c0, c0 + 2048), rtol, scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision,rtol,env", [("bf16x3", 1e-4, "FV3_B3_GRID"), ("f32", 1e-5, "FV3_DENSE_GRID")])
+def test_emulator_forced_multi_tile_blocks(gpu, precision, rtol, env, monkeypatch):
+    """A ragged grid (2,085 columns) on 4 persistent blocks: every block walks >= 4 tiles
+    (bf16x3: 17 tiles of 128; f32: 66 of 32), so the cross-tile prefetch of the LDS
+    input-group table, the LogTransform inputs and the residual reads run with the
+    emulator's features; must equal the default grid bit for bit."""
+    import torch
+
+    emu, raw = _emulator(ncol=2085, seed=9, precision=precision)
+    state = {k: torch.from_numpy(np.ascontiguousarray(v.T)).cuda() for k, v in raw.items()}
+    base = emu(state)
+    monkeypatch.setenv(env, "4")
+    forced = emu(state)
+    torch.cuda.synchronize()
+    monkeypatch.delenv(env)
+    for k in base:
+        assert torch.equal(base[k], forced[k]), k
+    _check_columns(forced, state, emu, np.arange(2085), rtol)
+
+
 @pytest.mark.gpu
 def test_microphysics_hook_updates_state_in_place(gpu):
     import torch

@@ -54,6 +54,32 @@ def test_oracle_matches_reference_regression_data(tag, agrid):
     _check_against_reference(result, _expected(_golden(), tag))
 
 
+def test_oracle_tracer_set_is_the_reference_list():
+    """_coarse_grain_fv_tracer_on_pressure (coarsen_restarts.py:859-887) returns exactly
+    FRACTION_TRACERS + NON_FRACTION_TRACERS: an extra tracer is dropped, a missing one
+    is a KeyError."""
+    grid, restarts = OR.kat_inputs()
+    extra = dict(restarts["fv_tracer.res"], extra_tracer=restarts["fv_tracer.res"]["sphum"])
+    result = OR.coarsen_restarts_on_pressure(2, grid, dict(restarts, **{"fv_tracer.res": extra}))
+    assert list(result["fv_tracer.res"]) == OR.FRACTION_TRACERS + OR.NON_FRACTION_TRACERS
+    short = {k: v for k, v in restarts["fv_tracer.res"].items() if k != "o3mr"}
+    with pytest.raises(KeyError):
+        OR.coarsen_restarts_on_pressure(2, grid, dict(restarts, **{"fv_tracer.res": short}))
+
+
+@pytest.mark.gpu
+def test_device_tracer_set_is_the_reference_list(gpu):
+    from fv3net_amd.restarts import FRACTION_TRACERS, NON_FRACTION_TRACERS, coarsen_restarts_on_pressure
+
+    grid, restarts = OR.kat_inputs()
+    extra = dict(restarts["fv_tracer.res"], extra_tracer=restarts["fv_tracer.res"]["sphum"])
+    result = coarsen_restarts_on_pressure(2, grid, dict(restarts, **{"fv_tracer.res": extra}))
+    assert list(result["fv_tracer.res"]) == FRACTION_TRACERS + NON_FRACTION_TRACERS
+    short = {k: v for k, v in restarts["fv_tracer.res"].items() if k != "o3mr"}
+    with pytest.raises(KeyError):
+        coarsen_restarts_on_pressure(2, grid, dict(restarts, **{"fv_tracer.res": short}))
+
+
 def test_oracle_hydrostatic_dz_closed_form():
     """hydrostatic_dz on an isothermal dry column: dz = -Rd T / g * log(p[k+1]/p[k])."""
     delp = np.full((1, 5, 1, 1), 1000.0)

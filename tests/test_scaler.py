@@ -144,3 +144,17 @@ def test_device_arithmetic_is_numpy_float64(gpu, dtype):
     s2.fit(X[:, 0].astype(np.float64))  # a 2-D variable: scalar statistics
     col = X[:, 0]
     assert (s2.normalize(col) == (col.astype(np.float64) - s2.mean) / s2.std).all()
+
+
+@pytest.mark.gpu
+def test_reassigned_statistics_are_not_served_stale(gpu):
+    """scaler.py:86-100 loads by assigning ``mean`` / ``std``: after a normalize has
+    cached device copies, a reassigned or in-place edited statistic must be used."""
+    scaler = StandardScaler()
+    x = np.random.default_rng(4).normal(3, 2, (50, 6))
+    scaler.fit(x)
+    scaler.normalize(x)
+    scaler.mean = scaler.mean + 1.0
+    np.testing.assert_array_equal(scaler.normalize(x), (x - scaler.mean) / scaler.std)
+    scaler.std *= 2.0
+    np.testing.assert_array_equal(scaler.normalize(x), (x - scaler.mean) / scaler.std)
