@@ -125,6 +125,13 @@ def with_counters(leg, rec, alg_bytes=None):
     for k in ("kernel", "mfma_busy_frac", "valu_busy_pct", "valu_utilization_pct"):
         if r.get(k) is not None:
             rec[k if k != "kernel" else "pmc_kernel"] = r[k]
+    if r.get("valu_issue_cu_cycles") and r.get("grbm_gui_active"):
+        # VALU issue roofline: the launch's instruction mix at the measured per-class
+        # issue peaks (tools/valu_calib.py -> profiles/valu_calib.json: 1.68 full-rate,
+        # 0.97 half-rate, 0.49 transcendental wave-instructions per CU-cycle) over the
+        # CU-cycles the launch took (GRBM_GUI_ACTIVE / 8 XCDs, the same dispatch)
+        rec["valu_issue_frac"] = r["valu_issue_cu_cycles"] / (W.N_CU * r["grbm_gui_active"] / 8)
+        rec["valu_mix"] = r.get("valu_mix")
     rec["pmc_profile"] = r.get("profile")
     return rec
 
@@ -200,6 +207,9 @@ def scaling_legs(dev, dist, rank, world, settle_ms=150.0):
         "scaling": "strong", "columns_global": wl.ncol_global, "columns_per_rank_max": wl.ncol,
         "global_means": [float(x) for x in means.cpu()],
         "limiter_profile_sum": float(profile.sum().item()),
+        "exchange_bytes_per_rank_per_step": wl.exchange_bytes,
+        "exchange": "all-gather of 6 float64 row partials per grid row (global means, folded in row order) + "
+                    "all-reduce of the 79 integer limiter counts (float64, exact in any order)",
         "note": "wall clock per step incl. the per-step all-gather; global_means / limiter_profile_sum after "
                 "one step from the seeded state carry the same bits at any N"}
     del wl
@@ -258,6 +268,99 @@ def host_to_host(dev, res, steps=10):
             "note": "float64 numpy in -> pinned double-buffered H2D -> fused predict (f64 read in place) -> pinned D2H -> float32 numpy"}
 
 
+def rank_call_host_to_host(dev, calls=30):
+    """The reference's real per-rank call: one rank's C48 subdomain,
+    (79, 48, 48) float64 host arrays of T / q in a Dataset, through the drop-in
+    ``DenseColumnPredictor.predict`` (pure_keras.py:98-118 boundary): host -> device,
+    the fused predict, float32 (79, 48, 48) numpy outputs back.  Wall time per call."""
+    from fv3net_amd import dataset as D
+    from fv3net_amd import workloads as W
+    from fv3net_amd.predictor import DenseColumnPredictor
+
+    wl = W.make_dense_workload(48, seed=3, device=dev)
+    cfg = wl.model.config
+    pred = DenseColumnPredictor(cfg.input_variables, cfg.output_variables, wl.model)
+    T = wl.inputs[0][0].double().cpu().numpy()  # tile 0: (z, y, x)
+    q = wl.inputs[1][0].double().cpu().numpy()
+    X = D.Dataset({cfg.input_variables[0]: D.DataArray(T, ["z", "y", "x"]),
+                   cfg.input_variables[1]: D.DataArray(q, ["z", "y", "x"])})
+    for _ in range(3):
+        out = pred.predict(X)
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        out = pred.predict(X)
+    wall = (time.perf_counter() - t0) / calls
+    assert out[cfg.output_variables[0]].values.dtype == np.float32
+    ncol = T.shape[1] * T.shape[2]
+    return {"columns_per_s": ncol / wall, "ms_per_call": wall * 1e3, "columns_per_call": ncol,
+            "host_bytes_per_call": T.nbytes + q.nbytes + 2 * ncol * 79 * 4,
+            "note": "one rank's (79,48,48) float64 numpy T/q Dataset -> DenseColumnPredictor.predict -> float32 "
+                    "(79,48,48) numpy dQ1/dQ2 Dataset (the drop-in call, host boundary included)"}
+
+
+def _ref_mappm_worker(args):
+    from oracle import mappm as OM
+
+    pe1, q, pe2, seconds = args
+    cols, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        OM.reference_mappm(pe1, q, pe2, 1, 1)
+        cols += pe1.shape[1]
+    return cols, time.perf_counter() - t0
+
+
+def reference_mappm_cpu_procs(procs=8, seconds=5.0):
+    """the reference mappm.f90 (flang, oracle/_ref) in ``procs``
+    single-threaded processes at once, each on its own config #3 columns: aggregate
+    columns/s."""
+    import multiprocessing as mp
+
+    from oracle import mappm as OM
+
+    if not OM.reference_available():
+        return None
+    rng = np.random.default_rng(1)
+    n = 4096
+    base = np.linspace(200.0, 1800.0, 79)[:, None]
+    jobs = []
+    for _ in range(procs):
+        delp = (base * rng.uniform(0.99, 1.01, (79, n))).astype(np.float32)
+        pe1 = np.concatenate([np.full((1, n), 300.0, np.float32), 300.0 + np.cumsum(delp, 0, dtype=np.float32)])
+        d2 = (base * rng.uniform(0.99, 1.01, (79, n))).astype(np.float32)
+        pe2 = np.concatenate([np.full((1, n), 300.0, np.float32), 300.0 + np.cumsum(d2, 0, dtype=np.float32)])
+        q = rng.normal(250.0, 10.0, (79, n)).astype(np.float32)
+        jobs.append((pe1, q, pe2, seconds))
+    with mp.get_context("spawn").Pool(procs) as pool:
+        res = pool.map(_ref_mappm_worker, jobs)
+    cols = sum(c for c, _ in res)
+    dt = max(t for _, t in res)
+    return {"value": cols / dt, "unit": "columns/s", "cores": procs, "kind": "reference",
+            "sample": f"{procs} processes x {seconds:.0f} s, each its own 4096 config #3 columns (79 -> 79, kord 1) "
+                      f"through the reference mappm.f90 (flang -O2, oracle/_ref) in 512-column chunks"}
+
+
+def coarsen_cpu_baseline(seconds=10.0):
+    """Config #3's coarsen on the host: oracle/coarsen.py (numpy + the C restatement of
+    mappm.f90, the reference's regrid_to_area_weighted_pressure -> weighted_block_average
+    arithmetic) on a bounded slab of a C384 tile, one field, f = 8: fine columns/s."""
+    from oracle import coarsen as OC
+
+    rng = np.random.default_rng(2)
+    ny, nx = 64, 384
+    base = np.linspace(200.0, 1800.0, 79)[None, :, None, None]
+    delp = (base * rng.uniform(0.99, 1.01, (1, 79, ny, nx))).astype(np.float32)
+    area = rng.uniform(0.5, 1.0, (1, ny, nx)).astype(np.float32)
+    T = rng.normal(250.0, 10.0, (1, 79, ny, nx)).astype(np.float32)
+    cols, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        OC.coarsen_on_pressure(delp, area, [T], 8)
+        cols += ny * nx
+    dt = time.perf_counter() - t0
+    return {"value": cols / dt, "unit": "fine columns/s", "cores": 1, "kind": "port",
+            "sample": f"{cols} fine columns ({ny}x{nx} slabs of a C384 tile, 79 levels, 1 field, f = 8) through "
+                      f"oracle/coarsen.py (numpy + the C restatement of mappm.f90), {dt:.1f} s, 1 core"}
+
+
 def reference_mappm_cpu(seconds=5.0):
     """The reference's own Fortran mappm (flang build in oracle/_ref)
     timed on one host core in 512-column chunks on config #3 columns (79 -> 79, kord 1).
@@ -312,6 +415,7 @@ def extra_measurements(dev, settle_ms=150.0):
         del wl
     try:
         out["mappm_c384_79to79_kord1"]["cpu_baseline"] = reference_mappm_cpu()
+        out["mappm_c384_79to79_kord1"]["cpu_baseline_8proc"] = reference_mappm_cpu_procs()
     except Exception as e:  # a report, never fatal
         log("reference mappm cpu baseline failed:", repr(e))
     # config #4: one ML-stepper step (predict + fused limiter/diagnostics/apply + global
@@ -357,9 +461,14 @@ def extra_measurements(dev, settle_ms=150.0):
             "fine_columns_per_s": wl.ncol_fine / t, "ms_per_step": t * 1e3, "hbm_gbs": gbs,
             "frac_hbm_peak": gbs / W.HBM_PEAK_GBS}, wl.bytes_per_column * wl.ncol_fine)
         del wl
+    try:
+        out["coarsen_c384_to_c48_1field"]["cpu_baseline"] = coarsen_cpu_baseline()
+    except Exception as e:  # a report, never fatal
+        log("coarsen cpu baseline failed:", repr(e))
     # host -> host (numpy float64 in, numpy float32 out) beside the device-resident legs
     for res in (48, 384):
         out[f"dense_c{res}_host_to_host"] = host_to_host(dev, res)
+    out["dense_c48_rank_call_host_to_host"] = rank_call_host_to_host(dev)
     torch.cuda.empty_cache()
     return out
 

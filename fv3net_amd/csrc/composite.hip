@@ -45,23 +45,23 @@ __global__ __launch_bounds__(256) void member_reduce_kernel(MemberArgs<T> a)
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
         if (a.op == FV3_REDUCE_MEAN) {
-            // np.nanmean: NaN -> 0, add.reduce along the member axis (the first member's
-            // value, then each next member in order), divided by the non-NaN count (a
-            // correctly rounded division; 0 / 0 = NaN when every member is NaN)
-            T v = a.m[0][i];
-            int cnt = !is_nan(v);
-            T s = is_nan(v) ? T(0) : v;
-            for (int j = 1; j < a.nm; ++j) {
-                v = a.m[j][i];
+            // np.nanmean: NaN -> 0, add.reduce along the member axis in member order from
+            // the identity +0.0 (so an all-(-0.0) column sums to +0.0), divided by the
+            // non-NaN count (a correctly rounded division; 0 / 0 = NaN when every member
+            // is NaN)
+            T s = T(0);
+            int cnt = 0;
+            for (int j = 0; j < a.nm; ++j) {
+                const T v = a.m[j][i];
                 cnt += !is_nan(v);
                 s = s + (is_nan(v) ? T(0) : v);
             }
             a.out[i] = s / (T)cnt;
         } else {
             // np.nanmedian (< 600 members: numpy.ma.median of the NaN-masked values):
-            // sort the unmasked values, low = v[(c - 1) / 2], high = v[c / 2], (low + high)
-            // / 2 in the array's dtype (also for odd counts, where low == high); NaN when
-            // every member is NaN
+            // sort the unmasked values, low = v[(c - 1) / 2], high = v[c / 2], then
+            // ma.sum([low, high]) / 2 in the array's dtype: the sum runs from the identity
+            // +0.0 (also for odd counts, where low == high); NaN when every member is NaN
             T v[kMaxMembers];
             int c = 0;
             for (int j = 0; j < a.nm; ++j) {
@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256) void member_reduce_kernel(MemberArgs<T> a)
                 a.out[i] = (T)NAN;
             } else {
                 const int h = c / 2, l = (c % 2) ? h : h - 1;
-                a.out[i] = (v[l] + v[h]) / (T)2;
+                a.out[i] = ((T(0) + v[l]) + v[h]) / (T)2;
             }
         }
     }

@@ -352,6 +352,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
     float* s_ep = s_denom + p.kp;                              // [6][kop]
     const int kop = 16 * p.n_otiles;
 
+    // issue priority over co-resident waves of other kernels (a VALU-bound remap beside
+    // this MFMA-bound predict): s_setprio takes an immediate
+    if (p.prio == 1) __builtin_amdgcn_s_setprio(1);
+    else if (p.prio == 2) __builtin_amdgcn_s_setprio(2);
+    else if (p.prio >= 3) __builtin_amdgcn_s_setprio(3);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int kr = lane >> 4;
@@ -1282,6 +1287,8 @@ static int dense_forward_impl(const fv3_dense_model* m, const void* const* input
     }
     int64_t grid = std::min<int64_t>(a.ntiles, (int64_t)res * n_cu);
     if (const char* e = getenv("FV3_DENSE_GRID")) grid = std::min<int64_t>(a.ntiles, std::max(1, atoi(e)));
+    a.prio = 0;
+    if (const char* e = getenv("FV3_DENSE_PRIO")) a.prio = std::max(0, std::min(3, atoi(e)));
     void* kargs[] = {&a};
     FV3_HIP(hipLaunchKernel(kfn, dim3((unsigned)grid), dim3(nt), kargs, lds, s));
     FV3_LAUNCH_CHECK();

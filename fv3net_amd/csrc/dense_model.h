@@ -67,6 +67,7 @@ struct DenseArgs {
     int has_log;            // any slot with a LogTransform (selects the staging variant)
     int fast_stage;         // every slot FPS-aligned: the short staging path
     long long* trace;       // profiling hook (fv3_dense_set_trace): [tiles][8] timestamps, or NULL
+    int prio;               // wave issue priority (s_setprio 0..3) for the whole kernel (FV3_DENSE_PRIO)
 };
 static_assert(sizeof(DenseArgs) <= 4096, "kernel arguments are limited to 4 KiB");
 

@@ -17,6 +17,7 @@ NZ = 79
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, dense f32 MFMA (= vector) peak
 BF16_MFMA_PEAK_TFLOPS = 2516.6  # MI355X_MICROARCH.md, dense bf16 MFMA peak
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
+N_CU = 256             # MI355X compute units (8 XCDs x 32)
 
 
 def c_columns(res: int, ntile: int = 6) -> int:

@@ -19,7 +19,8 @@ mkdir -p "$OUT"; export TMPDIR=/tmp
 SETS=("FETCH_SIZE"
       "WRITE_SIZE"
       "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE"
-      "VALUBusy VALUUtilization")
+      "VALUBusy VALUUtilization"
+      "SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT SQ_INSTS_SALU GRBM_GUI_ACTIVE")
 for leg in "${LEGS[@]}"; do
   mkdir -p "$OUT/$leg"
   i=0

@@ -17,6 +17,13 @@ import sys
 from collections import defaultdict
 
 N_LAST = 5
+# VALU issue model (tools/valu_calib.py on the box, profiles/valu_calib.json): measured
+# wave-instructions per CU per shader cycle at 8 waves/SIMD.  Full-rate class: f32
+# add/mul/fma and int32 (2 cycles per wave-instruction on a SIMD-32); trans (rcp, exp,
+# log, sqrt): 8 cycles; everything else the counters do not split out (compare,
+# cndmask, max/min, bfe, div_scale/fmas/fixup, cvt, packed f32): 4 cycles, the rate all
+# of those measured.
+VALU_RATE = {"full": 1.68, "half": 0.97, "trans": 0.49}
 # read width (bytes per lane) of each kernel's dominant streams
 WIDTH = {"dense_forward_kernel": 4, "dense_b3_kernel": 4, "mappm": 4, "regrid_coarsen": 4,
          "ml_epilogue_kernel": 8, "area_sums": 8, "level_sums": 4}
@@ -86,6 +93,16 @@ def main(root):
                 e["read_factor"], e["write_factor"] = fr, fw
             if "SQ_VALU_MFMA_BUSY_CYCLES" in c and c.get("SQ_BUSY_CU_CYCLES"):
                 e["mfma_busy_frac"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (4 * c["SQ_BUSY_CU_CYCLES"])
+            if "SQ_INSTS_VALU_ADD_F32" in c and "SQ_INSTS_VALU" in c:
+                full = sum(c.get(n, 0.0) for n in ("SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32",
+                                                    "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_INT32"))
+                trans = c.get("SQ_INSTS_VALU_TRANS_F32", 0.0)
+                mfma = c.get("SQ_INSTS_MFMA", 0.0)
+                half = max(0.0, c["SQ_INSTS_VALU"] - full - trans - mfma)
+                e["valu_mix"] = {"full_rate": full, "half_rate": half, "trans": trans}
+                # CU-cycles of VALU issue the kernel needs at the measured peaks, over the chip
+                e["valu_issue_cu_cycles"] = (full / VALU_RATE["full"] + half / VALU_RATE["half"]
+                                             + trans / VALU_RATE["trans"])
             rec[k] = e
         out["legs"][leg] = rec
     json.dump(out, sys.stdout, indent=1, sort_keys=True)

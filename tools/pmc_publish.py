@@ -83,6 +83,13 @@ def main(src, tag):
             "valu_utilization_pct": e.get("VALUUtilization"),
             "profile": tag,
         }
+        if e.get("valu_issue_cu_cycles") is not None:
+            # issue floor: the mix at the measured per-class peaks (tools/valu_calib.py)
+            # spread over 256 CUs, at the clock the launch held (GRBM_GUI_ACTIVE / 8 per
+            # wall second, MI355X_MICROARCH.md 'DVFS give-back')
+            traffic[bench_leg]["valu_issue_cu_cycles"] = e["valu_issue_cu_cycles"]
+            traffic[bench_leg]["valu_mix"] = e.get("valu_mix")
+            traffic[bench_leg]["grbm_gui_active"] = e.get("GRBM_GUI_ACTIVE")
     with open(traffic_path, "w") as f:
         json.dump(traffic, f, indent=1, sort_keys=True)
     print(f"published {tag}: {len(traffic)} legs in {traffic_path}")
