@@ -285,8 +285,8 @@ __device__ __forceinline__ void gemm_hidden(f32x4 (&acc)[NC][T4], const f32x4* _
 // next column tile is HT*64 f32x4 further); soff[i] = byte offset of tile i's weights
 constexpr int kOutTiles = OUT_TILES;  // output tiles per wave per pass
 constexpr int kOutRing = OUT_RING;    // output-weight ring depth (groups held; refilled kOutRing-1 ahead)
-template <int HT, int N, int NCC, int RD>
-__device__ __forceinline__ void gemm_out_tiles(f32x4 (&o)[kOutTiles][2], const f32x4* __restrict__ src, Rsrc rw,
+template <int HT, int N, int NCC, int RD, int NCA>
+__device__ __forceinline__ void gemm_out_tiles(f32x4 (&o)[kOutTiles][NCA], const f32x4* __restrict__ src, Rsrc rw,
                                                int voff, const int (&soff)[kOutTiles],
                                                f32x4 (&g)[RD][kOutTiles])
 {
@@ -794,9 +794,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
             int so[kOutTiles];
             const int n = whole_soff(j0, so);
             if (j0 > 0) prime_out_tiles<kOutRing>(go, rw, voff_o, so, n);
-            f32x4 o[kOutTiles][2];
+            f32x4 o[kOutTiles][NC];
 #pragma unroll
-            for (int i = 0; i < kOutTiles; ++i) o[i][0] = o[i][1] = zero4();
+            for (int i = 0; i < kOutTiles; ++i)
+#pragma unroll
+                for (int c = 0; c < NC; ++c) o[i][c] = zero4();
             if (n == 1)
                 gemm_out_tiles<HT, 1, NC, kOutRing>(o, hbuf + lane, rw, voff_o, so, go);
             else
@@ -816,7 +818,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
 #pragma unroll
             for (int i = 0; i < kOutTiles; ++i) so[i] = p.wo_off + m * (HP / 16) * 1024;
             if (k > 0 || n_whole > 0) prime_out_tiles<kOutRing>(go, rw, voff_o, so, 1);
-            f32x4 o[kOutTiles][2];
+            f32x4 o[kOutTiles][NC];
             o[0][0] = zero4();
             gemm_out_tiles<HT, 1, 1, kOutRing>(o, hbuf + c * HT * 64 + lane, rw, voff_o, so, go);
             epilogue(m, c, o[0][0]);
@@ -1191,7 +1193,7 @@ static int dense_forward_impl(const fv3_dense_model* m, const void* const* input
     }
     int nw = 8;
     if (const char* e = getenv("FV3_DENSE_NW")) nw = atoi(e) == 8 ? 8 : 4;
-    if (nc != 2 || m->w1_off8 < 0) nw = 4;
+    if (nc == 1 || m->w1_off8 < 0) nw = 4;
     const int nt = 64 * nw;
     if (nw == 8) {
         a.w1_off = m->w1_off8;
