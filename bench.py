@@ -130,7 +130,10 @@ def with_counters(leg, rec, alg_bytes=None):
         # issue peaks (tools/valu_calib.py -> profiles/valu_calib.json: 1.68 full-rate,
         # 0.97 half-rate, 0.49 transcendental wave-instructions per CU-cycle) over the
         # CU-cycles the launch took (GRBM_GUI_ACTIVE / 8 XCDs, the same dispatch)
-        rec["valu_issue_frac"] = r["valu_issue_cu_cycles"] / (W.N_CU * r["grbm_gui_active"] / 8)
+        cu_cycles = W.N_CU * r["grbm_gui_active"] / 8
+        rec["valu_issue_frac"] = r["valu_issue_cu_cycles"] / cu_cycles
+        if r.get("valu_issue_cu_cycles_lo"):  # the unsplit rest (v_mov among it) at full rate
+            rec["valu_issue_frac_lo"] = r["valu_issue_cu_cycles_lo"] / cu_cycles
         rec["valu_mix"] = r.get("valu_mix")
     rec["pmc_profile"] = r.get("profile")
     return rec
@@ -223,7 +226,10 @@ def scaling_legs(dev, dist, rank, world, settle_ms=150.0):
         "gpu_ms_per_step_rank0": t * 1e3,
         "bytes_per_column_kernels": wl.bytes_per_column,
         "hbm_gbs_per_gpu_kernels": wl.ncol * wl.bytes_per_column / t / 1e9,
-        "tflops_per_gpu_dense": wl.ncol * wl.flops_per_column / t / 1e12}
+        "tflops_per_gpu_dense": wl.ncol * wl.flops_per_column / t / 1e12,
+        # committed PMC evidence of the step's two kernels (world-1 profile)
+        "kernels": {"dense": with_counters("predict_mappm_c384", {}),
+                    "mappm_pair": with_counters("predict_mappm_c384_mappm", {})}}
     del wl
     torch.cuda.empty_cache()
     return out

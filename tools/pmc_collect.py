@@ -20,9 +20,10 @@ N_LAST = 5
 # VALU issue model (tools/valu_calib.py on the box, profiles/valu_calib.json): measured
 # wave-instructions per CU per shader cycle at 8 waves/SIMD.  Full-rate class: f32
 # add/mul/fma and int32 (2 cycles per wave-instruction on a SIMD-32); trans (rcp, exp,
-# log, sqrt): 8 cycles; everything else the counters do not split out (compare,
-# cndmask, max/min, bfe, div_scale/fmas/fixup, cvt, packed f32): 4 cycles, the rate all
-# of those measured.
+# log, sqrt): 8 cycles; the rest the counters do not split out is compare, cndmask,
+# max/min, bfe, div_scale/fmas/fixup, cvt and packed f32 (4 cycles, measured) but also
+# v_mov_b32 (2 cycles, measured): the floor is given with that rest at half rate (an
+# upper bound, `valu_issue_cu_cycles`) and at full rate (a lower bound, `_lo`).
 VALU_RATE = {"full": 1.68, "half": 0.97, "trans": 0.49}
 # read width (bytes per lane) of each kernel's dominant streams
 WIDTH = {"dense_forward_kernel": 4, "dense_b3_kernel": 4, "mappm": 4, "regrid_coarsen": 4,
@@ -103,6 +104,7 @@ def main(root):
                 # CU-cycles of VALU issue the kernel needs at the measured peaks, over the chip
                 e["valu_issue_cu_cycles"] = (full / VALU_RATE["full"] + half / VALU_RATE["half"]
                                              + trans / VALU_RATE["trans"])
+                e["valu_issue_cu_cycles_lo"] = (full + half) / VALU_RATE["full"] + trans / VALU_RATE["trans"]
             rec[k] = e
         out["legs"][leg] = rec
     json.dump(out, sys.stdout, indent=1, sort_keys=True)

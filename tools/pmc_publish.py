@@ -88,6 +88,7 @@ def main(src, tag):
             # spread over 256 CUs, at the clock the launch held (GRBM_GUI_ACTIVE / 8 per
             # wall second, MI355X_MICROARCH.md 'DVFS give-back')
             traffic[bench_leg]["valu_issue_cu_cycles"] = e["valu_issue_cu_cycles"]
+            traffic[bench_leg]["valu_issue_cu_cycles_lo"] = e.get("valu_issue_cu_cycles_lo")
             traffic[bench_leg]["valu_mix"] = e.get("valu_mix")
             traffic[bench_leg]["grbm_gui_active"] = e.get("GRBM_GUI_ACTIVE")
     with open(traffic_path, "w") as f:
