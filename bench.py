@@ -68,11 +68,19 @@ def timed_steps(step, steps, warmup, dist=None, settle_ms=0.0):
     tools/dense_trace.py), so without it a short K times the ramp, not the kernel."""
     import torch
 
+    # the settle keeps the GPU busy without a gap: the host waits on the event recorded
+    # a few batches back (bounding the queue), never on an empty queue, so the clock
+    # ramp is not reset by idle gaps every batch
     t_end = time.perf_counter() + settle_ms * 1e-3
+    marks = []
     while settle_ms > 0 and time.perf_counter() < t_end:
         for _ in range(100):
             step()
-        torch.cuda.synchronize()
+        ev = torch.cuda.Event()
+        ev.record()
+        marks.append(ev)
+        if len(marks) > 4:
+            marks.pop(0).synchronize()
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()

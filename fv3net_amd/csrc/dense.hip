@@ -443,7 +443,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         const int fdst = (meta >> 16) & 0x7ff;
         if constexpr (decltype(logc)::value)
             if (le > 0.0f) x = __logf_exact(x, le);  // LogTransform.forward (transforms.py:123-124); uniform
+#ifdef FV3_EXP_NONORM  // experiment only (results invalid): stage the raw values
+        const float y = x + 0.0f * (mu + rv);
+#else
         const float y = (x - mu) * rv;
+#endif
         const unsigned keep = 0u - (unsigned)(valid & (fq < ((meta >> 8) & 0xff)));
         L[fq < (meta & 0xff) ? tidx + ((fdst >> 4) * 256 + ((fdst >> 2) & 3)) : didx] =
             __builtin_bit_cast(float, __builtin_bit_cast(unsigned, y) & keep);
