@@ -346,11 +346,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
     static_assert(FPS == 8 || FPS == 16, "the staging address split assumes 8 or 16 rows per slot");
     typedef typename Frag<T4>::type FT;
     extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
-    f32x4* hbuf = lds;  // activations [NC][HT][64]; the staged inputs [NC][kp/16][64] alias it
+    f32x4* hbuf = lds;             // activations [NC][HT][64]
+    f32x4* sbuf = lds + p.lds_s;   // staged inputs [NC][kp/16][64], a buffer of their own: the
+                                   // next tile's inputs are staged while this tile runs
     float* s_mean = reinterpret_cast<float*>(lds + p.lds_x);  // [kp]
     float* s_denom = s_mean + p.kp;                            // [kp]
     float* s_ep = s_denom + p.kp;                              // [6][kop]
     const int kop = 16 * p.n_otiles;
+    // hidden-layer biases [1 + n_hidden_extra][HP], after the dummy f32x4: read from LDS,
+    // not memory, so the bias reads after the next tile's input loads are issued do not
+    // wait for those HBM loads (vector-memory loads complete in issue order)
+    float* s_bias = s_ep + 6 * kop + 4;
 
     // issue priority over co-resident waves of other kernels (a VALU-bound remap beside
     // this MFMA-bound predict): s_setprio takes an immediate
@@ -412,7 +418,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
     // normalise and write the staged inputs in B-operand order: for column tile c,
     // k-step s = 4g + r, k-slot kr, column cl the float index is
     // c*kp*16 + (g*64 + kr*16 + cl)*4 + r (one ds_read_b128 = a group's B operands)
-    float* xc = reinterpret_cast<float*>(hbuf) + (cb >> 4) * (p.kp * 16);
+    float* xc = reinterpret_cast<float*>(sbuf) + (cb >> 4) * (p.kp * 16);
     const int cl16 = cb & 15;
     auto xidx = [&](int f) { return ((f >> 4) * 64 + (f & 3) * 16 + cl16) * 4 + ((f >> 2) & 3); };
     float* s_dummy = s_ep + 6 * 16 * p.n_otiles;  // write-only sink
@@ -452,7 +458,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         L[fq < (meta & 0xff) ? tidx + ((fdst >> 4) * 256 + ((fdst >> 2) & 3)) : didx] =
             __builtin_bit_cast(float, __builtin_bit_cast(unsigned, y) & keep);
     };
-    auto store_x_fast = [&](KArgs& pk, int64_t tile, int fq, auto logc) {
+    auto store_x_fast = [&](KArgs& pk, int64_t tile, int fq, auto logc, bool zero_pad) {
         int64_t blk, ii;
         const bool valid = col_of(tile, blk, ii);
         // in batches (descriptors, constants, values) so the scalar and LDS reads of all
@@ -505,9 +511,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
                          valid, tidx, fq, logc);
             });
         }
-        for (int f = 4 * p.in_steps_total + fq; f < p.kp; f += FPS) xc[xidx(f)] = 0.0f;
+        if (zero_pad)  // the padding features: once, the buffer holds nothing else
+            for (int f = 4 * p.in_steps_total + fq; f < p.kp; f += FPS) xc[xidx(f)] = 0.0f;
     };
-    auto store_x = [&](KArgs& pk, int64_t tile, int fq, auto logc) {
+    auto store_x = [&](KArgs& pk, int64_t tile, int fq, auto logc, bool zero_pad) {
         int64_t blk, ii;
         const bool valid = col_of(tile, blk, ii);
         constexpr int B = 5;  // slots per batch: descriptors and constants read before any use
@@ -546,7 +553,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
                     s_denom[feat(mt[i], fq)], valid, fq, logc);
             });
         }
-        for (int f = 4 * p.in_steps_total + fq; f < p.kp; f += FPS) xc[xidx(f)] = 0.0f;
+        if (zero_pad)  // the padding features: once, the buffer holds nothing else
+            for (int f = 4 * p.in_steps_total + fq; f < p.kp; f += FPS) xc[xidx(f)] = 0.0f;
     };
 
     // ---- prologue: this tile's inputs and the layer-1 ring in flight, constants to LDS ----
@@ -605,6 +613,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         for (int i = threadIdx.x + NT * NE; i < 6 * kop; i += NT) s_ep[i] = p.oep[i];
     }
 #endif
+    for (int i = threadIdx.x; i < (1 + p.n_hidden_extra) * HP; i += NT) s_bias[i] = i < HP ? p.b1[i] : p.bh[i - HP];
 
     // output plan of this wave.  The first (n_otiles / NW) * NW output tiles go whole to
     // the waves (tile m to wave m % NW): one weight fetch feeds both column tiles.  The
@@ -626,9 +635,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         m = m_split + u / NC;
         c = u % NC;
     };
-    f32x4 go[kOutRing][kOutTiles];
-    FT gh[RD][4];
-    auto prime_after = [&](int l) {  // prime the ring of the layer that follows hidden layer l
+    // prime the ring of the layer that follows hidden layer l.  The rings (gh, go) are
+    // declared per tile, not across the tile loop: loop-carried ring registers made the
+    // compiler copy them at the merge after the next tile's input loads are issued, behind
+    // an s_waitcnt vmcnt(0) that waited for those HBM loads (vector-memory loads complete
+    // in issue order)
+    auto prime_after = [&](int l, auto& gh, auto& go) {
         if (l + 1 < p.n_hidden_extra) {
             prime_ring<RD, NW, FT>(gh, rw, voff, p.wh_off + (l + 1) * (HP / 4) * KS);
         } else if (n_whole > 0) {
@@ -644,11 +656,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
             prime_out_tiles<kOutRing>(go, rw, voff_o, so, 1);
         }
     };
-    tile_sync();
-
-    for (; tile < p.ntiles; tile += gridDim.x) {  // persistent over column tiles
-        trace_mark(p, tile, 5);
-        // opaque per tile: addresses derived from the thread's feature row are rebuilt
+    // stage this tile's inputs (into their own buffer: the stages of later tiles run
+    // inside the previous tile, before its output layer)
+    auto stage = [&](int64_t t, bool zero_pad) {
+        // opaque per stage: addresses derived from the thread's feature row are rebuilt
         // each tile instead of being hoisted out of the loop as 20 live 64-bit values
         int fq = fq0;
         asm volatile("" : "+v"(fq));
@@ -658,25 +669,33 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         asm volatile("" : "+s"(pt));
 #ifndef FV3_EXP_NOSTAGE  // experiment only (results invalid): no input staging
         if (p.fast_stage && p.has_log)
-            store_x_fast(*pt, tile, fq, std::true_type{});
+            store_x_fast(*pt, t, fq, std::true_type{}, zero_pad);
         else if (p.fast_stage)
-            store_x_fast(*pt, tile, fq, std::false_type{});
+            store_x_fast(*pt, t, fq, std::false_type{}, zero_pad);
         else if (p.has_log)
-            store_x(*pt, tile, fq, std::true_type{});
+            store_x(*pt, t, fq, std::true_type{}, zero_pad);
         else
-            store_x(*pt, tile, fq, std::false_type{});
+            store_x(*pt, t, fq, std::false_type{}, zero_pad);
 #endif
-        tile_sync();
+    };
+    if (tile < p.ntiles) stage(tile, true);
+    tile_sync();
+
+    for (; tile < p.ntiles; tile += gridDim.x) {  // persistent over column tiles
+        trace_mark(p, tile, 5);
         trace_mark(p, tile, 1);
+        const bool has_next = tile + gridDim.x < p.ntiles;
 
         // ---- layer 1: Dense(width) over the padded input features ----
+        f32x4 go[kOutRing][kOutTiles];
+        FT gh[RD][4];
         f32x4 acc[NC][T4];
 #pragma unroll
         for (int c = 0; c < NC; ++c)
 #pragma unroll
             for (int j = 0; j < T4; ++j) acc[c][j] = zero4();
         {
-            const f32x4* xq = hbuf + lane;  // + c*kp*4 + g*64
+            const f32x4* xq = sbuf + lane;  // + c*kp*4 + g*64
             const int ngroups = p.kp / 16;
             f32x4 xb[RD][NC];
 #pragma unroll
@@ -710,16 +729,22 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
                 });
             }
         }
-        // the next tile's inputs travel while this tile runs its remaining layers
-        if (tile + gridDim.x < p.ntiles) {
+        prime_after(-1, gh, go);
+        // no barrier before: the activations are free since the end of the last tile,
+        // and the staged inputs are not overwritten until after the next barrier
+        bias_relu_store<T4, NC, NW>(acc, s_bias, wave, lane, kr, hbuf);
+        // the next tile's inputs travel while this tile runs its remaining layers.  Issued
+        // after layer 1's weight loads and the next ring's: loads complete in issue order,
+        // so every weight wait after this point also waits for these HBM loads (measured:
+        // issued before the ring, C384 2.10 ms; here, 2.07 ms)
+        if (has_next) {
             KArgs* pn = &p;
             asm volatile("" : "+s"(pn));
+            int fq = fq0;
+            asm volatile("" : "+v"(fq));
             load_raw(*pn, tile + gridDim.x, fq);
         }
-        prime_after(-1);
-        tile_sync();  // every wave is done with the staged inputs
-        bias_relu_store<T4, NC, NW>(acc, p.b1, wave, lane, kr, hbuf);
-        tile_sync();
+        tile_sync();  // the activations are written; every wave is done with the staged inputs
         trace_mark(p, tile, 2);
 
         // ---- further hidden layers, in place ----
@@ -729,11 +754,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
 #pragma unroll
                 for (int j = 0; j < T4; ++j) acc[c][j] = zero4();
             gemm_hidden<T4, NC, RD, NW>(acc, hbuf, rw, voff, p.wh_off + l * (HP / 4) * KS, gh, lane);
-            prime_after(l);
+            prime_after(l, gh, go);
             tile_sync();  // every wave is done reading this layer's input
-            bias_relu_store<T4, NC, NW>(acc, p.bh + (size_t)l * HP, wave, lane, kr, hbuf);
+            bias_relu_store<T4, NC, NW>(acc, s_bias + (l + 1) * HP, wave, lane, kr, hbuf);
             tile_sync();
         }
+        // the next tile's inputs to their buffer, while the output layer's weight ring
+        // is in flight; ordered before the next tile's layer 1 by the barrier at the end
+        if (has_next) stage(tile + gridDim.x, false);
         trace_mark(p, tile, 3);
 
         // ---- output Dense layers + bias/denorm/limit/mask epilogue ----
@@ -1172,12 +1200,14 @@ static int dense_forward_impl(const fv3_dense_model* m, const void* const* input
     // (with 8-wave blocks, wide inputs keep 32-column tiles at one block per CU: the
     // emulator 7.12 -> 6.66 ms; 16-column tiles remain for widths < 128)
     const bool wide = (size_t)2 * 16 * 4 * m->kp > 64 * 1024;
-    // LDS of a block: activations (NC x HT tiles x 64 lanes x 16 B) or the staged inputs
-    // (NC x kp features x 16 columns), whichever is larger, then the constants and one
-    // dummy f32x4 (the staging stores of lanes past a slot's rows land there)
+    // LDS of a block: activations (NC x HT tiles x 64 lanes x 16 B), the staged inputs
+    // (NC x kp features x 16 columns), then the constants, one
+    // dummy f32x4 (the staging stores of lanes past a slot's rows land there) and the
+    // hidden-layer biases
     auto lds_of = [&](int c) {
         const size_t hb = (size_t)c * 16 * 64 * (size_t)m->ht, xb = (size_t)c * sizeof(float) * 16 * (size_t)m->kp;
-        return std::max(hb, xb) + sizeof(float) * (2 * (size_t)m->kp + 6 * 16 * (size_t)m->n_otiles) + 16;
+        return hb + xb + sizeof(float) * (2 * (size_t)m->kp + 6 * 16 * (size_t)m->n_otiles) + 16 +
+               sizeof(float) * (1 + (size_t)m->tmpl.n_hidden_extra) * 16 * (size_t)m->ht;
     };
     int nc = wide && (m->w1_off8 < 0 || lds_of(2) > 160 * 1024) ? 1 : 2;
     if (const char* e = getenv("FV3_DENSE_NC")) nc = atoi(e) == 1 ? 1 : 2;
@@ -1245,8 +1275,9 @@ static int dense_forward_impl(const fv3_dense_model* m, const void* const* input
         a.fast_stage = fast;
     }
     hipStream_t s = (hipStream_t)stream;
-    const size_t abytes = std::max((size_t)nc * 16 * 64 * (size_t)m->ht, (size_t)nc * sizeof(float) * 16 * (size_t)m->kp);
-    a.lds_x = (int)(abytes / 16);
+    const size_t hbytes = (size_t)nc * 16 * 64 * (size_t)m->ht, xbytes = (size_t)nc * sizeof(float) * 16 * (size_t)m->kp;
+    a.lds_s = (int)(hbytes / 16);
+    a.lds_x = (int)((hbytes + xbytes) / 16);
     const size_t lds = lds_of(nc);
     FV3_REQUIRE(lds <= 160 * 1024, "dense_forward: %d input features need too much LDS", m->kp);
     // (waves per SIMD targeted by register allocation, weight ring depth):

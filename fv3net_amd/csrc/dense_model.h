@@ -63,7 +63,8 @@ struct DenseArgs {
     int64_t ncol, ncol_blk, ntiles;
     int n_in, n_hidden_extra, n_otiles, kp;
     int in_steps_total, nslots;
-    int lds_x;              // f32x4 offset of the constants area (after activations / inputs)
+    int lds_x;              // f32x4 offset of the constants area (after activations and inputs)
+    int lds_s;              // f32x4 offset of the staged inputs (after the activations)
     int has_log;            // any slot with a LogTransform (selects the staging variant)
     int fast_stage;         // every slot FPS-aligned: the short staging path
     long long* trace;       // profiling hook (fv3_dense_set_trace): [tiles][8] timestamps, or NULL
