@@ -76,6 +76,18 @@ def run(res, nc, wpe=2, warm=20):
             prev = ee[ee <= t_s]
             if len(prev):
                 gaps.append(t_s - prev[-1])
+    # co-resident pairs: phase ends of the earlier- and later-finishing block of a 2-block CU
+    pairs = [np.where(cu == c)[0] for c in np.unique(cu) if (cu == c).sum() == 2]
+    if pairs:
+        a = np.array([sorted(pp, key=lambda i: ts[i, 5]) for pp in pairs])
+        for k, lab in ((0, "first-done"), (1, "second-done")):
+            sel = a[:, k]
+            print(f"   pair {lab:11s}: phase ends (us) " + " ".join(
+                f"{n}={ts[sel, i + 1].mean():5.1f}" for i, n in enumerate(names)))
+        single = np.array([np.where(cu == c)[0][0] for c in np.unique(cu) if (cu == c).sum() == 1])
+        if len(single):
+            print(f"   single-block CU  : phase ends (us) " + " ".join(
+                f"{n}={ts[single, i + 1].mean():5.1f}" for i, n in enumerate(names)))
     g = np.array(gaps) if gaps else np.zeros(1)
     print(f"   per-CU blocks in flight: max {np.max(conc_max):.0f}, time-mean {np.mean(conc_mean):.2f}; "
           f"refill gap p50 {np.percentile(g, 50):.2f} p90 {np.percentile(g, 90):.2f} us")
