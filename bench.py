@@ -138,7 +138,9 @@ def with_counters(leg, rec, alg_bytes=None):
         # issue peaks (tools/valu_calib.py -> profiles/valu_calib.json: 1.68 full-rate,
         # 0.97 half-rate, 0.49 transcendental wave-instructions per CU-cycle) over the
         # CU-cycles the launch took (GRBM_GUI_ACTIVE / 8 XCDs, the same dispatch)
-        cu_cycles = W.N_CU * r["grbm_gui_active"] / 8
+        from fv3net_amd.workloads import N_CU
+
+        cu_cycles = N_CU * r["grbm_gui_active"] / 8
         rec["valu_issue_frac"] = r["valu_issue_cu_cycles"] / cu_cycles
         if r.get("valu_issue_cu_cycles_lo"):  # the unsplit rest (v_mov among it) at full rate
             rec["valu_issue_frac_lo"] = r["valu_issue_cu_cycles_lo"] / cu_cycles
