@@ -284,6 +284,61 @@ def host_to_host(dev, res, steps=10):
             "note": "float64 numpy in -> pinned double-buffered H2D -> fused predict (f64 read in place) -> pinned D2H -> float32 numpy"}
 
 
+def predict_mappm_host_to_host(dev, res=384, steps=5):
+    """north_star's predict + mappm with the host boundary included: float64 numpy T/q
+    (z, rows, x) and float32 numpy edge pressures pe1/pe2 (z+1, columns; f2py hands the
+    reference's mappm float32 arrays) in, through the product's pinned double-buffered
+    staging, the fused predict reading float64 in place, the two-field mappm of both
+    tendencies, and the float32 remapped tendencies back to numpy.  Wall time per step."""
+    import torch
+
+    from fv3net_amd import transfer
+    from fv3net_amd import workloads as W
+    from fv3net_amd.mappm import MappmMultiPlan
+
+    wl = W.make_predict_mappm_workload(res, seed=21, device=dev)
+    T = wl.inputs[0].double().cpu().numpy()
+    q = wl.inputs[1].double().cpu().numpy()
+    pe1 = wl.pe1.cpu().numpy()
+    pe2 = wl.pe2.cpu().numpy()
+    dT = torch.empty(T.shape, dtype=torch.float64, device=dev)
+    dq = torch.empty(q.shape, dtype=torch.float64, device=dev)
+    d1 = torch.empty_like(wl.pe1)
+    d2 = torch.empty_like(wl.pe2)
+    bound = wl.model.bind([dT, dq], level_axes=[0, 0], outputs=wl.outputs, out_level_axis=0)
+    plan = MappmMultiPlan(d1, [o.view(o.shape[0], -1) for o in wl.outputs], d2, 1, 1, out=wl.remapped)
+    host_out = [np.empty(tuple(r.shape), np.float32) for r in wl.remapped]
+
+    def step():
+        transfer.h2d(T, out=dT)
+        transfer.h2d(q, out=dq)
+        transfer.h2d(pe1, out=d1)
+        transfer.h2d(pe2, out=d2)
+        bound()
+        plan()
+        for h, o in zip(host_out, wl.remapped):
+            transfer.d2h(o, out=h)
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    wall = (time.perf_counter() - t0) / steps
+    nbytes = T.nbytes + q.nbytes + pe1.nbytes + pe2.nbytes + sum(h.nbytes for h in host_out)
+    # the same state device-resident (float32 inputs: the f64 host values are their exact
+    # widening) must give the same bits
+    wl.step()
+    wl.step()
+    same = all(np.array_equal(h.view(np.uint32), r.cpu().numpy().view(np.uint32))
+               for h, r in zip(host_out, wl.remapped))
+    return {"columns_per_s": wl.ncol / wall, "ms_per_step": wall * 1e3, "host_bytes_per_step": nbytes,
+            "pcie_inclusive_gbs": nbytes / wall / 1e9, "bit_identical_to_device_resident": bool(same),
+            "note": "float64 numpy T/q + float32 numpy pe1/pe2 in -> pinned double-buffered H2D -> fused predict "
+                    "(f64 read in place) -> two-field mappm of dQ1/dQ2 (kord 1, iv 1) -> pinned D2H -> float32 numpy"}
+
+
 def rank_call_host_to_host(dev, calls=30):
     """The reference's real per-rank call: one rank's C48 subdomain,
     (79, 48, 48) float64 host arrays of T / q in a Dataset, through the drop-in
@@ -485,6 +540,7 @@ def extra_measurements(dev, settle_ms=150.0):
     for res in (48, 384):
         out[f"dense_c{res}_host_to_host"] = host_to_host(dev, res)
     out["dense_c48_rank_call_host_to_host"] = rank_call_host_to_host(dev)
+    out["predict_mappm_c384_host_to_host"] = predict_mappm_host_to_host(dev)
     torch.cuda.empty_cache()
     return out
 

@@ -41,3 +41,20 @@ def test_float64_host_inputs_cast_on_device(gpu):
     a = np.random.default_rng(0).normal(0, 1, (79, 3000)) * 10.0 ** np.random.default_rng(1).integers(-30, 30, (79, 1))
     t = _device.to_device_f32(a)
     assert (t.cpu().numpy().view(np.uint32) == a.astype(np.float32).view(np.uint32)).all()
+
+
+@pytest.mark.gpu
+def test_predict_mappm_host_to_host_matches_device_resident(gpu):
+    """north_star's predict + mappm through the host boundary (bench.py's
+    predict_mappm_c384_host_to_host leg, here at C24): float64 numpy T/q and float32
+    numpy edge pressures in, float32 numpy remapped tendencies out, bit-identical to the
+    same state run device-resident."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    rec = bench.predict_mappm_host_to_host(gpu, res=24, steps=1)
+    assert rec["bit_identical_to_device_resident"]
+    assert rec["host_bytes_per_step"] > 0
