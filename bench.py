@@ -70,17 +70,38 @@ def timed_steps(step, steps, warmup, dist=None, settle_ms=0.0):
 
     # the settle keeps the GPU busy without a gap: the host waits on the event recorded
     # a few batches back (bounding the queue), never on an empty queue, so the clock
-    # ramp is not reset by idle gaps every batch
-    t_end = time.perf_counter() + settle_ms * 1e-3
-    marks = []
-    while settle_ms > 0 and time.perf_counter() < t_end:
+    # ramp is not reset by idle gaps every batch.  It runs for at least settle_ms and
+    # then until the per-batch time has converged (the last 4 batches of 100 steps within
+    # 1 % of each other), at most 10x settle_ms: on a box that was idle before the
+    # process started, 300 ms left the first timed launches ~8 % slow (r03f: 46.3 us
+    # vs 42.7 us for the same kernel a minute later on the same box)
+    t_start = time.perf_counter()
+    t_min, t_max = t_start + settle_ms * 1e-3, t_start + 10.0 * settle_ms * 1e-3
+    marks, batch_ms = [], []
+    prev = None
+    while settle_ms > 0:
+        now = time.perf_counter()
+        if now >= t_max:
+            break
+        if now >= t_min and len(batch_ms) >= 4:
+            last = batch_ms[-4:]
+            if max(last) <= 1.01 * min(last):
+                break
+        if prev is None:
+            prev = torch.cuda.Event(enable_timing=True)
+            prev.record()
         for _ in range(100):
             step()
-        ev = torch.cuda.Event()
+        ev = torch.cuda.Event(enable_timing=True)
         ev.record()
-        marks.append(ev)
+        marks.append((prev, ev))
+        prev = ev
         if len(marks) > 4:
-            marks.pop(0).synchronize()
+            a, b = marks.pop(0)
+            b.synchronize()
+            batch_ms.append(a.elapsed_time(b))
+    for a, b in marks:
+        b.synchronize()
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()

@@ -92,7 +92,7 @@ def test_random_vs_oracle_bit_exact(gpu, km, kn, ncol):
 @pytest.mark.parametrize("km,kn,ncol", [(5, 9, 257), (79, 79, 777), (127, 40, 300)])
 def test_cs_lds_path_vs_oracle_bit_exact(gpu, km, kn, ncol, monkeypatch):
     """kord > 7 with the edge-solve scratch in LDS (FV3_MAPPM_LDS=1) instead of the
-    default global scratch: the same arithmetic, bit-identical."""
+    default register / global scratch: the same arithmetic, bit-identical."""
     from fv3net_amd.mappm import mappm_device
 
     monkeypatch.setenv("FV3_MAPPM_LDS", "1")
@@ -102,6 +102,61 @@ def test_cs_lds_path_vs_oracle_bit_exact(gpu, km, kn, ncol, monkeypatch):
         for iv in (0, 1, -1, 2):
             res = mappm_device(pe1, q, pe2, iv, kord).cpu().numpy()
             assert _bits_equal(res, oracle_mappm(pe1, q, pe2, iv, kord)), (kord, iv)
+
+
+@pytest.mark.parametrize("km,kn,ncol", [(5, 9, 257), (79, 79, 777), (127, 40, 300)])
+def test_cs_global_scratch_path_vs_oracle_bit_exact(gpu, km, kn, ncol, monkeypatch):
+    """kord > 7 with both edge-solve planes in the global scratch (FV3_MAPPM_CS=global;
+    the default keeps the edge values in registers up to km = 92): bit-identical."""
+    from fv3net_amd.mappm import mappm_device
+
+    monkeypatch.setenv("FV3_MAPPM_CS", "global")
+    rng = np.random.default_rng(km * kn + ncol + 1)
+    pe1, q, pe2 = _columns(rng, km, kn, ncol)
+    for kord in (8, 10, 13, 17):
+        for iv in (0, 1, -1, 2):
+            res = mappm_device(pe1, q, pe2, iv, kord).cpu().numpy()
+            assert _bits_equal(res, oracle_mappm(pe1, q, pe2, iv, kord)), (kord, iv)
+
+
+@pytest.mark.parametrize("km,kn,ncol", [(4, 3, 65), (29, 31, 300), (31, 31, 64), (32, 9, 100), (61, 61, 129),
+                                        (63, 70, 64), (89, 50, 200), (92, 92, 333), (93, 40, 70)])
+def test_cs_register_scratch_chunk_boundaries(gpu, km, kn, ncol):
+    """The register-resident edge values (mappm_cs_reg_kernel) at km around the 32-level
+    vector boundaries of k and k + 3, up to its km = 92 limit (93: the global kernel)."""
+    from fv3net_amd.mappm import mappm_device
+
+    rng = np.random.default_rng(km * 31 + kn)
+    pe1, q, pe2 = _columns(rng, km, kn, ncol)
+    for kord in (8, 9, 10, 11, 12, 13, 14, 15, 16, 17):
+        for iv in (0, 1, -1, 2):
+            res = mappm_device(pe1, q, pe2, iv, kord).cpu().numpy()
+            assert _bits_equal(res, oracle_mappm(pe1, q, pe2, iv, kord)), (kord, iv)
+
+
+def test_c384_scale_kord10_sampled_bit_exact(gpu):
+    """config #3's kord 10 leg at its C384 size (884,736 columns, 79->79) through the
+    default (register-scratch) kernel: sampled columns bit-exact against the oracle."""
+    import torch
+
+    from fv3net_amd.mappm import mappm_device
+
+    rng = np.random.default_rng(3841)
+    ncol, km = 6 * 384 * 384, 79
+    base = np.linspace(200, 1800, km, dtype=np.float32)[:, None]
+    delp = (base * rng.uniform(0.99, 1.01, (km, ncol))).astype(np.float32)
+    pe1 = np.concatenate([np.full((1, ncol), 300, np.float32), 300 + np.cumsum(delp, 0, dtype=np.float32)])
+    d2 = (base * rng.uniform(0.99, 1.01, (km, ncol))).astype(np.float32)
+    pe2 = np.concatenate([np.full((1, ncol), 300, np.float32), 300 + np.cumsum(d2, 0, dtype=np.float32)])
+    q = rng.normal(250, 10, (km, ncol)).astype(np.float32)
+    res = mappm_device(pe1, q, pe2, 1, 10)
+    torch.cuda.synchronize()
+    res = res.cpu().numpy()
+    assert np.isfinite(res).all()
+    idx = np.sort(np.concatenate([np.arange(64), rng.choice(ncol, 4096, replace=False), np.arange(ncol - 64, ncol)]))
+    idx = np.unique(idx)
+    ref = oracle_mappm(pe1[:, idx], q[:, idx], pe2[:, idx], 1, 10)
+    assert _bits_equal(res[:, idx], ref)
 
 
 def test_tile_layout_in_place(gpu):
