@@ -278,8 +278,9 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
     };
     // layer chunk: unit tile t accumulates A_t x B (one 32-deep k-step); tiles in pairs,
     // their MFMAs interleaved, fragments read one pair ahead
-    auto step_layer = [&](const bf16x8& bh, const bf16x8& bl) {
+    auto step_layer = [&](const bf16x8& bh, const bf16x8& bl, auto&& after_stage) {
         stage_next();
+        after_stage();  // loads issued after this chunk's weight loads (vmcnt is in order)
         bf16x8 fa[4][2];
         frag(slot, 0, fa[0]);
         frag(slot, 1, fa[1]);
@@ -314,11 +315,17 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
         // all 8 loads issued unconditionally (levels past nv read the group's first level,
         // always in range, and are zeroed after), so none waits behind a branch
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {  // read once: keep them from evicting the weight stream in L2
+        for (int j = 0; j < 8; ++j) {
 #ifdef FV3_B3_EXP_NOIN  // experiment only (results invalid): no input loads
             const float x = 1.0f + (float)(uintptr_t)(ptr + (j < nv ? j * ld : 0)) * 0.0f;
 #else
+#ifdef FV3_B3_EXP_NT_IN  // A/B: nontemporal input loads (round 2's default)
             const float x = __builtin_nontemporal_load(ptr + (j < nv ? j * ld : 0));
+#else
+            // plain (cacheable) loads: the residual outputs re-read T / q / qc one tile
+            // later (emulator C384 2.55 -> 2.36 ms against nontemporal loads, round 3)
+            const float x = ptr[j < nv ? j * ld : 0];
+#endif
 #endif
             raw[j] = j < nv ? x : 0.0f;
         }
@@ -459,12 +466,20 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
         for (int c = 0; c < p.n1; c += 2) {
             bf16x8 xh, xl;
             stage_in(rawA, c, xh, xl);
+#ifdef FV3_B3_EXP_INLATE
+            step_layer(xh, xl, [&]() { if (c + 2 < p.n1) load_in(rawA, c + 2); });
+#else
             if (c + 2 < p.n1) load_in(rawA, c + 2);
-            step_layer(xh, xl);
+            step_layer(xh, xl, [] {});
+#endif
             if (c + 1 < p.n1) {
                 stage_in(rawB, c + 1, xh, xl);
+#ifdef FV3_B3_EXP_INLATE
+                step_layer(xh, xl, [&]() { if (c + 3 < p.n1) load_in(rawB, c + 3); });
+#else
                 if (c + 3 < p.n1) load_in(rawB, c + 3);
-                step_layer(xh, xl);
+                step_layer(xh, xl, [] {});
+#endif
             }
         }
         hidden_epi(0);
@@ -473,7 +488,7 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
             zero_acc();
             sfor<KS>([&](auto cc) {
                 constexpr int c = decltype(cc)::value;
-                step_layer(Bh[c], Bl[c]);
+                step_layer(Bh[c], Bl[c], [] {});
             });
             hidden_epi(l + 1);
         }
@@ -487,10 +502,16 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
         b3f4 accP[2];
         float resN[2][4], resP[2][4];
         for (int oc = 0; oc < p.n_oc; ++oc) {
+#ifndef FV3_B3_EXP_RESLATE
             res_load(2 * oc, resN[0]);  // lands while this chunk and the next run their MFMAs
             res_load(2 * oc + 1, resN[1]);
+#endif
             acc[0] = acc[1] = b3f4{0.0f, 0.0f, 0.0f, 0.0f};
             stage_next();
+#ifdef FV3_B3_EXP_RESLATE  // after the weight loads: the next chunk's staging does not wait for them
+            res_load(2 * oc, resN[0]);
+            res_load(2 * oc + 1, resN[1]);
+#endif
             step_out();
             if (oc > 0) {  // finish the previous chunk while these MFMAs run
                 out_tile(accP[0], 2 * oc - 2, resP[0]);

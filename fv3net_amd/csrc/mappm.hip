@@ -18,7 +18,6 @@
 #include "mappm_multi.h"
 
 #include <cstdlib>
-#include <utility>
 
 namespace fv3 {
 namespace {
@@ -51,7 +50,7 @@ struct DevCol {
     }
 };
 
-struct LdsScr : PlainScrLoops<LdsScr> {
+struct LdsScr {
     float* base;  // [2][km+3][blockDim]
     int stride;   // blockDim.x
     int plane;    // (km+3) * blockDim.x
@@ -62,7 +61,7 @@ struct LdsScr : PlainScrLoops<LdsScr> {
 // The same [2][km+3][column] scratch in global memory (stream-ordered allocation):
 // coalesced like the column arrays, and unlike LDS (42 KB per 64 columns at km = 79,
 // i.e. 3 waves per CU) it leaves occupancy to the VGPR budget.
-struct GlobalScr : PlainScrLoops<GlobalScr> {
+struct GlobalScr {
     float* base;     // scratch + column
     int64_t stride;  // padded column count
     int64_t plane;   // (km+3) * stride
@@ -279,10 +278,7 @@ __global__ __launch_bounds__(64) void mappm_cs_kernel(MappmArgs a)
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= a.ncol) return;
-    LdsScr scr;
-    scr.base = lds + threadIdx.x;
-    scr.stride = (int)blockDim.x;
-    scr.plane = (a.km + 3) * (int)blockDim.x;
+    LdsScr scr{lds + threadIdx.x, (int)blockDim.x, (a.km + 3) * (int)blockDim.x};
     DevCol col = make_col(a, c);
     mappm_cs_column(col, scr, a.km, a.kn, a.iv, a.kord);
 }
@@ -292,78 +288,7 @@ __global__ __launch_bounds__(256) void mappm_cs_global_kernel(MappmArgs a)
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= a.ncol) return;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    GlobalScr scr;
-    scr.base = a.scratch + c;
-    scr.stride = stride;
-    scr.plane = (int64_t)(a.km + 3) * stride;
-    DevCol col = make_col(a, c);
-    mappm_cs_column(col, scr, a.km, a.kn, a.iv, a.kord);
-}
-
-// kord > 7 with the solved edge values in REGISTERS (km <= kRegScrMaxKm): edge(k),
-// k = 0..95, lives in three 32-wide vectors and only gam(k) goes to the global scratch
-// (one plane).  The edge values were the scratch's three round trips per level (forward
-// sweep write, back-substitution read + write, remap read); gam is written once and read
-// once.  Every edge access sits in a loop whose range of k + d lies in ONE vector, named
-// at compile time (RegScr::up / down split each loop at the 32-level boundaries), with a
-// wave-uniform element index, so the compiler indexes the registers in place
-// (s_set_gpr_idx) instead of going through scratch memory.
-typedef float v32f __attribute__((ext_vector_type(32)));
-constexpr int kRegScrMaxKm = 92;  // edge(L + 3) of the last layer: km + 3 <= 95
-
-template <typename F, int... I>
-__device__ __forceinline__ void cfor_impl(F&& f, std::integer_sequence<int, I...>)
-{
-    (f(std::integral_constant<int, I>{}), ...);
-}
-
-struct RegScr {
-    v32f &c0, &c1, &c2;  // the kernel's own locals: three separate allocas the compiler
-                         // promotes to registers (one struct of them stays in scratch)
-    float* gbase;    // gam plane + column
-    int64_t stride;  // padded column count
-    __device__ __forceinline__ float& g(int k) { return gbase[k * stride]; }
-    template <int C>
-    __device__ __forceinline__ v32f& vec()
-    {
-        if constexpr (C == 0) return c0;
-        else if constexpr (C == 1) return c1;
-        else return c2;
-    }
-    template <int C>
-    struct View {  // edge(j) for j >> 5 == C
-        RegScr& r;
-        __device__ __forceinline__ float get(int j) { return r.vec<C>()[j & 31]; }
-        __device__ __forceinline__ void set(int j, float v) { r.vec<C>()[j & 31] = v; }
-    };
-    template <class F>
-    __device__ __forceinline__ void up(int lo, int hi, int d, F&& f)
-    {
-        cfor_impl([&](auto cc) {
-            constexpr int C = decltype(cc)::value;
-            View<C> e{*this};
-            const int a = max(lo, 32 * C - d), b = min(hi, 32 * C + 31 - d);
-            for (int k = a; k <= b; ++k) f(k, e);
-        }, std::make_integer_sequence<int, 3>{});
-    }
-    template <class F>
-    __device__ __forceinline__ void down(int hi, int lo, int d, F&& f)
-    {
-        cfor_impl([&](auto cc) {
-            constexpr int C = 2 - decltype(cc)::value;
-            View<C> e{*this};
-            const int a = min(hi, 32 * C + 31 - d), b = max(lo, 32 * C - d);
-            for (int k = a; k >= b; --k) f(k, e);
-        }, std::make_integer_sequence<int, 3>{});
-    }
-};
-
-__global__ __launch_bounds__(256) void mappm_cs_reg_kernel(MappmArgs a)
-{
-    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= a.ncol) return;
-    v32f e0, e1, e2;
-    RegScr scr{e0, e1, e2, a.scratch + c, (int64_t)gridDim.x * blockDim.x};
+    GlobalScr scr{a.scratch + c, stride, (int64_t)(a.km + 3) * stride};
     DevCol col = make_col(a, c);
     mappm_cs_column(col, scr, a.km, a.kn, a.iv, a.kord);
 }
@@ -384,17 +309,7 @@ bool use_levels_kernel(const MappmArgs& a)
 int launch_mappm(MappmArgs a, hipStream_t stream)
 {
     if (a.ncol == 0) return FV3_OK;
-    const char* cs_path = getenv("FV3_MAPPM_CS");  // "global" / "lds": the older variants (A/B, tests)
-    if (a.kord > 7 && a.km <= kRegScrMaxKm && !getenv("FV3_MAPPM_LDS") && !(cs_path && cs_path[0] != 'r')) {
-        const int block = 256;
-        const int64_t grid = (a.ncol + block - 1) / block;
-        FV3_HIP(hipMallocAsync((void**)&a.scratch, sizeof(float) * (size_t)(a.km + 3) * (size_t)grid * block, stream));
-        hipLaunchKernelGGL(mappm_cs_reg_kernel, dim3((unsigned)grid), dim3(block), 0, stream, a);
-        FV3_LAUNCH_CHECK();
-        FV3_HIP(hipFreeAsync(a.scratch, stream));
-        return FV3_OK;
-    }
-    if (a.kord > 7 && !getenv("FV3_MAPPM_LDS") && !(cs_path && cs_path[0] == 'l')) {
+    if (a.kord > 7 && !getenv("FV3_MAPPM_LDS")) {
         const int block = 256;
         const int64_t grid = (a.ncol + block - 1) / block;
         FV3_HIP(hipMallocAsync((void**)&a.scratch, sizeof(float) * 2 * (size_t)(a.km + 3) * (size_t)grid * block,

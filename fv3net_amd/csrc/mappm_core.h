@@ -752,29 +752,8 @@ FV3_HD inline void mappm_ppm_column_by_output(Col& c, int km, int kn, int iv, in
 
 // ---- one column, kord > 7 (cs_profile path) ----
 //
-// `Scr` is per-column scratch of 2*(km+2) floats: edge(k) for k = 1..km+1 and gam(k),
-// gam addressed by scr.g(k).  Every access to the edge values goes through the loop
-// interface scr.up(lo, hi, d, f) / scr.down(hi, lo, d, f): f(k, E) for k = lo..hi
-// (ascending / descending), where E.get(j) / E.set(j, v) read / write edge(j) for
-// j = k + d only.  A plain scratch (LDS, global memory, the host test) is its own E
-// (PlainScrLoops); the device's register-resident scratch (mappm.hip) hands f a view
-// whose register vector is fixed at compile time for each range of k.
-template <class D>
-struct PlainScrLoops {
-    FV3_HD float get(int k) { return static_cast<D*>(this)->e(k); }
-    FV3_HD void set(int k, float v) { static_cast<D*>(this)->e(k) = v; }
-    template <class F>
-    FV3_HD void up(int lo, int hi, int, F&& f)
-    {
-        for (int k = lo; k <= hi; ++k) f(k, *static_cast<D*>(this));
-    }
-    template <class F>
-    FV3_HD void down(int hi, int lo, int, F&& f)
-    {
-        for (int k = hi; k >= lo; --k) f(k, *static_cast<D*>(this));
-    }
-};
-
+// `Scr` is per-column scratch of 2*(km+2) floats: edge(k) for k = 1..km+1 and
+// gam(k), addressed by scr.e(k) / scr.g(k) (LDS on the device).
 template <class Col, class Scr>
 FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int kord)
 {
@@ -788,32 +767,32 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
         if (iv == -2) {
             scr.g(2) = 0.5f;
             float qprev = 1.5f * qm1;
-            scr.up(1, 1, 0, [&](int k, auto& E) { E.set(k, qprev); });
+            scr.e(1) = qprev;
             float gk = 0.5f;  // gam(k)
             float pek = pe1v;
-            scr.up(2, km - 1, 0, [&](int k, auto& E) {
+            for (int k = 2; k <= km - 1; ++k) {
                 const float qk = c.q1(k);
                 const float pen = c.pe1(k + 1);
                 const float dpk = pen - pek;
                 const float grat = dpm1 / dpk;
                 const float bet = 2.0f + grat + grat - gk;
                 qprev = (3.0f * (qm1 + qk) - qprev) / bet;
-                E.set(k, qprev);
+                scr.e(k) = qprev;
                 gk = grat / bet;
                 scr.g(k + 1) = gk;
                 qm1 = qk; dpm1 = dpk; pek = pen;
-            });
+            }
             const float qkm = c.q1(km);
             const float dpkm = c.pe1(km + 1) - pek;
             const float grat = dpm1 / dpkm;
             qprev = (3.0f * (qm1 + qkm) - grat * qs - qprev) / (2.0f + grat + grat - gk);
-            scr.up(km, km, 0, [&](int k, auto& E) { E.set(k, qprev); });
-            scr.up(km + 1, km + 1, 0, [&](int k, auto& E) { E.set(k, qs); });
+            scr.e(km) = qprev;
+            scr.e(km + 1) = qs;
             float qn = qprev;
-            scr.down(km - 1, 1, 0, [&](int k, auto& E) {
-                qn = E.get(k) - scr.g(k + 1) * qn;
-                E.set(k, qn);
-            });
+            for (int k = km - 1; k >= 1; --k) {
+                qn = scr.e(k) - scr.g(k + 1) * qn;
+                scr.e(k) = qn;
+            }
         } else {
             float q2v = c.q1(2);
             float pe2v = c.pe1(3);
@@ -822,13 +801,13 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
             float bet = grat * (grat + 0.5f);
             float qprev = ((grat + grat) * (grat + 1.0f) * qm1 + q2v) / bet;
             float gprev = (1.0f + grat * (grat + 1.5f)) / bet;
-            scr.up(1, 1, 0, [&](int k, auto& E) { E.set(k, qprev); });
+            scr.e(1) = qprev;
             scr.g(1) = gprev;
             float d4 = 0.0f;
             float pek = pe1v;
             float qkm1 = qm1;
             float qk = qm1;
-            scr.up(2, km, 0, [&](int k, auto& E) {
+            for (int k = 2; k <= km; ++k) {
                 qk = c.q1(k);
                 const float pen = c.pe1(k + 1);
                 const float dpk = pen - pek;
@@ -836,19 +815,19 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
                 bet = 2.0f + d4 + d4 - gprev;
                 qprev = (3.0f * (qkm1 + d4 * qk) - qprev) / bet;
                 gprev = d4 / bet;
-                E.set(k, qprev);
+                scr.e(k) = qprev;
                 scr.g(k) = gprev;
                 qkm1 = qk; dpm1 = dpk; pek = pen;
-            });
+            }
             // qkm1 == qk == q(km) here; need q(km-1)
             const float a_bot = 1.0f + d4 * (d4 + 1.5f);
             const float qkmm1 = c.q1(km - 1);
             float qn = (2.0f * d4 * (d4 + 1.0f) * qk + qkmm1 - a_bot * qprev) / (d4 * (d4 + 0.5f) - a_bot * gprev);
-            scr.up(km + 1, km + 1, 0, [&](int k, auto& E) { E.set(k, qn); });
-            scr.down(km, 1, 0, [&](int k, auto& E) {
-                qn = E.get(k) - scr.g(k) * qn;
-                E.set(k, qn);
-            });
+            scr.e(km + 1) = qn;
+            for (int k = km; k >= 1; --k) {
+                qn = scr.e(k) - scr.g(k) * qn;
+                scr.e(k) = qn;
+            }
         }
     }
 
@@ -857,7 +836,8 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
 
     // constrained edge qc(k) (mappm.f90:207-260) from the solved edge e(k) and
     // q1(k-2..k+1); the large-scale constraints use gam(k) = q1(k) - q1(k-1).
-    auto edge_c = [&](int k, float q, float qkm2, float qkm1, float qk0, float qkp1) -> float {
+    auto edge_c = [&](int k, float qkm2, float qkm1, float qk0, float qkp1) -> float {
+        float q = scr.e(k);
         if (akord > 16 || k <= 1 || k >= km + 1) return q;
         if (k == 2 || k == km) {
             q = fmin2(q, fmax2(qkm1, qk0));
@@ -883,15 +863,12 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
     float qw[6], qcw[4];
     for (int i = 0; i < 6; ++i) qw[i] = q1_or0(i - 1);
     qcw[0] = 0.0f;
-    scr.up(1, 3, 0, [&](int k, auto& E) {
-        if (k == 1) qcw[1] = edge_c(1, E.get(1), 0.0f, 0.0f, qw[2], qw[3]);
-        else if (k == 2) qcw[2] = edge_c(2, E.get(2), 0.0f, qw[2], qw[3], qw[4]);
-        else qcw[3] = edge_c(3, E.get(3), qw[2], qw[3], qw[4], qw[5]);
-    });
+    qcw[1] = edge_c(1, 0.0f, 0.0f, qw[2], qw[3]);
+    qcw[2] = edge_c(2, 0.0f, qw[2], qw[3], qw[4]);
+    qcw[3] = edge_c(3, qw[2], qw[3], qw[4], qw[5]);
     float pl0 = c.pe1(1), pl1 = c.pe1(2);
 
-    // layer L reads edge(L + 3) for its window advance (d = 3)
-    scr.up(1, km, 3, [&](int L, auto& E) {
+    for (int L = 1; L <= km; ++L) {
         Ppm a{qw[2], qcw[1], qcw[2], 0.0f};
         if (akord > 16) {
             a.a6 = a6_of(a);  // perfectly linear scheme (mappm.f90:207-216)
@@ -1010,15 +987,14 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
         }
         const LayerView v{pl0, pl1, pl1 - pl0, qw[2], a};
         remap_layer_fast(s, v, ends, kn, c);
-        if (L < km) {
-            for (int i = 0; i < 5; ++i) qw[i] = qw[i + 1];
-            qw[5] = q1_or0(L + 4);
-            for (int i = 0; i < 3; ++i) qcw[i] = qcw[i + 1];
-            qcw[3] = (L + 3 <= km + 1) ? edge_c(L + 3, E.get(L + 3), qw[2], qw[3], qw[4], qw[5]) : 0.0f;
-            pl0 = pl1;
-            pl1 = c.pe1(L + 2);
-        }
-    });
+        if (L == km) break;
+        for (int i = 0; i < 5; ++i) qw[i] = qw[i + 1];
+        qw[5] = q1_or0(L + 4);
+        for (int i = 0; i < 3; ++i) qcw[i] = qcw[i + 1];
+        qcw[3] = (L + 3 <= km + 1) ? edge_c(L + 3, qw[2], qw[3], qw[4], qw[5]) : 0.0f;
+        pl0 = pl1;
+        pl1 = c.pe1(L + 2);
+    }
     remap_finish(s, ends, kn, c);
 }
 

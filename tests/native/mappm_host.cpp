@@ -2,7 +2,6 @@
 // Lets the CPU test suite check the one-pass algorithm bit-for-bit against the
 // oracle without a GPU.  Not part of the product library and never loaded by it.
 #include <cstdint>
-#include <algorithm>
 #include <vector>
 #include "../../fv3net_amd/csrc/mappm_core.h"
 
@@ -18,42 +17,10 @@ struct Col {
     void emit(int k, float v) { q2_[(int64_t)(k - 1) * ncol + i] = v; }
     float next_edge(int k) const { return (k + 1 <= kn + 1) ? pe2(k + 1) : 0.0f; }
 };
-struct Scr : fv3::PlainScrLoops<Scr> {
+struct Scr {
     std::vector<float> ev, gv;
     float& e(int k) { return ev[k]; }
     float& g(int k) { return gv[k]; }
-};
-// the device's register-resident scratch (mappm.hip RegScr) restated on the host: edge
-// values in three 32-float chunks, each loop split at the chunk boundaries of k + d with
-// the chunk fixed per piece; an access outside the piece's chunk is recorded (and must
-// never happen)
-struct ChunkScr {
-    float ch[3][32];
-    std::vector<float> gv;
-    int bad = 0;
-    float& g(int k) { return gv[k]; }
-    struct View {
-        ChunkScr& r;
-        int C;
-        float get(int j) { r.bad += (j >> 5) != C; return r.ch[C][j & 31]; }
-        void set(int j, float v) { r.bad += (j >> 5) != C; r.ch[C][j & 31] = v; }
-    };
-    template <class F>
-    void up(int lo, int hi, int d, F&& f)
-    {
-        for (int C = 0; C < 3; ++C) {
-            View e{*this, C};
-            for (int k = std::max(lo, 32 * C - d); k <= std::min(hi, 32 * C + 31 - d); ++k) f(k, e);
-        }
-    }
-    template <class F>
-    void down(int hi, int lo, int d, F&& f)
-    {
-        for (int C = 2; C >= 0; --C) {
-            View e{*this, C};
-            for (int k = std::min(hi, 32 * C + 31 - d); k >= std::max(lo, 32 * C - d); --k) f(k, e);
-        }
-    }
 };
 }  // namespace
 
@@ -61,9 +28,7 @@ extern "C" int host_mappm(int km, const float* pe1, const float* q1, int kn, con
                           float* q2, int64_t ncol, int iv, int kord)
 {
     if (km < 4 || kn < 1) return -1;
-    Scr scr;
-    scr.ev.assign(km + 3, 0.0f);
-    scr.gv.assign(km + 3, 0.0f);
+    Scr scr{std::vector<float>(km + 3), std::vector<float>(km + 3)};
     for (int64_t i = 0; i < ncol; ++i) {
         Col c{pe1, q1, pe2, q2, ncol, i, kn};
         if (kord > 7)
@@ -136,19 +101,4 @@ extern "C" int host_mappm_multi(int nf, int km, const float* pe1, const float* q
         case 4: run_n<4>(km, pe1, q1, kn, pe2, q2, ncol, iv, kord); return 0;
     }
     return -1;
-}
-
-// kord > 7 through the register-chunked scratch (km <= 92): -2 if any edge access fell
-// outside its piece's chunk
-extern "C" int host_mappm_cs_chunked(int km, const float* pe1, const float* q1, int kn, const float* pe2,
-                                     float* q2, int64_t ncol, int iv, int kord)
-{
-    if (km < 4 || kn < 1 || kord <= 7 || km > 92) return -1;
-    ChunkScr scr{};
-    scr.gv.assign(km + 3, 0.0f);
-    for (int64_t i = 0; i < ncol; ++i) {
-        Col c{pe1, q1, pe2, q2, ncol, i, kn};
-        fv3::mappm_cs_column(c, scr, km, kn, iv, kord);
-    }
-    return scr.bad ? -2 : 0;
 }

@@ -92,7 +92,7 @@ def test_random_vs_oracle_bit_exact(gpu, km, kn, ncol):
 @pytest.mark.parametrize("km,kn,ncol", [(5, 9, 257), (79, 79, 777), (127, 40, 300)])
 def test_cs_lds_path_vs_oracle_bit_exact(gpu, km, kn, ncol, monkeypatch):
     """kord > 7 with the edge-solve scratch in LDS (FV3_MAPPM_LDS=1) instead of the
-    default register / global scratch: the same arithmetic, bit-identical."""
+    default global scratch: the same arithmetic, bit-identical."""
     from fv3net_amd.mappm import mappm_device
 
     monkeypatch.setenv("FV3_MAPPM_LDS", "1")
@@ -104,39 +104,10 @@ def test_cs_lds_path_vs_oracle_bit_exact(gpu, km, kn, ncol, monkeypatch):
             assert _bits_equal(res, oracle_mappm(pe1, q, pe2, iv, kord)), (kord, iv)
 
 
-@pytest.mark.parametrize("km,kn,ncol", [(5, 9, 257), (79, 79, 777), (127, 40, 300)])
-def test_cs_global_scratch_path_vs_oracle_bit_exact(gpu, km, kn, ncol, monkeypatch):
-    """kord > 7 with both edge-solve planes in the global scratch (FV3_MAPPM_CS=global;
-    the default keeps the edge values in registers up to km = 92): bit-identical."""
-    from fv3net_amd.mappm import mappm_device
-
-    monkeypatch.setenv("FV3_MAPPM_CS", "global")
-    rng = np.random.default_rng(km * kn + ncol + 1)
-    pe1, q, pe2 = _columns(rng, km, kn, ncol)
-    for kord in (8, 10, 13, 17):
-        for iv in (0, 1, -1, 2):
-            res = mappm_device(pe1, q, pe2, iv, kord).cpu().numpy()
-            assert _bits_equal(res, oracle_mappm(pe1, q, pe2, iv, kord)), (kord, iv)
-
-
-@pytest.mark.parametrize("km,kn,ncol", [(4, 3, 65), (29, 31, 300), (31, 31, 64), (32, 9, 100), (61, 61, 129),
-                                        (63, 70, 64), (89, 50, 200), (92, 92, 333), (93, 40, 70)])
-def test_cs_register_scratch_chunk_boundaries(gpu, km, kn, ncol):
-    """The register-resident edge values (mappm_cs_reg_kernel) at km around the 32-level
-    vector boundaries of k and k + 3, up to its km = 92 limit (93: the global kernel)."""
-    from fv3net_amd.mappm import mappm_device
-
-    rng = np.random.default_rng(km * 31 + kn)
-    pe1, q, pe2 = _columns(rng, km, kn, ncol)
-    for kord in (8, 9, 10, 11, 12, 13, 14, 15, 16, 17):
-        for iv in (0, 1, -1, 2):
-            res = mappm_device(pe1, q, pe2, iv, kord).cpu().numpy()
-            assert _bits_equal(res, oracle_mappm(pe1, q, pe2, iv, kord)), (kord, iv)
-
-
 def test_c384_scale_kord10_sampled_bit_exact(gpu):
     """config #3's kord 10 leg at its C384 size (884,736 columns, 79->79) through the
-    default (register-scratch) kernel: sampled columns bit-exact against the oracle."""
+    default (global-scratch) kernel: the first / last wave and 4,096 sampled columns
+    bit-exact against the oracle."""
     import torch
 
     from fv3net_amd.mappm import mappm_device

@@ -83,7 +83,7 @@ def host_lib():
     subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
                     "-o", HOST_SO, HOST_SRC], check=True)
     lib = ctypes.CDLL(HOST_SO)
-    for fn in (lib.host_mappm, lib.host_mappm_cursor, lib.host_mappm_generic, lib.host_mappm_cs_chunked):
+    for fn in (lib.host_mappm, lib.host_mappm_cursor, lib.host_mappm_generic):
         fn.restype = ctypes.c_int
         fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                        ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
@@ -93,8 +93,7 @@ def host_lib():
 def _host(lib, pe1, q, pe2, iv, kord, cursor=False):
     pe1, q, pe2 = (np.ascontiguousarray(a, np.float32) for a in (pe1, q, pe2))
     out = np.empty((pe2.shape[0] - 1, q.shape[1]), np.float32)
-    fn = {True: lib.host_mappm_cursor, False: lib.host_mappm, "generic": lib.host_mappm_generic,
-          "chunked": lib.host_mappm_cs_chunked}[cursor]
+    fn = {True: lib.host_mappm_cursor, False: lib.host_mappm, "generic": lib.host_mappm_generic}[cursor]
     rc = fn(q.shape[0], pe1.ctypes.data, q.ctypes.data, pe2.shape[0] - 1, pe2.ctypes.data, out.ctypes.data,
             q.shape[1], iv, kord)
     assert rc == 0
@@ -110,48 +109,6 @@ def test_streaming_algorithm_matches_golden(host_lib):
                 for qn in ("qs", "qr"):
                     res = _host(host_lib, pe1, g[f"c{ci}_{qn}"], pe2, int(iv), int(kord))
                     assert _bits_equal(res, g[f"c{ci}_{qn}_k{kord}_iv{iv}"]), (ci, qn, kord, iv)
-
-
-def test_register_chunked_cs_scratch_matches_golden(host_lib):
-    """kord > 7 through the edge scratch as the device's register kernel lays it out
-    (mappm.hip RegScr: three 32-level chunks, every loop split at the chunk boundaries):
-    bit-identical to the golden vectors, and no access outside its piece's chunk
-    (host_mappm_cs_chunked returns -2 on one)."""
-    g = np.load(os.path.join(GOLDEN, "mappm_golden.npz"))
-    n = 0
-    for ci in range(len(g["cases"])):
-        pe1, pe2 = g[f"c{ci}_pe1"], g[f"c{ci}_pe2"]
-        if pe1.shape[0] - 1 > 92:
-            continue
-        for kord in g["kords"]:
-            if int(kord) <= 7:
-                continue
-            for iv in g["ivs"]:
-                for qn in ("qs", "qr"):
-                    res = _host(host_lib, pe1, g[f"c{ci}_{qn}"], pe2, int(iv), int(kord), cursor="chunked")
-                    assert _bits_equal(res, g[f"c{ci}_{qn}_k{kord}_iv{iv}"]), (ci, qn, kord, iv)
-                    n += 1
-    assert n > 0
-
-
-@pytest.mark.parametrize("km,kn", [(4, 3), (29, 31), (30, 50), (31, 31), (32, 9), (61, 61), (62, 20), (63, 70),
-                                   (79, 79), (89, 50), (92, 92)])
-def test_register_chunked_cs_scratch_matches_oracle(host_lib, km, kn):
-    """Chunk boundaries of k (forward / backward sweeps) and of k + 3 (the remap's edge
-    reads) at every position, iv = -2 (its own sweep) included."""
-    rng = np.random.default_rng(km * 7 + kn)
-    for kord in (8, 9, 10, 11, 12, 13, 14, 15, 16, 17):
-        for iv in (0, 1, -1, 2, -2):
-            ncol = 16
-            delp = rng.uniform(1, 3000, (km, ncol)).astype(np.float32)
-            pe1 = np.concatenate([np.full((1, ncol), 300, np.float32),
-                                  300 + np.cumsum(delp, 0, dtype=np.float32)])
-            pe2 = np.sort(rng.uniform(pe1[0] * 0.8, pe1[-1] * 1.1, (kn + 1, ncol)), 0).astype(np.float32)
-            q = (rng.normal(0, 1, (km, ncol)) * rng.choice([1e-4, 1, 300], (km, ncol))).astype(np.float32)
-            got = _host(host_lib, pe1, q, pe2, iv, kord, cursor="chunked")
-            assert _bits_equal(got, _host(host_lib, pe1, q, pe2, iv, kord)), (kord, iv)
-            if iv != -2:  # iv = -2 with kord > 7 reads the reference's uninitialised qs (UB)
-                assert _bits_equal(got, oracle_mappm(pe1, q, pe2, iv, kord)), (kord, iv)
 
 
 @pytest.mark.parametrize("kat", KATS, ids=["identity", "out_of_bounds", "nans"])
