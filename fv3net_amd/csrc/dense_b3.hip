@@ -55,6 +55,9 @@ constexpr int kB3Groups = 128;   // 8-feature input groups (<= 1024 padded input
 constexpr int kB3Cols = 128;     // columns per block tile: 8 waves x 16
 constexpr int kB3OutTiles = 32;  // 16-row output tiles (<= 512 padded output rows)
 constexpr int kB3Threads = 512;
+constexpr bool kB3GldsDefault = false;  // until the LDS-DMA pipeline is measured on the box
+constexpr int b3_slots(bool gl) { return gl ? 3 : 2; }
+constexpr int b3_in_bytes(bool gl) { return gl ? 2 * 8 * 8 * 64 * 4 : 0; }
 
 struct B3Pack {
     void* dbuf = nullptr;
@@ -182,7 +185,70 @@ __device__ __forceinline__ T sel4(int q, T a0, T a1, T a2, T a3)
     return (q & 2) ? hi : lo;
 }
 
-template <int HU>
+// s_waitcnt vmcnt(n) for a wave-uniform n (an immediate per value; n >= 47 waits for 47)
+__device__ __forceinline__ void vm_wait_le(int n)
+{
+    switch (n < 47 ? n : 47) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
+    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+    case 19: asm volatile("s_waitcnt vmcnt(19)" ::: "memory"); break;
+    case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    case 21: asm volatile("s_waitcnt vmcnt(21)" ::: "memory"); break;
+    case 22: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); break;
+    case 23: asm volatile("s_waitcnt vmcnt(23)" ::: "memory"); break;
+    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    case 25: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
+    case 26: asm volatile("s_waitcnt vmcnt(26)" ::: "memory"); break;
+    case 27: asm volatile("s_waitcnt vmcnt(27)" ::: "memory"); break;
+    case 28: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
+    case 29: asm volatile("s_waitcnt vmcnt(29)" ::: "memory"); break;
+    case 30: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
+    case 31: asm volatile("s_waitcnt vmcnt(31)" ::: "memory"); break;
+    case 32: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+    case 33: asm volatile("s_waitcnt vmcnt(33)" ::: "memory"); break;
+    case 34: asm volatile("s_waitcnt vmcnt(34)" ::: "memory"); break;
+    case 35: asm volatile("s_waitcnt vmcnt(35)" ::: "memory"); break;
+    case 36: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
+    case 37: asm volatile("s_waitcnt vmcnt(37)" ::: "memory"); break;
+    case 38: asm volatile("s_waitcnt vmcnt(38)" ::: "memory"); break;
+    case 39: asm volatile("s_waitcnt vmcnt(39)" ::: "memory"); break;
+    case 40: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
+    case 41: asm volatile("s_waitcnt vmcnt(41)" ::: "memory"); break;
+    case 42: asm volatile("s_waitcnt vmcnt(42)" ::: "memory"); break;
+    case 43: asm volatile("s_waitcnt vmcnt(43)" ::: "memory"); break;
+    case 44: asm volatile("s_waitcnt vmcnt(44)" ::: "memory"); break;
+    case 45: asm volatile("s_waitcnt vmcnt(45)" ::: "memory"); break;
+    case 46: asm volatile("s_waitcnt vmcnt(46)" ::: "memory"); break;
+    case 47: asm volatile("s_waitcnt vmcnt(47)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
+typedef __attribute__((address_space(1))) void* GlobalVoid;
+typedef __attribute__((address_space(3))) void* LdsVoid;
+
+// GL (default): the weight chunks and the layer-1 inputs go global -> LDS by LDS-DMA
+// (global_load_lds), a 3-slot weight ring with two chunks in flight; no staging registers
+// and no ds_write pass.  !GL: round 2's pipeline (weights through 16 staging registers and
+// ds_write_b128 into a 2-slot ring, inputs into registers), kept for A/B (FV3_B3_STAGE=reg).
+template <int HU, bool GL>
 __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2))) void dense_b3_kernel(B3Args pa)
 {
     (void)pa;
@@ -191,14 +257,16 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
     constexpr int KS = HU / 2;       // 32-deep k-steps over HP units
     constexpr int CB = 2048 * HU;    // chunk: HU A fragments x {hi, lo} x 64 lanes x 16 B
     constexpr int NST = CB / (16 * kB3Threads);  // 16-B loads per thread per chunk
+    constexpr int NSL = b3_slots(GL);            // weight ring slots
     static_assert(HU % 4 == 0 && NST >= 1, "unit tiles per layer must be a multiple of 4");
     extern __shared__ __attribute__((aligned(16))) b3f4 lds3[];
     char* ring = reinterpret_cast<char*>(lds3);
-    float* s_mean = reinterpret_cast<float*>(ring + 2 * CB);
+    float* s_in = reinterpret_cast<float*>(ring + NSL * CB);  // GL: [2][8 waves][8 levels][64 lanes]
+    float* s_mean = reinterpret_cast<float*>(ring + NSL * CB + b3_in_bytes(GL));
     float* s_rs = s_mean + p.kp1;
     float* s_bias = s_rs + p.kp1;             // [nh][HP]
     float* s_oc = s_bias + (1 + p.nhx) * HP;  // [6][kop]: bias, sigma, mean, lo, hi, mask
-    B3Grp* s_grp = reinterpret_cast<B3Grp*>(ring + 2 * CB + 4 * ((p.nconst + 7) & ~7));  // [4 n1]
+    B3Grp* s_grp = reinterpret_cast<B3Grp*>(reinterpret_cast<char*>(s_mean) + 4 * ((p.nconst + 7) & ~7));  // [4 n1]
     const int kop = p.kop;
 
     const int tid = threadIdx.x;
@@ -223,9 +291,11 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
     }
     b3_barrier();  // the group table is read by the first tile's input loads below
 
-    // ---- weight stream: LDS ring of 2 chunks, the chunk after next in registers ----
+    // ---- weight stream.  GL: LDS ring of 3 chunks filled by LDS-DMA, two ahead of use.
+    //      !GL: LDS ring of 2 chunks, the chunk after next in registers ----
     const Rsrc3 rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.wstream), 0, p.wbytes, 0x00020000);
-    b3f4 stg[NST];
+    const char* wsrc = reinterpret_cast<const char*>(p.wstream);
+    b3f4 stg[GL ? 1 : NST];
     auto load_stage = [&](int j) {
 #pragma unroll
         for (int q = 0; q < NST; ++q)
@@ -237,11 +307,24 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
         for (int q = 0; q < NST; ++q)
             *reinterpret_cast<b3f4*>(ring + slot * CB + q * 16 * kB3Threads + tid * 16) = stg[q];
     };
+    // chunk j of the stream into ring slot sl: NST LDS-DMA loads per thread; the LDS side
+    // of each is wave-uniform base + 16 B x lane, the chunk image being lane-linear
+    auto glds_w = [&](int j, int sl) {
+#pragma unroll
+        for (int q = 0; q < NST; ++q)
+            __builtin_amdgcn_global_load_lds((GlobalVoid)(wsrc + (size_t)j * CB + q * 16 * kB3Threads + tid * 16),
+                                             (LdsVoid)(ring + sl * CB + q * 16 * kB3Threads + wave * 1024), 16, 0, 0);
+    };
     int slot = 0;                         // ring slot of the chunk computed next
     int jn2 = p.nch > 2 ? 2 : 2 % p.nch;  // stream index of the chunk after next
-    load_stage(0);
-    write_stage(0);
-    load_stage(p.nch > 1 ? 1 : 0);
+    if constexpr (GL) {
+        glds_w(0, 0);
+        glds_w(p.nch > 1 ? 1 : 0, 1);
+    } else {
+        load_stage(0);
+        write_stage(0);
+        load_stage(p.nch > 1 ? 1 : 0);
+    }
 
     b3f4 acc[HU];
     auto zero_acc = [&]() {
@@ -266,21 +349,29 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
 #endif
     };
     auto stage_next = [&]() {
+        if constexpr (GL) {
+            glds_w(jn2, slot == 0 ? 2 : slot - 1);  // chunk +2 into the slot chunk -1 released
+        } else {
 #ifndef FV3_B3_EXP_NOSTAGE  // experiment only (results invalid): no weight streaming
-        write_stage(slot ^ 1);  // chunk +1 (its slot held chunk -1, released by the last barrier)
-        load_stage(jn2);        // chunk +2
+            write_stage(slot ^ 1);  // chunk +1 (its slot held chunk -1, released by the last barrier)
+            load_stage(jn2);        // chunk +2
 #endif
+        }
     };
-    auto advance = [&]() {
+    // end of a chunk.  GL: this wave's LDS-DMA of chunk +1 (issued one chunk ago) must have
+    // landed before the barrier that publishes it; `younger` = vector-memory operations this
+    // chunk issued after its own weight DMA (they, and that DMA, may stay in flight)
+    auto advance = [&](int younger) {
+        if constexpr (GL) vm_wait_le(NST + younger);
         b3_barrier();
-        slot ^= 1;
+        slot = GL ? (slot == NSL - 1 ? 0 : slot + 1) : (slot ^ 1);
         jn2 = jn2 + 1 == p.nch ? 0 : jn2 + 1;
     };
     // layer chunk: unit tile t accumulates A_t x B (one 32-deep k-step); tiles in pairs,
     // their MFMAs interleaved, fragments read one pair ahead
     auto step_layer = [&](const bf16x8& bh, const bf16x8& bl, auto&& after_stage) {
         stage_next();
-        after_stage();  // loads issued after this chunk's weight loads (vmcnt is in order)
+        const int younger = after_stage();  // loads issued after this chunk's weight loads (vmcnt is in order)
         bf16x8 fa[4][2];
         frag(slot, 0, fa[0]);
         frag(slot, 1, fa[1]);
@@ -292,7 +383,7 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
             }
             mma3x2(fa[t0 % 4][0], fa[t0 % 4][1], bh, bl, acc[t0], fa[t1 % 4][0], fa[t1 % 4][1], bh, bl, acc[t1]);
         });
-        advance();
+        advance(younger);
     };
 
     // ---- layer-1 inputs: B fragments straight from the [level][column] arrays ----
@@ -327,6 +418,26 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
             const float x = ptr[j < nv ? j * ld : 0];
 #endif
 #endif
+            raw[j] = j < nv ? x : 0.0f;
+        }
+    };
+    // GL: chunk c's inputs by LDS-DMA into this wave's rows of buffer `buf`: level j of
+    // every lane is one 4-byte LDS-DMA (lane-linear row [buf][wave][j][lane])
+    auto glds_in = [&](int buf, int c) {
+        const B3Grp& g = s_grp[4 * c + hq];
+        const int ld = g.ld;
+        const int nv = lvalid ? g.nv : 0;
+        const float* ptr = g.ptr + (int64_t)lblk * g.bs + lii;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            __builtin_amdgcn_global_load_lds((GlobalVoid)(ptr + (j < nv ? j * ld : 0)),
+                                             (LdsVoid)(s_in + ((buf * 8 + wave) * 8 + j) * 64), 4, 0, 0);
+    };
+    auto read_in = [&](int buf, int c, float (&raw)[8]) {  // GL: chunk c's values (landed, see advance)
+        const int nv = lvalid ? s_grp[4 * c + hq].nv : 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float x = s_in[((buf * 8 + wave) * 8 + j) * 64 + lane];
             raw[j] = j < nv ? x : 0.0f;
         }
     };
@@ -395,7 +506,7 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
     // after = before + to) are loaded one chunk ahead of their use.
     unsigned oblk = 0, oii = 0;
     bool ovalid = false;
-    auto res_load = [&](int T, float (&r)[4]) {
+    auto res_load = [&](int T, float (&r)[4]) -> int {  // returns the loads issued (0 or 4)
         const int e = p.otile[T];
         const int v = e & 0xff, z0 = (e >> 8) & 0xffff, nrow = e >> 24;
         if (v < kMaxVars && p.res_ptr[v]) {  // uniform
@@ -409,15 +520,16 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
                 const unsigned off = (ovalid & (row < nrow)) ? (rb + (unsigned)(z0 + row) * rld) * 4u : 0x80000000u;
                 r[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr_, (int)off, 0, 0));
             }
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) r[q] = 0.0f;
+            return 4;
         }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) r[q] = 0.0f;
+        return 0;
     };
-    auto out_tile = [&](const b3f4& a, int T, const float (&r)[4]) {
+    auto out_tile = [&](const b3f4& a, int T, const float (&r)[4]) -> int {  // returns the stores issued
         const int e = p.otile[T];
         const int v = e & 0xff, z0 = (e >> 8) & 0xffff, nrow = e >> 24;
-        if (v >= kMaxVars) return;  // padding tile (uniform)
+        if (v >= kMaxVars) return 0;  // padding tile (uniform)
         int R0 = 16 * T + 4 * hq;
         asm volatile("" : "+v"(R0));  // keep the constant reads next to their use
         const b3f4 bo = *reinterpret_cast<const b3f4*>(s_oc + R0);
@@ -446,15 +558,22 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
 #endif
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, (int)off, 0, 0);
         }
+        return 4;
     };
 
     float rawA[8], rawB[8];
     int64_t tile = blockIdx.x;
     set_load_tile(tile);
     if (tile < p.ntiles) {
-        load_in(rawA, 0);
-        if (p.n1 > 1) load_in(rawB, 1);
+        if constexpr (GL) {
+            glds_in(0, 0);
+            if (p.n1 > 1) glds_in(1, 1);
+        } else {
+            load_in(rawA, 0);
+            if (p.n1 > 1) load_in(rawB, 1);
+        }
     }
+    if constexpr (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     b3_barrier();  // constants and chunk 0 visible
 
     for (; tile < p.ntiles; tile += gridDim.x) {
@@ -463,22 +582,40 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
         ovalid = lvalid;
         // ---- layer 1 over the padded input features ----
         zero_acc();
+        if constexpr (GL) {
+            // chunk c: its inputs (buffer c & 1, landed by the wait at the end of chunk c - 1),
+            // then the weight DMA of chunk c + 2 and the input DMA of chunk c + 2 into the
+            // buffer just read
+            for (int c = 0; c < p.n1; ++c) {
+                bf16x8 xh, xl;
+                read_in(c & 1, c, rawA);
+                stage_in(rawA, c, xh, xl);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the reads above before the DMA refills the buffer
+                step_layer(xh, xl, [&]() {
+                    if (c + 2 < p.n1) {
+                        glds_in(c & 1, c + 2);
+                        return 8;
+                    }
+                    return 0;
+                });
+            }
+        } else
         for (int c = 0; c < p.n1; c += 2) {
             bf16x8 xh, xl;
             stage_in(rawA, c, xh, xl);
 #ifdef FV3_B3_EXP_INLATE
-            step_layer(xh, xl, [&]() { if (c + 2 < p.n1) load_in(rawA, c + 2); });
+            step_layer(xh, xl, [&]() { if (c + 2 < p.n1) load_in(rawA, c + 2); return 0; });
 #else
             if (c + 2 < p.n1) load_in(rawA, c + 2);
-            step_layer(xh, xl, [] {});
+            step_layer(xh, xl, [] { return 0; });
 #endif
             if (c + 1 < p.n1) {
                 stage_in(rawB, c + 1, xh, xl);
 #ifdef FV3_B3_EXP_INLATE
-                step_layer(xh, xl, [&]() { if (c + 3 < p.n1) load_in(rawB, c + 3); });
+                step_layer(xh, xl, [&]() { if (c + 3 < p.n1) load_in(rawB, c + 3); return 0; });
 #else
                 if (c + 3 < p.n1) load_in(rawB, c + 3);
-                step_layer(xh, xl, [] {});
+                step_layer(xh, xl, [] { return 0; });
 #endif
             }
         }
@@ -488,7 +625,7 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
             zero_acc();
             sfor<KS>([&](auto cc) {
                 constexpr int c = decltype(cc)::value;
-                step_layer(Bh[c], Bl[c], [] {});
+                step_layer(Bh[c], Bl[c], [] { return 0; });
             });
             hidden_epi(l + 1);
         }
@@ -496,11 +633,49 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
         const int64_t nt = tile + gridDim.x;
         if (nt < p.ntiles) {
             set_load_tile(nt);
-            load_in(rawA, 0);
-            if (p.n1 > 1) load_in(rawB, 1);
+            if constexpr (!GL) {
+                load_in(rawA, 0);
+                if (p.n1 > 1) load_in(rawB, 1);
+            }
         }
         b3f4 accP[2];
         float resN[2][4], resP[2][4];
+        if constexpr (GL) {
+            // chunk oc: the weight DMA of chunk +2, this chunk's residual loads (consumed
+            // one chunk later), the MFMAs, then the previous chunk's epilogue (8 stores).
+            // The next tile's input DMA (16 per thread) goes out with the last chunk.
+            for (int oc = 0; oc < p.n_oc; ++oc) {
+                acc[0] = acc[1] = b3f4{0.0f, 0.0f, 0.0f, 0.0f};
+                stage_next();
+                int younger = res_load(2 * oc, resN[0]);
+                younger += res_load(2 * oc + 1, resN[1]);
+                if (oc + 1 == p.n_oc && nt < p.ntiles) {
+                    glds_in(0, 0);
+                    younger += 8;
+                    if (p.n1 > 1) {
+                        glds_in(1, 1);
+                        younger += 8;
+                    }
+                }
+                step_out();
+                if (oc > 0) {
+                    younger += out_tile(accP[0], 2 * oc - 2, resP[0]);
+                    younger += out_tile(accP[1], 2 * oc - 1, resP[1]);
+                }
+                advance(younger);
+                accP[0] = acc[0];
+                accP[1] = acc[1];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    resP[0][q] = resN[0][q];
+                    resP[1][q] = resN[1][q];
+                }
+            }
+            out_tile(accP[0], 2 * p.n_oc - 2, resP[0]);
+            out_tile(accP[1], 2 * p.n_oc - 1, resP[1]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's inputs landed
+            continue;
+        }
         for (int oc = 0; oc < p.n_oc; ++oc) {
 #ifndef FV3_B3_EXP_RESLATE
             res_load(2 * oc, resN[0]);  // lands while this chunk and the next run their MFMAs
@@ -517,7 +692,7 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
                 out_tile(accP[0], 2 * oc - 2, resP[0]);
                 out_tile(accP[1], 2 * oc - 1, resP[1]);
             }
-            advance();
+            advance(0);
             accP[0] = acc[0];
             accP[1] = acc[1];
 #pragma unroll
@@ -785,10 +960,17 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
                              "dense_forward_ex: residual input %d spans too many elements for bf16x3", r);
     }
 
-    const void* kfn = b.hu == 4 ? (const void*)dense_b3_kernel<4>
-                      : b.hu == 8 ? (const void*)dense_b3_kernel<8>
-                                  : (const void*)dense_b3_kernel<16>;
-    const size_t lds = (size_t)2 * 2048 * b.hu + (size_t)4 * ((b.nconst + 7) & ~7) + sizeof(B3Grp) * 4 * b.n1;
+    // FV3_B3_STAGE=glds / reg: the LDS-DMA or the register-staged pipeline (A/B)
+    const char* stg_env = getenv("FV3_B3_STAGE");
+    const bool gl = stg_env ? stg_env[0] == 'g' : kB3GldsDefault;
+    const void* kfn = gl ? (b.hu == 4 ? (const void*)dense_b3_kernel<4, true>
+                            : b.hu == 8 ? (const void*)dense_b3_kernel<8, true>
+                                        : (const void*)dense_b3_kernel<16, true>)
+                         : (b.hu == 4 ? (const void*)dense_b3_kernel<4, false>
+                            : b.hu == 8 ? (const void*)dense_b3_kernel<8, false>
+                                        : (const void*)dense_b3_kernel<16, false>);
+    const size_t lds = (size_t)b3_slots(gl) * 2048 * b.hu + (size_t)b3_in_bytes(gl) +
+                       (size_t)4 * ((b.nconst + 7) & ~7) + sizeof(B3Grp) * 4 * b.n1;
     FV3_REQUIRE(lds <= 160 * 1024, "dense_forward_ex: model needs %zu bytes of LDS", lds);
     static std::mutex mu;
     static int n_cu = 0;
