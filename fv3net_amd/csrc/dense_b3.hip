@@ -55,7 +55,11 @@ constexpr int kB3Groups = 128;   // 8-feature input groups (<= 1024 padded input
 constexpr int kB3Cols = 128;     // columns per block tile: 8 waves x 16
 constexpr int kB3OutTiles = 32;  // 16-row output tiles (<= 512 padded output rows)
 constexpr int kB3Threads = 512;
-constexpr bool kB3GldsDefault = false;  // until the LDS-DMA pipeline is measured on the box
+// the LDS-DMA pipeline by default: emulator C384 2.41 -> 2.29-2.34 ms, 2x256 C384 827 -> 814-820 us
+// against the register-staged one on the same box (round 3; a variant holding the output
+// chunks' accumulators / residuals in two register sets instead of copying them measured
+// the same, within the run-to-run spread)
+constexpr bool kB3GldsDefault = true;
 constexpr int b3_slots(bool gl) { return gl ? 3 : 2; }
 constexpr int b3_in_bytes(bool gl) { return gl ? 2 * 8 * 8 * 64 * 4 : 0; }
 
