@@ -375,7 +375,7 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
     // their MFMAs interleaved, fragments read one pair ahead
     auto step_layer = [&](const bf16x8& bh, const bf16x8& bl, auto&& after_stage) {
         stage_next();
-        const int younger = after_stage();  // loads issued after this chunk's weight loads (vmcnt is in order)
+        const int younger = after_stage();  // GL: ops issued after this chunk's weight DMA (vmcnt is in order)
         bf16x8 fa[4][2];
         frag(slot, 0, fa[0]);
         frag(slot, 1, fa[1]);
@@ -607,20 +607,12 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
         for (int c = 0; c < p.n1; c += 2) {
             bf16x8 xh, xl;
             stage_in(rawA, c, xh, xl);
-#ifdef FV3_B3_EXP_INLATE
-            step_layer(xh, xl, [&]() { if (c + 2 < p.n1) load_in(rawA, c + 2); return 0; });
-#else
             if (c + 2 < p.n1) load_in(rawA, c + 2);
             step_layer(xh, xl, [] { return 0; });
-#endif
             if (c + 1 < p.n1) {
                 stage_in(rawB, c + 1, xh, xl);
-#ifdef FV3_B3_EXP_INLATE
-                step_layer(xh, xl, [&]() { if (c + 3 < p.n1) load_in(rawB, c + 3); return 0; });
-#else
                 if (c + 3 < p.n1) load_in(rawB, c + 3);
                 step_layer(xh, xl, [] { return 0; });
-#endif
             }
         }
         hidden_epi(0);
@@ -681,16 +673,10 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
             continue;
         }
         for (int oc = 0; oc < p.n_oc; ++oc) {
-#ifndef FV3_B3_EXP_RESLATE
             res_load(2 * oc, resN[0]);  // lands while this chunk and the next run their MFMAs
             res_load(2 * oc + 1, resN[1]);
-#endif
             acc[0] = acc[1] = b3f4{0.0f, 0.0f, 0.0f, 0.0f};
             stage_next();
-#ifdef FV3_B3_EXP_RESLATE  // after the weight loads: the next chunk's staging does not wait for them
-            res_load(2 * oc, resN[0]);
-            res_load(2 * oc + 1, resN[1]);
-#endif
             step_out();
             if (oc > 0) {  // finish the previous chunk while these MFMAs run
                 out_tile(accP[0], 2 * oc - 2, resP[0]);
