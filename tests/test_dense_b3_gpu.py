@@ -32,6 +32,14 @@ def _check(gpu_out, ref64, rtol=RTOL_B3):
         assert_per_level(g, r, rtol, f"output {o}")
 
 
+@pytest.fixture(autouse=True, params=["glds", "reg"])
+def b3_stage(request, monkeypatch):
+    """Every test on both staging pipelines of the kernel (FV3_B3_STAGE): LDS-DMA (the
+    default) and register staging."""
+    monkeypatch.setenv("FV3_B3_STAGE", request.param)
+    return request.param
+
+
 def _model(cfg_kwargs, seed=1, bias_scale=0.1, samples=None):
     from fv3net_amd.dense import DenseColumnModel, DenseModelConfig
 
