@@ -130,11 +130,7 @@ __device__ __forceinline__ void sfor(F&& f)
 // this wave's LDS writes done, then the workgroup barrier; global loads in flight (the
 // next weight chunk, the next inputs) are NOT drained (a __syncthreads() fence would
 // wait vmcnt(0) on gfx9, where loads and stores share the counter)
-#ifdef FV3_B3_EXP_NOBAR  // experiment only (results invalid): no chunk barriers
-__device__ __forceinline__ void b3_barrier() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-#else
 __device__ __forceinline__ void b3_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-#endif
 
 __device__ __forceinline__ float b3_log(float x, float eps) { return x != x ? x : logf(x > eps ? x : eps); }
 
