@@ -948,15 +948,20 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
 
     // FV3_B3_STAGE=glds / reg: the LDS-DMA or the register-staged pipeline (A/B)
     const char* stg_env = getenv("FV3_B3_STAGE");
-    const bool gl = stg_env ? stg_env[0] == 'g' : kB3GldsDefault;
+    auto lds_of = [&](bool g) {
+        return (size_t)b3_slots(g) * 2048 * b.hu + (size_t)b3_in_bytes(g) + (size_t)4 * ((b.nconst + 7) & ~7) +
+               sizeof(B3Grp) * 4 * b.n1;
+    };
+    // the LDS-DMA pipeline needs a third ring slot and the input rows: a model that only
+    // fits the register-staged pipeline's LDS runs on that one
+    const bool gl = (stg_env ? stg_env[0] == 'g' : kB3GldsDefault) && lds_of(true) <= 160 * 1024;
     const void* kfn = gl ? (b.hu == 4 ? (const void*)dense_b3_kernel<4, true>
                             : b.hu == 8 ? (const void*)dense_b3_kernel<8, true>
                                         : (const void*)dense_b3_kernel<16, true>)
                          : (b.hu == 4 ? (const void*)dense_b3_kernel<4, false>
                             : b.hu == 8 ? (const void*)dense_b3_kernel<8, false>
                                         : (const void*)dense_b3_kernel<16, false>);
-    const size_t lds = (size_t)b3_slots(gl) * 2048 * b.hu + (size_t)b3_in_bytes(gl) +
-                       (size_t)4 * ((b.nconst + 7) & ~7) + sizeof(B3Grp) * 4 * b.n1;
+    const size_t lds = lds_of(gl);
     FV3_REQUIRE(lds <= 160 * 1024, "dense_forward_ex: model needs %zu bytes of LDS", lds);
     static std::mutex mu;
     static int n_cu = 0;

@@ -99,6 +99,24 @@ def test_many_outputs_two_passes(gpu):
     _check(got, dense_predict(xs, m.oracle_params(), np.float64))
 
 
+def test_deep_wide_model_falls_back_to_register_staging(gpu):
+    """A model whose constants leave no room for the LDS-DMA pipeline's third ring slot
+    and input rows (16 x 64 inputs = the 1,024-feature maximum, 19 hidden layers of 256:
+    ~163 KB of LDS against 160) runs on the register-staged pipeline instead of failing.
+    Bound: BASELINE config #5's 1e-3 (the split's ~1e-5 per layer compounds over 20
+    layers: 2.2e-4 measured)."""
+    import torch
+
+    rng = np.random.default_rng(12)
+    n = 300
+    xs = [rng.normal(i, 1 + i, (n, 64)).astype(np.float32) for i in range(16)]
+    m = _model(dict(input_variables=[f"x{i}" for i in range(16)], output_variables=["a", "b"],
+                    in_nz=[64] * 16, out_nz=[79, 79], width=256, depth=20), samples=xs, bias_scale=0.02)
+    outs = m.forward([torch.from_numpy(x.T.copy()).cuda() for x in xs])
+    got = [o.cpu().numpy().reshape(o.shape[0], n).T for o in outs]
+    _check(got, dense_predict(xs, m.oracle_params(), np.float64), rtol=1e-3)
+
+
 def test_clip_limits_mask_and_scalar_input(gpu):
     import torch
 
