@@ -60,6 +60,12 @@ constexpr int kB3Threads = 512;
 // chunks' accumulators / residuals in two register sets instead of copying them measured
 // the same, within the run-to-run spread)
 constexpr bool kB3GldsDefault = true;
+// fragment ring: the A fragments of the next (kFR - 2) / 2 tile pairs are in flight while a
+// pair's MFMAs issue
+#ifndef FV3_B3_FR
+#define FV3_B3_FR 4
+#endif
+constexpr int kFR = FV3_B3_FR;
 constexpr int b3_slots(bool gl) { return gl ? 3 : 2; }
 constexpr int b3_in_bytes(bool gl) { return gl ? 2 * 8 * 8 * 64 * 4 : 0; }
 
@@ -372,16 +378,16 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
     auto step_layer = [&](const bf16x8& bh, const bf16x8& bl, auto&& after_stage) {
         stage_next();
         const int younger = after_stage();  // GL: ops issued after this chunk's weight DMA (vmcnt is in order)
-        bf16x8 fa[4][2];
-        frag(slot, 0, fa[0]);
-        frag(slot, 1, fa[1]);
+        bf16x8 fa[kFR][2];
+        sfor<kFR - 2>([&](auto ic) { frag(slot, decltype(ic)::value, fa[decltype(ic)::value]); });
         sfor<HU / 2>([&](auto pc) {
             constexpr int t0 = 2 * decltype(pc)::value, t1 = t0 + 1;
-            if constexpr (t0 + 2 < HU) {
-                frag(slot, t0 + 2, fa[(t0 + 2) % 4]);
-                frag(slot, t1 + 2, fa[(t1 + 2) % 4]);
+            if constexpr (t0 + kFR - 2 < HU) {
+                frag(slot, t0 + kFR - 2, fa[(t0 + kFR - 2) % kFR]);
+                frag(slot, t1 + kFR - 2, fa[(t1 + kFR - 2) % kFR]);
             }
-            mma3x2(fa[t0 % 4][0], fa[t0 % 4][1], bh, bl, acc[t0], fa[t1 % 4][0], fa[t1 % 4][1], bh, bl, acc[t1]);
+            mma3x2(fa[t0 % kFR][0], fa[t0 % kFR][1], bh, bl, acc[t0], fa[t1 % kFR][0], fa[t1 % kFR][1], bh, bl,
+                   acc[t1]);
         });
         advance(younger);
     };
@@ -483,17 +489,16 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
     };
     // output chunk: fragment i = 2q + ts accumulates tile ts of the chunk over k-step q
     auto step_out = [&]() {  // fragments 2q, 2q+1: k-step q of tiles 0 and 1, interleaved
-        bf16x8 fa[4][2];
-        frag(slot, 0, fa[0]);
-        frag(slot, 1, fa[1]);
+        bf16x8 fa[kFR][2];
+        sfor<kFR - 2>([&](auto ic) { frag(slot, decltype(ic)::value, fa[decltype(ic)::value]); });
         sfor<HU / 2>([&](auto qc) {
             constexpr int q = decltype(qc)::value, i0 = 2 * q, i1 = i0 + 1;
-            if constexpr (i0 + 2 < HU) {
-                frag(slot, i0 + 2, fa[(i0 + 2) % 4]);
-                frag(slot, i1 + 2, fa[(i1 + 2) % 4]);
+            if constexpr (i0 + kFR - 2 < HU) {
+                frag(slot, i0 + kFR - 2, fa[(i0 + kFR - 2) % kFR]);
+                frag(slot, i1 + kFR - 2, fa[(i1 + kFR - 2) % kFR]);
             }
-            mma3x2(fa[i0 % 4][0], fa[i0 % 4][1], Bh[q], Bl[q], acc[0], fa[i1 % 4][0], fa[i1 % 4][1], Bh[q], Bl[q],
-                   acc[1]);
+            mma3x2(fa[i0 % kFR][0], fa[i0 % kFR][1], Bh[q], Bl[q], acc[0], fa[i1 % kFR][0], fa[i1 % kFR][1], Bh[q],
+                   Bl[q], acc[1]);
         });
     };
 
