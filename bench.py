@@ -262,6 +262,17 @@ def scaling_legs(dev, dist, rank, world, settle_ms=150.0):
         "kernels": {"dense": with_counters("predict_mappm_c384", {}),
                     "mappm_pair": with_counters("predict_mappm_c384_mappm", {})}}
     del wl
+    # the same step with the predict on the bf16x6 kernel (f32-level error, 1e-5 per level)
+    wl = W.make_predict_mappm_workload(384, rank, world, seed=21, device=dev, precision="bf16x6")
+    wall, t = timed_steps(wl.step, steps, 2, dist, settle_ms=settle_ms)
+    wall = max_over_ranks(wall, dist, dev)
+    out["predict_mappm_c384_sharded_bf16x6"] = {
+        "columns_per_s": wl.ncol_global / (wall / steps), "ms_per_step": wall / steps * 1e3,
+        "scaling": "strong", "columns_global": wl.ncol_global, "columns_per_rank_max": wl.ncol,
+        "gpu_ms_per_step_rank0": t * 1e3, "precision": "bf16x6",
+        "kernels": {"dense": with_counters("predict_mappm_c384_bf16x6", {}),
+                    "mappm_pair": with_counters("predict_mappm_c384_mappm", {})}}
+    del wl
     torch.cuda.empty_cache()
     return out
 
@@ -543,6 +554,18 @@ def extra_measurements(dev, settle_ms=150.0):
         "columns_per_s": wl.ncol / t, "ms_per_step": t * 1e3, "tflops_f32_equiv": tf,
         "frac_bf16_mfma_peak": 3 * tf / W.BF16_MFMA_PEAK_TFLOPS}, wl.ncol * wl.bytes_per_column)
     del wl
+    # config #2's model on the bf16x6 kernel (three bf16 parts per operand, six MFMAs per
+    # f32 product: held to the exact-f32 kernel's 1e-5 per-level bound), C48 and C384
+    for res, n in ((48, 200), (384, 10)):
+        wl = W.make_dense_workload(res, seed=3, device=dev, precision="bf16x6")
+        wall, t = timed_steps(wl.step, n, 3, settle_ms=settle_ms)
+        tf = wl.ncol * wl.flops_per_column / t / 1e12
+        leg = f"dense_c{res}_bf16x6"
+        out[leg] = with_counters(leg, {
+            "columns_per_s": wl.ncol / t, "ms_per_step": t * 1e3, "tflops_f32_equiv": tf,
+            "frac_bf16_mfma_peak": 6 * tf / W.BF16_MFMA_PEAK_TFLOPS,
+            "tflops_f32_equiv_over_f32_peak": tf / W.FP32_MFMA_PEAK_TFLOPS}, wl.ncol * wl.bytes_per_column)
+        del wl
     # config #3: fused C384 -> C48 pressure-level coarsen (1 and 4 fields), fine columns/s
     for nf in (1, 4):
         wl = W.make_coarsen_workload(384, 8, nf, seed=7, device=dev)

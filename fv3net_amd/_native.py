@@ -78,6 +78,7 @@ ABI_VERSION = 4
 # fv3_dense_forward_ex precisions
 DENSE_F32 = 0
 DENSE_BF16X3 = 1
+DENSE_BF16X6 = 2
 
 # fv3_ml_epilogue_ex flags, fv3_tendency_columns modes
 EPI_HAS_DQ1 = 1

@@ -71,6 +71,7 @@ constexpr int b3_in_bytes(bool gl) { return gl ? 2 * 8 * 8 * 64 * 4 : 0; }
 
 struct B3Pack {
     void* dbuf = nullptr;
+    int ns = 2;  // bf16 parts per weight (2: bf16x3, 3: bf16x6)
     int hu = 0, hp = 0, kp1 = 0, n1 = 0, nhx = 0, n_oc = 0, kop = 0, nch = 0;
     int nconst = 0, wbytes = 0, any_log = 0;
     std::vector<int> gmeta;  // per 8-feature group: var | zstart << 4 | nvalid << 24
@@ -140,49 +141,53 @@ __device__ __forceinline__ void b3_barrier() { asm volatile("s_waitcnt lgkmcnt(0
 
 __device__ __forceinline__ float b3_log(float x, float eps) { return x != x ? x : logf(x > eps ? x : eps); }
 
-// y -> bf16 hi = rne(y), lo = rne(y - hi)  (y - hi is exact in f32)
-__device__ __forceinline__ void split8(const float (&y)[8], bf16x8& hi, bf16x8& lo)
+// y -> NS bf16 parts: part 0 = rne(y), part s = rne(y - parts 0..s-1) (every residual is
+// exact in f32).  NS = 2: hi + lo (~16 mantissa bits); NS = 3: hi + mid + lo (~24 bits).
+template <int NS>
+__device__ __forceinline__ void splitN(const float (&y)[8], bf16x8 (&o)[NS])
 {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const __bf16 h = (__bf16)y[j];
-        hi[j] = h;
-        lo[j] = (__bf16)(y[j] - (float)h);
+        float r = y[j];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const __bf16 h = (__bf16)r;
+            o[s][j] = h;
+            if (s + 1 < NS) r = r - (float)h;
+        }
     }
 }
 
-__device__ __forceinline__ b3f4 mma3(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl, b3f4 c)
+// the split products of one f32 product a*b, in issue order (part of a, part of b):
+// NS = 2 (bf16x3): hi*hi, lo*hi, hi*lo; NS = 3 (bf16x6): every pair of order <= 2 in the
+// parts' 2^-8 steps (hi*hi; mid*hi, hi*mid; mid*mid, lo*hi, hi*lo), ~2^-24 rel per product
+template <int NS>
+struct SplitTerms {
+    static constexpr int n = NS == 2 ? 3 : 6;
+    static constexpr int a[6] = {0, 1, 0, 1, 2, 0};
+    static constexpr int b[6] = {0, 0, 1, 1, 0, 2};
+};
+
+// two independent accumulations interleaved (c0 <- a0 x b0, c1 <- a1 x b1, each in the
+// SplitTerms order): no MFMA waits on the one just issued
+template <int NS>
+__device__ __forceinline__ void mma_x2(const bf16x8 (&a0)[NS], const bf16x8 (&b0)[NS], b3f4& c0,
+                                       const bf16x8 (&a1)[NS], const bf16x8 (&b1)[NS], b3f4& c1)
 {
+    using T = SplitTerms<NS>;
+#pragma unroll
+    for (int t = 0; t < T::n; ++t) {
 #ifdef FV3_B3_EXP_NOMFMA  // experiment only (results invalid): everything but the MFMAs
-    c[0] += (float)ah[0] + (float)al[1] + (float)bh[2] + (float)bl[3];
+        c0[0] += (float)a0[T::a[t]][t] + (float)b0[T::b[t]][t];
+        c1[0] += (float)a1[T::a[t]][t] + (float)b1[T::b[t]][t];
 #else
-    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[T::a[t]], b0[T::b[t]], c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[T::a[t]], b1[T::b[t]], c1, 0, 0, 0);
 #endif
-    return c;
+    }
 }
 
 // value of lane quarter q from 4 wave-uniform candidates
-// two independent accumulations interleaved (c0 <- a0 x b0, c1 <- a1 x b1, each in the
-// hi*hi, lo*hi, hi*lo order of mma3): no MFMA waits on the one just issued
-__device__ __forceinline__ void mma3x2(const bf16x8& ah0, const bf16x8& al0, const bf16x8& bh0, const bf16x8& bl0,
-                                       b3f4& c0, const bf16x8& ah1, const bf16x8& al1, const bf16x8& bh1,
-                                       const bf16x8& bl1, b3f4& c1)
-{
-#ifdef FV3_B3_EXP_NOMFMA
-    c0 = mma3(ah0, al0, bh0, bl0, c0);
-    c1 = mma3(ah1, al1, bh1, bl1, c1);
-#else
-    c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah0, bh0, c0, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah1, bh1, c1, 0, 0, 0);
-    c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al0, bh0, c0, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al1, bh1, c1, 0, 0, 0);
-    c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah0, bl0, c0, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah1, bl1, c1, 0, 0, 0);
-#endif
-}
-
 template <typename T>
 __device__ __forceinline__ T sel4(int q, T a0, T a1, T a2, T a3)
 {
@@ -254,15 +259,18 @@ typedef __attribute__((address_space(3))) void* LdsVoid;
 // (global_load_lds), a 3-slot weight ring with two chunks in flight; no staging registers
 // and no ds_write pass.  !GL: round 2's pipeline (weights through 16 staging registers and
 // ds_write_b128 into a 2-slot ring, inputs into registers), kept for A/B (FV3_B3_STAGE=reg).
-template <int HU, bool GL>
+// NS: bf16 parts per f32 operand (2: bf16x3, 3: bf16x6, see SplitTerms)
+template <int HU, bool GL, int NS>
 __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2))) void dense_b3_kernel(B3Args pa)
 {
     (void)pa;
     KB3& p = *(KB3*)(__builtin_amdgcn_kernarg_segment_ptr());
     constexpr int HP = 16 * HU;      // padded units
     constexpr int KS = HU / 2;       // 32-deep k-steps over HP units
-    constexpr int CB = 2048 * HU;    // chunk: HU A fragments x {hi, lo} x 64 lanes x 16 B
-    constexpr int NST = CB / (16 * kB3Threads);  // 16-B loads per thread per chunk
+    constexpr int CB = 1024 * NS * HU;  // chunk: HU A fragments x NS parts x 64 lanes x 16 B
+    // 16-B loads per thread per chunk; a chunk that is not a whole number of block-wide
+    // loads (HU = 4 at NS = 3: 1.5) has its last load on the first waves only (wave-uniform)
+    constexpr int NST = (CB + 16 * kB3Threads - 1) / (16 * kB3Threads);
     constexpr int NSL = b3_slots(GL);            // weight ring slots
     static_assert(HU % 4 == 0 && NST >= 1, "unit tiles per layer must be a multiple of 4");
     extern __shared__ __attribute__((aligned(16))) b3f4 lds3[];
@@ -300,26 +308,35 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
     // ---- weight stream.  GL: LDS ring of 3 chunks filled by LDS-DMA, two ahead of use.
     //      !GL: LDS ring of 2 chunks, the chunk after next in registers ----
     const Rsrc3 rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.wstream), 0, p.wbytes, 0x00020000);
+    auto part_ok = [&](int q) {  // this wave takes part in load q of a chunk
+        return CB % (16 * kB3Threads) == 0 || q + 1 < NST || q * 16 * kB3Threads + wave * 1024 < CB;
+    };
+    int nst_w = 0;  // loads of one chunk this wave issues (the count its vmcnt waits see)
+#pragma unroll
+    for (int q = 0; q < NST; ++q) nst_w += part_ok(q) ? 1 : 0;
     const char* wsrc = reinterpret_cast<const char*>(p.wstream);
     b3f4 stg[GL ? 1 : NST];
     auto load_stage = [&](int j) {
 #pragma unroll
         for (int q = 0; q < NST; ++q)
-            stg[q] = __builtin_bit_cast(
-                b3f4, __builtin_amdgcn_raw_buffer_load_b128(rw, tid * 16, j * CB + q * 16 * kB3Threads, 0));
+            if (part_ok(q))
+                stg[q] = __builtin_bit_cast(
+                    b3f4, __builtin_amdgcn_raw_buffer_load_b128(rw, tid * 16, j * CB + q * 16 * kB3Threads, 0));
     };
     auto write_stage = [&](int slot) {
 #pragma unroll
         for (int q = 0; q < NST; ++q)
-            *reinterpret_cast<b3f4*>(ring + slot * CB + q * 16 * kB3Threads + tid * 16) = stg[q];
+            if (part_ok(q)) *reinterpret_cast<b3f4*>(ring + slot * CB + q * 16 * kB3Threads + tid * 16) = stg[q];
     };
     // chunk j of the stream into ring slot sl: NST LDS-DMA loads per thread; the LDS side
     // of each is wave-uniform base + 16 B x lane, the chunk image being lane-linear
     auto glds_w = [&](int j, int sl) {
 #pragma unroll
         for (int q = 0; q < NST; ++q)
-            __builtin_amdgcn_global_load_lds((GlobalVoid)(wsrc + (size_t)j * CB + q * 16 * kB3Threads + tid * 16),
-                                             (LdsVoid)(ring + sl * CB + q * 16 * kB3Threads + wave * 1024), 16, 0, 0);
+            if (part_ok(q))
+                __builtin_amdgcn_global_load_lds((GlobalVoid)(wsrc + (size_t)j * CB + q * 16 * kB3Threads + tid * 16),
+                                                 (LdsVoid)(ring + sl * CB + q * 16 * kB3Threads + wave * 1024), 16, 0,
+                                                 0);
     };
     int slot = 0;                         // ring slot of the chunk computed next
     int jn2 = p.nch > 2 ? 2 : 2 % p.nch;  // stream index of the chunk after next
@@ -338,20 +355,20 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
         for (int t = 0; t < HU; ++t) acc[t] = b3f4{0.0f, 0.0f, 0.0f, 0.0f};
     };
 #ifdef FV3_B3_EXP_NOFRAG
-    bf16x8 fconst[2][2];
+    bf16x8 fconst[2][NS];
     for (int i = 0; i < 2; ++i)
-        for (int h = 0; h < 2; ++h) fconst[i][h] = *reinterpret_cast<const bf16x8*>(ring + i * 2048 + h * 1024 + lane * 16);
+        for (int h = 0; h < NS; ++h) fconst[i][h] = *reinterpret_cast<const bf16x8*>(ring + i * 1024 * NS + h * 1024 + lane * 16);
 #endif
-    // A fragment i of the chunk in slot sl: hi at i*2048, lo at i*2048 + 1024
-    auto frag = [&](int sl, int i, bf16x8 (&f)[2]) {
+    // A fragment i of the chunk in slot sl: part s at (NS i + s) * 1024
+    auto frag = [&](int sl, int i, bf16x8 (&f)[NS]) {
 #ifdef FV3_B3_EXP_NOFRAG  // experiment only (results invalid): one fragment, no LDS reads per step
         (void)sl;
-        f[0] = fconst[i & 1][0];
-        f[1] = fconst[i & 1][1];
+#pragma unroll
+        for (int h = 0; h < NS; ++h) f[h] = fconst[i & 1][h];
 #else
-        const char* a = ring + sl * CB + i * 2048 + lane * 16;
-        f[0] = *reinterpret_cast<const bf16x8*>(a);
-        f[1] = *reinterpret_cast<const bf16x8*>(a + 1024);
+        const char* a = ring + sl * CB + i * 1024 * NS + lane * 16;
+#pragma unroll
+        for (int h = 0; h < NS; ++h) f[h] = *reinterpret_cast<const bf16x8*>(a + h * 1024);
 #endif
     };
     auto stage_next = [&]() {
@@ -368,17 +385,17 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
     // landed before the barrier that publishes it; `younger` = vector-memory operations this
     // chunk issued after its own weight DMA (they, and that DMA, may stay in flight)
     auto advance = [&](int younger) {
-        if constexpr (GL) vm_wait_le(NST + younger);
+        if constexpr (GL) vm_wait_le(nst_w + younger);
         b3_barrier();
         slot = GL ? (slot == NSL - 1 ? 0 : slot + 1) : (slot ^ 1);
         jn2 = jn2 + 1 == p.nch ? 0 : jn2 + 1;
     };
     // layer chunk: unit tile t accumulates A_t x B (one 32-deep k-step); tiles in pairs,
     // their MFMAs interleaved, fragments read one pair ahead
-    auto step_layer = [&](const bf16x8& bh, const bf16x8& bl, auto&& after_stage) {
+    auto step_layer = [&](const bf16x8 (&bx)[NS], auto&& after_stage) {
         stage_next();
         const int younger = after_stage();  // GL: ops issued after this chunk's weight DMA (vmcnt is in order)
-        bf16x8 fa[kFR][2];
+        bf16x8 fa[kFR][NS];
         sfor<kFR - 2>([&](auto ic) { frag(slot, decltype(ic)::value, fa[decltype(ic)::value]); });
         sfor<HU / 2>([&](auto pc) {
             constexpr int t0 = 2 * decltype(pc)::value, t1 = t0 + 1;
@@ -386,8 +403,7 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
                 frag(slot, t0 + kFR - 2, fa[(t0 + kFR - 2) % kFR]);
                 frag(slot, t1 + kFR - 2, fa[(t1 + kFR - 2) % kFR]);
             }
-            mma3x2(fa[t0 % kFR][0], fa[t0 % kFR][1], bh, bl, acc[t0], fa[t1 % kFR][0], fa[t1 % kFR][1], bh, bl,
-                   acc[t1]);
+            mma_x2<NS>(fa[t0 % kFR], bx, acc[t0], fa[t1 % kFR], bx, acc[t1]);
         });
         advance(younger);
     };
@@ -447,7 +463,7 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
             raw[j] = j < nv ? x : 0.0f;
         }
     };
-    auto stage_in = [&](const float (&raw)[8], int c, bf16x8& bh, bf16x8& bl) {
+    auto stage_in = [&](const float (&raw)[8], int c, bf16x8 (&bx)[NS]) {
         const int f0 = 32 * c + 8 * hq;
         const b3f4 mu0 = *reinterpret_cast<const b3f4*>(s_mean + f0);
         const b3f4 mu1 = *reinterpret_cast<const b3f4*>(s_mean + f0 + 4);
@@ -465,13 +481,17 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) y[j] = (y[j] - (j < 4 ? mu0[j] : mu1[j - 4])) * (j < 4 ? rs0[j] : rs1[j - 4]);
-        split8(y, bh, bl);
+        splitN<NS>(y, bx);
     };
 
     // ---- activations: B fragments of the next layer (k-step c, element j of quarter q is
     //      unit 32c + 16(j>>2) + 4q + (j&3): registers of unit tiles 2c and 2c+1) ----
-    bf16x8 Bh[KS], Bl[KS];
-    auto hidden_epi = [&](int l) {  // relu(acc + bias_l) -> Bh/Bl
+    // NS = 2: split as soon as computed (B); NS = 3: kept in f32 (Y, 8 registers per k-step
+    // against 12 for the split) and split per chunk as the next hidden layer consumes it;
+    // the output layer, whose chunks each read every k-step, splits them all into B first
+    bf16x8 B[KS][NS];
+    float Y[NS == 3 ? KS : 1][8];
+    auto hidden_epi = [&](int l) {  // relu(acc + bias_l) -> B (NS = 2) / Y (NS = 3)
         sfor<KS>([&](auto cc) {
             constexpr int c = decltype(cc)::value;
             const b3f4 b0 = *reinterpret_cast<const b3f4*>(s_bias + l * HP + 32 * c + 4 * hq);
@@ -484,12 +504,26 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
                 y[r] = v0 > 0.0f ? v0 : 0.0f;
                 y[4 + r] = v1 > 0.0f ? v1 : 0.0f;
             }
-            split8(y, Bh[c], Bl[c]);
+            if constexpr (NS == 2) {
+                splitN<NS>(y, B[c]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) Y[c][j] = y[j];
+            }
         });
+    };
+    auto hidden_b = [&](auto cc, bf16x8 (&bx)[NS]) -> const bf16x8(&)[NS] {  // k-step c's B fragments
+        constexpr int c = decltype(cc)::value;
+        if constexpr (NS == 2) {
+            return B[c];
+        } else {
+            splitN<NS>(Y[c], bx);
+            return bx;
+        }
     };
     // output chunk: fragment i = 2q + ts accumulates tile ts of the chunk over k-step q
     auto step_out = [&]() {  // fragments 2q, 2q+1: k-step q of tiles 0 and 1, interleaved
-        bf16x8 fa[kFR][2];
+        bf16x8 fa[kFR][NS];
         sfor<kFR - 2>([&](auto ic) { frag(slot, decltype(ic)::value, fa[decltype(ic)::value]); });
         sfor<HU / 2>([&](auto qc) {
             constexpr int q = decltype(qc)::value, i0 = 2 * q, i1 = i0 + 1;
@@ -497,8 +531,7 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
                 frag(slot, i0 + kFR - 2, fa[(i0 + kFR - 2) % kFR]);
                 frag(slot, i1 + kFR - 2, fa[(i1 + kFR - 2) % kFR]);
             }
-            mma3x2(fa[i0 % kFR][0], fa[i0 % kFR][1], Bh[q], Bl[q], acc[0], fa[i1 % kFR][0], fa[i1 % kFR][1], Bh[q],
-                   Bl[q], acc[1]);
+            mma_x2<NS>(fa[i0 % kFR], B[q], acc[0], fa[i1 % kFR], B[q], acc[1]);
         });
     };
 
@@ -592,11 +625,11 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
             // then the weight DMA of chunk c + 2 and the input DMA of chunk c + 2 into the
             // buffer just read
             for (int c = 0; c < p.n1; ++c) {
-                bf16x8 xh, xl;
+                bf16x8 xb[NS];
                 read_in(c & 1, c, rawA);
-                stage_in(rawA, c, xh, xl);
+                stage_in(rawA, c, xb);
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the reads above before the DMA refills the buffer
-                step_layer(xh, xl, [&]() {
+                step_layer(xb, [&]() {
                     if (c + 2 < p.n1) {
                         glds_in(c & 1, c + 2);
                         return 8;
@@ -606,14 +639,14 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
             }
         } else
         for (int c = 0; c < p.n1; c += 2) {
-            bf16x8 xh, xl;
-            stage_in(rawA, c, xh, xl);
+            bf16x8 xb[NS];
+            stage_in(rawA, c, xb);
             if (c + 2 < p.n1) load_in(rawA, c + 2);
-            step_layer(xh, xl, [] { return 0; });
+            step_layer(xb, [] { return 0; });
             if (c + 1 < p.n1) {
-                stage_in(rawB, c + 1, xh, xl);
+                stage_in(rawB, c + 1, xb);
                 if (c + 3 < p.n1) load_in(rawB, c + 3);
-                step_layer(xh, xl, [] { return 0; });
+                step_layer(xb, [] { return 0; });
             }
         }
         hidden_epi(0);
@@ -621,11 +654,13 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
         for (int l = 0; l < p.nhx; ++l) {
             zero_acc();
             sfor<KS>([&](auto cc) {
-                constexpr int c = decltype(cc)::value;
-                step_layer(Bh[c], Bl[c], [] { return 0; });
+                bf16x8 tb[NS];
+                step_layer(hidden_b(cc, tb), [] { return 0; });
             });
             hidden_epi(l + 1);
         }
+        if constexpr (NS == 3)
+            sfor<KS>([&](auto cc) { splitN<NS>(Y[decltype(cc)::value], B[decltype(cc)::value]); });
         // ---- output layer, two 16-row tiles per chunk; the next tile's inputs start loading ----
         const int64_t nt = tile + gridDim.x;
         if (nt < p.ntiles) {
@@ -717,12 +752,13 @@ float bf16_f(uint16_t h)
 }  // namespace
 
 // ------------------------------------------------------------------------------------
-// host: pack the model once (fv3_dense_create) into the bf16x3 chunk stream
+// host: pack the model once (fv3_dense_create) into the bf16x3 and bf16x6 chunk streams
 // ------------------------------------------------------------------------------------
-int b3_pack(fv3_dense_model* m, const fv3_dense_desc* d)
+static int pack_ns(fv3_dense_model* m, const fv3_dense_desc* d, int NS, B3Pack** dst)
 {
     auto b = new B3Pack();
     std::unique_ptr<B3Pack> guard(b);
+    b->ns = NS;
     const int W = d->width;
     b->hu = W <= 64 ? 4 : (W <= 128 ? 8 : 16);
     b->hp = 16 * b->hu;
@@ -783,17 +819,20 @@ int b3_pack(fv3_dense_model* m, const fv3_dense_desc* d)
     b->n_oc = (int)b->otile.size() / 2;
     b->kop = 16 * (int)b->otile.size();
     b->nch = b->n1 + b->nhx * KS + b->n_oc;
-    const size_t cbe = (size_t)1024 * HU;  // bf16 elements per chunk
+    const size_t cbe = (size_t)512 * NS * HU;  // bf16 elements per chunk
     FV3_REQUIRE((size_t)b->nch * cbe * 2 < (1u << 31), "dense_create: model too large for the bf16x3 stream");
 
     std::vector<uint16_t> ws((size_t)b->nch * cbe, 0);
-    // fragment i of a chunk: lane (q = lane >> 4, r = lane & 15) element j is A[row r][k 8q + j]
+    // fragment i of a chunk: lane (q = lane >> 4, r = lane & 15) element j is A[row r][k 8q + j];
+    // part s of it (the kernel's splitN: rne of the residual of the parts before) at +512 s
     auto put = [&](int chunk, int i, int lane, int j, float v) {
-        const uint16_t hi = bf16_rne(v);
-        const uint16_t lo = bf16_rne(v - bf16_f(hi));
-        const size_t at = (size_t)chunk * cbe + ((size_t)(2 * i) * 64 + lane) * 8 + j;
-        ws[at] = hi;
-        ws[at + 512] = lo;
+        const size_t at = (size_t)chunk * cbe + ((size_t)(NS * i) * 64 + lane) * 8 + j;
+        float r = v;
+        for (int s = 0; s < NS; ++s) {
+            const uint16_t h = bf16_rne(r);
+            ws[at + 512 * s] = h;
+            r = r - bf16_f(h);
+        }
     };
     // layer 1: natural feature order, k = 32c + 8q + j; fragment t = unit tile t
     const float* K0 = d->hidden_kernel[0];
@@ -868,16 +907,25 @@ int b3_pack(fv3_dense_model* m, const fv3_dense_desc* d)
     FV3_HIP(hipMalloc(&b->dbuf, b->consts_off + cst.size() * 4));
     FV3_HIP(hipMemcpy(b->dbuf, ws.data(), ws.size() * 2, hipMemcpyHostToDevice));
     FV3_HIP(hipMemcpy((char*)b->dbuf + b->consts_off, cst.data(), cst.size() * 4, hipMemcpyHostToDevice));
-    m->b3 = guard.release();
+    *dst = guard.release();
     return FV3_OK;
+}
+
+int b3_pack(fv3_dense_model* m, const fv3_dense_desc* d)
+{
+    if (const int st = pack_ns(m, d, 2, &m->b3)) return st;
+    return pack_ns(m, d, 3, &m->b6);
 }
 
 void b3_free(fv3_dense_model* m)
 {
-    if (!m || !m->b3) return;
-    if (m->b3->dbuf) (void)hipFree(m->b3->dbuf);
-    delete m->b3;
-    m->b3 = nullptr;
+    if (!m) return;
+    for (B3Pack** pk : {&m->b3, &m->b6}) {
+        if (!*pk) continue;
+        if ((*pk)->dbuf) (void)hipFree((*pk)->dbuf);
+        delete *pk;
+        *pk = nullptr;
+    }
 }
 
 }  // namespace fv3
@@ -889,14 +937,16 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
     using namespace fv3;
     if (precision == FV3_DENSE_F32) return fv3_dense_forward(m, inputs, in_l, outputs, out_l, ncol, stream);
     clear_error();
-    FV3_REQUIRE(precision == FV3_DENSE_BF16X3, "dense_forward_ex: unknown precision %d", precision);
+    FV3_REQUIRE(precision == FV3_DENSE_BF16X3 || precision == FV3_DENSE_BF16X6,
+                "dense_forward_ex: unknown precision %d", precision);
     FV3_REQUIRE(m, "dense_forward_ex: NULL model");
-    FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, m->b3, "dense_forward_ex: this model has no bf16x3 pack "
+    const B3Pack* pk = precision == FV3_DENSE_BF16X6 ? m->b6 : m->b3;
+    FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, pk, "dense_forward_ex: this model has no bf16 split pack "
                      "(too many input features or output rows); use FV3_DENSE_F32");
     FV3_REQUIRE(ncol >= 0, "dense_forward_ex: ncol < 0");
     if (ncol == 0) return FV3_OK;
     FV3_REQUIRE(inputs && in_l && outputs && out_l, "dense_forward_ex: NULL argument");
-    const B3Pack& b = *m->b3;
+    const B3Pack& b = *pk;
     B3Args a{};
     const int64_t nb = in_l[0].ncol_blk;
     for (int v = 0; v < m->n_in; ++v) {
@@ -954,18 +1004,22 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
     // FV3_B3_STAGE=glds / reg: the LDS-DMA or the register-staged pipeline (A/B)
     const char* stg_env = getenv("FV3_B3_STAGE");
     auto lds_of = [&](bool g) {
-        return (size_t)b3_slots(g) * 2048 * b.hu + (size_t)b3_in_bytes(g) + (size_t)4 * ((b.nconst + 7) & ~7) +
+        return (size_t)b3_slots(g) * 1024 * b.ns * b.hu + (size_t)b3_in_bytes(g) + (size_t)4 * ((b.nconst + 7) & ~7) +
                sizeof(B3Grp) * 4 * b.n1;
     };
     // the LDS-DMA pipeline needs a third ring slot and the input rows: a model that only
     // fits the register-staged pipeline's LDS runs on that one
     const bool gl = (stg_env ? stg_env[0] == 'g' : kB3GldsDefault) && lds_of(true) <= 160 * 1024;
-    const void* kfn = gl ? (b.hu == 4 ? (const void*)dense_b3_kernel<4, true>
-                            : b.hu == 8 ? (const void*)dense_b3_kernel<8, true>
-                                        : (const void*)dense_b3_kernel<16, true>)
-                         : (b.hu == 4 ? (const void*)dense_b3_kernel<4, false>
-                            : b.hu == 8 ? (const void*)dense_b3_kernel<8, false>
-                                        : (const void*)dense_b3_kernel<16, false>);
+    auto pick = [&](auto ns) -> const void* {
+        constexpr int NS = decltype(ns)::value;
+        return gl ? (b.hu == 4 ? (const void*)dense_b3_kernel<4, true, NS>
+                     : b.hu == 8 ? (const void*)dense_b3_kernel<8, true, NS>
+                                 : (const void*)dense_b3_kernel<16, true, NS>)
+                  : (b.hu == 4 ? (const void*)dense_b3_kernel<4, false, NS>
+                     : b.hu == 8 ? (const void*)dense_b3_kernel<8, false, NS>
+                                 : (const void*)dense_b3_kernel<16, false, NS>);
+    };
+    const void* kfn = b.ns == 3 ? pick(std::integral_constant<int, 3>{}) : pick(std::integral_constant<int, 2>{});
     const size_t lds = lds_of(gl);
     FV3_REQUIRE(lds <= 160 * 1024, "dense_forward_ex: model needs %zu bytes of LDS", lds);
     static std::mutex mu;

@@ -72,7 +72,7 @@ struct DenseArgs {
 };
 static_assert(sizeof(DenseArgs) <= 4096, "kernel arguments are limited to 4 KiB");
 
-struct B3Pack;  // dense_b3.hip: the bf16x3 weight stream and its constants
+struct B3Pack;  // dense_b3.hip: a bf16 split weight stream (bf16x3 / bf16x6) and its constants
 
 }  // namespace fv3
 
@@ -85,7 +85,8 @@ struct fv3_dense_model {
     std::vector<fv3::DenseOutTile> otiles;
     void* dbuf = nullptr;
     fv3::DenseArgs tmpl{};  // device pointers filled, per-call fields empty
-    fv3::B3Pack* b3 = nullptr;
+    fv3::B3Pack* b3 = nullptr;  // bf16x3 weight stream (2 bf16 parts per weight)
+    fv3::B3Pack* b6 = nullptr;  // bf16x6 weight stream (3 parts)
 };
 
 namespace fv3 {

@@ -89,7 +89,7 @@ def _glorot(rng, fan_in, fan_out):
     return rng.uniform(-lim, lim, size=(fan_in, fan_out)).astype(np.float32)
 
 
-PRECISIONS = {"f32": _native.DENSE_F32, "bf16x3": _native.DENSE_BF16X3}
+PRECISIONS = {"f32": _native.DENSE_F32, "bf16x3": _native.DENSE_BF16X3, "bf16x6": _native.DENSE_BF16X6}
 
 
 class DenseColumnModel:
@@ -98,7 +98,8 @@ class DenseColumnModel:
     ``precision`` selects the fused kernel's arithmetic: ``"f32"`` (exact f32 products on
     v_mfma_f32_16x16x4_f32, the Keras precision) or ``"bf16x3"`` (each f32 operand split
     into bf16 hi + lo, three bf16 MFMAs per product; ~1e-5 rel, BASELINE config #5's
-    bf16-MFMA path)."""
+    bf16-MFMA path) or ``"bf16x6"`` (hi + mid + lo, six bf16 MFMAs per product: f32-level
+    error on bf16 MFMA, csrc/dense_b3.hip)."""
 
     def __init__(self, config: DenseModelConfig, params: Mapping[str, object], precision: str = "f32"):
         self.config = config

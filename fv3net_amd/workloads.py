@@ -324,7 +324,8 @@ class PredictMappmWorkload:
             self._plans()
 
 
-def make_predict_mappm_workload(res: int = 384, rank: int = 0, world: int = 1, seed: int = 0, device=None):
+def make_predict_mappm_workload(res: int = 384, rank: int = 0, world: int = 1, seed: int = 0, device=None,
+                                precision: str = "f32"):
     from .distributed import row_band
 
     device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -334,6 +335,7 @@ def make_predict_mappm_workload(res: int = 384, rank: int = 0, world: int = 1, s
     sample_T = T[0, :, :8, :8].reshape(NZ, -1).T.cpu().numpy()
     sample_q = q[0, :, :8, :8].reshape(NZ, -1).T.cpu().numpy()
     model = DenseColumnModel.random(dense_2x256_config(), seed=1, sample_inputs=[sample_T, sample_q])
+    model.precision = precision
     T, q = band(T), band(q)
     ncol = (r1 - r0) * res
     g = torch.Generator(device=device)

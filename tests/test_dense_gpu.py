@@ -155,7 +155,8 @@ def test_c384_throughput_shape_and_determinism(gpu):
     _check(got, dense_predict(sub, m.oracle_params(), np.float64))
 
 
-@pytest.mark.parametrize("res,precision", [(7, "f32"), (48, "f32"), (7, "bf16x3"), (48, "bf16x3")])
+@pytest.mark.parametrize("res,precision", [(7, "f32"), (48, "f32"), (7, "bf16x3"), (48, "bf16x3"), (7, "bf16x6"),
+                                           (48, "bf16x6")])
 def test_writes_stay_inside_outputs(gpu, res, precision):
     """Outputs as level slices of larger (tile, z, y, x) buffers pre-filled with NaN:
     the kernels write exactly the model's rows of the real columns (the f32 epilogue
@@ -177,7 +178,7 @@ def test_writes_stay_inside_outputs(gpu, res, precision):
     for b in bigs:
         assert torch.isnan(b[:, :5]).all() and torch.isnan(b[:, 84:]).all()
     got = [_to_samples(o.cpu().numpy()) for o in outs]
-    _check(got, dense_predict(samples, m.oracle_params(), np.float64), rtol=RTOL if precision == "f32" else 1e-4)
+    _check(got, dense_predict(samples, m.oracle_params(), np.float64), rtol=1e-4 if precision == "bf16x3" else RTOL)
 
 
 @pytest.mark.parametrize("res,width,ragged", [(12, 256, False), (48, 256, False), (7, 128, True), (12, 64, False)])
@@ -225,7 +226,7 @@ def test_bind_float64_state_sees_updates(gpu):
 
 
 @pytest.mark.parametrize("ncol,precision", [(1000, "f32"), (1000, "bf16x3"), (13824 + 37, "f32"),
-                                            (13824 + 37, "bf16x3")])
+                                            (13824 + 37, "bf16x3"), (1000, "bf16x6"), (13824 + 37, "bf16x6")])
 def test_residual_outputs_stay_inside(gpu, ncol, precision):
     """Regression for the memory fault fixed in round 1 (residual outputs read one level
     past a 79-level input): an emulator-style model whose output is input + de-normalised
@@ -251,7 +252,7 @@ def test_residual_outputs_stay_inside(gpu, ncol, precision):
     y = dense_predict([x, w], m.oracle_params(), np.float64)
     ref = [x.astype(np.float64) + y[0], w.astype(np.float64) + y[1]]
     got = [o.cpu().numpy().T for o in outs]
-    _check(got, ref, rtol=RTOL if precision == "f32" else 1e-4)
+    _check(got, ref, rtol=1e-4 if precision == "bf16x3" else RTOL)
 
 
 def test_bind_refuses_snapshot_inputs(gpu):

@@ -53,7 +53,7 @@ def _emulator(ncol=2048, seed=1, precision="bf16x3"):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("precision,rtol", [("bf16x3", 1e-4), ("f32", 1e-5)])
+@pytest.mark.parametrize("precision,rtol", [("bf16x3", 1e-4), ("bf16x6", 1e-5), ("f32", 1e-5)])
 def test_emulator_matches_oracle(gpu, precision, rtol):
     import torch
 
@@ -123,7 +123,7 @@ def _device_raw(ncol, nz=79, seed=5):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("precision,rtol", [("bf16x3", 1e-4), ("f32", 1e-5)])
+@pytest.mark.parametrize("precision,rtol", [("bf16x3", 1e-4), ("bf16x6", 1e-5), ("f32", 1e-5)])
 def test_emulator_c384_full_grid(gpu, precision, rtol):
     """BASELINE config #5 at its real size: 884,736 columns, so every persistent block
     walks many tiles (bf16x3: 6,912 tiles of 128 on one block per CU; f32: 27,648 tiles
@@ -175,7 +175,8 @@ def test_emulator_bf16x3_pipelines_agree(gpu, monkeypatch):
     _check_columns(reg, state, emu, np.arange(2085), 1e-4)
 
 
-@pytest.mark.parametrize("precision,rtol,env", [("bf16x3", 1e-4, "FV3_B3_GRID"), ("f32", 1e-5, "FV3_DENSE_GRID")])
+@pytest.mark.parametrize("precision,rtol,env", [("bf16x3", 1e-4, "FV3_B3_GRID"), ("bf16x6", 1e-5, "FV3_B3_GRID"),
+                                                ("f32", 1e-5, "FV3_DENSE_GRID")])
 def test_emulator_forced_multi_tile_blocks(gpu, precision, rtol, env, monkeypatch):
     """A ragged grid (2,085 columns) on 4 persistent blocks: every block walks >= 4 tiles
     (bf16x3: 17 tiles of 128; f32: 66 of 32), so the cross-tile prefetch of the LDS

@@ -55,7 +55,7 @@ def test_oracle_kat(dtype):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("precision", ["f32", "bf16x3"])
+@pytest.mark.parametrize("precision", ["f32", "bf16x3", "bf16x6"])
 def test_kernel_kat(gpu, precision):
     import torch
 

@@ -29,8 +29,9 @@ def timed(step, n):
 
 def report(name, wl, t, prec):
     flop = wl.ncol * wl.flops_per_column / t / 1e12
+    nm = {"bf16x3": 3, "bf16x6": 6}.get(prec)
     extra = f"{flop / F32_PEAK:.3f} of f32 MFMA peak" if prec == "f32" else \
-        f"{3 * flop / BF16_PEAK:.3f} of bf16 MFMA peak (3 MFMAs/product)"
+        f"{nm * flop / BF16_PEAK:.3f} of bf16 MFMA peak ({nm} MFMAs/product)"
     print(f"{name:18s} {prec:6s}: {t * 1e6:9.1f} us  {wl.ncol / t:.3e} col/s  {flop:6.1f} f32-equiv TFLOP/s  {extra}",
           flush=True)
 
@@ -46,3 +47,6 @@ if __name__ == "__main__":
         if "emulator" in which:
             wl = W.make_emulator_workload(384, seed=13, device=dev, precision=prec)
             report("emulator C384", wl, timed(wl.step, 10), prec)
+        if "pm" in which:  # predict + two-field mappm on one C384 state
+            wl = W.make_predict_mappm_workload(384, seed=21, device=dev, precision=prec)
+            report("predict+mappm C384", wl, timed(wl.step, 10), prec)
