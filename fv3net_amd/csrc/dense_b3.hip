@@ -52,9 +52,9 @@ typedef float b3f4 __attribute__((ext_vector_type(4)));
 namespace fv3 {
 
 constexpr int kB3Groups = 128;   // 8-feature input groups (<= 1024 padded input features)
-constexpr int kB3Cols = 128;     // columns per block tile: 8 waves x 16
+constexpr int kB3Cols = 128;     // columns per block tile: 8 waves x 16 (4-wave blocks: 64)
 constexpr int kB3OutTiles = 32;  // 16-row output tiles (<= 512 padded output rows)
-constexpr int kB3Threads = 512;
+constexpr int kB3Threads = 512;  // 8-wave blocks (4-wave blocks on small grids: 256)
 // the LDS-DMA pipeline by default: emulator C384 2.41 -> 2.29-2.34 ms, 2x256 C384 827 -> 814-820 us
 // against the register-staged one on the same box (round 3; a variant holding the output
 // chunks' accumulators / residuals in two register sets instead of copying them measured
@@ -66,8 +66,10 @@ constexpr bool kB3GldsDefault = true;
 #define FV3_B3_FR 4
 #endif
 constexpr int kFR = FV3_B3_FR;
-constexpr int b3_slots(bool gl) { return gl ? 3 : 2; }
-constexpr int b3_in_bytes(bool gl) { return gl ? 2 * 8 * 8 * 64 * 4 : 0; }
+// weight ring slots: SL (LDS-DMA pipeline: 3, or 2 where three chunks do not fit, e.g.
+// bf16x6 at width 256), 0 = the register-staged pipeline (2 slots)
+constexpr int b3_slots(int sl) { return sl > 0 ? sl : 2; }
+constexpr int b3_in_bytes(bool gl, int nwv) { return gl ? 2 * nwv * 8 * 64 * 4 : 0; }
 
 struct B3Pack {
     void* dbuf = nullptr;
@@ -260,8 +262,11 @@ typedef __attribute__((address_space(3))) void* LdsVoid;
 // and no ds_write pass.  !GL: round 2's pipeline (weights through 16 staging registers and
 // ds_write_b128 into a 2-slot ring, inputs into registers), kept for A/B (FV3_B3_STAGE=reg).
 // NS: bf16 parts per f32 operand (2: bf16x3, 3: bf16x6, see SplitTerms)
-template <int HU, bool GL, int NS>
-__global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2))) void dense_b3_kernel(B3Args pa)
+// NWV: waves per block (8; 4 on grids with fewer 128-column tiles than CUs, so every
+// CU gets a tile and each SIMD runs one 16-column wave)
+template <int HU, int SL, int NS, int NWV>
+__global__ __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(NWV == 4 ? 1 : 2, NWV == 4 ? 1 : 2))) void
+dense_b3_kernel(B3Args pa)
 {
     (void)pa;
     KB3& p = *(KB3*)(__builtin_amdgcn_kernarg_segment_ptr());
@@ -270,13 +275,15 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
     constexpr int CB = 1024 * NS * HU;  // chunk: HU A fragments x NS parts x 64 lanes x 16 B
     // 16-B loads per thread per chunk; a chunk that is not a whole number of block-wide
     // loads (HU = 4 at NS = 3: 1.5) has its last load on the first waves only (wave-uniform)
+    constexpr int kB3Threads = 64 * NWV, kB3Cols = 16 * NWV;  // this instantiation's block
     constexpr int NST = (CB + 16 * kB3Threads - 1) / (16 * kB3Threads);
-    constexpr int NSL = b3_slots(GL);            // weight ring slots
+    constexpr bool GL = SL > 0;
+    constexpr int NSL = b3_slots(SL);            // weight ring slots
     static_assert(HU % 4 == 0 && NST >= 1, "unit tiles per layer must be a multiple of 4");
     extern __shared__ __attribute__((aligned(16))) b3f4 lds3[];
     char* ring = reinterpret_cast<char*>(lds3);
     float* s_in = reinterpret_cast<float*>(ring + NSL * CB);  // GL: [2][8 waves][8 levels][64 lanes]
-    float* s_mean = reinterpret_cast<float*>(ring + NSL * CB + b3_in_bytes(GL));
+    float* s_mean = reinterpret_cast<float*>(ring + NSL * CB + b3_in_bytes(GL, NWV));
     float* s_rs = s_mean + p.kp1;
     float* s_bias = s_rs + p.kp1;             // [nh][HP]
     float* s_oc = s_bias + (1 + p.nhx) * HP;  // [6][kop]: bias, sigma, mean, lo, hi, mask
@@ -339,10 +346,11 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
                                                  0);
     };
     int slot = 0;                         // ring slot of the chunk computed next
-    int jn2 = p.nch > 2 ? 2 : 2 % p.nch;  // stream index of the chunk after next
+    // stream index of the chunk staged next (GL: chunk + NSL - 1, !GL: chunk + 2)
+    int jn2 = GL && NSL == 2 ? (p.nch > 1 ? 1 : 0) : (p.nch > 2 ? 2 : 2 % p.nch);
     if constexpr (GL) {
         glds_w(0, 0);
-        glds_w(p.nch > 1 ? 1 : 0, 1);
+        if constexpr (NSL == 3) glds_w(p.nch > 1 ? 1 : 0, 1);
     } else {
         load_stage(0);
         write_stage(0);
@@ -373,7 +381,7 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
     };
     auto stage_next = [&]() {
         if constexpr (GL) {
-            glds_w(jn2, slot == 0 ? 2 : slot - 1);  // chunk +2 into the slot chunk -1 released
+            glds_w(jn2, slot == 0 ? NSL - 1 : slot - 1);  // chunk +NSL-1 into the slot chunk -1 released
         } else {
 #ifndef FV3_B3_EXP_NOSTAGE  // experiment only (results invalid): no weight streaming
             write_stage(slot ^ 1);  // chunk +1 (its slot held chunk -1, released by the last barrier)
@@ -385,7 +393,8 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
     // landed before the barrier that publishes it; `younger` = vector-memory operations this
     // chunk issued after its own weight DMA (they, and that DMA, may stay in flight)
     auto advance = [&](int younger) {
-        if constexpr (GL) vm_wait_le(nst_w + younger);
+        // (two slots: the DMA this chunk issued is chunk +1 itself, so none of it may stay)
+        if constexpr (GL) vm_wait_le((NSL == 3 ? nst_w : 0) + younger);
         b3_barrier();
         slot = GL ? (slot == NSL - 1 ? 0 : slot + 1) : (slot ^ 1);
         jn2 = jn2 + 1 == p.nch ? 0 : jn2 + 1;
@@ -453,13 +462,13 @@ __global__ __launch_bounds__(kB3Threads) __attribute__((amdgpu_waves_per_eu(2, 2
 #pragma unroll
         for (int j = 0; j < 8; ++j)
             __builtin_amdgcn_global_load_lds((GlobalVoid)(ptr + (j < nv ? j * ld : 0)),
-                                             (LdsVoid)(s_in + ((buf * 8 + wave) * 8 + j) * 64), 4, 0, 0);
+                                             (LdsVoid)(s_in + ((buf * NWV + wave) * 8 + j) * 64), 4, 0, 0);
     };
     auto read_in = [&](int buf, int c, float (&raw)[8]) {  // GL: chunk c's values (landed, see advance)
         const int nv = lvalid ? s_grp[4 * c + hq].nv : 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const float x = s_in[((buf * 8 + wave) * 8 + j) * 64 + lane];
+            const float x = s_in[((buf * NWV + wave) * 8 + j) * 64 + lane];
             raw[j] = j < nv ? x : 0.0f;
         }
     };
@@ -982,7 +991,6 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
     a.any_log = b.any_log;
     a.ncol = ncol;
     a.ncol_blk = nb;
-    a.ntiles = (ncol + kB3Cols - 1) / kB3Cols;
     for (size_t g = 0; g < b.gmeta.size(); ++g) a.gmeta[g] = b.gmeta[g];
     for (size_t g = 0; g < b.otile.size(); ++g) a.otile[g] = b.otile[g];
     // the epilogue addresses outputs / residual inputs with 32-bit byte offsets
@@ -1003,29 +1011,8 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
 
     // FV3_B3_STAGE=glds / reg: the LDS-DMA or the register-staged pipeline (A/B)
     const char* stg_env = getenv("FV3_B3_STAGE");
-    auto lds_of = [&](bool g) {
-        return (size_t)b3_slots(g) * 1024 * b.ns * b.hu + (size_t)b3_in_bytes(g) + (size_t)4 * ((b.nconst + 7) & ~7) +
-               sizeof(B3Grp) * 4 * b.n1;
-    };
-    // the LDS-DMA pipeline needs a third ring slot and the input rows: a model that only
-    // fits the register-staged pipeline's LDS runs on that one
-    const bool gl = (stg_env ? stg_env[0] == 'g' : kB3GldsDefault) && lds_of(true) <= 160 * 1024;
-    auto pick = [&](auto ns) -> const void* {
-        constexpr int NS = decltype(ns)::value;
-        return gl ? (b.hu == 4 ? (const void*)dense_b3_kernel<4, true, NS>
-                     : b.hu == 8 ? (const void*)dense_b3_kernel<8, true, NS>
-                                 : (const void*)dense_b3_kernel<16, true, NS>)
-                  : (b.hu == 4 ? (const void*)dense_b3_kernel<4, false, NS>
-                     : b.hu == 8 ? (const void*)dense_b3_kernel<8, false, NS>
-                                 : (const void*)dense_b3_kernel<16, false, NS>);
-    };
-    const void* kfn = b.ns == 3 ? pick(std::integral_constant<int, 3>{}) : pick(std::integral_constant<int, 2>{});
-    const size_t lds = lds_of(gl);
-    FV3_REQUIRE(lds <= 160 * 1024, "dense_forward_ex: model needs %zu bytes of LDS", lds);
     static std::mutex mu;
     static int n_cu = 0;
-    static std::vector<std::pair<std::pair<const void*, size_t>, int>> resident;
-    int res = 0;
     {
         std::lock_guard<std::mutex> lock(mu);
         if (!n_cu) {
@@ -1033,10 +1020,50 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
             FV3_HIP(hipGetDevice(&dev));
             FV3_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
         }
+    }
+    // 4-wave blocks of 64 columns where 128-column tiles would leave CUs idle (C48: 108
+    // tiles of 128 on 256 CUs -> 216 of 64); FV3_B3_WAVES=4|8 forces one (A/B)
+    int nwv = (ncol + kB3Cols - 1) / kB3Cols < n_cu ? 4 : 8;
+    if (const char* e = getenv("FV3_B3_WAVES")) nwv = atoi(e) == 4 ? 4 : 8;
+    const int nthr = 64 * nwv, ncols = 16 * nwv;
+    a.ntiles = (ncol + ncols - 1) / ncols;
+    auto lds_of = [&](int sl) {
+        return (size_t)b3_slots(sl) * 1024 * b.ns * b.hu + (size_t)b3_in_bytes(sl > 0, nwv) +
+               (size_t)4 * ((b.nconst + 7) & ~7) + sizeof(B3Grp) * 4 * b.n1;
+    };
+    // the LDS-DMA pipeline with a 3-slot ring where it fits, else (bf16x6) with 2 slots;
+    // a model that only fits the register-staged pipeline's LDS runs on that one
+    int sl = 0;
+    if (stg_env ? stg_env[0] == 'g' : kB3GldsDefault)
+        sl = lds_of(3) <= 160 * 1024 ? 3 : (b.ns == 3 && lds_of(2) <= 160 * 1024 ? 2 : 0);
+    if (stg_env && stg_env[0] == 'g' && stg_env[1] == '2' && b.ns == 3 && lds_of(2) <= 160 * 1024) sl = 2;  // A/B
+    auto pick = [&](auto ns) -> const void* {
+        constexpr int NS = decltype(ns)::value;
+        auto by_hu = [&](auto slc) -> const void* {
+            constexpr int S = decltype(slc)::value;
+            if (nwv == 4)
+                return b.hu == 4 ? (const void*)dense_b3_kernel<4, S, NS, 4>
+                     : b.hu == 8 ? (const void*)dense_b3_kernel<8, S, NS, 4>
+                                 : (const void*)dense_b3_kernel<16, S, NS, 4>;
+            return b.hu == 4 ? (const void*)dense_b3_kernel<4, S, NS, 8>
+                 : b.hu == 8 ? (const void*)dense_b3_kernel<8, S, NS, 8>
+                             : (const void*)dense_b3_kernel<16, S, NS, 8>;
+        };
+        if constexpr (NS == 3)
+            if (sl == 2) return by_hu(std::integral_constant<int, 2>{});
+        return sl == 3 ? by_hu(std::integral_constant<int, 3>{}) : by_hu(std::integral_constant<int, 0>{});
+    };
+    const void* kfn = b.ns == 3 ? pick(std::integral_constant<int, 3>{}) : pick(std::integral_constant<int, 2>{});
+    const size_t lds = lds_of(sl);
+    FV3_REQUIRE(lds <= 160 * 1024, "dense_forward_ex: model needs %zu bytes of LDS", lds);
+    static std::vector<std::pair<std::pair<const void*, size_t>, int>> resident;
+    int res = 0;
+    {
+        std::lock_guard<std::mutex> lock(mu);
         for (auto& r : resident)
             if (r.first.first == kfn && r.first.second == lds) res = r.second;
         if (!res) {
-            FV3_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&res, kfn, kB3Threads, lds));
+            FV3_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&res, kfn, nthr, lds));
             res = std::max(1, res);
             resident.push_back({{kfn, lds}, res});
         }
@@ -1044,7 +1071,7 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
     int64_t grid = std::min<int64_t>(a.ntiles, (int64_t)res * n_cu);
     if (const char* e = getenv("FV3_B3_GRID")) grid = std::min<int64_t>(a.ntiles, std::max(1, atoi(e)));
     void* kargs[] = {&a};
-    FV3_HIP(hipLaunchKernel(kfn, dim3((unsigned)grid), dim3(kB3Threads), kargs, lds, (hipStream_t)stream));
+    FV3_HIP(hipLaunchKernel(kfn, dim3((unsigned)grid), dim3(nthr), kargs, lds, (hipStream_t)stream));
     FV3_LAUNCH_CHECK();
     return FV3_OK;
 }

@@ -41,7 +41,7 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["dense", "emulator"]
     for prec in os.environ.get("B3_PRECS", "bf16x3,f32").split(","):
         if "dense" in which:
-            for res, n in ((48, 200), (384, 10)):
+            for res, n in [(r, 200 if r < 384 else 10) for r in map(int, os.environ.get("B3_RES", "48,384").split(","))]:
                 wl = W.make_dense_workload(res, seed=1, device=dev, precision=prec)
                 report(f"dense C{res}", wl, timed(wl.step, n), prec)
         if "emulator" in which:
