@@ -7,3 +7,4 @@ for st in glds g2 reg; do
   FV3_B3_STAGE=$st B3_RES=384 B3_PRECS=bf16x6 timeout -k 10 120 python -u tools/b3_time.py dense > gpurun_out/b6_time_$st.log 2>&1 || exit 1
 done
 B3_PRECS=f32,bf16x6 timeout -k 10 200 python -u tools/b3_time.py pm emulator > gpurun_out/b6_time_pm.log 2>&1
+timeout -k 10 120 python -u tools/overlap_probe3.py > gpurun_out/b6_overlap.log 2>&1

@@ -5,7 +5,8 @@
 Legs are the kernels bench.py reports (its headline + every `extra` entry):
   dense_c48, dense_c384, dense_c384_bf16x3, emulator_c384 (bf16x3), emulator_c384_f32,
   mappm_c384_k1, mappm_c384_k10, mappm_c12, coarsen_1f, coarsen_4f, stepper_c96,
-  predict_mappm_c384.
+  predict_mappm_c384, and the bf16x6 legs dense_c48_bf16x6, dense_c384_bf16x6,
+  emulator_c384_bf16x6, predict_mappm_c384_bf16x6.
 Each leg warms up (untimed) before its N profiled launches; the collector keeps only the
 last N dispatches of the leg's dominant kernel.
 """
@@ -25,6 +26,12 @@ def make(leg, dev):
         return W.make_dense_workload(384, seed=3, device=dev)
     if leg == "dense_c384_bf16x3":
         return W.make_dense_workload(384, seed=3, device=dev, precision="bf16x3")
+    if leg in ("dense_c48_bf16x6", "dense_c384_bf16x6"):
+        return W.make_dense_workload(48 if "c48" in leg else 384, seed=3, device=dev, precision="bf16x6")
+    if leg == "emulator_c384_bf16x6":
+        return W.make_emulator_workload(384, seed=13, device=dev, precision="bf16x6")
+    if leg == "predict_mappm_c384_bf16x6":
+        return W.make_predict_mappm_workload(384, seed=17, device=dev, precision="bf16x6")
     if leg == "emulator_c384":
         return W.make_emulator_workload(384, seed=13, device=dev, precision="bf16x3")
     if leg == "emulator_c384_f32":

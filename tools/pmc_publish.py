@@ -35,6 +35,10 @@ LEGS = {
     "stepper_c96_predict": ("stepper_c96", "dense_forward_kernel"),
     "predict_mappm_c384": ("predict_mappm_c384", "dense_forward_kernel"),
     "predict_mappm_c384_mappm": ("predict_mappm_c384", "mappm_ppm_pair_kernel"),
+    "dense_c48_bf16x6": ("dense_c48_bf16x6", "dense_b3_kernel"),
+    "dense_c384_bf16x6": ("dense_c384_bf16x6", "dense_b3_kernel"),
+    "emulator_c384_bf16x6": ("emulator_c384_bf16x6", "dense_b3_kernel"),
+    "predict_mappm_c384_bf16x6": ("predict_mappm_c384_bf16x6", "dense_b3_kernel"),
 }
 KEEP = ("fv3::", "calib_")
 
