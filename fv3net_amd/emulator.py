@@ -18,8 +18,9 @@ hook's state dict, _emulate/microphysics.py:83-101), which is the kernel's
 
 Precision: ``"bf16x3"`` (the default, csrc/dense_b3.hip) runs every product on bf16
 MFMA with each f32 operand split into hi + lo (3 MFMAs per product, ~1e-5 against the
-float64 graph); ``"f32"`` runs exact-f32 MFMA (csrc/dense.hip, ~1e-6).  Config #5's
-contract is 1e-3 rel; the tests hold bf16x3 to 1e-4 and f32 to 1e-5 per level.
+float64 graph); ``"bf16x6"`` splits into hi + mid + lo (6 MFMAs per product, f32-level
+error); ``"f32"`` runs exact-f32 MFMA (csrc/dense.hip, ~1e-6).  Config #5's contract is
+1e-3 rel; the tests hold bf16x3 to 1e-4 and bf16x6 / f32 to 1e-5 per level.
 """
 import dataclasses
 from typing import Callable, Dict, List, Mapping, Optional

@@ -154,25 +154,33 @@ def test_emulator_c384_full_grid(gpu, precision, rtol):
 
 
 @pytest.mark.gpu
-def test_emulator_bf16x3_pipelines_agree(gpu, monkeypatch):
-    """The bf16x3 kernel's two staging pipelines (LDS-DMA, the default, and register
-    staging, FV3_B3_STAGE=reg) run the same arithmetic in the same order: bit-identical
-    outputs on a ragged grid forced to 4 persistent blocks (every block walks >= 4 tiles,
-    so the cross-tile input DMA, the residual reads and the 3-slot weight ring wrap
-    around), and within the oracle bound."""
+@pytest.mark.parametrize("precision,rtol", [("bf16x3", 1e-4), ("bf16x6", 1e-5)])
+def test_emulator_split_kernel_variants_agree(gpu, monkeypatch, precision, rtol):
+    """The split kernel's staging pipelines (LDS-DMA, the default, and register staging,
+    FV3_B3_STAGE=reg) and block shapes (8-wave and 4-wave blocks) run the same arithmetic in the same order per column:
+    bit-identical outputs on a ragged grid forced to 4 persistent blocks (every block
+    walks >= 4 tiles, so the cross-tile input DMA, the residual reads and the weight ring
+    wrap around), and within the oracle bound."""
     import torch
 
-    emu, raw = _emulator(ncol=2085, seed=11, precision="bf16x3")
+    emu, raw = _emulator(ncol=2085, seed=11, precision=precision)
     state = {k: torch.from_numpy(np.ascontiguousarray(v.T)).cuda() for k, v in raw.items()}
     monkeypatch.setenv("FV3_B3_GRID", "4")
-    monkeypatch.setenv("FV3_B3_STAGE", "glds")
-    glds = emu(state)
-    monkeypatch.setenv("FV3_B3_STAGE", "reg")
-    reg = emu(state)
+    runs = {}
+    for name, env in (("glds-w8", {"FV3_B3_STAGE": "glds", "FV3_B3_WAVES": "8"}),
+                      ("reg-w8", {"FV3_B3_STAGE": "reg", "FV3_B3_WAVES": "8"}),
+                      ("glds-w4", {"FV3_B3_STAGE": "glds", "FV3_B3_WAVES": "4"})):
+        for k in ("FV3_B3_STAGE", "FV3_B3_WAVES"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        runs[name] = emu(state)
     torch.cuda.synchronize()
-    for k in glds:
-        assert torch.equal(glds[k], reg[k]), k
-    _check_columns(reg, state, emu, np.arange(2085), 1e-4)
+    ref = runs.pop("glds-w8")
+    for name, out in runs.items():
+        for k in ref:
+            assert torch.equal(ref[k], out[k]), (name, k)
+    _check_columns(ref, state, emu, np.arange(2085), rtol)
 
 
 @pytest.mark.parametrize("precision,rtol,env", [("bf16x3", 1e-4, "FV3_B3_GRID"), ("bf16x6", 1e-5, "FV3_B3_GRID"),
