@@ -148,7 +148,7 @@ def count_sums_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def predict_mappm_worker(rank, world, port, out_dir, res, steps):
+def predict_mappm_worker(rank, world, port, out_dir, res, steps, precision="f32"):
     """north_star's predict + mappm (workloads.PredictMappmWorkload) on this rank's row
     band of one global C<res> state (gloo; ranks share the box's one GPU): the band's
     tendencies and remapped tendencies after ``steps`` steps."""
@@ -159,7 +159,7 @@ def predict_mappm_worker(rank, world, port, out_dir, res, steps):
 
     dist = init_gloo(rank, world, port)
     torch.cuda.set_device(0)
-    wl = W.make_predict_mappm_workload(res, rank, world, seed=3)
+    wl = W.make_predict_mappm_workload(res, rank, world, seed=3, precision=precision)
     for _ in range(steps):
         wl.step()
     torch.cuda.synchronize()

@@ -195,7 +195,8 @@ def test_gloo_count_sums_are_exact(tmp_path, world):
 
 
 @pytest.mark.gpu
-def test_sharded_predict_mappm_bit_identical_across_world_sizes(gpu, tmp_path):
+@pytest.mark.parametrize("precision", ["f32", "bf16x6"])
+def test_sharded_predict_mappm_bit_identical_across_world_sizes(gpu, tmp_path, precision):
     """north_star's predict + mappm sharded as 8(e) lays it out (row bands of one global
     state, no data-path exchange): at world 2 and 3 (gloo, processes sharing the GPU)
     each rank's band of tendencies and remapped tendencies equals the world-1 columns
@@ -203,7 +204,7 @@ def test_sharded_predict_mappm_bit_identical_across_world_sizes(gpu, tmp_path):
     res = 24
     for world in (1, 2, 3):
         (tmp_path / f"w{world}").mkdir()
-        _spawn(H.predict_mappm_worker, world, str(tmp_path / f"w{world}"), res, 2)
+        _spawn(H.predict_mappm_worker, world, str(tmp_path / f"w{world}"), res, 2, precision)
     one = np.load(tmp_path / "w1" / "out0.npy")
     assert np.isfinite(one).all()
     for world in (2, 3):
