@@ -529,6 +529,14 @@ def extra_measurements(dev, settle_ms=150.0):
         "columns_per_s": wl.ncol / (wall / 20), "ms_per_step": wall / 20 * 1e3,
         "note": "wall clock per step (several kernels + host glue); counters: the fused epilogue kernel"})
     del wl
+    # the same step with the predict on the bf16x6 split kernel (1e-5 per level like the
+    # f32 kernel); the float64 state is cast into bound float32 buffers each step
+    wl = W.make_stepper_workload(96, seed=11, device=dev, precision="bf16x6")
+    wall, t = timed_steps(wl.step, 20, 3, settle_ms=settle_ms)
+    out["stepper_c96_bf16x6"] = {
+        "columns_per_s": wl.ncol / (wall / 20), "ms_per_step": wall / 20 * 1e3, "precision": "bf16x6",
+        "note": "wall clock per step; predict on dense_b3_kernel<16,2,3,8> after two float64->float32 casts"}
+    del wl
     # config #5: Zhao-Carr microphysics emulator on a C384 state.  Its arithmetic is bf16
     # MFMA (1e-3 rel): the bf16x3 kernel (csrc/dense_b3.hip, 3 bf16 MFMAs per f32
     # product, so the bf16 roofline is priced at 3x the algorithmic FLOP); the exact-f32

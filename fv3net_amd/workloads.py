@@ -176,14 +176,23 @@ class StepperWorkload:
     ncol: int
     group: object = None
     bound: object = None
+    precision: str = "f32"
+    _in32: object = None
 
     def step(self):
         from .distributed import area_weighted_partials, combine_partials
         from .stepper import ml_epilogue
 
         T, q = self.state["air_temperature"], self.state["specific_humidity"]
-        if self.bound is None:  # validated once; float64 state read in place every step
-            self.bound = self.model.bind([T, q], level_axes=[1, 1])
+        if self.bound is None:  # validated once
+            if self.precision == "f32":  # the float64 state read in place every step
+                self.bound = self.model.bind([T, q], level_axes=[1, 1])
+            else:  # the split kernel reads float32: the state is cast into bound buffers each step
+                self._in32 = [T.to(torch.float32), q.to(torch.float32)]
+                self.bound = self.model.bind(self._in32, level_axes=[1, 1], precision=self.precision)
+        if self._in32 is not None:
+            self._in32[0].copy_(T)
+            self._in32[1].copy_(q)
         dq1, dq2 = self.bound()
         res = ml_epilogue(dq1, dq2, q, self.state["pressure_thickness_of_atmospheric_layer"], T, self.dt,
                           self.state["total_precipitation"], in_place=True, level_axis=1)
@@ -194,7 +203,7 @@ class StepperWorkload:
         return combine_partials(part, self.group)
 
 
-def make_stepper_workload(res: int = 96, seed: int = 0, device=None, group=None):
+def make_stepper_workload(res: int = 96, seed: int = 0, device=None, group=None, precision: str = "f32"):
     device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
     g = torch.Generator(device=device)
     g.manual_seed(seed)
@@ -218,7 +227,7 @@ def make_stepper_workload(res: int = 96, seed: int = 0, device=None, group=None)
                   rng.normal(0.0, 3e-8, sample_T.shape).astype(np.float32)]
     model = DenseColumnModel.random(dense_2x256_config(), seed=1, sample_inputs=[sample_T, sample_q],
                                     sample_outputs=sample_out)
-    return StepperWorkload(model, state, area, 900.0, 6 * res * res, group)
+    return StepperWorkload(model, state, area, 900.0, 6 * res * res, group, precision=precision)
 
 
 @dataclasses.dataclass

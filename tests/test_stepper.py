@@ -129,6 +129,30 @@ def test_stepper_workload_step(gpu):
 
 
 @pytest.mark.gpu
+def test_stepper_workload_bf16x6_predict(gpu):
+    """The config #4 step with the predict on the bf16x6 split kernel (the float64 state
+    cast into bound float32 buffers each step): its tendencies agree with the exact-f32
+    kernel's to 2e-5 per level (each within 1e-5 of the float64 graph), and two steps
+    re-read the updated state."""
+    import torch
+
+    from fv3net_amd import workloads as W
+    from tests.parity import assert_per_level
+
+    a = W.make_stepper_workload(12, seed=2)
+    b = W.make_stepper_workload(12, seed=2, precision="bf16x6")
+    for _ in range(2):
+        sa, sb = a.step(), b.step()
+        torch.cuda.synchronize()
+        for ta, tb in zip(a.bound.outputs, b.bound.outputs):
+            ref = ta.permute(1, 0, 2, 3).reshape(ta.shape[1], -1).T.double().cpu().numpy()
+            got = tb.permute(1, 0, 2, 3).reshape(tb.shape[1], -1).T.double().cpu().numpy()
+            assert_per_level(got, ref, 2e-5, "bf16x6 vs f32 tendencies")
+        assert torch.isfinite(sb).all() and torch.isfinite(sa).all()
+    assert (b.state["specific_humidity"] >= -1e-15).all()
+
+
+@pytest.mark.gpu
 def test_pure_ml_stepper_mirror(gpu):
     """PureMLStepper (machine_learning.py:239-315) over a DenseColumnPredictor: the
     tendencies/diagnostics equal the oracle epilogue applied to the model's own
