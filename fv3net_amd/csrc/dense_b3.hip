@@ -1,4 +1,5 @@
-// fv3net_amd — fused column-wise dense predict on bf16 MFMA with a 3-term split ("bf16x3").
+// fv3net_amd — fused column-wise dense predict on bf16 MFMA with split operands:
+// "bf16x3" (2 parts per operand, 3 MFMAs per product) and "bf16x6" (3 parts, 6 MFMAs).
 //
 // Same graph and boundary as dense.hip (the DenseModel of external/fv3fit/fv3fit/keras/
 // _models/dense.py:234-305 and the microphysics emulator's MLP, external/fv3fit/fv3fit/
@@ -12,6 +13,10 @@
 // operand: ~1e-5 rel against the float64 graph on the 2x256 DenseModel and the Zhao-Carr
 // emulator (plain bf16: 4.7e-3, outside BASELINE config #5's 1e-3).  Three bf16 MFMAs
 // cost 48 cycles per 16x16x32 block against 256 for exact f32, ~5.3x the f32 MFMA rate.
+// bf16x6 adds a third part (mid) and takes the six products of order <= 2 (SplitTerms):
+// ~24 bits per operand, held to the f32 kernel's 1e-5 per-level bound, 96 cycles per
+// block (2.7x the f32 rate); its 48 KiB chunks run a 2-slot LDS-DMA ring.
+// Grids with fewer 128-column tiles than CUs run 4-wave blocks of 64 columns (NWV = 4).
 //
 // Mapping (one 512-thread block per CU, 2 waves per SIMD, persistent over column tiles):
 //  * a block tile is 128 columns; wave w owns columns [16w, 16w+16) for the WHOLE network,
