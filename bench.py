@@ -277,6 +277,90 @@ def scaling_legs(dev, dist, rank, world, settle_ms=150.0):
     return out
 
 
+def rank_share_legs(dev, settle_ms=150.0, world=8):
+    """One rank's share of the 8-GPU target decompositions, run on this one GPU
+    (runtime/segmented_run/run.py:34-46 gives every rank its own
+    subdomain, runtime/metrics.py:18-32 is the per-step exchange): rank 0's band of the
+    flattened (tile, y) rows, each beside the full grid on the same GPU.
+    ``ratio_to_full_over_world`` = share time / (full-grid time / world): 1.0 is perfect
+    strong scaling of the per-GPU work; above 1 is where the 8-GPU curve flattens (the
+    smaller grid fills the 256 CUs less well, or fixed per-launch costs dominate)."""
+    import torch
+
+    from fv3net_amd import workloads as W
+
+    def kernel_time(fn, n):
+        _, t = timed_steps(fn, n, 3, settle_ms=settle_ms)
+        return t
+
+    out = {}
+    # config #4: C96 stepper, 6,912 columns per rank at world 8; the exchange (all-gather of
+    # the row partials + all-reduce of the limiter counts) stubbed by a local copy
+    rec = {}
+    for w in (1, world):
+        wl = W.make_sharded_stepper_workload(96, 0, w, seed=11, device=dev, stub_exchange=True)
+        steps = 30
+        wall, _ = timed_steps(wl.step, steps, 3, settle_ms=settle_ms)
+        tp = kernel_time(wl.bound, 30)  # the step's predict alone (float64 state read in place)
+        rec[w] = {"ncol": wl.ncol, "step_ms": wall / steps * 1e3, "predict_ms": tp * 1e3,
+                  "predict_frac_f32_mfma_peak": wl.ncol * wl.model.config.flops_per_column() / tp / 1e12
+                  / W.FP32_MFMA_PEAK_TFLOPS, "exchange_bytes": wl.exchange_bytes}
+        del wl
+    out["stepper_c96_rank_of_8"] = {
+        "columns_per_rank": rec[world]["ncol"], "ms_per_step": rec[world]["step_ms"],
+        "columns_per_s_per_gpu": rec[world]["ncol"] / (rec[world]["step_ms"] * 1e-3),
+        "predict_ms": rec[world]["predict_ms"], "predict_frac_f32_mfma_peak": rec[world]["predict_frac_f32_mfma_peak"],
+        "full_grid_ms_per_step": rec[1]["step_ms"], "full_grid_predict_ms": rec[1]["predict_ms"],
+        "ratio_to_full_over_world": rec[world]["step_ms"] / (rec[1]["step_ms"] / world),
+        "predict_ratio_to_full_over_world": rec[world]["predict_ms"] / (rec[1]["predict_ms"] / world),
+        "exchange_bytes_per_rank_per_step": rec[world]["exchange_bytes"],
+        "note": "wall clock per step (predict + fused epilogue + row partials + fold); exchange stubbed by a local "
+                "copy of the gathered bytes"}
+    # config #5: C384 emulator, 110,592 columns per rank at world 8
+    for prec in ("bf16x3", "f32"):
+        rec = {}
+        for w in (1, world):
+            wl = W.make_emulator_workload(384, seed=13, device=dev, precision=prec, world=w)
+            t = kernel_time(wl.step, 10)
+            tf = wl.ncol * wl.flops_per_column / t / 1e12
+            rec[w] = {"ncol": wl.ncol, "ms": t * 1e3,
+                      "frac": (3 * tf / W.BF16_MFMA_PEAK_TFLOPS) if prec == "bf16x3" else tf / W.FP32_MFMA_PEAK_TFLOPS}
+            del wl
+        key = "frac_bf16_mfma_peak" if prec == "bf16x3" else "frac_f32_mfma_peak"
+        out[f"emulator_c384_rank_of_8{'' if prec == 'bf16x3' else '_f32'}"] = {
+            "columns_per_rank": rec[world]["ncol"], "ms_per_step": rec[world]["ms"], key: rec[world]["frac"],
+            "columns_per_s_per_gpu": rec[world]["ncol"] / (rec[world]["ms"] * 1e-3), "precision": prec,
+            "full_grid_ms": rec[1]["ms"], f"full_grid_{key}": rec[1]["frac"],
+            "ratio_to_full_over_world": rec[world]["ms"] / (rec[1]["ms"] / world)}
+    # north_star's predict + mappm at C384 over 8: 110,592 columns per rank
+    for prec in ("f32", "bf16x6"):
+        rec = {}
+        for w in (1, world):
+            wl = W.make_predict_mappm_workload(384, 0, w, seed=21, device=dev, precision=prec)
+            wl.step()
+            t = kernel_time(wl.step, 10)
+            td = kernel_time(wl._bound, 10)
+            tm = kernel_time(wl._plans, 10)
+            tf = wl.ncol * wl.flops_per_column / td / 1e12
+            rec[w] = {"ncol": wl.ncol, "ms": t * 1e3, "dense_ms": td * 1e3, "mappm_ms": tm * 1e3,
+                      "dense_frac": tf / W.FP32_MFMA_PEAK_TFLOPS if prec == "f32" else 6 * tf / W.BF16_MFMA_PEAK_TFLOPS}
+            del wl
+        key = "dense_frac_f32_mfma_peak" if prec == "f32" else "dense_frac_bf16_mfma_peak"
+        out[f"predict_mappm_c384_rank_of_8{'' if prec == 'f32' else '_bf16x6'}"] = {
+            "columns_per_rank": rec[world]["ncol"], "ms_per_step": rec[world]["ms"],
+            "columns_per_s_per_gpu": rec[world]["ncol"] / (rec[world]["ms"] * 1e-3), "precision": prec,
+            "dense_ms": rec[world]["dense_ms"], "mappm_ms": rec[world]["mappm_ms"], key: rec[world]["dense_frac"],
+            "full_grid_ms": rec[1]["ms"], "full_grid_dense_ms": rec[1]["dense_ms"],
+            "full_grid_mappm_ms": rec[1]["mappm_ms"],
+            "ratio_to_full_over_world": rec[world]["ms"] / (rec[1]["ms"] / world),
+            "dense_ratio_to_full_over_world": rec[world]["dense_ms"] / (rec[1]["dense_ms"] / world),
+            "mappm_ratio_to_full_over_world": rec[world]["mappm_ms"] / (rec[1]["mappm_ms"] / world)}
+    for k in out:
+        out[k] = with_counters(k, out[k])
+    torch.cuda.empty_cache()
+    return out
+
+
 def host_to_host(dev, res, steps=10):
     """The reference's boundary crossing: float64 host (numpy) T/q in, H2D through the
     product's pinned double-buffered staging (fv3net_amd/transfer.py), the fused
@@ -433,8 +517,18 @@ def reference_mappm_cpu_procs(procs=8, seconds=5.0):
         pe2 = np.concatenate([np.full((1, n), 300.0, np.float32), 300.0 + np.cumsum(d2, 0, dtype=np.float32)])
         q = rng.normal(250.0, 10.0, (79, n)).astype(np.float32)
         jobs.append((pe1, q, pe2, seconds))
-    with mp.get_context("spawn").Pool(procs) as pool:
+    # close + join (not the context manager's terminate()): the workers finish their own
+    # interpreter shutdown, so no SIGTERM lands in a finalising worker (a profiler run
+    # would log those as "Aborted")
+    pool = mp.get_context("spawn").Pool(procs)
+    try:
         res = pool.map(_ref_mappm_worker, jobs)
+        pool.close()
+    except BaseException:
+        pool.terminate()
+        raise
+    finally:
+        pool.join()
     cols = sum(c for c, _ in res)
     dt = max(t for _, t in res)
     return {"value": cols / dt, "unit": "columns/s", "cores": procs, "kind": "reference",
@@ -594,6 +688,7 @@ def extra_measurements(dev, settle_ms=150.0):
     out["dense_c48_rank_call_host_to_host"] = rank_call_host_to_host(dev)
     out["predict_mappm_c384_host_to_host"] = predict_mappm_host_to_host(dev)
     torch.cuda.empty_cache()
+    out.update(rank_share_legs(dev, settle_ms))
     return out
 
 

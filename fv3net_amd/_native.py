@@ -19,6 +19,7 @@ FV3_ERR_UNSUPPORTED = 3
 EXPORTED_SYMBOLS = (
     "fv3_last_error",
     "fv3_abi_version",
+    "fv3_build_kind",
     "fv3_mappm",
     "fv3_mappm_ex",
     "fv3_mappm_multi",
@@ -73,7 +74,7 @@ EXPORTED_SYMBOLS = (
     "fv3_scale_levels",
     "fv3_adapter_apply",
 )
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # fv3_dense_forward_ex precisions
 DENSE_F32 = 0
@@ -159,6 +160,8 @@ class AdapterTarget(ctypes.Structure):
         ("n_preds", ctypes.c_int),
         ("state", ctypes.c_void_p),
         ("out", ctypes.c_void_p),
+        ("pred_f64", ctypes.c_uint),
+        ("out_f64", ctypes.c_int),
     ]
 
 
@@ -174,6 +177,7 @@ _D = ctypes.c_double
 _SIGNATURES = {
     "fv3_last_error": (ctypes.c_char_p, []),
     "fv3_abi_version": (_I, []),
+    "fv3_build_kind": (ctypes.c_char_p, []),
     "fv3_mappm": (_I, [_P, _P, _P, _P, _I64, _I, _I, _I, _I, _F, _P]),
     "fv3_mappm_ex": (_I, [_P, Layout, _P, Layout, _P, Layout, _P, Layout, _I64, _I, _I, _I, _I, _F, _P]),
     "fv3_mappm_multi": (_I, [_P, Layout, ctypes.POINTER(_P), ctypes.POINTER(Layout), _P, Layout, ctypes.POINTER(_P),
@@ -271,6 +275,10 @@ def load():
             fn.argtypes = args
         if lib.fv3_abi_version() != ABI_VERSION:
             raise NativeLibraryError("fv3net_amd ABI version mismatch: rebuild the extension")
+        if path == LIB and lib.fv3_build_kind() != b"product":
+            # experiment variants (results invalid by construction) load only when named
+            # explicitly through FV3NET_AMD_LIB
+            raise NativeLibraryError(f"{path} is not a product build: rebuild with fv3net_amd/build.py")
         _lib = lib
     return _lib
 

@@ -9,6 +9,7 @@ import concurrent.futures
 import glob
 import hashlib
 import os
+import re
 import subprocess
 
 PKG = os.path.dirname(os.path.abspath(__file__))
@@ -22,8 +23,24 @@ ARCH = os.environ.get("FV3_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: one rounding per operation, required for bit parity of the
 # mappm / coarsen paths with the x86 reference build (no FMA there).
-CFLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", f"--offload-arch={ARCH}"]
+# FV3_PRODUCT_BUILD: csrc/common.h refuses every experiment knob (FV3_EXP_*, results
+# invalid by construction) in this build; those compile only in tools/ variant builds.
+CFLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", f"--offload-arch={ARCH}", "-DFV3_PRODUCT_BUILD"]
 FLAGS = CFLAGS + ["-shared"]
+# environment variables hipcc / clang read extra flags from
+FLAG_ENV = ("HIPCC_COMPILE_FLAGS_APPEND", "HIPCC_LINK_FLAGS_APPEND", "HIPFLAGS", "CXXFLAGS", "CPPFLAGS")
+_EXP = re.compile(r"FV3_\w*EXP|FV3_EXPERIMENT")
+
+
+def check_product_flags(flags=None, env=None) -> None:
+    """Refuse an experiment knob anywhere in the product build's flags."""
+    env = os.environ if env is None else env
+    texts = [" ".join(CFLAGS if flags is None else flags)] + [env.get(k, "") for k in FLAG_ENV]
+    for t in texts:
+        m = _EXP.search(t)
+        if m:
+            raise RuntimeError(f"experiment knob {m.group(0)!r} in the product build flags: build variants with "
+                               "tools/build_*variant.sh")
 
 
 def sources():
@@ -64,6 +81,7 @@ def _compile(src, obj, verbose):
 
 def build(force: bool = False, verbose: bool = False) -> str:
     """Compile the extension if sources changed; returns the library path."""
+    check_product_flags()
     os.makedirs(OBJ_DIR, exist_ok=True)
     stamp = LIB + ".sha256"
     digest = _digest()

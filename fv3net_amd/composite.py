@@ -203,7 +203,7 @@ class EnsembleModel(Predictor):
         for t in members[1:]:
             if t.shape != members[0].shape:
                 raise ValueError(f"ensemble members disagree in shape: {tuple(t.shape)} vs {tuple(members[0].shape)}")
-        op = _native.REDUCE_MEDIAN if reduction.lower() == "median" else _native.REDUCE_MEAN
+        op = _native.REDUCE_MEDIAN if reduction == "median" else _native.REDUCE_MEAN
         out = torch.empty_like(members[0])
         ptrs = (ctypes.c_void_p * len(members))(*[t.data_ptr() for t in members])
         st = _native.load().fv3_member_reduce(ptrs, len(members), out.numel(), int(dtype == torch.float64), op,

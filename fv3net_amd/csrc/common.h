@@ -10,6 +10,25 @@
 
 #include "../../include/fv3net_amd.h"
 
+// Experiment knobs (FV3_EXP_* / FV3_B3_EXP_*) replace parts of a kernel to price them
+// (no MFMAs, no loads, ...): their results are invalid by construction.  They compile
+// only in the tools/ variant builds (tools/build_*variant.sh, which define
+// FV3_EXPERIMENT_BUILD and write tools/variants/, never fv3net_amd/_lib/).  The product
+// library is built by fv3net_amd/build.py with FV3_PRODUCT_BUILD, and any knob there is
+// a compile error.  tests/test_build_flags.py checks that every knob named in csrc/ is
+// listed here.
+#if defined(FV3_EXP_L1_WEIGHTS) || defined(FV3_EXP_NOINLOAD) || defined(FV3_EXP_NOMFMA) ||         \
+    defined(FV3_EXP_NONORM) || defined(FV3_EXP_NOPPM) || defined(FV3_EXP_NOPROFILE) ||             \
+    defined(FV3_EXP_NOREMAP) || defined(FV3_EXP_NOSTAGE) || defined(FV3_EXP_NOSTORE) ||            \
+    defined(FV3_EXP_NOWLOAD) || defined(FV3_B3_EXP_NOFRAG) || defined(FV3_B3_EXP_NOIN) ||          \
+    defined(FV3_B3_EXP_NOMFMA) || defined(FV3_B3_EXP_NOOUT) || defined(FV3_B3_EXP_NOSTAGE) ||      \
+    defined(FV3_EXPERIMENT_BUILD)
+#define FV3_EXPERIMENT_KNOBS 1
+#ifdef FV3_PRODUCT_BUILD
+#error "experiment knobs (results invalid) in the product build"
+#endif
+#endif
+
 namespace fv3 {
 
 void set_error(const char* fmt, ...);

@@ -104,56 +104,84 @@ __global__ __launch_bounds__(256) void scale_levels_kernel(ScaleArgs<T> a)
         a.out[(int64_t)k * a.ncol + c] = a.s[k] * (double)a.x[off + (int64_t)k * a.lay.ld];
 }
 
-template <typename DT>
 struct AdapterArgs {
     fv3_adapter_target t[FV3_ADAPTER_MAX_TARGETS];
-    int nt, limit, q_index, t_index;
+    int nt, limit, q_index, t_index, state_f64;
     int64_t n;
     double dt;
 };
 
-template <typename DT>
-__device__ __forceinline__ float tendency_sum(const fv3_adapter_target& t, int64_t i)
+// numpy's dtype flow in double arithmetic: a float32 intermediate is the double result
+// rounded to float (exact for + - * / of float32 operands: 53 >= 2 * 24 + 2 bits, so the
+// double rounding is innocuous), a Python-float constant takes the array operand's dtype
+// (NumPy weak scalars)
+__device__ __forceinline__ double as_dtype(double x, bool f64) { return f64 ? x : (double)(float)x; }
+
+__device__ __forceinline__ double load_as(const void* p, bool f64, int64_t i)
 {
-    // sum([prediction[item] for item in v]): Python's sum starts from the integer 0
-    float s = 0.0f;
-    for (int p = 0; p < t.n_preds; ++p) s = s + t.preds[p][i];
+    return f64 ? static_cast<const double*>(p)[i] : (double)static_cast<const float*>(p)[i];
+}
+
+// sum([prediction[item] for item in v]): Python's sum starts from the integer 0, so the
+// first term fixes the dtype (0 + -0.0 = +0.0) and the sum widens at the first float64
+// term (xarray aligns, numpy promotes pairwise in order)
+__device__ __forceinline__ double tendency_sum(const fv3_adapter_target& t, int64_t i, bool& wide)
+{
+    wide = t.pred_f64 & 1u;
+    double s = 0.0 + load_as(t.preds[0], wide, i);
+    for (int p = 1; p < t.n_preds; ++p) {
+        const bool w = (t.pred_f64 >> p) & 1u;
+        wide = wide || w;
+        s = as_dtype(s + load_as(t.preds[p], w, i), wide);
+    }
     return s;
 }
 
-template <typename DT>
-__global__ __launch_bounds__(256) void adapter_apply_kernel(AdapterArgs<DT> a)
+__global__ __launch_bounds__(256) void adapter_apply_kernel(AdapterArgs a)
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    const float dtf = (float)a.dt;  // float32 tendency * Python float -> float32
-    const DT dtd = (DT)a.dt;
-    const float cvf = (float)(kCp - kRdgas), lvf = (float)kLv;
-    const DT cv = (DT)(kCp - kRdgas), lv = (DT)kLv;
+    const double cv = kCp - kRdgas, lv = kLv, dt = a.dt;
+    const bool sw = a.state_f64 != 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-        float q2 = 0.0f;
-        DT q2n = 0;
+        double q2 = 0.0, q2n = 0.0;
+        bool wq = false;
         if (a.limit) {
-            // update_moisture_tendency_to_ensure_non_negative_humidity (machine_learning.py:77-80)
+            // update_moisture_tendency_to_ensure_non_negative_humidity (machine_learning.py:77-80):
+            // xr.where(sphum + q2 * dt >= 0, q2, -sphum / dt), dtype promote(q2, sphum)
             const fv3_adapter_target& tq = a.t[a.q_index];
-            q2 = tendency_sum<DT>(tq, i);
-            const DT sp = static_cast<const DT*>(tq.state)[i];
-            q2n = (sp + (DT)(q2 * dtf) >= (DT)0) ? (DT)q2 : (-sp) / dtd;
+            q2 = tendency_sum(tq, i, wq);
+            const double sp = load_as(tq.state, sw, i);
+            const double step = as_dtype(q2 * as_dtype(dt, wq), wq);
+            q2n = (as_dtype(sp + step, wq || sw) >= 0.0) ? q2 : as_dtype((-sp) / as_dtype(dt, sw), sw);
         }
         for (int g = 0; g < a.nt; ++g) {
             const fv3_adapter_target& t = a.t[g];
-            const DT x = static_cast<const DT*>(t.state)[i];
-            DT y;
+            const double x = load_as(t.state, sw, i);
+            double tend;
+            bool wt;
             if (a.limit && g == a.q_index) {
-                y = x + q2n * dtd;
+                tend = q2n, wt = wq || sw;
             } else if (a.limit && g == a.t_index) {
-                // update_temperature_tendency_to_conserve_mse (:83-88): moist static energy
-                // tendency in float32, the new temperature tendency in the state's dtype
-                const float m = cvf * tendency_sum<DT>(t, i) + lvf * q2;
-                y = x + (((DT)m - lv * q2n) / cv) * dtd;
+                // update_temperature_tendency_to_conserve_mse (:83-88): vcm
+                // moist_static_energy_tendency (cv * q1 + lv * q2) and temperature_tendency
+                // ((mse - lv * q2_new) / cv)
+                bool w1;
+                const double q1 = tendency_sum(t, i, w1);
+                const bool wm = w1 || wq, wn = wq || sw;
+                const double mse = as_dtype(as_dtype(as_dtype(cv, w1) * q1, w1) + as_dtype(as_dtype(lv, wq) * q2, wq), wm);
+                const double lq = as_dtype(as_dtype(lv, wn) * q2n, wn);
+                wt = wm || wn;
+                tend = as_dtype(as_dtype(mse - lq, wt) / as_dtype(cv, wt), wt);
             } else {
-                y = x + (DT)(tendency_sum<DT>(t, i) * dtf);
+                tend = tendency_sum(t, i, wt);
             }
-            static_cast<DT*>(t.out)[i] = y;
+            // inputs[name] + tendency * timestep
+            const bool wo = wt || sw;
+            const double y = as_dtype(x + as_dtype(tend * as_dtype(dt, wt), wt), wo);
+            if (wo)
+                static_cast<double*>(t.out)[i] = y;
+            else
+                static_cast<float*>(t.out)[i] = (float)y;
         }
     }
 }
@@ -230,6 +258,7 @@ extern "C" int fv3_adapter_apply(const fv3_adapter_target* targets, int n_target
                          "predicted.");
         FV3_REQUIRE(temp_target < n_targets && temp_target != sphum_target, "adapter_apply: bad temperature target");
     }
+    auto wide = [&](int g) { return (targets[g].pred_f64 & ((1u << targets[g].n_preds) - 1u)) != 0u; };
     for (int g = 0; g < n_targets; ++g) {
         const fv3_adapter_target& t = targets[g];
         FV3_REQUIRE(t.n_preds >= 1 && t.n_preds <= FV3_ADAPTER_MAX_PREDS, "adapter_apply: target %d has %d "
@@ -237,22 +266,21 @@ extern "C" int fv3_adapter_apply(const fv3_adapter_target* targets, int n_target
         FV3_REQUIRE(t.state && t.out, "adapter_apply: target %d: NULL state or output", g);
         for (int p = 0; p < t.n_preds; ++p) FV3_REQUIRE(t.preds[p], "adapter_apply: target %d: NULL prediction", g);
     }
-    if (n == 0) return FV3_OK;
-    const unsigned grid = elementwise_grid(n);
-    auto fill = [&](auto& a) {
-        for (int g = 0; g < n_targets; ++g) a.t[g] = targets[g];
-        a.nt = n_targets, a.limit = limit != 0, a.q_index = limit ? sphum_target : -1;
-        a.t_index = limit ? temp_target : -1, a.n = n, a.dt = dt;
-    };
-    if (state_f64) {
-        AdapterArgs<double> a{};
-        fill(a);
-        hipLaunchKernelGGL(adapter_apply_kernel<double>, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
-    } else {
-        AdapterArgs<float> a{};
-        fill(a);
-        hipLaunchKernelGGL(adapter_apply_kernel<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+    for (int g = 0; g < n_targets; ++g) {
+        // the output's numpy dtype: state + tendency * dt, the limited tendencies promoted
+        // with the humidity state and, for temperature, with the humidity tendency
+        bool wt = wide(g);
+        if (limit && (g == sphum_target || g == temp_target)) wt = wt || wide(sphum_target) || state_f64;
+        const bool wo = wt || state_f64;
+        FV3_REQUIRE((targets[g].out_f64 != 0) == wo, "adapter_apply: target %d output must be float%d", g,
+                    wo ? 64 : 32);
     }
+    if (n == 0) return FV3_OK;
+    AdapterArgs a{};
+    for (int g = 0; g < n_targets; ++g) a.t[g] = targets[g];
+    a.nt = n_targets, a.limit = limit != 0, a.q_index = limit ? sphum_target : -1;
+    a.t_index = limit ? temp_target : -1, a.n = n, a.dt = dt, a.state_f64 = state_f64 != 0;
+    hipLaunchKernelGGL(adapter_apply_kernel, dim3(elementwise_grid(n)), dim3(256), 0, (hipStream_t)stream, a);
     FV3_LAUNCH_CHECK();
     return FV3_OK;
 }

@@ -129,18 +129,13 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c)
 #endif
 }
 
-// the tile loop's workgroup barriers (FV3_EXP_NOBARRIER, experiment only: none)
+// the tile loop's workgroup barriers
 // Only LDS traffic is ordered by these barriers (staged inputs, activations, constants):
 // wait for this wave's LDS operations, then s_barrier.  Global loads in flight (the next
 // tile's inputs, the weight rings) are NOT drained, as __syncthreads() would (vmcnt(0)).
 __device__ __forceinline__ void tile_sync()
 {
-#if defined(FV3_EXP_NOBARRIER)
-#elif defined(FV3_EXP_OLDBAR)
-    __syncthreads();
-#else
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
 }
 
 // column data: plain loads / stores.  Measured (tools/et_ab.sh): nontemporal input
@@ -568,15 +563,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
     const int voff_o = lane * 16;                           // output-layer fragments
     constexpr int KS = NT * sizeof(FT);
     FT g1[RD][4];
-#ifdef FV3_EXP_OLDPROLOG
-    if (tile < p.ntiles) load_raw(p, tile, fq0);
-    prime_ring<RD, NW, FT>(g1, rw, voff, p.w1_off);
-    for (int i = threadIdx.x; i < p.kp; i += NT) {
-        s_mean[i] = p.in_mean[i];
-        s_denom[i] = p.in_denom[i];
-    }
-    for (int i = threadIdx.x; i < 6 * kop; i += NT) s_ep[i] = p.oep[i];
-#else
     // loads complete in issue order (one vmcnt counter): the constants and the layer-1
     // ring go first, so writing the constants to LDS and the first MFMAs do not wait
     // for the tile's inputs (HBM), which are issued last
@@ -615,7 +601,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         }
         for (int i = threadIdx.x + NT * NE; i < 6 * kop; i += NT) s_ep[i] = p.oep[i];
     }
-#endif
     for (int i = threadIdx.x; i < (1 + p.n_hidden_extra) * HP; i += NT) s_bias[i] = i < HP ? p.b1[i] : p.bh[i - HP];
 
     // output plan of this wave.  The first (n_otiles / NW) * NW output tiles go whole to
@@ -1113,13 +1098,12 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
     a.n_otiles = m->n_otiles;
     a.kp = m->kp;
     a.in_steps_total = m->steps_total;
-    if (const int st = b3_pack(m, d)) {  // the bf16x3 weight stream (fv3_dense_forward_ex)
+    // the bf16x3 / bf16x6 weight streams (fv3_dense_forward_ex); a model a split stream
+    // cannot hold still runs in exact f32 (b3_pack leaves that precision unsupported)
+    if (const int st = b3_pack(m, d)) {
         b3_free(m);
-        if (st != FV3_ERR_UNSUPPORTED) {
-            (void)hipFree(m->dbuf);
-            return st;
-        }
-        clear_error();  // a model the bf16x3 kernel cannot pack still runs in exact f32
+        (void)hipFree(m->dbuf);
+        return st;
     }
     *out = guard.release();
     return FV3_OK;
@@ -1214,8 +1198,11 @@ static int dense_forward_impl(const fv3_dense_model* m, const void* const* input
         return hb + xb + sizeof(float) * (2 * (size_t)m->kp + 6 * 16 * (size_t)m->n_otiles) + 16 +
                sizeof(float) * (1 + (size_t)m->tmpl.n_hidden_extra) * 16 * (size_t)m->ht;
     };
-    int nc = wide && (m->w1_off8 < 0 || lds_of(2) > 160 * 1024) ? 1 : 2;
-    if (const char* e = getenv("FV3_DENSE_NC")) nc = atoi(e) == 1 ? 1 : 2;
+    // any model whose 32-column tiles do not fit the LDS (deep models hold ~1 KiB of
+    // biases per hidden layer at width 256) runs 16-column tiles
+    const bool fits2 = lds_of(2) <= 160 * 1024;
+    int nc = (wide && m->w1_off8 < 0) || !fits2 ? 1 : 2;
+    if (const char* e = getenv("FV3_DENSE_NC")) nc = atoi(e) == 1 || !fits2 ? 1 : 2;
     // waves per block: 8, two per SIMD on one tile and each wave half the hidden units,
     // measured faster than 4 at every size after the staging work (C48 42.8 vs 47.9 us,
     // C96 141 vs 147 us, C384 2.15 vs 2.18 ms).  Needs 32-column tiles and width >= 128.

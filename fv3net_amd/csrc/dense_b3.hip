@@ -446,13 +446,9 @@ dense_b3_kernel(B3Args pa)
 #ifdef FV3_B3_EXP_NOIN  // experiment only (results invalid): no input loads
             const float x = 1.0f + (float)(uintptr_t)(ptr + (j < nv ? j * ld : 0)) * 0.0f;
 #else
-#ifdef FV3_B3_EXP_NT_IN  // A/B: nontemporal input loads (round 2's default)
-            const float x = __builtin_nontemporal_load(ptr + (j < nv ? j * ld : 0));
-#else
             // plain (cacheable) loads: the residual outputs re-read T / q / qc one tile
             // later (emulator C384 2.55 -> 2.36 ms against nontemporal loads, round 3)
             const float x = ptr[j < nv ? j * ld : 0];
-#endif
 #endif
             raw[j] = j < nv ? x : 0.0f;
         }
@@ -925,10 +921,22 @@ static int pack_ns(fv3_dense_model* m, const fv3_dense_desc* d, int NS, B3Pack**
     return FV3_OK;
 }
 
+// Each split stream is packed on its own: a model one of them cannot hold (too many
+// input features or output rows, a stream past 2 GiB) leaves only that precision
+// unsupported (fv3_dense_forward_ex returns FV3_ERR_UNSUPPORTED for it), and the exact-f32
+// path is never affected.  Only a HIP failure fails fv3_dense_create.
 int b3_pack(fv3_dense_model* m, const fv3_dense_desc* d)
 {
-    if (const int st = pack_ns(m, d, 2, &m->b3)) return st;
-    return pack_ns(m, d, 3, &m->b6);
+    for (int ns : {2, 3}) {
+        B3Pack** dst = ns == 2 ? &m->b3 : &m->b6;
+        const int st = pack_ns(m, d, ns, dst);
+        if (st == FV3_ERR_HIP) return st;
+        if (st != FV3_OK) {
+            *dst = nullptr;
+            clear_error();
+        }
+    }
+    return FV3_OK;
 }
 
 void b3_free(fv3_dense_model* m)

@@ -20,4 +20,12 @@ void clear_error() { g_err[0] = 0; }
 }  // namespace fv3
 
 extern "C" const char* fv3_last_error(void) { return g_err; }
-extern "C" int fv3_abi_version(void) { return 4; }
+extern "C" int fv3_abi_version(void) { return 5; }
+
+// "product": built by fv3net_amd/build.py with FV3_PRODUCT_BUILD and no experiment knob
+// (common.h refuses one); anything else is a tools/ variant.
+#if defined(FV3_PRODUCT_BUILD) && !defined(FV3_EXPERIMENT_KNOBS)
+extern "C" const char* fv3_build_kind(void) { return "product"; }
+#else
+extern "C" const char* fv3_build_kind(void) { return "experiment"; }
+#endif

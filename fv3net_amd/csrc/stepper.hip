@@ -70,10 +70,7 @@ __global__ __launch_bounds__(64) void ml_epilogue_kernel(EpilogueArgs<DT> a)
     // flight per thread set the HBM rate.  The explicit batches also keep the loads
     // ahead of the stores, which the compiler may not reorder itself since temp_out /
     // sphum_out may alias temp / sphum.  The z sums stay in level order.
-#ifndef FV3_EXP_EPI_U
-#define FV3_EXP_EPI_U 8
-#endif
-    constexpr int U = FV3_EXP_EPI_U;
+    constexpr int U = 8;
     float b_q1[2][U], b_q2[2][U];
     DT b_sp[2][U], b_dp[2][U], b_t[2][U];
     const bool want_t = a.temp_out != nullptr;

@@ -55,6 +55,15 @@ def _data(x):
     return getattr(x, "data", x)
 
 
+def _prediction_on_device(x, dev):
+    """A prediction as a contiguous device array in its own dtype when that is float64
+    (a TaperedModel / float64 ensemble returns float64) and float32 otherwise."""
+    t = x if torch.is_tensor(x) else torch.from_numpy(np.ascontiguousarray(np.asarray(x)))
+    if t.dtype == torch.float64:
+        return t.to(dev).contiguous()
+    return _device.to_device_f32(t)
+
+
 class Adapter:
     """transformers/fv3fit.py:53-109 (``predict`` / ``apply`` / ``partial_fit`` /
     ``input_variables``); ``models`` may be given directly instead of loaded from
@@ -127,21 +136,30 @@ class Adapter:
                 da = prediction[item]  # KeyError if the model does not predict it
                 if sdims is not None and tuple(da.dims) != sdims:
                     da = da.transpose(*sdims)  # xarray aligns the sum by dim name
-                pt = _device.to_device_f32(_data(da))
+                pt = _prediction_on_device(_data(da), dev)  # float64 predictions stay float64
                 if tuple(pt.shape) != tuple(st.shape):
                     raise ValueError(f"prediction {item} shape {tuple(pt.shape)} != state {name} "
                                      f"{tuple(st.shape)}")
                 keep.append(pt)
                 targets[g].preds[p] = pt.data_ptr()
+                if pt.dtype == torch.float64:
+                    targets[g].pred_f64 |= 1 << p
             targets[g].n_preds = len(items)
-            out = torch.empty_like(st)
-            outs[name] = out
             targets[g].state = st.data_ptr()
-            targets[g].out = out.data_ptr()
         if len(names) > _native.ADAPTER_MAX_TARGETS:
             raise NotImplementedError(f"at most {_native.ADAPTER_MAX_TARGETS} tendency targets")
         q_index = names.index(SPHUM) if limit else -1
         t_index = names.index(TEMP) if (limit and TEMP in names) else -1
+        for g, name in enumerate(names):
+            # numpy's result dtype of state + tendency * dt (the limited tendencies promoted
+            # with the humidity state and tendency, as xr.where and the MSE terms do)
+            wide = state_f64 or targets[g].pred_f64 != 0
+            if limit and g in (q_index, t_index):
+                wide = wide or targets[q_index].pred_f64 != 0
+            out = torch.empty(states[name].shape, dtype=torch.float64 if wide else torch.float32, device=dev)
+            outs[name] = out
+            targets[g].out = out.data_ptr()
+            targets[g].out_f64 = int(wide)
         n = next(iter(states.values())).numel()
         status = _native.load().fv3_adapter_apply(targets, len(names), n, state_f64, float(self.timestep), int(limit),
                                                   q_index, t_index, _device.stream_handle(None))

@@ -254,9 +254,14 @@ class ShardedStepperWorkload:
     counts: object = None
     partials: object = None
     exchange_bytes: int = 0
+    # > 1 without a process group: one rank's share of a ``stub_world``-rank run on one
+    # GPU, the exchange stubbed by a local copy of the same bytes (this band's partials
+    # replicated for every rank, then folded: the fold sees the full gathered row count)
+    stub_world: int = 1
 
     def step(self):
-        from .distributed import area_row_partials, global_count_sums, global_row_sums, level_sums, row_counts
+        from .distributed import (area_row_partials, fold_rows, global_count_sums, global_row_sums, level_sums,
+                                  row_counts)
         from .stepper import ml_epilogue
 
         T, q = self.state["air_temperature"], self.state["specific_humidity"]
@@ -273,6 +278,10 @@ class ShardedStepperWorkload:
                            res["column_heating_due_to_machine_learning"], res["total_precipitation"]],
                           self.area, out=local)
         limited = level_sums(res["specific_humidity_limiter_active"])  # [nz] exact column counts
+        if self.stub_world > 1 and self.group is None:
+            self.exchange_bytes = 8 * (local.shape[0] * 6 + limited.numel())
+            means = fold_rows(local.repeat(self.stub_world, 1))
+            return torch.cat([means, limited.clone()])
         if self.counts is None:  # the bands are fixed: their sizes are exchanged once
             self.counts = row_counts(local.shape[0], self.group)
             self.exchange_bytes = 8 * (max(self.counts) * 6 + limited.numel())
@@ -286,8 +295,10 @@ class ShardedStepperWorkload:
 
 
 def make_sharded_stepper_workload(res: int = 96, rank: int = 0, world: int = 1, seed: int = 0, device=None,
-                                  group=None):
-    """Every rank generates the same global state (seeded) and keeps its row band."""
+                                  group=None, stub_exchange: bool = False):
+    """Every rank generates the same global state (seeded) and keeps its row band.
+    ``stub_exchange``: no process group, the exchange replaced by a local copy of the
+    bytes ``world`` ranks would gather (one rank's share timed on one GPU)."""
     from .distributed import row_band
 
     wl = make_stepper_workload(res, seed=seed, device=device)
@@ -296,7 +307,7 @@ def make_sharded_stepper_workload(res: int = 96, rank: int = 0, world: int = 1, 
     band2 = lambda a: a.reshape(6 * res, res)[r0:r1].contiguous()  # noqa: E731
     state = {k: (band3(v) if v.dim() == 4 else band2(v)) for k, v in wl.state.items()}
     return ShardedStepperWorkload(wl.model, state, band2(wl.area), wl.dt, (r0, r1), (r1 - r0) * res,
-                                  6 * res * res, group)
+                                  6 * res * res, group, stub_world=world if stub_exchange else 1)
 
 
 @dataclasses.dataclass
@@ -381,11 +392,16 @@ class EmulatorWorkload:
         return self.emulator(self.state, out=self.out)
 
 
-def make_emulator_workload(res: int = 384, seed: int = 0, device=None, precision: str = "bf16x3"):
+def make_emulator_workload(res: int = 384, seed: int = 0, device=None, precision: str = "bf16x3",
+                           rank: int = 0, world: int = 1):
+    """``world`` > 1: this rank's band of the flattened (tile, y) rows only (config #5
+    over ``world`` GPUs: 110,592 columns per GPU at C384 over 8)."""
+    from .distributed import row_band
     from .emulator import MicrophysicsEmulator, zhao_carr_outputs
 
     device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-    ncol = c_columns(res)
+    r0, r1 = row_band(6 * res, rank, world)
+    ncol = (r1 - r0) * res
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     lev = lambda a, b: torch.linspace(a, b, NZ, device=device)[:, None]

@@ -51,7 +51,10 @@ extern "C" {
 
 const char* fv3_last_error(void);
 int fv3_abi_version(void); /* bumped on any signature change (2: emulator fields in fv3_dense_desc,
-                              3: fv3_dense_forward_ex, 4: composites + Adapter) */
+                              3: fv3_dense_forward_ex, 4: composites + Adapter,
+                              5: per-operand dtypes in fv3_adapter_target, fv3_build_kind) */
+const char* fv3_build_kind(void); /* "product" (fv3net_amd/build.py, no experiment knob compiled in)
+                                     or "experiment" (a tools/ variant: results may be invalid) */
 
 /*
  * Column layout of a [level, column] field.  Element (column c, level k) lives at
@@ -493,19 +496,24 @@ int fv3_scale_levels(const void* x, int x_f64, fv3_layout lay, const double* sca
 
 /* fv3_adapter_apply replaces Adapter.predict's arithmetic (transformers/fv3fit.py:66-83) for
  * every state variable updated by tendency predictions: tendency = 0 + p_0 + p_1 + ...
- * (float32 model outputs), out = state + tendency * dt in the state's dtype; with `limit`
- * the specific-humidity target (index sphum_target) and, if temp_target >= 0, the
- * air-temperature target go through non_negative_sphum_mse_conserving
- * (steppers/machine_learning.py:77-99) first.  Every array holds n contiguous elements;
- * out may alias state.  limit without a humidity target: FV3_ERR_UNSUPPORTED (the
- * reference's NotImplementedError). */
+ * (Python's sum), out = state + tendency * dt; with `limit` the specific-humidity target
+ * (index sphum_target) and, if temp_target >= 0, the air-temperature target go through
+ * non_negative_sphum_mse_conserving (steppers/machine_learning.py:77-99) first.  Every
+ * intermediate carries numpy's dtype: a prediction is float32 or float64 (bit p of
+ * pred_f64), the sum widens at the first float64 term, Python-float constants take the
+ * array's dtype, and out is float64 when the state or the (limited) tendency is
+ * (out_f64 must say so: FV3_ERR_INVALID otherwise).  Every array holds n contiguous
+ * elements; out may alias state when it has the state's dtype.  limit without a
+ * humidity target: FV3_ERR_UNSUPPORTED (the reference's NotImplementedError). */
 #define FV3_ADAPTER_MAX_PREDS 8
 #define FV3_ADAPTER_MAX_TARGETS 16
 typedef struct fv3_adapter_target {
-    const float* preds[FV3_ADAPTER_MAX_PREDS];
+    const void* preds[FV3_ADAPTER_MAX_PREDS]; /* float32, or float64 where pred_f64 has the bit */
     int n_preds;
     const void* state; /* float64 (state_f64) or float32 */
-    void* out;
+    void* out;         /* float64 (out_f64) or float32 */
+    unsigned pred_f64;
+    int out_f64;
 } fv3_adapter_target;
 int fv3_adapter_apply(const fv3_adapter_target* targets, int n_targets, int64_t n, int state_f64, double dt,
                       int limit, int sphum_target, int temp_target, void* stream);

@@ -324,3 +324,80 @@ def test_adapter_limit_needs_humidity(gpu, tmp_path):
     X = _c48_rank_state(np.random.default_rng(0))
     with pytest.raises(NotImplementedError):
         adapter.predict({k: X[k] for k in X})
+
+
+@pytest.mark.gpu
+def test_ensemble_reduction_dispatch_is_case_sensitive(gpu):
+    """models.py:239-260 validates ``reduction.lower()`` but dispatches on
+    ``self._reduction == "median"``: a 'Median' config reduces with the mean."""
+    from fv3net_amd.composite import EnsembleModel
+
+    models = []
+    for v in (0.0, 3.0, 5.0):
+        m = P.ConstantOutputPredictor(["input"], ["output"])
+        m.set_outputs(output=v)
+        models.append(m)
+    ds_in = D.Dataset({"input": D.DataArray(np.zeros([3, 3, 5]), ["x", "y", "z"])})
+    np.testing.assert_almost_equal(EnsembleModel(models, reduction="Median").predict(ds_in)["output"].values, 8.0 / 3)
+    np.testing.assert_almost_equal(EnsembleModel(models, reduction="median").predict(ds_in)["output"].values, 3.0)
+
+
+def test_oracle_adapter_float64_predictions_keep_float64():
+    """A TaperedModel returns float64 (scaling * data): the sum, the limiter and the
+    state update stay float64 even over a float32 state (numpy promotion)."""
+    rng = np.random.default_rng(1)
+    q = rng.uniform(0, 1e-5, (4, 6)).astype(np.float32)
+    T = rng.normal(260, 5, (4, 6)).astype(np.float32)
+    pred = {"dQ2": rng.normal(0, 1e-8, (4, 6)), "dQ1": rng.normal(0, 1e-4, (4, 6)).astype(np.float32)}
+    up = OC.adapter_predict(pred, {"specific_humidity": q, "air_temperature": T},
+                            {"dQ1": "air_temperature", "dQ2": "specific_humidity"}, {}, 900.0)
+    assert up["specific_humidity"].dtype == np.float64 and up["air_temperature"].dtype == np.float64
+    up = OC.adapter_predict(pred, {"specific_humidity": q, "air_temperature": T},
+                            {"dQ1": "air_temperature", "dQ2": "specific_humidity"}, {}, 900.0, False)
+    assert up["specific_humidity"].dtype == np.float64 and up["air_temperature"].dtype == np.float32
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("limit", [True, False])
+@pytest.mark.parametrize("state_dtype", [np.float64, np.float32])
+def test_adapter_over_tapered_model_matches_oracle(gpu, tmp_path, limit, state_dtype):
+    """The usual prognostic setup: Adapter over a TaperedModel nesting the
+    build's predictor.  The taper returns float64 dQ2 (dQ1 untapered stays float32); a
+    second model's float32 output is summed onto air_temperature after dQ1.  Each
+    target's sum, limiter and update keep numpy's dtype flow (float64 humidity update
+    over a float32 state), bit for bit against the oracle."""
+    import torch
+
+    from fv3net_amd.dense import DenseColumnModel, DenseModelConfig
+    from fv3net_amd.transformers import Adapter, Config
+
+    rng = np.random.default_rng(8)
+    nz, n = 79, 32
+    P.dump(_dense_predictor(seed=4), str(tmp_path / "base"))
+    _write_composite(str(tmp_path / "tapered"), "tapered_model", "tapered_model.yaml",
+                     {"model": str(tmp_path / "base"), "tapering": {"dQ2": {"cutoff": 30, "rate": 5.0}}})
+    cfg_b = DenseModelConfig(["air_temperature"], ["dT_extra"], [nz], [nz], width=64, depth=2)
+    mb = DenseColumnModel.random(cfg_b, seed=5, bias_scale=0.1,
+                                 sample_inputs=[rng.normal(260, 15, (512, nz)).astype(np.float32)],
+                                 sample_outputs=[rng.normal(0, 1e-5, (512, nz)).astype(np.float32)])
+    P.dump(P.DenseColumnPredictor(cfg_b.input_variables, cfg_b.output_variables, mb), str(tmp_path / "b"))
+    config = Config(url=[str(tmp_path / "tapered"), str(tmp_path / "b")],
+                    tendency_predictions={"dQ1": "air_temperature", "dT_extra": "air_temperature",
+                                          "dQ2": "specific_humidity"}, limit_negative_humidity=limit)
+    adapter = Adapter(config, 900.0)
+    T = rng.normal(260, 15, (nz, n, n)).astype(state_dtype)
+    q = rng.uniform(0, 2e-5, (nz, n, n)).astype(state_dtype)
+    inputs = {"air_temperature": D.DataArray(torch.from_numpy(T).cuda(), ["z", "y", "x"]),
+              "specific_humidity": D.DataArray(torch.from_numpy(q).cuda(), ["z", "y", "x"])}
+    updates = adapter.predict(inputs)
+    ds = D.Dataset(inputs)
+    prediction = {}
+    for m in adapter.model.models:
+        p = m.predict(ds)
+        prediction.update({k: p[k].transpose("z", "y", "x").values for k in p})
+    assert prediction["dQ2"].dtype == np.float64 and prediction["dQ1"].dtype == np.float32
+    ref = OC.adapter_predict(prediction, {"air_temperature": T, "specific_humidity": q},
+                             config.tendency_predictions, config.state_predictions, 900.0, limit)
+    assert sorted(updates) == sorted(ref)
+    for k, r in ref.items():
+        _bits(updates[k].values, r)

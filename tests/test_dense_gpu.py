@@ -83,6 +83,23 @@ def test_widths_depths_plain_layout(gpu, width, depth):
     _check(got, dense_predict([x1, x2], p, np.float64))
 
 
+def test_deep_model_falls_back_to_16_column_tiles(gpu):
+    """A deep, many-feature model (6 x 84 input levels, 59 hidden layers of 256) whose
+    32-column tiles would need more than 160 KiB of LDS (staged inputs + ~1 KiB of
+    biases per hidden layer): the kernel runs 16-column tiles instead of failing
+    (ADVICE r3), within the usual bound on a ragged grid."""
+    import torch
+
+    rng = np.random.default_rng(60)
+    n = 531
+    xs = [rng.normal(0, 1 + v, (n, 84)).astype(np.float32) for v in range(6)]
+    m = _model(dict(input_variables=[f"x{v}" for v in range(6)], output_variables=["y1", "y2"], in_nz=[84] * 6,
+                    out_nz=[79, 79], width=256, depth=60), samples=xs, bias_scale=0.01)
+    outs = m.forward([torch.from_numpy(x.T.copy()).cuda() for x in xs])
+    got = [o.cpu().numpy().T for o in outs]
+    _check(got, dense_predict(xs, m.oracle_params(), np.float64))
+
+
 def test_clip_limits_mask_and_scalar_input(gpu):
     """ClipConfig on inputs (kept slice) and outputs (zero mask), OutputLimit clamps,
     and a 2-D (single-level) input."""

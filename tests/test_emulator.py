@@ -183,6 +183,7 @@ def test_emulator_split_kernel_variants_agree(gpu, monkeypatch, precision, rtol)
     _check_columns(ref, state, emu, np.arange(2085), rtol)
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("precision,rtol,env", [("bf16x3", 1e-4, "FV3_B3_GRID"), ("bf16x6", 1e-5, "FV3_B3_GRID"),
                                                 ("f32", 1e-5, "FV3_DENSE_GRID")])
 def test_emulator_forced_multi_tile_blocks(gpu, precision, rtol, env, monkeypatch):

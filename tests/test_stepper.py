@@ -153,6 +153,38 @@ def test_stepper_workload_bf16x6_predict(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["bf16x6", "f32"])
+def test_stepper_workload_c96_matches_oracle(gpu, precision):
+    """Config #4 at its size (C96, 79 levels, float64 state): one step of the stepper
+    workload with the predict on the bf16x6 split kernel (and the exact-f32 kernel beside
+    it).  The predicted dQ1/dQ2 are held to north_star's 1e-5 per level against the
+    float64 DenseModel graph (oracle/dense.py) on the state's float32 inputs, and the
+    epilogue's state update to oracle/stepper.py applied to the kernel's own prediction,
+    bit for bit."""
+    import torch
+
+    from fv3net_amd import workloads as W
+    from oracle.dense import dense_predict
+    from tests.parity import assert_per_level
+
+    wl = W.make_stepper_workload(96, seed=3, precision=precision)
+    st0 = {k: v.clone() for k, v in wl.state.items()}
+    wl.step()
+    torch.cuda.synchronize()
+    zc = lambda a: a.permute(1, 0, 2, 3).reshape(a.shape[1], -1).cpu().numpy()  # noqa: E731
+    T0, q0 = zc(st0["air_temperature"]), zc(st0["specific_humidity"])
+    ref = dense_predict([T0.T.astype(np.float32), q0.T.astype(np.float32)], wl.model.oracle_params(), np.float64)
+    pred = [zc(o) for o in wl.bound.outputs]
+    for i, (g, r) in enumerate(zip(pred, ref)):
+        assert_per_level(g.T.astype(np.float64), r, 1e-5, f"{precision} C96 dQ{i + 1} vs float64 graph")
+    r = OS.epilogue(pred[0], pred[1], q0, zc(st0["pressure_thickness_of_atmospheric_layer"]), T0,
+                    st0["total_precipitation"].reshape(-1).cpu().numpy(), wl.dt)
+    _bits(zc(wl.state["air_temperature"]), r["air_temperature"])
+    _bits(zc(wl.state["specific_humidity"]), r["specific_humidity"])
+    _bits(wl.state["total_precipitation"].reshape(-1).cpu().numpy(), r["total_precipitation"])
+
+
+@pytest.mark.gpu
 def test_pure_ml_stepper_mirror(gpu):
     """PureMLStepper (machine_learning.py:239-315) over a DenseColumnPredictor: the
     tendencies/diagnostics equal the oracle epilogue applied to the model's own

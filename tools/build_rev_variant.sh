@@ -13,7 +13,7 @@ for f in $SRC "$@"; do git show $REV:fv3net_amd/csrc/$f > $T/fv3net_amd/csrc/$f;
 python3 -c "from fv3net_amd import build; build.build()" >/dev/null
 BASE=${SRC%.hip}
 OBJS=$(ls fv3net_amd/_lib/obj/*.o | grep -v "/$BASE\.")
-/opt/rocm/bin/hipcc -O3 -std=c++17 -ffp-contract=off -fPIC --offload-arch=gfx950 -I include \
+/opt/rocm/bin/hipcc -DFV3_EXPERIMENT_BUILD -O3 -std=c++17 -ffp-contract=off -fPIC --offload-arch=gfx950 -I include \
     -c $T/fv3net_amd/csrc/$SRC -o $T/v.o
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o tools/variants/lib$NAME.so $OBJS $T/v.o
 rm -rf $T

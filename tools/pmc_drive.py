@@ -52,6 +52,15 @@ def make(leg, dev):
         return W.make_stepper_workload(96, seed=11, device=dev)
     if leg == "predict_mappm_c384" and hasattr(W, "make_predict_mappm_workload"):
         return W.make_predict_mappm_workload(384, seed=17, device=dev)
+    # one rank's share of the 8-GPU decompositions (bench.py rank_share_legs)
+    if leg == "stepper_c96_r8":
+        return W.make_sharded_stepper_workload(96, 0, 8, seed=11, device=dev, stub_exchange=True)
+    if leg in ("emulator_c384_r8", "emulator_c384_f32_r8"):
+        return W.make_emulator_workload(384, seed=13, device=dev, precision="f32" if "f32" in leg else "bf16x3",
+                                        world=8)
+    if leg in ("predict_mappm_c384_r8", "predict_mappm_c384_bf16x6_r8"):
+        return W.make_predict_mappm_workload(384, 0, 8, seed=21, device=dev,
+                                             precision="bf16x6" if "bf16x6" in leg else "f32")
     raise SystemExit(f"unknown leg {leg}")
 
 

@@ -39,6 +39,12 @@ LEGS = {
     "dense_c384_bf16x6": ("dense_c384_bf16x6", "dense_b3_kernel"),
     "emulator_c384_bf16x6": ("emulator_c384_bf16x6", "dense_b3_kernel"),
     "predict_mappm_c384_bf16x6": ("predict_mappm_c384_bf16x6", "dense_b3_kernel"),
+    "stepper_c96_rank_of_8": ("stepper_c96_r8", "dense_forward_kernel"),
+    "emulator_c384_rank_of_8": ("emulator_c384_r8", "dense_b3_kernel"),
+    "emulator_c384_rank_of_8_f32": ("emulator_c384_f32_r8", "dense_forward_kernel"),
+    "predict_mappm_c384_rank_of_8": ("predict_mappm_c384_r8", "dense_forward_kernel"),
+    "predict_mappm_c384_rank_of_8_bf16x6": ("predict_mappm_c384_bf16x6_r8", "dense_b3_kernel"),
+    "predict_mappm_c384_rank_of_8_mappm": ("predict_mappm_c384_r8", "mappm_ppm_pair_kernel"),
 }
 KEEP = ("fv3::", "calib_")
 
