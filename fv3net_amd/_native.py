@@ -73,6 +73,8 @@ EXPORTED_SYMBOLS = (
     "fv3_member_reduce",
     "fv3_scale_levels",
     "fv3_adapter_apply",
+    "fv3_derived_elementwise",
+    "fv3_derived_columns",
 )
 ABI_VERSION = 5
 
@@ -165,6 +167,15 @@ class AdapterTarget(ctypes.Structure):
     ]
 
 
+class Field(ctypes.Structure):
+    """fv3_field: a float32 / float64 [level][column] operand of fv3_derived_columns."""
+    _fields_ = [
+        ("data", ctypes.c_void_p),
+        ("f64", ctypes.c_int),
+        ("lay", Layout),
+    ]
+
+
 _lib = None
 _lock = threading.Lock()
 
@@ -241,6 +252,10 @@ _SIGNATURES = {
     "fv3_member_reduce": (_I, [ctypes.POINTER(_P), _I, _I64, _I, _I, _P, _P]),
     "fv3_scale_levels": (_I, [_P, _I, Layout, _P, _I64, _I, _P, _P]),
     "fv3_adapter_apply": (_I, [ctypes.POINTER(AdapterTarget), _I, _I64, _I, _D, _I, _I, _I, _P]),
+    "fv3_derived_elementwise": (_I, [_I, ctypes.POINTER(_P), ctypes.POINTER(_I), _I, _P, _I, _I64,
+                                     ctypes.POINTER(_D), _I, _P]),
+    "fv3_derived_columns": (_I, [_I, ctypes.POINTER(Field), _I, ctypes.POINTER(Field), _I, _I64, _I,
+                                 ctypes.POINTER(_D), _I, _P]),
 }
 
 

@@ -518,6 +518,66 @@ typedef struct fv3_adapter_target {
 int fv3_adapter_apply(const fv3_adapter_target* targets, int n_targets, int64_t n, int state_f64, double dt,
                       int limit, int sphum_target, int temp_target, void* stream);
 
+/* Derived variables behind fv3fit's DerivedModel and TransformedPredictor
+ * (external/fv3fit/fv3fit/_shared/models.py:110-220, 279-337): the vcm.DerivedMapping
+ * (vcm/derived_mapping.py:123-127, 264-410) and vcm.DataTransform (vcm/data_transform.py:
+ * 65-323) entries a dQ1/dQ2 model feeds.  Operands are float32 or float64; every numpy
+ * intermediate keeps numpy's dtype (Python-float constants take the array's dtype), so the
+ * results are bit-identical to the numpy expressions.
+ *
+ * fv3_derived_elementwise: n contiguous elements per operand (a NULL operand of
+ * ADD / SUB after the first is zeros_like of its dtype), out in out_f64's dtype:
+ *   ADD / SUB       in0 + in1 + ... / in0 - in1 - ... (left to right, promoted)
+ *   IADD            in0 += in1 (promoted arithmetic, stored in in0's dtype)
+ *   SCALE           p0 * in0            DIV_SCALAR      in0 / p0
+ *   MSE             moist_static_energy_tendency(in0 = Q1, in1 = Q2[, in2 = T])
+ *   TEMP_TEND       temperature_tendency(in0 = Qm, in1 = Q2[, in2 = T])  (local.py:317-360)
+ *   INCLOUD_TO_GRIDCELL / GRIDCELL_TO_INCLOUD  (clouds.py:7-66): in0 = cloud fraction,
+ *                   in1 = condensate, p0 = climit1, p1 = climit2
+ *   MUL             in0 * in1           ONE_MINUS_MUL   (1 - in0) * in1
+ *   ISCLOSE_ONEHOT  where(isclose(in0, p0, rtol = p1, atol = p2), 1.0, 0.0), float64
+ *                   (derived_mapping.py:194-262) */
+#define FV3_EW_ADD 1
+#define FV3_EW_SUB 2
+#define FV3_EW_IADD 3
+#define FV3_EW_SCALE 4
+#define FV3_EW_DIV_SCALAR 5
+#define FV3_EW_MSE 6
+#define FV3_EW_TEMP_TEND 7
+#define FV3_EW_INCLOUD_TO_GRIDCELL 8
+#define FV3_EW_GRIDCELL_TO_INCLOUD 9
+#define FV3_EW_MUL 10
+#define FV3_EW_ONE_MINUS_MUL 11
+#define FV3_EW_ISCLOSE_ONEHOT 12
+int fv3_derived_elementwise(int op, const void* const* in, const int* in_f64, int n_in, void* out, int out_f64,
+                            int64_t n, const double* params, int n_params, void* stream);
+
+/* fv3_derived_columns: per column over nz levels ([level][column] under each field's
+ * layout; 2-D fields are one level):
+ *   MASS_INTEGRAL         out0 = [-]p1 * sum_z nan0(s x delp / g), x = in0, delp = in1,
+ *                         s = sign(p0), p1 NaN: no scale, p2 != 0: negated, p3 != 0: numpy's
+ *                         pairwise order of a z-last array (nz <= 128; else sequential, as
+ *                         numpy reduces a leading or middle axis) (vertically_dependent.py:
+ *                         18-22, 279-325)
+ *   TENDENCY_TO_FLUX      in0 tendency, in1 delp, in2 TOA net flux (NULL: zeros), in3
+ *                         surface upward flux; out0 = interface fluxes (nz levels), out1 =
+ *                         downward surface flux, rectified when p0 != 0 (flux_form.py:7-42)
+ *   IMPLIED_SURFACE_FLUX  the same inputs; out0 = TOA + up - <in0>, p1 as MASS_INTEGRAL's p3
+ *                         (flux_form.py:45-73)
+ *   FLUX_TO_TENDENCY      in0 fluxes (nz levels), in1 delp, in2 downward, in3 upward
+ *                         surface flux; out0 = -(g diff(flux) / delp) (flux_form.py:76-100) */
+typedef struct fv3_field {
+    const void* data;
+    int f64;
+    fv3_layout lay;
+} fv3_field;
+#define FV3_COL_MASS_INTEGRAL 1
+#define FV3_COL_TENDENCY_TO_FLUX 2
+#define FV3_COL_IMPLIED_SURFACE_FLUX 3
+#define FV3_COL_FLUX_TO_TENDENCY 4
+int fv3_derived_columns(int op, const fv3_field* in, int n_in, const fv3_field* out, int n_out, int64_t ncol, int nz,
+                        const double* params, int n_params, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -97,7 +97,15 @@ def test_deep_model_falls_back_to_16_column_tiles(gpu):
                     out_nz=[79, 79], width=256, depth=60), samples=xs, bias_scale=0.01)
     outs = m.forward([torch.from_numpy(x.T.copy()).cuda() for x in xs])
     got = [o.cpu().numpy().T for o in outs]
-    _check(got, dense_predict(xs, m.oracle_params(), np.float64))
+    p = m.oracle_params()
+    ref64, ref32 = dense_predict(xs, p, np.float64), dense_predict(xs, p, np.float32)
+    # 59 layers amplify float32 rounding (measured 1.5e-4 on the GPU): the bound is the
+    # numpy float32 graph's own worst level error against float64, with 3x headroom
+    from tests.parity import per_level_errors
+
+    for o, (g, r64, r32) in enumerate(zip(got, ref64, ref32)):
+        f32_err = np.nanmax(per_level_errors(r32, r64)[0])
+        assert_per_level(g, r64, max(RTOL, 3 * f32_err), f"deep model output {o} (float32 graph {f32_err:.2e})")
 
 
 def test_clip_limits_mask_and_scalar_input(gpu):
