@@ -76,7 +76,7 @@ EXPORTED_SYMBOLS = (
     "fv3_derived_elementwise",
     "fv3_derived_columns",
 )
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # fv3_dense_forward_ex precisions
 DENSE_F32 = 0
@@ -254,6 +254,8 @@ _SIGNATURES = {
     "fv3_adapter_apply": (_I, [ctypes.POINTER(AdapterTarget), _I, _I64, _I, _D, _I, _I, _I, _P]),
     "fv3_derived_elementwise": (_I, [_I, ctypes.POINTER(_P), ctypes.POINTER(_I), _I, _P, _I, _I64,
                                      ctypes.POINTER(_D), _I, _P]),
+    "fv3_host_register": (_I, [_P, ctypes.c_size_t]),
+    "fv3_host_unregister": (_I, [_P]),
     "fv3_derived_columns": (_I, [_I, ctypes.POINTER(Field), _I, ctypes.POINTER(Field), _I, _I64, _I,
                                  ctypes.POINTER(_D), _I, _P]),
 }

@@ -283,14 +283,41 @@ __global__ __launch_bounds__(64) void mappm_cs_kernel(MappmArgs a)
     mappm_cs_column(col, scr, a.km, a.kn, a.iv, a.kord);
 }
 
+// Grid-stride over the columns: thread slot s owns scratch column s and reuses it for
+// columns s, s + S, s + 2S, ... (S = grid threads).  The host sizes the grid to the
+// chip's resident threads, so the scratch is ~0.2 GB at km = 79 instead of one column
+// per grid column (0.58 GB at C384): it stays within the 256 MB MALL, and every
+// thread's write -> read-back round trip (forward sweep, back-substitution, stream)
+// is served on chip rather than from HBM.
 __global__ __launch_bounds__(256) void mappm_cs_global_kernel(MappmArgs a)
 {
-    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= a.ncol) return;
+    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    GlobalScr scr{a.scratch + c, stride, (int64_t)(a.km + 3) * stride};
-    DevCol col = make_col(a, c);
-    mappm_cs_column(col, scr, a.km, a.kn, a.iv, a.kord);
+    GlobalScr scr{a.scratch + slot, stride, (int64_t)(a.km + 3) * stride};
+    for (int64_t c = slot; c < a.ncol; c += stride) {
+        DevCol col = make_col(a, c);
+        mappm_cs_column(col, scr, a.km, a.kn, a.iv, a.kord);
+    }
+}
+
+// Grid of the kord > 7 kernel: the fewest grid-stride rounds the resident capacity
+// allows, then as few threads as give that many rounds (every slot runs the same
+// number of columns, up to one).  FV3_MAPPM_CS_ROUNDS=n forces n rounds (A/B).
+int64_t cs_grid(const MappmArgs& a, int block)
+{
+    static int cap = 0;  // resident blocks of the kernel on the whole chip
+    if (!cap) {
+        int dev = 0, n_cu = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mappm_cs_global_kernel, block, 0) != hipSuccess)
+            return -1;
+        cap = std::max(1, n_cu * per_cu);
+    }
+    const int64_t blocks = (a.ncol + block - 1) / block;
+    int64_t rounds = (blocks + cap - 1) / cap;
+    if (const char* e = getenv("FV3_MAPPM_CS_ROUNDS")) rounds = std::max<int64_t>(1, atoll(e));
+    return std::max<int64_t>(1, (blocks + rounds - 1) / rounds);
 }
 
 }  // namespace
@@ -311,7 +338,8 @@ int launch_mappm(MappmArgs a, hipStream_t stream)
     if (a.ncol == 0) return FV3_OK;
     if (a.kord > 7 && !getenv("FV3_MAPPM_LDS")) {
         const int block = 256;
-        const int64_t grid = (a.ncol + block - 1) / block;
+        const int64_t grid = cs_grid(a, block);
+        FV3_REQUIRE_CODE(FV3_ERR_HIP, grid > 0, "mappm: occupancy query for the kord>7 kernel failed");
         FV3_HIP(hipMallocAsync((void**)&a.scratch, sizeof(float) * 2 * (size_t)(a.km + 3) * (size_t)grid * block,
                                stream));
         hipLaunchKernelGGL(mappm_cs_global_kernel, dim3((unsigned)grid), dim3(block), 0, stream, a);

@@ -138,6 +138,48 @@ class PinnedStager:
         return out
 
 
+class HostPages:
+    """``with HostPages(arrays) as p:`` page-locks the arrays' own memory
+    (fv3_host_register) so that copies on the current stream DMA straight from / to it,
+    with no bounce buffer and no host memcpy; ``p.add(more)`` registers more arrays in
+    the block.  On exit the current stream is synchronised (every copy issued in the
+    block is complete) and what was registered here is released.  Arrays below
+    ``min_bytes`` (sharing pages with other allocations) and arrays whose pages cannot
+    be registered are left as they are: copies from them are pageable copies, which
+    the runtime completes before returning."""
+
+    def __init__(self, arrays=(), min_bytes: int = 64 << 10):
+        from . import _native
+
+        self._lib = _native.load()
+        self.min_bytes = int(min_bytes)
+        self._registered = []
+        self._pending = list(arrays)
+
+    def add(self, arrays):
+        for a in arrays:
+            if not (isinstance(a, np.ndarray) and a.flags.c_contiguous) or a.nbytes < self.min_bytes:
+                continue
+            if any(a.ctypes.data == p for p in self._registered):
+                continue
+            if self._lib.fv3_host_register(a.ctypes.data, a.nbytes) == 0:
+                self._registered.append(a.ctypes.data)
+
+    def __enter__(self):
+        self.add(self._pending)
+        self._pending = []
+        return self
+
+    def __exit__(self, *exc):
+        try:
+            torch.cuda.current_stream().synchronize()
+        finally:
+            for p in self._registered:
+                self._lib.fv3_host_unregister(p)
+            self._registered = []
+        return False
+
+
 _stagers = {}
 _stagers_lock = threading.Lock()
 

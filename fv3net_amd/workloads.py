@@ -178,28 +178,47 @@ class StepperWorkload:
     bound: object = None
     precision: str = "f32"
     _in32: object = None
+    # every step after the first replays one HIP graph of the device part (graphs.py)
+    graph: bool = True
+    _graph: object = None
 
-    def step(self):
-        from .distributed import area_weighted_partials, combine_partials
+    def _device_step(self):
+        """predict + epilogue + partials on the current stream, fixed buffers: the state
+        is updated in place and the new precipitation copied back into its own buffer."""
+        from .distributed import area_weighted_partials
         from .stepper import ml_epilogue
 
         T, q = self.state["air_temperature"], self.state["specific_humidity"]
-        if self.bound is None:  # validated once
-            if self.precision == "f32":  # the float64 state read in place every step
-                self.bound = self.model.bind([T, q], level_axes=[1, 1])
-            else:  # the split kernel reads float32: the state is cast into bound buffers each step
-                self._in32 = [T.to(torch.float32), q.to(torch.float32)]
-                self.bound = self.model.bind(self._in32, level_axes=[1, 1], precision=self.precision)
+        precip = self.state["total_precipitation"]
         if self._in32 is not None:
             self._in32[0].copy_(T)
             self._in32[1].copy_(q)
         dq1, dq2 = self.bound()
         res = ml_epilogue(dq1, dq2, q, self.state["pressure_thickness_of_atmospheric_layer"], T, self.dt,
-                          self.state["total_precipitation"], in_place=True, level_axis=1)
-        self.state["total_precipitation"] = res["total_precipitation"]
+                          precip, in_place=True, level_axis=1)
+        precip.copy_(res["total_precipitation"])
         diags = [res["net_moistening_due_to_machine_learning"], res["column_heating_due_to_machine_learning"],
-                 res["total_precipitation"]]
-        part = area_weighted_partials(diags, self.area)  # float64 diagnostics: the f64 reduction
+                 precip]
+        return area_weighted_partials(diags, self.area)  # float64 diagnostics: the f64 reduction
+
+    def step(self):
+        from .distributed import combine_partials
+        from .graphs import StepGraph
+
+        if self.bound is None:  # validated once; the first step runs eagerly
+            T, q = self.state["air_temperature"], self.state["specific_humidity"]
+            if self.precision == "f32":  # the float64 state read in place every step
+                self.bound = self.model.bind([T, q], level_axes=[1, 1])
+            else:  # the split kernel reads float32: the state is cast into bound buffers each step
+                self._in32 = [T.to(torch.float32), q.to(torch.float32)]
+                self.bound = self.model.bind(self._in32, level_axes=[1, 1], precision=self.precision)
+            part = self._device_step()
+        elif self.graph:
+            if self._graph is None:
+                self._graph = StepGraph(self._device_step)
+            part = self._graph()
+        else:
+            part = self._device_step()
         return combine_partials(part, self.group)
 
 
@@ -258,30 +277,54 @@ class ShardedStepperWorkload:
     # GPU, the exchange stubbed by a local copy of the same bytes (this band's partials
     # replicated for every rank, then folded: the fold sees the full gathered row count)
     stub_world: int = 1
+    # every step after the first replays HIP graphs of the device parts (graphs.py): one
+    # for the whole step when nothing is exchanged (one rank, or the stubbed exchange),
+    # else one before the collectives; the fold after them stays one eager launch
+    graph: bool = True
+    _graph: object = None
 
-    def step(self):
-        from .distributed import (area_row_partials, fold_rows, global_count_sums, global_row_sums, level_sums,
-                                  row_counts)
+    def _device_step(self):
+        """predict + epilogue + row partials + level counts on the current stream, fixed
+        buffers; with the stubbed exchange also its local copy and the fold."""
+        from .distributed import area_row_partials, fold_rows, level_sums
         from .stepper import ml_epilogue
 
         T, q = self.state["air_temperature"], self.state["specific_humidity"]
-        if self.bound is None:
-            self.bound = self.model.bind([T, q], level_axes=[0, 0])
+        precip = self.state["total_precipitation"]
         dq1, dq2 = self.bound()
         res = ml_epilogue(dq1, dq2, q, self.state["pressure_thickness_of_atmospheric_layer"], T, self.dt,
-                          self.state["total_precipitation"], in_place=True, level_axis=0)
-        self.state["total_precipitation"] = res["total_precipitation"]
-        if self.partials is None:  # [rows][3 (sum area*x, sum area) pairs]
-            self.partials = torch.empty((self.area.shape[0], 6), dtype=torch.float64, device=q.device)
+                          precip, in_place=True, level_axis=0)
+        precip.copy_(res["total_precipitation"])
         local = self.partials
         area_row_partials([res["net_moistening_due_to_machine_learning"],
-                           res["column_heating_due_to_machine_learning"], res["total_precipitation"]],
-                          self.area, out=local)
+                           res["column_heating_due_to_machine_learning"], precip], self.area, out=local)
         limited = level_sums(res["specific_humidity_limiter_active"])  # [nz] exact column counts
         if self.stub_world > 1 and self.group is None:
-            self.exchange_bytes = 8 * (local.shape[0] * 6 + limited.numel())
             means = fold_rows(local.repeat(self.stub_world, 1))
             return torch.cat([means, limited.clone()])
+        return local, limited
+
+    def step(self):
+        from .distributed import global_count_sums, global_row_sums, row_counts
+        from .graphs import StepGraph
+
+        if self.bound is None:  # validated once; the first step runs eagerly
+            T, q = self.state["air_temperature"], self.state["specific_humidity"]
+            self.bound = self.model.bind([T, q], level_axes=[0, 0])
+            # [rows][3 (sum area*x, sum area) pairs]
+            self.partials = torch.empty((self.area.shape[0], 6), dtype=torch.float64, device=q.device)
+            out = self._device_step()
+        elif self.graph:
+            if self._graph is None:
+                self._graph = StepGraph(self._device_step)
+            out = self._graph()
+        else:
+            out = self._device_step()
+        nz = self.state["specific_humidity"].shape[0]
+        if self.stub_world > 1 and self.group is None:
+            self.exchange_bytes = 8 * (self.partials.shape[0] * 6 + nz)
+            return out.clone()
+        local, limited = out
         if self.counts is None:  # the bands are fixed: their sizes are exchanged once
             self.counts = row_counts(local.shape[0], self.group)
             self.exchange_bytes = 8 * (max(self.counts) * 6 + limited.numel())

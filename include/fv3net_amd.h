@@ -38,6 +38,7 @@
 #ifndef FV3NET_AMD_H
 #define FV3NET_AMD_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -52,7 +53,8 @@ extern "C" {
 const char* fv3_last_error(void);
 int fv3_abi_version(void); /* bumped on any signature change (2: emulator fields in fv3_dense_desc,
                               3: fv3_dense_forward_ex, 4: composites + Adapter,
-                              5: per-operand dtypes in fv3_adapter_target, fv3_build_kind) */
+                              5: per-operand dtypes in fv3_adapter_target, fv3_build_kind,
+                              6: fv3_host_register / fv3_host_unregister) */
 const char* fv3_build_kind(void); /* "product" (fv3net_amd/build.py, no experiment knob compiled in)
                                      or "experiment" (a tools/ variant: results may be invalid) */
 
@@ -577,6 +579,17 @@ typedef struct fv3_field {
 #define FV3_COL_FLUX_TO_TENDENCY 4
 int fv3_derived_columns(int op, const fv3_field* in, int n_in, const fv3_field* out, int n_out, int64_t ncol, int nz,
                         const double* params, int n_params, void* stream);
+
+/*
+ * Page-lock / release a caller's host array so that H2D / D2H copies DMA straight from
+ * and to its pages (the drop-in call's host boundary, pure_keras.py:98-118 takes and
+ * returns host arrays).  fv3_host_register returns FV3_ERR_UNSUPPORTED (runtime error
+ * state cleared) when the pages cannot be registered, e.g. already registered or shared
+ * with another registered array: copy through staging then.  Unregister only what this
+ * call registered, after the copies using it have completed.
+ */
+int fv3_host_register(void* ptr, size_t bytes);
+int fv3_host_unregister(void* ptr);
 
 #ifdef __cplusplus
 }

@@ -164,6 +164,69 @@ def test_dense_predictor_end_to_end(gpu):
         pred.predict(D.Dataset({"air_temperature": X["air_temperature"]}))
 
 
+@pytest.mark.gpu
+def test_dense_predictor_host_arrays_page_locked_path(gpu):
+    """numpy inputs take the host-call path (the caller's pages registered for the call,
+    DMA straight to device buffers kept per shape, the bound kernel, DMA back into new
+    numpy arrays): bit-identical to the device-resident predict on the float32 values,
+    for float64 and float32 arrays, read-only arrays, repeated calls (fresh outputs each
+    call), a shape change, and arrays too small to register."""
+    import torch
+
+    from fv3net_amd import transfer
+    from fv3net_amd.dense import DenseColumnModel, DenseModelConfig
+
+    rng = np.random.default_rng(8)
+    cfg = DenseModelConfig(["air_temperature", "specific_humidity"], ["dQ1", "dQ2"], [79, 79], [79, 79],
+                           width=256, depth=3)
+    T = rng.normal(260, 15, (79, 48, 48))
+    q = rng.uniform(0, 0.02, (79, 48, 48))
+    m = DenseColumnModel.random(cfg, seed=3, sample_inputs=[T.reshape(79, -1).T, q.reshape(79, -1).T])
+    pred = P.DenseColumnPredictor(cfg.input_variables, cfg.output_variables, m)
+
+    def device_ref(T, q):
+        Xd = D.Dataset({"air_temperature": D.DataArray(torch.from_numpy(T.astype(np.float32)).cuda(), ["z", "y", "x"]),
+                        "specific_humidity": D.DataArray(torch.from_numpy(q.astype(np.float32)).cuda(),
+                                                         ["z", "y", "x"])})
+        o = pred.predict(Xd)
+        return [o[k].data.cpu().numpy() for k in ("dQ1", "dQ2")]
+
+    def host(T, q):
+        X = D.Dataset({"air_temperature": D.DataArray(T, ["z", "y", "x"]),
+                       "specific_humidity": D.DataArray(q, ["z", "y", "x"])})
+        o = pred.predict(X)
+        assert all(isinstance(o[k].values, np.ndarray) and o[k].values.dtype == np.float32 for k in ("dQ1", "dQ2"))
+        return [o[k].values for k in ("dQ1", "dQ2")]
+
+    ref = device_ref(T, q)
+    first = host(T, q)
+    for g, r in zip(first, ref):
+        assert (g.view(np.uint32) == r.view(np.uint32)).all()
+    ro_T, ro_q = T.copy(), q.copy()
+    ro_T.flags.writeable = False
+    ro_q.flags.writeable = False
+    again = host(ro_T, ro_q)
+    for g, a, r in zip(again, first, ref):
+        assert g is not a and (g.view(np.uint32) == r.view(np.uint32)).all()
+    T32, q32 = T.astype(np.float32), q.astype(np.float32)
+    for g, r in zip(host(T32, q32), ref):
+        assert (g.view(np.uint32) == r.view(np.uint32)).all()
+    # another shape (a smaller rank subdomain), then arrays below the registration size
+    for shape in ((79, 24, 48), (79, 4, 5)):
+        Ts, qs = T[:, :shape[1], :shape[2]].copy(), q[:, :shape[1], :shape[2]].copy()
+        for g, r in zip(host(Ts, qs), device_ref(Ts, qs)):
+            assert (g.view(np.uint32) == r.view(np.uint32)).all(), shape
+    # the registration helper: pages released on exit, a second registration refused cleanly
+    a = np.zeros(1 << 20)
+    with transfer.HostPages([a]) as p:
+        assert len(p._registered) == 1
+        with transfer.HostPages([a]) as p2:  # already registered: left alone
+            assert p2._registered == []
+    with transfer.HostPages([a]) as p:  # released above, registrable again
+        assert len(p._registered) == 1
+    torch.cuda.synchronize()
+
+
 def test_load_without_name_file_tries_every_registered_type(tmp_path):
     """io.py:76-88: a missing ``name`` file warns and tries each registered class."""
     ds = D.Dataset({"a": D.DataArray(np.random.rand(5, 3, 4), ["z", "y", "x"])})

@@ -129,6 +129,37 @@ def test_stepper_workload_step(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["full", "rank_of_4_stub", "rank_of_2_bf16x6"])
+def test_stepper_graph_replay_bit_identical_to_eager(gpu, kind):
+    """Steps 2.. of the stepper workloads replay one HIP graph of the device part
+    (fv3net_amd/graphs.py).  Four steps with the graph give the eager steps' bits: the
+    state (updated in place), the accumulated precipitation (copied back into its own
+    buffer inside the graph), the returned global sums and limiter profile."""
+    import torch
+
+    from fv3net_amd import workloads as W
+
+    def make(graph):
+        if kind == "full":
+            wl = W.make_stepper_workload(12, seed=4)
+        elif kind == "rank_of_4_stub":
+            wl = W.make_sharded_stepper_workload(12, 1, 4, seed=4, stub_exchange=True)
+        else:
+            wl = W.make_stepper_workload(12, seed=4, precision="bf16x6")
+        wl.graph = graph
+        return wl
+
+    eager, graphed = make(False), make(True)
+    for step in range(4):
+        a, b = eager.step(), graphed.step()
+        torch.cuda.synchronize()
+        assert torch.equal(a.view(torch.int64), b.view(torch.int64)), step
+        for k in eager.state:
+            assert torch.equal(eager.state[k], graphed.state[k]), (step, k)
+    assert graphed._graph is not None and graphed._graph.graph is not None
+
+
+@pytest.mark.gpu
 def test_stepper_workload_bf16x6_predict(gpu):
     """The config #4 step with the predict on the bf16x6 split kernel (the float64 state
     cast into bound float32 buffers each step): its tendencies agree with the exact-f32

@@ -1,0 +1,140 @@
+"""The drop-in rank call's host boundary: one rank's (79, 48, 48)
+float64 T / q numpy arrays in, float32 dQ1 / dQ2 numpy arrays out, 2,304 columns.
+
+Legs (wall time per call, same model, same bytes):
+  predict      DenseColumnPredictor.predict on a Dataset (the product call today)
+  staged       pinned staging buffers: np.copyto into them, async H2D, the bound
+               float64-in-place kernel, async D2H, np.copyto out
+  register     hipHostRegister of the caller's four arrays on every call, DMA straight
+               from / to their pages, hipHostUnregister after
+  registered   the same four arrays registered once (a caller that reuses its buffers)
+  pageable     torch's synchronous pageable copies of the same arrays
+  kernel       the bound kernel alone (device resident)
+Prints one JSON line."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fv3net_amd import dataset as D  # noqa: E402
+from fv3net_amd import workloads as W  # noqa: E402
+from fv3net_amd.predictor import DenseColumnPredictor  # noqa: E402
+
+
+def timeit(fn, n=50, warm=5):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / n * 1e3
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    wl = W.make_dense_workload(48, seed=3, device=dev)
+    cfg = wl.model.config
+    T = np.ascontiguousarray(wl.inputs[0][0].double().cpu().numpy())
+    q = np.ascontiguousarray(wl.inputs[1][0].double().cpu().numpy())
+    nz, ny, nx = T.shape
+    out_h = [np.empty((nz, ny, nx), np.float32) for _ in range(2)]
+    dT = torch.empty(T.shape, dtype=torch.float64, device=dev)
+    dq = torch.empty(q.shape, dtype=torch.float64, device=dev)
+    bound = wl.model.bind([dT, dq], level_axes=[0, 0])
+    outs = bound()
+    stream = torch.cuda.current_stream()
+    res = {}
+
+    pred = DenseColumnPredictor(cfg.input_variables, cfg.output_variables, wl.model)
+    X = D.Dataset({cfg.input_variables[0]: D.DataArray(T, ["z", "y", "x"]),
+                   cfg.input_variables[1]: D.DataArray(q, ["z", "y", "x"])})
+    ref = pred.predict(X)
+    res["predict_ms"] = timeit(lambda: pred.predict(X))
+
+    res["kernel_ms"] = timeit(lambda: bound())
+
+    def pageable():
+        dT.copy_(torch.from_numpy(T))
+        dq.copy_(torch.from_numpy(q))
+        o = bound()
+        for h, t in zip(out_h, o):
+            torch.from_numpy(h).copy_(t)
+    res["pageable_ms"] = timeit(pageable)
+
+    pin_in = [torch.empty(T.shape, dtype=torch.float64, pin_memory=True) for _ in range(2)]
+    pin_out = [torch.empty((nz, ny, nx), dtype=torch.float32, pin_memory=True) for _ in range(2)]
+    pin_in_np = [p.numpy() for p in pin_in]
+    pin_out_np = [p.numpy() for p in pin_out]
+
+    def staged():
+        np.copyto(pin_in_np[0], T)
+        dT.copy_(pin_in[0], non_blocking=True)
+        np.copyto(pin_in_np[1], q)
+        dq.copy_(pin_in[1], non_blocking=True)
+        o = bound()
+        for p, t in zip(pin_out, o):
+            p.copy_(t, non_blocking=True)
+        stream.synchronize()
+        for h, p in zip(out_h, pin_out_np):
+            np.copyto(h, p)
+    res["staged_ms"] = timeit(staged)
+
+    cudart = torch.cuda.cudart()
+    arrays = [T, q] + out_h
+
+    def reg(a):
+        st = cudart.cudaHostRegister(a.ctypes.data, a.nbytes, 0)
+        assert int(st) == 0, f"hipHostRegister failed: {st}"
+
+    def unreg(a):
+        st = cudart.cudaHostUnregister(a.ctypes.data)
+        assert int(st) == 0, f"hipHostUnregister failed: {st}"
+
+    tin = [torch.from_numpy(T), torch.from_numpy(q)]
+    tout = [torch.from_numpy(h) for h in out_h]
+
+    def direct():
+        dT.copy_(tin[0], non_blocking=True)
+        dq.copy_(tin[1], non_blocking=True)
+        o = bound()
+        for h, t in zip(tout, o):
+            h.copy_(t, non_blocking=True)
+        stream.synchronize()
+
+    def register_each():
+        for a in arrays:
+            reg(a)
+        direct()
+        for a in arrays:
+            unreg(a)
+    res["register_per_call_ms"] = timeit(register_each, n=20)
+
+    def reg_only():
+        for a in arrays:
+            reg(a)
+        for a in arrays:
+            unreg(a)
+    res["register_unregister_only_ms"] = timeit(reg_only, n=20)
+
+    for a in arrays:
+        reg(a)
+    res["registered_ms"] = timeit(direct)
+    same = all(np.array_equal(h.view(np.uint32), np.asarray(ref[n].values).view(np.uint32))
+               for h, n in zip(out_h, cfg.output_variables))
+    for a in arrays:
+        unreg(a)
+    res["registered_bit_identical_to_predict"] = bool(same)
+    res["host_bytes_per_call"] = T.nbytes + q.nbytes + sum(h.nbytes for h in out_h)
+    res["columns_per_call"] = ny * nx
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
