@@ -110,6 +110,11 @@ struct B3Args {
     int64_t out_ld[kMaxVars], out_bs[kMaxVars];
     const float* res_ptr[kMaxVars];
     int64_t res_ld[kMaxVars], res_bs[kMaxVars];
+    // profiling hook (fv3_dense_set_trace), NULL normally: per tile [8] int64 =
+    // wall clock (100 MHz) at tile start / layer 1 done / hidden done / tile end, CU id,
+    // shader clock at tile start / end, shader cycles wave 0 spent in the chunk waits
+    // (vmcnt + barrier) of the tile
+    long long* trace;
 };
 static_assert(sizeof(B3Args) <= 4096, "kernel arguments are limited to 4 KiB");
 
@@ -397,10 +402,19 @@ dense_b3_kernel(B3Args pa)
     // end of a chunk.  GL: this wave's LDS-DMA of chunk +1 (issued one chunk ago) must have
     // landed before the barrier that publishes it; `younger` = vector-memory operations this
     // chunk issued after its own weight DMA (they, and that DMA, may stay in flight)
+#ifdef FV3_B3_TRACE
+    long long wait_cyc = 0;  // trace only: wave 0's cycles in the chunk waits of this tile
+#endif
     auto advance = [&](int younger) {
+#ifdef FV3_B3_TRACE
+        const long long tw0 = p.trace ? (long long)__builtin_amdgcn_s_memtime() : 0;
+#endif
         // (two slots: the DMA this chunk issued is chunk +1 itself, so none of it may stay)
         if constexpr (GL) vm_wait_le((NSL == 3 ? nst_w : 0) + younger);
         b3_barrier();
+#ifdef FV3_B3_TRACE
+        if (p.trace) wait_cyc += (long long)__builtin_amdgcn_s_memtime() - tw0;
+#endif
         slot = GL ? (slot == NSL - 1 ? 0 : slot + 1) : (slot ^ 1);
         jn2 = jn2 + 1 == p.nch ? 0 : jn2 + 1;
     };
@@ -624,7 +638,30 @@ dense_b3_kernel(B3Args pa)
     if constexpr (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     b3_barrier();  // constants and chunk 0 visible
 
+    // trace slot: thread 0 of the block writes tile t's record.  Only in the tools/ trace
+    // variant (FV3_B3_TRACE): the clock reads are scheduling barriers that change the
+    // product kernel's instruction order even when the pointer is NULL
+    auto mark = [&](int slot) {
+#ifdef FV3_B3_TRACE
+        if (p.trace && tid == 0) {
+            long long* r = p.trace + tile * 8;
+            if (slot == 0) {
+                r[4] = (long long)__smid();
+                r[5] = (long long)__builtin_amdgcn_s_memtime();
+                wait_cyc = 0;
+            }
+            if (slot == 3) {
+                r[6] = (long long)__builtin_amdgcn_s_memtime();
+                r[7] = wait_cyc;
+            }
+            r[slot] = wall_clock64();
+        }
+#else
+        (void)slot;
+#endif
+    };
     for (; tile < p.ntiles; tile += gridDim.x) {
+        mark(0);
         oblk = lblk;
         oii = lii;
         ovalid = lvalid;
@@ -660,6 +697,7 @@ dense_b3_kernel(B3Args pa)
             }
         }
         hidden_epi(0);
+        mark(1);
         // ---- further hidden layers ----
         for (int l = 0; l < p.nhx; ++l) {
             zero_acc();
@@ -671,6 +709,7 @@ dense_b3_kernel(B3Args pa)
         }
         if constexpr (NS == 3)
             sfor<KS>([&](auto cc) { splitN<NS>(Y[decltype(cc)::value], B[decltype(cc)::value]); });
+        mark(2);
         // ---- output layer, two 16-row tiles per chunk; the next tile's inputs start loading ----
         const int64_t nt = tile + gridDim.x;
         if (nt < p.ntiles) {
@@ -716,6 +755,7 @@ dense_b3_kernel(B3Args pa)
             out_tile(accP[0], 2 * p.n_oc - 2, resP[0]);
             out_tile(accP[1], 2 * p.n_oc - 1, resP[1]);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's inputs landed
+            mark(3);
             continue;
         }
         for (int oc = 0; oc < p.n_oc; ++oc) {
@@ -739,6 +779,7 @@ dense_b3_kernel(B3Args pa)
         }
         out_tile(accP[0], 2 * p.n_oc - 2, resP[0]);
         out_tile(accP[1], 2 * p.n_oc - 1, resP[1]);
+        mark(3);
     }
 }
 
@@ -1004,6 +1045,7 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
     a.any_log = b.any_log;
     a.ncol = ncol;
     a.ncol_blk = nb;
+    a.trace = m->tmpl.trace;
     for (size_t g = 0; g < b.gmeta.size(); ++g) a.gmeta[g] = b.gmeta[g];
     for (size_t g = 0; g < b.otile.size(); ++g) a.otile[g] = b.otile[g];
     // the epilogue addresses outputs / residual inputs with 32-bit byte offsets

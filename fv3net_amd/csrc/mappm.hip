@@ -322,6 +322,17 @@ int64_t cs_grid(const MappmArgs& a, int block)
 
 }  // namespace
 
+// Block size of the one-lane-per-column kord <= 7 kernels.  Each lane walks its column
+// serially, so a launch is as long as its busiest CU's share of waves: 256-lane blocks
+// on a mid-size grid (one rank's C384 band at world 8, 110,592 columns = 432 blocks on
+// 256 CUs) leave 176 CUs with 8 waves and 80 with 4; 64-lane blocks deal the same 1,728
+// waves 6-7 per CU.  FV3_MAPPM_BLOCK=64|256 forces one (A/B; same results).
+int ppm_block(int64_t ncol)
+{
+    if (const char* e = getenv("FV3_MAPPM_BLOCK")) return atoi(e) == 64 ? 64 : 256;
+    return ncol < (int64_t)4 * 256 * 256 ? 64 : 256;
+}
+
 // kord <= 7: the level-parallel kernel while one lane per column leaves the chip
 // mostly idle (FV3_MAPPM_PATH=serial|levels overrides, for tests and A/B).
 bool use_levels_kernel(const MappmArgs& a)
@@ -360,7 +371,7 @@ int launch_mappm(MappmArgs a, hipStream_t stream)
         FV3_REQUIRE(a.ncol <= 0x7fffffff, "mappm: ncol too large for the level-parallel path");
         hipLaunchKernelGGL(mappm_ppm_levels_kernel, dim3((unsigned)a.ncol), dim3(block), lds, stream, a);
     } else {
-        const int block = 256;
+        const int block = ppm_block(a.ncol);
         const int64_t grid = (a.ncol + block - 1) / block;
         hipLaunchKernelGGL(mappm_ppm_kernel, dim3((unsigned)grid), dim3(block), 0, stream, a);
     }
@@ -488,7 +499,7 @@ extern "C" int fv3_mappm_multi(const float* pe1, fv3_layout pe1_l, const float* 
         for (; f + 2 <= n_fields; f += 2) {
             fv3::MappmPairArgs a{pe1, pe2, pe1_l, pe2_l, {q1[f], q1[f + 1]}, {q2[f], q2[f + 1]},
                                  {q1_l[f], q1_l[f + 1]}, {q2_l[f], q2_l[f + 1]}, ncol, km, kn, iv, kord};
-            const int block = 256;
+            const int block = fv3::ppm_block(ncol);
             const int64_t grid = (ncol + block - 1) / block;
             hipLaunchKernelGGL(fv3::mappm_ppm_pair_kernel, dim3((unsigned)grid), dim3(block), 0, s, a);
             FV3_LAUNCH_CHECK();

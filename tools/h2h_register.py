@@ -133,6 +133,29 @@ def main():
     res["registered_bit_identical_to_predict"] = bool(same)
     res["host_bytes_per_call"] = T.nbytes + q.nbytes + sum(h.nbytes for h in out_h)
     res["columns_per_call"] = ny * nx
+
+    # one C384 float64 field (560 MB) in and a float32 one (280 MB) out: the pinned
+    # staging of fv3net_amd.transfer against registering the caller's pages per call
+    from fv3net_amd import transfer
+
+    big = np.random.default_rng(1).normal(size=(6, 79, 384, 384))
+    dbig = torch.empty(big.shape, dtype=torch.float64, device=dev)
+    hout = np.empty(big.shape, np.float32)
+    dout = torch.empty(big.shape, dtype=torch.float32, device=dev)
+
+    def staged_big():
+        transfer.h2d(big, out=dbig)
+        transfer.d2h(dout, out=hout)
+
+    def reg_big():
+        with transfer.HostPages([big, hout]) as p:
+            assert len(p._registered) == 2
+            dbig.copy_(torch.from_numpy(big), non_blocking=True)
+            torch.from_numpy(hout).copy_(dout, non_blocking=True)
+
+    res["c384_field_staged_ms"] = timeit(staged_big, n=5, warm=1)
+    res["c384_field_registered_ms"] = timeit(reg_big, n=5, warm=1)
+    res["c384_field_bytes"] = big.nbytes + hout.nbytes
     print(json.dumps(res), flush=True)
 
 

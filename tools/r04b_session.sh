@@ -13,6 +13,8 @@ timeout -k 10 120 python3 tools/mappm_time.py > $OUT/mappm_time_r04b_new.log 2>&
 FV3_MAPPM_CS_ROUNDS=1 timeout -k 10 120 python3 tools/mappm_time.py > $OUT/mappm_time_r04b_old2.log 2>&1 || exit $?
 timeout -k 10 120 python3 tools/mappm_time.py > $OUT/mappm_time_r04b_new2.log 2>&1 || exit $?
 head -2 $OUT/mappm_time_r04b_*.log
+for b in 256 64 256 64; do FV3_MAPPM_BLOCK=$b timeout -k 10 120 python3 tools/mappm_block_ab.py >> $OUT/mappm_block_r04b.log 2>&1 || exit $?; done
+cat $OUT/mappm_block_r04b.log
 timeout -k 10 300 python3 tools/rank_share.py > $OUT/rank_share_r04b.json 2> $OUT/rank_share_r04b.err || exit $?
 timeout -k 10 180 python3 tools/h2h_register.py > $OUT/h2h_register_r04b.json 2> $OUT/h2h_register_r04b.err || exit $?
 echo done
