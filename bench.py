@@ -314,7 +314,8 @@ def rank_share_legs(dev, settle_ms=150.0, world=8):
         "ratio_to_full_over_world": rec[world]["step_ms"] / (rec[1]["step_ms"] / world),
         "predict_ratio_to_full_over_world": rec[world]["predict_ms"] / (rec[1]["predict_ms"] / world),
         "exchange_bytes_per_rank_per_step": rec[world]["exchange_bytes"],
-        "note": "wall clock per step (predict + fused epilogue + row partials + fold); exchange stubbed by a local "
+        "note": "wall clock per step (predict + fused epilogue + row partials + limiter counts + fold, every "
+                "launch marshalled once: workloads.ShardedStepperWorkload._bind); exchange stubbed by a local "
                 "copy of the gathered bytes"}
     # config #5: C384 emulator, 110,592 columns per rank at world 8
     for prec in ("bf16x3", "f32"):
@@ -621,7 +622,8 @@ def extra_measurements(dev, settle_ms=150.0):
     wall, t = timed_steps(wl.step, 20, 3, settle_ms=settle_ms)
     out["stepper_c96"] = with_counters("stepper_c96", {
         "columns_per_s": wl.ncol / (wall / 20), "ms_per_step": wall / 20 * 1e3,
-        "note": "wall clock per step (several kernels + host glue); counters: the fused epilogue kernel"})
+        "note": "wall clock per step (predict, fused epilogue, area partials: three C-ABI calls marshalled once, "
+                "workloads.StepperWorkload._bind); counters: the fused epilogue kernel"})
     del wl
     # the same step with the predict on the bf16x6 split kernel (1e-5 per level like the
     # f32 kernel); the float64 state is cast into bound float32 buffers each step

@@ -115,3 +115,20 @@ def level_layout(t, level_axis: int):
             raise ValueError(f"the block axes of a {shape} tensor with strides {st} do not flatten")
     ld = st[level_axis] if nz > 1 else plane
     return _native.layout(plane, ld, blk_stride), nblk * plane, nz
+
+
+class BoundLaunch:
+    """One C-ABI launch marshalled once over fixed device buffers, re-issued per call
+    with only the stream handle added: ``fn(*args, stream)``.  ``keep``: the tensors it
+    touches (kept alive, and ordered on a side stream like stream_handle does);
+    ``result``: what a call returns (its buffers are rewritten each time)."""
+
+    def __init__(self, fn, args, keep, what: str, result=None):
+        self.fn, self.args, self.keep, self.what, self.result = fn, tuple(args), list(keep), what, result
+
+    def __call__(self, stream=None):
+        h = stream if isinstance(stream, int) else stream_handle(stream, self.keep)
+        st = self.fn(*self.args, h)
+        if st:
+            _native.check(st, self.what)
+        return self.result

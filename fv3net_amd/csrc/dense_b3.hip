@@ -71,6 +71,27 @@ constexpr bool kB3GldsDefault = true;
 #define FV3_B3_FR 4
 #endif
 constexpr int kFR = FV3_B3_FR;
+// instruction order inside a chunk (A/B, same results): 0 = the compiler's; 1 = the next
+// pair's fragment reads pinned ahead of this pair's MFMAs (a scheduling barrier between
+// them, so the waits before the MFMAs leave the younger reads in flight); 2 = the same
+// order as scheduling-group hints (DS reads, then MFMAs, VALU free to fill in)
+#ifndef FV3_B3_SCHED
+#define FV3_B3_SCHED 0
+#endif
+__device__ __forceinline__ void b3_sched_pair()
+{
+#if FV3_B3_SCHED == 1
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+template <int NRD, int NMF>
+__device__ __forceinline__ void b3_sched_groups()
+{
+#if FV3_B3_SCHED == 2
+    __builtin_amdgcn_sched_group_barrier(0x100, NRD, 0);  // DS reads
+    __builtin_amdgcn_sched_group_barrier(0x008, NMF, 0);  // MFMAs
+#endif
+}
 // weight ring slots: SL (LDS-DMA pipeline: 3, or 2 where three chunks do not fit, e.g.
 // bf16x6 at width 256), 0 = the register-staged pipeline (2 slots)
 constexpr int b3_slots(int sl) { return sl > 0 ? sl : 2; }
@@ -431,7 +452,10 @@ dense_b3_kernel(B3Args pa)
                 frag(slot, t0 + kFR - 2, fa[(t0 + kFR - 2) % kFR]);
                 frag(slot, t1 + kFR - 2, fa[(t1 + kFR - 2) % kFR]);
             }
+            b3_sched_pair();
             mma_x2<NS>(fa[t0 % kFR], bx, acc[t0], fa[t1 % kFR], bx, acc[t1]);
+            b3_sched_groups<(t0 + kFR - 2 < HU) ? 2 * NS : 0, 2 * SplitTerms<NS>::n>();
+            b3_sched_pair();
         });
         advance(younger);
     };
@@ -555,7 +579,10 @@ dense_b3_kernel(B3Args pa)
                 frag(slot, i0 + kFR - 2, fa[(i0 + kFR - 2) % kFR]);
                 frag(slot, i1 + kFR - 2, fa[(i1 + kFR - 2) % kFR]);
             }
+            b3_sched_pair();
             mma_x2<NS>(fa[i0 % kFR], B[q], acc[0], fa[i1 % kFR], B[q], acc[1]);
+            b3_sched_groups<(i0 + kFR - 2 < HU) ? 2 * NS : 0, 2 * SplitTerms<NS>::n>();
+            b3_sched_pair();
         });
     };
 

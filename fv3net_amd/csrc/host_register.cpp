@@ -14,6 +14,16 @@ extern "C" int fv3_host_register(void* ptr, size_t bytes)
     using namespace fv3;
     clear_error();
     FV3_REQUIRE(ptr && bytes, "host_register: NULL pointer or zero size");
+    // Already page-locked (hipHostMalloc, or registered by the caller or an enclosing
+    // call): leave it to its owner.  The runtime accepts a second registration of the
+    // same range, and releasing it here could unpin memory the owner still relies on.
+    hipPointerAttribute_t at{};
+    const hipError_t q = hipPointerGetAttributes(&at, ptr);
+    if (q != hipSuccess) (void)hipGetLastError();
+    if (q == hipSuccess && at.type != hipMemoryTypeUnregistered) {
+        set_error("host_register: memory already page-locked or not host memory");
+        return FV3_ERR_UNSUPPORTED;
+    }
     const hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterDefault);
     if (e != hipSuccess) {
         // already registered (by the caller, or pages shared with another array) or not

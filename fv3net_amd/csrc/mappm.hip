@@ -283,55 +283,35 @@ __global__ __launch_bounds__(64) void mappm_cs_kernel(MappmArgs a)
     mappm_cs_column(col, scr, a.km, a.kn, a.iv, a.kord);
 }
 
-// Grid-stride over the columns: thread slot s owns scratch column s and reuses it for
-// columns s, s + S, s + 2S, ... (S = grid threads).  The host sizes the grid to the
-// chip's resident threads, so the scratch is ~0.2 GB at km = 79 instead of one column
-// per grid column (0.58 GB at C384): it stays within the 256 MB MALL, and every
-// thread's write -> read-back round trip (forward sweep, back-substitution, stream)
-// is served on chip rather than from HBM.
+// NT > 0: the bottom NT edges of the solve stay in registers (mappm_cs_column), 6 NT
+// fewer scratch accesses per column; the scratch keeps its full [2][km+3] shape
+template <int NT>
 __global__ __launch_bounds__(256) void mappm_cs_global_kernel(MappmArgs a)
 {
-    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.ncol) return;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    GlobalScr scr{a.scratch + slot, stride, (int64_t)(a.km + 3) * stride};
-    for (int64_t c = slot; c < a.ncol; c += stride) {
-        DevCol col = make_col(a, c);
-        mappm_cs_column(col, scr, a.km, a.kn, a.iv, a.kord);
-    }
+    GlobalScr scr{a.scratch + c, stride, (int64_t)(a.km + 3) * stride};
+    DevCol col = make_col(a, c);
+    mappm_cs_column<DevCol, GlobalScr, NT>(col, scr, a.km, a.kn, a.iv, a.kord);
 }
 
-// Grid of the kord > 7 kernel: the fewest grid-stride rounds the resident capacity
-// allows, then as few threads as give that many rounds (every slot runs the same
-// number of columns, up to one).  FV3_MAPPM_CS_ROUNDS=n forces n rounds (A/B).
-int64_t cs_grid(const MappmArgs& a, int block)
+// register-tail depth of the kord > 7 kernel; FV3_MAPPM_CS_NT=0|16|32|48 selects one
+// (A/B: every depth gives the same bits)
+constexpr int kCsTailDefault = 32;
+const void* cs_global_kernel()
 {
-    static int cap = 0;  // resident blocks of the kernel on the whole chip
-    if (!cap) {
-        int dev = 0, n_cu = 0, per_cu = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mappm_cs_global_kernel, block, 0) != hipSuccess)
-            return -1;
-        cap = std::max(1, n_cu * per_cu);
+    int nt = kCsTailDefault;
+    if (const char* e = getenv("FV3_MAPPM_CS_NT")) nt = atoi(e);
+    switch (nt) {
+    case 0: return (const void*)mappm_cs_global_kernel<0>;
+    case 16: return (const void*)mappm_cs_global_kernel<16>;
+    case 48: return (const void*)mappm_cs_global_kernel<48>;
+    default: return (const void*)mappm_cs_global_kernel<32>;
     }
-    const int64_t blocks = (a.ncol + block - 1) / block;
-    int64_t rounds = (blocks + cap - 1) / cap;
-    if (const char* e = getenv("FV3_MAPPM_CS_ROUNDS")) rounds = std::max<int64_t>(1, atoll(e));
-    return std::max<int64_t>(1, (blocks + rounds - 1) / rounds);
 }
 
 }  // namespace
-
-// Block size of the one-lane-per-column kord <= 7 kernels.  Each lane walks its column
-// serially, so a launch is as long as its busiest CU's share of waves: 256-lane blocks
-// on a mid-size grid (one rank's C384 band at world 8, 110,592 columns = 432 blocks on
-// 256 CUs) leave 176 CUs with 8 waves and 80 with 4; 64-lane blocks deal the same 1,728
-// waves 6-7 per CU.  FV3_MAPPM_BLOCK=64|256 forces one (A/B; same results).
-int ppm_block(int64_t ncol)
-{
-    if (const char* e = getenv("FV3_MAPPM_BLOCK")) return atoi(e) == 64 ? 64 : 256;
-    return ncol < (int64_t)4 * 256 * 256 ? 64 : 256;
-}
 
 // kord <= 7: the level-parallel kernel while one lane per column leaves the chip
 // mostly idle (FV3_MAPPM_PATH=serial|levels overrides, for tests and A/B).
@@ -349,11 +329,11 @@ int launch_mappm(MappmArgs a, hipStream_t stream)
     if (a.ncol == 0) return FV3_OK;
     if (a.kord > 7 && !getenv("FV3_MAPPM_LDS")) {
         const int block = 256;
-        const int64_t grid = cs_grid(a, block);
-        FV3_REQUIRE_CODE(FV3_ERR_HIP, grid > 0, "mappm: occupancy query for the kord>7 kernel failed");
+        const int64_t grid = (a.ncol + block - 1) / block;
         FV3_HIP(hipMallocAsync((void**)&a.scratch, sizeof(float) * 2 * (size_t)(a.km + 3) * (size_t)grid * block,
                                stream));
-        hipLaunchKernelGGL(mappm_cs_global_kernel, dim3((unsigned)grid), dim3(block), 0, stream, a);
+        void* kargs[] = {&a};
+        FV3_HIP(hipLaunchKernel(cs_global_kernel(), dim3((unsigned)grid), dim3(block), kargs, 0, stream));
         FV3_LAUNCH_CHECK();
         FV3_HIP(hipFreeAsync(a.scratch, stream));
         return FV3_OK;
@@ -371,7 +351,7 @@ int launch_mappm(MappmArgs a, hipStream_t stream)
         FV3_REQUIRE(a.ncol <= 0x7fffffff, "mappm: ncol too large for the level-parallel path");
         hipLaunchKernelGGL(mappm_ppm_levels_kernel, dim3((unsigned)a.ncol), dim3(block), lds, stream, a);
     } else {
-        const int block = ppm_block(a.ncol);
+        const int block = 256;
         const int64_t grid = (a.ncol + block - 1) / block;
         hipLaunchKernelGGL(mappm_ppm_kernel, dim3((unsigned)grid), dim3(block), 0, stream, a);
     }
@@ -499,7 +479,7 @@ extern "C" int fv3_mappm_multi(const float* pe1, fv3_layout pe1_l, const float* 
         for (; f + 2 <= n_fields; f += 2) {
             fv3::MappmPairArgs a{pe1, pe2, pe1_l, pe2_l, {q1[f], q1[f + 1]}, {q2[f], q2[f + 1]},
                                  {q1_l[f], q1_l[f + 1]}, {q2_l[f], q2_l[f + 1]}, ncol, km, kn, iv, kord};
-            const int block = fv3::ppm_block(ncol);
+            const int block = 256;
             const int64_t grid = (ncol + block - 1) / block;
             hipLaunchKernelGGL(fv3::mappm_ppm_pair_kernel, dim3((unsigned)grid), dim3(block), 0, s, a);
             FV3_LAUNCH_CHECK();

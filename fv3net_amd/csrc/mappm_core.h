@@ -753,12 +753,25 @@ FV3_HD inline void mappm_ppm_column_by_output(Col& c, int km, int kn, int iv, in
 // ---- one column, kord > 7 (cs_profile path) ----
 //
 // `Scr` is per-column scratch of 2*(km+2) floats: edge(k) for k = 1..km+1 and
-// gam(k), addressed by scr.e(k) / scr.g(k) (LDS on the device).
-template <class Col, class Scr>
+// gam(k), addressed by scr.e(k) / scr.g(k) (global memory or LDS on the device).
+//
+// NT > 0 (iv != -2, km >= NT + 1): the bottom NT edges never touch the scratch.  The
+// forward sweep keeps the last NT - 1 levels' (edge, gam) in registers, the
+// back-substitution runs over them first (fully unrolled, static register indices) and
+// leaves the solved edges kt..km+1 (kt = km + 2 - NT) in registers, and the main loop,
+// which reads every edge exactly once in increasing k, takes them from the front of that
+// register queue.  Same operations in the same order on the same values: the bits are
+// those of the all-scratch path, with 6 NT fewer scratch accesses per column (the
+// scratch round trips are most of kord > 7's HBM traffic).
+template <class Col, class Scr, int NT = 0>
 FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int kord)
 {
     const int akord = kord < 0 ? -kord : kord;
     const float qs = 0.0f;  // mappm passes an uninitialised qs (mappm.f90:33,49)
+    constexpr int NTR = NT > 0 ? NT : 1;
+    const bool tail = NT > 0 && iv != -2 && km >= NT + 1;
+    const int kt = tail ? km + 2 - NT : km + 2;  // first edge held in registers
+    float te[NTR], tg[NTR];                      // edge / gam of levels kt + j
 
     // ---- tridiagonal edge solve (mappm.f90:153-205): forward sweep into scratch ----
     {
@@ -807,7 +820,7 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
             float pek = pe1v;
             float qkm1 = qm1;
             float qk = qm1;
-            for (int k = 2; k <= km; ++k) {
+            auto sweep = [&](int k, float& e_out, float& g_out) {
                 qk = c.q1(k);
                 const float pen = c.pe1(k + 1);
                 const float dpk = pen - pek;
@@ -815,21 +828,54 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
                 bet = 2.0f + d4 + d4 - gprev;
                 qprev = (3.0f * (qkm1 + d4 * qk) - qprev) / bet;
                 gprev = d4 / bet;
-                scr.e(k) = qprev;
-                scr.g(k) = gprev;
+                e_out = qprev;
+                g_out = gprev;
                 qkm1 = qk; dpm1 = dpk; pek = pen;
+            };
+            const int kend = tail ? kt - 1 : km;
+            for (int k = 2; k <= kend; ++k) sweep(k, scr.e(k), scr.g(k));
+            if constexpr (NT > 0) {
+                if (tail) {
+#pragma unroll
+                    for (int j = 0; j < NT - 1; ++j) sweep(kt + j, te[j], tg[j]);  // k = kt .. km
+                }
             }
             // qkm1 == qk == q(km) here; need q(km-1)
             const float a_bot = 1.0f + d4 * (d4 + 1.5f);
             const float qkmm1 = c.q1(km - 1);
             float qn = (2.0f * d4 * (d4 + 1.0f) * qk + qkmm1 - a_bot * qprev) / (d4 * (d4 + 0.5f) - a_bot * gprev);
-            scr.e(km + 1) = qn;
-            for (int k = km; k >= 1; --k) {
+            int kb = km;  // back-substitution continues in the scratch from here
+            if constexpr (NT > 0) {
+                if (tail) {
+                    te[NT - 1] = qn;  // e(km+1)
+#pragma unroll
+                    for (int j = NT - 2; j >= 0; --j) {
+                        qn = te[j] - tg[j] * qn;
+                        te[j] = qn;
+                    }
+                    kb = kt - 1;
+                }
+            }
+            if (!tail) scr.e(km + 1) = qn;
+            for (int k = kb; k >= 1; --k) {
                 qn = scr.e(k) - scr.g(k) * qn;
                 scr.e(k) = qn;
             }
         }
     }
+    // solved edge e(k), read once per k in increasing k by edge_c below: the register
+    // queue's front from kt on
+    auto e_at = [&](int k) -> float {
+        if constexpr (NT > 0) {
+            if (tail && k >= kt) {
+                const float v = te[0];
+#pragma unroll
+                for (int j = 0; j + 1 < NT; ++j) te[j] = te[j + 1];
+                return v;
+            }
+        }
+        return scr.e(k);
+    };
 
     const ColumnEnds ends{c.pe1(1), c.pe1(km + 1), c.q1(1), c.q1(km)};
     RemapState s{1, false, 0.0f, 0.0f, c.pe2(1), c.pe2(2)};
@@ -837,7 +883,7 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
     // constrained edge qc(k) (mappm.f90:207-260) from the solved edge e(k) and
     // q1(k-2..k+1); the large-scale constraints use gam(k) = q1(k) - q1(k-1).
     auto edge_c = [&](int k, float qkm2, float qkm1, float qk0, float qkp1) -> float {
-        float q = scr.e(k);
+        float q = e_at(k);
         if (akord > 16 || k <= 1 || k >= km + 1) return q;
         if (k == 2 || k == km) {
             q = fmin2(q, fmax2(qkm1, qk0));

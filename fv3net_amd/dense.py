@@ -431,12 +431,13 @@ class BoundForward:
         model._last_bound = self
 
     def __call__(self, stream=None):
+        """``stream``: a torch stream, a raw hipStream_t handle (int), or None (current)."""
+        h = stream if isinstance(stream, int) else _device.stream_handle(stream, self.inputs + self.outputs)
         if self._in64:
-            st = self._fn(self._handle, self._in_ptrs, self._in_l, self._out_ptrs, self._out_l, self._ncol,
-                          _device.stream_handle(stream, self.inputs + self.outputs))
+            st = self._fn(self._handle, self._in_ptrs, self._in_l, self._out_ptrs, self._out_l, self._ncol, h)
         else:
             st = self._fn(self._handle, self._in_ptrs, self._in_l, self._out_ptrs, self._out_l, self._ncol,
-                          self._prec, _device.stream_handle(stream, self.inputs + self.outputs))
+                          self._prec, h)
         if st:
             _native.check(st, "dense_forward")
         return self.outputs

@@ -72,12 +72,7 @@ def segment_view(arr, seg: Segment):
     return arr[seg.tile, :, seg.y0:seg.y1]
 
 
-def area_weighted_partials(diags: Sequence, area, stream=None):
-    """Device float64 partials [n_diag, 2] = (sum(area * x_d), sum(area)) over this
-    rank's columns, computed by the deterministic two-stage HIP reduction
-    (csrc/reduce.hip).  ``diags``: CUDA tensors shaped like ``area``.  As numpy's
-    ``area * ds`` promotes, any float64 operand puts the whole reduction on the float64
-    kernel (float32 operands widened exactly); all-float32 inputs use the float32 one."""
+def _area_partials_setup(diags, area, out=None):
     _device.require_gpu()
     wide = any(_is_f64(t) for t in [area, *diags])
     if wide:
@@ -89,15 +84,37 @@ def area_weighted_partials(diags: Sequence, area, stream=None):
     for d in xs:
         if d.shape != area.shape:
             raise ValueError(f"diagnostic shape {tuple(d.shape)} != area shape {tuple(area.shape)}")
-    out = torch.empty((len(xs), 2), dtype=torch.float64, device=area.device)
-    if not xs:
-        return out
-    tab = (ctypes.c_void_p * len(xs))(*[d.data_ptr() for d in xs])
+    if out is None:
+        out = torch.empty((len(xs), 2), dtype=torch.float64, device=area.device)
+    elif not (out.dtype == torch.float64 and tuple(out.shape) == (len(xs), 2) and out.is_contiguous()):
+        raise ValueError(f"out must be a contiguous [{len(xs)}, 2] float64 tensor")
+    tab = (ctypes.c_void_p * max(len(xs), 1))(*[d.data_ptr() for d in xs])
     lib = _native.load()
     fn = lib.fv3_area_weighted_sums_f64 if wide else lib.fv3_area_weighted_sums
-    st = fn(tab, len(xs), area.data_ptr(), area.numel(), out.data_ptr(), _device.stream_handle(stream, [area, out] + xs))
+    return fn, (tab, len(xs), area.data_ptr(), area.numel(), out.data_ptr()), [area, out] + xs, out, len(xs)
+
+
+def area_weighted_partials(diags: Sequence, area, stream=None):
+    """Device float64 partials [n_diag, 2] = (sum(area * x_d), sum(area)) over this
+    rank's columns, computed by the deterministic two-stage HIP reduction
+    (csrc/reduce.hip).  ``diags``: CUDA tensors shaped like ``area``.  As numpy's
+    ``area * ds`` promotes, any float64 operand puts the whole reduction on the float64
+    kernel (float32 operands widened exactly); all-float32 inputs use the float32 one."""
+    fn, args, keep, out, n = _area_partials_setup(diags, area)
+    if not n:
+        return out
+    st = fn(*args, _device.stream_handle(stream, keep))
     _native.check(st, "area_weighted_sums")
     return out
+
+
+def bind_area_weighted_partials(diags: Sequence, area, out=None) -> "_device.BoundLaunch":
+    """area_weighted_partials over fixed buffers, marshalled once (the per-step reduction
+    of the stepper's diagnostics); each call rewrites and returns ``out``."""
+    fn, args, keep, out, n = _area_partials_setup(diags, area, out)
+    if not n:
+        raise ValueError("no diagnostics to reduce")
+    return _device.BoundLaunch(fn, args, keep, "area_weighted_sums", out)
 
 
 def _backend_device(group=None):
@@ -157,9 +174,7 @@ def globally_average_2d_diagnostics(diagnostics: dict, exclude: Sequence[str] = 
     return {k: float(m) for k, m in zip(names, means)}
 
 
-def level_sums(field, stream=None):
-    """Device float64 per-level horizontal sums of a (z, ...) field (deterministic
-    fixed-tree HIP reduction): the per-rank part of metrics.py:27-32."""
+def _level_sums_setup(field, out=None):
     _device.require_gpu()
     lib = _native.load()
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -175,10 +190,27 @@ def level_sums(field, stream=None):
     except ValueError:
         t = t.contiguous()
         lay, ncol, nz = _device.level_layout(t, 0)
-    out = torch.empty(nz, dtype=torch.float64, device=t.device)
-    st = fn(t.data_ptr(), lay, ncol, nz, out.data_ptr(), _device.stream_handle(stream, [t, out]))
+    if out is None:
+        out = torch.empty(nz, dtype=torch.float64, device=t.device)
+    elif not (out.dtype == torch.float64 and out.numel() == nz and out.is_contiguous()):
+        raise ValueError(f"out must be a contiguous float64 tensor of {nz} values")
+    return fn, (t.data_ptr(), lay, ncol, nz, out.data_ptr()), [t, out], out
+
+
+def level_sums(field, stream=None):
+    """Device float64 per-level horizontal sums of a (z, ...) field (deterministic
+    fixed-tree HIP reduction): the per-rank part of metrics.py:27-32."""
+    fn, args, keep, out = _level_sums_setup(field)
+    st = fn(*args, _device.stream_handle(stream, keep))
     _native.check(st, "level_sums")
     return out
+
+
+def bind_level_sums(field, out=None) -> "_device.BoundLaunch":
+    """level_sums of a fixed device field into a fixed ``out`` (e.g. a slice of a wider
+    result buffer), marshalled once."""
+    fn, args, keep, out = _level_sums_setup(field, out)
+    return _device.BoundLaunch(fn, args, keep, "level_sums", out)
 
 
 def globally_sum_3d_diagnostics(diagnostics: dict, include: Sequence[str], group=None) -> dict:
@@ -217,10 +249,7 @@ def _f64_on_device(t, dev):
     return t.to(dev, torch.float64).contiguous()
 
 
-def area_row_partials(diags: Sequence, area, stream=None, out=None):
-    """Device float64 [nrows, n_diag, 2]: per row of (rows, row_len) fields,
-    (sum area*x_d, sum area).  float64 if any operand is (numpy's promotion).  ``out``:
-    a [nrows, W >= 2 n_diag] float64 buffer whose leading columns receive them."""
+def _area_row_setup(diags, area, out=None):
     _device.require_gpu()
     wide = any(_is_f64(t) for t in [area, *diags])
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -240,16 +269,32 @@ def area_row_partials(diags: Sequence, area, stream=None, out=None):
     elif not (out.dtype == torch.float64 and out.dim() == 2 and out.shape[0] == nrows and out.stride(1) == 1
               and out.shape[1] >= 2 * len(xs)):
         raise ValueError(f"out must be a row-major [{nrows}, >= {2 * len(xs)}] float64 buffer")
-    if not xs or nrows == 0:
-        return out
-    tab = (ctypes.c_void_p * len(xs))(*[d.data_ptr() for d in xs])
+    tab = (ctypes.c_void_p * max(len(xs), 1))(*[d.data_ptr() for d in xs])
     lib = _native.load()
     fn = lib.fv3_area_weighted_row_sums_f64 if wide else lib.fv3_area_weighted_row_sums
     ld = out.stride(0) if out.dim() == 2 else 2 * len(xs)
-    st = fn(tab, len(xs), area.data_ptr(), nrows, row_len, out.data_ptr(), ld,
-            _device.stream_handle(stream, [area, out] + xs))
+    args = (tab, len(xs), area.data_ptr(), nrows, row_len, out.data_ptr(), ld)
+    return fn, args, [area, out] + xs, out, bool(xs) and nrows > 0
+
+
+def area_row_partials(diags: Sequence, area, stream=None, out=None):
+    """Device float64 [nrows, n_diag, 2]: per row of (rows, row_len) fields,
+    (sum area*x_d, sum area).  float64 if any operand is (numpy's promotion).  ``out``:
+    a [nrows, W >= 2 n_diag] float64 buffer whose leading columns receive them."""
+    fn, args, keep, out, work = _area_row_setup(diags, area, out)
+    if not work:
+        return out
+    st = fn(*args, _device.stream_handle(stream, keep))
     _native.check(st, "area_weighted_row_sums")
     return out
+
+
+def bind_area_row_partials(diags: Sequence, area, out=None) -> "_device.BoundLaunch":
+    """area_row_partials over fixed buffers, marshalled once; each call rewrites ``out``."""
+    fn, args, keep, out, work = _area_row_setup(diags, area, out)
+    if not work:
+        raise ValueError("no rows or diagnostics to reduce")
+    return _device.BoundLaunch(fn, args, keep, "area_weighted_row_sums", out)
 
 
 def level_row_partials(field, stream=None, out=None):
@@ -315,17 +360,32 @@ def gather_rows(local, group=None, counts: Optional[Sequence[int]] = None):
     return torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
 
 
-def fold_rows(rows, stream=None):
-    """Device float64 sums over the rows of [nrows, ...] partials, in row order (HIP)."""
+def _fold_setup(rows, out=None):
     _device.require_gpu()
     r = rows.to(torch.device("cuda", torch.cuda.current_device()), torch.float64).contiguous()
     nrows = int(r.shape[0])
     width = int(r[0].numel()) if nrows else int(np.prod(r.shape[1:], dtype=np.int64))
-    out = torch.empty(tuple(r.shape[1:]), dtype=torch.float64, device=r.device)
-    st = _native.load().fv3_fold_rows(r.data_ptr(), nrows, width, out.data_ptr(),
-                                      _device.stream_handle(stream, [r, out]))
+    if out is None:
+        out = torch.empty(tuple(r.shape[1:]), dtype=torch.float64, device=r.device)
+    elif not (out.dtype == torch.float64 and out.numel() == width and out.is_contiguous()):
+        raise ValueError(f"out must be a contiguous float64 tensor of {width} values")
+    return _native.load().fv3_fold_rows, (r.data_ptr(), nrows, width, out.data_ptr()), [r, out], out
+
+
+def fold_rows(rows, stream=None):
+    """Device float64 sums over the rows of [nrows, ...] partials, in row order (HIP)."""
+    fn, args, keep, out = _fold_setup(rows)
+    st = fn(*args, _device.stream_handle(stream, keep))
     _native.check(st, "fold_rows")
     return out
+
+
+def bind_fold_rows(rows, out=None) -> "_device.BoundLaunch":
+    """fold_rows of a fixed [nrows, ...] float64 device buffer into ``out``, marshalled once."""
+    if not (torch.is_tensor(rows) and rows.is_cuda and rows.dtype == torch.float64 and rows.is_contiguous()):
+        raise ValueError("bind_fold_rows needs a contiguous float64 CUDA buffer (read in place every call)")
+    fn, args, keep, out = _fold_setup(rows, out)
+    return _device.BoundLaunch(fn, args, keep, "fold_rows", out)
 
 
 def global_row_sums(local_rows, group=None, counts: Optional[Sequence[int]] = None):

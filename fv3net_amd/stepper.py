@@ -62,21 +62,13 @@ def is_tendency_variable(key) -> bool:
 
 
 # ------------------------------------------------------------------------ kernels
-def ml_epilogue(dq1, dq2, sphum, delp, temperature, dt: float, physics_precip=None,
-                mse_conserving: bool = True, hydrostatic: bool = False, label: str = "machine_learning",
-                in_place: bool = False, level_axis: int = 0, stream=None, has_dq1: bool = True,
-                has_dq2: bool = True) -> Dict[str, object]:
-    """Limiter + diagnostics + apply for one (dQ1, dQ2) prediction, one kernel.
-
-    ``level_axis`` is the vertical axis of every 3-D array (axes before it are
-    blocks such as tiles).  Returns device tensors: limited ``dQ1``/``dQ2`` (pre-fillna, as the stepper
-    returns them), ``specific_humidity_limiter_active`` (uint8), the updated
-    ``air_temperature``/``specific_humidity`` (written into the inputs when
-    ``in_place``), the column diagnostics of COLUMN_DIAGNOSTICS and, with
-    ``physics_precip``, the new ``total_precipitation``.  ``has_dq1``/``has_dq2`` False:
-    the model lacks that tendency, pass zeros (machine_learning.py:258-259); its state
-    variable is left as it is and its column diagnostic is zero.
-    """
+def _epilogue_setup(dq1, dq2, sphum, delp, temperature, dt, physics_precip, mse_conserving, hydrostatic, label,
+                    in_place, level_axis, has_dq1, has_dq2, column=None):
+    """Validate and marshal one fv3_ml_epilogue_ex call: (args without the stream,
+    tensors the launch touches, the output dict).  ``column``: a [7, ncol] buffer of the
+    state dtype for the column diagnostics (allocated here when None); its last row may
+    be ``physics_precip`` itself (the kernel reads a column's precipitation before
+    writing the new total to the same element)."""
     _device.require_gpu()
     state_dtype = sphum.dtype if isinstance(sphum, torch.Tensor) else torch.float64
     if state_dtype not in (torch.float32, torch.float64):
@@ -107,7 +99,11 @@ def ml_epilogue(dq1, dq2, sphum, delp, temperature, dt: float, physics_precip=No
         TEMP: temperature if in_place else torch.empty_like(temperature),
         SPHUM: sphum if in_place else torch.empty_like(sphum),
     }
-    column = torch.empty((7, ncol), dtype=state_dtype, device=dev)
+    if column is None:
+        column = torch.empty((7, ncol), dtype=state_dtype, device=dev)
+    elif not (column.dtype == state_dtype and tuple(column.shape) == (7, ncol) and column.is_contiguous()
+              and column.device == dev):
+        raise ValueError(f"column must be a contiguous [7, {ncol}] {state_dtype} CUDA tensor")
     precip = None
     if physics_precip is not None:
         precip = st(physics_precip).reshape(-1)
@@ -119,16 +115,62 @@ def ml_epilogue(dq1, dq2, sphum, delp, temperature, dt: float, physics_precip=No
                             out["specific_humidity_limiter_active"].data_ptr(), out[TEMP].data_ptr(),
                             out[SPHUM].data_ptr(), column.data_ptr(), ncol)
     flags = (_native.EPI_HAS_DQ1 if has_dq1 else 0) | (_native.EPI_HAS_DQ2 if has_dq2 else 0)
-    st_ = _native.load().fv3_ml_epilogue_ex(ctypes_byref(io), lay, ncol, nz, int(state_dtype == torch.float64),
-                                            float(dt), int(bool(mse_conserving)), int(bool(hydrostatic)), flags,
-                                            _device.stream_handle(stream, [dq1, dq2, sphum, delp, temperature, precip,
-                                                                           column] + list(out.values())))
-    _native.check(st_, "ml_epilogue")
+    args = (ctypes_byref(io), lay, ncol, nz, int(state_dtype == torch.float64), float(dt), int(bool(mse_conserving)),
+            int(bool(hydrostatic)), flags)
+    keep = [dq1, dq2, sphum, delp, temperature, precip, column] + list(out.values())
     for i, name in enumerate(COLUMN_DIAGNOSTICS):
         if name == TOTAL_PRECIP and precip is None:
             continue
         out[name.format(label=label)] = column[i].reshape(col_shape)
+    return (io, args), keep, out
+
+
+def ml_epilogue(dq1, dq2, sphum, delp, temperature, dt: float, physics_precip=None,
+                mse_conserving: bool = True, hydrostatic: bool = False, label: str = "machine_learning",
+                in_place: bool = False, level_axis: int = 0, stream=None, has_dq1: bool = True,
+                has_dq2: bool = True) -> Dict[str, object]:
+    """Limiter + diagnostics + apply for one (dQ1, dQ2) prediction, one kernel.
+
+    ``level_axis`` is the vertical axis of every 3-D array (axes before it are
+    blocks such as tiles).  Returns device tensors: limited ``dQ1``/``dQ2`` (pre-fillna, as the stepper
+    returns them), ``specific_humidity_limiter_active`` (uint8), the updated
+    ``air_temperature``/``specific_humidity`` (written into the inputs when
+    ``in_place``), the column diagnostics of COLUMN_DIAGNOSTICS and, with
+    ``physics_precip``, the new ``total_precipitation``.  ``has_dq1``/``has_dq2`` False:
+    the model lacks that tendency, pass zeros (machine_learning.py:258-259); its state
+    variable is left as it is and its column diagnostic is zero.
+    """
+    (_, args), keep, out = _epilogue_setup(dq1, dq2, sphum, delp, temperature, dt, physics_precip, mse_conserving,
+                                           hydrostatic, label, in_place, level_axis, has_dq1, has_dq2)
+    st_ = _native.load().fv3_ml_epilogue_ex(*args, _device.stream_handle(stream, keep))
+    _native.check(st_, "ml_epilogue")
     return out
+
+
+class BoundEpilogue:
+    """``ml_epilogue`` validated and marshalled once over fixed device buffers, then one
+    C-ABI call per timestep (the prognostic loop applies the same state buffers every
+    step; the per-call Python of ``ml_epilogue`` costs more than the kernel on one rank's
+    band).  ``column``: as ``_epilogue_setup``; passing a buffer whose last row is the
+    state's precipitation accumulates the total in place.  Calling returns the same
+    output dict every time (its tensors are rewritten)."""
+
+    def __init__(self, dq1, dq2, sphum, delp, temperature, dt: float, physics_precip=None,
+                 mse_conserving: bool = True, hydrostatic: bool = False, label: str = "machine_learning",
+                 in_place: bool = True, level_axis: int = 0, has_dq1: bool = True, has_dq2: bool = True,
+                 column=None):
+        (self._io, self._args), self._keep, self.out = _epilogue_setup(
+            dq1, dq2, sphum, delp, temperature, dt, physics_precip, mse_conserving, hydrostatic, label, in_place,
+            level_axis, has_dq1, has_dq2, column)
+        self._fn = _native.load().fv3_ml_epilogue_ex
+
+    def __call__(self, stream=None) -> Dict[str, object]:
+        """``stream``: a torch stream, a raw hipStream_t handle (int), or None (current)."""
+        h = stream if isinstance(stream, int) else _device.stream_handle(stream, self._keep)
+        st_ = self._fn(*self._args, h)
+        if st_:
+            _native.check(st_, "ml_epilogue")
+        return self.out
 
 
 def tendency_columns(tendency, delp, dt: float, mode: str, level_axis: int = 0, stream=None) -> Dict[str, object]:

@@ -178,48 +178,49 @@ class StepperWorkload:
     bound: object = None
     precision: str = "f32"
     _in32: object = None
-    # every step after the first replays one HIP graph of the device part (graphs.py)
-    graph: bool = True
-    _graph: object = None
+    _epi: object = None
+    _part: object = None
 
-    def _device_step(self):
-        """predict + epilogue + partials on the current stream, fixed buffers: the state
-        is updated in place and the new precipitation copied back into its own buffer."""
-        from .distributed import area_weighted_partials
-        from .stepper import ml_epilogue
+    def _bind(self):
+        """Validate and marshal every launch of the step once (the predict, the fused
+        epilogue, the area partials): a step is then three C-ABI calls on fixed buffers.
+        The state's precipitation becomes the last row of the epilogue's column buffer,
+        so the kernel accumulates it in place (it reads a column's total before writing
+        the new one)."""
+        from .distributed import bind_area_weighted_partials
+        from .stepper import BoundEpilogue
 
         T, q = self.state["air_temperature"], self.state["specific_humidity"]
+        if self.precision == "f32":  # the float64 state read in place every step
+            self.bound = self.model.bind([T, q], level_axes=[1, 1])
+        else:  # the split kernel reads float32: the state is cast into bound buffers each step
+            self._in32 = [T.to(torch.float32), q.to(torch.float32)]
+            self.bound = self.model.bind(self._in32, level_axes=[1, 1], precision=self.precision)
+        dq1, dq2 = self.bound.outputs
         precip = self.state["total_precipitation"]
-        if self._in32 is not None:
-            self._in32[0].copy_(T)
-            self._in32[1].copy_(q)
-        dq1, dq2 = self.bound()
-        res = ml_epilogue(dq1, dq2, q, self.state["pressure_thickness_of_atmospheric_layer"], T, self.dt,
-                          precip, in_place=True, level_axis=1)
-        precip.copy_(res["total_precipitation"])
+        column = torch.empty((7, precip.numel()), dtype=precip.dtype, device=precip.device)
+        column[6].copy_(precip.reshape(-1))
+        self.state["total_precipitation"] = column[6].view(precip.shape)
+        self._epi = BoundEpilogue(dq1, dq2, q, self.state["pressure_thickness_of_atmospheric_layer"], T, self.dt,
+                                  self.state["total_precipitation"], in_place=True, level_axis=1, column=column)
+        res = self._epi.out
         diags = [res["net_moistening_due_to_machine_learning"], res["column_heating_due_to_machine_learning"],
-                 precip]
-        return area_weighted_partials(diags, self.area)  # float64 diagnostics: the f64 reduction
+                 res["total_precipitation"]]
+        self._part = bind_area_weighted_partials(diags, self.area)  # float64 diagnostics: the f64 reduction
 
     def step(self):
+        from . import _device
         from .distributed import combine_partials
-        from .graphs import StepGraph
 
-        if self.bound is None:  # validated once; the first step runs eagerly
-            T, q = self.state["air_temperature"], self.state["specific_humidity"]
-            if self.precision == "f32":  # the float64 state read in place every step
-                self.bound = self.model.bind([T, q], level_axes=[1, 1])
-            else:  # the split kernel reads float32: the state is cast into bound buffers each step
-                self._in32 = [T.to(torch.float32), q.to(torch.float32)]
-                self.bound = self.model.bind(self._in32, level_axes=[1, 1], precision=self.precision)
-            part = self._device_step()
-        elif self.graph:
-            if self._graph is None:
-                self._graph = StepGraph(self._device_step)
-            part = self._graph()
-        else:
-            part = self._device_step()
-        return combine_partials(part, self.group)
+        if self.bound is None:
+            self._bind()
+        h = _device.stream_handle()
+        if self._in32 is not None:
+            self._in32[0].copy_(self.state["air_temperature"])
+            self._in32[1].copy_(self.state["specific_humidity"])
+        self.bound(h)
+        self._epi(h)
+        return combine_partials(self._part(h), self.group)
 
 
 def make_stepper_workload(res: int = 96, seed: int = 0, device=None, group=None, precision: str = "f32"):
@@ -277,58 +278,68 @@ class ShardedStepperWorkload:
     # GPU, the exchange stubbed by a local copy of the same bytes (this band's partials
     # replicated for every rank, then folded: the fold sees the full gathered row count)
     stub_world: int = 1
-    # every step after the first replays HIP graphs of the device parts (graphs.py): one
-    # for the whole step when nothing is exchanged (one rank, or the stubbed exchange),
-    # else one before the collectives; the fold after them stays one eager launch
-    graph: bool = True
-    _graph: object = None
+    _epi: object = None
+    _rows: object = None
+    _lev: object = None
+    _fold: object = None
+    _rep: object = None
+    _res: object = None
 
-    def _device_step(self):
-        """predict + epilogue + row partials + level counts on the current stream, fixed
-        buffers; with the stubbed exchange also its local copy and the fold."""
-        from .distributed import area_row_partials, fold_rows, level_sums
-        from .stepper import ml_epilogue
+    def _bind(self):
+        """Marshal every launch of the step once (predict, fused epilogue, row partials,
+        limiter level counts; with the stubbed exchange also the fold into one result
+        buffer): a step is then a handful of C-ABI calls on fixed buffers, no per-call
+        Python marshalling (which, on one rank's 6,912 columns, took longer than the
+        kernels).  The precipitation accumulates in place in the epilogue's column buffer."""
+        from .distributed import bind_area_row_partials, bind_fold_rows, bind_level_sums
+        from .stepper import BoundEpilogue
 
         T, q = self.state["air_temperature"], self.state["specific_humidity"]
+        self.bound = self.model.bind([T, q], level_axes=[0, 0])
+        dq1, dq2 = self.bound.outputs
         precip = self.state["total_precipitation"]
-        dq1, dq2 = self.bound()
-        res = ml_epilogue(dq1, dq2, q, self.state["pressure_thickness_of_atmospheric_layer"], T, self.dt,
-                          precip, in_place=True, level_axis=0)
-        precip.copy_(res["total_precipitation"])
-        local = self.partials
-        area_row_partials([res["net_moistening_due_to_machine_learning"],
-                           res["column_heating_due_to_machine_learning"], precip], self.area, out=local)
-        limited = level_sums(res["specific_humidity_limiter_active"])  # [nz] exact column counts
+        column = torch.empty((7, precip.numel()), dtype=precip.dtype, device=precip.device)
+        column[6].copy_(precip.reshape(-1))
+        self.state["total_precipitation"] = column[6].view(precip.shape)
+        self._epi = BoundEpilogue(dq1, dq2, q, self.state["pressure_thickness_of_atmospheric_layer"], T, self.dt,
+                                  self.state["total_precipitation"], in_place=True, level_axis=0, column=column)
+        res = self._epi.out
+        nrows, nz = self.area.shape[0], q.shape[0]
+        # [rows][3 (sum area*x, sum area) pairs]
+        self.partials = torch.empty((nrows, 6), dtype=torch.float64, device=q.device)
+        self._rows = bind_area_row_partials([res["net_moistening_due_to_machine_learning"],
+                                             res["column_heating_due_to_machine_learning"],
+                                             res["total_precipitation"]], self.area, out=self.partials)
+        limiter = res["specific_humidity_limiter_active"]
         if self.stub_world > 1 and self.group is None:
-            means = fold_rows(local.repeat(self.stub_world, 1))
-            return torch.cat([means, limited.clone()])
-        return local, limited
+            self._rep = torch.empty((self.stub_world * nrows, 6), dtype=torch.float64, device=q.device)
+            self._res = torch.empty(6 + nz, dtype=torch.float64, device=q.device)
+            self._fold = bind_fold_rows(self._rep, out=self._res[:6])
+            self._lev = bind_level_sums(limiter, out=self._res[6:])  # [nz] exact column counts
+            self.exchange_bytes = 8 * (nrows * 6 + nz)
+        else:
+            self._lev = bind_level_sums(limiter)
 
     def step(self):
+        from . import _device
         from .distributed import global_count_sums, global_row_sums, row_counts
-        from .graphs import StepGraph
 
-        if self.bound is None:  # validated once; the first step runs eagerly
-            T, q = self.state["air_temperature"], self.state["specific_humidity"]
-            self.bound = self.model.bind([T, q], level_axes=[0, 0])
-            # [rows][3 (sum area*x, sum area) pairs]
-            self.partials = torch.empty((self.area.shape[0], 6), dtype=torch.float64, device=q.device)
-            out = self._device_step()
-        elif self.graph:
-            if self._graph is None:
-                self._graph = StepGraph(self._device_step)
-            out = self._graph()
-        else:
-            out = self._device_step()
-        nz = self.state["specific_humidity"].shape[0]
-        if self.stub_world > 1 and self.group is None:
-            self.exchange_bytes = 8 * (self.partials.shape[0] * 6 + nz)
-            return out.clone()
-        local, limited = out
+        if self.bound is None:
+            self._bind()
+        h = _device.stream_handle()
+        self.bound(h)
+        self._epi(h)
+        self._rows(h)
+        limited = self._lev(h)
+        if self._fold is not None:  # stubbed exchange: this band's partials for every rank
+            nrows = self.partials.shape[0]
+            self._rep.view(self.stub_world, nrows, 6).copy_(self.partials.unsqueeze(0).expand(self.stub_world, -1, -1))
+            self._fold(h)
+            return self._res.clone()
         if self.counts is None:  # the bands are fixed: their sizes are exchanged once
-            self.counts = row_counts(local.shape[0], self.group)
+            self.counts = row_counts(self.partials.shape[0], self.group)
             self.exchange_bytes = 8 * (max(self.counts) * 6 + limited.numel())
-        means = global_row_sums(local, self.group, self.counts)
+        means = global_row_sums(self.partials, self.group, self.counts)
         return torch.cat([means, global_count_sums(limited, self.group).to(means.device)])
 
     @staticmethod

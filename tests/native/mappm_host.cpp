@@ -39,6 +39,26 @@ extern "C" int host_mappm(int km, const float* pe1, const float* q1, int kn, con
     return 0;
 }
 
+// kord > 7 with the bottom `nt` edges in registers (mappm_cs_column<..., NT>), as the
+// device kernel runs it: the same bits as host_mappm's all-scratch column
+extern "C" int host_mappm_cs_tail(int km, const float* pe1, const float* q1, int kn, const float* pe2,
+                                  float* q2, int64_t ncol, int iv, int kord, int nt)
+{
+    if (km < 4 || kn < 1 || kord <= 7) return -1;
+    Scr scr{std::vector<float>(km + 3), std::vector<float>(km + 3)};
+    for (int64_t i = 0; i < ncol; ++i) {
+        Col c{pe1, q1, pe2, q2, ncol, i, kn};
+        switch (nt) {
+        case 8: fv3::mappm_cs_column<Col, Scr, 8>(c, scr, km, kn, iv, kord); break;
+        case 16: fv3::mappm_cs_column<Col, Scr, 16>(c, scr, km, kn, iv, kord); break;
+        case 32: fv3::mappm_cs_column<Col, Scr, 32>(c, scr, km, kn, iv, kord); break;
+        case 48: fv3::mappm_cs_column<Col, Scr, 48>(c, scr, km, kn, iv, kord); break;
+        default: return -1;
+        }
+    }
+    return 0;
+}
+
 // same through the output-driven cursor (kord <= 7), as the fused coarsen kernel uses it
 extern "C" int host_mappm_cursor(int km, const float* pe1, const float* q1, int kn, const float* pe2,
                                  float* q2, int64_t ncol, int iv, int kord)

@@ -80,13 +80,22 @@ def test_oracle_matches_live_reference(kord):
 @pytest.fixture(scope="module")
 def host_lib():
     os.makedirs(os.path.dirname(HOST_SO), exist_ok=True)
+    # each process (pytest-xdist worker) builds its own file and renames it into place,
+    # so no worker loads a library another one is still writing
+    tmp = f"{HOST_SO}.{os.getpid()}.tmp"
     subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-                    "-o", HOST_SO, HOST_SRC], check=True)
-    lib = ctypes.CDLL(HOST_SO)
+                    "-o", tmp, HOST_SRC], check=True)
+    own = f"{HOST_SO[:-3]}.{os.getpid()}.so"
+    os.replace(tmp, own)
+    lib = ctypes.CDLL(own)
+    os.unlink(own)  # the mapping stays valid; nothing is left behind
     for fn in (lib.host_mappm, lib.host_mappm_cursor, lib.host_mappm_generic):
         fn.restype = ctypes.c_int
         fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                        ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
+    lib.host_mappm_cs_tail.restype = ctypes.c_int
+    lib.host_mappm_cs_tail.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int]
     return lib
 
 
@@ -259,3 +268,29 @@ def test_multi_field_streaming_bit_identical(host_lib, nf, km, kn):
                           iv, kord) == 0
                 for f in range(nf):
                     assert _bits_equal(out[f], _host(host_lib, pe1, q[f], pe2, iv, kord)), (nf, f, kord, iv)
+
+
+@pytest.mark.parametrize("km,kn", [(8, 5), (9, 9), (17, 12), (33, 40), (79, 79), (79, 50), (127, 40)])
+def test_cs_register_tail_is_bit_identical(host_lib, km, kn):
+    """kord > 7 with the bottom NT edges of the tridiagonal solve held in registers (the
+    device kernel's mappm_cs_column<.., NT>) gives the all-scratch column's bits, for every
+    kord > 7 and iv (iv = -2 and km < NT + 1 take the all-scratch path), on columns with
+    shared edges and unsorted output edges; and both match the oracle."""
+    rng = np.random.default_rng(km * 7 + kn)
+    ncol = 48
+    for kord in (8, 9, 10, 11, 12, 13, 14, 15, 16, 17):
+        for iv in (0, 1, -1, 2, -2):
+            delp = rng.uniform(1, 3000, (km, ncol)).astype(np.float32)
+            pe1 = np.concatenate([np.full((1, ncol), 300, np.float32), 300 + np.cumsum(delp, 0, dtype=np.float32)])
+            pe2 = np.sort(rng.uniform(pe1[0] * 0.8, pe1[-1] * 1.1, (kn + 1, ncol)), 0).astype(np.float32)
+            m = min(km, kn) + 1
+            pe2[: m // 2] = pe1[: m // 2]
+            pe2 = np.sort(pe2, 0)
+            pe2[:, :4] = pe2[::-1, :4]  # a few columns with decreasing output edges
+            q = (rng.normal(0, 1, (km, ncol)) * rng.choice([1e-4, 1, 300], (km, ncol))).astype(np.float32)
+            ref = _host(host_lib, pe1, q, pe2, iv, kord)
+            for nt in (8, 16, 32, 48):
+                out = np.empty((kn, ncol), np.float32)
+                assert host_lib.host_mappm_cs_tail(km, pe1.ctypes.data, q.ctypes.data, kn, pe2.ctypes.data,
+                                                   out.ctypes.data, ncol, iv, kord, nt) == 0
+                assert _bits_equal(out, ref), (kord, iv, nt)

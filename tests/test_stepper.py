@@ -129,34 +129,48 @@ def test_stepper_workload_step(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["full", "rank_of_4_stub", "rank_of_2_bf16x6"])
-def test_stepper_graph_replay_bit_identical_to_eager(gpu, kind):
-    """Steps 2.. of the stepper workloads replay one HIP graph of the device part
-    (fv3net_amd/graphs.py).  Four steps with the graph give the eager steps' bits: the
-    state (updated in place), the accumulated precipitation (copied back into its own
-    buffer inside the graph), the returned global sums and limiter profile."""
+@pytest.mark.parametrize("kind", ["full", "rank_of_4_stub", "full_bf16x6"])
+def test_bound_stepper_steps_bit_identical_to_unbound_calls(gpu, kind):
+    """The stepper workloads marshal every launch once (BoundForward, BoundEpilogue with
+    the precipitation accumulated in place in its column buffer, bound partials / level
+    counts / fold).  Four steps give, bit for bit, what the per-call product functions
+    (forward, ml_epilogue, area_weighted_partials / area_row_partials, level_sums,
+    fold_rows) give on a copy of the same state: the state, the accumulated
+    precipitation, the global sums and the limiter profile."""
     import torch
 
+    from fv3net_amd import distributed as D
     from fv3net_amd import workloads as W
+    from fv3net_amd.stepper import ml_epilogue
 
-    def make(graph):
-        if kind == "full":
-            wl = W.make_stepper_workload(12, seed=4)
-        elif kind == "rank_of_4_stub":
-            wl = W.make_sharded_stepper_workload(12, 1, 4, seed=4, stub_exchange=True)
-        else:
-            wl = W.make_stepper_workload(12, seed=4, precision="bf16x6")
-        wl.graph = graph
-        return wl
-
-    eager, graphed = make(False), make(True)
+    sharded = kind == "rank_of_4_stub"
+    if sharded:
+        wl = W.make_sharded_stepper_workload(12, 1, 4, seed=4, stub_exchange=True)
+    else:
+        wl = W.make_stepper_workload(12, seed=4, precision="bf16x6" if "bf16x6" in kind else "f32")
+    ref = {k: v.clone() for k, v in wl.state.items()}
+    ax = 0 if sharded else 1
+    names = ("net_moistening_due_to_machine_learning", "column_heating_due_to_machine_learning", "total_precipitation")
     for step in range(4):
-        a, b = eager.step(), graphed.step()
+        got = wl.step()
+        T, q = ref["air_temperature"], ref["specific_humidity"]
+        bf6 = "bf16x6" in kind  # the workload casts the state into float32 buffers for the split kernel
+        ins = [T.float(), q.float()] if bf6 else [T, q]
+        dq1, dq2 = wl.model.forward(ins, level_axes=[ax, ax], precision="bf16x6" if bf6 else None)
+        res = ml_epilogue(dq1, dq2, q, ref["pressure_thickness_of_atmospheric_layer"], T, wl.dt,
+                          ref["total_precipitation"], in_place=True, level_axis=ax)
+        ref["total_precipitation"] = res["total_precipitation"]
+        if sharded:
+            local = D.area_row_partials([res[n] for n in names], wl.area,
+                                        out=torch.empty((wl.area.shape[0], 6), dtype=torch.float64, device=q.device))
+            lim = D.level_sums(res["specific_humidity_limiter_active"])
+            want = torch.cat([D.fold_rows(local.repeat(4, 1)), lim])
+        else:
+            want = D.area_weighted_partials([res[n] for n in names], wl.area)
         torch.cuda.synchronize()
-        assert torch.equal(a.view(torch.int64), b.view(torch.int64)), step
-        for k in eager.state:
-            assert torch.equal(eager.state[k], graphed.state[k]), (step, k)
-    assert graphed._graph is not None and graphed._graph.graph is not None
+        assert torch.equal(got.view(torch.int64), want.view(torch.int64)), step
+        for k in ref:
+            assert torch.equal(wl.state[k].reshape(-1).view(torch.int64), ref[k].reshape(-1).view(torch.int64)), (step, k)
 
 
 @pytest.mark.gpu
