@@ -170,7 +170,21 @@ __device__ __forceinline__ void sfor(F&& f)
 // this wave's LDS writes done, then the workgroup barrier; global loads in flight (the
 // next weight chunk, the next inputs) are NOT drained (a __syncthreads() fence would
 // wait vmcnt(0) on gfx9, where loads and stores share the counter)
+#ifndef FV3_B3_BUILTIN_BARRIER
+#define FV3_B3_BUILTIN_BARRIER 0
+#endif
+#if FV3_B3_BUILTIN_BARRIER
+// the same two instructions as builtins, so the compiler's wait-count pass sees the
+// lgkm counter drained here (behind inline asm it assumes scalar loads may still be in
+// flight and then drains every later LDS wait to lgkmcnt(0))
+__device__ __forceinline__ void b3_barrier()
+{
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt / expcnt at their maximum (no wait)
+    __builtin_amdgcn_s_barrier();
+}
+#else
 __device__ __forceinline__ void b3_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+#endif
 
 __device__ __forceinline__ float b3_log(float x, float eps) { return x != x ? x : logf(x > eps ? x : eps); }
 
@@ -288,6 +302,38 @@ __device__ __forceinline__ void vm_wait_le(int n)
 typedef __attribute__((address_space(1))) void* GlobalVoid;
 typedef __attribute__((address_space(3))) void* LdsVoid;
 
+// LDS-DMA of 16 B (dwordx4) or 4 B (dword) per lane into the wave-uniform LDS byte address
+// `lds` (+ 16 B or 4 B x lane).  FV3_B3_GLDS_ASM: issued from inline asm (M0 saved and
+// restored in the same statement) instead of __builtin_amdgcn_global_load_lds.  The
+// compiler's wait-count pass files a builtin LDS-DMA as a pending LDS event of another
+// kind than the ds_reads and from then on drains every wait before an MFMA to
+// lgkmcnt(0), so the fragment reads of the next tile pair never overlap the current
+// pair's MFMAs; hidden in asm, it is not counted (it is a VM_CNT operation: the ring's
+// own counted vmcnt waits and the chunk barrier cover it) and the ds_read waits stay
+// counted.
+#ifndef FV3_B3_GLDS_ASM
+#define FV3_B3_GLDS_ASM 0
+#endif
+template <int BYTES>
+__device__ __forceinline__ void b3_glds(const void* g, const void* lds)
+{
+#if FV3_B3_GLDS_ASM
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(LdsVoid)lds);
+    unsigned keep;
+    if constexpr (BYTES == 16)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g), "s"(dst) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g), "s"(dst) : "memory");
+#else
+    if constexpr (BYTES == 16)
+        __builtin_amdgcn_global_load_lds((GlobalVoid)g, (LdsVoid)lds, 16, 0, 0);
+    else
+        __builtin_amdgcn_global_load_lds((GlobalVoid)g, (LdsVoid)lds, 4, 0, 0);
+#endif
+}
+
 // GL (default): the weight chunks and the layer-1 inputs go global -> LDS by LDS-DMA
 // (global_load_lds), a 3-slot weight ring with two chunks in flight; no staging registers
 // and no ds_write pass.  !GL: round 2's pipeline (weights through 16 staging registers and
@@ -372,9 +418,8 @@ dense_b3_kernel(B3Args pa)
 #pragma unroll
         for (int q = 0; q < NST; ++q)
             if (part_ok(q))
-                __builtin_amdgcn_global_load_lds((GlobalVoid)(wsrc + (size_t)j * CB + q * 16 * kB3Threads + tid * 16),
-                                                 (LdsVoid)(ring + sl * CB + q * 16 * kB3Threads + wave * 1024), 16, 0,
-                                                 0);
+                b3_glds<16>(wsrc + (size_t)j * CB + q * 16 * kB3Threads + tid * 16,
+                            ring + sl * CB + q * 16 * kB3Threads + wave * 1024);
     };
     int slot = 0;                         // ring slot of the chunk computed next
     // stream index of the chunk staged next (GL: chunk + NSL - 1, !GL: chunk + 2)
@@ -500,8 +545,7 @@ dense_b3_kernel(B3Args pa)
         const float* ptr = g.ptr + (int64_t)lblk * g.bs + lii;
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-            __builtin_amdgcn_global_load_lds((GlobalVoid)(ptr + (j < nv ? j * ld : 0)),
-                                             (LdsVoid)(s_in + ((buf * NWV + wave) * 8 + j) * 64), 4, 0, 0);
+            b3_glds<4>(ptr + (j < nv ? j * ld : 0), s_in + ((buf * NWV + wave) * 8 + j) * 64);
     };
     auto read_in = [&](int buf, int c, float (&raw)[8]) {  // GL: chunk c's values (landed, see advance)
         const int nv = lvalid ? s_grp[4 * c + hq].nv : 0;

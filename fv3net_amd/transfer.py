@@ -9,12 +9,17 @@ one piece at a time; here the host side of the copy (numpy <-> pinned buffer, th
 splitting each chunk) runs while the DMA of the previous chunk is in flight on a copy
 stream, so both directions run at the host-memcpy or PCIe rate, whichever is lower.
 
+Arrays of 64 KiB and more are instead page-locked in place for the copy (HostPages,
+fv3_host_register): the copy engines DMA straight from / to the caller's memory with no
+host memcpy at all; the staging path remains for memory that cannot be registered.
+
 Plumbing only: bytes are moved unchanged (float64 stays float64; the kernels that read
 float64 in place, or a device cast, do any conversion).
 """
 import concurrent.futures
 import os
 import threading
+from typing import Optional
 
 import numpy as np
 
@@ -24,6 +29,7 @@ except ImportError:  # pragma: no cover - torch is part of the image
     torch = None
 
 _CHUNK = 16 << 20  # bytes per staging buffer
+_MIN_REGISTER = 64 << 10  # arrays from here on are page-locked for their copy (HostPages)
 _MIN_SPLIT = 1 << 20  # host copies below this run on the calling thread
 
 
@@ -31,8 +37,11 @@ class PinnedStager:
     """Two pinned staging buffers, one copy stream, a small thread pool for the host
     memcpy.  One instance per device (``stager()``); calls are serialised."""
 
-    def __init__(self, device, chunk_bytes: int = _CHUNK, threads: int = 0, min_staged: int = None):
+    def __init__(self, device, chunk_bytes: int = _CHUNK, threads: int = 0, min_staged: int = None,
+                 min_register: Optional[int] = _MIN_REGISTER):
         self.device = torch.device(device)
+        # arrays of this size and more are page-locked for their copy (None: never)
+        self.min_register = min_register
         self.chunk = int(chunk_bytes)
         # below 4 chunks the driver's own pageable copy is faster (measured on the box:
         # a C48 float64 field, 8.7 MB, 22 GB/s pageable vs 19 staged; a C384 one, 560 MB,
@@ -70,6 +79,13 @@ class PinnedStager:
         nbytes = a.nbytes
         if nbytes == 0:
             return out
+        if self.min_register is not None and nbytes >= self.min_register:
+            # DMA straight from the caller's pages, registered for the copy: a C384 float64
+            # field in + a float32 one out, 18.4 ms staged -> 14.7 ms (tools/h2h_register.py)
+            with HostPages([a], self.min_register) as pages:
+                if pages.registered:
+                    out.view(-1).copy_(torch.from_numpy(a.reshape(-1)), non_blocking=True)
+                    return out  # leaving the block waits for the copy, then releases the pages
         if nbytes < self.min_staged:
             out.view(-1).copy_(torch.from_numpy(a.reshape(-1)))
             return out
@@ -105,6 +121,11 @@ class PinnedStager:
         nbytes = out.nbytes
         if nbytes == 0:
             return out
+        if self.min_register is not None and nbytes >= self.min_register:
+            with HostPages([out], self.min_register) as pages:
+                if pages.registered:
+                    torch.from_numpy(out.reshape(-1)).copy_(t.view(-1), non_blocking=True)
+                    return out
         if nbytes < self.min_staged:
             np.copyto(out.reshape(-1), t.view(-1).cpu().numpy())
             return out
@@ -155,6 +176,11 @@ class HostPages:
         self.min_bytes = int(min_bytes)
         self._registered = []
         self._pending = list(arrays)
+
+    @property
+    def registered(self) -> int:
+        """How many arrays this block registered."""
+        return len(self._registered)
 
     def add(self, arrays):
         for a in arrays:

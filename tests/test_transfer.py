@@ -7,12 +7,16 @@ import pytest
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [np.float32, np.float64, np.uint8, np.int64])
-def test_round_trip_bit_exact(gpu, dtype):
+@pytest.mark.parametrize("register", [None, 1 << 13])
+def test_round_trip_bit_exact(gpu, dtype, register):
+    """Both host paths: pinned staging (register None) and the caller's pages registered
+    for the copy (arrays of 8 KiB and more here; small ones stay pageable copies)."""
     import torch
 
     from fv3net_amd import transfer
 
-    st = transfer.PinnedStager(torch.device("cuda", 0), chunk_bytes=1 << 16, threads=4, min_staged=1 << 12)
+    st = transfer.PinnedStager(torch.device("cuda", 0), chunk_bytes=1 << 16, threads=4, min_staged=1 << 12,
+                               min_register=register)
     rng = np.random.default_rng(3)
     for n in (0, 1, 1000, (1 << 16) // np.dtype(dtype).itemsize, 3 * (1 << 16) + 17, 1 << 20):
         a = (rng.normal(0, 1e3, n) if np.dtype(dtype).kind == "f" else rng.integers(0, 200, n)).astype(dtype)

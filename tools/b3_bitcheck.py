@@ -1,0 +1,39 @@
+"""Hash of the split kernel's outputs (emulator C384 bf16x3 / bf16x6, 2x256 C48 and C384
+bf16x3 / bf16x6, both block shapes) under the library FV3NET_AMD_LIB names: a scheduling
+variant of csrc/dense_b3.hip must print the product library's hashes (same arithmetic
+in the same order)."""
+import hashlib
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fv3net_amd import workloads as W  # noqa: E402
+
+
+def digest(ts):
+    h = hashlib.sha256()
+    for t in ts:
+        h.update(t.contiguous().view(torch.int32).cpu().numpy().tobytes())
+    return h.hexdigest()[:16]
+
+
+if __name__ == "__main__":
+    dev = torch.device("cuda", 0)
+    for prec in ("bf16x3", "bf16x6"):
+        wl = W.make_emulator_workload(384, seed=13, device=dev, precision=prec)
+        wl.step()
+        torch.cuda.synchronize()
+        print(f"emulator C384 {prec} {digest(list(wl.out.values()))}", flush=True)
+        del wl
+        for res in (48, 384):
+            for waves in ("4", "8"):
+                os.environ["FV3_B3_WAVES"] = waves
+                wl = W.make_dense_workload(res, seed=1, device=dev, precision=prec)
+                wl.step()
+                wl.step()
+                torch.cuda.synchronize()
+                print(f"dense C{res} {prec} waves={waves} {digest(wl.outputs)}", flush=True)
+                del wl
+            os.environ.pop("FV3_B3_WAVES", None)
