@@ -296,18 +296,22 @@ __global__ __launch_bounds__(256) void mappm_cs_global_kernel(MappmArgs a)
     mappm_cs_column<DevCol, GlobalScr, NT>(col, scr, a.km, a.kn, a.iv, a.kord);
 }
 
-// register-tail depth of the kord > 7 kernel; FV3_MAPPM_CS_NT=0|16|32|48 selects one
-// (A/B: every depth gives the same bits)
-constexpr int kCsTailDefault = 32;
-const void* cs_global_kernel()
+// register-tail depth of the kord > 7 kernel (every depth gives the same bits).  Measured
+// on MI355X (tools/mappm_nt_ab.py, profiles/r04c_mappm_nt.log), C384 79 -> 79: at
+// 884,736 columns NT = 0 / 16 / 32 / 48 take 0.89 / 0.97 / 1.12 / 1.24 ms (the registers
+// cost occupancy: 60 -> 78 / 100 / 132 VGPRs, 8 -> 6 / 4 / 3 waves per SIMD, and the
+// launch needs it more than the scratch bytes saved); at one rank's 110,592 columns,
+// where occupancy is not the limit, 0.232 / 0.223 / 0.218 / 0.212 ms.  So the tail is
+// used on small grids only.  FV3_MAPPM_CS_NT=0|16|32|48 forces a depth (A/B).
+const void* cs_global_kernel(int64_t ncol)
 {
-    int nt = kCsTailDefault;
+    int nt = ncol < 262144 ? 48 : 0;
     if (const char* e = getenv("FV3_MAPPM_CS_NT")) nt = atoi(e);
     switch (nt) {
     case 0: return (const void*)mappm_cs_global_kernel<0>;
     case 16: return (const void*)mappm_cs_global_kernel<16>;
-    case 48: return (const void*)mappm_cs_global_kernel<48>;
-    default: return (const void*)mappm_cs_global_kernel<32>;
+    case 32: return (const void*)mappm_cs_global_kernel<32>;
+    default: return (const void*)mappm_cs_global_kernel<48>;
     }
 }
 
@@ -333,7 +337,7 @@ int launch_mappm(MappmArgs a, hipStream_t stream)
         FV3_HIP(hipMallocAsync((void**)&a.scratch, sizeof(float) * 2 * (size_t)(a.km + 3) * (size_t)grid * block,
                                stream));
         void* kargs[] = {&a};
-        FV3_HIP(hipLaunchKernel(cs_global_kernel(), dim3((unsigned)grid), dim3(block), kargs, 0, stream));
+        FV3_HIP(hipLaunchKernel(cs_global_kernel(a.ncol), dim3((unsigned)grid), dim3(block), kargs, 0, stream));
         FV3_LAUNCH_CHECK();
         FV3_HIP(hipFreeAsync(a.scratch, stream));
         return FV3_OK;
