@@ -95,7 +95,7 @@ __device__ __forceinline__ void b3_sched_groups()
 // weight ring slots: SL (LDS-DMA pipeline: 3, or 2 where three chunks do not fit, e.g.
 // bf16x6 at width 256), 0 = the register-staged pipeline (2 slots)
 constexpr int b3_slots(int sl) { return sl > 0 ? sl : 2; }
-constexpr int b3_in_bytes(bool gl, int nwv, int cpw) { return gl ? 2 * nwv * cpw * 8 * 64 * 4 : 0; }
+constexpr int b3_in_bytes(bool gl, int nwv) { return gl ? 2 * nwv * 8 * 64 * 4 : 0; }
 
 struct B3Pack {
     void* dbuf = nullptr;
@@ -340,10 +340,8 @@ __device__ __forceinline__ void b3_glds(const void* g, const void* lds)
 // ds_write_b128 into a 2-slot ring, inputs into registers), kept for A/B (FV3_B3_STAGE=reg).
 // NS: bf16 parts per f32 operand (2: bf16x3, 3: bf16x6, see SplitTerms)
 // NWV: waves per block (8; 4 on grids with fewer 128-column tiles than CUs, so every
-// CU gets a tile and each SIMD runs one 16-column wave).  CPW: 16-column tiles per wave
-// (2 only with NWV = 4, one wave per SIMD and its 512 registers): every A fragment read
-// from LDS feeds CPW column tiles, halving the fragment reads per MFMA
-template <int HU, int SL, int NS, int NWV, int CPW>
+// CU gets a tile and each SIMD runs one 16-column wave)
+template <int HU, int SL, int NS, int NWV>
 __global__ __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(NWV == 4 ? 1 : 2, NWV == 4 ? 1 : 2))) void
 dense_b3_kernel(B3Args pa)
 {
@@ -354,16 +352,15 @@ dense_b3_kernel(B3Args pa)
     constexpr int CB = 1024 * NS * HU;  // chunk: HU A fragments x NS parts x 64 lanes x 16 B
     // 16-B loads per thread per chunk; a chunk that is not a whole number of block-wide
     // loads (HU = 4 at NS = 3: 1.5) has its last load on the first waves only (wave-uniform)
-    constexpr int kB3Threads = 64 * NWV, kB3Cols = 16 * NWV * CPW;  // this instantiation's block
-    static_assert(CPW == 1 || NWV == 4, "two column tiles per wave need the 1-wave-per-SIMD budget");
+    constexpr int kB3Threads = 64 * NWV, kB3Cols = 16 * NWV;  // this instantiation's block
     constexpr int NST = (CB + 16 * kB3Threads - 1) / (16 * kB3Threads);
     constexpr bool GL = SL > 0;
     constexpr int NSL = b3_slots(SL);            // weight ring slots
     static_assert(HU % 4 == 0 && NST >= 1, "unit tiles per layer must be a multiple of 4");
     extern __shared__ __attribute__((aligned(16))) b3f4 lds3[];
     char* ring = reinterpret_cast<char*>(lds3);
-    float* s_in = reinterpret_cast<float*>(ring + NSL * CB);  // GL: [2][NWV waves][CPW][8 levels][64 lanes]
-    float* s_mean = reinterpret_cast<float*>(ring + NSL * CB + b3_in_bytes(GL, NWV, CPW));
+    float* s_in = reinterpret_cast<float*>(ring + NSL * CB);  // GL: [2][8 waves][8 levels][64 lanes]
+    float* s_mean = reinterpret_cast<float*>(ring + NSL * CB + b3_in_bytes(GL, NWV));
     float* s_rs = s_mean + p.kp1;
     float* s_bias = s_rs + p.kp1;             // [nh][HP]
     float* s_oc = s_bias + (1 + p.nhx) * HP;  // [6][kop]: bias, sigma, mean, lo, hi, mask
@@ -436,12 +433,10 @@ dense_b3_kernel(B3Args pa)
         load_stage(p.nch > 1 ? 1 : 0);
     }
 
-    b3f4 acc[CPW][HU];
+    b3f4 acc[HU];
     auto zero_acc = [&]() {
 #pragma unroll
-        for (int ct = 0; ct < CPW; ++ct)
-#pragma unroll
-            for (int t = 0; t < HU; ++t) acc[ct][t] = b3f4{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int t = 0; t < HU; ++t) acc[t] = b3f4{0.0f, 0.0f, 0.0f, 0.0f};
     };
 #ifdef FV3_B3_EXP_NOFRAG
     bf16x8 fconst[2][NS];
@@ -490,9 +485,8 @@ dense_b3_kernel(B3Args pa)
         jn2 = jn2 + 1 == p.nch ? 0 : jn2 + 1;
     };
     // layer chunk: unit tile t accumulates A_t x B (one 32-deep k-step); tiles in pairs,
-    // their MFMAs interleaved, fragments read one pair ahead; bx[ct] = column tile ct's
-    // B fragments
-    auto step_layer = [&](const bf16x8 (&bx)[CPW][NS], auto&& after_stage) {
+    // their MFMAs interleaved, fragments read one pair ahead
+    auto step_layer = [&](const bf16x8 (&bx)[NS], auto&& after_stage) {
         stage_next();
         const int younger = after_stage();  // GL: ops issued after this chunk's weight DMA (vmcnt is in order)
         bf16x8 fa[kFR][NS];
@@ -504,36 +498,30 @@ dense_b3_kernel(B3Args pa)
                 frag(slot, t1 + kFR - 2, fa[(t1 + kFR - 2) % kFR]);
             }
             b3_sched_pair();
-#pragma unroll
-            for (int ct = 0; ct < CPW; ++ct)
-                mma_x2<NS>(fa[t0 % kFR], bx[ct], acc[ct][t0], fa[t1 % kFR], bx[ct], acc[ct][t1]);
-            b3_sched_groups<(t0 + kFR - 2 < HU) ? 2 * NS : 0, 2 * CPW * SplitTerms<NS>::n>();
+            mma_x2<NS>(fa[t0 % kFR], bx, acc[t0], fa[t1 % kFR], bx, acc[t1]);
+            b3_sched_groups<(t0 + kFR - 2 < HU) ? 2 * NS : 0, 2 * SplitTerms<NS>::n>();
             b3_sched_pair();
         });
         advance(younger);
     };
 
     // ---- layer-1 inputs: B fragments straight from the [level][column] arrays ----
-    // per column tile ct of the wave: column address of the tile being loaded (block, index in block)
-    unsigned lblk[CPW] = {}, lii[CPW] = {};
-    bool lvalid[CPW] = {};
+    unsigned lblk = 0, lii = 0;  // column address of the tile being loaded (block, index in block)
+    bool lvalid = false;
     auto set_load_tile = [&](int64_t tile) {
-#pragma unroll
-        for (int ct = 0; ct < CPW; ++ct) {
-            const int64_t c = tile * kB3Cols + (wave * CPW + ct) * 16 + cl;
-            lvalid[ct] = c < p.ncol;
-            const int64_t cc = lvalid[ct] ? c : 0;
-            const int64_t b = p.ncol_blk < p.ncol ? cc / p.ncol_blk : 0;
-            lblk[ct] = (unsigned)b;
-            lii[ct] = (unsigned)(cc - b * p.ncol_blk);
-        }
+        const int64_t c = tile * kB3Cols + wave * 16 + cl;
+        lvalid = c < p.ncol;
+        const int64_t cc = lvalid ? c : 0;
+        const int64_t b = p.ncol_blk < p.ncol ? cc / p.ncol_blk : 0;
+        lblk = (unsigned)b;
+        lii = (unsigned)(cc - b * p.ncol_blk);
     };
-    auto load_in = [&](float (&raw)[8], int c, int ct) {  // chunk c: group 4c + hq, 8 levels
+    auto load_in = [&](float (&raw)[8], int c) {  // chunk c: group 4c + hq, 8 levels
         const B3Grp& g = s_grp[4 * c + hq];
         const int ld = g.ld;  // the host checks 8 * ld < 2^31
-        const int nv = lvalid[ct] ? g.nv : 0;
+        const int nv = lvalid ? g.nv : 0;
         typedef const __attribute__((address_space(1))) float* GPtr;
-        const GPtr ptr = (GPtr)(g.ptr + (int64_t)lblk[ct] * g.bs + lii[ct]);
+        const GPtr ptr = (GPtr)(g.ptr + (int64_t)lblk * g.bs + lii);
         // all 8 loads issued unconditionally (levels past nv read the group's first level,
         // always in range, and are zeroed after), so none waits behind a branch
 #pragma unroll
@@ -549,24 +537,21 @@ dense_b3_kernel(B3Args pa)
         }
     };
     // GL: chunk c's inputs by LDS-DMA into this wave's rows of buffer `buf`: level j of
-    // every lane is one 4-byte LDS-DMA (lane-linear row [buf][wave][ct][j][lane]); 8 CPW loads
+    // every lane is one 4-byte LDS-DMA (lane-linear row [buf][wave][j][lane])
     auto glds_in = [&](int buf, int c) {
         const B3Grp& g = s_grp[4 * c + hq];
         const int ld = g.ld;
+        const int nv = lvalid ? g.nv : 0;
+        const float* ptr = g.ptr + (int64_t)lblk * g.bs + lii;
 #pragma unroll
-        for (int ct = 0; ct < CPW; ++ct) {
-            const int nv = lvalid[ct] ? g.nv : 0;
-            const float* ptr = g.ptr + (int64_t)lblk[ct] * g.bs + lii[ct];
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                b3_glds<4>(ptr + (j < nv ? j * ld : 0), s_in + (((buf * NWV + wave) * CPW + ct) * 8 + j) * 64);
-        }
+        for (int j = 0; j < 8; ++j)
+            b3_glds<4>(ptr + (j < nv ? j * ld : 0), s_in + ((buf * NWV + wave) * 8 + j) * 64);
     };
-    auto read_in = [&](int buf, int c, int ct, float (&raw)[8]) {  // GL: chunk c's values (landed, see advance)
-        const int nv = lvalid[ct] ? s_grp[4 * c + hq].nv : 0;
+    auto read_in = [&](int buf, int c, float (&raw)[8]) {  // GL: chunk c's values (landed, see advance)
+        const int nv = lvalid ? s_grp[4 * c + hq].nv : 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const float x = s_in[(((buf * NWV + wave) * CPW + ct) * 8 + j) * 64 + lane];
+            const float x = s_in[((buf * NWV + wave) * 8 + j) * 64 + lane];
             raw[j] = j < nv ? x : 0.0f;
         }
     };
@@ -596,40 +581,35 @@ dense_b3_kernel(B3Args pa)
     // NS = 2: split as soon as computed (B); NS = 3: kept in f32 (Y, 8 registers per k-step
     // against 12 for the split) and split per chunk as the next hidden layer consumes it;
     // the output layer, whose chunks each read every k-step, splits them all into B first
-    bf16x8 B[KS][CPW][NS];
-    float Y[NS == 3 ? KS : 1][CPW][8];
+    bf16x8 B[KS][NS];
+    float Y[NS == 3 ? KS : 1][8];
     auto hidden_epi = [&](int l) {  // relu(acc + bias_l) -> B (NS = 2) / Y (NS = 3)
         sfor<KS>([&](auto cc) {
             constexpr int c = decltype(cc)::value;
             const b3f4 b0 = *reinterpret_cast<const b3f4*>(s_bias + l * HP + 32 * c + 4 * hq);
             const b3f4 b1 = *reinterpret_cast<const b3f4*>(s_bias + l * HP + 32 * c + 16 + 4 * hq);
+            float y[8];
 #pragma unroll
-            for (int ct = 0; ct < CPW; ++ct) {
-                float y[8];
+            for (int r = 0; r < 4; ++r) {
+                const float v0 = acc[2 * c][r] + b0[r];
+                const float v1 = acc[2 * c + 1][r] + b1[r];
+                y[r] = v0 > 0.0f ? v0 : 0.0f;
+                y[4 + r] = v1 > 0.0f ? v1 : 0.0f;
+            }
+            if constexpr (NS == 2) {
+                splitN<NS>(y, B[c]);
+            } else {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float v0 = acc[ct][2 * c][r] + b0[r];
-                    const float v1 = acc[ct][2 * c + 1][r] + b1[r];
-                    y[r] = v0 > 0.0f ? v0 : 0.0f;
-                    y[4 + r] = v1 > 0.0f ? v1 : 0.0f;
-                }
-                if constexpr (NS == 2) {
-                    splitN<NS>(y, B[c][ct]);
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) Y[c][ct][j] = y[j];
-                }
+                for (int j = 0; j < 8; ++j) Y[c][j] = y[j];
             }
         });
     };
-    // k-step c's B fragments of every column tile
-    auto hidden_b = [&](auto cc, bf16x8 (&bx)[CPW][NS]) -> const bf16x8(&)[CPW][NS] {
+    auto hidden_b = [&](auto cc, bf16x8 (&bx)[NS]) -> const bf16x8(&)[NS] {  // k-step c's B fragments
         constexpr int c = decltype(cc)::value;
         if constexpr (NS == 2) {
             return B[c];
         } else {
-#pragma unroll
-            for (int ct = 0; ct < CPW; ++ct) splitN<NS>(Y[c][ct], bx[ct]);
+            splitN<NS>(Y[c], bx);
             return bx;
         }
     };
@@ -644,10 +624,8 @@ dense_b3_kernel(B3Args pa)
                 frag(slot, i1 + kFR - 2, fa[(i1 + kFR - 2) % kFR]);
             }
             b3_sched_pair();
-#pragma unroll
-            for (int ct = 0; ct < CPW; ++ct)
-                mma_x2<NS>(fa[i0 % kFR], B[q][ct], acc[ct][0], fa[i1 % kFR], B[q][ct], acc[ct][1]);
-            b3_sched_groups<(i0 + kFR - 2 < HU) ? 2 * NS : 0, 2 * CPW * SplitTerms<NS>::n>();
+            mma_x2<NS>(fa[i0 % kFR], B[q], acc[0], fa[i1 % kFR], B[q], acc[1]);
+            b3_sched_groups<(i0 + kFR - 2 < HU) ? 2 * NS : 0, 2 * SplitTerms<NS>::n>();
             b3_sched_pair();
         });
     };
@@ -659,20 +637,20 @@ dense_b3_kernel(B3Args pa)
     // elements); lanes that must not store (padding rows, columns past the end) get an
     // offset past the range, so no branch per row.  Residual inputs (Difference.backward:
     // after = before + to) are loaded one chunk ahead of their use.
-    unsigned oblk[CPW] = {}, oii[CPW] = {};
-    bool ovalid[CPW] = {};
-    auto res_load = [&](int T, int ct, float (&r)[4]) -> int {  // returns the loads issued (0 or 4)
+    unsigned oblk = 0, oii = 0;
+    bool ovalid = false;
+    auto res_load = [&](int T, float (&r)[4]) -> int {  // returns the loads issued (0 or 4)
         const int e = p.otile[T];
         const int v = e & 0xff, z0 = (e >> 8) & 0xffff, nrow = e >> 24;
         if (v < kMaxVars && p.res_ptr[v]) {  // uniform
             const Rsrc3 rr_ = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.res_ptr[v]), 0, 0x7ffffffc,
                                                                 0x00020000);
-            const unsigned rb = oblk[ct] * (unsigned)p.res_bs[v] + oii[ct];
+            const unsigned rb = oblk * (unsigned)p.res_bs[v] + oii;
             const unsigned rld = (unsigned)p.res_ld[v];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int row = 4 * hq + q;
-                const unsigned off = (ovalid[ct] & (row < nrow)) ? (rb + (unsigned)(z0 + row) * rld) * 4u : 0x80000000u;
+                const unsigned off = (ovalid & (row < nrow)) ? (rb + (unsigned)(z0 + row) * rld) * 4u : 0x80000000u;
                 r[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr_, (int)off, 0, 0));
             }
             return 4;
@@ -681,7 +659,7 @@ dense_b3_kernel(B3Args pa)
         for (int q = 0; q < 4; ++q) r[q] = 0.0f;
         return 0;
     };
-    auto out_tile = [&](const b3f4& a, int T, int ct, const float (&r)[4]) -> int {  // returns the stores issued
+    auto out_tile = [&](const b3f4& a, int T, const float (&r)[4]) -> int {  // returns the stores issued
         const int e = p.otile[T];
         const int v = e & 0xff, z0 = (e >> 8) & 0xffff, nrow = e >> 24;
         if (v >= kMaxVars) return 0;  // padding tile (uniform)
@@ -694,7 +672,7 @@ dense_b3_kernel(B3Args pa)
         const b3f4 hi = *reinterpret_cast<const b3f4*>(s_oc + 4 * kop + R0);
         const b3f4 mk = *reinterpret_cast<const b3f4*>(s_oc + 5 * kop + R0);
         const Rsrc3 ro = __builtin_amdgcn_make_buffer_rsrc(p.out_ptr[v], 0, 0x7ffffffc, 0x00020000);
-        const unsigned ob = oblk[ct] * (unsigned)p.out_bs[v] + oii[ct];
+        const unsigned ob = oblk * (unsigned)p.out_bs[v] + oii;
         const unsigned old_ = (unsigned)p.out_ld[v];
         const bool has_res = p.res_ptr[v] != nullptr;  // uniform
 #pragma unroll
@@ -707,7 +685,7 @@ dense_b3_kernel(B3Args pa)
             if (y >= hi[q]) y = hi[q];
             y = y * mk[q];
             if (has_res) y = r[q] + y;
-            const unsigned off = (ovalid[ct] & (row < nrow)) ? (ob + (unsigned)(z0 + row) * old_) * 4u : 0x80000000u;
+            const unsigned off = (ovalid & (row < nrow)) ? (ob + (unsigned)(z0 + row) * old_) * 4u : 0x80000000u;
 #ifdef FV3_B3_EXP_NOOUT  // experiment only (results invalid): store only a value that is never true
             if (y == 1234.5f)
 #endif
@@ -716,11 +694,7 @@ dense_b3_kernel(B3Args pa)
         return 4;
     };
 
-    float rawA[CPW][8], rawB[CPW][8];
-    auto load_in_all = [&](float (&raw)[CPW][8], int c) {
-#pragma unroll
-        for (int ct = 0; ct < CPW; ++ct) load_in(raw[ct], c, ct);
-    };
+    float rawA[8], rawB[8];
     int64_t tile = blockIdx.x;
     set_load_tile(tile);
     if (tile < p.ntiles) {
@@ -728,8 +702,8 @@ dense_b3_kernel(B3Args pa)
             glds_in(0, 0);
             if (p.n1 > 1) glds_in(1, 1);
         } else {
-            load_in_all(rawA, 0);
-            if (p.n1 > 1) load_in_all(rawB, 1);
+            load_in(rawA, 0);
+            if (p.n1 > 1) load_in(rawB, 1);
         }
     }
     if constexpr (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -759,12 +733,9 @@ dense_b3_kernel(B3Args pa)
     };
     for (; tile < p.ntiles; tile += gridDim.x) {
         mark(0);
-#pragma unroll
-        for (int ct = 0; ct < CPW; ++ct) {
-            oblk[ct] = lblk[ct];
-            oii[ct] = lii[ct];
-            ovalid[ct] = lvalid[ct];
-        }
+        oblk = lblk;
+        oii = lii;
+        ovalid = lvalid;
         // ---- layer 1 over the padded input features ----
         zero_acc();
         if constexpr (GL) {
@@ -772,32 +743,27 @@ dense_b3_kernel(B3Args pa)
             // then the weight DMA of chunk c + 2 and the input DMA of chunk c + 2 into the
             // buffer just read
             for (int c = 0; c < p.n1; ++c) {
-                bf16x8 xb[CPW][NS];
-#pragma unroll
-                for (int ct = 0; ct < CPW; ++ct) {
-                    read_in(c & 1, c, ct, rawA[ct]);
-                    stage_in(rawA[ct], c, xb[ct]);
-                }
+                bf16x8 xb[NS];
+                read_in(c & 1, c, rawA);
+                stage_in(rawA, c, xb);
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the reads above before the DMA refills the buffer
                 step_layer(xb, [&]() {
                     if (c + 2 < p.n1) {
                         glds_in(c & 1, c + 2);
-                        return 8 * CPW;
+                        return 8;
                     }
                     return 0;
                 });
             }
         } else
         for (int c = 0; c < p.n1; c += 2) {
-            bf16x8 xb[CPW][NS];
-#pragma unroll
-            for (int ct = 0; ct < CPW; ++ct) stage_in(rawA[ct], c, xb[ct]);
-            if (c + 2 < p.n1) load_in_all(rawA, c + 2);
+            bf16x8 xb[NS];
+            stage_in(rawA, c, xb);
+            if (c + 2 < p.n1) load_in(rawA, c + 2);
             step_layer(xb, [] { return 0; });
             if (c + 1 < p.n1) {
-#pragma unroll
-                for (int ct = 0; ct < CPW; ++ct) stage_in(rawB[ct], c + 1, xb[ct]);
-                if (c + 3 < p.n1) load_in_all(rawB, c + 3);
+                stage_in(rawB, c + 1, xb);
+                if (c + 3 < p.n1) load_in(rawB, c + 3);
                 step_layer(xb, [] { return 0; });
             }
         }
@@ -807,98 +773,83 @@ dense_b3_kernel(B3Args pa)
         for (int l = 0; l < p.nhx; ++l) {
             zero_acc();
             sfor<KS>([&](auto cc) {
-                bf16x8 tb[CPW][NS];
+                bf16x8 tb[NS];
                 step_layer(hidden_b(cc, tb), [] { return 0; });
             });
             hidden_epi(l + 1);
         }
         if constexpr (NS == 3)
-            sfor<KS>([&](auto cc) {
-#pragma unroll
-                for (int ct = 0; ct < CPW; ++ct) splitN<NS>(Y[decltype(cc)::value][ct], B[decltype(cc)::value][ct]);
-            });
+            sfor<KS>([&](auto cc) { splitN<NS>(Y[decltype(cc)::value], B[decltype(cc)::value]); });
         mark(2);
         // ---- output layer, two 16-row tiles per chunk; the next tile's inputs start loading ----
         const int64_t nt = tile + gridDim.x;
         if (nt < p.ntiles) {
             set_load_tile(nt);
             if constexpr (!GL) {
-                load_in_all(rawA, 0);
-                if (p.n1 > 1) load_in_all(rawB, 1);
+                load_in(rawA, 0);
+                if (p.n1 > 1) load_in(rawB, 1);
             }
         }
-        b3f4 accP[CPW][2];
-        float resN[CPW][2][4], resP[CPW][2][4];
-        auto roll = [&]() {  // this chunk's accumulators / residuals become the previous chunk's
-#pragma unroll
-            for (int ct = 0; ct < CPW; ++ct) {
-                accP[ct][0] = acc[ct][0];
-                accP[ct][1] = acc[ct][1];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    resP[ct][0][q] = resN[ct][0][q];
-                    resP[ct][1][q] = resN[ct][1][q];
-                }
-            }
-        };
-        auto res_loads = [&](int oc) {
-            int n = 0;
-#pragma unroll
-            for (int ct = 0; ct < CPW; ++ct) {
-                n += res_load(2 * oc, ct, resN[ct][0]);
-                n += res_load(2 * oc + 1, ct, resN[ct][1]);
-            }
-            return n;
-        };
-        auto out_prev = [&](int oc) {  // the epilogue of output chunk oc (accP / resP)
-            int n = 0;
-#pragma unroll
-            for (int ct = 0; ct < CPW; ++ct) {
-                n += out_tile(accP[ct][0], 2 * oc, ct, resP[ct][0]);
-                n += out_tile(accP[ct][1], 2 * oc + 1, ct, resP[ct][1]);
-            }
-            return n;
-        };
-        auto zero_out_acc = [&]() {
-#pragma unroll
-            for (int ct = 0; ct < CPW; ++ct) acc[ct][0] = acc[ct][1] = b3f4{0.0f, 0.0f, 0.0f, 0.0f};
-        };
+        b3f4 accP[2];
+        float resN[2][4], resP[2][4];
         if constexpr (GL) {
             // chunk oc: the weight DMA of chunk +2, this chunk's residual loads (consumed
             // one chunk later), the MFMAs, then the previous chunk's epilogue (8 stores).
             // The next tile's input DMA (16 per thread) goes out with the last chunk.
             for (int oc = 0; oc < p.n_oc; ++oc) {
-                zero_out_acc();
+                acc[0] = acc[1] = b3f4{0.0f, 0.0f, 0.0f, 0.0f};
                 stage_next();
-                int younger = res_loads(oc);
+                int younger = res_load(2 * oc, resN[0]);
+                younger += res_load(2 * oc + 1, resN[1]);
                 if (oc + 1 == p.n_oc && nt < p.ntiles) {
                     glds_in(0, 0);
-                    younger += 8 * CPW;
+                    younger += 8;
                     if (p.n1 > 1) {
                         glds_in(1, 1);
-                        younger += 8 * CPW;
+                        younger += 8;
                     }
                 }
                 step_out();
-                if (oc > 0) younger += out_prev(oc - 1);
+                if (oc > 0) {
+                    younger += out_tile(accP[0], 2 * oc - 2, resP[0]);
+                    younger += out_tile(accP[1], 2 * oc - 1, resP[1]);
+                }
                 advance(younger);
-                roll();
+                accP[0] = acc[0];
+                accP[1] = acc[1];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    resP[0][q] = resN[0][q];
+                    resP[1][q] = resN[1][q];
+                }
             }
-            out_prev(p.n_oc - 1);
+            out_tile(accP[0], 2 * p.n_oc - 2, resP[0]);
+            out_tile(accP[1], 2 * p.n_oc - 1, resP[1]);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's inputs landed
             mark(3);
             continue;
         }
         for (int oc = 0; oc < p.n_oc; ++oc) {
-            res_loads(oc);  // lands while this chunk and the next run their MFMAs
-            zero_out_acc();
+            res_load(2 * oc, resN[0]);  // lands while this chunk and the next run their MFMAs
+            res_load(2 * oc + 1, resN[1]);
+            acc[0] = acc[1] = b3f4{0.0f, 0.0f, 0.0f, 0.0f};
             stage_next();
             step_out();
-            if (oc > 0) out_prev(oc - 1);  // finish the previous chunk while these MFMAs run
+            if (oc > 0) {  // finish the previous chunk while these MFMAs run
+                out_tile(accP[0], 2 * oc - 2, resP[0]);
+                out_tile(accP[1], 2 * oc - 1, resP[1]);
+            }
             advance(0);
-            roll();
+            accP[0] = acc[0];
+            accP[1] = acc[1];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                resP[0][q] = resN[0][q];
+                resP[1][q] = resN[1][q];
+            }
         }
-        out_prev(p.n_oc - 1);
+        out_tile(accP[0], 2 * p.n_oc - 2, resP[0]);
+        out_tile(accP[1], 2 * p.n_oc - 1, resP[1]);
         mark(3);
     }
 }
@@ -1200,14 +1151,10 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
     // tiles of 128 on 256 CUs -> 216 of 64); FV3_B3_WAVES=4|8 forces one (A/B)
     int nwv = (ncol + kB3Cols - 1) / kB3Cols < n_cu ? 4 : 8;
     if (const char* e = getenv("FV3_B3_WAVES")) nwv = atoi(e) == 4 ? 4 : 8;
-    // FV3_B3_CPW=2: 4-wave blocks of 128 columns, two column tiles per wave (A/B)
-    int cpw = 1;
-    if (const char* e = getenv("FV3_B3_CPW")) cpw = atoi(e) == 2 ? 2 : 1;
-    if (cpw == 2) nwv = 4;
-    const int nthr = 64 * nwv, ncols = 16 * nwv * cpw;
+    const int nthr = 64 * nwv, ncols = 16 * nwv;
     a.ntiles = (ncol + ncols - 1) / ncols;
     auto lds_of = [&](int sl) {
-        return (size_t)b3_slots(sl) * 1024 * b.ns * b.hu + (size_t)b3_in_bytes(sl > 0, nwv, cpw) +
+        return (size_t)b3_slots(sl) * 1024 * b.ns * b.hu + (size_t)b3_in_bytes(sl > 0, nwv) +
                (size_t)4 * ((b.nconst + 7) & ~7) + sizeof(B3Grp) * 4 * b.n1;
     };
     // the LDS-DMA pipeline with a 3-slot ring where it fits, else (bf16x6) with 2 slots;
@@ -1220,17 +1167,13 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
         constexpr int NS = decltype(ns)::value;
         auto by_hu = [&](auto slc) -> const void* {
             constexpr int S = decltype(slc)::value;
-            if (cpw == 2)
-                return b.hu == 4 ? (const void*)dense_b3_kernel<4, S, NS, 4, 2>
-                     : b.hu == 8 ? (const void*)dense_b3_kernel<8, S, NS, 4, 2>
-                                 : (const void*)dense_b3_kernel<16, S, NS, 4, 2>;
             if (nwv == 4)
-                return b.hu == 4 ? (const void*)dense_b3_kernel<4, S, NS, 4, 1>
-                     : b.hu == 8 ? (const void*)dense_b3_kernel<8, S, NS, 4, 1>
-                                 : (const void*)dense_b3_kernel<16, S, NS, 4, 1>;
-            return b.hu == 4 ? (const void*)dense_b3_kernel<4, S, NS, 8, 1>
-                 : b.hu == 8 ? (const void*)dense_b3_kernel<8, S, NS, 8, 1>
-                             : (const void*)dense_b3_kernel<16, S, NS, 8, 1>;
+                return b.hu == 4 ? (const void*)dense_b3_kernel<4, S, NS, 4>
+                     : b.hu == 8 ? (const void*)dense_b3_kernel<8, S, NS, 4>
+                                 : (const void*)dense_b3_kernel<16, S, NS, 4>;
+            return b.hu == 4 ? (const void*)dense_b3_kernel<4, S, NS, 8>
+                 : b.hu == 8 ? (const void*)dense_b3_kernel<8, S, NS, 8>
+                             : (const void*)dense_b3_kernel<16, S, NS, 8>;
         };
         if constexpr (NS == 3)
             if (sl == 2) return by_hu(std::integral_constant<int, 2>{});

@@ -38,19 +38,16 @@ def _check(gpu_out, ref64, rtol=None):
         assert_per_level(g, r, rtol, f"output {o}")
 
 
-@pytest.fixture(autouse=True, params=[("glds", None), ("glds", "8"), ("glds", "4"), ("glds", "c2"), ("reg", None)],
-                ids=["glds", "glds-w8", "glds-w4", "glds-c2", "reg"])
+@pytest.fixture(autouse=True, params=[("glds", None), ("glds", "8"), ("glds", "4"), ("reg", None)],
+                ids=["glds", "glds-w8", "glds-w4", "reg"])
 def b3_stage(request, monkeypatch):
     """Every test on both staging pipelines of the kernel (FV3_B3_STAGE): LDS-DMA (the
     default) and register staging; the LDS-DMA one also with the block shape forced
     (FV3_B3_WAVES: 8-wave blocks of 128 columns, 4-wave blocks of 64, which the host picks
-    for grids with fewer 128-column tiles than CUs; c2: 4-wave blocks of 128 columns, two
-    16-column tiles per wave, FV3_B3_CPW=2)."""
+    for grids with fewer 128-column tiles than CUs)."""
     stage, waves = request.param
     monkeypatch.setenv("FV3_B3_STAGE", stage)
-    if waves == "c2":
-        monkeypatch.setenv("FV3_B3_CPW", "2")
-    elif waves:
+    if waves:
         monkeypatch.setenv("FV3_B3_WAVES", waves)
     return request.param
 
