@@ -76,7 +76,7 @@ EXPORTED_SYMBOLS = (
     "fv3_derived_elementwise",
     "fv3_derived_columns",
 )
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 # fv3_dense_forward_ex precisions
 DENSE_F32 = 0
@@ -255,6 +255,18 @@ _SIGNATURES = {
     "fv3_derived_elementwise": (_I, [_I, ctypes.POINTER(_P), ctypes.POINTER(_I), _I, _P, _I, _I64,
                                      ctypes.POINTER(_D), _I, _P]),
     "fv3_host_register": (_I, [_P, ctypes.c_size_t]),
+    "fv3_plan_create": (_I, [ctypes.POINTER(_P)]),
+    "fv3_plan_destroy": (_I, [_P]),
+    "fv3_plan_size": (_I, [_P]),
+    "fv3_plan_run": (_I, [_P, _P]),
+    "fv3_plan_add_dense_forward": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(Layout), ctypes.POINTER(_P),
+                                        ctypes.POINTER(Layout), _I64, _I, _I]),
+    "fv3_plan_add_ml_epilogue": (_I, [_P, ctypes.POINTER(EpilogueIO), Layout, _I64, _I, _I, _D, _I, _I, _I]),
+    "fv3_plan_add_area_weighted_sums_f64": (_I, [_P, ctypes.POINTER(_P), _I, _P, _I64, _P]),
+    "fv3_plan_add_area_weighted_row_sums_f64": (_I, [_P, ctypes.POINTER(_P), _I, _P, _I64, _I, _P, _I64]),
+    "fv3_plan_add_level_sums_u8": (_I, [_P, _P, Layout, _I64, _I, _P]),
+    "fv3_plan_add_fold_rows": (_I, [_P, _P, _I64, _I, _P]),
+    "fv3_plan_add_copy": (_I, [_P, _P, _P, ctypes.c_size_t]),
     "fv3_host_unregister": (_I, [_P]),
     "fv3_derived_columns": (_I, [_I, ctypes.POINTER(Field), _I, ctypes.POINTER(Field), _I, _I64, _I,
                                  ctypes.POINTER(_D), _I, _P]),

@@ -425,44 +425,6 @@ __global__ __launch_bounds__(256) void mappm_ppm_pair_kernel(MappmPairArgs a)
     mappm_ppm_columns<2>(d, a.km, a.kn, a.iv, a.kord);
 }
 
-// Several fields on the same edges, one lane per (column, field): blockIdx.y is the field.
-// Below kFieldLanesMaxCols columns the one-lane-per-column kernels run too few waves to
-// hide their per-level latency (one rank's C384 band at world 8, 110,592 columns: 1.7
-// waves per SIMD), so there the fields take a lane each, doubling the waves of a
-// two-field call, instead of sharing one lane (mappm_ppm_pair_kernel: less arithmetic,
-// which is what binds on full grids).  Each field keeps the bits of its own call.
-constexpr int kFieldLanes = 8;  // fields per launch
-constexpr int64_t kFieldLanesMaxCols = 262144;
-struct MappmFieldsArgs {
-    const float* pe1;
-    const float* pe2;
-    fv3_layout l_pe1, l_pe2;
-    const float* q1[kFieldLanes];
-    float* q2[kFieldLanes];
-    fv3_layout l_q1[kFieldLanes], l_q2[kFieldLanes];
-    int64_t ncol;
-    int km, kn, iv, kord;
-};
-
-__global__ __launch_bounds__(256) void mappm_ppm_fields_kernel(MappmFieldsArgs a)
-{
-    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= a.ncol) return;
-    const int f = blockIdx.y;
-    const MappmArgs one{a.pe1, a.q1[f], a.pe2, a.q2[f], a.l_pe1, a.l_q1[f], a.l_pe2, a.l_q2[f],
-                        a.ncol, a.km, a.kn, a.iv, a.kord, nullptr};
-    DevCol col = make_col(one, c);
-    mappm_ppm_column(col, a.km, a.kn, a.iv, a.kord);
-}
-
-// FV3_MAPPM_FIELDS=pair|lanes forces one scheme (A/B; every scheme gives the same bits)
-bool use_field_lanes(int64_t ncol, int n_fields)
-{
-    if (n_fields < 2) return false;
-    if (const char* e = getenv("FV3_MAPPM_FIELDS")) return e[0] == 'l';
-    return ncol < kFieldLanesMaxCols;
-}
-
 }  // namespace fv3
 
 using fv3::MappmArgs;
@@ -518,22 +480,6 @@ extern "C" int fv3_mappm_multi(const float* pe1, fv3_layout pe1_l, const float* 
     // pairs on the streaming kord <= 7 kernel; the level-parallel (small grids) and
     // cs_profile (kord > 7) paths, and an odd last field, one field per launch
     MappmArgs one{pe1, nullptr, pe2, nullptr, pe1_l, {}, pe2_l, {}, ncol, km, kn, iv, kord, nullptr};
-    if (kord <= 7 && !fv3::use_levels_kernel(one) && fv3::use_field_lanes(ncol, n_fields)) {
-        for (; f < n_fields; f += fv3::kFieldLanes) {
-            const int nf = std::min(fv3::kFieldLanes, n_fields - f);
-            fv3::MappmFieldsArgs a{pe1, pe2, pe1_l, pe2_l, {}, {}, {}, {}, ncol, km, kn, iv, kord};
-            for (int i = 0; i < nf; ++i) {
-                a.q1[i] = q1[f + i];
-                a.q2[i] = q2[f + i];
-                a.l_q1[i] = q1_l[f + i];
-                a.l_q2[i] = q2_l[f + i];
-            }
-            const int block = 256;
-            const int64_t grid = (ncol + block - 1) / block;
-            hipLaunchKernelGGL(fv3::mappm_ppm_fields_kernel, dim3((unsigned)grid, (unsigned)nf), dim3(block), 0, s, a);
-            FV3_LAUNCH_CHECK();
-        }
-    }
     if (kord <= 7 && !fv3::use_levels_kernel(one)) {
         for (; f + 2 <= n_fields; f += 2) {
             fv3::MappmPairArgs a{pe1, pe2, pe1_l, pe2_l, {q1[f], q1[f + 1]}, {q2[f], q2[f + 1]},

@@ -7,6 +7,7 @@ from typing import List, Optional
 import numpy as np
 
 from .dense import DenseColumnModel, DenseModelConfig
+from .plan import LaunchPlan
 
 try:
     import torch
@@ -180,6 +181,7 @@ class StepperWorkload:
     _in32: object = None
     _epi: object = None
     _part: object = None
+    _plan: object = None
 
     def _bind(self):
         """Validate and marshal every launch of the step once (the predict, the fused
@@ -207,6 +209,7 @@ class StepperWorkload:
         diags = [res["net_moistening_due_to_machine_learning"], res["column_heating_due_to_machine_learning"],
                  res["total_precipitation"]]
         self._part = bind_area_weighted_partials(diags, self.area)  # float64 diagnostics: the f64 reduction
+        self._plan = LaunchPlan([self.bound, self._epi, self._part])  # one C-ABI call per step
 
     def step(self):
         from . import _device
@@ -218,9 +221,8 @@ class StepperWorkload:
         if self._in32 is not None:
             self._in32[0].copy_(self.state["air_temperature"])
             self._in32[1].copy_(self.state["specific_humidity"])
-        self.bound(h)
-        self._epi(h)
-        return combine_partials(self._part(h), self.group)
+        self._plan(h)
+        return combine_partials(self._part.result, self.group)
 
 
 def make_stepper_workload(res: int = 96, seed: int = 0, device=None, group=None, precision: str = "f32"):
@@ -284,6 +286,7 @@ class ShardedStepperWorkload:
     _fold: object = None
     _rep: object = None
     _res: object = None
+    _plan: object = None
 
     def _bind(self):
         """Marshal every launch of the step once (predict, fused epilogue, row partials,
@@ -319,6 +322,13 @@ class ShardedStepperWorkload:
             self.exchange_bytes = 8 * (nrows * 6 + nz)
         else:
             self._lev = bind_level_sums(limiter)
+        # one C-ABI call per step: predict, epilogue, row partials, limiter counts (and,
+        # with the stubbed exchange, this band's partials copied for every rank + the fold)
+        self._plan = LaunchPlan([self.bound, self._epi, self._rows, self._lev])
+        if self._fold is not None:
+            for r in range(self.stub_world):
+                self._plan.copy(self._rep[r * nrows:(r + 1) * nrows], self.partials)
+            self._plan.add(self._fold)
 
     def step(self):
         from . import _device
@@ -326,15 +336,9 @@ class ShardedStepperWorkload:
 
         if self.bound is None:
             self._bind()
-        h = _device.stream_handle()
-        self.bound(h)
-        self._epi(h)
-        self._rows(h)
-        limited = self._lev(h)
-        if self._fold is not None:  # stubbed exchange: this band's partials for every rank
-            nrows = self.partials.shape[0]
-            self._rep.view(self.stub_world, nrows, 6).copy_(self.partials.unsqueeze(0).expand(self.stub_world, -1, -1))
-            self._fold(h)
+        self._plan(_device.stream_handle())
+        limited = self._lev.result
+        if self._fold is not None:  # stubbed exchange: the fold of every rank's (this band's) rows
             return self._res.clone()
         if self.counts is None:  # the bands are fixed: their sizes are exchanged once
             self.counts = row_counts(self.partials.shape[0], self.group)

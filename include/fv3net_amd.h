@@ -54,7 +54,8 @@ const char* fv3_last_error(void);
 int fv3_abi_version(void); /* bumped on any signature change (2: emulator fields in fv3_dense_desc,
                               3: fv3_dense_forward_ex, 4: composites + Adapter,
                               5: per-operand dtypes in fv3_adapter_target, fv3_build_kind,
-                              6: fv3_host_register / fv3_host_unregister) */
+                              6: fv3_host_register / fv3_host_unregister,
+                              7: fv3_plan_*) */
 const char* fv3_build_kind(void); /* "product" (fv3net_amd/build.py, no experiment knob compiled in)
                                      or "experiment" (a tools/ variant: results may be invalid) */
 
@@ -590,6 +591,37 @@ int fv3_derived_columns(int op, const fv3_field* in, int n_in, const fv3_field* 
  */
 int fv3_host_register(void* ptr, size_t bytes);
 int fv3_host_unregister(void* ptr);
+
+/*
+ * Launch plan: a fixed sequence of this library's launches over fixed device buffers,
+ * recorded once and issued by one call per timestep (the prognostic loop applies the
+ * same state buffers every step; runtime/loop.py:604-628 around
+ * runtime/steppers/machine_learning.py:239-309).  Each fv3_plan_add_* takes the
+ * arguments of the entry point it names, minus the stream; fv3_plan_run issues them in
+ * order on `stream` and returns the first failing status.  Every buffer named must stay
+ * allocated while the plan is used; the dense model must outlive the plan.
+ */
+typedef struct fv3_plan fv3_plan;
+int fv3_plan_create(fv3_plan** out);
+int fv3_plan_destroy(fv3_plan* plan);
+int fv3_plan_size(const fv3_plan* plan);
+int fv3_plan_run(const fv3_plan* plan, void* stream);
+/* fv3_dense_forward_f64in (inputs_f64 != 0) or fv3_dense_forward_ex at `precision` */
+int fv3_plan_add_dense_forward(fv3_plan* plan, const fv3_dense_model* model, const void* const* inputs,
+                               const fv3_layout* in_l, float* const* outputs, const fv3_layout* out_l, int64_t ncol,
+                               int precision, int inputs_f64);
+int fv3_plan_add_ml_epilogue(fv3_plan* plan, const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, int nz,
+                             int state_f64, double dt, int mse_conserving, int hydrostatic, int flags);
+int fv3_plan_add_area_weighted_sums_f64(fv3_plan* plan, const double* const* diags, int n_diag, const double* area,
+                                        int64_t n, double* out);
+int fv3_plan_add_area_weighted_row_sums_f64(fv3_plan* plan, const double* const* diags, int n_diag,
+                                            const double* area, int64_t nrows, int row_len, double* partial,
+                                            int64_t partial_ld);
+int fv3_plan_add_level_sums_u8(fv3_plan* plan, const unsigned char* x, fv3_layout x_l, int64_t ncol, int nz,
+                               double* out);
+int fv3_plan_add_fold_rows(fv3_plan* plan, const double* rows, int64_t nrows, int width, double* out);
+/* device-to-device copy of `bytes` */
+int fv3_plan_add_copy(fv3_plan* plan, void* dst, const void* src, size_t bytes);
 
 #ifdef __cplusplus
 }

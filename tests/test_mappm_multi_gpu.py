@@ -14,16 +14,11 @@ from tests.test_mappm_gpu import _bits_equal, _columns
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["pair", "lanes", "levels"])
+@pytest.fixture(params=["serial", "levels"])
 def path(request, monkeypatch):
-    """One lane per column: `pair`, pairs of fields on the two-field streaming kernel
-    (full grids); `lanes`, one lane per (column, field) (mid-size grids,
-    mappm_ppm_fields_kernel); `levels`: the small-grid kernel, one field per launch."""
-    if request.param == "levels":
-        monkeypatch.setenv("FV3_MAPPM_PATH", "levels")
-    else:
-        monkeypatch.setenv("FV3_MAPPM_PATH", "serial")
-        monkeypatch.setenv("FV3_MAPPM_FIELDS", request.param)
+    """`serial` (one lane per column): pairs of fields on the two-field streaming
+    kernel; `levels`: the small-grid kernel, one field per launch."""
+    monkeypatch.setenv("FV3_MAPPM_PATH", request.param)
     return request.param
 
 
