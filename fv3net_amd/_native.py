@@ -267,6 +267,7 @@ _SIGNATURES = {
     "fv3_plan_add_level_sums_u8": (_I, [_P, _P, Layout, _I64, _I, _P]),
     "fv3_plan_add_fold_rows": (_I, [_P, _P, _I64, _I, _P]),
     "fv3_plan_add_copy": (_I, [_P, _P, _P, ctypes.c_size_t]),
+    "fv3_plan_add_repeat": (_I, [_P, _P, _P, ctypes.c_size_t, _I]),
     "fv3_host_unregister": (_I, [_P]),
     "fv3_derived_columns": (_I, [_I, ctypes.POINTER(Field), _I, ctypes.POINTER(Field), _I, _I64, _I,
                                  ctypes.POINTER(_D), _I, _P]),

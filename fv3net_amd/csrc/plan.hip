@@ -24,6 +24,18 @@ struct fv3_plan {
     std::vector<std::function<int(void*)>> ops;
 };
 
+namespace {
+// dst[t][i] = src[i], t < times, over 4-byte words (one launch for every copy)
+__global__ __launch_bounds__(256) void repeat_words_kernel(const unsigned* __restrict__ src, int64_t n, int times,
+                                                           unsigned* __restrict__ dst)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned v = src[i];
+    for (int t = 0; t < times; ++t) dst[(int64_t)t * n + i] = v;
+}
+}  // namespace
+
 extern "C" int fv3_plan_create(fv3_plan** out)
 {
     using namespace fv3;
@@ -148,6 +160,24 @@ extern "C" int fv3_plan_add_copy(fv3_plan* plan, void* dst, const void* src, siz
     FV3_REQUIRE(plan && (bytes == 0 || (dst && src)), "plan_add_copy: bad argument");
     plan->ops.push_back([=](void* s) -> int {
         if (bytes) FV3_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)s));
+        return FV3_OK;
+    });
+    return FV3_OK;
+}
+
+// `times` back-to-back copies of `bytes` (a multiple of 4) into dst, one launch
+extern "C" int fv3_plan_add_repeat(fv3_plan* plan, void* dst, const void* src, size_t bytes, int times)
+{
+    using namespace fv3;
+    clear_error();
+    FV3_REQUIRE(plan && times >= 0 && bytes % 4 == 0, "plan_add_repeat: bad argument (bytes must be a multiple of 4)");
+    FV3_REQUIRE(bytes == 0 || times == 0 || (dst && src), "plan_add_repeat: NULL array");
+    const int64_t n = (int64_t)(bytes / 4);
+    plan->ops.push_back([=](void* s) -> int {
+        if (n == 0 || times == 0) return FV3_OK;
+        hipLaunchKernelGGL(repeat_words_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)s,
+                           (const unsigned*)src, n, times, (unsigned*)dst);
+        FV3_LAUNCH_CHECK();
         return FV3_OK;
     });
     return FV3_OK;

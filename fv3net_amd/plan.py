@@ -71,6 +71,18 @@ class LaunchPlan:
         self._keep.append((dst, src))
         return self
 
+    def repeat(self, dst, src, times: int):
+        """``times`` back-to-back copies of ``src``'s bytes into ``dst`` (contiguous CUDA
+        tensors, dst holding exactly ``times`` copies), one launch."""
+        n = src.numel() * src.element_size()
+        if not (dst.is_cuda and src.is_cuda and dst.is_contiguous() and src.is_contiguous()
+                and dst.numel() * dst.element_size() == n * times and n % 4 == 0):
+            raise ValueError("plan repeat: contiguous CUDA tensors, dst = times x src bytes (a multiple of 4)")
+        _native.check(self._lib.fv3_plan_add_repeat(self._h, dst.data_ptr(), src.data_ptr(), n, int(times)),
+                      "plan_add_repeat")
+        self._keep.append((dst, src))
+        return self
+
     def __call__(self, stream=None):
         h = stream if isinstance(stream, int) else _device.stream_handle(stream)
         st = self._lib.fv3_plan_run(self._h, h)

@@ -326,8 +326,7 @@ class ShardedStepperWorkload:
         # with the stubbed exchange, this band's partials copied for every rank + the fold)
         self._plan = LaunchPlan([self.bound, self._epi, self._rows, self._lev])
         if self._fold is not None:
-            for r in range(self.stub_world):
-                self._plan.copy(self._rep[r * nrows:(r + 1) * nrows], self.partials)
+            self._plan.repeat(self._rep, self.partials, self.stub_world)
             self._plan.add(self._fold)
 
     def step(self):

@@ -622,6 +622,8 @@ int fv3_plan_add_level_sums_u8(fv3_plan* plan, const unsigned char* x, fv3_layou
 int fv3_plan_add_fold_rows(fv3_plan* plan, const double* rows, int64_t nrows, int width, double* out);
 /* device-to-device copy of `bytes` */
 int fv3_plan_add_copy(fv3_plan* plan, void* dst, const void* src, size_t bytes);
+/* `times` back-to-back copies of `bytes` (a multiple of 4) of src into dst, one launch */
+int fv3_plan_add_repeat(fv3_plan* plan, void* dst, const void* src, size_t bytes, int times);
 
 #ifdef __cplusplus
 }

@@ -82,6 +82,11 @@ def test_plan_refuses_unknown_ops(gpu):
     x = torch.from_numpy(np.arange(10.0)).cuda()
     y = torch.zeros_like(x)
     plan.copy(y, x)
+    z = torch.zeros((3, 10), dtype=torch.float64, device="cuda")
+    plan.repeat(z, x, 3)
+    with pytest.raises(ValueError):
+        plan.repeat(torch.zeros((2, 10), dtype=torch.float64, device="cuda"), x, 3)
     plan()
     torch.cuda.synchronize()
     assert torch.equal(x, y)
+    assert all(torch.equal(z[t], x) for t in range(3))
