@@ -1033,21 +1033,94 @@ static int pack_ns(fv3_dense_model* m, const fv3_dense_desc* d, int NS, B3Pack**
     return FV3_OK;
 }
 
+// A host copy of the parts of fv3_dense_desc that pack_ns reads (the caller's arrays are
+// only valid during fv3_dense_create): the bf16x6 stream, which only bf16x6 callers need,
+// is packed from it on the first bf16x6 forward instead of with every model.
+struct B3Desc {
+    fv3_dense_desc d{};
+    std::vector<std::vector<float>> hk, hb, ok, ob;
+    std::vector<const float*> hkp, hbp, okp, obp;
+    std::vector<float> in_mean, in_sigma, out_mean, out_sigma, out_min, out_max, out_mask;
+};
+
+static B3Desc* copy_desc(const fv3_dense_model* m, const fv3_dense_desc* d)
+{
+    auto c = std::make_unique<B3Desc>();
+    const int W = d->width, kin = m->k_in, kout = m->k_out;
+    auto vec = [](const float* p, size_t n) { return p ? std::vector<float>(p, p + n) : std::vector<float>(); };
+    c->in_mean = vec(d->in_mean, kin);
+    c->in_sigma = vec(d->in_sigma, kin);
+    c->out_mean = vec(d->out_mean, kout);
+    c->out_sigma = vec(d->out_sigma, kout);
+    c->out_min = vec(d->out_min, kout);
+    c->out_max = vec(d->out_max, kout);
+    c->out_mask = vec(d->out_mask, kout);
+    for (int l = 0; l < d->n_hidden; ++l) {
+        c->hk.push_back(vec(d->hidden_kernel[l], (size_t)(l == 0 ? kin : W) * W));
+        c->hb.push_back(vec(d->hidden_bias[l], W));
+    }
+    for (int v = 0; v < m->n_out; ++v) {
+        c->ok.push_back(vec(d->out_kernel[v], (size_t)W * m->out_nz[v]));
+        c->ob.push_back(vec(d->out_bias[v], m->out_nz[v]));
+    }
+    for (auto& x : c->hk) c->hkp.push_back(x.data());
+    for (auto& x : c->hb) c->hbp.push_back(x.data());
+    for (auto& x : c->ok) c->okp.push_back(x.data());
+    for (auto& x : c->ob) c->obp.push_back(x.data());
+    c->d = *d;
+    c->d.in_mean = c->in_mean.data();
+    c->d.in_sigma = c->in_sigma.data();
+    c->d.out_mean = c->out_mean.data();
+    c->d.out_sigma = c->out_sigma.data();
+    c->d.out_min = d->out_min ? c->out_min.data() : nullptr;
+    c->d.out_max = d->out_max ? c->out_max.data() : nullptr;
+    c->d.out_mask = d->out_mask ? c->out_mask.data() : nullptr;
+    c->d.hidden_kernel = c->hkp.data();
+    c->d.hidden_bias = c->hbp.data();
+    c->d.out_kernel = c->okp.data();
+    c->d.out_bias = c->obp.data();
+    // pack_ns reads nothing else of the description (the rest is in the model)
+    c->d.in_nz = nullptr;
+    c->d.in_clip = nullptr;
+    c->d.out_nz = nullptr;
+    c->d.in_log_eps = nullptr;
+    c->d.out_residual = nullptr;
+    return c.release();
+}
+
 // Each split stream is packed on its own: a model one of them cannot hold (too many
 // input features or output rows, a stream past 2 GiB) leaves only that precision
 // unsupported (fv3_dense_forward_ex returns FV3_ERR_UNSUPPORTED for it), and the exact-f32
-// path is never affected.  Only a HIP failure fails fv3_dense_create.
+// path is never affected.  Only a HIP failure fails fv3_dense_create.  The bf16x3 stream
+// is packed here; the bf16x6 one (1.5x its size) on the first bf16x6 forward.
 int b3_pack(fv3_dense_model* m, const fv3_dense_desc* d)
 {
-    for (int ns : {2, 3}) {
-        B3Pack** dst = ns == 2 ? &m->b3 : &m->b6;
-        const int st = pack_ns(m, d, ns, dst);
-        if (st == FV3_ERR_HIP) return st;
-        if (st != FV3_OK) {
-            *dst = nullptr;
-            clear_error();
-        }
+    const int st = pack_ns(m, d, 2, &m->b3);
+    if (st == FV3_ERR_HIP) return st;
+    if (st != FV3_OK) {
+        m->b3 = nullptr;
+        clear_error();
     }
+    m->b6_src = copy_desc(m, d);
+    return FV3_OK;
+}
+
+// the bf16x6 stream of `m`, packed now if this is its first use (nullptr: unsupported
+// for this model, with the reason in fv3_last_error; HIP failures return FV3_ERR_HIP)
+static int b6_stream(const fv3_dense_model* cm, const B3Pack** out)
+{
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lock(mu);
+    fv3_dense_model* m = const_cast<fv3_dense_model*>(cm);  // the lazily packed stream only
+    if (!m->b6 && m->b6_src) {
+        const int st = pack_ns(m, &m->b6_src->d, 3, &m->b6);
+        if (st == FV3_ERR_HIP) return st;  // keep the source: a later call may retry
+        if (st != FV3_OK) m->b6 = nullptr;
+        delete m->b6_src;
+        m->b6_src = nullptr;
+        if (st != FV3_OK) return st;
+    }
+    *out = m->b6;
     return FV3_OK;
 }
 
@@ -1060,6 +1133,8 @@ void b3_free(fv3_dense_model* m)
         delete *pk;
         *pk = nullptr;
     }
+    delete m->b6_src;
+    m->b6_src = nullptr;
 }
 
 }  // namespace fv3
@@ -1074,7 +1149,12 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
     FV3_REQUIRE(precision == FV3_DENSE_BF16X3 || precision == FV3_DENSE_BF16X6,
                 "dense_forward_ex: unknown precision %d", precision);
     FV3_REQUIRE(m, "dense_forward_ex: NULL model");
-    const B3Pack* pk = precision == FV3_DENSE_BF16X6 ? m->b6 : m->b3;
+    const B3Pack* pk = m->b3;
+    if (precision == FV3_DENSE_BF16X6) {
+        const int st = b6_stream(m, &pk);
+        if (st == FV3_ERR_HIP) return st;
+        if (st != FV3_OK) pk = nullptr;
+    }
     FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, pk, "dense_forward_ex: this model has no bf16 split pack "
                      "(too many input features or output rows); use FV3_DENSE_F32");
     FV3_REQUIRE(ncol >= 0, "dense_forward_ex: ncol < 0");

@@ -15,6 +15,7 @@
 // Area sums: fixed-shape two-level tree (per-block partials from wave butterflies in a
 // fixed order, then one block folds them) so the result is bitwise reproducible run to
 // run for a given column count.
+#include <type_traits>
 #include "common.h"
 
 namespace fv3 {
@@ -198,8 +199,16 @@ int level_sums_impl(const T* x, fv3_layout x_l, int64_t ncol, int nz, double* ou
         FV3_HIP(hipMemsetAsync(out, 0, sizeof(double) * (size_t)nz, s));
         return FV3_OK;
     }
-    const int nslice = (int)std::min<int64_t>(kLevelMaxSlices, (ncol + kLevelSlice - 1) / kLevelSlice);
+    // integer counts are exact in any order: their blocks take 8x the columns, so one
+    // rank's band (<= 32,768 columns) is one launch writing the sums directly
+    const int64_t per = std::is_same<T, unsigned char>::value ? 8 * kLevelSlice : kLevelSlice;
+    const int nslice = (int)std::min<int64_t>(kLevelMaxSlices, (ncol + per - 1) / per);
     const int64_t slice = (ncol + nslice - 1) / nslice;
+    if (nslice == 1) {  // stage 2 of one partial is the identity: skip it and its scratch
+        hipLaunchKernelGGL(level_sums_stage1<T>, dim3(1, nz), dim3(kSumBlock), 0, s, x, x_l, ncol, slice, out);
+        FV3_LAUNCH_CHECK();
+        return FV3_OK;
+    }
     void* scratch = nullptr;
     FV3_HIP(hipMallocAsync(&scratch, sizeof(double) * (size_t)nz * nslice, s));
     double* part = (double*)scratch;
