@@ -22,7 +22,8 @@
     defined(FV3_EXP_NOREMAP) || defined(FV3_EXP_NOSTAGE) || defined(FV3_EXP_NOSTORE) ||            \
     defined(FV3_EXP_NOWLOAD) || defined(FV3_B3_EXP_NOFRAG) || defined(FV3_B3_EXP_NOIN) ||          \
     defined(FV3_B3_EXP_NOMFMA) || defined(FV3_B3_EXP_NOOUT) || defined(FV3_B3_EXP_NOSTAGE) ||      \
-    defined(FV3_B3_TRACE) || defined(FV3_EXPERIMENT_BUILD)
+    defined(FV3_B3_EXP_NORES) || defined(FV3_B3_EXP_NOEPI) || defined(FV3_B3_TRACE) ||             \
+    defined(FV3_EXPERIMENT_BUILD)
 #define FV3_EXPERIMENT_KNOBS 1
 #ifdef FV3_PRODUCT_BUILD
 #error "experiment knobs (results invalid) in the product build"

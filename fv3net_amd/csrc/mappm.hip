@@ -51,6 +51,79 @@ struct DevCol {
     }
 };
 
+// DevCol with buffer loads: q1(k) / pe1(k) at a uniform level k are one
+// `buffer_load_dword` of (resource over the array) + (the lane's byte offset, VGPR) +
+// (the level's byte offset, SGPR soffset), so every load in flight holds one data VGPR
+// and no 64-bit address (DevCol's each hold an address pair, which the compiler does not
+// fold into a uniform-base form by itself).  The host checks every array spans < 4 GiB.
+// emit / next_edge walk per-lane pointers as in DevCol.
+#ifndef FV3_MAPPM_EDGE_AHEAD
+#define FV3_MAPPM_EDGE_AHEAD 1  // DevColBuf::next_edge's load one call ahead (0: tools A/B builds)
+#endif
+typedef __amdgpu_buffer_rsrc_t MRsrc;
+__device__ __forceinline__ MRsrc mrsrc(const void* p)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0xffffffffu, 0x00020000);
+}
+__device__ __forceinline__ float bload(MRsrc r, uint32_t voff, uint32_t soff)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
+}
+
+struct DevColBuf {
+    MRsrc r_pe1, r_q1;
+    uint32_t o_pe1, o_q1;     // lane byte offsets
+    uint32_t lb_pe1, lb_q1;   // level strides in bytes
+    const float* pe2_;
+    float* q2_;
+    int64_t ld_pe2, ld_q2;
+    int kn;
+    const float* pe2_next;  // the edge after nb
+    float nb;               // pe2(k + 1) for the next next_edge(k), loaded one call ahead
+    __device__ __forceinline__ float q1(int k) const { return bload(r_q1, o_q1, (uint32_t)(k - 1) * lb_q1); }
+    __device__ __forceinline__ float pe1(int k) const { return bload(r_pe1, o_pe1, (uint32_t)(k - 1) * lb_pe1); }
+    __device__ __forceinline__ float pe2(int k) const { return pe2_[(int64_t)(k - 1) * ld_pe2]; }
+    __device__ __forceinline__ void emit(int, float v)
+    {
+        *q2_ = v;
+        q2_ += ld_q2;
+    }
+    __device__ __forceinline__ float next_edge(int k)
+    {
+        if (k + 1 > kn + 1) return 0.0f;
+#if FV3_MAPPM_EDGE_AHEAD
+        const float r = nb;
+        pe2_next += ld_pe2;
+        nb = (k + 2 <= kn + 1) ? *pe2_next : 0.0f;
+#else  // A/B variant builds: loaded at the call
+        const float r = *pe2_next;
+        pe2_next += ld_pe2;
+#endif
+        return r;
+    }
+};
+
+// GlobalScr through buffer loads / stores (the host checks the scratch is < 4 GiB);
+// e(k) / g(k) are proxies: read as a float, assigned by a store
+struct GlobalScrBuf {
+    MRsrc r;
+    uint32_t o;   // lane byte offset
+    uint32_t sb;  // level stride in bytes
+    uint32_t pb;  // plane stride in bytes
+    struct Ref {
+        MRsrc r;
+        uint32_t o, so;
+        __device__ __forceinline__ operator float() const { return bload(r, o, so); }
+        __device__ __forceinline__ Ref& operator=(float v)
+        {
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)o, (int)so, 0);
+            return *this;
+        }
+    };
+    __device__ __forceinline__ Ref e(int k) const { return Ref{r, o, (uint32_t)k * sb}; }
+    __device__ __forceinline__ Ref g(int k) const { return Ref{r, o, pb + (uint32_t)k * sb}; }
+};
+
 struct LdsScr {
     float* base;  // [2][km+3][blockDim]
     int stride;   // blockDim.x
@@ -286,15 +359,37 @@ __global__ __launch_bounds__(64) void mappm_cs_kernel(MappmArgs a)
 
 // NT > 0: the bottom NT edges of the solve stay in registers (mappm_cs_column), 6 NT
 // fewer scratch accesses per column; the scratch keeps its full [2][km+3] shape
-template <int NT>
+// PF > 0: loads run PF levels ahead in the solve, one layer ahead in the main loop
+// (mappm_cs_column).  C32: buffer loads / stores at 32-bit offsets (DevColBuf / GlobalScrBuf).
+template <int NT, int PF, bool C32>
 __global__ __launch_bounds__(256) void mappm_cs_global_kernel(MappmArgs a)
 {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= a.ncol) return;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    GlobalScr scr{a.scratch + c, stride, (int64_t)(a.km + 3) * stride};
-    DevCol col = make_col(a, c);
-    mappm_cs_column<DevCol, GlobalScr, NT>(col, scr, a.km, a.kn, a.iv, a.kord);
+    if constexpr (C32) {
+        GlobalScrBuf scr{mrsrc(a.scratch), (uint32_t)(c * 4), (uint32_t)(stride * 4),
+                         (uint32_t)((a.km + 3) * stride * 4)};
+        DevColBuf d;
+        d.r_pe1 = mrsrc(a.pe1);
+        d.r_q1 = mrsrc(a.q1);
+        d.o_pe1 = (uint32_t)(col_offset(a.l_pe1, c) * 4);
+        d.o_q1 = (uint32_t)(col_offset(a.l_q1, c) * 4);
+        d.lb_pe1 = (uint32_t)(a.l_pe1.ld * 4);
+        d.lb_q1 = (uint32_t)(a.l_q1.ld * 4);
+        d.pe2_ = a.pe2 + col_offset(a.l_pe2, c);
+        d.q2_ = a.q2 + col_offset(a.l_q2, c);
+        d.ld_pe2 = a.l_pe2.ld;
+        d.ld_q2 = a.l_q2.ld;
+        d.kn = a.kn;
+        d.pe2_next = d.pe2_ + 2 * d.ld_pe2;
+        d.nb = a.kn >= 2 ? *d.pe2_next : 0.0f;
+        mappm_cs_column<DevColBuf, GlobalScrBuf, NT, PF>(d, scr, a.km, a.kn, a.iv, a.kord);
+    } else {
+        GlobalScr scr{a.scratch + c, stride, (int64_t)(a.km + 3) * stride};
+        DevCol col = make_col(a, c);
+        mappm_cs_column<DevCol, GlobalScr, NT, PF>(col, scr, a.km, a.kn, a.iv, a.kord);
+    }
 }
 
 // register-tail depth of the kord > 7 kernel (every depth gives the same bits).  Measured
@@ -304,16 +399,41 @@ __global__ __launch_bounds__(256) void mappm_cs_global_kernel(MappmArgs a)
 // launch needs it more than the scratch bytes saved); at one rank's 110,592 columns,
 // where occupancy is not the limit, 0.232 / 0.223 / 0.218 / 0.212 ms.  So the tail is
 // used on small grids only.  FV3_MAPPM_CS_NT=0|16|32|48 forces a depth (A/B).
-const void* cs_global_kernel(int64_t ncol)
+const void* cs_global_kernel(const MappmArgs& a, int64_t nlanes)
 {
+    const int64_t ncol = a.ncol;
     int nt = ncol < 262144 ? 48 : 0;
     if (const char* e = getenv("FV3_MAPPM_CS_NT")) nt = atoi(e);
-    switch (nt) {
-    case 0: return (const void*)mappm_cs_global_kernel<0>;
-    case 16: return (const void*)mappm_cs_global_kernel<16>;
-    case 32: return (const void*)mappm_cs_global_kernel<32>;
-    default: return (const void*)mappm_cs_global_kernel<48>;
+    // load distance (tools/mappm_pf_ab.py, profiles/r04l_mappm_pf.log; C384 79 -> 79 kord
+    // 10 with buffer operations): 884,736 columns PF = 0 / 2 / 4 / 8 0.909 / 0.761 /
+    // 0.798 / 0.836 ms (64-bit addresses, PF = 0: 0.871); 110,592 columns (register tail)
+    // 0.224 / 0.185 / 0.182 / 0.182 ms
+    int pf = nt ? 4 : 2;
+    if (const char* e = getenv("FV3_MAPPM_CS_PF")) pf = atoi(e);
+    // 32-bit lane byte offsets when every column offset (and the scratch) fits
+    // buffer operations at 32-bit byte offsets when every array (and the scratch) spans
+    // < 4 GiB: the last column's offset plus km levels
+    auto fits = [&](const fv3_layout& l, int nlev) {
+        if (l.ld < 0 || l.blk_stride < 0) return false;
+        const int64_t c = ncol - 1;
+        const int64_t off = (l.ncol_blk <= 0 || c < l.ncol_blk) ? c : (c / l.ncol_blk) * l.blk_stride + c % l.ncol_blk;
+        return 4 * (off + (int64_t)nlev * l.ld) < (1ll << 32) - 4;
+    };
+    bool c32 = fits(a.l_pe1, a.km + 1) && fits(a.l_q1, a.km) && 4 * nlanes * 2 * (int64_t)(a.km + 3) < (1ll << 32) - 4;
+    if (const char* e = getenv("FV3_MAPPM_CS_C32")) c32 = c32 && atoi(e) != 0;
+#define FV3_CS_PF(NT_, C_)                                                        \
+    switch (pf) {                                                                 \
+    case 0: return (const void*)mappm_cs_global_kernel<NT_, 0, C_>;               \
+    case 4: return (const void*)mappm_cs_global_kernel<NT_, 4, C_>;               \
+    case 8: return (const void*)mappm_cs_global_kernel<NT_, 8, C_>;               \
+    default: return (const void*)mappm_cs_global_kernel<NT_, 2, C_>;              \
     }
+    if (c32) {
+        if (nt) { FV3_CS_PF(48, true) } else { FV3_CS_PF(0, true) }
+    }
+    if (nt) { FV3_CS_PF(48, false) }
+    FV3_CS_PF(0, false)
+#undef FV3_CS_PF
 }
 
 }  // namespace
@@ -338,7 +458,7 @@ int launch_mappm(MappmArgs a, hipStream_t stream)
         FV3_HIP(hipMallocAsync((void**)&a.scratch, sizeof(float) * 2 * (size_t)(a.km + 3) * (size_t)grid * block,
                                stream));
         void* kargs[] = {&a};
-        FV3_HIP(hipLaunchKernel(cs_global_kernel(a.ncol), dim3((unsigned)grid), dim3(block), kargs, 0, stream));
+        FV3_HIP(hipLaunchKernel(cs_global_kernel(a, grid * block), dim3((unsigned)grid), dim3(block), kargs, 0, stream));
         FV3_LAUNCH_CHECK();
         FV3_HIP(hipFreeAsync(a.scratch, stream));
         return FV3_OK;

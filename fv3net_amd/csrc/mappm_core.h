@@ -37,6 +37,8 @@
 namespace fv3 {
 
 FV3_HD inline float fmax2(float a, float b) { return a > b ? a : b; }
+FV3_HD inline int imin2(int a, int b) { return a < b ? a : b; }
+FV3_HD inline int imax2(int a, int b) { return a > b ? a : b; }
 FV3_HD inline float fmin2(float a, float b) { return a < b ? a : b; }
 FV3_HD inline float fmax3(float a, float b, float c) { return fmax2(fmax2(a, b), c); }
 FV3_HD inline float fmin3(float a, float b, float c) { return fmin2(fmin2(a, b), c); }
@@ -763,7 +765,16 @@ FV3_HD inline void mappm_ppm_column_by_output(Col& c, int km, int kn, int iv, in
 // register queue.  Same operations in the same order on the same values: the bits are
 // those of the all-scratch path, with 6 NT fewer scratch accesses per column (the
 // scratch round trips are most of kord > 7's HBM traffic).
-template <class Col, class Scr, int NT = 0>
+//
+// PF > 0: the loads run ahead of their use.  The scratch stores of each level may alias
+// the next level's loads as far as the compiler can tell, so as written every level of
+// the forward sweep and of the back-substitution waits out one full memory round trip
+// (load, wait, compute, store).  With PF, the sweep's q1 / pe1 and the
+// back-substitution's edge / gam are loaded PF levels ahead into a register ring (loop
+// unrolled by PF, static ring indices), and the main loop's q1 / edge / pe1 one layer
+// ahead.  Loads only move earlier, past stores to other addresses: the same values, the
+// same bits.
+template <class Col, class Scr, int NT = 0, int PF = 0>
 FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int kord)
 {
     const int akord = kord < 0 ? -kord : kord;
@@ -820,9 +831,8 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
             float pek = pe1v;
             float qkm1 = qm1;
             float qk = qm1;
-            auto sweep = [&](int k, float& e_out, float& g_out) {
-                qk = c.q1(k);
-                const float pen = c.pe1(k + 1);
+            auto sweep_v = [&](float qkv, float pen, auto&& e_out, auto&& g_out) {
+                qk = qkv;
                 const float dpk = pen - pek;
                 d4 = dpm1 / dpk;
                 bet = 2.0f + d4 + d4 - gprev;
@@ -832,8 +842,47 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
                 g_out = gprev;
                 qkm1 = qk; dpm1 = dpk; pek = pen;
             };
+            auto sweep = [&](int k, auto&& e_out, auto&& g_out) { sweep_v(c.q1(k), c.pe1(k + 1), e_out, g_out); };
             const int kend = tail ? kt - 1 : km;
-            for (int k = 2; k <= kend; ++k) sweep(k, scr.e(k), scr.g(k));
+            if constexpr (PF > 0) {
+                // blocks of PF levels in two register sets: block b + 1's loads are issued
+                // when block b starts, so they have a whole block to land.  (The compiler
+                // runs a block's independent divisions ahead, so it waits for the whole
+                // block's loads at its start.)  Two static sets, the loop unrolled by two
+                // blocks: no register copies across the back edge, which would wait for
+                // the loads in flight.  Loads past kend are clamped to km: spare loads.
+                float qa[PF], pa[PF], qb[PF], pb[PF];
+                auto load_blk = [&](float (&q)[PF], float (&p)[PF], int k0) {
+#pragma unroll
+                    for (int j = 0; j < PF; ++j) {
+                        const int kk = imin2(k0 + j, km);
+                        q[j] = c.q1(kk);
+                        p[j] = c.pe1(kk + 1);
+                    }
+                };
+                auto run_blk = [&](const float (&q)[PF], const float (&p)[PF], int k0, int n) {
+#pragma unroll
+                    for (int j = 0; j < PF; ++j)
+                        if (j < n) sweep_v(q[j], p[j], scr.e(k0 + j), scr.g(k0 + j));
+                };
+                load_blk(qa, pa, 2);
+                int k = 2;
+                for (; k + 2 * PF - 1 <= kend; k += 2 * PF) {
+                    load_blk(qb, pb, k + PF);
+                    run_blk(qa, pa, k, PF);
+                    load_blk(qa, pa, k + 2 * PF);
+                    run_blk(qb, pb, k + PF, PF);
+                }
+                if (k + PF - 1 <= kend) {  // one whole block left (qa), then < PF levels (qb)
+                    load_blk(qb, pb, k + PF);
+                    run_blk(qa, pa, k, PF);
+                    run_blk(qb, pb, k + PF, kend - (k + PF) + 1);
+                } else {
+                    run_blk(qa, pa, k, kend - k + 1);
+                }
+            } else {
+                for (int k = 2; k <= kend; ++k) sweep(k, scr.e(k), scr.g(k));
+            }
             if constexpr (NT > 0) {
                 if (tail) {
 #pragma unroll
@@ -857,9 +906,48 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
                 }
             }
             if (!tail) scr.e(km + 1) = qn;
-            for (int k = kb; k >= 1; --k) {
-                qn = scr.e(k) - scr.g(k) * qn;
-                scr.e(k) = qn;
+            if constexpr (PF > 0) {
+                // descending blocks of PF levels in two register sets, as in the sweep;
+                // loads below level 1 are clamped to 1 (spare loads, never used), and a
+                // block's loads precede the stores of the block before it in program order
+                float ea[PF], ga[PF], eb[PF], gb[PF];
+                auto load_blk = [&](float (&e)[PF], float (&g)[PF], int k0) {
+#pragma unroll
+                    for (int j = 0; j < PF; ++j) {
+                        const int kk = imax2(k0 - j, 1);
+                        e[j] = scr.e(kk);
+                        g[j] = scr.g(kk);
+                    }
+                };
+                auto run_blk = [&](const float (&e)[PF], const float (&g)[PF], int k0, int n) {
+#pragma unroll
+                    for (int j = 0; j < PF; ++j) {
+                        if (j < n) {
+                            qn = e[j] - g[j] * qn;
+                            scr.e(k0 - j) = qn;
+                        }
+                    }
+                };
+                load_blk(ea, ga, kb);
+                int k = kb;
+                for (; k - (2 * PF - 1) >= 1; k -= 2 * PF) {
+                    load_blk(eb, gb, k - PF);
+                    run_blk(ea, ga, k, PF);
+                    load_blk(ea, ga, k - 2 * PF);
+                    run_blk(eb, gb, k - PF, PF);
+                }
+                if (k - (PF - 1) >= 1) {
+                    load_blk(eb, gb, k - PF);
+                    run_blk(ea, ga, k, PF);
+                    run_blk(eb, gb, k - PF, k - PF);
+                } else {
+                    run_blk(ea, ga, k, k);
+                }
+            } else {
+                for (int k = kb; k >= 1; --k) {
+                    qn = scr.e(k) - scr.g(k) * qn;
+                    scr.e(k) = qn;
+                }
             }
         }
     }
@@ -882,8 +970,7 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
 
     // constrained edge qc(k) (mappm.f90:207-260) from the solved edge e(k) and
     // q1(k-2..k+1); the large-scale constraints use gam(k) = q1(k) - q1(k-1).
-    auto edge_c = [&](int k, float qkm2, float qkm1, float qk0, float qkp1) -> float {
-        float q = e_at(k);
+    auto edge_cv = [&](int k, float q, float qkm2, float qkm1, float qk0, float qkp1) -> float {
         if (akord > 16 || k <= 1 || k >= km + 1) return q;
         if (k == 2 || k == km) {
             q = fmin2(q, fmax2(qkm1, qk0));
@@ -903,6 +990,9 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
         }
         return q;
     };
+    auto edge_c = [&](int k, float qkm2, float qkm1, float qk0, float qkp1) -> float {
+        return edge_cv(k, e_at(k), qkm2, qkm1, qk0, qkp1);
+    };
     auto q1_or0 = [&](int k) -> float { return (k >= 1 && k <= km) ? c.q1(k) : 0.0f; };
 
     // rolling windows at layer L: qw[i] = q1(L-2+i) (i=0..5), qcw[i] = qc(L-1+i) (i=0..3)
@@ -915,6 +1005,19 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
     float pl0 = c.pe1(1), pl1 = c.pe1(2);
 
     for (int L = 1; L <= km; ++L) {
+        // PF: q1(L + 4), edge(L + 3), pe1(L + 2), which the end of layer L takes into the
+        // windows, are loaded at its start (ahead of the layer's stores, so the compiler
+        // keeps them there): the layer's arithmetic covers their latency.  Locals, not
+        // loop-carried registers: a register copy at the loop's back edge would wait for
+        // a load in flight.
+        float nq = 0.0f, ne = 0.0f, np = 0.0f;
+        if constexpr (PF > 0) {
+            if (L < km) {
+                nq = q1_or0(L + 4);
+                if (L + 3 <= km + 1) ne = e_at(L + 3);
+                np = c.pe1(L + 2);
+            }
+        }
         Ppm a{qw[2], qcw[1], qcw[2], 0.0f};
         if (akord > 16) {
             a.a6 = a6_of(a);  // perfectly linear scheme (mappm.f90:207-216)
@@ -1035,11 +1138,17 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
         remap_layer_fast(s, v, ends, kn, c);
         if (L == km) break;
         for (int i = 0; i < 5; ++i) qw[i] = qw[i + 1];
-        qw[5] = q1_or0(L + 4);
         for (int i = 0; i < 3; ++i) qcw[i] = qcw[i + 1];
-        qcw[3] = (L + 3 <= km + 1) ? edge_c(L + 3, qw[2], qw[3], qw[4], qw[5]) : 0.0f;
         pl0 = pl1;
-        pl1 = c.pe1(L + 2);
+        if constexpr (PF > 0) {
+            qw[5] = nq;
+            qcw[3] = (L + 3 <= km + 1) ? edge_cv(L + 3, ne, qw[2], qw[3], qw[4], qw[5]) : 0.0f;
+            pl1 = np;
+        } else {
+            qw[5] = q1_or0(L + 4);
+            qcw[3] = (L + 3 <= km + 1) ? edge_c(L + 3, qw[2], qw[3], qw[4], qw[5]) : 0.0f;
+            pl1 = c.pe1(L + 2);
+        }
     }
     remap_finish(s, ends, kn, c);
 }

@@ -182,6 +182,35 @@ __global__ __launch_bounds__(64) void level_sums_stage2(const double* __restrict
     if (threadIdx.x == 0) out[k] = s;
 }
 
+// uint8 counts of one band, one block per level: 16-byte loads, each summed by four
+// v_sad_u8 (|b - 0| summed over the word's bytes, exact), then the block's integer sum
+// (exact in any order) written as a double.  Rows 16-byte aligned (host check).
+__global__ __launch_bounds__(kSumBlock) void level_counts_u8_vec(const unsigned char* __restrict__ x, int64_t ld,
+                                                                 int64_t ncol, double* __restrict__ out)
+{
+    __shared__ double sh[kSumBlock / 64];
+    const int k = blockIdx.y;
+    const unsigned char* row = x + (int64_t)k * ld;
+    const int64_t nv = ncol / 16;
+    unsigned s = 0;
+    for (int64_t i = threadIdx.x; i < nv; i += kSumBlock) {
+        const uint4 w = reinterpret_cast<const uint4*>(row)[i];
+        s = __builtin_amdgcn_sad_u8(w.x, 0u, s);
+        s = __builtin_amdgcn_sad_u8(w.y, 0u, s);
+        s = __builtin_amdgcn_sad_u8(w.z, 0u, s);
+        s = __builtin_amdgcn_sad_u8(w.w, 0u, s);
+    }
+    for (int64_t c = nv * 16 + threadIdx.x; c < ncol; c += kSumBlock) s += row[c];
+    const double w = wave_sum((double)s);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = w;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = sh[0];
+        for (int v = 1; v < kSumBlock / 64; ++v) t += sh[v];
+        out[k] = t;
+    }
+}
+
 }  // namespace
 }  // namespace fv3
 
@@ -205,6 +234,15 @@ int level_sums_impl(const T* x, fv3_layout x_l, int64_t ncol, int nz, double* ou
     const int nslice = (int)std::min<int64_t>(kLevelMaxSlices, (ncol + per - 1) / per);
     const int64_t slice = (ncol + nslice - 1) / nslice;
     if (nslice == 1) {  // stage 2 of one partial is the identity: skip it and its scratch
+        if constexpr (std::is_same<T, unsigned char>::value) {
+            // integer counts: 16-byte loads when every row is 16-byte aligned
+            if ((x_l.ncol_blk <= 0 || x_l.ncol_blk >= ncol) && ((uintptr_t)x % 16) == 0 && (x_l.ld % 16) == 0 &&
+                x_l.ld >= 0 && ncol <= (int64_t)1 << 24) {
+                hipLaunchKernelGGL(level_counts_u8_vec, dim3(1, nz), dim3(kSumBlock), 0, s, x, x_l.ld, ncol, out);
+                FV3_LAUNCH_CHECK();
+                return FV3_OK;
+            }
+        }
         hipLaunchKernelGGL(level_sums_stage1<T>, dim3(1, nz), dim3(kSumBlock), 0, s, x, x_l, ncol, slice, out);
         FV3_LAUNCH_CHECK();
         return FV3_OK;

@@ -12,7 +12,9 @@
 //   fillna_tendency + filled fraction                       loop.py:103-110
 //   add_tendency: T += dQ1 dt, q += dQ2 dt                   loop.py:202-219
 //   precipitation_sum                                        diagnostics/compute.py:21-39
-// One thread per column walking the levels in order (coalesced [level][column] rows).
+// Level-parallel (a thread per (column, level set), the column sums added in level order
+// by one thread per (sum, column) from LDS), or one thread per column walking the levels
+// in order where the levels are too many for the LDS.
 // The arithmetic replays the reference's dtype flow: f32 model tendencies combined
 // with Python-float constants stay f32, anything mixed with the state is in the
 // state's dtype DT, column sums run over z in order from +0.0 skipping NaN (xarray's
@@ -53,23 +55,102 @@ struct EpilogueArgs {
 template <typename DT>
 __device__ __forceinline__ DT nan0(DT x) { return x != x ? DT(0) : x; }
 
+// One level of one column: the limiter, the limited / filled tendencies and the updated
+// state written, and the level's terms of the four column sums returned (each already
+// nan0'd: the sums add them in level order from +0.0).
+template <typename DT>
+struct EpiLevel {
+    DT h, m, nm, ch;  // mass_integrate terms: heating change, moistening change, net moistening, column heating
+    bool nan1, nan2;
+};
+
+template <typename DT>
+__device__ __forceinline__ EpiLevel<DT> epi_level(const EpilogueArgs<DT>& a, int64_t i, float q1, float q2, DT sp,
+                                                  DT dp, DT t)
+{
+    const float dtf = (float)a.dt;  // f32 array * Python float -> f32
+    const DT dtd = (DT)a.dt;
+    const float cvf = (float)(kCp - kRdgas), lvf = (float)kLv;
+    const DT cv = (DT)(kCp - kRdgas), lv = (DT)kLv, g = (DT)kGravity;
+    DT q1n, q2n;
+    if (a.mse) {
+        // update_moisture_tendency_to_ensure_non_negative_humidity (machine_learning.py:77-80)
+        const float d = q2 * dtf;
+        q2n = (sp + (DT)d >= (DT)0) ? (DT)q2 : (-sp) / dtd;
+        // update_temperature_tendency_to_conserve_mse (:83-88)
+        const float m = cvf * q1 + lvf * q2;
+        q1n = ((DT)m - lv * q2n) / cv;
+    } else {
+        // non_negative_sphum (:67-74)
+        const float delta = q2 * dtf;
+        const DT ratio = (-sp) / (DT)(dtf * q2);
+        const bool keep = sp + (DT)delta >= (DT)0;
+        q1n = keep ? (DT)q1 : ratio * (DT)q1;
+        q2n = keep ? (DT)q2 : ratio * (DT)q2;
+    }
+    EpiLevel<DT> r;
+    // mass_integrate terms: (x * delp) / g, NaN-skipping sum from +0.0
+    r.h = nan0((q1n - (DT)q1) * dp / g);
+    r.m = nan0((q2n - (DT)q2) * dp / g);
+    // compute_diagnostics reads the tendency dict: zeros for a tendency the model lacks
+    r.nm = nan0(q2n * dp / g);
+    r.ch = nan0(q1n * dp / g);
+    if (a.dq1_out) {
+        a.dq1_out[i] = q1n;
+        a.dq2_out[i] = q2n;
+    }
+    if (a.active) a.active[i] = ((DT)q2 != q2n) ? 1 : 0;
+    // fillna_tendency + add_tendency
+    // (only the tendencies the model predicts are applied, loop.py:202-219)
+    r.nan1 = q1n != q1n;
+    r.nan2 = q2n != q2n;
+    if (a.temp_out) a.temp_out[i] = a.has_dq1 ? t + (r.nan1 ? (DT)0 : q1n) * dtd : t;
+    if (a.sphum_out) a.sphum_out[i] = a.has_dq2 ? sp + (r.nan2 ? (DT)0 : q2n) * dtd : sp;
+    return r;
+}
+
+// the column diagnostics from the four sums and the filled-level counts
+template <typename DT>
+__device__ __forceinline__ void epi_column_out(const EpilogueArgs<DT>& a, int64_t c, int s, DT sum, int n)
+{
+    const DT cv = (DT)(kCp - kRdgas);
+    const DT ch = a.hydrostatic ? (DT)kCp : cv;
+    DT* o = a.col + c;
+    switch (s) {
+    case 0:
+        o[0 * a.col_ld] = ch * sum;                    // column_integrated_dQ1_change_non_neg_sphum_constraint
+        o[4 * a.col_ld] = (DT)((double)n / a.nz);      // dQ1_filled_frac
+        break;
+    case 1:
+        o[1 * a.col_ld] = sum;                         // column_integrated_dQ2_change_non_neg_sphum_constraint
+        o[5 * a.col_ld] = (DT)((double)n / a.nz);      // dQ2_filled_frac
+        break;
+    case 2:
+        o[2 * a.col_ld] = sum;                         // net_moistening_due_to_<label>
+        if (a.precip) {
+            const DT total = a.precip[c] + ((-sum) * (DT)a.dt) * (DT)(1.0 / 1000);
+            o[6 * a.col_ld] = total >= (DT)0 ? total : (DT)0;  // total_precipitation
+        }
+        break;
+    default:
+        o[3 * a.col_ld] = ch * sum;                    // column_heating_due_to_<label>
+    }
+}
+
+// One thread per column walking the levels in order: the kernel for levels too many for
+// the level-parallel kernel's LDS (FV3_EPILOGUE_PATH=columns forces it).
 template <typename DT>
 __global__ __launch_bounds__(64) void ml_epilogue_kernel(EpilogueArgs<DT> a)
 {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= a.ncol) return;
     const int64_t off = col_offset(a.lay, c);
-    const float dtf = (float)a.dt;        // f32 array * Python float -> f32
-    const DT dtd = (DT)a.dt;
-    const float cvf = (float)(kCp - kRdgas), lvf = (float)kLv;
-    const DT cv = (DT)(kCp - kRdgas), lv = (DT)kLv, g = (DT)kGravity;
     DT s_h = 0, s_m = 0, s_nm = 0, s_ch = 0;
     int n1 = 0, n2 = 0;
     // Levels are fetched in batches of U, the next batch issued before the current one
-    // is processed: with at most one wave per SIMD (C96 = 864 waves) the loads in
-    // flight per thread set the HBM rate.  The explicit batches also keep the loads
-    // ahead of the stores, which the compiler may not reorder itself since temp_out /
-    // sphum_out may alias temp / sphum.  The z sums stay in level order.
+    // is processed.  The explicit batches also keep the loads ahead of the stores, which
+    // the compiler may not reorder itself since temp_out / sphum_out may alias temp /
+    // sphum.  The z sums stay in level order.
     constexpr int U = 8;
     float b_q1[2][U], b_q2[2][U];
     DT b_sp[2][U], b_dp[2][U], b_t[2][U];
@@ -87,41 +168,13 @@ __global__ __launch_bounds__(64) void ml_epilogue_kernel(EpilogueArgs<DT> a)
         }
     };
     auto level = [&](int k, float q1, float q2, DT sp, DT dp, DT t) {
-        const int64_t i = off + (int64_t)k * a.lay.ld;
-        DT q1n, q2n;
-        if (a.mse) {
-            // update_moisture_tendency_to_ensure_non_negative_humidity (machine_learning.py:77-80)
-            const float d = q2 * dtf;
-            q2n = (sp + (DT)d >= (DT)0) ? (DT)q2 : (-sp) / dtd;
-            // update_temperature_tendency_to_conserve_mse (:83-88)
-            const float m = cvf * q1 + lvf * q2;
-            q1n = ((DT)m - lv * q2n) / cv;
-        } else {
-            // non_negative_sphum (:67-74)
-            const float delta = q2 * dtf;
-            const DT ratio = (-sp) / (DT)(dtf * q2);
-            const bool keep = sp + (DT)delta >= (DT)0;
-            q1n = keep ? (DT)q1 : ratio * (DT)q1;
-            q2n = keep ? (DT)q2 : ratio * (DT)q2;
-        }
-        // mass_integrate terms: (x * delp) / g, NaN-skipping sum from +0.0
-        s_h = s_h + nan0((q1n - (DT)q1) * dp / g);
-        s_m = s_m + nan0((q2n - (DT)q2) * dp / g);
-        // compute_diagnostics reads the tendency dict: zeros for a tendency the model lacks
-        if (a.has_dq2) s_nm = s_nm + nan0(q2n * dp / g);
-        if (a.has_dq1) s_ch = s_ch + nan0(q1n * dp / g);
-        if (a.dq1_out) {
-            a.dq1_out[i] = q1n;
-            a.dq2_out[i] = q2n;
-        }
-        if (a.active) a.active[i] = ((DT)q2 != q2n) ? 1 : 0;
-        // fillna_tendency + add_tendency
-        // (only the tendencies the model predicts are applied, loop.py:202-219)
-        const bool nan1 = q1n != q1n, nan2 = q2n != q2n;
-        n1 += nan1;
-        n2 += nan2;
-        if (want_t) a.temp_out[i] = a.has_dq1 ? t + (nan1 ? (DT)0 : q1n) * dtd : t;
-        if (a.sphum_out) a.sphum_out[i] = a.has_dq2 ? sp + (nan2 ? (DT)0 : q2n) * dtd : sp;
+        const EpiLevel<DT> r = epi_level(a, off + (int64_t)k * a.lay.ld, q1, q2, sp, dp, t);
+        s_h = s_h + r.h;
+        s_m = s_m + r.m;
+        if (a.has_dq2) s_nm = s_nm + r.nm;
+        if (a.has_dq1) s_ch = s_ch + r.ch;
+        n1 += r.nan1;
+        n2 += r.nan2;
     };
     fetch(0, 0);
     for (int k0 = 0; k0 < a.nz; k0 += 2 * U) {
@@ -137,20 +190,83 @@ __global__ __launch_bounds__(64) void ml_epilogue_kernel(EpilogueArgs<DT> a)
                 level(k0 + U + u, b_q1[1][u], b_q2[1][u], b_sp[1][u], b_dp[1][u], b_t[1][u]);
     }
     if (a.col) {
-        const DT ch = a.hydrostatic ? (DT)kCp : cv;
-        DT* o = a.col + c;
-        o[0 * a.col_ld] = ch * s_h;  // column_integrated_dQ1_change_non_neg_sphum_constraint
-        o[1 * a.col_ld] = s_m;       // column_integrated_dQ2_change_non_neg_sphum_constraint
-        o[2 * a.col_ld] = s_nm;      // net_moistening_due_to_<label>
-        o[3 * a.col_ld] = ch * s_ch; // column_heating_due_to_<label>
-        o[4 * a.col_ld] = (DT)((double)n1 / a.nz);  // dQ1_filled_frac
-        o[5 * a.col_ld] = (DT)((double)n2 / a.nz);  // dQ2_filled_frac
-        if (a.precip) {
-            const DT total = a.precip[c] + ((-s_nm) * dtd) * (DT)(1.0 / 1000);
-            o[6 * a.col_ld] = total >= (DT)0 ? total : (DT)0;  // total_precipitation
-        }
+        epi_column_out(a, c, 0, s_h, n1);
+        epi_column_out(a, c, 1, s_m, n2);
+        epi_column_out(a, c, 2, s_nm, 0);
+        epi_column_out(a, c, 3, s_ch, 0);
     }
 }
+
+// Level-parallel: a block of kEpiCols columns x kEpiLanes level lanes.  Each thread runs
+// the levels lane, lane + kEpiLanes, ... of its column (every level's work is
+// independent) and leaves the four sum terms in LDS; then one thread per (sum, column)
+// adds its column's terms in level order from +0.0, the same additions as the column
+// kernel.  One rank's 6,912 columns are 108 waves in the column kernel (one per CU, a
+// serial 79-level chain each: 44 us); here 1,728.
+constexpr int kEpiCols = 16, kEpiLanes = 16, kEpiU = 3;
+template <typename DT>
+__global__ __launch_bounds__(kEpiCols * kEpiLanes) void ml_epilogue_levels_kernel(EpilogueArgs<DT> a)
+{
+    extern __shared__ __align__(16) unsigned char epi_smem[];
+    DT* terms = reinterpret_cast<DT*>(epi_smem);                    // [4][nz][kEpiCols]
+    int* cnt = reinterpret_cast<int*>(terms + 4 * a.nz * kEpiCols);  // [2][kEpiCols]
+    const int cl = threadIdx.x % kEpiCols, lane = threadIdx.x / kEpiCols;
+    const int64_t c = (int64_t)blockIdx.x * kEpiCols + cl;
+    if (threadIdx.x < 2 * kEpiCols) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    if (c < a.ncol) {
+        const int64_t off = col_offset(a.lay, c);
+        const bool want_t = a.temp_out != nullptr;
+        int n1 = 0, n2 = 0;
+        // kEpiU levels' loads issued before any of their stores (temp_out / sphum_out may
+        // alias temp / sphum, so the compiler keeps loads behind earlier stores)
+        for (int k0 = lane; k0 < a.nz; k0 += kEpiU * kEpiLanes) {
+            float q1[kEpiU], q2[kEpiU];
+            DT sp[kEpiU], dp[kEpiU], t[kEpiU];
+#pragma unroll
+            for (int u = 0; u < kEpiU; ++u) {
+                int k = k0 + u * kEpiLanes;
+                k = k < a.nz ? k : a.nz - 1;  // clamped: re-reads a level, never used
+                const int64_t i = off + (int64_t)k * a.lay.ld;
+                q1[u] = a.dq1[i];
+                q2[u] = a.dq2[i];
+                sp[u] = a.sphum[i];
+                dp[u] = a.delp[i];
+                t[u] = want_t ? a.temp[i] : (DT)0;
+            }
+#pragma unroll
+            for (int u = 0; u < kEpiU; ++u) {
+                const int k = k0 + u * kEpiLanes;
+                if (k < a.nz) {
+                    const EpiLevel<DT> r = epi_level(a, off + (int64_t)k * a.lay.ld, q1[u], q2[u], sp[u], dp[u], t[u]);
+                    terms[(0 * a.nz + k) * kEpiCols + cl] = r.h;
+                    terms[(1 * a.nz + k) * kEpiCols + cl] = r.m;
+                    terms[(2 * a.nz + k) * kEpiCols + cl] = r.nm;
+                    terms[(3 * a.nz + k) * kEpiCols + cl] = r.ch;
+                    n1 += r.nan1;
+                    n2 += r.nan2;
+                }
+            }
+        }
+        if (n1) atomicAdd(&cnt[cl], n1);
+        if (n2) atomicAdd(&cnt[kEpiCols + cl], n2);
+    }
+    __syncthreads();
+    if (a.col && threadIdx.x < 4 * kEpiCols && c < a.ncol) {
+        const int s = lane;  // 0..3: which sum
+        const bool on = s < 2 || (s == 2 ? a.has_dq2 : a.has_dq1);
+        DT sum = 0;
+        if (on) {
+            const DT* tp = terms + (int64_t)s * a.nz * kEpiCols + cl;
+            for (int k = 0; k < a.nz; ++k) sum = sum + tp[k * kEpiCols];
+        }
+        epi_column_out(a, c, s, sum, s < 2 ? cnt[s * kEpiCols + cl] : 0);
+    }
+}
+
+constexpr size_t kEpiMaxSmem = 48 << 10;  // f64 state: nz <= 95
+constexpr int64_t kEpiLevelsMaxCols = 32768;
+size_t epi_levels_smem(int nz, size_t dt_size) { return 4 * (size_t)nz * kEpiCols * dt_size + 2 * kEpiCols * sizeof(int); }
 
 template <typename DT>
 int epilogue_impl(const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, int nz, double dt, int mse_conserving,
@@ -186,9 +302,24 @@ int epilogue_impl(const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, int n
     a.has_dq1 = (flags & FV3_EPI_HAS_DQ1) != 0;
     a.has_dq2 = (flags & FV3_EPI_HAS_DQ2) != 0;
     a.dt = dt;
-    const int block = 64;  // one wave: C96's 864 waves spread over every CU (256-thread blocks left 40 idle)
-    const int64_t grid = (ncol + block - 1) / block;
-    hipLaunchKernelGGL(ml_epilogue_kernel<DT>, dim3((unsigned)grid), dim3(block), 0, (hipStream_t)stream, a);
+    // level-parallel on small grids (one rank's share of C96 over 8, 6,912 columns: step
+    // 0.092 -> 0.061 ms), the column kernel on large ones (full C96, 55,296 columns:
+    // 0.2065 vs 0.2080 ms) (tools/epi_ab.py, profiles/r04j_epi_ab.log);
+    // FV3_EPILOGUE_PATH=levels|columns forces one
+    const size_t smem = epi_levels_smem(nz, sizeof(DT));
+    const char* path = getenv("FV3_EPILOGUE_PATH");
+    bool levels = ncol <= kEpiLevelsMaxCols;
+    if (path && path[0] == 'c') levels = false;
+    if (path && path[0] == 'l') levels = true;
+    if (levels && smem <= kEpiMaxSmem) {
+        const int64_t grid = (ncol + kEpiCols - 1) / kEpiCols;
+        hipLaunchKernelGGL(ml_epilogue_levels_kernel<DT>, dim3((unsigned)grid), dim3(kEpiCols * kEpiLanes), smem,
+                           (hipStream_t)stream, a);
+    } else {
+        const int block = 64;  // one wave: C96's 864 waves spread over every CU (256-thread blocks left 40 idle)
+        const int64_t grid = (ncol + block - 1) / block;
+        hipLaunchKernelGGL(ml_epilogue_kernel<DT>, dim3((unsigned)grid), dim3(block), 0, (hipStream_t)stream, a);
+    }
     FV3_LAUNCH_CHECK();
     return FV3_OK;
 }

@@ -59,6 +59,31 @@ extern "C" int host_mappm_cs_tail(int km, const float* pe1, const float* q1, int
     return 0;
 }
 
+// kord > 7 with the loads run `pf` levels ahead (mappm_cs_column<..., NT, PF>) and the
+// bottom `nt` edges in registers, as the device kernel runs it
+template <int NT>
+static int cs_pf(Col& c, Scr& scr, int km, int kn, int iv, int kord, int pf)
+{
+    switch (pf) {
+    case 2: fv3::mappm_cs_column<Col, Scr, NT, 2>(c, scr, km, kn, iv, kord); return 0;
+    case 4: fv3::mappm_cs_column<Col, Scr, NT, 4>(c, scr, km, kn, iv, kord); return 0;
+    case 8: fv3::mappm_cs_column<Col, Scr, NT, 8>(c, scr, km, kn, iv, kord); return 0;
+    default: return -1;
+    }
+}
+extern "C" int host_mappm_cs_prefetch(int km, const float* pe1, const float* q1, int kn, const float* pe2,
+                                      float* q2, int64_t ncol, int iv, int kord, int nt, int pf)
+{
+    if (km < 4 || kn < 1 || kord <= 7) return -1;
+    Scr scr{std::vector<float>(km + 3), std::vector<float>(km + 3)};
+    for (int64_t i = 0; i < ncol; ++i) {
+        Col c{pe1, q1, pe2, q2, ncol, i, kn};
+        const int st = nt == 0 ? cs_pf<0>(c, scr, km, kn, iv, kord, pf) : cs_pf<16>(c, scr, km, kn, iv, kord, pf);
+        if (st) return st;
+    }
+    return 0;
+}
+
 // same through the output-driven cursor (kord <= 7), as the fused coarsen kernel uses it
 extern "C" int host_mappm_cursor(int km, const float* pe1, const float* q1, int kn, const float* pe2,
                                  float* q2, int64_t ncol, int iv, int kord)

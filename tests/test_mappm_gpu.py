@@ -104,6 +104,29 @@ def test_cs_lds_path_vs_oracle_bit_exact(gpu, km, kn, ncol, monkeypatch):
             assert _bits_equal(res, oracle_mappm(pe1, q, pe2, iv, kord)), (kord, iv)
 
 
+@pytest.mark.parametrize("nt,pf,c32", [(0, 0, 0), (0, 2, 0), (0, 0, 1), (0, 2, 1), (0, 4, 1), (0, 8, 1), (48, 0, 1),
+                                        (48, 8, 1), (48, 4, 0)])
+def test_cs_kernel_variants_vs_oracle_bit_exact(gpu, nt, pf, c32, monkeypatch, mappm_path):
+    """Every build of the global-scratch kord > 7 kernel: register tail depth NT, load
+    distance PF (two register sets of PF levels in the solve), buffer operations at 32-bit
+    offsets or 64-bit addresses: the same bits as the oracle, on level counts around the
+    blocks' remainders."""
+    from fv3net_amd.mappm import mappm_device
+
+    if mappm_path != "serial":
+        pytest.skip("kord > 7 has one kernel family; run once")
+    monkeypatch.setenv("FV3_MAPPM_CS_NT", str(nt))
+    monkeypatch.setenv("FV3_MAPPM_CS_PF", str(pf))
+    monkeypatch.setenv("FV3_MAPPM_CS_C32", str(c32))
+    for km, kn, ncol in ((5, 9, 257), (17, 12, 333), (50, 60, 300), (79, 79, 777), (127, 40, 300)):
+        rng = np.random.default_rng(km * 31 + kn + ncol + pf)
+        pe1, q, pe2 = _columns(rng, km, kn, ncol)
+        for kord in (8, 9, 10, 11, 12, 13, 14, 15, 16, 17):
+            for iv in (0, 1, -1, 2):
+                res = mappm_device(pe1, q, pe2, iv, kord).cpu().numpy()
+                assert _bits_equal(res, oracle_mappm(pe1, q, pe2, iv, kord)), (km, kn, kord, iv)
+
+
 def test_c384_scale_kord10_sampled_bit_exact(gpu):
     """config #3's kord 10 leg at its C384 size (884,736 columns, 79->79) through the
     default (global-scratch) kernel: the first / last wave and 4,096 sampled columns

@@ -93,6 +93,10 @@ def host_lib():
         fn.restype = ctypes.c_int
         fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                        ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
+    lib.host_mappm_cs_prefetch.restype = ctypes.c_int
+    lib.host_mappm_cs_prefetch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_int]
     lib.host_mappm_cs_tail.restype = ctypes.c_int
     lib.host_mappm_cs_tail.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int]
@@ -270,7 +274,8 @@ def test_multi_field_streaming_bit_identical(host_lib, nf, km, kn):
                     assert _bits_equal(out[f], _host(host_lib, pe1, q[f], pe2, iv, kord)), (nf, f, kord, iv)
 
 
-@pytest.mark.parametrize("km,kn", [(8, 5), (9, 9), (17, 12), (33, 40), (79, 79), (79, 50), (127, 40)])
+@pytest.mark.parametrize("km,kn", [(4, 4), (5, 3), (6, 9), (7, 7), (8, 5), (9, 9), (17, 12), (33, 40), (79, 79),
+                                   (79, 50), (127, 40)])
 def test_cs_register_tail_is_bit_identical(host_lib, km, kn):
     """kord > 7 with the bottom NT edges of the tridiagonal solve held in registers (the
     device kernel's mappm_cs_column<.., NT>) gives the all-scratch column's bits, for every
@@ -294,3 +299,9 @@ def test_cs_register_tail_is_bit_identical(host_lib, km, kn):
                 assert host_lib.host_mappm_cs_tail(km, pe1.ctypes.data, q.ctypes.data, kn, pe2.ctypes.data,
                                                    out.ctypes.data, ncol, iv, kord, nt) == 0
                 assert _bits_equal(out, ref), (kord, iv, nt)
+            # the loads run ahead (mappm_cs_column<.., NT, PF>): same bits
+            for nt, pf in ((0, 2), (0, 4), (0, 8), (16, 4)):
+                out = np.empty((kn, ncol), np.float32)
+                assert host_lib.host_mappm_cs_prefetch(km, pe1.ctypes.data, q.ctypes.data, kn, pe2.ctypes.data,
+                                                       out.ctypes.data, ncol, iv, kord, nt, pf) == 0
+                assert _bits_equal(out, ref), (kord, iv, nt, pf)

@@ -128,3 +128,23 @@ def test_level_sums_keep_dtype(gpu):
     flag = (rng.uniform(size=(79, 24, 24)) < 0.3).astype(np.uint8)
     got = D.level_sums(torch.from_numpy(flag).cuda()).cpu().numpy()
     np.testing.assert_array_equal(got, flag.sum(axis=(1, 2)).astype(np.float64))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ncol", [1, 15, 16, 17, 255, 6912, 6913, 32768, 40000, 100000])
+def test_level_sums_u8_counts_exact(gpu, ncol):
+    """uint8 level sums: one band in one launch (16-byte loads summed by v_sad_u8 when the
+    rows are 16-byte aligned, the scalar kernel on a misaligned view), several slices past
+    32,768 columns; arbitrary byte values, not only 0/1 flags: exact integers."""
+    import torch
+
+    from fv3net_amd import distributed as D
+
+    rng = np.random.default_rng(ncol)
+    v = rng.integers(0, 256, size=(9, ncol), dtype=np.uint8)
+    t = torch.from_numpy(v).cuda()
+    got = D.level_sums(t).cpu().numpy()
+    np.testing.assert_array_equal(got, v.sum(axis=1, dtype=np.int64).astype(np.float64))
+    if ncol > 1:  # a view starting one byte in: rows not 16-byte aligned
+        got = D.level_sums(t[:, 1:]).cpu().numpy()
+        np.testing.assert_array_equal(got, v[:, 1:].sum(axis=1, dtype=np.int64).astype(np.float64))

@@ -47,8 +47,12 @@ def _bits(a, b):
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("mse", [True, False])
 @pytest.mark.parametrize("hydrostatic", [False, True])
-def test_epilogue_bit_identical_to_oracle(gpu, dtype, mse, hydrostatic):
+@pytest.mark.parametrize("path", ["levels", "columns"])
+def test_epilogue_bit_identical_to_oracle(gpu, dtype, mse, hydrostatic, path, monkeypatch):
+    """Both epilogue kernels: level-parallel (the default) and one thread per column."""
     import torch
+
+    monkeypatch.setenv("FV3_EPILOGUE_PATH", path)
 
     from fv3net_amd.stepper import ml_epilogue
 
@@ -68,11 +72,16 @@ def test_epilogue_bit_identical_to_oracle(gpu, dtype, mse, hydrostatic):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nz", [1, 3, 8, 9, 16, 17, 24, 33])
-def test_epilogue_level_batches(gpu, nz):
-    """The kernel fetches levels in double-buffered batches of 8: every remainder of nz
-    (fewer levels than one batch, exact multiples, one past) stays bit-identical."""
+@pytest.mark.parametrize("nz", [1, 3, 8, 9, 16, 17, 24, 33, 47, 48, 49, 79, 95, 96, 130])
+@pytest.mark.parametrize("path", ["levels", "columns"])
+def test_epilogue_level_batches(gpu, nz, path, monkeypatch):
+    """The column kernel fetches levels in double-buffered batches of 8, the level-parallel
+    one in batches of 3 per level lane of 16 (and hands nz > 95 to the column kernel):
+    every remainder of nz (fewer levels than one batch, exact multiples, one past) stays
+    bit-identical, on 130 columns (a partial block of 16)."""
     import torch
+
+    monkeypatch.setenv("FV3_EPILOGUE_PATH", path)
 
     from fv3net_amd.stepper import ml_epilogue
 
