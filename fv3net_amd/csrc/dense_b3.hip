@@ -131,6 +131,7 @@ struct B3Args {
     int64_t out_ld[kMaxVars], out_bs[kMaxVars];
     const float* res_ptr[kMaxVars];
     int64_t res_ld[kMaxVars], res_bs[kMaxVars];
+    int ovec;  // TR: every output / residual row 16-byte aligned (16-byte accesses)
     // profiling hook (fv3_dense_set_trace), NULL normally: per tile [8] int64 =
     // wall clock (100 MHz) at tile start / layer 1 done / hidden done / tile end, CU id,
     // shader clock at tile start / end, shader cycles wave 0 spent in the chunk waits
@@ -155,6 +156,7 @@ struct B3Grp {
 };
 static_assert(sizeof(B3Grp) == 32, "B3Grp is read as two 16-byte words");
 typedef __amdgpu_buffer_rsrc_t Rsrc3;
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 template <typename F, int... I>
 __device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, I...>)
@@ -230,6 +232,26 @@ __device__ __forceinline__ void mma_x2(const bf16x8 (&a0)[NS], const bf16x8 (&b0
 #else
         c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[T::a[t]], b0[T::b[t]], c0, 0, 0, 0);
         c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[T::a[t]], b1[T::b[t]], c1, 0, 0, 0);
+#endif
+    }
+}
+
+// mma_x2 with the operands' roles swapped: the same registers, the same split products
+// (SplitTerms is symmetric in a and b), D^T in the accumulator layout: lane l holds
+// columns 4 (l >> 4) .. + 3 of row l & 15 (the transposed output layer, TR below)
+template <int NS>
+__device__ __forceinline__ void mma_x2t(const bf16x8 (&a0)[NS], const bf16x8 (&b0)[NS], b3f4& c0,
+                                        const bf16x8 (&a1)[NS], const bf16x8 (&b1)[NS], b3f4& c1)
+{
+    using T = SplitTerms<NS>;
+#pragma unroll
+    for (int t = 0; t < T::n; ++t) {
+#ifdef FV3_B3_EXP_NOMFMA  // experiment only (results invalid): everything but the MFMAs
+        c0[0] += (float)a0[T::a[t]][t] + (float)b0[T::b[t]][t];
+        c1[0] += (float)a1[T::a[t]][t] + (float)b1[T::b[t]][t];
+#else
+        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[T::b[t]], a0[T::a[t]], c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[T::b[t]], a1[T::a[t]], c1, 0, 0, 0);
 #endif
     }
 }
@@ -341,7 +363,12 @@ __device__ __forceinline__ void b3_glds(const void* g, const void* lds)
 // NS: bf16 parts per f32 operand (2: bf16x3, 3: bf16x6, see SplitTerms)
 // NWV: waves per block (8; 4 on grids with fewer 128-column tiles than CUs, so every
 // CU gets a tile and each SIMD runs one 16-column wave)
-template <int HU, int SL, int NS, int NWV>
+// TR: the transposed output layer (operands swapped, mma_x2t): each lane holds 4
+// consecutive columns of one output row, so the epilogue reads its constants once per
+// row and moves a lane's residuals and results in one 16-byte load / store (p.ovec:
+// every output / residual row 16-byte aligned; else 4 dword accesses).  The host picks
+// TR when 4-column groups never cross a column block.
+template <int HU, int SL, int NS, int NWV, bool TR = false>
 __global__ __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(NWV == 4 ? 1 : 2, NWV == 4 ? 1 : 2))) void
 dense_b3_kernel(B3Args pa)
 {
@@ -624,7 +651,10 @@ dense_b3_kernel(B3Args pa)
                 frag(slot, i1 + kFR - 2, fa[(i1 + kFR - 2) % kFR]);
             }
             b3_sched_pair();
-            mma_x2<NS>(fa[i0 % kFR], B[q], acc[0], fa[i1 % kFR], B[q], acc[1]);
+            if constexpr (TR)
+                mma_x2t<NS>(fa[i0 % kFR], B[q], acc[0], fa[i1 % kFR], B[q], acc[1]);
+            else
+                mma_x2<NS>(fa[i0 % kFR], B[q], acc[0], fa[i1 % kFR], B[q], acc[1]);
             b3_sched_groups<(i0 + kFR - 2 < HU) ? 2 * NS : 0, 2 * SplitTerms<NS>::n>();
             b3_sched_pair();
         });
@@ -639,7 +669,77 @@ dense_b3_kernel(B3Args pa)
     // after = before + to) are loaded one chunk ahead of their use.
     unsigned oblk = 0, oii = 0;
     bool ovalid = false;
+    // TR: this lane's 4-column group (columns 4 hq .. + 3 of the wave's 16): block, index
+    // of its first column, valid columns (0..4)
+    unsigned o4blk = 0, o4ii = 0;
+    int o4n = 0;
+    auto res_load_tr = [&](int T, float (&r)[4]) -> int {  // a lower bound of the loads issued
+        const int e = p.otile[T];
+        const int v = e & 0xff, z0 = (e >> 8) & 0xffff, nrow = e >> 24;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) r[q] = 0.0f;
+        if (!(v < kMaxVars && p.res_ptr[v])) return 0;  // uniform
+        const Rsrc3 rr_ = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.res_ptr[v]), 0, 0x7ffffffc,
+                                                            0x00020000);
+        const bool rowok = cl < nrow;
+        const unsigned off = (o4blk * (unsigned)p.res_bs[v] + o4ii + (unsigned)(z0 + cl) * (unsigned)p.res_ld[v]) * 4u;
+        if (p.ovec && o4n == 4 && rowok) {
+            const v4u w = __builtin_amdgcn_raw_buffer_load_b128(rr_, (int)off, 0, 0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) r[q] = __builtin_bit_cast(float, w[q]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const unsigned o = (rowok && q < o4n) ? off + 4u * q : 0x80000000u;
+                r[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr_, (int)o, 0, 0));
+            }
+        }
+        return p.ovec ? 1 : 4;
+    };
+    auto out_tile_tr = [&](const b3f4& a, int T, const float (&r)[4]) -> int {  // a lower bound of the stores
+        const int e = p.otile[T];
+        const int v = e & 0xff, z0 = (e >> 8) & 0xffff, nrow = e >> 24;
+        if (v >= kMaxVars) return 0;  // padding tile (uniform)
+        int R0 = 16 * T + cl;
+        asm volatile("" : "+v"(R0));  // keep the constant reads next to their use
+        const float bo = s_oc[R0], sg = s_oc[kop + R0], mu = s_oc[2 * kop + R0];
+        const float lo = s_oc[3 * kop + R0], hi = s_oc[4 * kop + R0], mk = s_oc[5 * kop + R0];
+        const Rsrc3 ro = __builtin_amdgcn_make_buffer_rsrc(p.out_ptr[v], 0, 0x7ffffffc, 0x00020000);
+        const bool has_res = p.res_ptr[v] != nullptr;  // uniform
+        float y[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float t = a[q] + bo;
+            t = t * sg;
+            t = t + mu;
+            if (t < lo) t = lo;
+            if (t >= hi) t = hi;
+            t = t * mk;
+            if (has_res) t = r[q] + t;
+            y[q] = t;
+        }
+        const bool rowok = cl < nrow;
+        const unsigned off = (o4blk * (unsigned)p.out_bs[v] + o4ii + (unsigned)(z0 + cl) * (unsigned)p.out_ld[v]) * 4u;
+#ifdef FV3_B3_EXP_NOOUT  // experiment only (results invalid): store only a value that is never true
+        if (y[0] == 1234.5f)
+#endif
+        {
+            if (p.ovec && o4n == 4 && rowok) {
+                const v4u w = {__builtin_bit_cast(unsigned, y[0]), __builtin_bit_cast(unsigned, y[1]),
+                               __builtin_bit_cast(unsigned, y[2]), __builtin_bit_cast(unsigned, y[3])};
+                __builtin_amdgcn_raw_buffer_store_b128(w, ro, (int)off, 0, 0);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const unsigned o = (rowok && q < o4n) ? off + 4u * q : 0x80000000u;
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y[q]), ro, (int)o, 0, 0);
+                }
+            }
+        }
+        return p.ovec ? 1 : 4;
+    };
     auto res_load = [&](int T, float (&r)[4]) -> int {  // returns the loads issued (0 or 4)
+        if constexpr (TR) return res_load_tr(T, r);
         const int e = p.otile[T];
         const int v = e & 0xff, z0 = (e >> 8) & 0xffff, nrow = e >> 24;
 #ifdef FV3_B3_EXP_NORES  // experiment only (results invalid): no residual loads
@@ -664,6 +764,7 @@ dense_b3_kernel(B3Args pa)
         return 0;
     };
     auto out_tile = [&](const b3f4& a, int T, const float (&r)[4]) -> int {  // returns the stores issued
+        if constexpr (TR) return out_tile_tr(a, T, r);
         const int e = p.otile[T];
         const int v = e & 0xff, z0 = (e >> 8) & 0xffff, nrow = e >> 24;
         if (v >= kMaxVars) return 0;  // padding tile (uniform)
@@ -750,6 +851,15 @@ dense_b3_kernel(B3Args pa)
         oblk = lblk;
         oii = lii;
         ovalid = lvalid;
+        if constexpr (TR) {
+            const int64_t c4 = tile * kB3Cols + wave * 16 + 4 * hq;
+            const int64_t nv4 = p.ncol - c4;
+            o4n = nv4 <= 0 ? 0 : (nv4 >= 4 ? 4 : (int)nv4);
+            const int64_t cc = o4n > 0 ? c4 : 0;
+            const int64_t b = p.ncol_blk < p.ncol ? cc / p.ncol_blk : 0;
+            o4blk = (unsigned)b;
+            o4ii = (unsigned)(cc - b * p.ncol_blk);
+        }
         // ---- layer 1 over the padded input features ----
         zero_acc();
         if constexpr (GL) {
@@ -1257,10 +1367,38 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
     if (stg_env ? stg_env[0] == 'g' : kB3GldsDefault)
         sl = lds_of(3) <= 160 * 1024 ? 3 : (b.ns == 3 && lds_of(2) <= 160 * 1024 ? 2 : 0);
     if (stg_env && stg_env[0] == 'g' && stg_env[1] == '2' && b.ns == 3 && lds_of(2) <= 160 * 1024) sl = 2;  // A/B
+    // the transposed output layer (TR) on the LDS-DMA pipeline when 4-column groups never
+    // cross a column block; 16-byte epilogue accesses when every output / residual row is
+    // 16-byte aligned.  FV3_B3_TR=0 keeps the row-per-lane epilogue (A/B, tests).
+    bool tr = sl > 0 && (nb >= ncol || nb % 4 == 0);
+    if (const char* e = getenv("FV3_B3_TR")) tr = tr && atoi(e) != 0;
+    {
+        bool vec = true;
+        auto al = [&](const void* ptr, const fv3_layout& l) {
+            return ((uintptr_t)ptr % 16) == 0 && l.ld % 4 == 0 && (nb >= ncol || l.blk_stride % 4 == 0);
+        };
+        for (int v = 0; v < m->n_out; ++v) {
+            vec = vec && al(outputs[v], out_l[v]);
+            const int r = m->out_residual[v];
+            if (r >= 0) vec = vec && al(inputs[r], in_l[r]);
+        }
+        a.ovec = vec ? 1 : 0;
+    }
     auto pick = [&](auto ns) -> const void* {
         constexpr int NS = decltype(ns)::value;
         auto by_hu = [&](auto slc) -> const void* {
             constexpr int S = decltype(slc)::value;
+            if constexpr (S > 0) {
+                if (tr) {
+                    if (nwv == 4)
+                        return b.hu == 4 ? (const void*)dense_b3_kernel<4, S, NS, 4, true>
+                             : b.hu == 8 ? (const void*)dense_b3_kernel<8, S, NS, 4, true>
+                                         : (const void*)dense_b3_kernel<16, S, NS, 4, true>;
+                    return b.hu == 4 ? (const void*)dense_b3_kernel<4, S, NS, 8, true>
+                         : b.hu == 8 ? (const void*)dense_b3_kernel<8, S, NS, 8, true>
+                                     : (const void*)dense_b3_kernel<16, S, NS, 8, true>;
+                }
+            }
             if (nwv == 4)
                 return b.hu == 4 ? (const void*)dense_b3_kernel<4, S, NS, 4>
                      : b.hu == 8 ? (const void*)dense_b3_kernel<8, S, NS, 4>

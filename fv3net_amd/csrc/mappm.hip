@@ -26,6 +26,10 @@ namespace {
 // The remap consumer emits q2(k) for k = 1, 2, ... and asks for next_edge(k) for
 // k = 2, 3, ... strictly in order, so both walk running pointers: no per-lane 64-bit
 // index multiply per output level.
+#ifndef FV3_MAPPM_EDGE_AHEAD
+#define FV3_MAPPM_EDGE_AHEAD 1  // next_edge's load one call ahead (0: tools A/B builds)
+#endif
+
 struct DevCol {
     const float* pe1_;
     const float* q1_;
@@ -33,7 +37,8 @@ struct DevCol {
     float* q2_;
     int64_t ld_pe1, ld_q1, ld_pe2, ld_q2;
     int kn;
-    const float* pe2_next;  // pe2(k + 1) for the next next_edge(k)
+    const float* pe2_next;  // the edge after nb
+    float nb;               // pe2(k + 1) for the next next_edge(k), loaded one call ahead
     __device__ __forceinline__ float q1(int k) const { return q1_[(int64_t)(k - 1) * ld_q1]; }
     __device__ __forceinline__ float pe1(int k) const { return pe1_[(int64_t)(k - 1) * ld_pe1]; }
     __device__ __forceinline__ float pe2(int k) const { return pe2_[(int64_t)(k - 1) * ld_pe2]; }
@@ -45,8 +50,14 @@ struct DevCol {
     __device__ __forceinline__ float next_edge(int k)
     {
         if (k + 1 > kn + 1) return 0.0f;
+#if FV3_MAPPM_EDGE_AHEAD
+        const float r = nb;
+        pe2_next += ld_pe2;
+        nb = (k + 2 <= kn + 1) ? *pe2_next : 0.0f;
+#else
         const float r = *pe2_next;
         pe2_next += ld_pe2;
+#endif
         return r;
     }
 };
@@ -57,9 +68,6 @@ struct DevCol {
 // and no 64-bit address (DevCol's each hold an address pair, which the compiler does not
 // fold into a uniform-base form by itself).  The host checks every array spans < 4 GiB.
 // emit / next_edge walk per-lane pointers as in DevCol.
-#ifndef FV3_MAPPM_EDGE_AHEAD
-#define FV3_MAPPM_EDGE_AHEAD 1  // DevColBuf::next_edge's load one call ahead (0: tools A/B builds)
-#endif
 typedef __amdgpu_buffer_rsrc_t MRsrc;
 __device__ __forceinline__ MRsrc mrsrc(const void* p)
 {
@@ -167,6 +175,7 @@ __device__ __forceinline__ DevCol make_col(const MappmArgs& a, int64_t c)
     d.ld_q2 = a.l_q2.ld;
     d.kn = a.kn;
     d.pe2_next = d.pe2_ + 2 * d.ld_pe2;
+    d.nb = d.kn >= 2 ? *d.pe2_next : 0.0f;
     return d;
 }
 
@@ -175,7 +184,7 @@ __global__ __launch_bounds__(256) void mappm_ppm_kernel(MappmArgs a)
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= a.ncol) return;
     DevCol col = make_col(a, c);
-    mappm_ppm_column(col, a.km, a.kn, a.iv, a.kord);
+    mappm_ppm_column<DevCol, true, true>(col, a.km, a.kn, a.iv, a.kord);
 }
 
 // tools/mappm_small_time.py, kord 1 79->79: C48 (13,824 columns) 142 -> 38 us, C96
@@ -507,6 +516,7 @@ struct DevColPair {
     int64_t ld_pe1, ld_pe2, ld_q1[2], ld_q2[2];
     int kn;
     const float* pe2_next;
+    float nb;  // as DevCol::nb
     __device__ __forceinline__ float q1(int f, int k) const { return q1_[f][(int64_t)(k - 1) * ld_q1[f]]; }
     __device__ __forceinline__ float pe1(int k) const { return pe1_[(int64_t)(k - 1) * ld_pe1]; }
     __device__ __forceinline__ float pe2(int k) const { return pe2_[(int64_t)(k - 1) * ld_pe2]; }
@@ -518,8 +528,14 @@ struct DevColPair {
     __device__ __forceinline__ float next_edge(int k)
     {
         if (k + 1 > kn + 1) return 0.0f;
+#if FV3_MAPPM_EDGE_AHEAD
+        const float r = nb;
+        pe2_next += ld_pe2;
+        nb = (k + 2 <= kn + 1) ? *pe2_next : 0.0f;
+#else
         const float r = *pe2_next;
         pe2_next += ld_pe2;
+#endif
         return r;
     }
 };
@@ -542,6 +558,7 @@ __global__ __launch_bounds__(256) void mappm_ppm_pair_kernel(MappmPairArgs a)
     }
     d.kn = a.kn;
     d.pe2_next = d.pe2_ + 2 * d.ld_pe2;
+    d.nb = d.kn >= 2 ? *d.pe2_next : 0.0f;
     mappm_ppm_columns<2>(d, a.km, a.kn, a.iv, a.kord);
 }
 

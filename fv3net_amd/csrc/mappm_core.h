@@ -386,7 +386,11 @@ FV3_HD inline void layer_hook(C&, long) {}
 //   float pe2(int k)  k = 1..kn+1        void emit(int k, float v)
 //   float next_edge(int k) -> pe2(k+1) or 0 when k+1 > kn+1
 // FAST selects remap_layer_fast (default) or the reference-shaped remap_layer (host A/B).
-template <class Col, bool FAST = true>
+// CARRY: level L + 4's loads issued one iteration ahead and carried across the loop's
+// back edge (the mappm kernel: measured faster there, 0.527 vs 0.535 ms at C384 kord 1)
+// or at the iteration's start (the coarsen kernels: 1 field 0.767 -> 0.753 ms,
+// profiles/r04o_remap_ab.log).  Same loads, same bits.
+template <class Col, bool FAST = true, bool CARRY = false>
 FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
 {
     // window state E_L: q(L..L+3), dp(L..L+3), pe1(L..L+4), dc(L..L+2), ALraw(L..L+2), h2(L-1..L+1)
@@ -438,14 +442,23 @@ FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
     RemapState s{1, false, 0.0f, 0.0f, c.pe2(1), c.pe2(2)};
 
     // level j = L + 4 is ingested at the end of iteration L; its q1 / pe1 are read one
-    // iteration earlier, so each load has a whole layer of arithmetic to arrive
-    float q_pf = 0.0f, pe_pf = 0.0f;
-    if (5 <= km) {
-        q_pf = c.q1(5);
-        pe_pf = c.pe1(6);
+    // iteration earlier (CARRY) or at the iteration's start (ahead of its stores, so the
+    // compiler keeps them there), so each load has arithmetic to arrive behind
+    float qc_pf = 0.0f, pec_pf = 0.0f;
+    if constexpr (CARRY) {
+        if (5 <= km) {
+            qc_pf = c.q1(5);
+            pec_pf = c.pe1(6);
+        }
     }
-
     for (int L = 1; L <= km; ++L) {
+        float q_pf = qc_pf, pe_pf = pec_pf;
+        if constexpr (!CARRY) {
+            if (L + 4 <= km) {
+                q_pf = c.q1(L + 4);
+                pe_pf = c.pe1(L + 5);
+            }
+        }
         // ---- emit the final coefficients of layer L ----
         Ppm a{qv[0], alv[0], (L < km) ? alv[1] : ar_km, 0.0f};
         const float dcL = dcv[0];
@@ -479,9 +492,11 @@ FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
             pen = pe_pf;
             dpn = pen - pev[4];
         }
-        if (j + 1 <= km) {  // prefetch level j + 1
-            q_pf = c.q1(j + 1);
-            pe_pf = c.pe1(j + 2);
+        if constexpr (CARRY) {
+            if (j + 1 <= km) {  // level j + 1, for the next iteration
+                qc_pf = c.q1(j + 1);
+                pec_pf = c.pe1(j + 2);
+            }
         }
         const int m = L + 3;  // dc(m), ALraw(m)
         float dcm = 0.0f, alm = 0.0f;

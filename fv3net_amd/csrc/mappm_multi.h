@@ -238,7 +238,7 @@ template <int NF, class Col>
 FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord)
 {
     // window state E_L as in mappm_ppm_column, the q-dependent parts per field
-    float qv[NF][4], dcv[NF][3], alv[NF][3], h2v[NF][3], ar_km[NF], q_pf[NF];
+    float qv[NF][4], dcv[NF][3], alv[NF][3], h2v[NF][3], ar_km[NF];
     float dpv[4], pev[5];
     const bool huynh = kord >= 7;
 
@@ -273,7 +273,6 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord)
             // h2(2) = ppm_h2(dc1, dc3, dp(1), dp(2), dp(3))
             h2v[f][2] = huynh ? 2.0f * (dc3 / dpv[2] - dc1 / dpv[0]) / hden * d0sq : 0.0f;
             ar_km[f] = 0.0f;
-            q_pf[f] = 0.0f;
         }
     }
 
@@ -291,13 +290,14 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord)
     s.xv = false;
     for (int f = 0; f < NF; ++f) s.qsum[f] = 0.0f;
 
-    float pe_pf = 0.0f;
-    if (5 <= km) {
-        for (int f = 0; f < NF; ++f) q_pf[f] = c.q1(f, 5);
-        pe_pf = c.pe1(6);
-    }
-
     for (int L = 1; L <= km; ++L) {
+        // level L + 4's q1 / pe1 read at the iteration's start, as in mappm_ppm_column
+        float q_pf[NF], pe_pf = 0.0f;
+        for (int f = 0; f < NF; ++f) q_pf[f] = 0.0f;
+        if (L + 4 <= km) {
+            for (int f = 0; f < NF; ++f) q_pf[f] = c.q1(f, L + 4);
+            pe_pf = c.pe1(L + 5);
+        }
         // ---- the final coefficients of layer L, per field ----
         LayerViewN<NF> v;
         v.pl0 = pev[0];
@@ -333,10 +333,6 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord)
             for (int f = 0; f < NF; ++f) qn[f] = q_pf[f];
             pen = pe_pf;
             dpn = pen - pev[4];
-        }
-        if (j + 1 <= km) {
-            for (int f = 0; f < NF; ++f) q_pf[f] = c.q1(f, j + 1);
-            pe_pf = c.pe1(j + 2);
         }
         const int m = L + 3;
         float dcm[NF], alm[NF];

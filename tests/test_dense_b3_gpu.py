@@ -38,17 +38,21 @@ def _check(gpu_out, ref64, rtol=None):
         assert_per_level(g, r, rtol, f"output {o}")
 
 
-@pytest.fixture(autouse=True, params=[("glds", None), ("glds", "8"), ("glds", "4"), ("reg", None)],
-                ids=["glds", "glds-w8", "glds-w4", "reg"])
+@pytest.fixture(autouse=True, params=[("glds", None, None), ("glds", "8", None), ("glds", "4", None),
+                                      ("glds", None, "0"), ("reg", None, None)],
+                ids=["glds", "glds-w8", "glds-w4", "glds-rows", "reg"])
 def b3_stage(request, monkeypatch):
     """Every test on both staging pipelines of the kernel (FV3_B3_STAGE): LDS-DMA (the
     default) and register staging; the LDS-DMA one also with the block shape forced
     (FV3_B3_WAVES: 8-wave blocks of 128 columns, 4-wave blocks of 64, which the host picks
-    for grids with fewer 128-column tiles than CUs)."""
-    stage, waves = request.param
+    for grids with fewer 128-column tiles than CUs) and with the row-per-lane output layer
+    instead of the transposed one (FV3_B3_TR=0)."""
+    stage, waves, tr = request.param
     monkeypatch.setenv("FV3_B3_STAGE", stage)
     if waves:
         monkeypatch.setenv("FV3_B3_WAVES", waves)
+    if tr:
+        monkeypatch.setenv("FV3_B3_TR", tr)
     return request.param
 
 

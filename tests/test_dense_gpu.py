@@ -252,12 +252,20 @@ def test_bind_float64_state_sees_updates(gpu):
 
 @pytest.mark.parametrize("ncol,precision", [(1000, "f32"), (1000, "bf16x3"), (13824 + 37, "f32"),
                                             (13824 + 37, "bf16x3"), (1000, "bf16x6"), (13824 + 37, "bf16x6")])
-def test_residual_outputs_stay_inside(gpu, ncol, precision):
+@pytest.mark.parametrize("tr", ["1", "0"])
+def test_residual_outputs_stay_inside(gpu, ncol, precision, tr, monkeypatch):
     """Regression for the memory fault fixed in round 1 (residual outputs read one level
     past a 79-level input): an emulator-style model whose output is input + de-normalised
     difference (Difference.backward), residual input an EXACT-size [79, ncol] tensor,
-    ragged last tile for both kernels, outputs written into NaN-filled level slices."""
+    ragged last tile for both kernels, outputs written into NaN-filled level slices.  The
+    split kernel with its transposed output layer (FV3_B3_TR=1: 16-byte residual loads and
+    stores at 1,000 columns, dword ones at 13,861, whose rows are not 16-byte aligned) and
+    without (0)."""
     import torch
+
+    if precision == "f32" and tr == "0":
+        pytest.skip("the exact-f32 kernel has one output layer")
+    monkeypatch.setenv("FV3_B3_TR", tr)
 
     rng = np.random.default_rng(ncol)
     x = rng.normal(250.0, 10.0, (ncol, 79)).astype(np.float32)

@@ -89,7 +89,7 @@ def host_lib():
     os.replace(tmp, own)
     lib = ctypes.CDLL(own)
     os.unlink(own)  # the mapping stays valid; nothing is left behind
-    for fn in (lib.host_mappm, lib.host_mappm_cursor, lib.host_mappm_generic):
+    for fn in (lib.host_mappm, lib.host_mappm_cursor, lib.host_mappm_generic, lib.host_mappm_carry):
         fn.restype = ctypes.c_int
         fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                        ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
@@ -106,7 +106,8 @@ def host_lib():
 def _host(lib, pe1, q, pe2, iv, kord, cursor=False):
     pe1, q, pe2 = (np.ascontiguousarray(a, np.float32) for a in (pe1, q, pe2))
     out = np.empty((pe2.shape[0] - 1, q.shape[1]), np.float32)
-    fn = {True: lib.host_mappm_cursor, False: lib.host_mappm, "generic": lib.host_mappm_generic}[cursor]
+    fn = {True: lib.host_mappm_cursor, False: lib.host_mappm, "generic": lib.host_mappm_generic,
+          "carry": lib.host_mappm_carry}[cursor]
     rc = fn(q.shape[0], pe1.ctypes.data, q.ctypes.data, pe2.shape[0] - 1, pe2.ctypes.data, out.ctypes.data,
             q.shape[1], iv, kord)
     assert rc == 0
@@ -122,6 +123,9 @@ def test_streaming_algorithm_matches_golden(host_lib):
                 for qn in ("qs", "qr"):
                     res = _host(host_lib, pe1, g[f"c{ci}_{qn}"], pe2, int(iv), int(kord))
                     assert _bits_equal(res, g[f"c{ci}_{qn}_k{kord}_iv{iv}"]), (ci, qn, kord, iv)
+                    if kord <= 7:  # the device mappm kernel's build (loads carried one level ahead)
+                        res = _host(host_lib, pe1, g[f"c{ci}_{qn}"], pe2, int(iv), int(kord), cursor="carry")
+                        assert _bits_equal(res, g[f"c{ci}_{qn}_k{kord}_iv{iv}"]), (ci, qn, kord, iv, "carry")
 
 
 @pytest.mark.parametrize("kat", KATS, ids=["identity", "out_of_bounds", "nans"])
