@@ -684,9 +684,14 @@ dense_b3_kernel(B3Args pa)
         const bool rowok = cl < nrow;
         const unsigned off = (o4blk * (unsigned)p.res_bs[v] + o4ii + (unsigned)(z0 + cl) * (unsigned)p.res_ld[v]) * 4u;
         if (p.ovec && o4n == 4 && rowok) {
-            const v4u w = __builtin_amdgcn_raw_buffer_load_b128(rr_, (int)off, 0, 0);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) r[q] = __builtin_bit_cast(float, w[q]);
+            // a plain 16-byte global load: this toolchain's clang lowers
+            // __builtin_amdgcn_raw_buffer_load_b128 to ONE dword load splatted over the
+            // four lanes of the vector (seen in the ISA), so the buffer form is not used
+            const float4 w = *reinterpret_cast<const float4*>(p.res_ptr[v] + off / 4u);
+            r[0] = w.x;
+            r[1] = w.y;
+            r[2] = w.z;
+            r[3] = w.w;
         } else {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {

@@ -370,7 +370,7 @@ __global__ __launch_bounds__(64) void mappm_cs_kernel(MappmArgs a)
 // fewer scratch accesses per column; the scratch keeps its full [2][km+3] shape
 // PF > 0: loads run PF levels ahead in the solve, one layer ahead in the main loop
 // (mappm_cs_column).  C32: buffer loads / stores at 32-bit offsets (DevColBuf / GlobalScrBuf).
-template <int NT, int PF, bool C32>
+template <int NT, int PF, bool C32, int KORD = 0>
 __global__ __launch_bounds__(256) void mappm_cs_global_kernel(MappmArgs a)
 {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -393,7 +393,7 @@ __global__ __launch_bounds__(256) void mappm_cs_global_kernel(MappmArgs a)
         d.kn = a.kn;
         d.pe2_next = d.pe2_ + 2 * d.ld_pe2;
         d.nb = a.kn >= 2 ? *d.pe2_next : 0.0f;
-        mappm_cs_column<DevColBuf, GlobalScrBuf, NT, PF>(d, scr, a.km, a.kn, a.iv, a.kord);
+        mappm_cs_column<DevColBuf, GlobalScrBuf, NT, PF, KORD>(d, scr, a.km, a.kn, a.iv, a.kord);
     } else {
         GlobalScr scr{a.scratch + c, stride, (int64_t)(a.km + 3) * stride};
         DevCol col = make_col(a, c);
@@ -436,6 +436,13 @@ const void* cs_global_kernel(const MappmArgs& a, int64_t nlanes)
     case 4: return (const void*)mappm_cs_global_kernel<NT_, 4, C_>;               \
     case 8: return (const void*)mappm_cs_global_kernel<NT_, 8, C_>;               \
     default: return (const void*)mappm_cs_global_kernel<NT_, 2, C_>;              \
+    }
+    // kord 10 (config #3's kord > 7 leg) at the default load distances: the column
+    // specialised for it (FV3_MAPPM_CS_KORD=0: the generic one, A/B)
+    const char* ke = getenv("FV3_MAPPM_CS_KORD");
+    if (c32 && (a.kord == 10 || a.kord == -10) && !(ke && atoi(ke) == 0)) {
+        if (nt && pf == 4) return (const void*)mappm_cs_global_kernel<48, 4, true, 10>;
+        if (!nt && pf == 2) return (const void*)mappm_cs_global_kernel<0, 2, true, 10>;
     }
     if (c32) {
         if (nt) { FV3_CS_PF(48, true) } else { FV3_CS_PF(0, true) }

@@ -789,10 +789,13 @@ FV3_HD inline void mappm_ppm_column_by_output(Col& c, int km, int kn, int iv, in
 // unrolled by PF, static ring indices), and the main loop's q1 / edge / pe1 one layer
 // ahead.  Loads only move earlier, past stores to other addresses: the same values, the
 // same bits.
-template <class Col, class Scr, int NT = 0, int PF = 0>
+//
+// KORD > 0: the column for |kord| = KORD only (the host dispatches it for that kord): the
+// kord switch and the flags that kord never reads fold away at compile time.
+template <class Col, class Scr, int NT = 0, int PF = 0, int KORD = 0>
 FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int kord)
 {
-    const int akord = kord < 0 ? -kord : kord;
+    const int akord = KORD > 0 ? KORD : (kord < 0 ? -kord : kord);
     const float qs = 0.0f;  // mappm passes an uninitialised qs (mappm.f90:33,49)
     constexpr int NTR = NT > 0 ? NT : 1;
     const bool tail = NT > 0 && iv != -2 && km >= NT + 1;
@@ -1019,6 +1022,26 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
     qcw[3] = edge_c(3, qw[2], qw[3], qw[4], qw[5]);
     float pl0 = c.pe1(1), pl1 = c.pe1(2);
 
+    // subgrid flags of layers L-1, L, L+1 (mappm.f90:269-288), index i = 0, 1, 2 of the
+    // window: each layer's flags are computed once, as index 2, and shift with the window
+    bool extm[3] = {false, false, false}, ext5[3] = {false, false, false}, ext6[3] = {false, false, false};
+    auto flags = [&](int i, int k) {
+        const float qkm = qw[i], qk = qw[i + 1], qkp = qw[i + 2];
+        const float ql = qcw[i], qr = qcw[i + 1];
+        if (k == 1 || k == km)
+            extm[i] = (ql - qk) * (qr - qk) > 0.0f;
+        else
+            extm[i] = (qk - qkm) * (qkp - qk) < 0.0f;
+        const float x0 = 2.0f * qk - (ql + qr);
+        const float x1 = fabsf(ql - qr);
+        ext5[i] = fabsf(x0) > x1;
+        ext6[i] = fabsf(3.0f * x0) > x1;
+    };
+    if (akord <= 16) {
+        flags(0, 0);  // layer 0: never read
+        flags(1, 1);
+    }
+
     for (int L = 1; L <= km; ++L) {
         // PF: q1(L + 4), edge(L + 3), pe1(L + 2), which the end of layer L takes into the
         // windows, are loaded at its start (ahead of the layer's stores, so the compiler
@@ -1037,21 +1060,7 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
         if (akord > 16) {
             a.a6 = a6_of(a);  // perfectly linear scheme (mappm.f90:207-216)
         } else {
-            // subgrid flags of layers L-1, L, L+1 (mappm.f90:269-288): index i = 0,1,2
-            bool extm[3], ext5[3], ext6[3];
-            for (int i = 0; i < 3; ++i) {
-                const int k = L - 1 + i;
-                const float qkm = qw[i], qk = qw[i + 1], qkp = qw[i + 2];
-                const float ql = qcw[i], qr = qcw[i + 1];
-                if (k == 1 || k == km)
-                    extm[i] = (ql - qk) * (qr - qk) > 0.0f;
-                else
-                    extm[i] = (qk - qkm) * (qkp - qk) < 0.0f;
-                const float x0 = 2.0f * qk - (ql + qr);
-                const float x1 = fabsf(ql - qr);
-                ext5[i] = fabsf(x0) > x1;
-                ext6[i] = fabsf(3.0f * x0) > x1;
-            }
+            flags(2, L + 1);
             const float g_m1 = qw[1] - qw[0];  // gam(L-1)
             const float g_0 = qw[2] - qw[1];   // gam(L)
             const float g_p1 = qw[3] - qw[2];  // gam(L+1)
@@ -1154,6 +1163,11 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
         if (L == km) break;
         for (int i = 0; i < 5; ++i) qw[i] = qw[i + 1];
         for (int i = 0; i < 3; ++i) qcw[i] = qcw[i + 1];
+        for (int i = 0; i < 2; ++i) {
+            extm[i] = extm[i + 1];
+            ext5[i] = ext5[i + 1];
+            ext6[i] = ext6[i + 1];
+        }
         pl0 = pl1;
         if constexpr (PF > 0) {
             qw[5] = nq;

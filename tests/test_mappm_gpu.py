@@ -104,13 +104,15 @@ def test_cs_lds_path_vs_oracle_bit_exact(gpu, km, kn, ncol, monkeypatch):
             assert _bits_equal(res, oracle_mappm(pe1, q, pe2, iv, kord)), (kord, iv)
 
 
-@pytest.mark.parametrize("nt,pf,c32", [(0, 0, 0), (0, 2, 0), (0, 0, 1), (0, 2, 1), (0, 4, 1), (0, 8, 1), (48, 0, 1),
-                                        (48, 8, 1), (48, 4, 0)])
-def test_cs_kernel_variants_vs_oracle_bit_exact(gpu, nt, pf, c32, monkeypatch, mappm_path):
+@pytest.mark.parametrize("nt,pf,c32,kspec", [(0, 0, 0, 1), (0, 2, 0, 1), (0, 0, 1, 1), (0, 2, 1, 1), (0, 2, 1, 0),
+                                              (0, 4, 1, 1), (0, 8, 1, 1), (48, 0, 1, 1), (48, 8, 1, 1), (48, 4, 1, 1),
+                                              (48, 4, 1, 0), (48, 4, 0, 1)])
+def test_cs_kernel_variants_vs_oracle_bit_exact(gpu, nt, pf, c32, kspec, monkeypatch, mappm_path):
     """Every build of the global-scratch kord > 7 kernel: register tail depth NT, load
     distance PF (two register sets of PF levels in the solve), buffer operations at 32-bit
-    offsets or 64-bit addresses: the same bits as the oracle, on level counts around the
-    blocks' remainders."""
+    offsets or 64-bit addresses, the column specialised for kord 10 (the default load
+    distances with buffer operations) or not: the same bits as the oracle, on level counts
+    around the blocks' remainders."""
     from fv3net_amd.mappm import mappm_device
 
     if mappm_path != "serial":
@@ -118,6 +120,7 @@ def test_cs_kernel_variants_vs_oracle_bit_exact(gpu, nt, pf, c32, monkeypatch, m
     monkeypatch.setenv("FV3_MAPPM_CS_NT", str(nt))
     monkeypatch.setenv("FV3_MAPPM_CS_PF", str(pf))
     monkeypatch.setenv("FV3_MAPPM_CS_C32", str(c32))
+    monkeypatch.setenv("FV3_MAPPM_CS_KORD", str(kspec))
     for km, kn, ncol in ((5, 9, 257), (17, 12, 333), (50, 60, 300), (79, 79, 777), (127, 40, 300)):
         rng = np.random.default_rng(km * 31 + kn + ncol + pf)
         pe1, q, pe2 = _columns(rng, km, kn, ncol)
