@@ -413,11 +413,12 @@ const void* cs_global_kernel(const MappmArgs& a, int64_t nlanes)
     const int64_t ncol = a.ncol;
     int nt = ncol < 262144 ? 48 : 0;
     if (const char* e = getenv("FV3_MAPPM_CS_NT")) nt = atoi(e);
-    // load distance (tools/mappm_pf_ab.py, profiles/r04l_mappm_pf.log; C384 79 -> 79 kord
-    // 10 with buffer operations): 884,736 columns PF = 0 / 2 / 4 / 8 0.909 / 0.761 /
-    // 0.798 / 0.836 ms (64-bit addresses, PF = 0: 0.871); 110,592 columns (register tail)
-    // 0.224 / 0.185 / 0.182 / 0.182 ms
-    int pf = nt ? 4 : 2;
+    // load distance (tools/mappm_pf_ab.py; C384 79 -> 79 kord 10, buffer operations):
+    // before the rolling subgrid flags (profiles/r04l_mappm_pf.log) 884,736 columns PF =
+    // 0 / 2 / 4 / 8 0.909 / 0.761 / 0.798 / 0.836 ms (64-bit addresses, PF = 0: 0.871),
+    // 110,592 columns (register tail) 0.224 / 0.185 / 0.182 / 0.182 ms; with them
+    // (profiles/r04q_mappm_kord_ab.log) PF = 2 / 4 0.772 / 0.765 ms and 0.175 / 0.170 ms
+    int pf = 4;
     if (const char* e = getenv("FV3_MAPPM_CS_PF")) pf = atoi(e);
     // 32-bit lane byte offsets when every column offset (and the scratch) fits
     // buffer operations at 32-bit byte offsets when every array (and the scratch) spans
@@ -437,13 +438,13 @@ const void* cs_global_kernel(const MappmArgs& a, int64_t nlanes)
     case 8: return (const void*)mappm_cs_global_kernel<NT_, 8, C_>;               \
     default: return (const void*)mappm_cs_global_kernel<NT_, 2, C_>;              \
     }
-    // kord 10 (config #3's kord > 7 leg) at the default load distances: the column
-    // specialised for it (FV3_MAPPM_CS_KORD=0: the generic one, A/B)
+    // kord 10 under the register tail at the default load distance: the column
+    // specialised for it (0.170 -> 0.168 ms at 110,592 columns; on the full grid the
+    // specialised build measured slower, 0.772 -> 0.806 ms at PF = 2, so it is not used
+    // there; profiles/r04q_mappm_kord_ab.log).  FV3_MAPPM_CS_KORD=0: the generic column.
     const char* ke = getenv("FV3_MAPPM_CS_KORD");
-    if (c32 && (a.kord == 10 || a.kord == -10) && !(ke && atoi(ke) == 0)) {
-        if (nt && pf == 4) return (const void*)mappm_cs_global_kernel<48, 4, true, 10>;
-        if (!nt && pf == 2) return (const void*)mappm_cs_global_kernel<0, 2, true, 10>;
-    }
+    if (c32 && nt && pf == 4 && (a.kord == 10 || a.kord == -10) && !(ke && atoi(ke) == 0))
+        return (const void*)mappm_cs_global_kernel<48, 4, true, 10>;
     if (c32) {
         if (nt) { FV3_CS_PF(48, true) } else { FV3_CS_PF(0, true) }
     }
