@@ -443,9 +443,11 @@ const void* cs_global_kernel(const MappmArgs& a, int64_t nlanes)
     // specialised build measured slower, 0.772 -> 0.806 ms at PF = 2, so it is not used
     // there; profiles/r04q_mappm_kord_ab.log).  FV3_MAPPM_CS_KORD=0: the generic column.
     const char* ke = getenv("FV3_MAPPM_CS_KORD");
-    if (c32 && nt && pf == 4 && (a.kord == 10 || a.kord == -10) && !(ke && atoi(ke) == 0))
+    if (c32 && nt == 48 && pf == 4 && (a.kord == 10 || a.kord == -10) && !(ke && atoi(ke) == 0))
         return (const void*)mappm_cs_global_kernel<48, 4, true, 10>;
     if (c32) {
+        if (nt == 8) { FV3_CS_PF(8, true) }    // A/B only (FV3_MAPPM_CS_NT=8|16)
+        if (nt == 16) { FV3_CS_PF(16, true) }
         if (nt) { FV3_CS_PF(48, true) } else { FV3_CS_PF(0, true) }
     }
     if (nt) { FV3_CS_PF(48, false) }
