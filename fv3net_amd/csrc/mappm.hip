@@ -569,7 +569,10 @@ __global__ __launch_bounds__(256) void mappm_ppm_pair_kernel(MappmPairArgs a)
     d.kn = a.kn;
     d.pe2_next = d.pe2_ + 2 * d.ld_pe2;
     d.nb = d.kn >= 2 ? *d.pe2_next : 0.0f;
-    mappm_ppm_columns<2>(d, a.km, a.kn, a.iv, a.kord);
+#ifndef FV3_MAPPM_PAIR_CARRY
+#define FV3_MAPPM_PAIR_CARRY 1  // 0: tools A/B builds
+#endif
+    mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0>(d, a.km, a.kn, a.iv, a.kord);
 }
 
 }  // namespace fv3

@@ -234,7 +234,9 @@ FV3_HD inline void remap_finish_n(RemapStateN<NF>& s, const ColumnEndsN<NF>& e, 
 }
 
 // ---- NF columns on one pressure column, kord <= 7, fully streaming ----
-template <int NF, class Col>
+// CARRY: as mappm_ppm_column's (level L + 4's loads one iteration ahead, carried across
+// the back edge, or at the iteration's start); same loads, same bits.
+template <int NF, class Col, bool CARRY = false>
 FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord)
 {
     // window state E_L as in mappm_ppm_column, the q-dependent parts per field
@@ -290,13 +292,24 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord)
     s.xv = false;
     for (int f = 0; f < NF; ++f) s.qsum[f] = 0.0f;
 
+    float qc_pf[NF], pec_pf = 0.0f;
+    for (int f = 0; f < NF; ++f) qc_pf[f] = 0.0f;
+    if constexpr (CARRY) {
+        if (5 <= km) {
+            for (int f = 0; f < NF; ++f) qc_pf[f] = c.q1(f, 5);
+            pec_pf = c.pe1(6);
+        }
+    }
     for (int L = 1; L <= km; ++L) {
-        // level L + 4's q1 / pe1 read at the iteration's start, as in mappm_ppm_column
-        float q_pf[NF], pe_pf = 0.0f;
-        for (int f = 0; f < NF; ++f) q_pf[f] = 0.0f;
-        if (L + 4 <= km) {
-            for (int f = 0; f < NF; ++f) q_pf[f] = c.q1(f, L + 4);
-            pe_pf = c.pe1(L + 5);
+        // level L + 4's q1 / pe1: carried from the previous iteration (CARRY) or read at
+        // this iteration's start, as in mappm_ppm_column
+        float q_pf[NF], pe_pf = pec_pf;
+        for (int f = 0; f < NF; ++f) q_pf[f] = qc_pf[f];
+        if constexpr (!CARRY) {
+            if (L + 4 <= km) {
+                for (int f = 0; f < NF; ++f) q_pf[f] = c.q1(f, L + 4);
+                pe_pf = c.pe1(L + 5);
+            }
         }
         // ---- the final coefficients of layer L, per field ----
         LayerViewN<NF> v;
@@ -333,6 +346,12 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord)
             for (int f = 0; f < NF; ++f) qn[f] = q_pf[f];
             pen = pe_pf;
             dpn = pen - pev[4];
+        }
+        if constexpr (CARRY) {
+            if (j + 1 <= km) {  // level j + 1, for the next iteration
+                for (int f = 0; f < NF; ++f) qc_pf[f] = c.q1(f, j + 1);
+                pec_pf = c.pe1(j + 2);
+            }
         }
         const int m = L + 3;
         float dcm[NF], alm[NF];

@@ -137,16 +137,25 @@ struct ColN {
     void emit(int f, int k, float v) { q2_[((int64_t)f * kn + (k - 1)) * ncol + i] = v; }
     float next_edge(int k) const { return (k + 1 <= kn + 1) ? pe2(k + 1) : 0.0f; }
 };
-template <int NF>
+template <int NF, bool CARRY = false>
 void run_n(int km, const float* pe1, const float* q1, int kn, const float* pe2, float* q2, int64_t ncol, int iv,
            int kord)
 {
     for (int64_t i = 0; i < ncol; ++i) {
         ColN c{pe1, q1, pe2, q2, ncol, i, km, kn};
-        fv3::mappm_ppm_columns<NF>(c, km, kn, iv, kord);
+        fv3::mappm_ppm_columns<NF, ColN, CARRY>(c, km, kn, iv, kord);
     }
 }
 }  // namespace
+
+// two fields with level L + 4's loads carried one iteration ahead (the device pair kernel)
+extern "C" int host_mappm_pair_carry(int km, const float* pe1, const float* q1, int kn, const float* pe2, float* q2,
+                                     int64_t ncol, int iv, int kord)
+{
+    if (km < 4 || kn < 1 || kord > 7) return -1;
+    run_n<2, true>(km, pe1, q1, kn, pe2, q2, ncol, iv, kord);
+    return 0;
+}
 
 extern "C" int host_mappm_multi(int nf, int km, const float* pe1, const float* q1, int kn, const float* pe2,
                                 float* q2, int64_t ncol, int iv, int kord)

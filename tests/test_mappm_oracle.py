@@ -276,6 +276,15 @@ def test_multi_field_streaming_bit_identical(host_lib, nf, km, kn):
                           iv, kord) == 0
                 for f in range(nf):
                     assert _bits_equal(out[f], _host(host_lib, pe1, q[f], pe2, iv, kord)), (nf, f, kord, iv)
+                if nf == 2:  # the device pair kernel's build (loads carried one level ahead)
+                    carry = np.empty_like(out)
+                    cf = host_lib.host_mappm_pair_carry
+                    cf.restype = ctypes.c_int
+                    cf.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
+                    assert cf(km, pe1.ctypes.data, q.ctypes.data, kn, pe2.ctypes.data, carry.ctypes.data, ncol, iv,
+                              kord) == 0
+                    assert _bits_equal(carry, out), (kord, iv, "carry")
 
 
 @pytest.mark.parametrize("km,kn", [(4, 4), (5, 3), (6, 9), (7, 7), (8, 5), (9, 9), (17, 12), (33, 40), (79, 79),
