@@ -12,6 +12,7 @@ Weights are held in Keras' own layout (kernel ``[fan_in, fan_out]``, bias
 import ctypes
 import dataclasses
 import os
+import warnings
 from typing import Dict, List, Mapping, Optional, Sequence, Tuple
 
 import numpy as np
@@ -366,6 +367,101 @@ class DenseColumnModel:
                              "device buffers the kernel reads in place, or call forward() each step")
         return self._last_bound
 
+    # ---- host arrays in, host arrays out (the drop-in call on numpy data) ----------
+    _PIPELINE_MIN_BYTES = 64 << 20
+
+    def forward_host(self, arrays: Sequence, level_axes: Optional[Sequence[int]] = None,
+                     precision: Optional[str] = None, out: Optional[Sequence[np.ndarray]] = None) -> List[np.ndarray]:
+        """numpy inputs -> numpy float32 outputs (pure_keras.py:98-118 predicts on host
+        arrays).  The arrays' own pages are page-locked for the call
+        (``transfer.HostPages``: the copy engines DMA straight from and to them) and the
+        inputs land in device buffers of their own dtype (a float64 state is read in place
+        by the kernel), cached per shape with the bound kernel.
+
+        Inputs with a common leading block axis (tiles: ``(tile, z, y, x)``, level axis
+        > 0) over ``_PIPELINE_MIN_BYTES`` run pipelined over the blocks on three streams:
+        block b + 1's host-to-device copies, block b's predict and block b - 1's
+        device-to-host copies overlap (PCIe is full duplex: in and out at once).  The
+        same kernels on the same columns, so the outputs are bit-identical to one call.
+        ``out``: float32 numpy arrays to write (else fresh ones; a caller that reuses
+        them across calls saves first-touch page faults on the fresh pages)."""
+        from . import transfer
+
+        arrays = [np.ascontiguousarray(a) for a in arrays]
+        axes = list(level_axes) if level_axes is not None else [0] * len(arrays)
+        n0 = arrays[0].shape[0] if arrays[0].ndim else 0
+        blocks = (n0 >= 2 and all(a.ndim >= 2 and a.shape[0] == n0 and ax is not None and ax > 0
+                                  for a, ax in zip(arrays, axes))
+                  and sum(a.nbytes for a in arrays) >= self._PIPELINE_MIN_BYTES)
+        key = (tuple((a.shape, a.dtype.str, ax) for a, ax in zip(arrays, axes)), precision, blocks)
+        ent = getattr(self, "_host_call", None)
+        if ent is None or ent[0] != key or ent[1][0].device.index != torch.cuda.current_device():
+            _device.require_gpu()
+            dev = torch.device("cuda", torch.cuda.current_device())
+            bufs = [torch.empty(a.shape, dtype=torch.from_numpy(a[:0].reshape(-1)).dtype, device=dev) for a in arrays]
+            if blocks:
+                sub_axes = [ax - 1 for ax in axes]
+                runs = [self._bind_or_forward([b[t] for b in bufs], sub_axes, precision) for t in range(n0)]
+                streams = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
+            else:
+                runs = [self._bind_or_forward(bufs, axes, precision)]
+                streams = None
+            ent = (key, bufs, runs, streams)
+            self._host_call = ent
+        _, bufs, runs, streams = ent
+
+        def src(a):
+            if a.flags.writeable:
+                return torch.from_numpy(a)
+            with warnings.catch_warnings():  # only read: torch's non-writable-array warning does not apply
+                warnings.simplefilter("ignore", UserWarning)
+                return torch.from_numpy(a)
+
+        with transfer.HostPages(arrays) as pages:
+            cur = torch.cuda.current_stream()
+            if streams is None:
+                for a, b in zip(arrays, bufs):
+                    b.copy_(src(a), non_blocking=True)
+                outs = runs[0]()
+                host = _host_outputs(out, [tuple(o.shape) for o in outs])
+                pages.add(host)
+                for h, o in zip(host, outs):
+                    torch.from_numpy(h).copy_(o, non_blocking=True)
+                return host  # HostPages synchronised the stream before releasing the pages
+            s_in, s_out = streams
+            s_in.wait_stream(cur)  # after whatever the caller queued on these buffers
+            s_out.wait_stream(cur)
+            ev_in = []
+            with torch.cuda.stream(s_in):
+                for t in range(n0):
+                    for a, b in zip(arrays, bufs):
+                        b[t].copy_(src(a[t]), non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(s_in)
+                    ev_in.append(ev)
+            host = None
+            for t in range(n0):
+                cur.wait_event(ev_in[t])
+                outs = runs[t](cur)
+                if host is None:
+                    host = _host_outputs(out, [(n0,) + tuple(o.shape) for o in outs])
+                    pages.add(host)
+                ev = torch.cuda.Event()
+                ev.record(cur)
+                s_out.wait_event(ev)
+                with torch.cuda.stream(s_out):
+                    for h, o in zip(host, outs):
+                        torch.from_numpy(h[t]).copy_(o, non_blocking=True)
+            cur.wait_stream(s_out)  # HostPages' exit synchronises the current stream
+            cur.wait_stream(s_in)
+        return host
+
+    def _bind_or_forward(self, bufs, axes, precision):
+        try:  # validated once; re-launched on the same buffers every call
+            return self.bind(bufs, level_axes=axes, precision=precision)
+        except (ValueError, NotImplementedError):  # inputs the kernel reads through a copy
+            return lambda stream=None: self.forward(bufs, level_axes=axes, stream=stream, precision=precision)
+
     # ---- persistence -------------------------------------------------------------
     _WEIGHTS = "weights.npz"
     _CONFIG = "dense_config.yaml"
@@ -405,6 +501,17 @@ class DenseColumnModel:
             in_sigma=[z[f"input_{v}/sigma"] for v in range(len(config.in_nz))],
         )
         return cls(config, p)
+
+
+def _host_outputs(out, shapes):
+    if out is None:
+        return [np.empty(sh, np.float32) for sh in shapes]
+    out = list(out)
+    if len(out) != len(shapes) or any(not (isinstance(o, np.ndarray) and o.dtype == np.float32 and o.shape == sh
+                                           and o.flags.c_contiguous and o.flags.writeable)
+                                      for o, sh in zip(out, shapes)):
+        raise ValueError(f"out: writable contiguous float32 numpy arrays of shapes {shapes}")
+    return out
 
 
 class BoundForward:

@@ -297,44 +297,10 @@ class DenseColumnPredictor(Predictor):
 
     def _host_forward(self, arrays, axes):
         """Host arrays in, host float32 arrays out, for the drop-in call on numpy data
-        (pure_keras.py:98-118 predicts on host arrays).  The caller's pages are
-        page-locked for the call (fv3_host_register) so the copy engines DMA straight
-        from and to them; the inputs land in device buffers of their own dtype kept per
-        shape (a float64 state is read in place by the kernel), the bound kernel runs
-        on them, and the outputs come back into freshly allocated numpy arrays."""
-        from . import transfer
-
-        key = tuple((a.shape, a.dtype.str, ax) for a, ax in zip(arrays, axes))
-        ent = getattr(self, "_host_call", None)
-        if ent is None or ent[0] != key or ent[1][0].device.index != torch.cuda.current_device():
-            from . import _device
-
-            _device.require_gpu()
-            dev = torch.device("cuda", torch.cuda.current_device())
-            bufs = [torch.empty(a.shape, dtype=torch.from_numpy(a[:0].reshape(-1)).dtype, device=dev)
-                    for a in arrays]
-            try:  # validated once; re-launched on the same buffers every call
-                run = self.model.bind(bufs, level_axes=axes)
-            except (ValueError, NotImplementedError):  # inputs the kernel reads through a copy
-                run = lambda: self.model.forward(bufs, level_axes=axes)  # noqa: E731
-            ent = (key, bufs, run)
-            self._host_call = ent
-        _, bufs, run = ent
-        with transfer.HostPages(arrays) as pages:
-            for a, b in zip(arrays, bufs):
-                if not a.flags.writeable:  # only read: torch's non-writable-array warning does not apply
-                    with warnings.catch_warnings():
-                        warnings.simplefilter("ignore", UserWarning)
-                        src = torch.from_numpy(a)
-                else:
-                    src = torch.from_numpy(a)
-                b.copy_(src, non_blocking=True)
-            outs = run()
-            host = [np.empty(tuple(o.shape), np.float32) for o in outs]
-            pages.add(host)
-            for h, o in zip(host, outs):
-                torch.from_numpy(h).copy_(o, non_blocking=True)
-        return host  # HostPages synchronised the stream before releasing the pages
+        (pure_keras.py:98-118 predicts on host arrays): ``DenseColumnModel.forward_host``
+        (the caller's pages page-locked for the copies, device buffers of the inputs' own
+        dtype cached per shape, tile blocks pipelined over three streams)."""
+        return self.model.forward_host(arrays, axes)
 
     # -- persistence ------------------------------------------------------------
     def dump(self, path: str) -> None:
