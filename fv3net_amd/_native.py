@@ -76,7 +76,7 @@ EXPORTED_SYMBOLS = (
     "fv3_derived_elementwise",
     "fv3_derived_columns",
 )
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # fv3_dense_forward_ex precisions
 DENSE_F32 = 0
@@ -269,6 +269,7 @@ _SIGNATURES = {
     "fv3_plan_add_copy": (_I, [_P, _P, _P, ctypes.c_size_t]),
     "fv3_plan_add_repeat": (_I, [_P, _P, _P, ctypes.c_size_t, _I]),
     "fv3_host_unregister": (_I, [_P]),
+    "fv3_copy_to_host": (_I, [_P, _P, ctypes.c_size_t, _P]),
     "fv3_derived_columns": (_I, [_I, ctypes.POINTER(Field), _I, ctypes.POINTER(Field), _I, _I64, _I,
                                  ctypes.POINTER(_D), _I, _P]),
 }

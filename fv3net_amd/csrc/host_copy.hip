@@ -1,0 +1,61 @@
+// fv3net_amd — device-to-host copies as a kernel writing the caller's page-locked pages.
+//
+// The pipelined host call (DenseColumnModel.forward_host) overlaps the
+// inputs' host-to-device copies with the outputs' device-to-host copies.  Issued as two
+// copy-engine streams, the two directions overlapped in some runs and ran nearly in
+// sequence in others (the runtime's engine choice).  Here the out-copy is a kernel on the
+// compute stream that stores straight into the registered host pages over PCIe (16-byte
+// vector stores), leaving the copy engines to the in-copies.
+#include "common.h"
+
+namespace fv3 {
+namespace {
+
+__global__ __launch_bounds__(256) void copy_to_host_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                           int64_t n16)
+{
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride) dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(64) void copy_tail_kernel(const unsigned char* __restrict__ src,
+                                                       unsigned char* __restrict__ dst, int n)
+{
+    if ((int)threadIdx.x < n) dst[threadIdx.x] = src[threadIdx.x];
+}
+
+}  // namespace
+}  // namespace fv3
+
+extern "C" int fv3_copy_to_host(void* host_dst, const void* dev_src, size_t bytes, void* stream)
+{
+    using namespace fv3;
+    clear_error();
+    FV3_REQUIRE(host_dst && dev_src, "copy_to_host: NULL pointer");
+    if (!bytes) return FV3_OK;
+    void* d = nullptr;
+    const hipError_t e = hipHostGetDevicePointer(&d, host_dst, 0);
+    if (e != hipSuccess || !d) {
+        (void)hipGetLastError();
+        set_error("copy_to_host: host memory not page-locked / mapped (%s)", hipGetErrorString(e));
+        return FV3_ERR_UNSUPPORTED;
+    }
+    FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, ((uintptr_t)d % 16) == 0 && ((uintptr_t)dev_src % 16) == 0,
+                     "copy_to_host: 16-byte aligned buffers only");
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t n16 = (int64_t)(bytes / 16);
+    if (n16) {
+        const int64_t blocks = std::min<int64_t>((n16 + 255) / 256, 4096);
+        hipLaunchKernelGGL(copy_to_host_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+                           reinterpret_cast<const uint4*>(dev_src), reinterpret_cast<uint4*>(d), n16);
+        FV3_LAUNCH_CHECK();
+    }
+    const int tail = (int)(bytes % 16);
+    if (tail) {
+        hipLaunchKernelGGL(copy_tail_kernel, dim3(1), dim3(64), 0, s,
+                           reinterpret_cast<const unsigned char*>(dev_src) + 16 * n16,
+                           reinterpret_cast<unsigned char*>(d) + 16 * n16, tail);
+        FV3_LAUNCH_CHECK();
+    }
+    return FV3_OK;
+}

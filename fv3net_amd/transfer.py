@@ -182,6 +182,10 @@ class HostPages:
         """How many arrays this block registered."""
         return len(self._registered)
 
+    def is_registered(self, a) -> bool:
+        """Whether this block page-locked ``a``'s memory."""
+        return isinstance(a, np.ndarray) and a.ctypes.data in self._registered
+
     def add(self, arrays):
         for a in arrays:
             if not (isinstance(a, np.ndarray) and a.flags.c_contiguous) or a.nbytes < self.min_bytes:

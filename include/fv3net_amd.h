@@ -55,7 +55,7 @@ int fv3_abi_version(void); /* bumped on any signature change (2: emulator fields
                               3: fv3_dense_forward_ex, 4: composites + Adapter,
                               5: per-operand dtypes in fv3_adapter_target, fv3_build_kind,
                               6: fv3_host_register / fv3_host_unregister,
-                              7: fv3_plan_*) */
+                              7: fv3_plan_*, 8: fv3_copy_to_host) */
 const char* fv3_build_kind(void); /* "product" (fv3net_amd/build.py, no experiment knob compiled in)
                                      or "experiment" (a tools/ variant: results may be invalid) */
 
@@ -591,6 +591,14 @@ int fv3_derived_columns(int op, const fv3_field* in, int n_in, const fv3_field* 
  */
 int fv3_host_register(void* ptr, size_t bytes);
 int fv3_host_unregister(void* ptr);
+
+/* Copy `bytes` of device memory into page-locked host memory (fv3_host_register'ed or
+ * pinned) with a kernel on `stream` that stores into the host pages over PCIe, instead of
+ * a copy engine: the pipelined host call's out-copies, beside the copy engines' in-copies
+ * (DESIGN.md §3.7).  FV3_ERR_UNSUPPORTED when the host memory is not page-locked or the
+ * buffers are not 16-byte aligned (the caller copies with hipMemcpyAsync instead).  No
+ * reference counterpart: a transport detail of the drop-in call (pure_keras.py:98-118). */
+int fv3_copy_to_host(void* host_dst, const void* dev_src, size_t bytes, void* stream);
 
 /*
  * Launch plan: a fixed sequence of this library's launches over fixed device buffers,

@@ -272,12 +272,17 @@ def test_dense_predictor_level_axis_anywhere(gpu, dims):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-def test_forward_host_tile_pipeline_bit_identical(gpu, dtype):
+@pytest.mark.parametrize("kernel_out", ["1", "0"])
+def test_forward_host_tile_pipeline_bit_identical(gpu, dtype, kernel_out, monkeypatch):
     """DenseColumnModel.forward_host over (tile, z, y, x) numpy arrays: the tile blocks
     pipelined over three streams (threshold lowered so a C12 state takes the path) give
     the bits of the device-resident forward of the same values, on repeated calls, with
-    fresh outputs each call; a level-leading array (no block axis) takes the one-call path."""
+    fresh outputs each call; the out-copies by the fv3_copy_to_host kernel into the
+    registered pages (FV3_D2H_KERNEL=1) or by the copy engines (0); a level-leading array
+    (no block axis) takes the one-call path."""
     import torch
+
+    monkeypatch.setenv("FV3_D2H_KERNEL", kernel_out)
 
     from fv3net_amd.dense import DenseColumnModel, DenseModelConfig
 

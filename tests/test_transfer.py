@@ -62,3 +62,27 @@ def test_predict_mappm_host_to_host_matches_device_resident(gpu):
     rec = bench.predict_mappm_host_to_host(gpu, res=24, steps=1)
     assert rec["bit_identical_to_device_resident"]
     assert rec["host_bytes_per_step"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nbytes", [16, 4096, 4100, 1 << 20, (1 << 20) + 7])
+def test_copy_to_host_kernel(gpu, nbytes):
+    """fv3_copy_to_host: a kernel storing device bytes into registered host pages (16-byte
+    vector stores and a byte tail) gives the bytes; unregistered host memory is refused
+    with FV3_ERR_UNSUPPORTED (the caller then uses the copy engines)."""
+    import torch
+
+    from fv3net_amd import _native
+    from fv3net_amd.transfer import HostPages
+
+    lib = _native.load()
+    src = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda")
+    host = np.zeros(max(nbytes, 1 << 16), np.uint8)  # >= HostPages' 64 KiB minimum
+    with HostPages([host], min_bytes=0) as pages:
+        assert pages.is_registered(host)
+        st = lib.fv3_copy_to_host(host.ctypes.data, src.data_ptr(), nbytes, torch.cuda.current_stream().cuda_stream)
+        assert st == 0, st
+    assert np.array_equal(host[:nbytes], src.cpu().numpy())
+    assert not host[nbytes:].any()
+    plain = np.zeros(nbytes, np.uint8)
+    assert lib.fv3_copy_to_host(plain.ctypes.data, src.data_ptr(), nbytes, 0) == _native.FV3_ERR_UNSUPPORTED
