@@ -394,12 +394,15 @@ def host_to_host(dev, res, steps=10):
                     "streams above 64 MiB (C384)"}
 
 
-def predict_mappm_host_to_host(dev, res=384, steps=5):
+def predict_mappm_host_to_host(dev, res=384, steps=5, bands=6):
     """north_star's predict + mappm with the host boundary included: float64 numpy T/q
     (z, rows, x) and float32 numpy edge pressures pe1/pe2 (z+1, columns; f2py hands the
-    reference's mappm float32 arrays) in, through the product's pinned double-buffered
-    staging, the fused predict reading float64 in place, the two-field mappm of both
-    tendencies, and the float32 remapped tendencies back to numpy.  Wall time per step."""
+    reference's mappm float32 arrays) in, the fused predict reading float64 in place, the
+    two-field mappm of both tendencies, and the float32 remapped tendencies back to numpy.
+    The caller's pages are page-locked for the call (``transfer.HostPages``) and the
+    columns run in ``bands`` bands pipelined over three streams: band b + 1's pitched
+    in-copies (``transfer.copy_band``), band b's predict + remap and band b - 1's
+    out-copies overlap.  Wall time per step."""
     import torch
 
     from fv3net_amd import transfer
@@ -411,23 +414,44 @@ def predict_mappm_host_to_host(dev, res=384, steps=5):
     q = wl.inputs[1].double().cpu().numpy()
     pe1 = wl.pe1.cpu().numpy()
     pe2 = wl.pe2.cpu().numpy()
-    dT = torch.empty(T.shape, dtype=torch.float64, device=dev)
-    dq = torch.empty(q.shape, dtype=torch.float64, device=dev)
+    nz, ncol = T.shape[0], wl.ncol
+    T2, q2 = T.reshape(nz, ncol), q.reshape(nz, ncol)
+    dT = torch.empty((nz, ncol), dtype=torch.float64, device=dev)
+    dq = torch.empty((nz, ncol), dtype=torch.float64, device=dev)
     d1 = torch.empty_like(wl.pe1)
     d2 = torch.empty_like(wl.pe2)
-    bound = wl.model.bind([dT, dq], level_axes=[0, 0], outputs=wl.outputs, out_level_axis=0)
-    plan = MappmMultiPlan(d1, [o.view(o.shape[0], -1) for o in wl.outputs], d2, 1, 1, out=wl.remapped)
+    outs = [o.view(nz, ncol) for o in wl.outputs]
     host_out = [np.empty(tuple(r.shape), np.float32) for r in wl.remapped]
+    # band edges on whole grid rows
+    rows = ncol // res
+    edges = [res * (rows * b // bands) for b in range(bands + 1)]
+    runs = []
+    for b in range(bands):
+        c0, c1 = edges[b], edges[b + 1]
+        bound = wl.model.bind([dT[:, c0:c1], dq[:, c0:c1]], level_axes=[0, 0],
+                              outputs=[o[:, c0:c1] for o in outs], out_level_axis=0)
+        plan = MappmMultiPlan(d1[:, c0:c1], [o[:, c0:c1] for o in outs], d2[:, c0:c1], 1, 1,
+                              out=[r[:, c0:c1] for r in wl.remapped])
+        runs.append((c0, c1, bound, plan))
+    s_in, s_out = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
 
     def step():
-        transfer.h2d(T, out=dT)
-        transfer.h2d(q, out=dq)
-        transfer.h2d(pe1, out=d1)
-        transfer.h2d(pe2, out=d2)
-        bound()
-        plan()
-        for h, o in zip(host_out, wl.remapped):
-            transfer.d2h(o, out=h)
+        with transfer.HostPages([T, q, pe1, pe2] + host_out):
+            cur = torch.cuda.current_stream()
+            ev_in = []
+            for c0, c1, _, _ in runs:  # every band's in-copies first, on their own stream
+                for h, d in ((T2, dT), (q2, dq), (pe1, d1), (pe2, d2)):
+                    transfer.copy_band(d[:, c0:c1], h[:, c0:c1], s_in)
+                ev = torch.cuda.Event()
+                ev.record(s_in)
+                ev_in.append(ev)
+            for (c0, c1, bound, plan), ev in zip(runs, ev_in):
+                cur.wait_event(ev)
+                bound(cur)
+                plan()
+                for h, r in zip(host_out, wl.remapped):
+                    transfer.copy_band(h[:, c0:c1], r[:, c0:c1], s_out)
+            cur.wait_stream(s_out)  # HostPages' exit synchronises the current stream
 
     for _ in range(2):
         step()
@@ -445,8 +469,10 @@ def predict_mappm_host_to_host(dev, res=384, steps=5):
                for h, r in zip(host_out, wl.remapped))
     return {"columns_per_s": wl.ncol / wall, "ms_per_step": wall * 1e3, "host_bytes_per_step": nbytes,
             "pcie_inclusive_gbs": nbytes / wall / 1e9, "bit_identical_to_device_resident": bool(same),
-            "note": "float64 numpy T/q + float32 numpy pe1/pe2 in -> pinned double-buffered H2D -> fused predict "
-                    "(f64 read in place) -> two-field mappm of dQ1/dQ2 (kord 1, iv 1) -> pinned D2H -> float32 numpy"}
+            "bands": bands,
+            "note": "float64 numpy T/q + float32 numpy pe1/pe2 in (pages registered per call) -> per column band: "
+                    "pitched H2D, fused predict (f64 read in place), two-field mappm of dQ1/dQ2 (kord 1, iv 1), "
+                    "pitched D2H into float32 numpy; bands pipelined over three streams"}
 
 
 def rank_call_host_to_host(dev, calls=30):

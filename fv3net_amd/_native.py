@@ -270,6 +270,8 @@ _SIGNATURES = {
     "fv3_plan_add_repeat": (_I, [_P, _P, _P, ctypes.c_size_t, _I]),
     "fv3_host_unregister": (_I, [_P]),
     "fv3_copy_to_host": (_I, [_P, _P, ctypes.c_size_t, _P]),
+    "fv3_copy_2d": (_I, [_P, ctypes.c_size_t, _P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
+                         _P]),
     "fv3_derived_columns": (_I, [_I, ctypes.POINTER(Field), _I, ctypes.POINTER(Field), _I, _I64, _I,
                                  ctypes.POINTER(_D), _I, _P]),
 }

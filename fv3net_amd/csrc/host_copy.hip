@@ -59,3 +59,23 @@ extern "C" int fv3_copy_to_host(void* host_dst, const void* dev_src, size_t byte
     }
     return FV3_OK;
 }
+
+// A pitched (2-D) copy between host and device on `stream`: `height` rows of `width`
+// bytes, rows `spitch` / `dpitch` bytes apart.  A band of columns of a level-leading
+// [level][column] array is such a copy, one row per level (the pipelined host call over
+// column bands, bench.py predict + mappm host-to-host).  kind 1: host to device, 2:
+// device to host.  Host memory should be page-locked (fv3_host_register) for the copy
+// to be asynchronous.
+extern "C" int fv3_copy_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height,
+                           int kind, void* stream)
+{
+    using namespace fv3;
+    clear_error();
+    FV3_REQUIRE(dst && src, "copy_2d: NULL pointer");
+    FV3_REQUIRE(kind == 1 || kind == 2, "copy_2d: kind %d (1: host to device, 2: device to host)", kind);
+    FV3_REQUIRE(width <= dpitch && width <= spitch, "copy_2d: row wider than its pitch");
+    if (!width || !height) return FV3_OK;
+    FV3_HIP(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height,
+                             kind == 1 ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, (hipStream_t)stream));
+    return FV3_OK;
+}

@@ -442,15 +442,16 @@ class DenseColumnModel:
             host = None
             lib = _native.load()
             hcur = cur.cuda_stream
-            kernel_out = os.environ.get("FV3_D2H_KERNEL", "1") != "0"
+            kernel_out = os.environ.get("FV3_D2H_KERNEL", "0") == "1"
             for t in range(n0):
                 cur.wait_event(ev_in[t])
                 outs = runs[t](cur)
                 if host is None:
                     host = _host_outputs(out, [(n0,) + tuple(o.shape) for o in outs])
                     pages.add(host)
-                    # out-copies as a kernel storing into the registered host pages, on the
-                    # compute stream (fv3_copy_to_host): the copy engines keep the in-copies
+                    # FV3_D2H_KERNEL=1: out-copies as a kernel storing into the registered
+                    # host pages on the compute stream (fv3_copy_to_host), the copy engines
+                    # keeping the in-copies; default: the copy engines both ways
                     kernel_out = kernel_out and all(pages.is_registered(h) for h in host)
                 done = False
                 if kernel_out:

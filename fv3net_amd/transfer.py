@@ -163,8 +163,8 @@ class HostPages:
     """``with HostPages(arrays) as p:`` page-locks the arrays' own memory
     (fv3_host_register) so that copies on the current stream DMA straight from / to it,
     with no bounce buffer and no host memcpy; ``p.add(more)`` registers more arrays in
-    the block.  On exit the current stream is synchronised (every copy issued in the
-    block is complete) and what was registered here is released.  Arrays below
+    the block.  On exit the device is synchronised (every copy issued in the block, on
+    any stream, is complete) and what was registered here is released.  Arrays below
     ``min_bytes`` (sharing pages with other allocations) and arrays whose pages cannot
     be registered are left as they are: copies from them are pageable copies, which
     the runtime completes before returning."""
@@ -202,7 +202,12 @@ class HostPages:
 
     def __exit__(self, *exc):
         try:
-            torch.cuda.current_stream().synchronize()
+            # the whole device, not only the current stream: a copy or kernel that a
+            # caller put on a side stream must not touch the pages after they are released
+            if self._registered:
+                torch.cuda.synchronize()
+            else:
+                torch.cuda.current_stream().synchronize()
         finally:
             for p in self._registered:
                 self._lib.fv3_host_unregister(p)
@@ -232,3 +237,31 @@ def h2d(arr, out=None, device=None):
 
 def d2h(t, out=None):
     return stager(t.device).d2h(t, out)
+
+
+def copy_band(dst, src, stream=None):
+    """One pitched copy (fv3_copy_2d) between a numpy array view and a CUDA tensor view of
+    the same shape whose first axis (levels) is a fixed pitch apart and whose remaining
+    axes are contiguous within each level: e.g. ``a[:, c0:c1]`` of a [level][column]
+    array, a band of columns.  Host to device when ``src`` is numpy, else device to host;
+    enqueued on ``stream`` (a torch stream or None for the current one).  The host memory
+    should be page-locked (``HostPages``) for the copy to be asynchronous."""
+    from . import _device, _native
+
+    host, dev = (src, dst) if isinstance(src, np.ndarray) else (dst, src)
+    if not (isinstance(host, np.ndarray) and torch.is_tensor(dev) and dev.is_cuda):
+        raise ValueError("copy_band: one numpy array and one CUDA tensor")
+    if tuple(host.shape) != tuple(dev.shape) or host.itemsize != dev.element_size() or host.ndim < 1:
+        raise ValueError(f"copy_band: shapes / dtypes differ ({host.shape} {host.dtype}, {tuple(dev.shape)} {dev.dtype})")
+    if not (host[0].flags.c_contiguous and dev[0].is_contiguous()):
+        raise ValueError("copy_band: each level's elements must be contiguous")
+    width = host[0].nbytes
+    h_pitch = host.strides[0] if host.shape[0] > 1 else width
+    d_pitch = dev.stride(0) * dev.element_size() if dev.shape[0] > 1 else width
+    lib = _native.load()
+    h = _device.stream_handle(stream, [dev])
+    if host is src:
+        st = lib.fv3_copy_2d(dev.data_ptr(), d_pitch, host.ctypes.data, h_pitch, width, host.shape[0], 1, h)
+    else:
+        st = lib.fv3_copy_2d(host.ctypes.data, h_pitch, dev.data_ptr(), d_pitch, width, host.shape[0], 2, h)
+    _native.check(st, "copy_band")

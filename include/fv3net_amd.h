@@ -55,7 +55,7 @@ int fv3_abi_version(void); /* bumped on any signature change (2: emulator fields
                               3: fv3_dense_forward_ex, 4: composites + Adapter,
                               5: per-operand dtypes in fv3_adapter_target, fv3_build_kind,
                               6: fv3_host_register / fv3_host_unregister,
-                              7: fv3_plan_*, 8: fv3_copy_to_host) */
+                              7: fv3_plan_*, 8: fv3_copy_to_host, fv3_copy_2d) */
 const char* fv3_build_kind(void); /* "product" (fv3net_amd/build.py, no experiment knob compiled in)
                                      or "experiment" (a tools/ variant: results may be invalid) */
 
@@ -599,6 +599,13 @@ int fv3_host_unregister(void* ptr);
  * buffers are not 16-byte aligned (the caller copies with hipMemcpyAsync instead).  No
  * reference counterpart: a transport detail of the drop-in call (pure_keras.py:98-118). */
 int fv3_copy_to_host(void* host_dst, const void* dev_src, size_t bytes, void* stream);
+
+/* Pitched copy between host and device on `stream` (hipMemcpy2DAsync): `height` rows of
+ * `width` bytes, `spitch` / `dpitch` bytes apart; kind 1 host to device, 2 device to
+ * host.  A column band of a [level][column] array, one row per level: the pipelined
+ * host call over column bands.  No reference counterpart (transport). */
+int fv3_copy_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height, int kind,
+                void* stream);
 
 /*
  * Launch plan: a fixed sequence of this library's launches over fixed device buffers,
