@@ -192,6 +192,39 @@ def test_kernel_c384_to_c48_sampled_and_deterministic(gpu):
     _bits_equal(a[2:3, :, 8:16, 24:32], r)
 
 
+def test_oracle_preserves_constant_fields():
+    """A size-independent property (pinned here on the oracle): the pressure regrid of a
+    constant profile is that constant (its PPM parabola is flat) and the area-weighted
+    block average of a constant is that constant, to float32 rounding (measured 2.4e-7)."""
+    rng = np.random.default_rng(5)
+    delp, area, _, _ = _smooth_state(rng, 1, 79, 32, 32)
+    for c in (273.15, 0.0123):
+        (r,), _ = OC.coarsen_on_pressure(delp, area, [np.full_like(delp, c)], 8)
+        assert np.isfinite(r).all()
+        assert np.abs(r / np.float32(c) - 1).max() <= 1e-6
+
+
+@pytest.mark.gpu
+def test_kernel_c384_to_c48_constant_fields_preserved(gpu):
+    """The same property at BASELINE config #3's full size (C384 -> C48, 79 levels), every
+    coarse cell, with two fields in one call (the kernel's two-field pass)."""
+    import torch
+
+    from fv3net_amd.coarsen import coarsen_on_pressure
+
+    rng = np.random.default_rng(3843)
+    delp, area, _, _ = _smooth_state(rng, 6, 79, 384, 384)
+    consts = {"T": 273.15, "q": 0.0123}
+    fields = {k: np.full_like(delp, c) for k, c in consts.items()}
+    out, _ = coarsen_on_pressure(delp, area, fields, 8)
+    torch.cuda.synchronize()
+    for k, c in consts.items():
+        r = out[k].cpu().numpy()
+        assert r.shape == (6, 79, 48, 48)
+        assert np.isfinite(r).all(), k
+        assert np.abs(r / np.float32(c) - 1).max() <= 1e-6, k
+
+
 @pytest.mark.gpu
 def test_regrid_vertical_device_matches_oracle(gpu):
     """regridz.regrid_vertical semantics (z last, new-nlevels, error paths)."""
