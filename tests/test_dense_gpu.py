@@ -180,6 +180,35 @@ def test_c384_throughput_shape_and_determinism(gpu):
     _check(got, dense_predict(sub, m.oracle_params(), np.float64))
 
 
+@pytest.mark.parametrize("precision", ["f32", "bf16x3", "bf16x6"])
+def test_c384_columns_independent_of_position(gpu, precision):
+    """A size-independent property at the full C384 grid (884,736 columns): the columns
+    are 37 template columns repeated (37 is prime to every tile width, so each template
+    lands on every lane, wave, tile and block position), and every copy's outputs carry
+    exactly its template's bits.  The 37 templates are held to the float64 graph."""
+    import torch
+
+    rng = np.random.default_rng(3844)
+    ntile, nz, n, nt = 6, 79, 384, 37
+    tT = rng.normal(260, 15, (nt, nz)).astype(np.float32)
+    tq = rng.uniform(0, 0.02, (nt, nz)).astype(np.float32)
+    ncol = ntile * n * n
+    pick = torch.arange(ncol, device="cuda") % nt
+    # (tile, z, y, x) with column index (tile, y, x) -> template index % 37
+    to_grid = lambda t: torch.from_numpy(t).cuda()[pick].reshape(ntile, n, n, nz).permute(0, 3, 1, 2).contiguous()  # noqa: E731
+    T, q = to_grid(tT), to_grid(tq)
+    m = _model(dict(input_variables=["T", "q"], output_variables=["dQ1", "dQ2"], in_nz=[79, 79],
+                    out_nz=[79, 79], width=256, depth=3), samples=[tT, tq])
+    outs = m.forward([T, q], level_axes=[1, 1], precision=precision)
+    torch.cuda.synchronize()
+    got = []
+    for o in outs:
+        cols = o.permute(0, 2, 3, 1).reshape(ncol, nz)  # [column, z]
+        assert torch.equal(cols, cols[:nt][pick]), "a copy differs from its template"
+        got.append(cols[:nt].cpu().numpy())
+    _check(got, dense_predict([tT, tq], m.oracle_params(), np.float64), rtol=1e-4 if precision == "bf16x3" else RTOL)
+
+
 @pytest.mark.parametrize("res,precision", [(7, "f32"), (48, "f32"), (7, "bf16x3"), (48, "bf16x3"), (7, "bf16x6"),
                                            (48, "bf16x6")])
 def test_writes_stay_inside_outputs(gpu, res, precision):

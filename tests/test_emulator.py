@@ -154,6 +154,27 @@ def test_emulator_c384_full_grid(gpu, precision, rtol):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["bf16x3", "f32"])
+def test_emulator_c384_columns_independent_of_position(gpu, precision):
+    """Config #5 at its full size, a size-independent property: 37 template columns
+    (37 is prime to every tile width) repeated over all 884,736 columns, and every copy's
+    outputs carry exactly its template's bits, wherever it falls (lane, wave, tile,
+    block, the residual reads one tile ahead)."""
+    import torch
+
+    ncol, nt = 6 * 384 * 384, 37
+    emu, _ = _emulator(precision=precision)
+    pick = torch.arange(ncol, device="cuda") % nt
+    raw = {k: v[:, pick].contiguous() for k, v in _device_raw(nt, seed=9).items()}
+    out = emu(raw)
+    torch.cuda.synchronize()
+    for k, v in out.items():
+        tmpl = v[:nt] if v.ndim == 1 else v[:, :nt]
+        want = tmpl[pick] if v.ndim == 1 else tmpl[:, pick]
+        assert torch.equal(v, want), k
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("precision,rtol", [("bf16x3", 1e-4), ("bf16x6", 1e-5)])
 def test_emulator_split_kernel_variants_agree(gpu, monkeypatch, precision, rtol):
     """The split kernel's staging pipelines (LDS-DMA, the default, and register staging,

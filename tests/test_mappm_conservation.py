@@ -113,3 +113,26 @@ def test_c384_two_field_pass_conserves_both(gpu):
     torch.cuda.synchronize()
     _check_dev(q, pe1, outs[0], pe2)
     _check_dev(t, pe1, outs[1], pe2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kord", [1, 10])
+def test_c384_columns_independent_of_position(gpu, kord):
+    """37 template columns (edges and values) repeated over the 884,736 columns: every
+    copy's remap carries exactly its template's bits, whichever lane, wave, scratch slot
+    or level tail serves it."""
+    import torch
+
+    from fv3net_amd.mappm import mappm_device, mappm_device_multi
+
+    nt = 37
+    pe1, q, pe2 = _columns_dev(kord + 41, 79, 79, nt)
+    _, t, _ = _columns_dev(kord + 42, 79, 79, nt, positive=True)
+    pick = torch.arange(NCOL_C384, device="cuda") % nt
+    rep = lambda a: a[:, pick].contiguous()  # noqa: E731
+    P1, Q, P2, Tq = rep(pe1), rep(q), rep(pe2), rep(t)
+    outs = [mappm_device(P1, Q, P2, 1, kord)] + list(mappm_device_multi(P1, [Q, Tq], P2, 1, kord))
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        assert torch.equal(o, o[:, :nt][:, pick]), i
+    assert torch.equal(outs[0], outs[1])  # the two-field pass: bit-identical to one field
