@@ -239,6 +239,45 @@ def test_stepper_workload_c96_matches_oracle(gpu, precision):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["f32", "bf16x6"])
+def test_stepper_c96_columns_independent_of_position(gpu, precision):
+    """Config #4 at its full size, a size-independent property: the state is 37 template
+    columns repeated over the 55,296 columns (37 is prime to every tile width), and after
+    two steps every copy of the updated state, the predicted tendencies and the column
+    diagnostics carries exactly its template's bits."""
+    import torch
+
+    from fv3net_amd import workloads as W
+
+    wl = W.make_stepper_workload(96, seed=5, precision=precision)
+    ncol, nt = wl.ncol, 37
+    pick = torch.arange(ncol, device="cuda") % nt
+
+    def cols(t):
+        if t.dim() == 4:  # (tile, z, y, x)
+            return t.permute(1, 0, 2, 3).reshape(t.shape[1], -1)
+        assert t.numel() % ncol == 0
+        return t.reshape(-1, ncol)
+
+    for v in wl.state.values():
+        c = cols(v)
+        rep = c[:, :nt][:, pick]
+        if v.dim() == 4:
+            v.copy_(rep.reshape(v.shape[1], v.shape[0], v.shape[2], v.shape[3]).permute(1, 0, 2, 3))
+        else:
+            v.copy_(rep.reshape(v.shape))
+    for _ in range(2):
+        wl.step()
+    torch.cuda.synchronize()
+    checked = dict(wl.state)
+    checked.update({f"dQ{i + 1}": o for i, o in enumerate(wl.bound.outputs)})
+    checked.update({f"out:{k}": v for k, v in wl._epi.out.items() if torch.is_tensor(v)})
+    for k, v in checked.items():
+        c = cols(v)
+        assert torch.equal(c, c[:, :nt][:, pick]), k
+
+
+@pytest.mark.gpu
 def test_pure_ml_stepper_mirror(gpu):
     """PureMLStepper (machine_learning.py:239-315) over a DenseColumnPredictor: the
     tendencies/diagnostics equal the oracle epilogue applied to the model's own
