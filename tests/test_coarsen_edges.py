@@ -214,3 +214,38 @@ def test_kernel_c384_to_c48_sampled_and_deterministic(gpu):
     assert a.shape == (6, 79, 49, 48)
     assert (a.view(np.uint32) == b.view(np.uint32)).all()
     assert np.isfinite(a).all()
+
+
+def test_oracle_preserves_constant_winds():
+    """A size-independent property, pinned on the oracle: a constant wind stays that
+    constant through the edge pressure regrid and the edge-weighted block average
+    (measured 2.4e-7), for both staggerings."""
+    rng = np.random.default_rng(5)
+    delp, u, v, dx, dy = _winds_state(rng, 79, 48, np.float32)
+    for c in (12.5, -3.25):
+        (ru,) = OC.coarsen_edges_on_pressure(delp, dx, [np.full_like(u, c)], 8, "x")
+        (rv,) = OC.coarsen_edges_on_pressure(delp, dy, [np.full_like(v, c)], 8, "y")
+        for r in (ru, rv):
+            assert np.isfinite(r).all()
+            assert np.abs(r / np.float32(c) - 1).max() <= 1e-6
+
+
+@pytest.mark.gpu
+def test_kernel_c384_to_c48_constant_winds_preserved(gpu):
+    """The same property at config #3's full size (C384 -> C48, 79 levels), every coarse
+    edge of u and v."""
+    import torch
+
+    from fv3net_amd.coarsen import coarsen_edges_on_pressure
+
+    rng = np.random.default_rng(3845)
+    delp, u, v, dx, dy = _winds_state(rng, 79, 384, np.float32)
+    for c in (12.5, -3.25):
+        ru = coarsen_edges_on_pressure(delp, dx, {"u": np.full_like(u, c)}, 8, "x")["u"]
+        rv = coarsen_edges_on_pressure(delp, dy, {"v": np.full_like(v, c)}, 8, "y")["v"]
+        torch.cuda.synchronize()
+        for r, shape in ((ru, (6, 79, 49, 48)), (rv, (6, 79, 48, 49))):
+            r = r.cpu().numpy()
+            assert r.shape == shape
+            assert np.isfinite(r).all()
+            assert np.abs(r / np.float32(c) - 1).max() <= 1e-6
