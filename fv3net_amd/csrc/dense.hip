@@ -666,6 +666,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
             store_x(*pt, t, fq, std::false_type{}, zero_pad);
 #endif
     };
+    // the staging reads every feature's normalisation constants, which other waves wrote
+    // to LDS above: without this barrier a wave whose constants had not yet been written
+    // read what an earlier kernel left in the LDS (the first tile of a block: inf outputs
+    // after a bf16x6 launch, tests/test_stepper.py::test_two_model_stepper_matches_oracle)
+    tile_sync();
     if (tile < p.ntiles) stage(tile, true);
     tile_sync();
     if (p.prio == 0) __builtin_amdgcn_s_setprio(0);
