@@ -218,11 +218,11 @@ def test_dense_predictor_host_arrays_page_locked_path(gpu):
             assert (g.view(np.uint32) == r.view(np.uint32)).all(), shape
     # the registration helper: pages released on exit, a second registration refused cleanly
     a = np.zeros(1 << 20)
-    with transfer.HostPages([a]) as p:
+    with transfer.HostPages([a], enable=True) as p:
         assert len(p._registered) == 1
-        with transfer.HostPages([a]) as p2:  # already registered: left alone
+        with transfer.HostPages([a], enable=True) as p2:  # already registered: left alone
             assert p2._registered == []
-    with transfer.HostPages([a]) as p:  # released above, registrable again
+    with transfer.HostPages([a], enable=True) as p:  # released above, registrable again
         assert len(p._registered) == 1
     torch.cuda.synchronize()
 

@@ -78,7 +78,7 @@ def test_copy_to_host_kernel(gpu, nbytes):
     lib = _native.load()
     src = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda")
     host = np.zeros(max(nbytes, 1 << 16), np.uint8)  # >= HostPages' 64 KiB minimum
-    with HostPages([host], min_bytes=0) as pages:
+    with HostPages([host], min_bytes=0, enable=True) as pages:
         assert pages.is_registered(host)
         st = lib.fv3_copy_to_host(host.ctypes.data, src.data_ptr(), nbytes, torch.cuda.current_stream().cuda_stream)
         assert st == 0, st
