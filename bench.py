@@ -363,18 +363,20 @@ def rank_share_legs(dev, settle_ms=150.0, world=8):
 
 
 def host_to_host(dev, res, steps=10):
-    """The reference's boundary crossing: float64 host (numpy) T/q in, H2D through the
-    product's pinned double-buffered staging (fv3net_amd/transfer.py), the fused
-    predict reading float64 in place, float32 dQ1/dQ2 copied back to host numpy the same
-    way (pure_keras.py:98-118 runs on host arrays).  Wall time per step."""
+    """The reference's boundary crossing: float64 host (numpy) T/q in, H2D as pageable
+    copies or through the library's staging blocks (fv3net_amd/transfer.py), the fused
+    predict reading float64 in place, float32 dQ1/dQ2 DMA'd back into the library's
+    page-locked arena arrays (pure_keras.py:98-118 runs on host arrays).  Wall time per
+    step."""
     import torch
 
+    from fv3net_amd import transfer
     from fv3net_amd import workloads as W
 
     wl = W.make_dense_workload(res, seed=3, device=dev)
     T = wl.inputs[0].double().cpu().numpy()
     q = wl.inputs[1].double().cpu().numpy()
-    host_out = [np.empty(T.shape, np.float32), np.empty(T.shape, np.float32)]
+    host_out = [transfer.empty_host(T.shape, np.float32), transfer.empty_host(T.shape, np.float32)]
 
     def step():  # the product's host boundary (the predictor's numpy path), outputs reused
         wl.model.forward_host([T, q], [1, 1], out=host_out)
@@ -389,9 +391,10 @@ def host_to_host(dev, res, steps=10):
     nbytes = T.nbytes + q.nbytes + sum(h.nbytes for h in host_out)
     return {"columns_per_s": wl.ncol / wall, "ms_per_step": wall * 1e3, "host_bytes_per_step": nbytes,
             "pcie_inclusive_gbs": nbytes / wall / 1e9,
-            "note": "float64 numpy in -> DenseColumnModel.forward_host: the caller's pages page-locked, H2D, the "
-                    "fused predict (f64 read in place), D2H into float32 numpy; tile blocks pipelined over three "
-                    "streams above 64 MiB (C384)"}
+            "host_path": transfer.host_path(),
+            "note": "float64 numpy in -> DenseColumnModel.forward_host: H2D (see host_path), the fused predict "
+                    "(f64 read in place), D2H into float32 numpy outputs reused across calls (library arena "
+                    "when host_path is pinned); tile blocks pipelined over three streams above 64 MiB (C384)"}
 
 
 def predict_mappm_host_to_host(dev, res=384, steps=5, bands=6):
@@ -399,8 +402,9 @@ def predict_mappm_host_to_host(dev, res=384, steps=5, bands=6):
     (z, rows, x) and float32 numpy edge pressures pe1/pe2 (z+1, columns; f2py hands the
     reference's mappm float32 arrays) in, the fused predict reading float64 in place, the
     two-field mappm of both tendencies, and the float32 remapped tendencies back to numpy.
-    The caller's pages are page-locked for the call (``transfer.HostPages``) and the
-    columns run in ``bands`` bands pipelined over three streams: band b + 1's pitched
+    The caller's inputs cross as pageable pitched copies (caller memory is never
+    page-locked), the outputs live in the library's page-locked arena (reused across
+    calls), and the columns run in ``bands`` bands pipelined over three streams: band b + 1's pitched
     in-copies (``transfer.copy_band``), band b's predict + remap and band b - 1's
     out-copies overlap.  Wall time per step."""
     import torch
@@ -421,7 +425,7 @@ def predict_mappm_host_to_host(dev, res=384, steps=5, bands=6):
     d1 = torch.empty_like(wl.pe1)
     d2 = torch.empty_like(wl.pe2)
     outs = [o.view(nz, ncol) for o in wl.outputs]
-    host_out = [np.empty(tuple(r.shape), np.float32) for r in wl.remapped]
+    host_out = [transfer.empty_host(tuple(r.shape), np.float32) for r in wl.remapped]
     # band edges on whole grid rows
     rows = ncol // res
     edges = [res * (rows * b // bands) for b in range(bands + 1)]
@@ -436,22 +440,21 @@ def predict_mappm_host_to_host(dev, res=384, steps=5, bands=6):
     s_in, s_out = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
 
     def step():
-        with transfer.HostPages([T, q, pe1, pe2] + host_out):
-            cur = torch.cuda.current_stream()
-            ev_in = []
-            for c0, c1, _, _ in runs:  # every band's in-copies first, on their own stream
-                for h, d in ((T2, dT), (q2, dq), (pe1, d1), (pe2, d2)):
-                    transfer.copy_band(d[:, c0:c1], h[:, c0:c1], s_in)
-                ev = torch.cuda.Event()
-                ev.record(s_in)
-                ev_in.append(ev)
-            for (c0, c1, bound, plan), ev in zip(runs, ev_in):
-                cur.wait_event(ev)
-                bound(cur)
-                plan()
-                for h, r in zip(host_out, wl.remapped):
-                    transfer.copy_band(h[:, c0:c1], r[:, c0:c1], s_out)
-            cur.wait_stream(s_out)  # HostPages' exit synchronises the current stream
+        cur = torch.cuda.current_stream()
+        for c0, c1, bound, plan in runs:
+            # band b's in-copies (pitched, the runtime's pageable path: the host waits for
+            # them while band b - 1's predict, remap and out-copies run)
+            for h, d in ((T2, dT), (q2, dq), (pe1, d1), (pe2, d2)):
+                transfer.copy_band(d[:, c0:c1], h[:, c0:c1], s_in.cuda_stream)
+            ev = torch.cuda.Event()
+            ev.record(s_in)
+            cur.wait_event(ev)
+            bound(cur)
+            plan()
+            for h, r in zip(host_out, wl.remapped):  # arena outputs: asynchronous DMA
+                transfer.copy_band(h[:, c0:c1], r[:, c0:c1], s_out)
+        cur.wait_stream(s_out)
+        cur.synchronize()
 
     for _ in range(2):
         step()
@@ -470,7 +473,8 @@ def predict_mappm_host_to_host(dev, res=384, steps=5, bands=6):
     return {"columns_per_s": wl.ncol / wall, "ms_per_step": wall * 1e3, "host_bytes_per_step": nbytes,
             "pcie_inclusive_gbs": nbytes / wall / 1e9, "bit_identical_to_device_resident": bool(same),
             "bands": bands,
-            "note": "float64 numpy T/q + float32 numpy pe1/pe2 in (pages registered per call) -> per column band: "
+            "host_path": transfer.host_path(),
+            "note": "float64 numpy T/q + float32 numpy pe1/pe2 in (see host_path) -> per column band: "
                     "pitched H2D, fused predict (f64 read in place), two-field mappm of dQ1/dQ2 (kord 1, iv 1), "
                     "pitched D2H into float32 numpy; bands pipelined over three streams"}
 
@@ -481,6 +485,7 @@ def rank_call_host_to_host(dev, calls=30):
     ``DenseColumnPredictor.predict`` (pure_keras.py:98-118 boundary): host -> device,
     the fused predict, float32 (79, 48, 48) numpy outputs back.  Wall time per call."""
     from fv3net_amd import dataset as D
+    from fv3net_amd import transfer
     from fv3net_amd import workloads as W
     from fv3net_amd.predictor import DenseColumnPredictor
 
@@ -501,8 +506,10 @@ def rank_call_host_to_host(dev, calls=30):
     ncol = T.shape[1] * T.shape[2]
     return {"columns_per_s": ncol / wall, "ms_per_call": wall * 1e3, "columns_per_call": ncol,
             "host_bytes_per_call": T.nbytes + q.nbytes + 2 * ncol * 79 * 4,
+            "host_path": transfer.host_path(),
             "note": "one rank's (79,48,48) float64 numpy T/q Dataset -> DenseColumnPredictor.predict -> float32 "
-                    "(79,48,48) numpy dQ1/dQ2 Dataset (the drop-in call, host boundary included)"}
+                    "(79,48,48) numpy dQ1/dQ2 Dataset, fresh outputs each call (the drop-in call, host boundary "
+                    "included)"}
 
 
 def _ref_mappm_worker(args):

@@ -75,8 +75,18 @@ EXPORTED_SYMBOLS = (
     "fv3_adapter_apply",
     "fv3_derived_elementwise",
     "fv3_derived_columns",
+    "fv3_host_copy",
+    "fv3_host_alloc",
+    "fv3_host_free",
+    "fv3_host_arena_limit",
+    "fv3_host_memory_stats",
+    "fv3_copy_to_host",
+    "fv3_copy_2d",
+    "fv3_center_rotate_winds",
+    "fv3_sum_squares",
+    "fv3_cos_zenith",
 )
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 # fv3_dense_forward_ex precisions
 DENSE_F32 = 0
@@ -176,6 +186,19 @@ class Field(ctypes.Structure):
     ]
 
 
+MAX_DIMS = 6
+
+
+class Strided(ctypes.Structure):
+    """fv3_strided: a float32 / float64 operand addressed by element strides over the dims
+    of a result (0: broadcast)."""
+    _fields_ = [
+        ("data", ctypes.c_void_p),
+        ("f64", ctypes.c_int),
+        ("stride", ctypes.c_int64 * MAX_DIMS),
+    ]
+
+
 _lib = None
 _lock = threading.Lock()
 
@@ -254,7 +277,11 @@ _SIGNATURES = {
     "fv3_adapter_apply": (_I, [ctypes.POINTER(AdapterTarget), _I, _I64, _I, _D, _I, _I, _I, _P]),
     "fv3_derived_elementwise": (_I, [_I, ctypes.POINTER(_P), ctypes.POINTER(_I), _I, _P, _I, _I64,
                                      ctypes.POINTER(_D), _I, _P]),
-    "fv3_host_register": (_I, [_P, ctypes.c_size_t]),
+    "fv3_host_copy": (_I, [_P, _P, ctypes.c_size_t, _I, _P]),
+    "fv3_host_alloc": (_I, [ctypes.c_size_t, ctypes.POINTER(_P)]),
+    "fv3_host_free": (_I, [_P]),
+    "fv3_host_arena_limit": (_I, [ctypes.c_size_t]),
+    "fv3_host_memory_stats": (_I, [ctypes.POINTER(ctypes.c_uint64)]),
     "fv3_plan_create": (_I, [ctypes.POINTER(_P)]),
     "fv3_plan_destroy": (_I, [_P]),
     "fv3_plan_size": (_I, [_P]),
@@ -268,12 +295,16 @@ _SIGNATURES = {
     "fv3_plan_add_fold_rows": (_I, [_P, _P, _I64, _I, _P]),
     "fv3_plan_add_copy": (_I, [_P, _P, _P, ctypes.c_size_t]),
     "fv3_plan_add_repeat": (_I, [_P, _P, _P, ctypes.c_size_t, _I]),
-    "fv3_host_unregister": (_I, [_P]),
     "fv3_copy_to_host": (_I, [_P, _P, ctypes.c_size_t, _P]),
     "fv3_copy_2d": (_I, [_P, ctypes.c_size_t, _P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
                          _P]),
     "fv3_derived_columns": (_I, [_I, ctypes.POINTER(Field), _I, ctypes.POINTER(Field), _I, _I64, _I,
                                  ctypes.POINTER(_D), _I, _P]),
+    "fv3_center_rotate_winds": (_I, [_I, ctypes.POINTER(_I64), Strided, _I64, Strided, _I64, ctypes.POINTER(Strided),
+                                     _P, _I, _P, _I, _P]),
+    "fv3_sum_squares": (_I, [ctypes.POINTER(_P), ctypes.POINTER(_I), _I, _I64, _P, _P]),
+    "fv3_cos_zenith": (_I, [_I, ctypes.POINTER(_I64), Strided, _I, Strided, _I, ctypes.POINTER(_I64), _P, _I64, _P,
+                            _P]),
 }
 
 

@@ -147,6 +147,23 @@ __global__ __launch_bounds__(256) void derived_elementwise_kernel(EwArgs a)
         case FV3_EW_ONE_MINUS_MUL:  // (1 - x) * y (derived_mapping.py:194-195)
             r = as_dtype(as_dtype(1.0 - x, w0) * y, w0 || w1);
             break;
+        case FV3_EW_SIGN_PARALLEL:  // sign(x / y) * abs(y) (derived_mapping.py:163-174)
+        {
+            const bool w = w0 || w1;
+            const double q = as_dtype(x / y, w);
+            const double sg = q > 0.0 ? 1.0 : q < 0.0 ? -1.0 : q == 0.0 ? 0.0 : q;  // np.sign (NaN stays)
+            r = as_dtype(sg * fabs(y), w);
+            break;
+        }
+        case FV3_EW_PROJECT:  // (x * y + z * u) / norm (derived_mapping.py:177-187)
+        {
+            const bool w2_ = a.f64[2], w3 = a.f64[3];
+            const double z = ld(a.in[2], w2_, i), u = ld(a.in[3], w3, i);
+            const bool wa = w0 || w1, wb = w2_ || w3, ws = wa || wb, wr = ws || a.p[1] != 0.0;
+            const double s = as_dtype(as_dtype(x * y, wa) + as_dtype(z * u, wb), ws);
+            r = as_dtype(s / a.p[0], wr);
+            break;
+        }
         case FV3_EW_ISCLOSE_ONEHOT:  // xr.where(isclose(x, p0), 1.0, 0.0): float64 one-hot
         {
             // np.isclose within_tol: |x - y| <= atol + rtol |y| in x's dtype (p1 = rtol,
@@ -297,6 +314,153 @@ __global__ __launch_bounds__(256) void derived_columns_kernel(ColArgs a)
     }
 }
 
+// ---------------------------------------------------------------------------------
+// strided operands over a result of up to FV3_MAX_DIMS dims (xarray's alignment by dim
+// name): the D-grid wind rotation and the solar zenith angle
+// ---------------------------------------------------------------------------------
+struct Shape {
+    int ndim;
+    int64_t n[FV3_MAX_DIMS];
+};
+
+// the element offset of result element i in an operand with strides st
+__device__ __forceinline__ void unravel(const Shape& sh, int64_t i, int64_t* idx)
+{
+    for (int d = sh.ndim - 1; d >= 0; --d) {
+        const int64_t q = i / sh.n[d];
+        idx[d] = i - q * sh.n[d];
+        i = q;
+    }
+}
+
+__device__ __forceinline__ int64_t offset(const Shape& sh, const int64_t* idx, const int64_t* st)
+{
+    int64_t o = 0;
+    for (int d = 0; d < sh.ndim; ++d) o += idx[d] * st[d];
+    return o;
+}
+
+struct RotArgs {
+    Shape sh;
+    int64_t n;
+    fv3_strided x, y, c[4];
+    int64_t xs, ys;
+    void* east;
+    void* north;
+    int east_f64, north_f64;
+};
+
+// rotate.py:9-56: centre both D-grid components (coarsen.py:54-75: 0.5 * (edge +
+// edge.shift(1)) dropping the first edge, i.e. 0.5 * (e[j + 1] + e[j])), then the 2x2
+// rotation by the grid's coefficients; one thread per centred element
+__global__ __launch_bounds__(256) void center_rotate_kernel(RotArgs a)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const bool wx = a.x.f64, wy = a.y.f64;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+        int64_t idx[FV3_MAX_DIMS];
+        unravel(a.sh, i, idx);
+        const int64_t ox = offset(a.sh, idx, a.x.stride), oy = offset(a.sh, idx, a.y.stride);
+        const double xc = as_dtype(0.5 * as_dtype(ld(a.x.data, wx, ox + a.xs) + ld(a.x.data, wx, ox), wx), wx);
+        const double yc = as_dtype(0.5 * as_dtype(ld(a.y.data, wy, oy + a.ys) + ld(a.y.data, wy, oy), wy), wy);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            void* out = r ? a.north : a.east;
+            if (!out) continue;
+            const fv3_strided& cu = a.c[2 * r];
+            const fv3_strided& cv = a.c[2 * r + 1];
+            const bool wu = cu.f64 || wx, wv = cv.f64 || wy;
+            const double pu = as_dtype(ld(cu.data, cu.f64, offset(a.sh, idx, cu.stride)) * xc, wu);
+            const double pv = as_dtype(ld(cv.data, cv.f64, offset(a.sh, idx, cv.stride)) * yc, wv);
+            st(out, r ? a.north_f64 : a.east_f64, i, as_dtype(pu + pv, wu || wv));
+        }
+    }
+}
+
+// sum of squares, stage 1: block b sums a fixed strided subset in float64, then a fixed
+// tree; stage 2 folds the block partials in a fixed tree (deterministic for a given n)
+constexpr int kSqBlocks = 512;
+
+__device__ double block_sum(double v, double* lds)
+{
+    lds[threadIdx.x] = v;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) lds[threadIdx.x] += lds[threadIdx.x + s];
+        __syncthreads();
+    }
+    return lds[0];
+}
+
+struct SqArgs {
+    const void* in[kMaxIn];
+    int f64[kMaxIn];
+    int n_arr;
+    int64_t n;
+};
+
+__global__ __launch_bounds__(256) void sum_squares_stage1(SqArgs a, double* partial)
+{
+    __shared__ double lds[256];
+    double s = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int j = 0; j < a.n_arr; ++j)
+        for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += stride) {
+            const double v = ld(a.in[j], a.f64[j], i);
+            s += v * v;
+        }
+    const double t = block_sum(s, lds);
+    if (threadIdx.x == 0) partial[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(256) void sum_squares_stage2(const double* partial, int nb, double* out)
+{
+    __shared__ double lds[256];
+    double s = 0.0;
+    for (int i = threadIdx.x; i < nb; i += 256) s += partial[i];
+    const double t = block_sum(s, lds);
+    if (threadIdx.x == 0) out[0] = t;
+}
+
+struct ZenArgs {
+    Shape sh;
+    int64_t n;
+    fv3_strided lon, lat;
+    int lon_rad, lat_rad;
+    int64_t tst[FV3_MAX_DIMS];
+    const double* terms;  // [4][nt]: gmst, ra, sin(dec), cos(dec)
+    int64_t nt;
+    double* out;
+};
+
+// degrees -> radians in the operand's dtype (lon * RAD_PER_DEG; np.rad2deg first for a
+// radian-valued DataArray)
+__device__ __forceinline__ double to_rad(double v, bool w, bool rad_units)
+{
+    constexpr double kRadPerDeg = 3.141592653589793 / 180.0, kDegPerRad = 180.0 / 3.141592653589793;
+    if (rad_units) v = as_dtype(v * as_dtype(kDegPerRad, w), w);
+    return as_dtype(v * as_dtype(kRadPerDeg, w), w);
+}
+
+__global__ __launch_bounds__(256) void cos_zenith_kernel(ZenArgs a)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const bool wo = a.lon.f64, wa = a.lat.f64;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+        int64_t idx[FV3_MAX_DIMS];
+        unravel(a.sh, i, idx);
+        const int64_t t = offset(a.sh, idx, a.tst);
+        const double lon = to_rad(ld(a.lon.data, wo, offset(a.sh, idx, a.lon.stride)), wo, a.lon_rad);
+        const double lat = to_rad(ld(a.lat.data, wa, offset(a.sh, idx, a.lat.stride)), wa, a.lat_rad);
+        const double gmst = a.terms[t], ra = a.terms[a.nt + t];
+        const double sdec = a.terms[2 * a.nt + t], cdec = a.terms[3 * a.nt + t];
+        const double sl = wa ? sin(lat) : (double)sinf((float)lat);
+        const double cl = wa ? cos(lat) : (double)cosf((float)lat);
+        const double h = (gmst + lon) - ra;  // local mean sidereal time - right ascension
+        a.out[i] = sl * sdec + cl * cdec * cos(h);
+    }
+}
+
 }  // namespace
 }  // namespace fv3
 
@@ -308,15 +472,17 @@ extern "C" int fv3_derived_elementwise(int op, const void* const* in, const int*
     FV3_REQUIRE(n >= 0, "derived_elementwise: negative size");
     FV3_REQUIRE(n_in >= 1 && n_in <= kMaxIn && in && in_f64, "derived_elementwise: 1..%d inputs", kMaxIn);
     FV3_REQUIRE(n_params >= 0 && n_params <= 4 && (n_params == 0 || params), "derived_elementwise: bad parameters");
-    FV3_REQUIRE(op >= FV3_EW_ADD && op <= FV3_EW_ISCLOSE_ONEHOT, "derived_elementwise: unknown op %d", op);
+    FV3_REQUIRE(op >= FV3_EW_ADD && op <= FV3_EW_PROJECT, "derived_elementwise: unknown op %d", op);
     const bool unary = op == FV3_EW_SCALE || op == FV3_EW_DIV_SCALAR || op == FV3_EW_ISCLOSE_ONEHOT;
     const int need = op == FV3_EW_ISCLOSE_ONEHOT ? 3
                    : (op == FV3_EW_SCALE || op == FV3_EW_DIV_SCALAR) ? 1
-                   : (op == FV3_EW_INCLOUD_TO_GRIDCELL || op == FV3_EW_GRIDCELL_TO_INCLOUD) ? 2 : 0;
+                   : (op == FV3_EW_INCLOUD_TO_GRIDCELL || op == FV3_EW_GRIDCELL_TO_INCLOUD || op == FV3_EW_PROJECT) ? 2
+                                                                                                       : 0;
     FV3_REQUIRE(n_params >= need, "derived_elementwise: op %d needs %d parameters", op, need);
     FV3_REQUIRE((op == FV3_EW_MSE || op == FV3_EW_TEMP_TEND) ? (n_in == 2 || n_in == 3)
                 : unary ? n_in == 1
-                : (op == FV3_EW_ADD || op == FV3_EW_SUB) ? n_in >= 2 : n_in == 2,
+                : (op == FV3_EW_ADD || op == FV3_EW_SUB) ? n_in >= 2
+                : op == FV3_EW_PROJECT ? n_in == 4 : n_in == 2,
                 "derived_elementwise: op %d got %d inputs", op, n_in);
     if (n == 0) return FV3_OK;
     FV3_REQUIRE(out, "derived_elementwise: NULL output");
@@ -369,6 +535,109 @@ extern "C" int fv3_derived_columns(int op, const fv3_field* in, int n_in, const 
     for (int j = 0; j < n_params && j < 4; ++j) a.p[j] = params[j];
     hipLaunchKernelGGL(derived_columns_kernel, dim3((unsigned)((ncol + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, a);
+    FV3_LAUNCH_CHECK();
+    return FV3_OK;
+}
+
+namespace {
+bool shape_ok(int ndim, const int64_t* shape, fv3::Shape& sh, int64_t& n)
+{
+    if (ndim < 1 || ndim > FV3_MAX_DIMS || !shape) return false;
+    sh.ndim = ndim;
+    n = 1;
+    for (int d = 0; d < ndim; ++d) {
+        if (shape[d] < 0) return false;
+        sh.n[d] = shape[d];
+        n *= shape[d];
+    }
+    return true;
+}
+
+unsigned ew_grid(int64_t n)
+{
+    const int64_t g = (n + 255) / 256;
+    return (unsigned)(g < 8192 ? g : 8192);
+}
+}  // namespace
+
+extern "C" int fv3_center_rotate_winds(int ndim, const int64_t* shape, fv3_strided x_wind, int64_t x_stag,
+                                       fv3_strided y_wind, int64_t y_stag, const fv3_strided* coeff, void* eastward,
+                                       int east_f64, void* northward, int north_f64, void* stream)
+{
+    using namespace fv3;
+    clear_error();
+    RotArgs a{};
+    FV3_REQUIRE(shape_ok(ndim, shape, a.sh, a.n), "center_rotate_winds: 1..%d dims of size >= 0", FV3_MAX_DIMS);
+    FV3_REQUIRE(coeff, "center_rotate_winds: NULL coefficients");
+    if (a.n == 0) return FV3_OK;
+    FV3_REQUIRE(x_wind.data && y_wind.data, "center_rotate_winds: NULL wind");
+    FV3_REQUIRE(x_stag != 0 && y_stag != 0, "center_rotate_winds: zero staggered stride");
+    a.x = x_wind, a.y = y_wind, a.xs = x_stag, a.ys = y_stag;
+    for (int j = 0; j < 4; ++j) a.c[j] = coeff[j];
+    const bool wx = x_wind.f64, wy = y_wind.f64;
+    if (eastward) {
+        FV3_REQUIRE(coeff[0].data && coeff[1].data, "center_rotate_winds: NULL eastward coefficient");
+        const bool w = (coeff[0].f64 || wx) || (coeff[1].f64 || wy);
+        FV3_REQUIRE((east_f64 != 0) == w, "center_rotate_winds: eastward must be float%d (numpy's promotion)",
+                    w ? 64 : 32);
+    }
+    if (northward) {
+        FV3_REQUIRE(coeff[2].data && coeff[3].data, "center_rotate_winds: NULL northward coefficient");
+        const bool w = (coeff[2].f64 || wx) || (coeff[3].f64 || wy);
+        FV3_REQUIRE((north_f64 != 0) == w, "center_rotate_winds: northward must be float%d (numpy's promotion)",
+                    w ? 64 : 32);
+    }
+    a.east = eastward, a.north = northward, a.east_f64 = east_f64 != 0, a.north_f64 = north_f64 != 0;
+    hipLaunchKernelGGL(center_rotate_kernel, dim3(ew_grid(a.n)), dim3(256), 0, (hipStream_t)stream, a);
+    FV3_LAUNCH_CHECK();
+    return FV3_OK;
+}
+
+extern "C" int fv3_sum_squares(const void* const* in, const int* in_f64, int n_arr, int64_t n, double* out,
+                               void* stream)
+{
+    using namespace fv3;
+    clear_error();
+    FV3_REQUIRE(in && in_f64 && out && n_arr >= 1 && n_arr <= kMaxIn && n >= 0, "sum_squares: bad arguments");
+    SqArgs a{};
+    for (int j = 0; j < n_arr; ++j) {
+        FV3_REQUIRE(in[j] || n == 0, "sum_squares: input %d is NULL", j);
+        a.in[j] = in[j];
+        a.f64[j] = in_f64[j] != 0;
+    }
+    a.n_arr = n_arr, a.n = n;
+    hipStream_t s = (hipStream_t)stream;
+    double* partial = nullptr;
+    FV3_HIP(hipMallocAsync((void**)&partial, kSqBlocks * sizeof(double), s));
+    hipLaunchKernelGGL(sum_squares_stage1, dim3(kSqBlocks), dim3(256), 0, s, a, partial);
+    hipLaunchKernelGGL(sum_squares_stage2, dim3(1), dim3(256), 0, s, partial, kSqBlocks, out);
+    const hipError_t e = hipGetLastError();
+    FV3_HIP(hipFreeAsync(partial, s));
+    FV3_HIP(e);
+    return FV3_OK;
+}
+
+extern "C" int fv3_cos_zenith(int ndim, const int64_t* shape, fv3_strided lon, int lon_rad, fv3_strided lat,
+                              int lat_rad, const int64_t* time_stride, const double* terms, int64_t n_times,
+                              double* out, void* stream)
+{
+    using namespace fv3;
+    clear_error();
+    ZenArgs a{};
+    FV3_REQUIRE(shape_ok(ndim, shape, a.sh, a.n), "cos_zenith: 1..%d dims of size >= 0", FV3_MAX_DIMS);
+    if (a.n == 0) return FV3_OK;
+    FV3_REQUIRE(lon.data && lat.data && time_stride && terms && out && n_times >= 1, "cos_zenith: NULL operand");
+    a.lon = lon, a.lat = lat, a.lon_rad = lon_rad != 0, a.lat_rad = lat_rad != 0;
+    int64_t tmax = 0;
+    for (int d = 0; d < ndim; ++d) {
+        FV3_REQUIRE(time_stride[d] >= 0, "cos_zenith: negative time stride");
+        a.tst[d] = time_stride[d];
+        tmax += (shape[d] - 1) * time_stride[d];
+    }
+    FV3_REQUIRE(tmax < n_times, "cos_zenith: time strides address %lld of %lld time values", (long long)tmax + 1,
+                (long long)n_times);
+    a.terms = terms, a.nt = n_times, a.out = out;
+    hipLaunchKernelGGL(cos_zenith_kernel, dim3(ew_grid(a.n)), dim3(256), 0, (hipStream_t)stream, a);
     FV3_LAUNCH_CHECK();
     return FV3_OK;
 }

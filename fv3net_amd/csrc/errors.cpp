@@ -20,7 +20,7 @@ void clear_error() { g_err[0] = 0; }
 }  // namespace fv3
 
 extern "C" const char* fv3_last_error(void) { return g_err; }
-extern "C" int fv3_abi_version(void) { return 8; }
+extern "C" int fv3_abi_version(void) { return 9; }
 
 // "product": built by fv3net_amd/build.py with FV3_PRODUCT_BUILD and no experiment knob
 // (common.h refuses one); anything else is a tools/ variant.

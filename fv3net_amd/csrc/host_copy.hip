@@ -1,12 +1,16 @@
-// fv3net_amd — device-to-host copies as a kernel writing the caller's page-locked pages.
+// fv3net_amd — host <-> device copies of the drop-in call, and device-to-host copies as a
+// kernel storing into the library's page-locked arena (host_memory.cpp).
 //
 // The pipelined host call (DenseColumnModel.forward_host) overlaps the
 // inputs' host-to-device copies with the outputs' device-to-host copies.  Issued as two
 // copy-engine streams, the two directions overlapped in some runs and ran nearly in
 // sequence in others (the runtime's engine choice).  Here the out-copy is a kernel on the
-// compute stream that stores straight into the registered host pages over PCIe (16-byte
+// compute stream that stores straight into the arena's page-locked pages over PCIe (16-byte
 // vector stores), leaving the copy engines to the in-copies.
+#include <algorithm>
+
 #include "common.h"
+#include "host_memory.h"
 
 namespace fv3 {
 namespace {
@@ -27,17 +31,35 @@ __global__ __launch_bounds__(64) void copy_tail_kernel(const unsigned char* __re
 }  // namespace
 }  // namespace fv3
 
+extern "C" int fv3_host_copy(void* dst, const void* src, size_t bytes, int kind, void* stream)
+{
+    using namespace fv3;
+    clear_error();
+    FV3_REQUIRE(dst && src, "host_copy: NULL pointer");
+    FV3_REQUIRE(kind == 1 || kind == 2, "host_copy: kind %d (1: host to device, 2: device to host)", kind);
+    if (!bytes) return FV3_OK;
+    // arena memory: asynchronous DMA; anything else: the runtime's pageable copy, which it
+    // completes before returning (the caller's buffer is free on return)
+    FV3_HIP(hipMemcpyAsync(dst, src, bytes, kind == 1 ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost,
+                           (hipStream_t)stream));
+    return FV3_OK;
+}
+
 extern "C" int fv3_copy_to_host(void* host_dst, const void* dev_src, size_t bytes, void* stream)
 {
     using namespace fv3;
     clear_error();
     FV3_REQUIRE(host_dst && dev_src, "copy_to_host: NULL pointer");
     if (!bytes) return FV3_OK;
+    // only the library's own page-locked memory, which outlives the kernel (an arena block
+    // returns to the cache only when no array refers to it)
+    FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, hostmem::inside((uintptr_t)host_dst, bytes),
+                     "copy_to_host: host range not inside one fv3_host_alloc block");
     void* d = nullptr;
     const hipError_t e = hipHostGetDevicePointer(&d, host_dst, 0);
     if (e != hipSuccess || !d) {
         (void)hipGetLastError();
-        set_error("copy_to_host: host memory not page-locked / mapped (%s)", hipGetErrorString(e));
+        set_error("copy_to_host: host memory not mapped (%s)", hipGetErrorString(e));
         return FV3_ERR_UNSUPPORTED;
     }
     FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, ((uintptr_t)d % 16) == 0 && ((uintptr_t)dev_src % 16) == 0,
@@ -64,8 +86,8 @@ extern "C" int fv3_copy_to_host(void* host_dst, const void* dev_src, size_t byte
 // bytes, rows `spitch` / `dpitch` bytes apart.  A band of columns of a level-leading
 // [level][column] array is such a copy, one row per level (the pipelined host call over
 // column bands, bench.py predict + mappm host-to-host).  kind 1: host to device, 2:
-// device to host.  Host memory should be page-locked (fv3_host_register) for the copy
-// to be asynchronous.
+// device to host.  Asynchronous when the host rows are arena memory (fv3_host_alloc);
+// otherwise the runtime's pageable copy.
 extern "C" int fv3_copy_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height,
                            int kind, void* stream)
 {

@@ -105,6 +105,10 @@ class Dataset:
         if isinstance(key, (list, tuple)) and not (isinstance(key, tuple) and key in self._vars):
             return Dataset({k: self[k] for k in key}, coords=self.coords, attrs=self.attrs)
         if key not in self._vars:
+            if key in self.coords:  # a coordinate, as xarray's ds[name] gives it
+                c = self.coords[key]
+                return DataArray(c, (key,) if c.ndim == 1 else tuple(f"dim_{k}" for k in range(c.ndim)),
+                                 {key: c} if c.ndim == 1 else None, name=key)
             raise KeyError(key)
         da = self._vars[key]
         coords = {d: self.coords[d] for d in da.dims if d in self.coords}

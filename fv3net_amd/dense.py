@@ -12,7 +12,6 @@ Weights are held in Keras' own layout (kernel ``[fan_in, fan_out]``, bias
 import ctypes
 import dataclasses
 import os
-import warnings
 from typing import Dict, List, Mapping, Optional, Sequence, Tuple
 
 import numpy as np
@@ -373,9 +372,8 @@ class DenseColumnModel:
     def forward_host(self, arrays: Sequence, level_axes: Optional[Sequence[int]] = None,
                      precision: Optional[str] = None, out: Optional[Sequence[np.ndarray]] = None) -> List[np.ndarray]:
         """numpy inputs -> numpy float32 outputs (pure_keras.py:98-118 predicts on host
-        arrays).  The arrays' own pages are page-locked for the call
-        (``transfer.HostPages``: the copy engines DMA straight from and to them) and the
-        inputs land in device buffers of their own dtype (a float64 state is read in place
+        arrays).  The inputs cross as pageable copies or through the library's staging
+        blocks (``transfer.PinnedStager``; caller memory is never page-locked) and land in device buffers of their own dtype (a float64 state is read in place
         by the kernel), cached per shape with the bound kernel.
 
         Inputs with a common leading block axis (tiles: ``(tile, z, y, x)``, level axis
@@ -383,8 +381,9 @@ class DenseColumnModel:
         block b + 1's host-to-device copies, block b's predict and block b - 1's
         device-to-host copies overlap (PCIe is full duplex: in and out at once).  The
         same kernels on the same columns, so the outputs are bit-identical to one call.
-        ``out``: float32 numpy arrays to write (else fresh ones; a caller that reuses
-        them across calls saves first-touch page faults on the fresh pages)."""
+        ``out``: float32 numpy arrays to write, else arrays in the library's page-locked
+        arena (``transfer.empty_host``: DMA targets with no registration per call, their
+        pages reused once the caller drops them)."""
         from . import transfer
 
         arrays = [np.ascontiguousarray(a) for a in arrays]
@@ -410,63 +409,55 @@ class DenseColumnModel:
             self._host_call = ent
         _, bufs, runs, streams = ent
 
-        def src(a):
-            if a.flags.writeable:
-                return torch.from_numpy(a)
-            with warnings.catch_warnings():  # only read: torch's non-writable-array warning does not apply
-                warnings.simplefilter("ignore", UserWarning)
-                return torch.from_numpy(a)
-
-        with transfer.HostPages(arrays) as pages:
-            cur = torch.cuda.current_stream()
-            if streams is None:
-                for a, b in zip(arrays, bufs):
-                    b.copy_(src(a), non_blocking=True)
-                outs = runs[0]()
-                host = _host_outputs(out, [tuple(o.shape) for o in outs])
-                pages.add(host)
+        st = transfer.stager(bufs[0].device)
+        cur = torch.cuda.current_stream()
+        hcur = cur.cuda_stream
+        if streams is None:
+            for a, b in zip(arrays, bufs):
+                st.h2d(a, out=b, stream=cur)
+            outs = runs[0]()
+            host = _host_outputs(out, [tuple(o.shape) for o in outs])
+            for h, o in zip(host, outs):
+                transfer.host_copy(h, o, hcur)  # arena outputs: DMA; caller arrays: pageable
+            cur.synchronize()
+            return host
+        s_in, s_out = streams
+        s_in.wait_stream(cur)  # after whatever the caller queued on these buffers
+        s_out.wait_stream(cur)
+        host = None
+        lib = _native.load()
+        kernel_out = os.environ.get("FV3_D2H_KERNEL", "0") == "1"
+        self._last_kernel_out = False
+        for t in range(n0):
+            # block t's inputs: staged (host memcpy into arena blocks) or pageable copies,
+            # on s_in while the compute stream still runs block t - 1
+            for a, b in zip(arrays, bufs):
+                st.h2d(a[t], out=b[t], stream=s_in)
+            ev = torch.cuda.Event()
+            ev.record(s_in)
+            cur.wait_event(ev)
+            outs = runs[t](cur)
+            if host is None:
+                host = _host_outputs(out, [(n0,) + tuple(o.shape) for o in outs])
+                # FV3_D2H_KERNEL=1: out-copies as a kernel storing into the arena's pages
+                # on the compute stream (fv3_copy_to_host), the copy engines keeping the
+                # in-copies; default: the copy engines both ways
+                kernel_out = kernel_out and all(transfer.is_arena(h) for h in host)
+            done = False
+            if kernel_out:
+                done = all(lib.fv3_copy_to_host(h[t].ctypes.data, o.data_ptr(), o.numel() * 4, hcur) == 0
+                           for h, o in zip(host, outs))
+                kernel_out = done
+                self._last_kernel_out = done
+            if not done:
+                ev = torch.cuda.Event()
+                ev.record(cur)
+                s_out.wait_event(ev)
                 for h, o in zip(host, outs):
-                    torch.from_numpy(h).copy_(o, non_blocking=True)
-                return host  # HostPages synchronised the stream before releasing the pages
-            s_in, s_out = streams
-            s_in.wait_stream(cur)  # after whatever the caller queued on these buffers
-            s_out.wait_stream(cur)
-            ev_in = []
-            with torch.cuda.stream(s_in):
-                for t in range(n0):
-                    for a, b in zip(arrays, bufs):
-                        b[t].copy_(src(a[t]), non_blocking=True)
-                    ev = torch.cuda.Event()
-                    ev.record(s_in)
-                    ev_in.append(ev)
-            host = None
-            lib = _native.load()
-            hcur = cur.cuda_stream
-            kernel_out = os.environ.get("FV3_D2H_KERNEL", "0") == "1"
-            for t in range(n0):
-                cur.wait_event(ev_in[t])
-                outs = runs[t](cur)
-                if host is None:
-                    host = _host_outputs(out, [(n0,) + tuple(o.shape) for o in outs])
-                    pages.add(host)
-                    # FV3_D2H_KERNEL=1: out-copies as a kernel storing into the registered
-                    # host pages on the compute stream (fv3_copy_to_host), the copy engines
-                    # keeping the in-copies; default: the copy engines both ways
-                    kernel_out = kernel_out and all(pages.is_registered(h) for h in host)
-                done = False
-                if kernel_out:
-                    done = all(lib.fv3_copy_to_host(h[t].ctypes.data, o.data_ptr(), o.numel() * 4, hcur) == 0
-                               for h, o in zip(host, outs))
-                    kernel_out = done
-                if not done:
-                    ev = torch.cuda.Event()
-                    ev.record(cur)
-                    s_out.wait_event(ev)
-                    with torch.cuda.stream(s_out):
-                        for h, o in zip(host, outs):
-                            torch.from_numpy(h[t]).copy_(o, non_blocking=True)
-            cur.wait_stream(s_out)  # HostPages' exit synchronises the current stream
-            cur.wait_stream(s_in)
+                    transfer.host_copy(h[t], o, s_out.cuda_stream)
+        cur.wait_stream(s_out)
+        cur.wait_stream(s_in)
+        cur.synchronize()
         return host
 
     def _bind_or_forward(self, bufs, axes, precision):
@@ -518,7 +509,10 @@ class DenseColumnModel:
 
 def _host_outputs(out, shapes):
     if out is None:
-        return [np.empty(sh, np.float32) for sh in shapes]
+        from . import transfer
+
+        # page-locked arena blocks (reused once the caller drops them)
+        return [transfer.empty_host(sh, np.float32) for sh in shapes]
     out = list(out)
     if len(out) != len(shapes) or any(not (isinstance(o, np.ndarray) and o.dtype == np.float32 and o.shape == sh
                                            and o.flags.c_contiguous and o.flags.writeable)

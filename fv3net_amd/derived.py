@@ -9,12 +9,14 @@ Reference (paths under /root/reference/external):
                            entries :123-127, 264-410
 * ``DataTransform`` / ``ChainedDataTransform``          vcm/vcm/data_transform.py:15-370
 
-Every DerivedMapping entry is computed on the device except the solar zenith angle and
-the D-grid wind rotations (cos_zenith_angle, dQu/dQv, eastward/northward_wind and the
-wind-parallel projections): those are known by name, so the reference's ValueError for an
-unknown variable and its input bookkeeping stay exact, but computing one raises
-NotImplementedError.  Every DataTransform of the registry is mirrored.  Arithmetic keeps numpy's dtype flow (bit-identical to
-oracle/derived.py); device tensors stay on the device, host arrays come back as host arrays.
+Every DerivedMapping entry of derived_mapping.py is computed on the device, the D-grid wind
+rotation (dQu / dQv / eastward_wind / northward_wind, rotate.py:9-56 with coarsen.py:54-75's
+edge centring, one fused kernel) and the solar zenith angle (_zenith_angle.py: the
+per-time factors on the host, the per-point cosine on the device) included.  Every
+DataTransform of the registry is mirrored.  Arithmetic keeps numpy's dtype flow
+(bit-identical to oracle/derived.py; the zenith angle's sin / cos and the wind norm's
+summation order to rounding); device tensors stay on the device, host arrays come back
+as host arrays.
 """
 import ctypes
 import dataclasses
@@ -59,6 +61,7 @@ CLIMIT1, CLIMIT2 = 1.0e-3, 5.0e-2
 
 EW_ADD, EW_SUB, EW_IADD, EW_SCALE, EW_DIV_SCALAR, EW_MSE, EW_TEMP_TEND = 1, 2, 3, 4, 5, 6, 7
 EW_INCLOUD_TO_GRIDCELL, EW_GRIDCELL_TO_INCLOUD, EW_MUL, EW_ONE_MINUS_MUL, EW_ISCLOSE_ONEHOT = 8, 9, 10, 11, 12
+EW_SIGN_PARALLEL, EW_PROJECT = 13, 14
 COL_MASS_INTEGRAL, COL_TENDENCY_TO_FLUX, COL_IMPLIED_SURFACE_FLUX, COL_FLUX_TO_TENDENCY = 1, 2, 3, 4
 
 
@@ -306,24 +309,298 @@ class DerivedMapping(Mapping):
         return nonderived + maybe
 
 
-def _not_mirrored(name):
-    def f(self):
-        raise NotImplementedError(f"derived variable {name!r} is not computed by fv3net_amd (the mirrored "
-                                  "entries are the ones a dQ1/dQ2 model feeds)")
-    return f
+# --------------------------------------------------- D-grid wind rotation (rotate.py)
+EDGE_TO_CENTER_DIMS = {"x_interface": "x", "y_interface": "y"}  # rotate.py:7
+ROTATION_COEFFS = ("eastward_wind_u_coeff", "eastward_wind_v_coeff", "northward_wind_u_coeff",
+                   "northward_wind_v_coeff")
 
 
-# the reference registry by name (derived_mapping.py:114-192): entries that need the
-# solar zenith angle or the D-grid wind rotation (edge centering) are known, not computed
-for _name, _req, _nd in (
-        ("cos_zenith_angle", ["time", "lon", "lat"], False),
-        ("dQu", ["dQxwind", "dQywind"], True), ("dQv", ["dQxwind", "dQywind"], True),
-        ("eastward_wind", None, True), ("northward_wind", None, True),
-        ("dQu_parallel_to_eastward_wind", ["eastward_wind", "dQu"], False),
-        ("dQv_parallel_to_northward_wind", ["northward_wind", "dQv"], False),
-        ("horizontal_wind_tendency_parallel_to_horizontal_wind", ["eastward_wind", "dQu", "northward_wind", "dQv"],
-         False)):
-    DerivedMapping.register(_name, required_inputs=_req, use_nonderived_if_exists=_nd)(_not_mirrored(_name))
+def _strided(t, dims, out_dims, rename=None):
+    """fv3_strided of device tensor ``t`` (dims ``dims``) over a result with ``out_dims``:
+    its element stride per result dim (a dim renamed by ``rename`` {own: result} maps to
+    the result's), 0 where ``t`` lacks the dim."""
+    rename = rename or {}
+    own = {rename.get(d, d): k for k, d in enumerate(dims)}
+    st = [int(t.stride(own[d])) if d in own else 0 for d in out_dims]
+    return _native.Strided(t.data_ptr(), _f64(t), (ctypes.c_int64 * _native.MAX_DIMS)(*st))
+
+
+def _staggered_dim(da):
+    """coarsen.py:54-75's choice: the first of x_interface, y_interface that the array has."""
+    for dim in EDGE_TO_CENTER_DIMS:
+        if dim in da.dims:
+            return dim
+    raise ValueError("Variable to shift to center must be centered on one horizontal axis and edge-valued on the "
+                     "other.")
+
+
+def center_and_rotate_xy_winds(wind_rotation_matrix, x_component, y_component, ctx: _Ctx = None):
+    """vcm/cubedsphere/rotate.py:9-56 (with coarsen.py:54-75's centering): D-grid x/y winds
+    to A-grid (eastward, northward), one fused HIP kernel (fv3_center_rotate_winds):
+    0.5 * (e[j + 1] + e[j]) on each component's staggered dim, then the 2x2 rotation by the
+    grid's coefficients broadcast by dim name, in numpy's dtype flow.  Returns DataArrays
+    in the centred x component's dims (northward in the centred y component's)."""
+    ctx = ctx or _Ctx()
+    _device.require_gpu()
+    coeffs = [wind_rotation_matrix[name] for name in ROTATION_COEFFS]
+    sx, sy = _staggered_dim(x_component), _staggered_dim(y_component)
+    cx = tuple(EDGE_TO_CENTER_DIMS[d] if d == sx else d for d in x_component.dims)
+    cy = tuple(EDGE_TO_CENTER_DIMS[d] if d == sy else d for d in y_component.dims)
+    if len(set(cx)) != len(cx) or len(set(cy)) != len(cy):
+        raise ValueError(f"centring {x_component.dims} / {y_component.dims} repeats a dimension")
+    if set(cx) != set(cy):
+        raise ValueError(f"centred winds have different dims: {cx} vs {cy}")
+    sizes = {}
+    for da, stag, cd in ((x_component, sx, cx), (y_component, sy, cy)):
+        for d, c in zip(da.dims, cd):
+            n = da.sizes[d] - 1 if d == stag else da.sizes[d]
+            if sizes.setdefault(c, n) != n:
+                raise ValueError(f"conflicting sizes for dimension {c!r}: {n} vs {sizes[c]}")
+    for c in coeffs:
+        for d, n in c.sizes.items():
+            if d not in sizes:
+                raise ValueError(f"rotation coefficient dims {c.dims} not among the winds' {cx}")
+            if sizes[d] != n:
+                raise ValueError(f"conflicting sizes for dimension {d!r}: {n} vs {sizes[d]}")
+    if len(cx) > _native.MAX_DIMS:
+        raise NotImplementedError(f"more than {_native.MAX_DIMS} dims")
+    shape = tuple(sizes[d] for d in cx)
+    xt, yt = ctx.dev(x_component.data), ctx.dev(y_component.data)
+    ct = [ctx.dev(c.data) for c in coeffs]
+    ops_x = _strided(xt, x_component.dims, cx, {sx: EDGE_TO_CENTER_DIMS[sx]})
+    ops_y = _strided(yt, y_component.dims, cx, {sy: EDGE_TO_CENTER_DIMS[sy]})
+    ops_c = (_native.Strided * 4)(*[_strided(t, c.dims, cx) for t, c in zip(ct, coeffs)])
+    wx, wy = xt.dtype == torch.float64, yt.dtype == torch.float64
+    f64 = [t.dtype == torch.float64 for t in ct]
+    e_dt = torch.float64 if (f64[0] or wx or f64[1] or wy) else torch.float32
+    n_dt = torch.float64 if (f64[2] or wx or f64[3] or wy) else torch.float32
+    east = torch.empty(shape, dtype=e_dt, device=xt.device)
+    north = torch.empty(shape, dtype=n_dt, device=xt.device)
+    # every offset the kernel forms stays inside the operands (checked here: no launch
+    # with a stride that could leave an array)
+    for t, da, stag in ((xt, x_component, sx), (yt, y_component, sy)):
+        if t.shape[da.dims.index(stag)] < 1 or tuple(t.shape) != tuple(da.shape):
+            raise ValueError("wind data and dims disagree")
+    shp = (ctypes.c_int64 * len(shape))(*shape)
+    st = _native.load().fv3_center_rotate_winds(
+        len(shape), shp, ops_x, int(xt.stride(x_component.dims.index(sx))), ops_y,
+        int(yt.stride(y_component.dims.index(sy))), ops_c, east.data_ptr(), int(e_dt == torch.float64),
+        north.data_ptr(), int(n_dt == torch.float64), _device.stream_handle(None))
+    _native.check(st, "center_rotate_winds")
+    # coords: the rotation matrix's x / y (rotate.py:27-30), the winds' other coords
+    coords = {d: x_component.coords[d] for d in cx if d in x_component.coords and d not in ("x", "y")}
+    for c in coeffs:
+        for d in ("x", "y"):
+            if d in c.coords:
+                coords.setdefault(d, c.coords[d])
+    e_da = _da(ctx.back(east), cx, None, {})
+    e_da.coords.update({d: v for d, v in coords.items() if d in cx})
+    n_dev = north if cy == cx else north.permute(*[cx.index(d) for d in cy]).contiguous()
+    n_da = _da(ctx.back(n_dev), cy, None, {})
+    n_da.coords.update({d: v for d, v in coords.items() if d in cy})
+    return e_da, n_da
+
+
+def _rotate(self, x, y):
+    """derived_mapping.py:129-140."""
+    wind_rotation_matrix = self.dataset(list(ROTATION_COEFFS))
+    return center_and_rotate_xy_winds(wind_rotation_matrix, self[x], self[y])
+
+
+@DerivedMapping.register("dQu", required_inputs=["dQxwind", "dQywind"], use_nonderived_if_exists=True)
+def _dqu(self):
+    return _rotate(self, "dQxwind", "dQywind")[0]
+
+
+@DerivedMapping.register("dQv", required_inputs=["dQxwind", "dQywind"], use_nonderived_if_exists=True)
+def _dqv(self):
+    return _rotate(self, "dQxwind", "dQywind")[1]
+
+
+@DerivedMapping.register("eastward_wind", use_nonderived_if_exists=True)
+def _eastward_wind(self):
+    return _rotate(self, "x_wind", "y_wind")[0]
+
+
+@DerivedMapping.register("northward_wind", use_nonderived_if_exists=True)
+def _northward_wind(self):
+    return _rotate(self, "x_wind", "y_wind")[1]
+
+
+@DerivedMapping.register("dQu_parallel_to_eastward_wind", required_inputs=["eastward_wind", "dQu"])
+def _dqu_parallel(self):
+    # sign(eastward_wind / dQu) * abs(dQu) (derived_mapping.py:163-167)
+    return _ew_da(EW_SIGN_PARALLEL, [self["eastward_wind"], self["dQu"]])
+
+
+@DerivedMapping.register("dQv_parallel_to_northward_wind", required_inputs=["northward_wind", "dQv"])
+def _dqv_parallel(self):
+    return _ew_da(EW_SIGN_PARALLEL, [self["northward_wind"], self["dQv"]])
+
+
+@DerivedMapping.register("horizontal_wind_tendency_parallel_to_horizontal_wind",
+                         required_inputs=["eastward_wind", "dQu", "northward_wind", "dQv"])
+def _horizontal_parallel(self):
+    """derived_mapping.py:177-187: (E dQu + N dQv) / np.linalg.norm((E, N)), the norm of
+    BOTH whole arrays (one scalar: np.linalg.norm of the stacked pair, no axis)."""
+    E, dqu, N, dqv = self["eastward_wind"], self["dQu"], self["northward_wind"], self["dQv"]
+    ctx = _Ctx()
+    norm, norm64 = wind_norm(E, N, ctx)
+    return _ew_da(EW_PROJECT, [E, dqu, N, dqv], [norm, float(norm64)], ctx=ctx)
+
+
+def wind_norm(E, N, ctx: _Ctx = None):
+    """np.linalg.norm((E, N)) for two arrays of one shape: sqrt of the sum of squares of
+    every element, in promote(E, N) (a float32 pair gives a float32 norm).  The squares are
+    summed in float64 on the device (fv3_sum_squares, a fixed order): BLAS's dot order is
+    its own, so the norm agrees with numpy's to rounding, not bitwise.  Returns (norm as a
+    Python float, is_float64)."""
+    ctx = ctx or _Ctx()
+    _device.require_gpu()
+    if tuple(E.shape) != tuple(N.shape):
+        raise ValueError(f"setting an array element with a sequence: shapes {tuple(E.shape)} and {tuple(N.shape)}")
+    et, nt = ctx.dev(E.data).contiguous(), ctx.dev(N.data).contiguous()
+    w = et.dtype == torch.float64 or nt.dtype == torch.float64
+    out = torch.empty(1, dtype=torch.float64, device=et.device)
+    st = _native.load().fv3_sum_squares((ctypes.c_void_p * 2)(et.data_ptr(), nt.data_ptr()),
+                                        (ctypes.c_int * 2)(_f64(et), _f64(nt)), 2, et.numel(), out.data_ptr(),
+                                        _device.stream_handle(None))
+    _native.check(st, "sum_squares")
+    s = float(out.cpu().item())
+    return (float(np.sqrt(np.float64(s))) if w else float(np.sqrt(np.float32(s)))), w
+
+
+# ------------------------------------------------ solar zenith angle (_zenith_angle.py)
+RAD_PER_DEG = np.pi / 180.0
+
+
+def _days_from_2000(times) -> np.ndarray:
+    """_zenith_angle.py:96-112 for an array of datetime.datetime or Julian-calendar times
+    (cftime.DatetimeJulian; cftime is absent here: emulation.JulianTime): days since
+    2000-01-01 12:00 of the same calendar, float64 (microseconds / 86400e6)."""
+    import datetime
+
+    from .emulation import JulianTime
+
+    flat = np.asarray(times, dtype=object).ravel()
+    date_type = type(flat[0])
+    if date_type not in (datetime.datetime, JulianTime):
+        raise ValueError(f"model_time has an invalid date type. It must be either datetime.datetime or "
+                         f"cftime.DatetimeJulian. Got {date_type}.")
+    epoch = date_type(2000, 1, 1, 12, 0)
+    us = np.array([(t - epoch) // datetime.timedelta(microseconds=1) for t in flat], dtype=np.int64)
+    return us.astype(np.float64) / np.float64(86400000000)
+
+
+def solar_terms(times) -> np.ndarray:
+    """The time-dependent factors of _zenith_angle.py:115-244 per time value, float64
+    [4][n]: Greenwich mean sidereal time, the sun's right ascension, and the sine and
+    cosine of its declination.  A few numbers per time value, on the host in numpy (the
+    reference's own expressions); the per-point part runs in fv3_cos_zenith."""
+    days = _days_from_2000(times)
+    jc = days / 36525.0
+    theta = 67310.54841 + jc * (876600 * 3600 + 8640184.812866 + jc * (0.093104 - jc * 6.2 * 10e-6))
+    gmst = np.deg2rad(theta / 240.0) % (2 * np.pi)
+    mean_anomaly = np.deg2rad(357.52910 + 35999.05030 * jc - 0.0001559 * jc * jc - 0.00000048 * jc * jc * jc)
+    mean_longitude = np.deg2rad(280.46645 + 36000.76983 * jc + 0.0003032 * (jc ** 2))
+    d_l = np.deg2rad((1.914600 - 0.004817 * jc - 0.000014 * (jc ** 2)) * np.sin(mean_anomaly)
+                     + (0.019993 - 0.000101 * jc) * np.sin(2 * mean_anomaly) + 0.000290 * np.sin(3 * mean_anomaly))
+    eclon = mean_longitude + d_l
+    eps = np.deg2rad(23.0 + 26.0 / 60 + 21.406 / 3600.0
+                     - (46.836769 * jc - 0.0001831 * (jc ** 2) + 0.00200340 * (jc ** 3) - 0.576e-6 * (jc ** 4)
+                        - 4.34e-8 * (jc ** 5)) / 3600.0)
+    x = np.cos(eclon)
+    y = np.cos(eps) * np.sin(eclon)
+    z = np.sin(eps) * np.sin(eclon)
+    r = np.sqrt(1.0 - z * z)
+    dec = np.arctan2(z, r)
+    ra = 2 * np.arctan2(y, (x + r))
+    return np.stack([gmst, ra, np.sin(dec), np.cos(dec)]).astype(np.float64)
+
+
+def _is_rad(da) -> bool:
+    return isinstance(da, dsmod.DataArray) and "rad" in str(da.attrs.get("units", "")).lower()
+
+
+def cos_zenith_angle(time, lon, lat, ctx: _Ctx = None):
+    """vcm.cos_zenith_angle (_zenith_angle.py:54-93): float64 cosine of the solar zenith
+    angle at ``time`` (UTC: a datetime.datetime / Julian-calendar time, an array of them,
+    or a DataArray of them) for ``lon`` / ``lat`` in degrees (DataArrays whose units name
+    radians are converted, as _ensure_units_of_degrees).  DataArray inputs broadcast by
+    dim name like xr.apply_ufunc (the result's dims: time's, then lon's, then lat's new
+    ones) and give a DataArray named "cos_zenith_angle"; numpy inputs broadcast like
+    numpy.  The time factors come from the host (solar_terms), each point from
+    fv3_cos_zenith on the device."""
+    ctx = ctx or _Ctx()
+    _device.require_gpu()
+    as_da = isinstance(lon, dsmod.DataArray)
+    if as_da:
+        tda = time if isinstance(time, dsmod.DataArray) else None
+        parts = ([tda] if tda is not None else []) + [lon, lat]
+        dims: List[Hashable] = []
+        sizes = {}
+        for da in parts:
+            for d, n in da.sizes.items():
+                if d not in dims:
+                    dims.append(d)
+                    sizes[d] = n
+                elif sizes[d] != n:
+                    raise ValueError(f"conflicting sizes for dimension {d!r}: {n} vs {sizes[d]}")
+        shape = tuple(sizes[d] for d in dims)
+        tvals = np.asarray(tda.values if tda is not None else time, dtype=object)
+        tdims = tuple(tda.dims) if tda is not None else ()
+        lt, at = ctx.dev(lon.data), ctx.dev(lat.data)
+        lon_op, lat_op = _strided(lt, lon.dims, dims), _strided(at, lat.dims, dims)
+        tcont = np.ascontiguousarray(tvals)
+        tst = {d: tcont.strides[k] // tcont.itemsize for k, d in enumerate(tdims)}
+        tstride = [int(tst.get(d, 0)) for d in dims]
+    else:
+        larr, aarr = np.asarray(lon), np.asarray(lat)
+        if larr.dtype not in (np.float32, np.float64):
+            larr = larr.astype(np.float64)
+        if aarr.dtype not in (np.float32, np.float64):
+            aarr = aarr.astype(np.float64)
+        tvals = np.asarray(time, dtype=object)
+        shape = np.broadcast_shapes(tvals.shape, larr.shape, aarr.shape)
+        dims = list(range(len(shape))) or [0]
+        shape = shape or (1,)
+
+        def bstrides(a):
+            a = np.ascontiguousarray(a)
+            pad = len(shape) - a.ndim
+            return [0 if k < pad or a.shape[k - pad] == 1 else a.strides[k - pad] // a.itemsize
+                    for k in range(len(shape))], a
+
+        ls, larr = bstrides(larr)
+        as_, aarr = bstrides(aarr)
+        tstride, tcont = bstrides(tvals)
+        lt = torch.from_numpy(larr).cuda()
+        at = torch.from_numpy(aarr).cuda()
+        lon_op = _native.Strided(lt.data_ptr(), _f64(lt), (ctypes.c_int64 * _native.MAX_DIMS)(*ls))
+        lat_op = _native.Strided(at.data_ptr(), _f64(at), (ctypes.c_int64 * _native.MAX_DIMS)(*as_))
+    if len(shape) > _native.MAX_DIMS:
+        raise NotImplementedError(f"more than {_native.MAX_DIMS} dims")
+    terms = torch.from_numpy(np.ascontiguousarray(solar_terms(tcont))).cuda()
+    nt = int(terms.shape[1])
+    out = torch.empty(shape, dtype=torch.float64, device=lt.device)
+    st = _native.load().fv3_cos_zenith(
+        len(shape), (ctypes.c_int64 * len(shape))(*shape), lon_op, int(_is_rad(lon)), lat_op, int(_is_rad(lat)),
+        (ctypes.c_int64 * len(shape))(*tstride), terms.data_ptr(), nt, out.data_ptr(), _device.stream_handle(None))
+    _native.check(st, "cos_zenith")
+    if not as_da:
+        res = out.cpu().numpy()
+        return res.reshape(np.broadcast_shapes(np.asarray(time, dtype=object).shape, np.shape(lon), np.shape(lat)))
+    coords = {}
+    for da in parts:
+        for d, v in da.coords.items():
+            coords.setdefault(d, v)
+    return dsmod.DataArray(ctx.back(out), dims, coords, {"units": ""}, "cos_zenith_angle")
+
+
+@DerivedMapping.register("cos_zenith_angle", required_inputs=["time", "lon", "lat"])
+def _cos_zenith(self):
+    return cos_zenith_angle(self["time"], self["lon"], self["lat"])
+
 
 ALBEDO = "surface_diffused_shortwave_albedo"
 DSW_OVERRIDE = "override_for_time_adjusted_total_sky_downward_shortwave_flux_at_surface"

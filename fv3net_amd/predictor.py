@@ -298,8 +298,8 @@ class DenseColumnPredictor(Predictor):
     def _host_forward(self, arrays, axes):
         """Host arrays in, host float32 arrays out, for the drop-in call on numpy data
         (pure_keras.py:98-118 predicts on host arrays): ``DenseColumnModel.forward_host``
-        (the caller's pages page-locked for the copies, device buffers of the inputs' own
-        dtype cached per shape, tile blocks pipelined over three streams)."""
+        (device buffers of the inputs' own dtype cached per shape, outputs in the library's
+        page-locked arena, tile blocks pipelined over three streams)."""
         return self.model.forward_host(arrays, axes)
 
     # -- persistence ------------------------------------------------------------

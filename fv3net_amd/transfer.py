@@ -1,25 +1,29 @@
-"""Host <-> device copies of numpy arrays through pinned, double-buffered staging.
+"""Host <-> device copies of numpy arrays: the library's page-locked arena, pinned staging,
+or the runtime's pageable copies.
 
 The reference predicts on host arrays: ``PureKerasModel.predict`` stacks an xarray
 Dataset into numpy and returns numpy-backed outputs
 (external/fv3fit/fv3fit/keras/_models/shared/pure_keras.py:98-118), and the prognostic
 run hands the predictor host state every step.  On this path each call crosses PCIe
-twice.  A copy from pageable numpy memory goes through the driver's own bounce buffer
-one piece at a time; here the host side of the copy (numpy <-> pinned buffer, threads
-splitting each chunk) runs while the DMA of the previous chunk is in flight on a copy
-stream, so both directions run at the host-memcpy or PCIe rate, whichever is lower.
+twice.
 
-Arrays of 64 KiB and more are instead page-locked in place for the copy (HostPages,
-fv3_host_register): the copy engines DMA straight from / to the caller's memory with no
-host memcpy at all; the staging path remains for memory that cannot be registered.
+* Arrays handed back to the caller come from the library's page-locked arena
+  (``empty_host``, ``fv3_host_alloc``): DMA targets with no registration per call, their
+  pages reused (already faulted in) once the caller drops them.
+* Caller arrays are never page-locked (csrc/host_memory.cpp, DESIGN.md §3.7: round 4's
+  per-call registration of the caller's pages faulted later pageable copies).  Large ones
+  cross through staging blocks of the arena: the host side of the copy (numpy -> staging
+  block, threads splitting each chunk) runs while the DMA of the previous chunk is in
+  flight on a copy stream.  Smaller ones take the runtime's pageable copy, measured faster
+  there.  An arena array (``empty_host``) as input is DMA'd directly.
 
 Plumbing only: bytes are moved unchanged (float64 stays float64; the kernels that read
 float64 in place, or a device cast, do any conversion).
 """
 import concurrent.futures
+import ctypes
 import os
 import threading
-from typing import Optional
 
 import numpy as np
 
@@ -28,46 +32,131 @@ try:
 except ImportError:  # pragma: no cover - torch is part of the image
     torch = None
 
-_CHUNK = 16 << 20  # bytes per staging buffer
-_MIN_REGISTER = 64 << 10  # arrays from here on are page-locked for their copy (HostPages)
+_CHUNK = 16 << 20  # bytes per staging block
+_MIN_ARENA = 64 << 10  # d2h results from here on land in the arena
 _MIN_SPLIT = 1 << 20  # host copies below this run on the calling thread
 
 
-def register_enabled() -> bool:
-    """Whether HostPages page-locks the caller's arrays (``FV3_HOST_REGISTER=1``).
+def arena_enabled() -> bool:
+    """Whether host results go to the library's page-locked arena (default on;
+    ``FV3_HOST_ARENA=0``: plain numpy arrays and pageable copies)."""
+    return os.environ.get("FV3_HOST_ARENA", "1") != "0"
 
-    Off by default since the round-4 closing runs.  Two full GPU-test runs that exercised
-    the registered host path hit an illegal-address fault. One was in the usual test
-    order, before HostPages synchronised the device on exit. The other was with the test
-    files reversed: an H2D copy of an output array just after its pages were released.
-    Neither was reproduced in isolation, and the cause is not established (DESIGN.md
-    §3.7). With the switch off, host arrays cross through the pinned staging buffers or
-    as pageable copies, as in round 3.  The registered path stays available and tested."""
-    return os.environ.get("FV3_HOST_REGISTER", "0") == "1"
+
+def host_path() -> str:
+    """What the host boundary does now, for the bench records."""
+    if arena_enabled():
+        return ("arena: outputs DMA'd into the library's page-locked arena (reused across calls); inputs staged "
+                "through arena blocks (64 MiB and more) or pageable copies; no caller memory is page-locked")
+    return "pageable: FV3_HOST_ARENA=0, outputs in plain numpy arrays, pageable or staged copies"
+
+
+class _ArenaBlock:
+    """Owner of one ``fv3_host_alloc`` block, exported to numpy through the array
+    interface: the numpy array (and every view of it) keeps this object alive, and the
+    block returns to the library's cache when the last one is dropped."""
+
+    __slots__ = ("ptr", "__array_interface__", "__weakref__")
+
+    def __init__(self, ptr: int, shape, dtype: np.dtype):
+        self.ptr = ptr
+        self.__array_interface__ = {"data": (ptr, False), "shape": tuple(shape), "typestr": dtype.str,
+                                    "strides": None, "version": 3}
+
+    def __del__(self):
+        try:
+            _lib().fv3_host_free(self.ptr)
+        except Exception:  # pragma: no cover - interpreter shutdown
+            pass
+
+
+def _lib():
+    from . import _native
+
+    return _native.load()
+
+
+def empty_host(shape, dtype=np.float32) -> np.ndarray:
+    """An uninitialised C-contiguous numpy array in page-locked memory owned by the
+    library (``fv3_host_alloc``): the copy engines DMA into it asynchronously with no
+    registration per call, and its pages are reused (already faulted in) by a later array
+    of the same size once this one is dropped.  Plain ``np.empty`` when the arena is off
+    (``FV3_HOST_ARENA=0``) or cannot allocate."""
+    dtype = np.dtype(dtype)
+    shape = tuple(int(n) for n in (shape if isinstance(shape, (tuple, list)) else (shape,)))
+    nbytes = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
+    if nbytes == 0 or not arena_enabled():
+        return np.empty(shape, dtype)
+    p = ctypes.c_void_p()
+    if _lib().fv3_host_alloc(nbytes, ctypes.byref(p)) != 0 or not p.value:
+        return np.empty(shape, dtype)
+    return np.asarray(_ArenaBlock(p.value, shape, dtype))
+
+
+def is_arena(a) -> bool:
+    """Whether ``a`` (or the array it views) lives in an ``empty_host`` block."""
+    while isinstance(a, np.ndarray):
+        a = a.base
+    return isinstance(a, _ArenaBlock)
+
+
+def memory_stats() -> dict:
+    """The arena's counters: live / cached bytes and blocks (fv3_host_memory_stats)."""
+    st = (ctypes.c_uint64 * 3)()
+    _lib().fv3_host_memory_stats(st)
+    return {"arena_live": st[0], "arena_cached": st[1], "blocks": st[2]}
+
+
+def host_copy(dst, src, stream=None) -> None:
+    """One copy between a C-contiguous numpy array and a contiguous CUDA tensor of the same
+    byte size (either direction) on ``stream`` (torch stream, raw handle or None: the
+    current stream), ``fv3_host_copy``: asynchronous DMA when the host array is arena
+    memory (keep it alive and unchanged until the stream is done), else the runtime's
+    pageable copy, complete on return."""
+    from . import _device, _native
+
+    h2d = isinstance(src, np.ndarray)
+    host, dev = (src, dst) if h2d else (dst, src)
+    if not (isinstance(host, np.ndarray) and torch.is_tensor(dev) and dev.is_cuda):
+        raise ValueError("host_copy: one numpy array and one CUDA tensor")
+    if not (host.flags.c_contiguous and dev.is_contiguous()) or host.nbytes != dev.numel() * dev.element_size():
+        raise ValueError("host_copy: contiguous operands of the same byte size")
+    if host.nbytes == 0:
+        return
+    h = stream if isinstance(stream, int) else _device.stream_handle(stream, [dev])
+    if h2d:
+        st = _lib().fv3_host_copy(dev.data_ptr(), host.ctypes.data, host.nbytes, 1, h)
+    else:
+        st = _lib().fv3_host_copy(host.ctypes.data, dev.data_ptr(), host.nbytes, 2, h)
+    _native.check(st, "host_copy")
 
 
 class PinnedStager:
-    """Two pinned staging buffers, one copy stream, a small thread pool for the host
+    """Two staging blocks of the arena, one copy stream, a small thread pool for the host
     memcpy.  One instance per device (``stager()``); calls are serialised."""
 
     def __init__(self, device, chunk_bytes: int = _CHUNK, threads: int = 0, min_staged: int = None,
-                 min_register: Optional[int] = _MIN_REGISTER):
+                 min_arena: int = _MIN_ARENA):
         self.device = torch.device(device)
-        # arrays of this size and more are page-locked for their copy (None: never)
-        self.min_register = min_register
         self.chunk = int(chunk_bytes)
+        # d2h results of this size and more land in the arena (None: never)
+        self.min_arena = min_arena
         # below 4 chunks the driver's own pageable copy is faster (measured on the box:
         # a C48 float64 field, 8.7 MB, 22 GB/s pageable vs 19 staged; a C384 one, 560 MB,
         # 11 vs 46 GB/s)
         self.min_staged = 4 * self.chunk if min_staged is None else int(min_staged)
-        self._bufs = [torch.empty(self.chunk, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
-        self._host = [b.numpy() for b in self._bufs]
-        self._done = [None, None]  # event after the last DMA that used buffer i
+        self._host = [None, None]  # the staging blocks, allocated on first use
+        self._done = [None, None]  # event after the last DMA that used block i
         self._stream = torch.cuda.Stream(device=self.device)
         n = threads or min(8, os.cpu_count() or 1)
         self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=n) if n > 1 else None
         self._nthreads = n
         self._lock = threading.Lock()
+
+    def _block(self, b: int) -> np.ndarray:
+        if self._host[b] is None:
+            self._host[b] = empty_host((self.chunk,), np.uint8)
+        return self._host[b]
 
     def _memcpy(self, dst: np.ndarray, src: np.ndarray) -> None:
         """dst[:] = src for two uint8 vectors, split over the pool when large."""
@@ -81,9 +170,10 @@ class PinnedStager:
         for f in futs:
             f.result()
 
-    def h2d(self, arr, out=None):
-        """numpy array -> CUDA tensor of the same dtype and shape (``out`` if given:
-        a contiguous CUDA tensor of the same dtype and size)."""
+    def h2d(self, arr, out=None, stream=None):
+        """numpy array -> CUDA tensor of the same dtype and shape (``out`` if given: a
+        contiguous CUDA tensor of the same dtype and size), ordered on ``stream`` (default
+        the current one).  The caller may reuse ``arr`` as soon as this returns."""
         a = np.ascontiguousarray(arr)
         if out is None:
             out = torch.empty(a.shape, dtype=torch.from_numpy(a[:0].reshape(-1)).dtype, device=self.device)
@@ -92,59 +182,56 @@ class PinnedStager:
         nbytes = a.nbytes
         if nbytes == 0:
             return out
-        if self.min_register is not None and nbytes >= self.min_register:
-            # DMA straight from the caller's pages, registered for the copy: a C384 float64
-            # field in + a float32 one out, 18.4 ms staged -> 14.7 ms (tools/h2h_register.py)
-            with HostPages([a], self.min_register) as pages:
-                if pages.registered:
-                    out.view(-1).copy_(torch.from_numpy(a.reshape(-1)), non_blocking=True)
-                    return out  # leaving the block waits for the copy, then releases the pages
+        cur = stream if stream is not None else torch.cuda.current_stream(self.device)
+        if is_arena(a):  # page-locked already: one DMA
+            host_copy(out.view(-1), a.reshape(-1), cur.cuda_stream)
+            cur.synchronize()
+            return out
         if nbytes < self.min_staged:
-            out.view(-1).copy_(torch.from_numpy(a.reshape(-1)))
+            host_copy(out.view(-1), a.reshape(-1), cur.cuda_stream)  # the runtime's pageable copy
             return out
         src = a.reshape(-1).view(np.uint8)
         dst = out.view(-1).view(torch.uint8)
-        cur = torch.cuda.current_stream(self.device)
         with self._lock:
             self._stream.wait_stream(cur)  # `out` may have been allocated / used on cur
             for i, off in enumerate(range(0, nbytes, self.chunk)):
                 b = i & 1
                 if self._done[b] is not None:
-                    self._done[b].synchronize()  # the DMA reading this buffer is finished
+                    self._done[b].synchronize()  # the DMA reading this block is finished
                 n = min(self.chunk, nbytes - off)
-                self._memcpy(self._host[b][:n], src[off:off + n])
-                with torch.cuda.stream(self._stream):
-                    dst[off:off + n].copy_(self._bufs[b][:n], non_blocking=True)
-                    ev = torch.cuda.Event()
-                    ev.record(self._stream)
-                    self._done[b] = ev
+                blk = self._block(b)
+                self._memcpy(blk[:n], src[off:off + n])
+                host_copy(dst[off:off + n], blk[:n], self._stream.cuda_stream)
+                ev = torch.cuda.Event()
+                ev.record(self._stream)
+                self._done[b] = ev
             cur.wait_stream(self._stream)
         out.record_stream(self._stream)
         return out
 
     def d2h(self, t, out=None) -> np.ndarray:
-        """CUDA tensor -> numpy array of the same dtype and shape (``out`` if given)."""
+        """CUDA tensor -> numpy array of the same dtype and shape (``out`` if given; else an
+        arena array from ``min_arena`` bytes on).  Complete on return."""
         t = t.detach()
         if not t.is_contiguous():
             t = t.contiguous()
         if out is None:
-            out = np.empty(tuple(t.shape), dtype=torch.empty(0, dtype=t.dtype).numpy().dtype)
+            dt = torch.empty(0, dtype=t.dtype).numpy().dtype
+            nb = t.numel() * t.element_size()
+            out = (empty_host(tuple(t.shape), dt) if self.min_arena is not None and nb >= self.min_arena
+                   else np.empty(tuple(t.shape), dtype=dt))
         if not (out.flags.c_contiguous and out.nbytes == t.numel() * t.element_size()):
             raise ValueError("d2h: out must be a C-contiguous array of the tensor's size")
         nbytes = out.nbytes
         if nbytes == 0:
             return out
-        if self.min_register is not None and nbytes >= self.min_register:
-            with HostPages([out], self.min_register) as pages:
-                if pages.registered:
-                    torch.from_numpy(out.reshape(-1)).copy_(t.view(-1), non_blocking=True)
-                    return out
-        if nbytes < self.min_staged:
-            np.copyto(out.reshape(-1), t.view(-1).cpu().numpy())
+        cur = torch.cuda.current_stream(self.device)
+        if is_arena(out) or nbytes < self.min_staged:  # one DMA, or the runtime's pageable copy
+            host_copy(out.reshape(-1), t.view(-1), cur.cuda_stream)
+            cur.synchronize()
             return out
         src = t.view(-1).view(torch.uint8)
         dst = out.reshape(-1).view(np.uint8)
-        cur = torch.cuda.current_stream(self.device)
         offs = list(range(0, nbytes, self.chunk))
         with self._lock:
             self._stream.wait_stream(cur)  # the producer of `t` ran on cur
@@ -154,11 +241,10 @@ class PinnedStager:
                 if self._done[b] is not None:
                     self._done[b].synchronize()
                 n = min(self.chunk, nbytes - offs[i])
-                with torch.cuda.stream(self._stream):
-                    self._bufs[b][:n].copy_(src[offs[i]:offs[i] + n], non_blocking=True)
-                    ev = torch.cuda.Event()
-                    ev.record(self._stream)
-                    self._done[b] = ev
+                host_copy(self._block(b)[:n], src[offs[i]:offs[i] + n], self._stream.cuda_stream)
+                ev = torch.cuda.Event()
+                ev.record(self._stream)
+                self._done[b] = ev
 
             issue(0)
             for i in range(len(offs)):
@@ -170,66 +256,6 @@ class PinnedStager:
                 self._memcpy(dst[offs[i]:offs[i] + n], self._host[b][:n])
         t.record_stream(self._stream)
         return out
-
-
-class HostPages:
-    """``with HostPages(arrays) as p:`` page-locks the arrays' own memory
-    (fv3_host_register) so that copies on the current stream DMA straight from / to it,
-    with no bounce buffer and no host memcpy; ``p.add(more)`` registers more arrays in
-    the block.  On exit the device is synchronised (every copy issued in the block, on
-    any stream, is complete) and what was registered here is released.  Arrays below
-    ``min_bytes`` (sharing pages with other allocations) and arrays whose pages cannot
-    be registered are left as they are: copies from them are pageable copies, which
-    the runtime completes before returning."""
-
-    def __init__(self, arrays=(), min_bytes: int = 64 << 10, enable: Optional[bool] = None):
-        from . import _native
-
-        self._lib = _native.load()
-        self.min_bytes = int(min_bytes)
-        # None: the process-wide switch (register_enabled); False: register nothing
-        self.enable = register_enabled() if enable is None else bool(enable)
-        self._registered = []
-        self._pending = list(arrays)
-
-    @property
-    def registered(self) -> int:
-        """How many arrays this block registered."""
-        return len(self._registered)
-
-    def is_registered(self, a) -> bool:
-        """Whether this block page-locked ``a``'s memory."""
-        return isinstance(a, np.ndarray) and a.ctypes.data in self._registered
-
-    def add(self, arrays):
-        if not self.enable:
-            return
-        for a in arrays:
-            if not (isinstance(a, np.ndarray) and a.flags.c_contiguous) or a.nbytes < self.min_bytes:
-                continue
-            if any(a.ctypes.data == p for p in self._registered):
-                continue
-            if self._lib.fv3_host_register(a.ctypes.data, a.nbytes) == 0:
-                self._registered.append(a.ctypes.data)
-
-    def __enter__(self):
-        self.add(self._pending)
-        self._pending = []
-        return self
-
-    def __exit__(self, *exc):
-        try:
-            # the whole device, not only the current stream: a copy or kernel that a
-            # caller put on a side stream must not touch the pages after they are released
-            if self._registered:
-                torch.cuda.synchronize()
-            else:
-                torch.cuda.current_stream().synchronize()
-        finally:
-            for p in self._registered:
-                self._lib.fv3_host_unregister(p)
-            self._registered = []
-        return False
 
 
 _stagers = {}
@@ -248,8 +274,8 @@ def stager(device=None) -> PinnedStager:
         return s
 
 
-def h2d(arr, out=None, device=None):
-    return stager(device if device is not None else (out.device if out is not None else None)).h2d(arr, out)
+def h2d(arr, out=None, device=None, stream=None):
+    return stager(device if device is not None else (out.device if out is not None else None)).h2d(arr, out, stream)
 
 
 def d2h(t, out=None):
@@ -261,8 +287,10 @@ def copy_band(dst, src, stream=None):
     the same shape whose first axis (levels) is a fixed pitch apart and whose remaining
     axes are contiguous within each level: e.g. ``a[:, c0:c1]`` of a [level][column]
     array, a band of columns.  Host to device when ``src`` is numpy, else device to host;
-    enqueued on ``stream`` (a torch stream or None for the current one).  The host memory
-    should be page-locked (``HostPages``) for the copy to be asynchronous."""
+    enqueued on ``stream`` (a torch stream, a raw handle, or None for the current one; a
+    torch stream other than the current one first waits for the current one, a raw handle
+    does not).  Asynchronous when
+    the host array is arena memory (``empty_host``), else the runtime's pageable copy."""
     from . import _device, _native
 
     host, dev = (src, dst) if isinstance(src, np.ndarray) else (dst, src)
@@ -276,7 +304,7 @@ def copy_band(dst, src, stream=None):
     h_pitch = host.strides[0] if host.shape[0] > 1 else width
     d_pitch = dev.stride(0) * dev.element_size() if dev.shape[0] > 1 else width
     lib = _native.load()
-    h = _device.stream_handle(stream, [dev])
+    h = stream if isinstance(stream, int) else _device.stream_handle(stream, [dev])
     if host is src:
         st = lib.fv3_copy_2d(dev.data_ptr(), d_pitch, host.ctypes.data, h_pitch, width, host.shape[0], 1, h)
     else:

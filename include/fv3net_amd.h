@@ -55,7 +55,10 @@ int fv3_abi_version(void); /* bumped on any signature change (2: emulator fields
                               3: fv3_dense_forward_ex, 4: composites + Adapter,
                               5: per-operand dtypes in fv3_adapter_target, fv3_build_kind,
                               6: fv3_host_register / fv3_host_unregister,
-                              7: fv3_plan_*, 8: fv3_copy_to_host, fv3_copy_2d) */
+                              7: fv3_plan_*, 8: fv3_copy_to_host, fv3_copy_2d,
+                              9: fv3_host_alloc / free / copy, the arena, replace
+                                 fv3_host_register / unregister; wind rotation,
+                                 fv3_sum_squares, fv3_cos_zenith) */
 const char* fv3_build_kind(void); /* "product" (fv3net_amd/build.py, no experiment knob compiled in)
                                      or "experiment" (a tools/ variant: results may be invalid) */
 
@@ -539,7 +542,10 @@ int fv3_adapter_apply(const fv3_adapter_target* targets, int n_targets, int64_t 
  *                   in1 = condensate, p0 = climit1, p1 = climit2
  *   MUL             in0 * in1           ONE_MINUS_MUL   (1 - in0) * in1
  *   ISCLOSE_ONEHOT  where(isclose(in0, p0, rtol = p1, atol = p2), 1.0, 0.0), float64
- *                   (derived_mapping.py:194-262) */
+ *                   (derived_mapping.py:194-262)
+ *   SIGN_PARALLEL   sign(in0 / in1) * abs(in1)  (derived_mapping.py:163-174)
+ *   PROJECT         (in0 * in1 + in2 * in3) / p0, p0 in float64 if p1 != 0 else float32
+ *                   (derived_mapping.py:177-187; p0 the norm from fv3_sum_squares) */
 #define FV3_EW_ADD 1
 #define FV3_EW_SUB 2
 #define FV3_EW_IADD 3
@@ -552,6 +558,8 @@ int fv3_adapter_apply(const fv3_adapter_target* targets, int n_targets, int64_t 
 #define FV3_EW_MUL 10
 #define FV3_EW_ONE_MINUS_MUL 11
 #define FV3_EW_ISCLOSE_ONEHOT 12
+#define FV3_EW_SIGN_PARALLEL 13
+#define FV3_EW_PROJECT 14
 int fv3_derived_elementwise(int op, const void* const* in, const int* in_f64, int n_in, void* out, int out_f64,
                             int64_t n, const double* params, int n_params, void* stream);
 
@@ -581,21 +589,72 @@ typedef struct fv3_field {
 int fv3_derived_columns(int op, const fv3_field* in, int n_in, const fv3_field* out, int n_out, int64_t ncol, int nz,
                         const double* params, int n_params, void* stream);
 
-/*
- * Page-lock / release a caller's host array so that H2D / D2H copies DMA straight from
- * and to its pages (the drop-in call's host boundary, pure_keras.py:98-118 takes and
- * returns host arrays).  fv3_host_register returns FV3_ERR_UNSUPPORTED (runtime error
- * state cleared) when the pages cannot be registered, e.g. already registered or shared
- * with another registered array: copy through staging then.  Unregister only what this
- * call registered, after the copies using it have completed.
- */
-int fv3_host_register(void* ptr, size_t bytes);
-int fv3_host_unregister(void* ptr);
+/* A float32 / float64 operand addressed by element strides over the dims of a result of
+ * `ndim` <= FV3_MAX_DIMS dims (stride 0: broadcast along that dim, as xarray aligns
+ * operands by dim name). */
+#define FV3_MAX_DIMS 6
+typedef struct fv3_strided {
+    const void* data;
+    int f64;
+    int64_t stride[FV3_MAX_DIMS];
+} fv3_strided;
 
-/* Copy `bytes` of device memory into page-locked host memory (fv3_host_register'ed or
- * pinned) with a kernel on `stream` that stores into the host pages over PCIe, instead of
- * a copy engine: the pipelined host call's out-copies, beside the copy engines' in-copies
- * (DESIGN.md §3.7).  FV3_ERR_UNSUPPORTED when the host memory is not page-locked or the
+/* D-grid x/y winds (or wind tendencies) to A-grid eastward/northward
+ * (vcm/cubedsphere/rotate.py:9-56 center_and_rotate_xy_winds, coarsen.py:54-75
+ * shift_edge_var_to_center; derived_mapping.py:130-160 dQu / dQv / eastward_wind /
+ * northward_wind).  The result has `shape` (the centered dims, contiguous outputs):
+ *   xc = 0.5 * (x[i + x_stag] + x[i])   (x's dtype; x_stag: the stride of x's staggered
+ *   yc = 0.5 * (y[i + y_stag] + y[i])    dim, the edge one past the cell),
+ *   eastward  = coeff[0] * xc + coeff[1] * yc,  northward = coeff[2] * xc + coeff[3] * yc
+ * coeff = eastward_wind_u_coeff, eastward_wind_v_coeff, northward_wind_u_coeff,
+ * northward_wind_v_coeff; numpy's dtype flow (each product in its operands' promoted
+ * dtype, the sum in the products'), bit-identical to the numpy expressions.  `eastward` /
+ * `northward` may be NULL (not wanted); their dtypes must be the promoted ones. */
+int fv3_center_rotate_winds(int ndim, const int64_t* shape, fv3_strided x_wind, int64_t x_stag, fv3_strided y_wind,
+                            int64_t y_stag, const fv3_strided* coeff, void* eastward, int east_f64, void* northward,
+                            int north_f64, void* stream);
+
+/* sum over the n_arr arrays of n contiguous elements each of x^2, accumulated in float64
+ * in a fixed order (deterministic), into *out (device, one double): the square of
+ * np.linalg.norm((a, b)) (derived_mapping.py:184). */
+int fv3_sum_squares(const void* const* in, const int* in_f64, int n_arr, int64_t n, double* out, void* stream);
+
+/* Cosine of the solar zenith angle (vcm/calc/_zenith_angle.py:54-244, derived_mapping.py:
+ * 114-120) over a result of `shape`: lon / lat in degrees (or radians when *_rad != 0:
+ * np.rad2deg first, as _ensure_units_of_degrees), the time-dependent terms precomputed
+ * on the host per time value into `terms` (device, float64 [4][n_times]: Greenwich mean
+ * sidereal time, right ascension, sin and cos of the declination), `time_stride`
+ * the element strides of the time index over the result's dims.  float64 out:
+ *   sin(lat r) sin(dec) + cos(lat r) cos(dec) cos((gmst + lon r) - ra),  r = pi / 180,
+ * lon r / lat r and their sine / cosine in the operand's dtype (numpy's flow). */
+int fv3_cos_zenith(int ndim, const int64_t* shape, fv3_strided lon, int lon_rad, fv3_strided lat, int lat_rad,
+                   const int64_t* time_stride, const double* terms, int64_t n_times, double* out, void* stream);
+
+/*
+ * Host memory of the drop-in call (pure_keras.py:98-118 takes and returns host arrays;
+ * csrc/host_memory.cpp).  No reference counterpart: transport only.  The
+ * library page-locks only memory it allocates itself (never a caller's array).
+ *
+ * fv3_host_alloc: a page-locked, page-aligned host block (hipHostMalloc) owned by the
+ * library, cached after fv3_host_free for reuse by a later fv3_host_alloc of the same
+ * page-rounded size: the arrays a host call hands back, and staging.
+ * fv3_host_arena_limit sets the cached bytes kept (default 8 GiB; beyond it blocks are
+ * released).  stats[3]: live bytes, cached bytes, blocks.
+ *
+ * fv3_host_copy: one host <-> device copy on `stream` (kind 1: host to device, 2: device
+ * to host): asynchronous DMA for arena memory, the runtime's pageable copy (complete on
+ * return) otherwise.
+ */
+int fv3_host_alloc(size_t bytes, void** out);
+int fv3_host_free(void* ptr);
+int fv3_host_arena_limit(size_t cached_bytes);
+int fv3_host_memory_stats(uint64_t* stats);
+int fv3_host_copy(void* dst, const void* src, size_t bytes, int kind, void* stream);
+
+/* Copy `bytes` of device memory into host memory of this library (inside one
+ * fv3_host_alloc block) with a kernel on `stream` that stores
+ * into the host pages over PCIe, instead of a copy engine: the pipelined host call's out-copies, beside the copy engines' in-copies
+ * (DESIGN.md §3.7).  FV3_ERR_UNSUPPORTED when the host range is not such memory or the
  * buffers are not 16-byte aligned (the caller copies with hipMemcpyAsync instead).  No
  * reference counterpart: a transport detail of the drop-in call (pure_keras.py:98-118). */
 int fv3_copy_to_host(void* host_dst, const void* dev_src, size_t bytes, void* stream);
@@ -603,7 +662,8 @@ int fv3_copy_to_host(void* host_dst, const void* dev_src, size_t bytes, void* st
 /* Pitched copy between host and device on `stream` (hipMemcpy2DAsync): `height` rows of
  * `width` bytes, `spitch` / `dpitch` bytes apart; kind 1 host to device, 2 device to
  * host.  A column band of a [level][column] array, one row per level: the pipelined
- * host call over column bands.  No reference counterpart (transport). */
+ * host call over column bands.  Asynchronous for arena rows (fv3_host_alloc), the
+ * runtime's pageable copy otherwise.  No reference counterpart (transport). */
 int fv3_copy_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height, int kind,
                 void* stream);
 

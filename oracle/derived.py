@@ -249,3 +249,149 @@ def apply_transform(name, ds, **kw):
     else:
         raise NotImplementedError(name)
     return ds
+
+
+# ---------------------------------------------------------------------------------
+# D-grid wind rotation (vcm/cubedsphere/rotate.py:9-56, coarsen.py:54-75) and the
+# wind-parallel projections (derived_mapping.py:129-187).  Pinned by the reference KATs
+# external/vcm/tests/test__rotate.py:7-34 (rotate_xy_winds at 45 degrees),
+# test_derived_mapping.py:86-90 (zero coefficients) and :33-58 (projection cases).
+# Arrays carry their dims explicitly: (ndarray, dims); coefficients broadcast by name.
+# ---------------------------------------------------------------------------------
+EDGE_TO_CENTER_DIMS = {"x_interface": "x", "y_interface": "y"}
+
+
+def shift_edge_var_to_center(a, dims):
+    """coarsen.py:54-75: 0.5 * (edge + edge.shift(1)) without the first edge, along the
+    first of x_interface / y_interface the array has; returns (array, centred dims)."""
+    for d in EDGE_TO_CENTER_DIMS:
+        if d in dims:
+            ax = dims.index(d)
+            n = a.shape[ax]
+            hi = np.take(a, np.arange(1, n), axis=ax)
+            lo = np.take(a, np.arange(0, n - 1), axis=ax)
+            return 0.5 * (hi + lo), tuple(EDGE_TO_CENTER_DIMS[x] if x == d else x for x in dims)
+    raise ValueError("Variable to shift to center must be centered on one horizontal axis and edge-valued on the "
+                     "other.")
+
+
+def _bcast(a, dims, out_dims):
+    """``a`` (dims ``dims``) transposed and expanded to ``out_dims`` (a view)."""
+    own = [d for d in out_dims if d in dims]
+    a = np.transpose(a, [dims.index(d) for d in own])
+    shape = [a.shape[own.index(d)] if d in dims else 1 for d in out_dims]
+    return a.reshape(shape)
+
+
+def rotate_xy_winds(coeffs, xc, yc, dims):
+    """rotate.py:40-56: eastward = eu xc + ev yc, northward = nu xc + nv yc (numpy's
+    promotion), in ``dims`` (xc and yc already in them).  coeffs: 4 (array, dims)."""
+    c = [_bcast(a, d, dims) for a, d in coeffs]
+    east = c[0] * xc + c[1] * yc
+    north = c[2] * xc + c[3] * yc
+    shape = np.broadcast_shapes(xc.shape, yc.shape)
+    return np.broadcast_to(east, shape).copy(), np.broadcast_to(north, shape).copy()
+
+
+def center_and_rotate_xy_winds(coeffs, x, x_dims, y, y_dims):
+    """rotate.py:9-37: both components centred, then rotated; results in the centred x
+    component's dims (northward transposed to the centred y component's)."""
+    xc, cx = shift_edge_var_to_center(x, tuple(x_dims))
+    yc, cy = shift_edge_var_to_center(y, tuple(y_dims))
+    yc_in_x = np.transpose(yc, [cy.index(d) for d in cx])
+    east, north = rotate_xy_winds(coeffs, xc, yc_in_x, cx)
+    return (east, cx), (np.transpose(north, [cx.index(d) for d in cy]).copy(), cy)
+
+
+def parallel_to_wind(wind, tendency):
+    """derived_mapping.py:163-174: sign(wind / tendency) * abs(tendency)."""
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return np.sign(wind / tendency) * abs(tendency)
+
+
+def horizontal_wind_tendency_parallel_to_horizontal_wind(E, dQu, N, dQv):
+    """derived_mapping.py:177-187 (np.linalg.norm of the stacked pair: one scalar)."""
+    return (E * dQu + N * dQv) / np.linalg.norm((E, N))
+
+
+# ---------------------------------------------------------------------------------
+# Solar zenith angle (vcm/calc/_zenith_angle.py:54-244).  Pinned by the reference KATs
+# external/vcm/tests/test__zenith_angle.py:9-90 (twelve points, the invalid-calendar
+# ValueError, the DataArray name and the radian-units conversion).  Times are
+# datetime.datetime (proleptic Gregorian) or JulianDate (the Julian calendar that
+# cftime.DatetimeJulian holds; cftime is absent here).
+# ---------------------------------------------------------------------------------
+RAD_PER_DEG = np.pi / 180.0
+
+
+class JulianDate:
+    """A Julian-calendar date whose differences are exact timedeltas (the part of
+    cftime.DatetimeJulian _days_from_2000 uses)."""
+
+    def __init__(self, year, month, day, hour=0, minute=0, second=0):
+        self.year, self.month, self.day, self.hour, self.minute, self.second = year, month, day, hour, minute, second
+
+    def _seconds(self):
+        a = (14 - self.month) // 12
+        y = self.year + 4800 - a
+        m = self.month + 12 * a - 3
+        jdn = self.day + (153 * m + 2) // 5 + 365 * y + y // 4 - 32083
+        return ((jdn * 24 + self.hour) * 60 + self.minute) * 60 + self.second
+
+    def __sub__(self, other):
+        import datetime
+
+        return datetime.timedelta(seconds=self._seconds() - other._seconds())
+
+
+def days_from_2000(model_time, julian_types=(JulianDate,)):
+    import datetime
+
+    flat = np.asarray(model_time, dtype=object).ravel()
+    date_type = type(flat[0])
+    if date_type not in (datetime.datetime,) + tuple(julian_types):
+        raise ValueError(f"model_time has an invalid date type. It must be either datetime.datetime or "
+                         f"cftime.DatetimeJulian. Got {date_type}.")
+    epoch = date_type(2000, 1, 1, 12, 0)
+    diff = np.array([t - epoch for t in flat], dtype=object).reshape(np.shape(model_time))
+    return np.asarray(diff).astype("timedelta64[us]") / np.timedelta64(1, "D")
+
+
+def _gmst(days):
+    jc = days / 36525.0
+    theta = 67310.54841 + jc * (876600 * 3600 + 8640184.812866 + jc * (0.093104 - jc * 6.2 * 10e-6))
+    return np.deg2rad(theta / 240.0) % (2 * np.pi)
+
+
+def _sun_ecliptic_longitude(days):
+    jc = days / 36525.0
+    mean_anomaly = np.deg2rad(357.52910 + 35999.05030 * jc - 0.0001559 * jc * jc - 0.00000048 * jc * jc * jc)
+    mean_longitude = np.deg2rad(280.46645 + 36000.76983 * jc + 0.0003032 * (jc ** 2))
+    d_l = np.deg2rad((1.914600 - 0.004817 * jc - 0.000014 * (jc ** 2)) * np.sin(mean_anomaly)
+                     + (0.019993 - 0.000101 * jc) * np.sin(2 * mean_anomaly) + 0.000290 * np.sin(3 * mean_anomaly))
+    return mean_longitude + d_l
+
+
+def _obliquity_star(jc):
+    return np.deg2rad(23.0 + 26.0 / 60 + 21.406 / 3600.0
+                      - (46.836769 * jc - 0.0001831 * (jc ** 2) + 0.00200340 * (jc ** 3) - 0.576e-6 * (jc ** 4)
+                         - 4.34e-8 * (jc ** 5)) / 3600.0)
+
+
+def _right_ascension_declination(days):
+    eps = _obliquity_star(days / 36525.0)
+    eclon = _sun_ecliptic_longitude(days)
+    x = np.cos(eclon)
+    y = np.cos(eps) * np.sin(eclon)
+    z = np.sin(eps) * np.sin(eclon)
+    r = np.sqrt(1.0 - z * z)
+    return 2 * np.arctan2(y, (x + r)), np.arctan2(z, r)
+
+
+def cos_zenith_angle(model_time, lon, lat, julian_types=(JulianDate,)):
+    """_zenith_angle.py:54-93, 225-244 for numpy inputs (degrees), broadcast like numpy."""
+    days = days_from_2000(model_time, julian_types)
+    lon_rad, lat_rad = lon * RAD_PER_DEG, lat * RAD_PER_DEG
+    ra, dec = _right_ascension_declination(days)
+    h_angle = _gmst(days) + lon_rad - ra
+    return np.sin(lat_rad) * np.sin(dec) + np.cos(lat_rad) * np.cos(dec) * np.cos(h_angle)

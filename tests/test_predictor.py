@@ -165,12 +165,12 @@ def test_dense_predictor_end_to_end(gpu):
 
 
 @pytest.mark.gpu
-def test_dense_predictor_host_arrays_page_locked_path(gpu):
-    """numpy inputs take the host-call path (the caller's pages registered for the call,
-    DMA straight to device buffers kept per shape, the bound kernel, DMA back into new
-    numpy arrays): bit-identical to the device-resident predict on the float32 values,
-    for float64 and float32 arrays, read-only arrays, repeated calls (fresh outputs each
-    call), a shape change, and arrays too small to register."""
+def test_dense_predictor_host_arrays_arena_path(gpu):
+    """numpy inputs take the host-call path (copies to device buffers kept per shape, the
+    bound kernel, DMA back into arrays of the library's page-locked arena):
+    bit-identical to the device-resident predict on the float32 values, for float64 and
+    float32 arrays, read-only arrays, repeated calls (fresh outputs each call), a shape
+    change, and small arrays."""
     import torch
 
     from fv3net_amd import transfer
@@ -211,19 +211,13 @@ def test_dense_predictor_host_arrays_page_locked_path(gpu):
     T32, q32 = T.astype(np.float32), q.astype(np.float32)
     for g, r in zip(host(T32, q32), ref):
         assert (g.view(np.uint32) == r.view(np.uint32)).all()
-    # another shape (a smaller rank subdomain), then arrays below the registration size
+    # another shape (a smaller rank subdomain), then small arrays
     for shape in ((79, 24, 48), (79, 4, 5)):
         Ts, qs = T[:, :shape[1], :shape[2]].copy(), q[:, :shape[1], :shape[2]].copy()
         for g, r in zip(host(Ts, qs), device_ref(Ts, qs)):
             assert (g.view(np.uint32) == r.view(np.uint32)).all(), shape
-    # the registration helper: pages released on exit, a second registration refused cleanly
-    a = np.zeros(1 << 20)
-    with transfer.HostPages([a], enable=True) as p:
-        assert len(p._registered) == 1
-        with transfer.HostPages([a], enable=True) as p2:  # already registered: left alone
-            assert p2._registered == []
-    with transfer.HostPages([a], enable=True) as p:  # released above, registrable again
-        assert len(p._registered) == 1
+    # outputs of the numpy path live in the library's page-locked arena
+    assert transfer.is_arena(first[0]) and transfer.is_arena(again[1])
     torch.cuda.synchronize()
 
 
@@ -278,7 +272,7 @@ def test_forward_host_tile_pipeline_bit_identical(gpu, dtype, kernel_out, monkey
     pipelined over three streams (threshold lowered so a C12 state takes the path) give
     the bits of the device-resident forward of the same values, on repeated calls, with
     fresh outputs each call; the out-copies by the fv3_copy_to_host kernel into the
-    registered pages (FV3_D2H_KERNEL=1) or by the copy engines (0); a level-leading array
+    arena pages (FV3_D2H_KERNEL=1) or by the copy engines (0); a level-leading array
     (no block axis) takes the one-call path."""
     import torch
 
@@ -297,6 +291,8 @@ def test_forward_host_tile_pipeline_bit_identical(gpu, dtype, kernel_out, monkey
     a = m.forward_host([T, q], [1, 1])
     b = m.forward_host([T, q], [1, 1])
     assert m._host_call[3] is not None  # the pipelined path
+    # fresh outputs live in the page-locked arena, so FV3_D2H_KERNEL=1 takes the kernel
+    assert m._last_kernel_out == (kernel_out == "1")
     assert a[0] is not b[0]
     for x, y, r in zip(a, b, ref):
         assert x.shape == r.shape and x.dtype == np.float32

@@ -7,16 +7,16 @@ import pytest
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [np.float32, np.float64, np.uint8, np.int64])
-@pytest.mark.parametrize("register", [None, 1 << 13])
-def test_round_trip_bit_exact(gpu, dtype, register):
-    """Both host paths: pinned staging (register None) and the caller's pages registered
-    for the copy (arrays of 8 KiB and more here; small ones stay pageable copies)."""
+@pytest.mark.parametrize("arena", [None, 1 << 13])
+def test_round_trip_bit_exact(gpu, dtype, arena):
+    """Every host path: staging through arena blocks, pageable copies, and results in arena
+    arrays (from 8 KiB here) or plain ones (arena None)."""
     import torch
 
     from fv3net_amd import transfer
 
     st = transfer.PinnedStager(torch.device("cuda", 0), chunk_bytes=1 << 16, threads=4, min_staged=1 << 12,
-                               min_register=register)
+                               min_arena=arena)
     rng = np.random.default_rng(3)
     for n in (0, 1, 1000, (1 << 16) // np.dtype(dtype).itemsize, 3 * (1 << 16) + 17, 1 << 20):
         a = (rng.normal(0, 1e3, n) if np.dtype(dtype).kind == "f" else rng.integers(0, 200, n)).astype(dtype)
@@ -67,23 +67,26 @@ def test_predict_mappm_host_to_host_matches_device_resident(gpu):
 @pytest.mark.gpu
 @pytest.mark.parametrize("nbytes", [16, 4096, 4100, 1 << 20, (1 << 20) + 7])
 def test_copy_to_host_kernel(gpu, nbytes):
-    """fv3_copy_to_host: a kernel storing device bytes into registered host pages (16-byte
-    vector stores and a byte tail) gives the bytes; unregistered host memory is refused
-    with FV3_ERR_UNSUPPORTED (the caller then uses the copy engines)."""
+    """fv3_copy_to_host: a kernel storing device bytes into the library's page-locked host
+    memory (16-byte vector stores and a byte tail) gives the bytes, into an arena block;
+    a misaligned arena address or a range past the block is refused, and memory outside
+    the arena (a plain array) is refused with FV3_ERR_UNSUPPORTED (the caller then uses the
+    copy engines)."""
     import torch
 
-    from fv3net_amd import _native
-    from fv3net_amd.transfer import HostPages
+    from fv3net_amd import _native, transfer
 
     lib = _native.load()
     src = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda")
-    host = np.zeros(max(nbytes, 1 << 16), np.uint8)  # >= HostPages' 64 KiB minimum
-    with HostPages([host], min_bytes=0, enable=True) as pages:
-        assert pages.is_registered(host)
-        st = lib.fv3_copy_to_host(host.ctypes.data, src.data_ptr(), nbytes, torch.cuda.current_stream().cuda_stream)
-        assert st == 0, st
-    assert np.array_equal(host[:nbytes], src.cpu().numpy())
-    assert not host[nbytes:].any()
+    h = torch.cuda.current_stream().cuda_stream
+    arena = transfer.empty_host((max(nbytes, 1 << 16),), np.uint8)
+    arena[:] = 0
+    assert transfer.is_arena(arena)
+    assert lib.fv3_copy_to_host(arena.ctypes.data, src.data_ptr(), nbytes, h) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(arena[:nbytes], src.cpu().numpy()) and not arena[nbytes:].any()
+    assert lib.fv3_copy_to_host(arena[1:].ctypes.data, src.data_ptr(), nbytes, h) == _native.FV3_ERR_UNSUPPORTED
+    torch.cuda.synchronize()
     plain = np.zeros(nbytes, np.uint8)
     assert lib.fv3_copy_to_host(plain.ctypes.data, src.data_ptr(), nbytes, 0) == _native.FV3_ERR_UNSUPPORTED
 
@@ -92,8 +95,8 @@ def test_copy_to_host_kernel(gpu, nbytes):
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_copy_band_pitched_both_ways(gpu, dtype):
     """transfer.copy_band: a band of columns of a [level][column] numpy array to the same
-    band of a device array and back (one pitched copy each, registered pages and plain
-    ones), other columns untouched; mismatched shapes and non-contiguous levels refused."""
+    band of a device array and back (one pitched copy each), other columns untouched;
+    mismatched shapes and non-contiguous levels refused."""
     import torch
 
     from fv3net_amd import transfer
@@ -102,13 +105,12 @@ def test_copy_band_pitched_both_ways(gpu, dtype):
     a = rng.normal(size=(79, 3000)).astype(dtype)
     d = torch.zeros((79, 3000), dtype=torch.from_numpy(a[:0]).dtype, device="cuda")
     back = np.full_like(a, -1)
-    with transfer.HostPages([a, back]):
-        transfer.copy_band(d[:, 512:1536], a[:, 512:1536])
-        transfer.copy_band(back[:, 512:1536], d[:, 512:1536])
+    transfer.copy_band(d[:, 512:1536], a[:, 512:1536])
+    transfer.copy_band(back[:, 512:1536], d[:, 512:1536])
     assert np.array_equal(d[:, 512:1536].cpu().numpy(), a[:, 512:1536])
     assert (d[:, :512] == 0).all() and (d[:, 1536:] == 0).all()
     assert np.array_equal(back[:, 512:1536], a[:, 512:1536]) and (back[:, :512] == -1).all()
-    small = np.ascontiguousarray(a[:3, :5])  # unregistered pages: a synchronous copy
+    small = np.ascontiguousarray(a[:3, :5])  # pageable memory: a synchronous copy
     transfer.copy_band(d[:3, :5], small)
     torch.cuda.synchronize()
     assert np.array_equal(d[:3, :5].cpu().numpy(), small)
