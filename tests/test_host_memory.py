@@ -150,7 +150,7 @@ def test_host_path_sequence_of_the_r04z5_fault(gpu):
         up = torch.from_numpy(got[1]).cuda()  # a pageable (or arena) copy of the output's pages
         back = (up * 2).cpu().numpy()
         assert (back == got[1] * 2).all()
-        del got, up, back, Tc, qc, outs
+        del got, up, back, Tc, qc, outs, g  # g: the comparison loop's last output
         if it % 5 == 0:
             gc.collect()
     gc.collect()
