@@ -329,8 +329,15 @@ def test_derived_model_dqu_dqv_over_dense_predictors(gpu, tmp_path, device):
         yaml.safe_dump({"models": [str(tmp_path / k) for k in "abc"]}, f)
     with open(comb / "name", "w") as f:
         f.write("combined_output_model")
-    P.dump(DerivedModel(P.load(str(comb)), ["dQu", "dQv"]), str(tmp_path / "derived"))
-    model = P.load(str(tmp_path / "derived"))
+    # combined_output_model has no dump (models.py:19-62), so the derived model's yaml is
+    # written by hand as well, pointing at it
+    der = tmp_path / "derived"
+    der.mkdir()
+    with open(der / "derived_model.yaml", "w") as f:
+        yaml.safe_dump({"model": str(comb), "derived_output_variables": ["dQu", "dQv"]}, f)
+    with open(der / "name", "w") as f:
+        f.write("derived_model")
+    model = P.load(str(der))
     assert isinstance(model, DerivedModel)
     conv = (lambda v: torch.from_numpy(v).cuda()) if device else (lambda v: v)
     arr = {"Ta": rng.normal(260, 15, (NZ, n + 1, n)), "qa": rng.uniform(0, 0.02, (NZ, n + 1, n)),
