@@ -303,55 +303,85 @@ def _dense(inputs, output, seed):
     return P.DenseColumnPredictor(cfg.input_variables, cfg.output_variables, m)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("device", [True, False])
-def test_derived_model_dqu_dqv_over_dense_predictors(gpu, tmp_path, device):
-    """A derived_model of dQu / dQv over a combined_output_model of two mi355x-dense
-    predictors (dQxwind on the y-staggered grid, dQywind on the x-staggered one) and a
-    constant predictor of the rotation coefficients, loaded through the registry:
-    dQu / dQv are the oracle's centre-and-rotate of the direct predictions, bit for bit."""
-    import torch
+def _write(path, name, config_file, config):
     import yaml
 
-    from fv3net_amd.derived import DerivedModel
+    path.mkdir()
+    with open(path / config_file, "w") as f:
+        yaml.safe_dump(config, f)
+    with open(path / "name", "w") as f:
+        f.write(name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("device", [True, False])
+def test_dqu_dqv_from_dense_predictions_on_staggered_grids(gpu, device):
+    """Two mi355x-dense predictors, one on the y-staggered grid predicting dQxwind, one on
+    the x-staggered grid predicting dQywind (each sees its own Dataset: PureKerasModel.predict
+    stacks every dim of its input, pure_keras.py:110, so one model cannot take both grids),
+    merged with the grid's rotation coefficients into a DerivedMapping, as the prognostic
+    run's derived state does: dQu / dQv are the oracle's centre-and-rotate of the
+    predictions, bit for bit, and the predictions pass through unchanged."""
+    import torch
+
+    from fv3net_amd.derived import DerivedMapping
+    from fv3net_amd.stepper import merge
 
     n = 24
     rng = np.random.default_rng(3)
     a, b = _dense(["Ta", "qa"], "dQxwind", 1), _dense(["Tb", "qb"], "dQywind", 2)
-    c = P.ConstantOutputPredictor(["grid"], list(COEFFS))
-    c.set_outputs(eastward_wind_u_coeff=0.8, eastward_wind_v_coeff=-0.6, northward_wind_u_coeff=0.6,
-                  northward_wind_v_coeff=0.8)
-    for name, m in (("a", a), ("b", b), ("c", c)):
-        P.dump(m, str(tmp_path / name))
-    comb = tmp_path / "combined"
-    comb.mkdir()
-    with open(comb / "combined_output_model.yaml", "w") as f:
-        yaml.safe_dump({"models": [str(tmp_path / k) for k in "abc"]}, f)
-    with open(comb / "name", "w") as f:
-        f.write("combined_output_model")
-    # combined_output_model has no dump (models.py:19-62), so the derived model's yaml is
-    # written by hand as well, pointing at it
-    der = tmp_path / "derived"
-    der.mkdir()
-    with open(der / "derived_model.yaml", "w") as f:
-        yaml.safe_dump({"model": str(comb), "derived_output_variables": ["dQu", "dQv"]}, f)
-    with open(der / "name", "w") as f:
-        f.write("derived_model")
-    model = P.load(str(der))
-    assert isinstance(model, DerivedModel)
     conv = (lambda v: torch.from_numpy(v).cuda()) if device else (lambda v: v)
-    arr = {"Ta": rng.normal(260, 15, (NZ, n + 1, n)), "qa": rng.uniform(0, 0.02, (NZ, n + 1, n)),
-           "Tb": rng.normal(260, 15, (NZ, n, n + 1)), "qb": rng.uniform(0, 0.02, (NZ, n, n + 1))}
-    X = D.Dataset({k: D.DataArray(conv(v), ["z", "y_interface", "x"] if k[-1] == "a" else ["z", "y", "x_interface"])
-                   for k, v in arr.items()})
-    X["grid"] = D.DataArray(conv(np.zeros((n, n))), ["y", "x"])
+    Xa = D.Dataset({k: D.DataArray(conv(rng.normal(260, 15, (NZ, n + 1, n)) if k == "Ta" else
+                                        rng.uniform(0, 0.02, (NZ, n + 1, n))), ["z", "y_interface", "x"])
+                    for k in ("Ta", "qa")})
+    Xb = D.Dataset({k: D.DataArray(conv(rng.normal(260, 15, (NZ, n, n + 1)) if k == "Tb" else
+                                        rng.uniform(0, 0.02, (NZ, n, n + 1))), ["z", "y", "x_interface"])
+                    for k in ("Tb", "qb")})
+    coeffs = [rng.uniform(-1, 1, (n, n)) for _ in COEFFS]
+    rot = D.Dataset({k: D.DataArray(conv(c), ["y", "x"]) for k, c in zip(COEFFS, coeffs)})
+    xw, yw = a.predict(Xa)["dQxwind"], b.predict(Xb)["dQywind"]
+    dm = DerivedMapping(merge([D.Dataset({"dQxwind": xw, "dQywind": yw}), rot]))
+    (e, ed), (nn, nd) = OD.center_and_rotate_xy_winds([(c, ("y", "x")) for c in coeffs], xw.values, xw.dims,
+                                                      yw.values, yw.dims)
+    got_u, got_v = dm["dQu"], dm["dQv"]
+    assert got_u.dims == ed and got_v.dims == nd
+    _bits(got_u.values, e, "dQu")
+    _bits(got_v.values, nn, "dQv")
+    _bits(dm["dQxwind"].values, xw.values, "dQxwind passes through")
+
+
+@pytest.mark.gpu
+def test_derived_model_dqu_dqv_through_the_registry(gpu, tmp_path):
+    """derived_model(dQu, dQv) over a combined_output_model loaded by path (yaml + name
+    files, models.py:19-62, 110-220): members predicting dQxwind on the y-staggered grid,
+    dQywind on the x-staggered grid and the rotation coefficients on cell centres
+    (constant-output predictors, which stack only their own inputs, testing.py:70-73).
+    dQu / dQv equal the oracle's centre-and-rotate of the members' predictions, bit for
+    bit, on host arrays."""
+    from fv3net_amd.derived import DerivedModel
+
+    n = 6
+    rng = np.random.default_rng(8)
+    members = []
+    for name, inp, outs in (("u", "u_grid", {"dQxwind": rng.normal(0, 1e-3, NZ)}),
+                            ("v", "v_grid", {"dQywind": rng.normal(0, 1e-3, NZ)}),
+                            ("c", "grid", dict(zip(COEFFS, (0.8, -0.6, 0.6, 0.8))))):
+        m = P.ConstantOutputPredictor([inp], list(outs))
+        m.set_outputs(**outs)
+        P.dump(m, str(tmp_path / name))
+        members.append(str(tmp_path / name))
+    _write(tmp_path / "combined", "combined_output_model", "combined_output_model.yaml", {"models": members})
+    _write(tmp_path / "derived", "derived_model", "derived_model.yaml",
+           {"model": str(tmp_path / "combined"), "derived_output_variables": ["dQu", "dQv"]})
+    model = P.load(str(tmp_path / "derived"))
+    assert isinstance(model, DerivedModel) and {"dQu", "dQv"} <= set(model.output_variables)
+    X = D.Dataset({"u_grid": D.DataArray(np.zeros((n + 1, n)), ["y_interface", "x"]),
+                   "v_grid": D.DataArray(np.zeros((n, n + 1)), ["y", "x_interface"]),
+                   "grid": D.DataArray(np.zeros((n, n)), ["y", "x"])})
     out = model.predict(X)
-    xw = a.predict(X)["dQxwind"]
-    yw = b.predict(X)["dQywind"]
-    xv, yv = xw.values, yw.values
-    coeffs = [(np.full((n, n), v), ("y", "x")) for v in (0.8, -0.6, 0.6, 0.8)]
-    (e, ed), (nn, nd) = OD.center_and_rotate_xy_winds(coeffs, xv, xw.dims, yv, yw.dims)
+    xw, yw = out["dQxwind"], out["dQywind"]
+    coeffs = [(out[k].transpose("y", "x").values, ("y", "x")) for k in COEFFS]
+    (e, ed), (nn, nd) = OD.center_and_rotate_xy_winds(coeffs, xw.values, xw.dims, yw.values, yw.dims)
     assert out["dQu"].dims == ed and out["dQv"].dims == nd
     _bits(out["dQu"].values, e, "dQu")
     _bits(out["dQv"].values, nn, "dQv")
-    _bits(out["dQxwind"].values, xv, "dQxwind passes through")
