@@ -347,6 +347,16 @@ def load():
     return _lib
 
 
+def variant(name: str):
+    """A kernel-variant selector from the environment (A/B runs and the tests that pin every
+    variant): ``os.environ[name]``, but only while ``FV3_VARIANTS=1``; otherwise None, so the
+    product path is the same under any environment (the C side reads its selectors the
+    same way, csrc/common.h ``variant_env``)."""
+    if os.environ.get("FV3_VARIANTS") != "1":
+        return None
+    return os.environ.get(name)
+
+
 def check(status: int, what: str = ""):
     """Map a C-ABI status to the reference's exception types."""
     if status == FV3_OK:

@@ -824,14 +824,14 @@ int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* f
     // FV3_COARSEN_CURSOR=1 selects the scratch-free output-driven path for A/B)
     // FV3_COARSEN_PATH = cells (default for f >= 2) | rows (the f-wave row-segment
     // blocks with a per-lane scratch column) | cursor (rows, scratch-free cursor remap)
-    const char* path = getenv("FV3_COARSEN_PATH");
-    const bool cursor = (path && path[0] == 'c' && path[1] == 'u') || getenv("FV3_COARSEN_CURSOR");
+    const char* path = fv3::variant_env("FV3_COARSEN_PATH");
+    const bool cursor = (path && path[0] == 'c' && path[1] == 'u') || fv3::variant_env("FV3_COARSEN_CURSOR");
     const bool cells = !cursor && factor >= 2 && !(path && path[0] == 'r');
     void* scratch = nullptr;
     if (cells) {
         // fields remapped NF = 2 at a time (one streaming pass shares the pressure work;
         // FV3_COARSEN_NF=1 for A/B)
-        const char* nfe = getenv("FV3_COARSEN_NF");
+        const char* nfe = fv3::variant_env("FV3_COARSEN_NF");
         const int NF = (n_fields >= 2 && !(nfe && nfe[0] == '1')) ? 2 : 1;
         const int ff = factor * factor, G = 64 / ff;
         const int CH = std::min(8, 64 / (G * factor));
@@ -922,7 +922,7 @@ int regrid_coarsen_edge_impl(const DT* delp, const float* spacing, const float* 
     const size_t lds = sizeof(DT) * (size_t)C * (km + 1);
     hipStream_t s = (hipStream_t)stream;
     void* scratch = nullptr;  // per-lane remapped columns (see regrid_coarsen_impl)
-    if (n_fields > 0 && !getenv("FV3_COARSEN_CURSOR"))
+    if (n_fields > 0 && !fv3::variant_env("FV3_COARSEN_CURSOR"))
         FV3_HIP(hipMallocAsync(&scratch, sizeof(float) * (size_t)km * (size_t)blocks * 64, s));
     a.scratch = (float*)scratch;
     if (scratch)

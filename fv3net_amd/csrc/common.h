@@ -35,6 +35,11 @@ namespace fv3 {
 void set_error(const char* fmt, ...);
 void clear_error();
 
+// A kernel-variant selector (A/B builds' knobs and the tests that pin every variant
+// bit-identical): the value of environment variable `name`, but only while FV3_VARIANTS=1
+// is set; otherwise NULL, so the product path is the same under any environment.
+const char* variant_env(const char* name);
+
 #define FV3_REQUIRE(cond, ...)                     \
     do {                                           \
         if (!(cond)) {                             \

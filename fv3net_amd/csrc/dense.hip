@@ -1075,7 +1075,7 @@ extern "C" int fv3_dense_create(const fv3_dense_desc* d, fv3_dense_model** out)
         total += (p.bytes + 255) / 256 * 256;
     }
     size_t alloc = total;
-    if (const char* e = getenv("FV3_DENSE_PAD_MB")) alloc = std::max(alloc, (size_t)atoi(e) << 20);
+    if (const char* e = fv3::variant_env("FV3_DENSE_PAD_MB")) alloc = std::max(alloc, (size_t)atoi(e) << 20);
     FV3_HIP(hipMalloc(&m->dbuf, alloc));
     for (auto& p : pcs)
         if (p.bytes) FV3_HIP(hipMemcpy((char*)m->dbuf + p.off, p.src, p.bytes, hipMemcpyHostToDevice));
@@ -1207,7 +1207,7 @@ static int dense_forward_impl(const fv3_dense_model* m, const void* const* input
     // biases per hidden layer at width 256) runs 16-column tiles
     const bool fits2 = lds_of(2) <= 160 * 1024;
     int nc = (wide && m->w1_off8 < 0) || !fits2 ? 1 : 2;
-    if (const char* e = getenv("FV3_DENSE_NC")) nc = atoi(e) == 1 || !fits2 ? 1 : 2;
+    if (const char* e = fv3::variant_env("FV3_DENSE_NC")) nc = atoi(e) == 1 || !fits2 ? 1 : 2;
     // waves per block: 8, two per SIMD on one tile and each wave half the hidden units,
     // measured faster than 4 at every size after the staging work (C48 42.8 vs 47.9 us,
     // C96 141 vs 147 us, C384 2.15 vs 2.18 ms).  Needs 32-column tiles and width >= 128.
@@ -1223,7 +1223,7 @@ static int dense_forward_impl(const fv3_dense_model* m, const void* const* input
         }
     }
     int nw = 8;
-    if (const char* e = getenv("FV3_DENSE_NW")) nw = atoi(e) == 8 ? 8 : 4;
+    if (const char* e = fv3::variant_env("FV3_DENSE_NW")) nw = atoi(e) == 8 ? 8 : 4;
     if (nc == 1 || m->w1_off8 < 0) nw = 4;
     const int nt = 64 * nw;
     if (nw == 8) {
@@ -1268,7 +1268,7 @@ static int dense_forward_impl(const fv3_dense_model* m, const void* const* input
                              "dense_forward: input %d spans more than 2^32 elements", a.slot_meta[q] >> 27);
             fast = fast && fdst % fps == 0;
         }
-        if (getenv("FV3_DENSE_SLOWSTAGE")) fast = false;  // A/B
+        if (fv3::variant_env("FV3_DENSE_SLOWSTAGE")) fast = false;  // A/B
         a.fast_stage = fast;
     }
     hipStream_t s = (hipStream_t)stream;
@@ -1280,7 +1280,7 @@ static int dense_forward_impl(const fv3_dense_model* m, const void* const* input
     // (waves per SIMD targeted by register allocation, weight ring depth):
     // FV3_DENSE_CFG = "3,2" (default) | "2,3" | "4,2" (A/B)
     int wpe = 3, rd = 2;  // measured best at C48 and C384
-    if (const char* e = getenv("FV3_DENSE_CFG")) {
+    if (const char* e = fv3::variant_env("FV3_DENSE_CFG")) {
         if (!strcmp(e, "2,3")) wpe = 2, rd = 3;
         else if (!strcmp(e, "4,2")) wpe = 4, rd = 2;
     }
@@ -1320,9 +1320,9 @@ static int dense_forward_impl(const fv3_dense_model* m, const void* const* input
         resident.push_back({kfn, lds, res});
     }
     int64_t grid = std::min<int64_t>(a.ntiles, (int64_t)res * n_cu);
-    if (const char* e = getenv("FV3_DENSE_GRID")) grid = std::min<int64_t>(a.ntiles, std::max(1, atoi(e)));
+    if (const char* e = fv3::variant_env("FV3_DENSE_GRID")) grid = std::min<int64_t>(a.ntiles, std::max(1, atoi(e)));
     a.prio = 0;
-    if (const char* e = getenv("FV3_DENSE_PRIO")) a.prio = std::max(0, std::min(3, atoi(e)));
+    if (const char* e = fv3::variant_env("FV3_DENSE_PRIO")) a.prio = std::max(0, std::min(3, atoi(e)));
     void* kargs[] = {&a};
     FV3_HIP(hipLaunchKernel(kfn, dim3((unsigned)grid), dim3(nt), kargs, lds, s));
     FV3_LAUNCH_CHECK();

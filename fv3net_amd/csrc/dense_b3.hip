@@ -1345,7 +1345,7 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
     }
 
     // FV3_B3_STAGE=glds / reg: the LDS-DMA or the register-staged pipeline (A/B)
-    const char* stg_env = getenv("FV3_B3_STAGE");
+    const char* stg_env = fv3::variant_env("FV3_B3_STAGE");
     static std::mutex mu;
     static int n_cu = 0;
     {
@@ -1359,7 +1359,7 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
     // 4-wave blocks of 64 columns where 128-column tiles would leave CUs idle (C48: 108
     // tiles of 128 on 256 CUs -> 216 of 64); FV3_B3_WAVES=4|8 forces one (A/B)
     int nwv = (ncol + kB3Cols - 1) / kB3Cols < n_cu ? 4 : 8;
-    if (const char* e = getenv("FV3_B3_WAVES")) nwv = atoi(e) == 4 ? 4 : 8;
+    if (const char* e = fv3::variant_env("FV3_B3_WAVES")) nwv = atoi(e) == 4 ? 4 : 8;
     const int nthr = 64 * nwv, ncols = 16 * nwv;
     a.ntiles = (ncol + ncols - 1) / ncols;
     auto lds_of = [&](int sl) {
@@ -1376,7 +1376,7 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
     // cross a column block; 16-byte epilogue accesses when every output / residual row is
     // 16-byte aligned.  FV3_B3_TR=0 keeps the row-per-lane epilogue (A/B, tests).
     bool tr = sl > 0 && (nb >= ncol || nb % 4 == 0);
-    if (const char* e = getenv("FV3_B3_TR")) tr = tr && atoi(e) != 0;
+    if (const char* e = fv3::variant_env("FV3_B3_TR")) tr = tr && atoi(e) != 0;
     {
         bool vec = true;
         auto al = [&](const void* ptr, const fv3_layout& l) {
@@ -1432,7 +1432,7 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
         }
     }
     int64_t grid = std::min<int64_t>(a.ntiles, (int64_t)res * n_cu);
-    if (const char* e = getenv("FV3_B3_GRID")) grid = std::min<int64_t>(a.ntiles, std::max(1, atoi(e)));
+    if (const char* e = fv3::variant_env("FV3_B3_GRID")) grid = std::min<int64_t>(a.ntiles, std::max(1, atoi(e)));
     void* kargs[] = {&a};
     FV3_HIP(hipLaunchKernel(kfn, dim3((unsigned)grid), dim3(nthr), kargs, lds, (hipStream_t)stream));
     FV3_LAUNCH_CHECK();

@@ -1,6 +1,7 @@
 // fv3net_amd — thread-local error text for the C ABI (never throws across it).
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -17,6 +18,11 @@ void set_error(const char* fmt, ...)
     va_end(ap);
 }
 void clear_error() { g_err[0] = 0; }
+const char* variant_env(const char* name)
+{
+    const char* on = getenv("FV3_VARIANTS");
+    return (on && on[0] == '1' && on[1] == 0) ? getenv(name) : nullptr;
+}
 }  // namespace fv3
 
 extern "C" const char* fv3_last_error(void) { return g_err; }

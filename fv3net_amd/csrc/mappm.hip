@@ -412,14 +412,14 @@ const void* cs_global_kernel(const MappmArgs& a, int64_t nlanes)
 {
     const int64_t ncol = a.ncol;
     int nt = ncol < 262144 ? 48 : 0;
-    if (const char* e = getenv("FV3_MAPPM_CS_NT")) nt = atoi(e);
+    if (const char* e = fv3::variant_env("FV3_MAPPM_CS_NT")) nt = atoi(e);
     // load distance (tools/mappm_pf_ab.py; C384 79 -> 79 kord 10, buffer operations):
     // before the rolling subgrid flags (profiles/r04l_mappm_pf.log) 884,736 columns PF =
     // 0 / 2 / 4 / 8 0.909 / 0.761 / 0.798 / 0.836 ms (64-bit addresses, PF = 0: 0.871),
     // 110,592 columns (register tail) 0.224 / 0.185 / 0.182 / 0.182 ms; with them
     // (profiles/r04q_mappm_kord_ab.log) PF = 2 / 4 0.772 / 0.765 ms and 0.175 / 0.170 ms
     int pf = 4;
-    if (const char* e = getenv("FV3_MAPPM_CS_PF")) pf = atoi(e);
+    if (const char* e = fv3::variant_env("FV3_MAPPM_CS_PF")) pf = atoi(e);
     // 32-bit lane byte offsets when every column offset (and the scratch) fits
     // buffer operations at 32-bit byte offsets when every array (and the scratch) spans
     // < 4 GiB: the last column's offset plus km levels
@@ -430,7 +430,7 @@ const void* cs_global_kernel(const MappmArgs& a, int64_t nlanes)
         return 4 * (off + (int64_t)nlev * l.ld) < (1ll << 32) - 4;
     };
     bool c32 = fits(a.l_pe1, a.km + 1) && fits(a.l_q1, a.km) && 4 * nlanes * 2 * (int64_t)(a.km + 3) < (1ll << 32) - 4;
-    if (const char* e = getenv("FV3_MAPPM_CS_C32")) c32 = c32 && atoi(e) != 0;
+    if (const char* e = fv3::variant_env("FV3_MAPPM_CS_C32")) c32 = c32 && atoi(e) != 0;
 #define FV3_CS_PF(NT_, C_)                                                        \
     switch (pf) {                                                                 \
     case 0: return (const void*)mappm_cs_global_kernel<NT_, 0, C_>;               \
@@ -442,7 +442,7 @@ const void* cs_global_kernel(const MappmArgs& a, int64_t nlanes)
     // specialised for it (0.170 -> 0.168 ms at 110,592 columns; on the full grid the
     // specialised build measured slower, 0.772 -> 0.806 ms at PF = 2, so it is not used
     // there; profiles/r04q_mappm_kord_ab.log).  FV3_MAPPM_CS_KORD=0: the generic column.
-    const char* ke = getenv("FV3_MAPPM_CS_KORD");
+    const char* ke = fv3::variant_env("FV3_MAPPM_CS_KORD");
     if (c32 && nt == 48 && pf == 4 && (a.kord == 10 || a.kord == -10) && !(ke && atoi(ke) == 0))
         return (const void*)mappm_cs_global_kernel<48, 4, true, 10>;
     if (c32) {
@@ -461,7 +461,7 @@ const void* cs_global_kernel(const MappmArgs& a, int64_t nlanes)
 // mostly idle (FV3_MAPPM_PATH=serial|levels overrides, for tests and A/B).
 bool use_levels_kernel(const MappmArgs& a)
 {
-    const char* p = getenv("FV3_MAPPM_PATH");
+    const char* p = fv3::variant_env("FV3_MAPPM_PATH");
     if (p && p[0] == 's') return false;
     if (a.km > 1000 || a.kn > 1000) return false;
     if (p && p[0] == 'l') return true;
@@ -471,7 +471,7 @@ bool use_levels_kernel(const MappmArgs& a)
 int launch_mappm(MappmArgs a, hipStream_t stream)
 {
     if (a.ncol == 0) return FV3_OK;
-    if (a.kord > 7 && !getenv("FV3_MAPPM_LDS")) {
+    if (a.kord > 7 && !fv3::variant_env("FV3_MAPPM_LDS")) {
         const int block = 256;
         const int64_t grid = (a.ncol + block - 1) / block;
         FV3_HIP(hipMallocAsync((void**)&a.scratch, sizeof(float) * 2 * (size_t)(a.km + 3) * (size_t)grid * block,

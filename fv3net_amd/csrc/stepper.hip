@@ -307,7 +307,7 @@ int epilogue_impl(const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, int n
     // 0.2065 vs 0.2080 ms) (tools/epi_ab.py, profiles/r04j_epi_ab.log);
     // FV3_EPILOGUE_PATH=levels|columns forces one
     const size_t smem = epi_levels_smem(nz, sizeof(DT));
-    const char* path = getenv("FV3_EPILOGUE_PATH");
+    const char* path = fv3::variant_env("FV3_EPILOGUE_PATH");
     bool levels = ncol <= kEpiLevelsMaxCols;
     if (path && path[0] == 'c') levels = false;
     if (path && path[0] == 'l') levels = true;

@@ -372,8 +372,8 @@ class DenseColumnModel:
     def forward_host(self, arrays: Sequence, level_axes: Optional[Sequence[int]] = None,
                      precision: Optional[str] = None, out: Optional[Sequence[np.ndarray]] = None) -> List[np.ndarray]:
         """numpy inputs -> numpy float32 outputs (pure_keras.py:98-118 predicts on host
-        arrays).  The inputs cross as pageable copies or through the library's staging
-        blocks (``transfer.PinnedStager``; caller memory is never page-locked) and land in device buffers of their own dtype (a float64 state is read in place
+        arrays).  The inputs cross as the runtime's pageable copies (caller memory is never
+        page-locked) and land in device buffers of their own dtype (a float64 state is read in place
         by the kernel), cached per shape with the bound kernel.
 
         Inputs with a common leading block axis (tiles: ``(tile, z, y, x)``, level axis
@@ -426,11 +426,11 @@ class DenseColumnModel:
         s_out.wait_stream(cur)
         host = None
         lib = _native.load()
-        kernel_out = os.environ.get("FV3_D2H_KERNEL", "0") == "1"
+        kernel_out = _native.variant("FV3_D2H_KERNEL") == "1"
         self._last_kernel_out = False
         for t in range(n0):
-            # block t's inputs: staged (host memcpy into arena blocks) or pageable copies,
-            # on s_in while the compute stream still runs block t - 1
+            # block t's inputs (the runtime's pageable copies: the host waits for them while
+            # the compute stream runs block t - 1 and s_out copies block t - 2's outputs)
             for a, b in zip(arrays, bufs):
                 st.h2d(a[t], out=b[t], stream=s_in)
             ev = torch.cuda.Event()

@@ -11,11 +11,11 @@ twice.
   (``empty_host``, ``fv3_host_alloc``): DMA targets with no registration per call, their
   pages reused (already faulted in) once the caller drops them.
 * Caller arrays are never page-locked (csrc/host_memory.cpp, DESIGN.md §3.7: round 4's
-  per-call registration of the caller's pages faulted later pageable copies).  Large ones
-  cross through staging blocks of the arena: the host side of the copy (numpy -> staging
-  block, threads splitting each chunk) runs while the DMA of the previous chunk is in
-  flight on a copy stream.  Smaller ones take the runtime's pageable copy, measured faster
-  there.  An arena array (``empty_host``) as input is DMA'd directly.
+  per-call registration of the caller's pages faulted later pageable copies).  They take
+  the runtime's pageable copy (56 GB/s for a C384 field, profiles/r05e_host_ab.json); an
+  arena array (``empty_host``) as input is DMA'd directly.  ``PinnedStager`` can also
+  stage through arena blocks (the host memcpy, threads splitting each chunk, overlapping
+  the DMA of the previous chunk) for a caller that sets ``min_staged``.
 
 Plumbing only: bytes are moved unchanged (float64 stays float64; the kernels that read
 float64 in place, or a device cast, do any conversion).
@@ -141,10 +141,12 @@ class PinnedStager:
         self.chunk = int(chunk_bytes)
         # d2h results of this size and more land in the arena (None: never)
         self.min_arena = min_arena
-        # below 4 chunks the driver's own pageable copy is faster (measured on the box:
-        # a C48 float64 field, 8.7 MB, 22 GB/s pageable vs 19 staged; a C384 one, 560 MB,
-        # 11 vs 46 GB/s)
-        self.min_staged = 4 * self.chunk if min_staged is None else int(min_staged)
+        # the runtime's own pageable copy is the default at every size: with no caller
+        # memory registered it measured at least as fast as staging (profiles/
+        # r05e_host_ab.json: one C384 float64 field, 560 MB, 9.9 ms pageable = 56 GB/s
+        # against 10.6-14.9 ms staged; one rank's two (79, 48, 48) fields 0.079 ms against
+        # 0.11-0.22 ms).  Staging stays for a caller that asks for it (min_staged).
+        self.min_staged = (1 << 62) if min_staged is None else int(min_staged)
         self._host = [None, None]  # the staging blocks, allocated on first use
         self._done = [None, None]  # event after the last DMA that used block i
         self._stream = torch.cuda.Stream(device=self.device)

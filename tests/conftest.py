@@ -15,6 +15,13 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running CPU test")
 
 
+def set_variant(monkeypatch, name: str, value: str) -> None:
+    """Select a kernel variant for one test: the library reads variant selectors only
+    while FV3_VARIANTS=1 (csrc/common.h variant_env, _native.variant)."""
+    monkeypatch.setenv("FV3_VARIANTS", "1")
+    monkeypatch.setenv(name, value)
+
+
 @pytest.fixture(scope="session")
 def gpu():
     import torch

@@ -14,7 +14,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN
+from conftest import GOLDEN, set_variant
 from oracle import coarsen as OC
 
 FACTOR = 2
@@ -116,7 +116,7 @@ def test_kernel_vs_oracle_random(gpu, factor, n, dtype, path, monkeypatch):
     the row segments with the scratch-free output-driven cursor."""
     from fv3net_amd.coarsen import coarsen_on_pressure
 
-    monkeypatch.setenv("FV3_COARSEN_PATH", path)
+    set_variant(monkeypatch, "FV3_COARSEN_PATH", path)
 
     rng = np.random.default_rng(factor * 100 + n)
     delp, area, T, q = _smooth_state(rng, 6, 79, n, n)
@@ -139,7 +139,7 @@ def test_kernel_steep_cells_overflow_columns(gpu, path, dtype, monkeypatch):
     Still bit-identical to the oracle, on both paths."""
     from fv3net_amd.coarsen import coarsen_on_pressure
 
-    monkeypatch.setenv("FV3_COARSEN_PATH", path)
+    set_variant(monkeypatch, "FV3_COARSEN_PATH", path)
     rng = np.random.default_rng(11)
     delp, area, T, q = _smooth_state(rng, 6, 79, 16, 16)
     delp[:, -40:] *= rng.uniform(0.05, 4.0, (6, 1, 16, 16)).astype(np.float32)

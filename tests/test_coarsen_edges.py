@@ -16,7 +16,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN
+from conftest import GOLDEN, set_variant
 from oracle import coarsen as OC
 
 FACTOR = 2
@@ -161,7 +161,7 @@ def test_kernel_vs_oracle_random(gpu, factor, n, dtype, path, monkeypatch):
     from fv3net_amd.coarsen import coarsen_edges_on_pressure
 
     if path == "cursor":
-        monkeypatch.setenv("FV3_COARSEN_CURSOR", "1")
+        set_variant(monkeypatch, "FV3_COARSEN_CURSOR", "1")
 
     rng = np.random.default_rng(factor * 10 + n)
     delp, u, v, dx, dy = _winds_state(rng, 40, n, dtype)

@@ -18,6 +18,8 @@ bound, 1e-5 per level: the 1e-5 rel tendency contract of north_star on bf16 MFMA
 import numpy as np
 import pytest
 
+from conftest import set_variant
+
 from oracle.dense import dense_predict
 from tests.parity import assert_per_level
 
@@ -48,11 +50,11 @@ def b3_stage(request, monkeypatch):
     for grids with fewer 128-column tiles than CUs) and with the row-per-lane output layer
     instead of the transposed one (FV3_B3_TR=0)."""
     stage, waves, tr = request.param
-    monkeypatch.setenv("FV3_B3_STAGE", stage)
+    set_variant(monkeypatch, "FV3_B3_STAGE", stage)
     if waves:
-        monkeypatch.setenv("FV3_B3_WAVES", waves)
+        set_variant(monkeypatch, "FV3_B3_WAVES", waves)
     if tr:
-        monkeypatch.setenv("FV3_B3_TR", tr)
+        set_variant(monkeypatch, "FV3_B3_TR", tr)
     return request.param
 
 

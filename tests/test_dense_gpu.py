@@ -9,6 +9,8 @@ satisfy the same bound, so the kernel is as close to the truth as Keras is.
 import numpy as np
 import pytest
 
+from conftest import set_variant
+
 from oracle.dense import dense_predict
 from tests.parity import assert_per_level
 
@@ -325,7 +327,7 @@ def test_residual_outputs_stay_inside(gpu, ncol, precision, tr, monkeypatch):
 
     if precision == "f32" and tr == "0":
         pytest.skip("the exact-f32 kernel has one output layer")
-    monkeypatch.setenv("FV3_B3_TR", tr)
+    set_variant(monkeypatch, "FV3_B3_TR", tr)
 
     rng = np.random.default_rng(ncol)
     x = rng.normal(250.0, 10.0, (ncol, 79)).astype(np.float32)

@@ -6,6 +6,8 @@ max over columns / max |ref| of each level)."""
 import numpy as np
 import pytest
 
+from conftest import set_variant
+
 from oracle import emulator as OE
 from tests.parity import assert_per_level
 
@@ -186,7 +188,7 @@ def test_emulator_split_kernel_variants_agree(gpu, monkeypatch, precision, rtol)
 
     emu, raw = _emulator(ncol=2085, seed=11, precision=precision)
     state = {k: torch.from_numpy(np.ascontiguousarray(v.T)).cuda() for k, v in raw.items()}
-    monkeypatch.setenv("FV3_B3_GRID", "4")
+    set_variant(monkeypatch, "FV3_B3_GRID", "4")
     runs = {}
     for name, env in (("glds-w8", {"FV3_B3_STAGE": "glds", "FV3_B3_WAVES": "8"}),
                       ("reg-w8", {"FV3_B3_STAGE": "reg", "FV3_B3_WAVES": "8"}),
@@ -217,7 +219,7 @@ def test_emulator_forced_multi_tile_blocks(gpu, precision, rtol, env, monkeypatc
     emu, raw = _emulator(ncol=2085, seed=9, precision=precision)
     state = {k: torch.from_numpy(np.ascontiguousarray(v.T)).cuda() for k, v in raw.items()}
     base = emu(state)
-    monkeypatch.setenv(env, "4")
+    set_variant(monkeypatch, env, "4")
     forced = emu(state)
     torch.cuda.synchronize()
     monkeypatch.delenv(env)

@@ -8,7 +8,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN
+from conftest import GOLDEN, set_variant
 from oracle.mappm import oracle_mappm
 
 pytestmark = pytest.mark.gpu
@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 def mappm_path(request, monkeypatch):
     """Every test runs on both kord <= 7 kernels: one lane per column (`serial`) and
     one block per column, one lane per level (`levels`, the small-ncol default)."""
-    monkeypatch.setenv("FV3_MAPPM_PATH", request.param)
+    set_variant(monkeypatch, "FV3_MAPPM_PATH", request.param)
     return request.param
 
 
@@ -95,7 +95,7 @@ def test_cs_lds_path_vs_oracle_bit_exact(gpu, km, kn, ncol, monkeypatch):
     default global scratch: the same arithmetic, bit-identical."""
     from fv3net_amd.mappm import mappm_device
 
-    monkeypatch.setenv("FV3_MAPPM_LDS", "1")
+    set_variant(monkeypatch, "FV3_MAPPM_LDS", "1")
     rng = np.random.default_rng(km * kn + ncol)
     pe1, q, pe2 = _columns(rng, km, kn, ncol)
     for kord in (8, 10, 13, 17):
@@ -117,10 +117,10 @@ def test_cs_kernel_variants_vs_oracle_bit_exact(gpu, nt, pf, c32, kspec, monkeyp
 
     if mappm_path != "serial":
         pytest.skip("kord > 7 has one kernel family; run once")
-    monkeypatch.setenv("FV3_MAPPM_CS_NT", str(nt))
-    monkeypatch.setenv("FV3_MAPPM_CS_PF", str(pf))
-    monkeypatch.setenv("FV3_MAPPM_CS_C32", str(c32))
-    monkeypatch.setenv("FV3_MAPPM_CS_KORD", str(kspec))
+    set_variant(monkeypatch, "FV3_MAPPM_CS_NT", str(nt))
+    set_variant(monkeypatch, "FV3_MAPPM_CS_PF", str(pf))
+    set_variant(monkeypatch, "FV3_MAPPM_CS_C32", str(c32))
+    set_variant(monkeypatch, "FV3_MAPPM_CS_KORD", str(kspec))
     for km, kn, ncol in ((5, 9, 257), (17, 12, 333), (50, 60, 300), (79, 79, 777), (127, 40, 300)):
         rng = np.random.default_rng(km * 31 + kn + ncol + pf)
         pe1, q, pe2 = _columns(rng, km, kn, ncol)
@@ -220,14 +220,13 @@ def test_c384_scale_sampled_bit_exact(gpu):
     assert _bits_equal(res[:, idx], ref)
 
 
-def test_unsorted_edges_fall_back_per_column(gpu):
+def test_unsorted_edges_fall_back_per_column(gpu, monkeypatch):
     """Columns whose pe1 or pe2 are not non-decreasing (or hold NaN) take the serial
     streaming code inside the level-parallel kernel; sorted neighbours in the same launch
     do not.  Both kernels agree bit for bit.  A negative layer thickness with sorted pe2
     also matches the oracle; out-of-order or NaN pe2 hits the reference's failed search
     (mappm.f90:58-124 leaves q2 undefined), where the product writes NaN, so there only
     the two kernels are compared."""
-    import os as _os
 
     from fv3net_amd.mappm import mappm_device
 
@@ -241,9 +240,9 @@ def test_unsorted_edges_fall_back_per_column(gpu):
     for kord in (1, 4, 6, 7):
         for iv in (0, 1, -1):
             for p2, vs_oracle in ((pe2, True), (bad2, False)):
-                _os.environ["FV3_MAPPM_PATH"] = "levels"
+                set_variant(monkeypatch, "FV3_MAPPM_PATH", "levels")
                 a = mappm_device(pe1, q, p2, iv, kord).cpu().numpy()
-                _os.environ["FV3_MAPPM_PATH"] = "serial"
+                set_variant(monkeypatch, "FV3_MAPPM_PATH", "serial")
                 b = mappm_device(pe1, q, p2, iv, kord).cpu().numpy()
                 assert _bits_equal(a, b), (kord, iv, vs_oracle)
                 if vs_oracle:

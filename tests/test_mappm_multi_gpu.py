@@ -8,6 +8,8 @@ csrc/mappm_multi.h computes the pressure-only part once per pair of fields.
 import numpy as np
 import pytest
 
+from conftest import set_variant
+
 from oracle.mappm import oracle_mappm
 from tests.test_mappm_gpu import _bits_equal, _columns
 
@@ -18,7 +20,7 @@ pytestmark = pytest.mark.gpu
 def path(request, monkeypatch):
     """`serial` (one lane per column): pairs of fields on the two-field streaming
     kernel; `levels`: the small-grid kernel, one field per launch."""
-    monkeypatch.setenv("FV3_MAPPM_PATH", request.param)
+    set_variant(monkeypatch, "FV3_MAPPM_PATH", request.param)
     return request.param
 
 
@@ -52,7 +54,7 @@ def test_multi_c384_pair_kernel_sampled(gpu, monkeypatch):
 
     from fv3net_amd.mappm import mappm_device, mappm_device_multi
 
-    monkeypatch.setenv("FV3_MAPPM_PATH", "serial")
+    set_variant(monkeypatch, "FV3_MAPPM_PATH", "serial")
     rng = np.random.default_rng(385)
     ncol, km = 6 * 384 * 384, 79
     base = np.linspace(200, 1800, km, dtype=np.float32)[:, None]
@@ -78,7 +80,7 @@ def test_multi_tile_layout_in_place(gpu, monkeypatch):
 
     from fv3net_amd.mappm import mappm_device_multi
 
-    monkeypatch.setenv("FV3_MAPPM_PATH", "serial")
+    set_variant(monkeypatch, "FV3_MAPPM_PATH", "serial")
     rng = np.random.default_rng(8)
     ntile, km, ny, nx = 6, 79, 12, 12
     ncol = ntile * ny * nx

@@ -9,6 +9,8 @@ import os
 import numpy as np
 import pytest
 
+from conftest import set_variant
+
 from tests.parity import assert_per_level
 
 from fv3net_amd import dataset as D
@@ -276,7 +278,7 @@ def test_forward_host_tile_pipeline_bit_identical(gpu, dtype, kernel_out, monkey
     (no block axis) takes the one-call path."""
     import torch
 
-    monkeypatch.setenv("FV3_D2H_KERNEL", kernel_out)
+    set_variant(monkeypatch, "FV3_D2H_KERNEL", kernel_out)
 
     from fv3net_amd.dense import DenseColumnModel, DenseModelConfig
 

@@ -3,6 +3,8 @@ restatement of the reference's dtype flow, bit for bit (oracle/stepper.py)."""
 import numpy as np
 import pytest
 
+from conftest import set_variant
+
 from oracle import stepper as OS
 
 
@@ -52,7 +54,7 @@ def test_epilogue_bit_identical_to_oracle(gpu, dtype, mse, hydrostatic, path, mo
     """Both epilogue kernels: level-parallel (the default) and one thread per column."""
     import torch
 
-    monkeypatch.setenv("FV3_EPILOGUE_PATH", path)
+    set_variant(monkeypatch, "FV3_EPILOGUE_PATH", path)
 
     from fv3net_amd.stepper import ml_epilogue
 
@@ -81,7 +83,7 @@ def test_epilogue_level_batches(gpu, nz, path, monkeypatch):
     bit-identical, on 130 columns (a partial block of 16)."""
     import torch
 
-    monkeypatch.setenv("FV3_EPILOGUE_PATH", path)
+    set_variant(monkeypatch, "FV3_EPILOGUE_PATH", path)
 
     from fv3net_amd.stepper import ml_epilogue
 
