@@ -394,7 +394,7 @@ def host_to_host(dev, res, steps=10):
             "host_path": transfer.host_path(),
             "note": "float64 numpy in -> DenseColumnModel.forward_host: H2D (see host_path), the fused predict "
                     "(f64 read in place), D2H into float32 numpy outputs reused across calls (library arena "
-                    "when host_path is pinned); tile blocks pipelined over three streams above 64 MiB (C384)"}
+                    "when host_path is arena); tile blocks pipelined over two streams above 64 MiB (C384)"}
 
 
 def predict_mappm_host_to_host(dev, res=384, steps=5, bands=6):
@@ -404,9 +404,9 @@ def predict_mappm_host_to_host(dev, res=384, steps=5, bands=6):
     two-field mappm of both tendencies, and the float32 remapped tendencies back to numpy.
     The caller's inputs cross as pageable pitched copies (caller memory is never
     page-locked), the outputs live in the library's page-locked arena (reused across
-    calls), and the columns run in ``bands`` bands pipelined over three streams: band b + 1's pitched
-    in-copies (``transfer.copy_band``), band b's predict + remap and band b - 1's
-    out-copies overlap.  Wall time per step."""
+    calls), and the columns run in ``bands`` bands pipelined over two streams: band b + 1's
+    pitched in-copies (``transfer.copy_band``) and band b's out-copies overlap.  Wall time
+    per step."""
     import torch
 
     from fv3net_amd import transfer
@@ -437,18 +437,15 @@ def predict_mappm_host_to_host(dev, res=384, steps=5, bands=6):
         plan = MappmMultiPlan(d1[:, c0:c1], [o[:, c0:c1] for o in outs], d2[:, c0:c1], 1, 1,
                               out=[r[:, c0:c1] for r in wl.remapped])
         runs.append((c0, c1, bound, plan))
-    s_in, s_out = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    s_out = torch.cuda.Stream(device=dev)
 
     def step():
         cur = torch.cuda.current_stream()
         for c0, c1, bound, plan in runs:
-            # band b's in-copies (pitched, the runtime's pageable path: the host waits for
-            # them while band b - 1's predict, remap and out-copies run)
+            # band b's in-copies (pitched, the runtime's pageable path, on the compute
+            # stream: the host waits for them while band b - 1's out-copies run on s_out)
             for h, d in ((T2, dT), (q2, dq), (pe1, d1), (pe2, d2)):
-                transfer.copy_band(d[:, c0:c1], h[:, c0:c1], s_in.cuda_stream)
-            ev = torch.cuda.Event()
-            ev.record(s_in)
-            cur.wait_event(ev)
+                transfer.copy_band(d[:, c0:c1], h[:, c0:c1], cur.cuda_stream)
             bound(cur)
             plan()
             for h, r in zip(host_out, wl.remapped):  # arena outputs: asynchronous DMA
@@ -476,7 +473,7 @@ def predict_mappm_host_to_host(dev, res=384, steps=5, bands=6):
             "host_path": transfer.host_path(),
             "note": "float64 numpy T/q + float32 numpy pe1/pe2 in (see host_path) -> per column band: "
                     "pitched H2D, fused predict (f64 read in place), two-field mappm of dQ1/dQ2 (kord 1, iv 1), "
-                    "pitched D2H into float32 numpy; bands pipelined over three streams"}
+                    "pitched D2H into float32 numpy; bands pipelined over two streams"}
 
 
 def rank_call_host_to_host(dev, calls=30):

@@ -377,9 +377,9 @@ class DenseColumnModel:
         by the kernel), cached per shape with the bound kernel.
 
         Inputs with a common leading block axis (tiles: ``(tile, z, y, x)``, level axis
-        > 0) over ``_PIPELINE_MIN_BYTES`` run pipelined over the blocks on three streams:
-        block b + 1's host-to-device copies, block b's predict and block b - 1's
-        device-to-host copies overlap (PCIe is full duplex: in and out at once).  The
+        > 0) over ``_PIPELINE_MIN_BYTES`` run pipelined over the blocks on two streams:
+        block b + 1's host-to-device copies and block b's device-to-host copies overlap
+        (PCIe is full duplex: in and out at once).  The
         same kernels on the same columns, so the outputs are bit-identical to one call.
         ``out``: float32 numpy arrays to write, else arrays in the library's page-locked
         arena (``transfer.empty_host``: DMA targets with no registration per call, their
@@ -421,21 +421,19 @@ class DenseColumnModel:
                 transfer.host_copy(h, o, hcur)  # arena outputs: DMA; caller arrays: pageable
             cur.synchronize()
             return host
-        s_in, s_out = streams
-        s_in.wait_stream(cur)  # after whatever the caller queued on these buffers
-        s_out.wait_stream(cur)
+        _, s_out = streams
+        s_out.wait_stream(cur)  # after whatever the caller queued on these buffers
         host = None
         lib = _native.load()
         kernel_out = _native.variant("FV3_D2H_KERNEL") == "1"
         self._last_kernel_out = False
         for t in range(n0):
-            # block t's inputs (the runtime's pageable copies: the host waits for them while
-            # the compute stream runs block t - 1 and s_out copies block t - 2's outputs)
+            # block t's inputs: the runtime's pageable copies, on the compute stream (the
+            # host waits for them while s_out copies block t - 1's outputs).  On a side
+            # stream of their own the two directions ran nearly in sequence: C384 30.3 ms
+            # against 22.2 ms (profiles/r05g_host_ab.json, pipe_in_*)
             for a, b in zip(arrays, bufs):
-                st.h2d(a[t], out=b[t], stream=s_in)
-            ev = torch.cuda.Event()
-            ev.record(s_in)
-            cur.wait_event(ev)
+                st.h2d(a[t], out=b[t], stream=cur)
             outs = runs[t](cur)
             if host is None:
                 host = _host_outputs(out, [(n0,) + tuple(o.shape) for o in outs])
@@ -456,7 +454,6 @@ class DenseColumnModel:
                 for h, o in zip(host, outs):
                     transfer.host_copy(h[t], o, s_out.cuda_stream)
         cur.wait_stream(s_out)
-        cur.wait_stream(s_in)
         cur.synchronize()
         return host
 

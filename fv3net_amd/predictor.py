@@ -349,10 +349,9 @@ def _make_output(X, result: Dict, xr_in: bool):
             data_vars[name] = xr.DataArray(arr, dims=dims, coords={d: coords[d] for d in dims if d in coords})
         return xr.Dataset(data_vars)
     out = dsmod.Dataset()
+    src_is_torch = any(torch is not None and isinstance(dsmod.variable_data(X, n), torch.Tensor) for n in X)
     for name, (dims, t) in result.items():
         data = t
-        src_is_torch = any(torch is not None and isinstance(dsmod.variable_data(X, n), torch.Tensor)
-                           for n in X)
         if not src_is_torch and hasattr(t, "detach"):
             data = _to_host(t)
         out[name] = dsmod.DataArray(data, dims, {d: coords[d] for d in dims if d in coords})
