@@ -299,7 +299,7 @@ class DenseColumnPredictor(Predictor):
         """Host arrays in, host float32 arrays out, for the drop-in call on numpy data
         (pure_keras.py:98-118 predicts on host arrays): ``DenseColumnModel.forward_host``
         (device buffers of the inputs' own dtype cached per shape, outputs in the library's
-        page-locked arena, tile blocks pipelined over three streams)."""
+        page-locked arena, tile blocks pipelined over two streams)."""
         return self.model.forward_host(arrays, axes)
 
     # -- persistence ------------------------------------------------------------
