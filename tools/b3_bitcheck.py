@@ -2,6 +2,9 @@
 bf16x3 / bf16x6, both block shapes) under the library FV3NET_AMD_LIB names: a scheduling
 variant of csrc/dense_b3.hip must print the product library's hashes (same arithmetic
 in the same order)."""
+import os as _os
+
+_os.environ.setdefault("FV3_VARIANTS", "1")  # A/B tool: kernel-variant selectors on
 import hashlib
 import os
 import sys

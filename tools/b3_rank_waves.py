@@ -1,6 +1,9 @@
 """The split kernel on one rank's C384 band over 8 GPUs (110,592 columns: 864 tiles of
 128 columns for 256 CUs, 3.4 per CU) under the block shape FV3_B3_WAVES selects (8:
 128-column tiles; 4: 64-column tiles, 6.75 per CU).  Mean launch ms."""
+import os as _os
+
+_os.environ.setdefault("FV3_VARIANTS", "1")  # A/B tool: kernel-variant selectors on
 import os
 import sys
 

@@ -6,6 +6,9 @@ from the product kernel's), so the phase split is indicative; its launch time is
 beside the product's from the same process for comparison.  Per tile: layer 1, hidden
 layers, output layer (us), shader clock, and the fraction of the tile wave 0 spent in the
 chunk waits (vmcnt + barrier)."""
+import os as _os
+
+_os.environ.setdefault("FV3_VARIANTS", "1")  # A/B tool: kernel-variant selectors on
 import os
 import sys
 

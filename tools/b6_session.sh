@@ -1,4 +1,5 @@
 set -o pipefail
+export FV3_VARIANTS=1  # A/B tool: the library reads kernel-variant selectors only with this set
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_dense_b3_gpu.py tests/test_normalization_kat.py -m gpu > gpurun_out/b6_tests.log 2>&1 || exit 1
 for w in 4 8; do
   FV3_B3_WAVES=$w B3_RES=48 B3_PRECS=bf16x3,bf16x6 timeout -k 10 120 python -u tools/b3_time.py dense > gpurun_out/b6_time_w$w.log 2>&1 || exit 1

@@ -1,6 +1,9 @@
 """Coarsen C384 -> C48 (f = 8, 79 levels) launch time with 0 fields (pass 1 only: the
 coarse delp / phalf), 1 and 4 fields; the remap's share is the difference.
 FV3_COARSEN_PATH=cells|rows|cursor in the environment selects the kernel path."""
+import os as _os
+
+_os.environ.setdefault("FV3_VARIANTS", "1")  # A/B tool: kernel-variant selectors on
 import os
 import sys
 

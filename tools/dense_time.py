@@ -1,5 +1,8 @@
 """Mean launch time of the fused dense kernel at C48 and C384 (events around N
 back-to-back launches); env knobs (FV3_DENSE_*) are read by the library per launch."""
+import os as _os
+
+_os.environ.setdefault("FV3_VARIANTS", "1")  # A/B tool: kernel-variant selectors on
 import os
 import sys
 

@@ -4,6 +4,9 @@
 
 Prints, over all blocks of one launch: phase durations (staging, layer 1, hidden,
 output), block start-time spread, blocks per CU and the kernel span, in us."""
+import os as _os
+
+_os.environ.setdefault("FV3_VARIANTS", "1")  # A/B tool: kernel-variant selectors on
 import argparse
 import os
 import sys

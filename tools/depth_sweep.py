@@ -1,4 +1,7 @@
 """Marginal cost per hidden layer (steady-state MFMA efficiency) vs fixed per-tile overhead."""
+import os as _os
+
+_os.environ.setdefault("FV3_VARIANTS", "1")  # A/B tool: kernel-variant selectors on
 import os, sys, numpy as np, torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fv3net_amd import workloads as W

@@ -1,5 +1,8 @@
 """Time the C384 -> C48 edge-weighted coarsen (u on x edges, 79 levels) on both remap
 paths: input-driven through the scratch column (default) and the cursor."""
+import os as _os
+
+_os.environ.setdefault("FV3_VARIANTS", "1")  # A/B tool: kernel-variant selectors on
 import os
 import sys
 

@@ -1,6 +1,9 @@
 """The stepper epilogue's two kernels (FV3_EPILOGUE_PATH=levels|columns, read per launch),
 interleaved twice: one rank's share of C96 over 8 (bound step, stubbed exchange) and the
 full C96 step.  ms per step."""
+import os as _os
+
+_os.environ.setdefault("FV3_VARIANTS", "1")  # A/B tool: kernel-variant selectors on
 import os
 import sys
 

@@ -2,6 +2,9 @@
 one rank's C384 band over 8 GPUs (110,592 columns) and the full grid (884,736), under the
 multi-field scheme FV3_MAPPM_FIELDS selects (pair | lanes; unset: the library's choice).
 Mean launch ms."""
+import os as _os
+
+_os.environ.setdefault("FV3_VARIANTS", "1")  # A/B tool: kernel-variant selectors on
 import os
 import sys
 

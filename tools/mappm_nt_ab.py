@@ -1,5 +1,8 @@
 """kord-10 mappm (C384, 79 -> 79, and one rank's C384 band over 8) under the register-tail
 depth FV3_MAPPM_CS_NT selects (unset: the library default).  Mean launch ms."""
+import os as _os
+
+_os.environ.setdefault("FV3_VARIANTS", "1")  # A/B tool: kernel-variant selectors on
 import os
 import sys
 

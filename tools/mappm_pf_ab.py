@@ -1,6 +1,9 @@
 """kord-10 mappm (C384, 79 -> 79, and one rank's C384 band over 8) under each load
 distance FV3_MAPPM_CS_PF of the kord > 7 kernel (read per launch), interleaved twice.
 Mean launch ms."""
+import os as _os
+
+_os.environ.setdefault("FV3_VARIANTS", "1")  # A/B tool: kernel-variant selectors on
 import os
 import sys
 

@@ -1,5 +1,8 @@
 """kord 1 mappm launch time vs column count on both kernels (FV3_MAPPM_PATH): picks
 the level-parallel kernel's ncol threshold (csrc/mappm.hip kLevelsMaxCols)."""
+import os as _os
+
+_os.environ.setdefault("FV3_VARIANTS", "1")  # A/B tool: kernel-variant selectors on
 import os
 import sys
 

@@ -3,6 +3,9 @@ on one MI355X?  C384 (884,736 columns).  Times, with events on each stream:
   dense alone at several persistent grids (FV3_DENSE_GRID), mappm pair alone, the two
   back to back, and the two on two streams at once on independent buffers (an upper
   bound for any overlap scheme).  Results are timings only (no parity claims)."""
+import os as _os
+
+_os.environ.setdefault("FV3_VARIANTS", "1")  # A/B tool: kernel-variant selectors on
 import os
 import sys
 import time

@@ -2,6 +2,9 @@
 launched together on two streams (C384)?  Per-stream end events against one start
 event; grid 256 (one 8-wave dense block per CU, room for mappm waves) and the default
 grid.  Timings only."""
+import os as _os
+
+_os.environ.setdefault("FV3_VARIANTS", "1")  # A/B tool: kernel-variant selectors on
 import os
 import sys
 

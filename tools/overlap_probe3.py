@@ -3,6 +3,9 @@ launched together on two streams (C384), for both block shapes of the split kern
 (FV3_B3_WAVES=8: 8-wave blocks, 2 dense waves per SIMD and ~220 VGPRs each, no room for
 remap waves; 4: one dense wave per SIMD, ~310 of the 512 registers, room for two 92-VGPR
 remap waves).  Per-stream end events against one start event.  Timings only."""
+import os as _os
+
+_os.environ.setdefault("FV3_VARIANTS", "1")  # A/B tool: kernel-variant selectors on
 import os
 import sys
 

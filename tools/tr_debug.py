@@ -1,5 +1,8 @@
 """Debug: the split kernel's transposed output layer (FV3_B3_TR=1) against the row-per-lane
 one (0) on the emulator's 2,048 columns: per output, the levels and columns that differ."""
+import os as _os
+
+_os.environ.setdefault("FV3_VARIANTS", "1")  # A/B tool: kernel-variant selectors on
 import os
 import sys
 
