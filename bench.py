@@ -582,6 +582,64 @@ def coarsen_cpu_baseline(seconds=10.0):
                       f"oracle/coarsen.py (numpy + the C restatement of mappm.f90), {dt:.1f} s, 1 core"}
 
 
+def _blas_threads():
+    from threadpoolctl import threadpool_info
+
+    return int(max([i.get("num_threads", 1) for i in threadpool_info()] + [1]))
+
+
+def stepper_cpu_baseline(wl, seconds=10.0):
+    """Config #4's step on the host: the numpy restatement of the predict (oracle/dense.py,
+    float32, Keras-default batch_size=32 chunks as PureKerasModel.predict runs it,
+    pure_keras.py:112) then oracle/stepper.py's limiter / diagnostics / apply epilogue
+    (the reference's numpy arithmetic, machine_learning.py:239-309) on one C96 tile of the
+    same float64 state: columns/s."""
+    from oracle import stepper as OS
+    from oracle.dense import dense_predict
+
+    p = wl.model.oracle_params()
+    st = {k: v[0].reshape(v.shape[1], -1).cpu().numpy() if v.dim() == 4 else v[0].reshape(-1).cpu().numpy()
+          for k, v in wl.state.items()}
+    T, q = st["air_temperature"], st["specific_humidity"]
+    delp, precip = st["pressure_thickness_of_atmospheric_layer"], st["total_precipitation"]
+    Ts, qs = T.T.astype(np.float32), q.T.astype(np.float32)
+    n = Ts.shape[0]
+    cols, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        outs = [dense_predict([Ts[s:s + 32], qs[s:s + 32]], p, np.float32) for s in range(0, n, 32)]
+        dq1 = np.concatenate([o[0] for o in outs]).T
+        dq2 = np.concatenate([o[1] for o in outs]).T
+        OS.epilogue(dq1, dq2, q, delp, T, precip, wl.dt)
+        cols += n
+    dt = time.perf_counter() - t0
+    threads = _blas_threads()
+    return {"value": cols / dt, "unit": "columns/s", "cores": threads, "kind": "port",
+            "sample": f"{cols} columns of one C96 tile ({n}/pass): oracle/dense.py float32 predict in batch_size=32 "
+                      f"chunks + oracle/stepper.py epilogue on the float64 state, {dt:.1f} s; numpy BLAS "
+                      f"threads={threads}"}
+
+
+def emulator_cpu_baseline(wl, seconds=10.0, ncol=16384, batch=1024):
+    """Config #5 on the host: oracle/emulator.py's forward (the emulator's numpy
+    restatement, float32) over ``ncol`` columns of the same C384 state in the reference's
+    batch_size=1024 chunks (external/emulation/emulation/models.py:20): columns/s."""
+    from oracle import emulator as OE
+
+    raw = {k: v[:, :ncol].T.contiguous().cpu().numpy() for k, v in wl.state.items()}
+    params = wl.emulator.params_by_name()
+    spec = OE.zhao_carr_spec()
+    cols, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for s in range(0, ncol, batch):
+            OE.forward({k: v[s:s + batch] for k, v in raw.items()}, spec, params, np.float32)
+        cols += ncol
+    dt = time.perf_counter() - t0
+    threads = _blas_threads()
+    return {"value": cols / dt, "unit": "columns/s", "cores": threads, "kind": "port",
+            "sample": f"{cols} columns ({ncol} of the C384 state per pass) through oracle/emulator.py float32 in "
+                      f"batch_size={batch} chunks, {dt:.1f} s; numpy BLAS threads={threads}"}
+
+
 def reference_mappm_cpu(seconds=5.0):
     """The reference's own Fortran mappm (flang build in oracle/_ref)
     timed on one host core in 512-column chunks on config #3 columns (79 -> 79, kord 1).
@@ -647,6 +705,10 @@ def extra_measurements(dev, settle_ms=150.0):
         "columns_per_s": wl.ncol / (wall / 20), "ms_per_step": wall / 20 * 1e3,
         "note": "wall clock per step (predict, fused epilogue, area partials: three C-ABI calls marshalled once, "
                 "workloads.StepperWorkload._bind); counters: the fused epilogue kernel"})
+    try:
+        out["stepper_c96"]["cpu_baseline"] = stepper_cpu_baseline(wl)
+    except Exception as e:  # a report, never fatal
+        log("stepper cpu baseline failed:", repr(e))
     del wl
     # the same step with the predict on the bf16x6 split kernel (1e-5 per level like the
     # f32 kernel); the float64 state is cast into bound float32 buffers each step
@@ -672,6 +734,11 @@ def extra_measurements(dev, settle_ms=150.0):
             rec["frac_bf16_mfma_peak"] = (3 if prec == "bf16x3" else 6) * tf / W.BF16_MFMA_PEAK_TFLOPS
         leg = {"bf16x3": "emulator_c384", "bf16x6": "emulator_c384_bf16x6", "f32": "emulator_c384_f32"}[prec]
         out[leg] = with_counters(leg, rec, wl.ncol * wl.bytes_per_column)
+        if prec == "bf16x3":
+            try:
+                out[leg]["cpu_baseline"] = emulator_cpu_baseline(wl)
+            except Exception as e:  # a report, never fatal
+                log("emulator cpu baseline failed:", repr(e))
         del wl
     # config #2's model on the bf16x3 kernel (8e-6 rel: not the headline's exact-f32 path)
     wl = W.make_dense_workload(384, seed=3, device=dev, precision="bf16x3")
