@@ -14,9 +14,10 @@ HIP kernels (csrc/composite.hip, ``fv3_member_reduce`` / ``fv3_scale_levels``). 
 composite hands back the kind of data its members produced (device tensors stay on
 the device; host arrays come back as host arrays).
 
-Not mirrored: ``DerivedModel`` and ``TransformedPredictor`` (their post-processing is
-vcm.DerivedMapping / vcm.DataTransform, a catalogue of diagnostics outside this path),
-``OutOfSampleModel`` (needs a novelty detector, an sklearn model).
+``DerivedModel`` ("derived_model") and ``TransformedPredictor``
+("output_transformed_model") live in derived.py, over the vcm.DerivedMapping /
+vcm.DataTransform catalogues.  Not mirrored: ``OutOfSampleModel`` (it needs a novelty
+detector, an sklearn model).
 """
 import ctypes
 import dataclasses

@@ -168,6 +168,27 @@ def test_sharded_stepper_two_ranks_bit_identical_to_one(gpu, tmp_path):
 
 
 @pytest.mark.gpu
+def test_sharded_stepper_c96_world4_bit_identical_to_one(gpu, tmp_path):
+    """Config #4's own geometry: C96 over 4 ranks, 144 of the 576 (tile, y) rows each (4
+    processes on one GPU, gloo exchange).  After two steps the global means / limiter
+    profile carry the world-1 bits on every rank, and each rank's state band equals the
+    world-1 state's rows."""
+    for world in (1, 4):
+        (tmp_path / f"w{world}").mkdir()
+        _spawn(H.sharded_stepper_worker, world, str(tmp_path / f"w{world}"), 96, 2)
+    one = np.load(tmp_path / "w1" / "total0.npy")
+    q1 = np.load(tmp_path / "w1" / "q0.npy")
+    for r in range(4):
+        t = np.load(tmp_path / "w4" / f"total{r}.npy")
+        assert (t.view(np.uint64) == one.view(np.uint64)).all(), r
+        r0, r1 = np.load(tmp_path / "w4" / f"rows{r}.npy")
+        assert r1 - r0 == 144
+        q = np.load(tmp_path / "w4" / f"q{r}.npy")
+        assert (q.view(np.uint64) == q1[:, r0:r1].view(np.uint64)).all(), r
+    assert np.isfinite(one).all() and one[6:].sum() > 0
+
+
+@pytest.mark.gpu
 def test_sharded_stepper_rccl_exchange_matches_gloo(gpu, tmp_path):
     """The RCCL (nccl backend) branch of the per-step exchange (device tensors in the
     all-gather) on the box's one GPU (world 1: RCCL runs one rank per device): the same
