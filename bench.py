@@ -722,7 +722,7 @@ def extra_measurements(dev, settle_ms=150.0):
     # MFMA (1e-3 rel): the bf16x3 kernel (csrc/dense_b3.hip, 3 bf16 MFMAs per f32
     # product, so the bf16 roofline is priced at 3x the algorithmic FLOP); the exact-f32
     # kernel beside it for comparison
-    for prec in ("bf16x3", "bf16x6", "f32", "bf16"):
+    for prec in ("bf16x3", "bf16x6", "f32"):
         wl = W.make_emulator_workload(384, seed=13, device=dev, precision=prec)
         wall, t = timed_steps(wl.step, 10, 3, settle_ms=settle_ms)
         tf = wl.ncol * wl.flops_per_column / t / 1e12
@@ -731,9 +731,8 @@ def extra_measurements(dev, settle_ms=150.0):
         if prec == "f32":
             rec["frac_f32_mfma_peak"] = tf / W.FP32_MFMA_PEAK_TFLOPS
         else:
-            rec["frac_bf16_mfma_peak"] = {"bf16": 1, "bf16x3": 3, "bf16x6": 6}[prec] * tf / W.BF16_MFMA_PEAK_TFLOPS
-        leg = {"bf16x3": "emulator_c384", "bf16x6": "emulator_c384_bf16x6", "f32": "emulator_c384_f32",
-               "bf16": "emulator_c384_bf16"}[prec]
+            rec["frac_bf16_mfma_peak"] = (3 if prec == "bf16x3" else 6) * tf / W.BF16_MFMA_PEAK_TFLOPS
+        leg = {"bf16x3": "emulator_c384", "bf16x6": "emulator_c384_bf16x6", "f32": "emulator_c384_f32"}[prec]
         out[leg] = with_counters(leg, rec, wl.ncol * wl.bytes_per_column)
         if prec == "bf16x3":
             try:

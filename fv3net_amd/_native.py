@@ -92,7 +92,6 @@ ABI_VERSION = 9
 DENSE_F32 = 0
 DENSE_BF16X3 = 1
 DENSE_BF16X6 = 2
-DENSE_BF16 = 3
 
 # fv3_ml_epilogue_ex flags, fv3_tendency_columns modes
 EPI_HAS_DQ1 = 1

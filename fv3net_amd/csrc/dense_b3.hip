@@ -208,12 +208,11 @@ __device__ __forceinline__ void splitN(const float (&y)[8], bf16x8 (&o)[NS])
 }
 
 // the split products of one f32 product a*b, in issue order (part of a, part of b):
-// NS = 1 (bf16): hi*hi, the operands rounded to bf16 (BASELINE config #5's arithmetic);
 // NS = 2 (bf16x3): hi*hi, lo*hi, hi*lo; NS = 3 (bf16x6): every pair of order <= 2 in the
 // parts' 2^-8 steps (hi*hi; mid*hi, hi*mid; mid*mid, lo*hi, hi*lo), ~2^-24 rel per product
 template <int NS>
 struct SplitTerms {
-    static constexpr int n = NS == 1 ? 1 : (NS == 2 ? 3 : 6);
+    static constexpr int n = NS == 2 ? 3 : 6;
     static constexpr int a[6] = {0, 1, 0, 1, 2, 0};
     static constexpr int b[6] = {0, 0, 1, 1, 0, 2};
 };
@@ -624,7 +623,7 @@ dense_b3_kernel(B3Args pa)
                 y[r] = v0 > 0.0f ? v0 : 0.0f;
                 y[4 + r] = v1 > 0.0f ? v1 : 0.0f;
             }
-            if constexpr (NS <= 2) {
+            if constexpr (NS == 2) {
                 splitN<NS>(y, B[c]);
             } else {
 #pragma unroll
@@ -634,7 +633,7 @@ dense_b3_kernel(B3Args pa)
     };
     auto hidden_b = [&](auto cc, bf16x8 (&bx)[NS]) -> const bf16x8(&)[NS] {  // k-step c's B fragments
         constexpr int c = decltype(cc)::value;
-        if constexpr (NS <= 2) {
+        if constexpr (NS == 2) {
             return B[c];
         } else {
             splitN<NS>(Y[c], bx);
@@ -1222,8 +1221,7 @@ static B3Desc* copy_desc(const fv3_dense_model* m, const fv3_dense_desc* d)
 // input features or output rows, a stream past 2 GiB) leaves only that precision
 // unsupported (fv3_dense_forward_ex returns FV3_ERR_UNSUPPORTED for it), and the exact-f32
 // path is never affected.  Only a HIP failure fails fv3_dense_create.  The bf16x3 stream
-// is packed here; the bf16x6 one (1.5x its size) and the bf16 one on their first use,
-// from a host copy of the description kept with the model.
+// is packed here; the bf16x6 one (1.5x its size) on the first bf16x6 forward.
 int b3_pack(fv3_dense_model* m, const fv3_dense_desc* d)
 {
     const int st = pack_ns(m, d, 2, &m->b3);
@@ -1236,33 +1234,29 @@ int b3_pack(fv3_dense_model* m, const fv3_dense_desc* d)
     return FV3_OK;
 }
 
-// the bf16 (ns 1) or bf16x6 (ns 3) stream of `m`, packed now if this is its first use
-// (nullptr: unsupported for this model, with the reason in fv3_last_error; HIP failures
-// return FV3_ERR_HIP)
-static int lazy_stream(const fv3_dense_model* cm, int ns, const B3Pack** out)
+// the bf16x6 stream of `m`, packed now if this is its first use (nullptr: unsupported
+// for this model, with the reason in fv3_last_error; HIP failures return FV3_ERR_HIP)
+static int b6_stream(const fv3_dense_model* cm, const B3Pack** out)
 {
     static std::mutex mu;
     std::lock_guard<std::mutex> lock(mu);
-    fv3_dense_model* m = const_cast<fv3_dense_model*>(cm);  // the lazily packed streams only
-    B3Pack** slot = ns == 3 ? &m->b6 : &m->b1;
-    bool* tried = ns == 3 ? &m->b6_tried : &m->b1_tried;
-    if (!*slot && !*tried && m->b6_src) {
-        const int st = pack_ns(m, &m->b6_src->d, ns, slot);
-        if (st == FV3_ERR_HIP) return st;  // a later call may retry
-        *tried = true;
-        if (st != FV3_OK) {
-            *slot = nullptr;
-            return st;
-        }
+    fv3_dense_model* m = const_cast<fv3_dense_model*>(cm);  // the lazily packed stream only
+    if (!m->b6 && m->b6_src) {
+        const int st = pack_ns(m, &m->b6_src->d, 3, &m->b6);
+        if (st == FV3_ERR_HIP) return st;  // keep the source: a later call may retry
+        if (st != FV3_OK) m->b6 = nullptr;
+        delete m->b6_src;
+        m->b6_src = nullptr;
+        if (st != FV3_OK) return st;
     }
-    *out = *slot;
-    return *slot ? FV3_OK : FV3_ERR_UNSUPPORTED;
+    *out = m->b6;
+    return FV3_OK;
 }
 
 void b3_free(fv3_dense_model* m)
 {
     if (!m) return;
-    for (B3Pack** pk : {&m->b1, &m->b3, &m->b6}) {
+    for (B3Pack** pk : {&m->b3, &m->b6}) {
         if (!*pk) continue;
         if ((*pk)->dbuf) (void)hipFree((*pk)->dbuf);
         delete *pk;
@@ -1281,12 +1275,12 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
     using namespace fv3;
     if (precision == FV3_DENSE_F32) return fv3_dense_forward(m, inputs, in_l, outputs, out_l, ncol, stream);
     clear_error();
-    FV3_REQUIRE(precision == FV3_DENSE_BF16X3 || precision == FV3_DENSE_BF16X6 || precision == FV3_DENSE_BF16,
+    FV3_REQUIRE(precision == FV3_DENSE_BF16X3 || precision == FV3_DENSE_BF16X6,
                 "dense_forward_ex: unknown precision %d", precision);
     FV3_REQUIRE(m, "dense_forward_ex: NULL model");
     const B3Pack* pk = m->b3;
-    if (precision == FV3_DENSE_BF16X6 || precision == FV3_DENSE_BF16) {
-        const int st = lazy_stream(m, precision == FV3_DENSE_BF16X6 ? 3 : 1, &pk);
+    if (precision == FV3_DENSE_BF16X6) {
+        const int st = b6_stream(m, &pk);
         if (st == FV3_ERR_HIP) return st;
         if (st != FV3_OK) pk = nullptr;
     }
@@ -1422,9 +1416,7 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
             if (sl == 2) return by_hu(std::integral_constant<int, 2>{});
         return sl == 3 ? by_hu(std::integral_constant<int, 3>{}) : by_hu(std::integral_constant<int, 0>{});
     };
-    const void* kfn = b.ns == 3   ? pick(std::integral_constant<int, 3>{})
-                      : b.ns == 2 ? pick(std::integral_constant<int, 2>{})
-                                  : pick(std::integral_constant<int, 1>{});
+    const void* kfn = b.ns == 3 ? pick(std::integral_constant<int, 3>{}) : pick(std::integral_constant<int, 2>{});
     const size_t lds = lds_of(sl);
     FV3_REQUIRE(lds <= 160 * 1024, "dense_forward_ex: model needs %zu bytes of LDS", lds);
     static std::vector<std::pair<std::pair<const void*, size_t>, int>> resident;

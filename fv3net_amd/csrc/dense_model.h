@@ -72,7 +72,7 @@ struct DenseArgs {
 };
 static_assert(sizeof(DenseArgs) <= 4096, "kernel arguments are limited to 4 KiB");
 
-struct B3Pack;  // dense_b3.hip: a bf16 split weight stream (bf16 / bf16x3 / bf16x6) and its constants
+struct B3Pack;  // dense_b3.hip: a bf16 split weight stream (bf16x3 / bf16x6) and its constants
 struct B3Desc;  // dense_b3.hip: a host copy of the model description (the bf16x6 stream is packed from it on first use)
 
 }  // namespace fv3
@@ -88,9 +88,7 @@ struct fv3_dense_model {
     fv3::DenseArgs tmpl{};  // device pointers filled, per-call fields empty
     fv3::B3Pack* b3 = nullptr;  // bf16x3 weight stream (2 bf16 parts per weight)
     fv3::B3Pack* b6 = nullptr;  // bf16x6 weight stream (3 parts), packed on the first bf16x6 forward
-    fv3::B3Pack* b1 = nullptr;  // bf16 weight stream (1 part), packed on the first bf16 forward
-    bool b6_tried = false, b1_tried = false;  // a lazy pack was attempted (unsupported: not retried)
-    fv3::B3Desc* b6_src = nullptr;  // what b6 / b1 are packed from (kept with the model)
+    fv3::B3Desc* b6_src = nullptr;  // what b6 is packed from (released once packed)
 };
 
 namespace fv3 {

@@ -89,8 +89,7 @@ def _glorot(rng, fan_in, fan_out):
     return rng.uniform(-lim, lim, size=(fan_in, fan_out)).astype(np.float32)
 
 
-PRECISIONS = {"f32": _native.DENSE_F32, "bf16x3": _native.DENSE_BF16X3, "bf16x6": _native.DENSE_BF16X6,
-              "bf16": _native.DENSE_BF16}
+PRECISIONS = {"f32": _native.DENSE_F32, "bf16x3": _native.DENSE_BF16X3, "bf16x6": _native.DENSE_BF16X6}
 
 
 class DenseColumnModel:

@@ -170,15 +170,11 @@ int fv3_dense_forward_f64in(const fv3_dense_model* model, const double* const* i
  *   FV3_DENSE_BF16X6  every f32 operand split into bf16 hi + mid + lo (~24 mantissa
  *                     bits), products as the six split terms of order <= 2
  *                     (hi*hi, mid*hi, hi*mid, mid*mid, lo*hi, hi*lo), f32 accumulation:
- *                     f32-level error, within the 1e-5 rel tendency contract;
- *   FV3_DENSE_BF16    every operand (normalised inputs, activations, weights) rounded to
- *                     bf16, one v_mfma_f32_16x16x32_bf16 per product, f32 accumulation:
- *                     BASELINE config #5's arithmetic (bf16 MFMA, 1e-3 rel).
+ *                     f32-level error, within the 1e-5 rel tendency contract.
  * Same graph, layouts and in-place semantics as fv3_dense_forward. */
 #define FV3_DENSE_F32 0
 #define FV3_DENSE_BF16X3 1
 #define FV3_DENSE_BF16X6 2
-#define FV3_DENSE_BF16 3
 int fv3_dense_forward_ex(const fv3_dense_model* model, const float* const* inputs,
                          const fv3_layout* in_l, float* const* outputs, const fv3_layout* out_l,
                          int64_t ncol, int precision, void* stream);

@@ -58,12 +58,9 @@ def b3_stage(request, monkeypatch):
     return request.param
 
 
-@pytest.fixture(autouse=True, params=[("bf16x3", 1e-4), ("bf16x6", 1e-5), ("bf16", 2e-2)], ids=["b3", "b6", "b1"])
+@pytest.fixture(autouse=True, params=[("bf16x3", 1e-4), ("bf16x6", 1e-5)], ids=["b3", "b6"])
 def split_parts(request):
-    """Every test with two (bf16x3, bound 1e-4) and three (bf16x6, bound 1e-5) bf16 parts,
-    and with one (bf16: every operand rounded to bf16, config #5's arithmetic; 2e-2 here
-    on models with no emulator structure, where an operand layout or permutation error
-    would be O(1); the emulator is held to its 1e-3 contract in test_emulator.py)."""
+    """Every test with two (bf16x3, bound 1e-4) and three (bf16x6, bound 1e-5) bf16 parts."""
     global PREC, RTOL_B3
     PREC, RTOL_B3 = request.param
     yield request.param
