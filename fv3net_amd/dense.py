@@ -12,6 +12,7 @@ Weights are held in Keras' own layout (kernel ``[fan_in, fan_out]``, bias
 import ctypes
 import dataclasses
 import os
+import weakref
 from typing import Dict, List, Mapping, Optional, Sequence, Tuple
 
 import numpy as np
@@ -105,6 +106,7 @@ class DenseColumnModel:
         self.config = config
         self.params = dict(params)
         self._handles: Dict[int, int] = {}
+        self._plans = weakref.WeakSet()  # LaunchPlans holding a bound forward of this model
         self.precision = precision
         self._validate()
 
@@ -265,8 +267,14 @@ class DenseColumnModel:
         return h.value
 
     def close(self):
+        """Free the native model handles.  Refused while a live LaunchPlan holds a bound
+        forward of this model (the native plan replays the raw handle); a BoundForward
+        called after close() raises instead of launching on the freed handle."""
         if not self._handles:
             return
+        if any(p._h for p in list(self._plans)):
+            raise RuntimeError("DenseColumnModel.close: a LaunchPlan still replays a bound forward of this "
+                               "model; close the plan first")
         lib = _native.load()
         for h in self._handles.values():
             lib.fv3_dense_destroy(h)
@@ -544,6 +552,8 @@ class BoundForward:
     def __call__(self, stream=None):
         """``stream``: a torch stream, a raw hipStream_t handle (int), or None (current)."""
         h = stream if isinstance(stream, int) else _device.stream_handle(stream, self.inputs + self.outputs)
+        if self._handle not in self.model._handles.values():
+            raise RuntimeError("BoundForward: the model was closed; bind again")
         if self._in64:
             st = self._fn(self._handle, self._in_ptrs, self._in_l, self._out_ptrs, self._out_l, self._ncol, h)
         else:

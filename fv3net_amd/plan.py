@@ -50,6 +50,8 @@ class LaunchPlan:
             st = lib.fv3_plan_add_dense_forward(
                 self._h, bound._handle, ctypes.cast(bound._in_ptrs, ctypes.POINTER(ctypes.c_void_p)), bound._in_l,
                 bound._out_ptrs, bound._out_l, bound._ncol, bound._prec, int(bound._in64))
+            if not st:
+                bound.model._plans.add(self)  # the model refuses close() while this plan lives
         elif isinstance(bound, BoundEpilogue):
             st = lib.fv3_plan_add_ml_epilogue(self._h, ctypes.byref(bound._io), *bound._args[1:])
         elif isinstance(bound, _device.BoundLaunch) and getattr(bound.fn, "__name__", None) in _PLAN_OPS:

@@ -90,3 +90,28 @@ def test_plan_refuses_unknown_ops(gpu):
     torch.cuda.synchronize()
     assert torch.equal(x, y)
     assert all(torch.equal(z[t], x) for t in range(3))
+
+
+def test_model_close_refused_while_a_plan_replays_it(gpu):
+    """The native plan replays the model's raw handle: close() is refused while a live
+    plan holds a bound forward of the model, allowed once the plan is closed; a bound
+    forward called after close() raises rather than launching on the freed handle."""
+    import torch
+
+    from fv3net_amd import workloads as W
+    from fv3net_amd.plan import LaunchPlan
+
+    wl = W.make_dense_workload(12, seed=2)
+    bound = wl.model.bind(wl.inputs, level_axes=[1, 1])
+    plan = LaunchPlan([bound])
+    with pytest.raises(RuntimeError, match="LaunchPlan"):
+        wl.model.close()
+    plan()
+    torch.cuda.synchronize()
+    plan.close()
+    wl.model.close()
+    with pytest.raises(RuntimeError, match="closed"):
+        bound()
+    # a fresh bind after close makes a new handle and runs
+    wl.model.bind(wl.inputs, level_axes=[1, 1])()
+    torch.cuda.synchronize()
