@@ -21,7 +21,10 @@ import numpy as np
 
 
 def _shape(data) -> Tuple[int, ...]:
-    return tuple(int(s) for s in data.shape)
+    shape = data.shape
+    if type(shape) is tuple:  # numpy: already ints
+        return shape
+    return tuple(int(s) for s in shape)
 
 
 def _to_numpy(data):
@@ -48,6 +51,14 @@ class DataArray:
                 self.coords[k] = np.asarray(v)
         self.attrs = dict(attrs or {})
         self.name = name
+
+    @classmethod
+    def _view(cls, data, dims, coords, attrs, name):
+        """A DataArray over already-validated parts (a Dataset's own variable), no copies
+        or checks: the hot path of ``Dataset.__getitem__``."""
+        da = cls.__new__(cls)
+        da.data, da.dims, da.coords, da.attrs, da.name = data, dims, coords, attrs, name
+        return da
 
     @property
     def shape(self):
@@ -82,6 +93,7 @@ class Dataset:
     def __init__(self, data_vars: Optional[Mapping] = None, coords: Optional[Mapping] = None,
                  attrs: Optional[Mapping] = None):
         self._vars: "OrderedDict[Hashable, DataArray]" = OrderedDict()
+        self._sizes: Dict[Hashable, int] = {}  # dim -> size over the variables (kept by __setitem__)
         self.coords: Dict[Hashable, np.ndarray] = OrderedDict((k, np.asarray(v)) for k, v in (coords or {}).items())
         self.attrs = dict(attrs or {})
         for k, v in (data_vars or {}).items():
@@ -92,14 +104,22 @@ class Dataset:
             value = DataArray(value[1], value[0])
         if not isinstance(value, DataArray):
             raise TypeError("Dataset values must be DataArray or (dims, data)")
-        for d, n in value.sizes.items():
-            other = self.dims.get(d)
+        sizes = dict(zip(value.dims, value.shape))
+        for d, n in sizes.items():
+            other = self._sizes.get(d)
             if other is not None and other != n:
                 raise ValueError(f"conflicting sizes for dimension {d!r}: {n} vs {other}")
         for k, v in value.coords.items():
             self.coords.setdefault(k, v)
         value.name = name
+        replaced = name in self._vars
         self._vars[name] = value
+        if replaced:  # the old variable's dims may be gone
+            self._sizes = {}
+            for v in self._vars.values():
+                self._sizes.update(zip(v.dims, v.shape))
+        else:
+            self._sizes.update(sizes)
 
     def __getitem__(self, key):
         if isinstance(key, (list, tuple)) and not (isinstance(key, tuple) and key in self._vars):
@@ -111,8 +131,8 @@ class Dataset:
                                  {key: c} if c.ndim == 1 else None, name=key)
             raise KeyError(key)
         da = self._vars[key]
-        coords = {d: self.coords[d] for d in da.dims if d in self.coords}
-        return DataArray(da.data, da.dims, coords, da.attrs, key)
+        coords = OrderedDict((d, self.coords[d]) for d in da.dims if d in self.coords)
+        return DataArray._view(da.data, da.dims, coords, dict(da.attrs), key)
 
     def __contains__(self, key):
         return key in self._vars
@@ -133,9 +153,7 @@ class Dataset:
     @property
     def dims(self) -> Mapping[Hashable, int]:
         """Sorted mapping dim -> size (xarray 0.19 SortedKeysDict semantics)."""
-        sizes: Dict[Hashable, int] = {}
-        for v in self._vars.values():
-            sizes.update(v.sizes)
+        sizes = self._sizes
         return OrderedDict((d, sizes[d]) for d in sorted(sizes, key=str))
 
     @property

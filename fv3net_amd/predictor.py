@@ -232,6 +232,56 @@ class DenseColumnPredictor(Predictor):
     # -- predict ----------------------------------------------------------------
     def predict(self, X):
         xr_in = dsmod.is_xarray(X)
+        plan = None
+        if not xr_in and isinstance(X, dsmod.Dataset):
+            # the call's layout decisions depend only on the variables' names, dims, shapes
+            # and array kinds: a prognostic run passes the same layout every step
+            sig = tuple((k, v.dims, v.data.shape, type(v.data), getattr(v.data, "dtype", None))
+                        for k, v in X.data_vars.items())
+            cache = self.__dict__.setdefault("_plans", {})
+            plan = cache.get(sig)
+            if plan is None:
+                plan = self._plan(X)
+                if len(cache) > 16:
+                    cache.clear()
+                cache[sig] = plan
+        else:
+            plan = self._plan(X)
+        in_specs, out_specs, host, src_is_torch = plan
+        own = isinstance(X, dsmod.Dataset)
+        tensors, axes = [], []
+        for name, axis, perm, lead in in_specs:
+            data = X.data_vars[name].data if own else dsmod.variable_data(X, name)
+            is_torch = torch is not None and isinstance(data, torch.Tensor)
+            if perm is not None:
+                data = data.permute(*perm) if is_torch else np.transpose(np.asarray(data), perm)
+            elif not is_torch:
+                data = np.asarray(data)
+            if lead:
+                data = data[None, ...]
+            tensors.append(_as_contig(data))
+            axes.append(axis)
+        if host:
+            outs = self._host_forward(tensors, axes)  # numpy in, numpy out
+        else:
+            outs = self.model.forward(tensors, level_axes=axes)
+        result = {}
+        for (name, reshape, tgt, perm), t in zip(out_specs, outs):
+            if reshape is not None:  # scalar_singleton_dim squeeze (pure_keras.py:85-90)
+                t = t.reshape(reshape)
+            if isinstance(t, np.ndarray):
+                t = t if perm is None else np.ascontiguousarray(np.transpose(t, perm))
+            else:
+                t = (t if perm is None else t.permute(*perm)).contiguous()
+            result[name] = (tgt, t)
+        return _make_output(X, result, xr_in, src_is_torch)
+
+    def _plan(self, X):
+        """Validate X against the model and fix the call's layout: per input (name, the
+        level axis the kernel reads, the permutation to [level] + column order or None,
+        a level axis to add for a 2-D input), per output (name, the squeeze shape of a
+        one-level output, the output dims in the input's order, the permutation there or
+        None), whether the call is numpy in / numpy out, whether X holds torch data."""
         cfg = self.model.config
         all_dims = list(dsmod.dataset_dims(X))
         stack_dims = [d for d in all_dims if d not in self._unstacked_dims]
@@ -246,54 +296,41 @@ class DenseColumnPredictor(Predictor):
         first = sub[self.input_variables[0]]
         col_dims = [d for d in first.dims if d not in self._unstacked_dims]
         col_shape = [dict(zip(first.dims, first.shape))[d] for d in col_dims]
-        tensors, axes = [], []
+        in_specs, axes, host = [], [], True
         for v, name in enumerate(self.input_variables):
             da = sub[name]
             lv = _level_dim(da.dims, self._unstacked_dims)
             if set(d for d in da.dims if d != lv) != set(col_dims):
                 raise ValueError(f"{name} dims {da.dims} do not share the horizontal dims {col_dims}")
             data = dsmod.variable_data(X, name)
-            is_torch = torch is not None and isinstance(data, torch.Tensor)
+            host = host and not (torch is not None and isinstance(data, torch.Tensor)) and \
+                np.asarray(data).dtype in (np.float32, np.float64)
             if lv and [d for d in da.dims if d != lv] == col_dims:
                 # horizontal dims already in column order: the kernel reads the array in
                 # place with the level axis where it is, e.g. (tile, z, y, x)
-                tensors.append(data if is_torch else np.asarray(data))
+                in_specs.append((name, da.dims.index(lv), None, False))
                 axes.append(da.dims.index(lv))
                 continue
             order = ([lv] if lv else []) + col_dims
             perm = [da.dims.index(d) for d in order]
-            if is_torch:
-                t = data.permute(*perm) if perm != list(range(len(perm))) else data
-            else:
-                t = np.transpose(np.asarray(data), perm) if perm != list(range(len(perm))) else np.asarray(data)
-            tensors.append(t if lv else t[None, ...])
+            in_specs.append((name, 0, perm if perm != list(range(len(perm))) else None, not lv))
             axes.append(0)
-        tensors = [_as_contig(t) for t in tensors]
-        if all(isinstance(t, np.ndarray) and t.dtype in (np.float32, np.float64) for t in tensors):
-            outs = self._host_forward(tensors, axes)  # numpy in, numpy out
-        else:
-            outs = self.model.forward(tensors, level_axes=axes)
         # back to the input's dim order (match_prediction_to_input_coords)
         order = dsmod.infer_dimension_order(X)
-        result = {}
+        out_specs = []
         ax0 = axes[0]  # the outputs carry their level axis where the first input had it
         for o, name in enumerate(self.output_variables):
-            nz = cfg.out_nz[o]
-            t = outs[o]
-            if nz == 1:  # scalar_singleton_dim squeeze (pure_keras.py:85-90)
-                dims = list(col_dims)
-                t = t.reshape(col_shape)
+            dims = list(col_dims)
+            reshape = None
+            if cfg.out_nz[o] == 1:
+                reshape = tuple(col_shape)
             else:
-                dims = list(col_dims)
                 dims.insert(ax0, self._unstacked_dims[0])
             tgt = [d for d in order if d in dims] + [d for d in dims if d not in order]
             perm = [dims.index(d) for d in tgt]
-            if isinstance(t, np.ndarray):
-                t = t if perm == list(range(len(perm))) else np.ascontiguousarray(np.transpose(t, perm))
-            else:
-                t = t.permute(*perm).contiguous()
-            result[name] = (tgt, t)
-        return _make_output(X, result, xr_in)
+            out_specs.append((name, reshape, tgt, perm if perm != list(range(len(perm))) else None))
+        src_is_torch = any(torch is not None and isinstance(dsmod.variable_data(X, n), torch.Tensor) for n in X)
+        return in_specs, out_specs, host, src_is_torch
 
     def _host_forward(self, arrays, axes):
         """Host arrays in, host float32 arrays out, for the drop-in call on numpy data
@@ -337,7 +374,7 @@ def _to_host(t) -> np.ndarray:
     return t.detach().numpy()
 
 
-def _make_output(X, result: Dict, xr_in: bool):
+def _make_output(X, result: Dict, xr_in: bool, src_is_torch: Optional[bool] = None):
     """Build the output dataset of the input's kind; coords copied from the input."""
     coords = getattr(X, "coords", {})
     if xr_in:
@@ -349,7 +386,8 @@ def _make_output(X, result: Dict, xr_in: bool):
             data_vars[name] = xr.DataArray(arr, dims=dims, coords={d: coords[d] for d in dims if d in coords})
         return xr.Dataset(data_vars)
     out = dsmod.Dataset()
-    src_is_torch = any(torch is not None and isinstance(dsmod.variable_data(X, n), torch.Tensor) for n in X)
+    if src_is_torch is None:
+        src_is_torch = any(torch is not None and isinstance(dsmod.variable_data(X, n), torch.Tensor) for n in X)
     for name, (dims, t) in result.items():
         data = t
         if not src_is_torch and hasattr(t, "detach"):
