@@ -438,6 +438,7 @@ def predict_mappm_host_to_host(dev, res=384, steps=5, bands=6):
                               out=[r[:, c0:c1] for r in wl.remapped])
         runs.append((c0, c1, bound, plan))
     s_out = torch.cuda.Stream(device=dev)
+    s_idle = torch.cuda.Stream(device=dev)  # transfer.copy_fence
 
     def step():
         cur = torch.cuda.current_stream()
@@ -446,6 +447,7 @@ def predict_mappm_host_to_host(dev, res=384, steps=5, bands=6):
             # stream: the host waits for them while band b - 1's out-copies run on s_out)
             for h, d in ((T2, dT), (q2, dq), (pe1, d1), (pe2, d2)):
                 transfer.copy_band(d[:, c0:c1], h[:, c0:c1], cur.cuda_stream)
+            transfer.copy_fence(cur, s_idle)
             bound(cur)
             plan()
             for h, r in zip(host_out, wl.remapped):  # arena outputs: asynchronous DMA

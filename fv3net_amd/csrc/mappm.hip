@@ -575,6 +575,83 @@ __global__ __launch_bounds__(256) void mappm_ppm_pair_kernel(MappmPairArgs a)
     mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0>(d, a.km, a.kn, a.iv, a.kord);
 }
 
+// Small grids with one lane per column left the SIMDs short of waves (one rank's share
+// of C384 at world 8, 110,592 columns: 1.7 waves per SIMD, the serial remap's latency
+// unhidden).  Here each column runs on TWO lanes of one wave, l and l + 32 (each half
+// wave reads 32 consecutive columns): the first streams outputs 1 .. kB - 1, the second
+// kB .. kn from the input layer where the single pass begins output kB (mappm_multi.h,
+// "two lanes per column"), both on the same loop, so a wave's trip count is the longer
+// half's.  The pressure scans that prove the split exact are shared the same way (pe1
+// on the first lane, pe2 on the second, exchanged by a lane shuffle); a column that
+// fails them runs the single pass on its first lane.
+__global__ __launch_bounds__(256) void mappm_ppm_pair_split_kernel(MappmPairArgs a)
+{
+    const int lane = threadIdx.x & 63;
+    const int part = lane >> 5;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t c0 = wave * 32 + (lane & 31);
+    const bool valid = c0 < a.ncol;
+    const int64_t c = valid ? c0 : a.ncol - 1;  // spare lanes scan the last column, then leave
+    DevColPair d;
+    d.pe1_ = a.pe1 + col_offset(a.l_pe1, c);
+    d.pe2_ = a.pe2 + col_offset(a.l_pe2, c);
+    d.ld_pe1 = a.l_pe1.ld;
+    d.ld_pe2 = a.l_pe2.ld;
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+        d.q1_[f] = a.q1[f] + col_offset(a.l_q1[f], c);
+        d.q2_[f] = a.q2[f] + col_offset(a.l_q2[f], c);
+        d.ld_q1[f] = a.l_q1[f].ld;
+        d.ld_q2[f] = a.l_q2[f].ld;
+    }
+    d.kn = a.kn;
+    const int km = a.km, kn = a.kn;
+    const int kB = kn / 2 + 1;
+    int ok = 0, cnt = 0;
+    if (kn >= 2) {
+        if (part == 0)
+            split_scan_pe1(d, km, d.pe2(kB), ok, cnt);
+        else
+            ok = split_scan_pe2(d, kn);
+    }
+    const int both = ok & __shfl_xor(ok, 32);
+    const int cnt0 = __shfl(cnt, lane & 31);  // the first lane's count
+    if (!valid) return;
+    if (!both) {  // unsorted or NaN edges, or one output layer: the single pass
+        if (part == 0) {
+            d.pe2_next = d.pe2_ + 2 * d.ld_pe2;
+            d.nb = kn >= 2 ? *d.pe2_next : 0.0f;
+            mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0>(d, km, kn, a.iv, a.kord);
+        }
+        return;
+    }
+    if (part == 0) {
+        d.pe2_next = d.pe2_ + 2 * d.ld_pe2;
+        d.nb = *d.pe2_next;  // kn >= 2
+        mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0, true>(d, km, kn, a.iv, a.kord, 1, kB - 1, 1);
+    } else {
+        // outputs from kB on: the output pointers and the edge cursor where the single
+        // pass has them once output kB - 1 is written
+        for (int f = 0; f < 2; ++f) d.q2_[f] += (int64_t)(kB - 1) * d.ld_q2[f];
+        d.pe2_next = d.pe2_ + (int64_t)(kB + 1) * d.ld_pe2;
+        d.nb = (kB + 2 <= kn + 1) ? *d.pe2_next : 0.0f;
+        const int L0 = split_first_layer(d, km, d.pe2(kB), cnt0);
+        mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0, true>(d, km, kn, a.iv, a.kord, kB, kn, L0);
+    }
+}
+
+// the two-lane pair kernel between the level-parallel kernel's range and this many
+// columns (FV3_MAPPM_SPLIT=0|1 for A/B: never / from kLevelsMaxCols on)
+constexpr int64_t kSplitMaxCols = 262144;
+
+bool use_split_kernel(int64_t ncol)
+{
+    const char* p = fv3::variant_env("FV3_MAPPM_SPLIT");
+    if (p && p[0] == '0') return false;
+    if (p && p[0] == '1') return true;
+    return ncol < kSplitMaxCols;
+}
+
 }  // namespace fv3
 
 using fv3::MappmArgs;
@@ -635,8 +712,13 @@ extern "C" int fv3_mappm_multi(const float* pe1, fv3_layout pe1_l, const float* 
             fv3::MappmPairArgs a{pe1, pe2, pe1_l, pe2_l, {q1[f], q1[f + 1]}, {q2[f], q2[f + 1]},
                                  {q1_l[f], q1_l[f + 1]}, {q2_l[f], q2_l[f + 1]}, ncol, km, kn, iv, kord};
             const int block = 256;
-            const int64_t grid = (ncol + block - 1) / block;
-            hipLaunchKernelGGL(fv3::mappm_ppm_pair_kernel, dim3((unsigned)grid), dim3(block), 0, s, a);
+            if (fv3::use_split_kernel(ncol)) {  // two lanes per column: 64 threads per 32 columns
+                const int64_t grid = ((ncol + 31) / 32 * 64 + block - 1) / block;
+                hipLaunchKernelGGL(fv3::mappm_ppm_pair_split_kernel, dim3((unsigned)grid), dim3(block), 0, s, a);
+            } else {
+                const int64_t grid = (ncol + block - 1) / block;
+                hipLaunchKernelGGL(fv3::mappm_ppm_pair_kernel, dim3((unsigned)grid), dim3(block), 0, s, a);
+            }
             FV3_LAUNCH_CHECK();
         }
     }

@@ -233,29 +233,118 @@ FV3_HD inline void remap_finish_n(RemapStateN<NF>& s, const ColumnEndsN<NF>& e, 
     }
 }
 
+// ---- two lanes per column (small grids): where the second lane starts ----
+// A column's outputs split at kB: one lane streams outputs 1 .. kB - 1 from input layer
+// 1, the other outputs kB .. kn from the input layer L0 where the single streaming pass
+// begins output kB.  With non-decreasing pe1 and pe2 that is the first L with
+// pe2(kB) <= pe1(L + 1) (pe1(1) < pe2(kB) < pe1(km + 1); an output's top edge lies in the
+// layer where the previous output ended, and no earlier layer reaches it), i.e.
+// L0 = 1 + #{L : pe1(L + 1) < pe2(kB)}.  The scan is split so each lane does one half:
+// split_scan_pe1 (non-decreasing pe1, the count), split_scan_pe2 (non-decreasing pe2);
+// a column failing either (or holding NaNs) runs the single pass on one lane.
+template <class Col>
+FV3_HD inline void split_scan_pe1(Col& c, int km, float t, int& ok, int& cnt)
+{
+    float prev = c.pe1(1);
+    ok = 1;
+    cnt = 0;
+    for (int k = 2; k <= km + 1; ++k) {
+        const float v = c.pe1(k);
+        ok &= prev <= v;
+        cnt += v < t;
+        prev = v;
+    }
+}
+template <class Col>
+FV3_HD inline int split_scan_pe2(Col& c, int kn)
+{
+    float prev = c.pe2(1);
+    int ok = 1;
+    for (int k = 2; k <= kn + 1; ++k) {
+        const float v = c.pe2(k);
+        ok &= prev <= v;
+        prev = v;
+    }
+    return ok;
+}
+
+// the second lane's first input layer from the pe1 count (pe2(kB) outside (pe1(1),
+// pe1(km + 1)): the boundary outputs, emitted from layer 1 on as the single pass does)
+template <class Col>
+FV3_HD inline int split_first_layer(Col& c, int km, float t, int cnt)
+{
+    return (t <= c.pe1(1) || t >= c.pe1(km + 1)) ? 1 : 1 + cnt;
+}
+
 // ---- NF columns on one pressure column, kord <= 7, fully streaming ----
 // CARRY: as mappm_ppm_column's (level L + 4's loads one iteration ahead, carried across
 // the back edge, or at the iteration's start); same loads, same bits.
-template <int NF, class Col, bool CARRY = false>
-FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord)
+// SPLIT: this lane emits outputs k_first .. k_last only (a column on two lanes, above).
+// k_first > 1 starts the remap fresh at output k_first: from input layer L_first with
+// the window E_{L_first} built directly from its local stencil (every entry the same
+// expression on the same operands as the streaming advance computes it) when
+// 4 <= L_first <= km - 3, else from layer 1 (the layers above output k_first's top edge
+// pass without a remap event).  A lane stops once it has emitted k_last.
+template <int NF, class Col, bool CARRY = false, bool SPLIT = false>
+FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord, int k_first = 1, int k_last = 0,
+                                     int L_first = 1)
 {
     // window state E_L as in mappm_ppm_column, the q-dependent parts per field
     float qv[NF][4], dcv[NF][3], alv[NF][3], h2v[NF][3], ar_km[NF];
     float dpv[4], pev[5];
     const bool huynh = kord >= 7;
+    int L_start = 1;
+    if constexpr (SPLIT) {
+        if (k_first > 1 && L_first >= 4 && L_first <= km - 3) L_start = L_first;
+    }
+    const int kn_out = SPLIT ? k_last : kn;  // the last output this lane emits
 
+    ColumnEndsN<NF> ends;
+    ends.pe_bot = c.pe1(km + 1);
+    for (int f = 0; f < NF; ++f) ends.q_bot[f] = c.q1(f, km);
+    if (SPLIT && L_start > 1) {
+        ends.pe_top = c.pe1(1);
+        for (int f = 0; f < NF; ++f) ends.q_top[f] = c.q1(f, 1);
+        // E_{L0} from levels L0 - 3 .. L0 + 4: index i <-> level L0 - 3 + i
+        const int l0 = L_start - 3;
+        float pw[8], dw[7];
+        for (int i = 0; i < 8; ++i) pw[i] = c.pe1(l0 + i);
+        for (int i = 0; i < 7; ++i) dw[i] = pw[i + 1] - pw[i];
+        DcShared pd[6];
+        for (int i = 1; i <= 5; ++i) pd[i] = ppm_dc_shared(dw[i - 1], dw[i], dw[i + 1]);  // dc(L0-2 .. L0+2)
+        AlShared pa[6];
+        for (int i = 3; i <= 5; ++i) pa[i] = ppm_al_shared(dw[i - 2], dw[i - 1], dw[i], dw[i + 1]);  // AL(L0 .. L0+2)
+        for (int f = 0; f < NF; ++f) {
+            float qw[7], dcw[6];
+            for (int i = 0; i < 7; ++i) qw[i] = c.q1(f, l0 + i);
+            for (int i = 1; i <= 5; ++i) dcw[i] = ppm_dc_field(pd[i], qw[i - 1], qw[i], qw[i + 1], dw[i]);
+            for (int i = 0; i < 4; ++i) qv[f][i] = qw[3 + i];
+            for (int i = 0; i < 3; ++i) {
+                dcv[f][i] = dcw[3 + i];
+                alv[f][i] = ppm_al_field(pa[3 + i], dw[2 + i], dw[3 + i], qw[2 + i], qw[3 + i], dcw[2 + i], dcw[3 + i]);
+                // h2(k), k = L0 - 1 + i: the streaming advance's expression (k >= 3 here)
+                const int j = 2 + i;
+                const int k = L_start - 1 + i;
+                if (huynh && k <= km - 1) {
+                    const float hden = dw[j] + 0.5f * (dw[j - 1] + dw[j + 1]);
+                    const float d0sq = dw[j] * dw[j];
+                    h2v[f][i] = 2.0f * (dcw[j + 1] / dw[j + 1] - dcw[j - 1] / dw[j - 1]) / hden * d0sq;
+                } else {
+                    h2v[f][i] = 0.0f;
+                }
+            }
+            ar_km[f] = 0.0f;
+        }
+        for (int i = 0; i < 5; ++i) pev[i] = pw[3 + i];
+        for (int i = 0; i < 4; ++i) dpv[i] = dw[3 + i];
+    } else {
     for (int f = 0; f < NF; ++f)
         for (int i = 0; i < 4; ++i) qv[f][i] = c.q1(f, 1 + i);
     for (int i = 0; i < 5; ++i) pev[i] = c.pe1(1 + i);
     for (int i = 0; i < 4; ++i) dpv[i] = pev[i + 1] - pev[i];
 
-    ColumnEndsN<NF> ends;
     ends.pe_top = pev[0];
-    ends.pe_bot = c.pe1(km + 1);
-    for (int f = 0; f < NF; ++f) {
-        ends.q_top[f] = qv[f][0];
-        ends.q_bot[f] = c.q1(f, km);
-    }
+    for (int f = 0; f < NF; ++f) ends.q_top[f] = qv[f][0];
 
     {
         const DcShared p2 = ppm_dc_shared(dpv[0], dpv[1], dpv[2]);
@@ -277,17 +366,18 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord)
             ar_km[f] = 0.0f;
         }
     }
+    }
 
     int lmt = kord - 3;
     lmt = lmt > 0 ? lmt : 0;
     if (iv == 0) lmt = lmt < 2 ? lmt : 2;
 
     RemapStateN<NF> s;
-    s.k = 1;
+    s.k = SPLIT ? k_first : 1;
     s.accum = false;
     s.dpsum = 0.0f;
-    s.t = c.pe2(1);
-    s.b = c.pe2(2);
+    s.t = c.pe2(s.k);
+    s.b = c.pe2(s.k + 1);
     s.xt = 0.0f;
     s.xv = false;
     for (int f = 0; f < NF; ++f) s.qsum[f] = 0.0f;
@@ -295,12 +385,12 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord)
     float qc_pf[NF], pec_pf = 0.0f;
     for (int f = 0; f < NF; ++f) qc_pf[f] = 0.0f;
     if constexpr (CARRY) {
-        if (5 <= km) {
-            for (int f = 0; f < NF; ++f) qc_pf[f] = c.q1(f, 5);
-            pec_pf = c.pe1(6);
+        if (L_start + 4 <= km) {
+            for (int f = 0; f < NF; ++f) qc_pf[f] = c.q1(f, L_start + 4);
+            pec_pf = c.pe1(L_start + 5);
         }
     }
-    for (int L = 1; L <= km; ++L) {
+    for (int L = L_start; L <= km; ++L) {
         // level L + 4's q1 / pe1: carried from the previous iteration (CARRY) or read at
         // this iteration's start, as in mappm_ppm_column
         float q_pf[NF], pe_pf = pec_pf;
@@ -334,10 +424,13 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord)
             v.ar[f] = a.ar;
             v.a6[f] = a.a6;
         }
-        remap_layer_n<NF>(s, v, ends, kn, c);
+        remap_layer_n<NF>(s, v, ends, kn_out, c);
         layer_hook(c, 0);
 
         if (L == km) break;
+        if constexpr (SPLIT) {
+            if (s.k > kn_out) return;  // this lane's outputs are done
+        }
         // ---- advance the window E_L -> E_{L+1} ----
         const int j = L + 4;
         float qn[NF], pen = 0.0f, dpn = 0.0f;
@@ -393,7 +486,7 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord)
         dpv[0] = dpv[1]; dpv[1] = dpv[2]; dpv[2] = dpv[3]; dpv[3] = dpn;
         pev[0] = pev[1]; pev[1] = pev[2]; pev[2] = pev[3]; pev[3] = pev[4]; pev[4] = pen;
     }
-    remap_finish_n<NF>(s, ends, kn, c);
+    remap_finish_n<NF>(s, ends, kn_out, c);
 }
 
 // A one-field view of an NF-interface column, so NF = 1 runs the single-field

@@ -409,6 +409,7 @@ class DenseColumnModel:
             if blocks:
                 sub_axes = [ax - 1 for ax in axes]
                 runs = [self._bind_or_forward([b[t] for b in bufs], sub_axes, precision) for t in range(n0)]
+                # (an idle stream for transfer.copy_fence, the out-copy stream)
                 streams = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
             else:
                 runs = [self._bind_or_forward(bufs, axes, precision)]
@@ -442,6 +443,7 @@ class DenseColumnModel:
             # against 22.2 ms (profiles/r05g_host_ab.json, pipe_in_*)
             for a, b in zip(arrays, bufs):
                 st.h2d(a[t], out=b[t], stream=cur)
+            transfer.copy_fence(cur, streams[0])
             outs = runs[t](cur)
             if host is None:
                 host = _host_outputs(out, [(n0,) + tuple(o.shape) for o in outs])

@@ -16,11 +16,14 @@ from tests.test_mappm_gpu import _bits_equal, _columns
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["serial", "levels"])
+@pytest.fixture(params=["split", "serial", "levels"])
 def path(request, monkeypatch):
-    """`serial` (one lane per column): pairs of fields on the two-field streaming
-    kernel; `levels`: the small-grid kernel, one field per launch."""
-    set_variant(monkeypatch, "FV3_MAPPM_PATH", request.param)
+    """`split`: pairs of fields on the two-field streaming kernel, each column on two
+    lanes (the default below 262,144 columns); `serial`: the same kernel one lane per
+    column (FV3_MAPPM_SPLIT=0); `levels`: the small-grid kernel, one field per launch."""
+    set_variant(monkeypatch, "FV3_MAPPM_PATH", "levels" if request.param == "levels" else "serial")
+    if request.param != "levels":
+        set_variant(monkeypatch, "FV3_MAPPM_SPLIT", "1" if request.param == "split" else "0")
     return request.param
 
 
@@ -170,3 +173,46 @@ def test_multi_on_a_side_stream(gpu, path):
     for q, o in zip((q0, q1), outs):
         assert _bits_equal(o.cpu().numpy(), oracle_mappm(pe1, q, pe2, 1, 1))
     assert _bits_equal(one.cpu().numpy(), oracle_mappm(pe1, q1, pe2, 1, 1))
+
+
+@pytest.mark.parametrize("kn", [79, 50, 2, 1])
+def test_two_lane_pair_kernel_rank_share_size(gpu, kn, monkeypatch):
+    """One rank's share of C384 at world 8 (110,592 columns, the two-lane kernel's range
+    by default): whole arrays bit-identical to the one-lane pair kernel and sampled
+    columns to the oracle, on columns that take every start of the second lane (a
+    direct window, output kB above the top or below the bottom, kB's layer near either
+    end) and columns that keep the single pass (unsorted pe2, a NaN edge); a
+    zero-thickness layer stays on two lanes."""
+    import torch
+
+    from fv3net_amd.mappm import mappm_device_multi
+
+    rng = np.random.default_rng(110592 + kn)
+    ncol, km = 110592, 79
+    base = np.linspace(200, 1800, km, dtype=np.float32)[:, None]
+    delp = (base * rng.uniform(0.9, 1.1, (km, ncol))).astype(np.float32)
+    pe1 = np.concatenate([np.full((1, ncol), 300, np.float32), 300 + np.cumsum(delp, 0, dtype=np.float32)])
+    top, bot = pe1[0], pe1[-1]
+    a = rng.choice([-0.3, 0.0, 0.0, 0.5], ncol)
+    b = rng.choice([0.4, 1.0, 1.0, 1.3], ncol)
+    a, b = np.minimum(a, b - 0.05), b
+    frac = np.sort(rng.uniform(a, b, (kn + 1, ncol)), 0)
+    pe2 = (top + (bot - top) * frac).astype(np.float32)
+    pe2[:, :64] = pe2[::-1, :64]  # decreasing
+    pe1[40, 64:96] = np.nan
+    pe1[20, 96:128] = pe1[19, 96:128]  # a zero-thickness layer: still sorted
+    qs = [rng.normal(250, 10, (km, ncol)).astype(np.float32), rng.uniform(0, 0.02, (km, ncol)).astype(np.float32)]
+    d = [torch.from_numpy(x).cuda() for x in (pe1, pe2, *qs)]
+    default = mappm_device_multi(d[0], d[2:], d[1], 1, 1)
+    res = {}
+    for split in ("1", "0"):
+        set_variant(monkeypatch, "FV3_MAPPM_SPLIT", split)
+        res[split] = mappm_device_multi(d[0], d[2:], d[1], 1, 1)
+    for x, y, z in zip(res["1"], res["0"], default):
+        assert torch.equal(x.view(torch.int32), y.view(torch.int32))
+        assert torch.equal(x.view(torch.int32), z.view(torch.int32))
+    idx = np.concatenate([np.arange(160), np.sort(rng.choice(np.arange(160, ncol), 1500, replace=False))])
+    for q, o in zip(qs, res["1"]):
+        with np.errstate(all="ignore"):
+            ref = oracle_mappm(pe1[:, idx], q[:, idx], pe2[:, idx], 1, 1)
+        assert _bits_equal(o.cpu().numpy()[:, idx], ref)

@@ -318,3 +318,51 @@ def test_cs_register_tail_is_bit_identical(host_lib, km, kn):
                 assert host_lib.host_mappm_cs_prefetch(km, pe1.ctypes.data, q.ctypes.data, kn, pe2.ctypes.data,
                                                        out.ctypes.data, ncol, iv, kord, nt, pf) == 0
                 assert _bits_equal(out, ref), (kord, iv, nt, pf)
+
+
+@pytest.mark.parametrize("nf", [1, 2])
+@pytest.mark.parametrize("km,kn", [(4, 40), (79, 79), (79, 50), (20, 5), (12, 2), (79, 120)])
+def test_two_lane_column_split_bit_identical(host_lib, nf, km, kn):
+    """A column on two lanes (the small-grid pair kernel): outputs 1 .. kB-1 streamed from
+    layer 1, kB .. kn from the layer where the single pass begins output kB, its window
+    built from the local stencil (or, walk = 1 / out of the direct range, from layer 1).
+    Every split point, both start modes, every PPM kord and iv, on columns with
+    zero-thickness layers, shared edges, edges beyond both ends, unsorted and NaN edges
+    (which keep the single pass): the single pass's bits."""
+    fn = host_lib.host_mappm_split
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    mf = host_lib.host_mappm_multi
+    mf.restype = ctypes.c_int
+    mf.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
+    rng = np.random.default_rng(km * 31 + kn * 3 + nf)
+    ncol = 40
+    kbs = sorted({0, 2, kn} | {int(k) for k in rng.integers(2, kn + 1, 3)}) if kn >= 2 else [0]
+    for kord in (0, 1, 2, 3, 4, 5, 6, 7):
+        for iv in (0, 1, -1, 2, -2):
+            delp = rng.uniform(1, 3000, (km, ncol)).astype(np.float32)
+            delp[rng.random((km, ncol)) < 0.05] = 0.0
+            pe1 = np.concatenate([np.full((1, ncol), 300, np.float32),
+                                  300 + np.cumsum(delp, 0, dtype=np.float32)])
+            lo = rng.choice([0.5, 0.8, 1.0, 1.01], ncol)[None, :]
+            hi = rng.choice([0.9, 1.0, 1.1, 2.0], ncol)[None, :]
+            pe2 = np.sort(rng.uniform(pe1[0] * lo, pe1[-1] * hi, (kn + 1, ncol)), 0).astype(np.float32)
+            m = min(km, kn) + 1
+            pe2[: m // 3, :10] = pe1[: m // 3, :10]  # shared edges
+            pe2 = np.sort(pe2, 0)
+            pe2[:, 10:13] = pe2[::-1, 10:13]  # decreasing output edges: single pass
+            pe1[km // 2, 13] = np.nan  # NaN input edge: single pass
+            pe1[1:, 14] = pe1[:-1, 14]  # a repeated edge: zero-thickness first layer
+            q = (rng.normal(0, 1, (nf, km, ncol)) * rng.choice([1e-4, 1, 300], (nf, km, ncol))).astype(np.float32)
+            ref = np.empty((nf, kn, ncol), np.float32)
+            with np.errstate(all="ignore"):
+                assert mf(nf, km, pe1.ctypes.data, q.ctypes.data, kn, pe2.ctypes.data, ref.ctypes.data, ncol,
+                          iv, kord) == 0
+                for kb in kbs:
+                    for walk in (0, 1):
+                        out = np.full((nf, kn, ncol), 7.0, np.float32)
+                        assert fn(nf, km, pe1.ctypes.data, q.ctypes.data, kn, pe2.ctypes.data, out.ctypes.data,
+                                  ncol, iv, kord, kb, walk) == 0
+                        assert _bits_equal(out, ref), (kord, iv, kb, walk)
