@@ -397,7 +397,7 @@ def host_to_host(dev, res, steps=10):
                     "when host_path is arena); tile blocks pipelined over two streams above 64 MiB (C384)"}
 
 
-def predict_mappm_host_to_host(dev, res=384, steps=5, bands=6):
+def predict_mappm_host_to_host(dev, res=384, steps=5, bands=6, fence=True):
     """north_star's predict + mappm with the host boundary included: float64 numpy T/q
     (z, rows, x) and float32 numpy edge pressures pe1/pe2 (z+1, columns; f2py hands the
     reference's mappm float32 arrays) in, the fused predict reading float64 in place, the
@@ -447,7 +447,8 @@ def predict_mappm_host_to_host(dev, res=384, steps=5, bands=6):
             # stream: the host waits for them while band b - 1's out-copies run on s_out)
             for h, d in ((T2, dT), (q2, dq), (pe1, d1), (pe2, d2)):
                 transfer.copy_band(d[:, c0:c1], h[:, c0:c1], cur.cuda_stream)
-            transfer.copy_fence(cur, s_idle)
+            if fence:
+                transfer.copy_fence(cur, s_idle)
             bound(cur)
             plan()
             for h, r in zip(host_out, wl.remapped):  # arena outputs: asynchronous DMA

@@ -53,6 +53,8 @@ EXPORTED_SYMBOLS = (
     "fv3_level_row_sums_u8",
     "fv3_level_row_sums_f64",
     "fv3_fold_rows",
+    "fv3_step_partials_f64",
+    "fv3_fold_rows_repeat",
     "fv3_ml_epilogue",
     "fv3_ml_epilogue_ex",
     "fv3_tendency_columns",
@@ -86,7 +88,7 @@ EXPORTED_SYMBOLS = (
     "fv3_sum_squares",
     "fv3_cos_zenith",
 )
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 # fv3_dense_forward_ex precisions
 DENSE_F32 = 0
@@ -255,6 +257,8 @@ _SIGNATURES = {
     "fv3_level_row_sums_u8": (_I, [_P, _I, _I64, _I, _I64, _P, _I64, _P]),
     "fv3_level_row_sums_f64": (_I, [_P, _I, _I64, _I, _I64, _P, _I64, _P]),
     "fv3_fold_rows": (_I, [_P, _I64, _I, _P, _P]),
+    "fv3_step_partials_f64": (_I, [ctypes.POINTER(_P), _I, _P, _I64, _I, _P, _I64, _P, Layout, _I64, _I, _P, _P]),
+    "fv3_fold_rows_repeat": (_I, [_P, _I64, _I, _I, _P, _P, _P]),
     "fv3_time_blend": (_I, [_P, _I, _P, _I, _P, _I64, _D, _P]),
     "fv3_range_mask": (_I, [_P, _P, _I64, _D, _D, _I, _I, _I, _P]),
     "fv3_classify_one_hot": (_I, [_P, _I, _I64, _P, _I, _I, _I, _P]),
@@ -293,6 +297,9 @@ _SIGNATURES = {
     "fv3_plan_add_area_weighted_row_sums_f64": (_I, [_P, ctypes.POINTER(_P), _I, _P, _I64, _I, _P, _I64]),
     "fv3_plan_add_level_sums_u8": (_I, [_P, _P, Layout, _I64, _I, _P]),
     "fv3_plan_add_fold_rows": (_I, [_P, _P, _I64, _I, _P]),
+    "fv3_plan_add_step_partials_f64": (_I, [_P, ctypes.POINTER(_P), _I, _P, _I64, _I, _P, _I64, _P, Layout, _I64, _I,
+                                            _P]),
+    "fv3_plan_add_fold_rows_repeat": (_I, [_P, _P, _I64, _I, _I, _P, _P]),
     "fv3_plan_add_copy": (_I, [_P, _P, _P, ctypes.c_size_t]),
     "fv3_plan_add_repeat": (_I, [_P, _P, _P, ctypes.c_size_t, _I]),
     "fv3_copy_to_host": (_I, [_P, _P, ctypes.c_size_t, _P]),

@@ -617,27 +617,26 @@ __global__ __launch_bounds__(256) void mappm_ppm_pair_split_kernel(MappmPairArgs
     const int both = ok & __shfl_xor(ok, 32);
     const int cnt0 = __shfl(cnt, lane & 31);  // the first lane's count
     if (!valid) return;
-    if (!both) {  // unsorted or NaN edges, or one output layer: the single pass
+    // this lane's outputs [kf, kl] and first input layer; ONE call site below, so the
+    // two halves of a wave run the same loop together (separate calls would run one
+    // after the other under the exec mask)
+    int kf = 1, kl = kn, Lf = 1;
+    if (both) {
         if (part == 0) {
-            d.pe2_next = d.pe2_ + 2 * d.ld_pe2;
-            d.nb = kn >= 2 ? *d.pe2_next : 0.0f;
-            mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0>(d, km, kn, a.iv, a.kord);
+            kl = kB - 1;
+        } else {
+            kf = kB;
+            Lf = split_first_layer(d, km, d.pe2(kB), cnt0);
         }
-        return;
+    } else if (part == 1) {
+        return;  // unsorted or NaN edges, or one output layer: the single pass on the first lane
     }
-    if (part == 0) {
-        d.pe2_next = d.pe2_ + 2 * d.ld_pe2;
-        d.nb = *d.pe2_next;  // kn >= 2
-        mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0, true>(d, km, kn, a.iv, a.kord, 1, kB - 1, 1);
-    } else {
-        // outputs from kB on: the output pointers and the edge cursor where the single
-        // pass has them once output kB - 1 is written
-        for (int f = 0; f < 2; ++f) d.q2_[f] += (int64_t)(kB - 1) * d.ld_q2[f];
-        d.pe2_next = d.pe2_ + (int64_t)(kB + 1) * d.ld_pe2;
-        d.nb = (kB + 2 <= kn + 1) ? *d.pe2_next : 0.0f;
-        const int L0 = split_first_layer(d, km, d.pe2(kB), cnt0);
-        mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0, true>(d, km, kn, a.iv, a.kord, kB, kn, L0);
-    }
+    // the output pointers and the edge cursor where the single pass has them once
+    // output kf - 1 is written
+    for (int f = 0; f < 2; ++f) d.q2_[f] += (int64_t)(kf - 1) * d.ld_q2[f];
+    d.pe2_next = d.pe2_ + (int64_t)(kf + 1) * d.ld_pe2;
+    d.nb = (kf + 2 <= kn + 1) ? *d.pe2_next : 0.0f;
+    mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0, true>(d, km, kn, a.iv, a.kord, kf, kl, Lf);
 }
 
 // the two-lane pair kernel between the level-parallel kernel's range and this many

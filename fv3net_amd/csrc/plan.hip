@@ -152,6 +152,32 @@ extern "C" int fv3_plan_add_fold_rows(fv3_plan* plan, const double* rows, int64_
     return FV3_OK;
 }
 
+extern "C" int fv3_plan_add_step_partials_f64(fv3_plan* plan, const double* const* diags, int n_diag,
+                                              const double* area, int64_t nrows, int row_len, double* partial,
+                                              int64_t partial_ld, const unsigned char* limiter, fv3_layout lim_l,
+                                              int64_t ncol, int nz, double* level_out)
+{
+    using namespace fv3;
+    clear_error();
+    FV3_REQUIRE(plan && diags && n_diag >= 0, "plan_add_step_partials_f64: bad argument");
+    std::vector<const double*> d(diags, diags + n_diag);
+    plan->ops.push_back([=](void* s) {
+        return fv3_step_partials_f64(d.data(), n_diag, area, nrows, row_len, partial, partial_ld, limiter, lim_l,
+                                     ncol, nz, level_out, s);
+    });
+    return FV3_OK;
+}
+
+extern "C" int fv3_plan_add_fold_rows_repeat(fv3_plan* plan, const double* rows, int64_t nrows, int width,
+                                             int times, double* rep, double* out)
+{
+    using namespace fv3;
+    clear_error();
+    FV3_REQUIRE(plan, "plan_add_fold_rows_repeat: NULL plan");
+    plan->ops.push_back([=](void* s) { return fv3_fold_rows_repeat(rows, nrows, width, times, rep, out, s); });
+    return FV3_OK;
+}
+
 // device-to-device copy of `bytes` (hipMemcpyAsync on the plan's stream)
 extern "C" int fv3_plan_add_copy(fv3_plan* plan, void* dst, const void* src, size_t bytes)
 {

@@ -185,11 +185,9 @@ __global__ __launch_bounds__(64) void level_sums_stage2(const double* __restrict
 // uint8 counts of one band, one block per level: 16-byte loads, each summed by four
 // v_sad_u8 (|b - 0| summed over the word's bytes, exact), then the block's integer sum
 // (exact in any order) written as a double.  Rows 16-byte aligned (host check).
-__global__ __launch_bounds__(kSumBlock) void level_counts_u8_vec(const unsigned char* __restrict__ x, int64_t ld,
-                                                                 int64_t ncol, double* __restrict__ out)
+__device__ __forceinline__ void level_count_u8(const unsigned char* __restrict__ x, int64_t ld, int64_t ncol, int k,
+                                               double* __restrict__ out, double* sh)
 {
-    __shared__ double sh[kSumBlock / 64];
-    const int k = blockIdx.y;
     const unsigned char* row = x + (int64_t)k * ld;
     const int64_t nv = ncol / 16;
     unsigned s = 0;
@@ -209,6 +207,13 @@ __global__ __launch_bounds__(kSumBlock) void level_counts_u8_vec(const unsigned 
         for (int v = 1; v < kSumBlock / 64; ++v) t += sh[v];
         out[k] = t;
     }
+}
+
+__global__ __launch_bounds__(kSumBlock) void level_counts_u8_vec(const unsigned char* __restrict__ x, int64_t ld,
+                                                                 int64_t ncol, double* __restrict__ out)
+{
+    __shared__ double sh[kSumBlock / 64];
+    level_count_u8(x, ld, ncol, blockIdx.y, out, sh);
 }
 
 }  // namespace
@@ -350,12 +355,11 @@ extern "C" int fv3_area_weighted_sums_f64(const double* const* diags, int n_diag
 namespace fv3 {
 namespace {
 
+// row r's partials on one wave (lane = threadIdx.x % 64)
 template <typename T>
-__global__ __launch_bounds__(64) void area_row_sums_kernel(DiagPtrs<T> d, int n_diag, const T* __restrict__ area,
-                                                           int row_len, double* __restrict__ out, int64_t out_ld)
+__device__ __forceinline__ void area_row_sum(const DiagPtrs<T>& d, int n_diag, const T* __restrict__ area, int row_len,
+                                             double* __restrict__ out, int64_t out_ld, int64_t r, int lane)
 {
-    const int64_t r = blockIdx.x;
-    const int lane = threadIdx.x;
     const T* a = area + r * row_len;
     double sa = 0.0;
     for (int c = lane; c < row_len; c += 64) sa += (double)a[c];
@@ -371,6 +375,55 @@ __global__ __launch_bounds__(64) void area_row_sums_kernel(DiagPtrs<T> d, int n_
             o[2 * j + 1] = sa;
         }
     }
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void area_row_sums_kernel(DiagPtrs<T> d, int n_diag, const T* __restrict__ area,
+                                                           int row_len, double* __restrict__ out, int64_t out_ld)
+{
+    area_row_sum(d, n_diag, area, row_len, out, out_ld, blockIdx.x, threadIdx.x);
+}
+
+// One step's per-rank reductions in ONE launch (the stepper step's area-weighted row
+// partials and limiter level counts): blocks [0, nb_rows) take four grid
+// rows each, one wave per row, exactly as area_row_sums_kernel (same lanes, same order);
+// the nz blocks after them one level's uint8 count each, exactly as level_counts_u8_vec.
+// Two launches of ~5 us became one on one rank's share.
+__global__ __launch_bounds__(kSumBlock) void step_partials_kernel(DiagPtrs<double> d, int n_diag,
+                                                                  const double* __restrict__ area, int64_t nrows,
+                                                                  int row_len, double* __restrict__ partial,
+                                                                  int64_t partial_ld, const unsigned char* __restrict__ lim,
+                                                                  int64_t lim_ld, int64_t ncol,
+                                                                  double* __restrict__ level_out)
+{
+    __shared__ double sh[kSumBlock / 64];
+    const int64_t nb_rows = (nrows + 3) / 4;
+    if ((int64_t)blockIdx.x < nb_rows) {
+        const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+        if (r < nrows) area_row_sum(d, n_diag, area, row_len, partial, partial_ld, r, threadIdx.x & 63);
+        return;  // no block-wide barrier on this side
+    }
+    level_count_u8(lim, lim_ld, ncol, (int)(blockIdx.x - nb_rows), level_out, sh);
+}
+
+// the stub exchange's copy and the fold in one launch: rep[t * nrows + r][j] =
+// rows[r][j] for t < times (the bytes an all-gather of `times` ranks' partials moves),
+// and out[j] folded over rep's rows exactly as fold_rows_kernel (lane l the rows
+// l, l + 64, ... in order, then the butterfly): each lane sums the values it writes
+__global__ __launch_bounds__(64) void fold_rows_repeat_kernel(const double* __restrict__ rows, int64_t nrows, int width,
+                                                              int times, double* __restrict__ rep,
+                                                              double* __restrict__ out)
+{
+    const int j = blockIdx.x;
+    const int64_t n = nrows * times;
+    double s = 0.0;
+    for (int64_t r = threadIdx.x; r < n; r += 64) {
+        const double v = rows[(r % nrows) * width + j];
+        rep[r * width + j] = v;
+        s += v;
+    }
+    s = wave_sum(s);
+    if (threadIdx.x == 0) out[j] = s;
 }
 
 // per (row, level) sums of a (nz, nrows, row_len) float64 field: out[r][k], one wave each
@@ -500,6 +553,52 @@ extern "C" int fv3_fold_rows(const double* rows, int64_t nrows, int width, doubl
     FV3_REQUIRE(rows && out, "fold_rows: NULL array");
     hipLaunchKernelGGL(fv3::fold_rows_kernel, dim3((unsigned)width), dim3(64), 0, (hipStream_t)stream, rows, nrows,
                        width, out);
+    FV3_LAUNCH_CHECK();
+    return FV3_OK;
+}
+
+extern "C" int fv3_step_partials_f64(const double* const* diags, int n_diag, const double* area, int64_t nrows,
+                                     int row_len, double* partial, int64_t partial_ld, const unsigned char* limiter,
+                                     fv3_layout lim_l, int64_t ncol, int nz, double* level_out, void* stream)
+{
+    using namespace fv3;
+    clear_error();
+    FV3_REQUIRE(n_diag >= 1 && n_diag <= 64, "step_partials: n_diag must be in [1, 64]");
+    FV3_REQUIRE(nrows >= 1 && nrows < 0x7fffffff && row_len >= 1 && partial_ld >= 2 * n_diag,
+                "step_partials: bad row sizes nrows=%lld row_len=%d ld=%lld", (long long)nrows, row_len,
+                (long long)partial_ld);
+    FV3_REQUIRE(ncol >= 0 && nz >= 1 && nz <= 65535, "step_partials: bad sizes ncol=%lld nz=%d", (long long)ncol, nz);
+    FV3_REQUIRE(diags && area && partial && limiter && level_out, "step_partials: NULL array");
+    FV3_REQUIRE(ncol == 0 || layout_ok(lim_l, ncol), "step_partials: bad limiter layout");
+    for (int j = 0; j < n_diag; ++j) FV3_REQUIRE(diags[j], "step_partials: NULL diagnostic %d", j);
+    // the fused launch reads the limiter rows as level_counts_u8_vec does; anything else
+    // takes the two launches it fuses
+    const bool vec = ncol > 0 && (lim_l.ncol_blk <= 0 || lim_l.ncol_blk >= ncol) && ((uintptr_t)limiter % 16) == 0 &&
+                     (lim_l.ld % 16) == 0 && lim_l.ld >= 0 && ncol <= ((int64_t)1 << 24);
+    if (!vec || variant_env("FV3_STEP_PARTIALS_SPLIT")) {
+        const int st = fv3_area_weighted_row_sums_f64(diags, n_diag, area, nrows, row_len, partial, partial_ld, stream);
+        if (st != FV3_OK) return st;
+        return fv3_level_sums_u8(limiter, lim_l, ncol, nz, level_out, stream);
+    }
+    DiagPtrs<double> dp{};
+    for (int j = 0; j < n_diag; ++j) dp.p[j] = diags[j];
+    const int64_t nb = (nrows + 3) / 4 + nz;
+    hipLaunchKernelGGL(step_partials_kernel, dim3((unsigned)nb), dim3(kSumBlock), 0, (hipStream_t)stream, dp, n_diag,
+                       area, nrows, row_len, partial, partial_ld, limiter, lim_l.ld, ncol, level_out);
+    FV3_LAUNCH_CHECK();
+    return FV3_OK;
+}
+
+extern "C" int fv3_fold_rows_repeat(const double* rows, int64_t nrows, int width, int times, double* rep, double* out,
+                                    void* stream)
+{
+    fv3::clear_error();
+    FV3_REQUIRE(nrows >= 1 && width >= 0 && times >= 1 && nrows * (int64_t)times < ((int64_t)1 << 40),
+                "fold_rows_repeat: bad sizes nrows=%lld width=%d times=%d", (long long)nrows, width, times);
+    if (width == 0) return FV3_OK;
+    FV3_REQUIRE(rows && rep && out, "fold_rows_repeat: NULL array");
+    hipLaunchKernelGGL(fv3::fold_rows_repeat_kernel, dim3((unsigned)width), dim3(64), 0, (hipStream_t)stream, rows,
+                       nrows, width, times, rep, out);
     FV3_LAUNCH_CHECK();
     return FV3_OK;
 }

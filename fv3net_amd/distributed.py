@@ -297,6 +297,46 @@ def bind_area_row_partials(diags: Sequence, area, out=None) -> "_device.BoundLau
     return _device.BoundLaunch(fn, args, keep, "area_weighted_row_sums", out)
 
 
+def bind_step_partials(diags: Sequence, area, limiter, out=None, level_out=None) -> "_device.BoundLaunch":
+    """One launch for a stepper step's per-rank reductions (fv3_step_partials_f64): the
+    area-weighted row partials of float64 ``diags`` over ``area`` (as
+    bind_area_row_partials, into ``out``) and the per-level counts of the uint8
+    ``limiter`` flags (as bind_level_sums, into ``level_out``), each with the bits of its
+    own launch.  The result is ``(out, level_out)``."""
+    rfn, rargs, rkeep, out, work = _area_row_setup(diags, area, out)
+    if not work:
+        raise ValueError("no rows or diagnostics to reduce")
+    if rfn.__name__ != "fv3_area_weighted_row_sums_f64":
+        raise ValueError("bind_step_partials: float64 diagnostics or area")
+    lfn, largs, lkeep, level_out = _level_sums_setup(limiter, level_out)
+    if lfn.__name__ != "fv3_level_sums_u8":
+        raise ValueError("bind_step_partials: uint8 limiter flags")
+    lib = _native.load()
+    args = rargs + (largs[0], largs[1], largs[2], largs[3], largs[4])
+    return _device.BoundLaunch(lib.fv3_step_partials_f64, args, rkeep + lkeep, "step_partials", (out, level_out))
+
+
+def bind_fold_rows_repeat(rows, times: int, rep=None, out=None) -> "_device.BoundLaunch":
+    """The stubbed exchange and its fold in one launch (fv3_fold_rows_repeat): ``rep``
+    receives ``times`` copies of ``rows`` (the bytes an all-gather over ``times`` ranks
+    moves), ``out`` the fold over them (bind_fold_rows of ``rep``, the same bits)."""
+    if not (torch.is_tensor(rows) and rows.is_cuda and rows.dtype == torch.float64 and rows.is_contiguous()
+            and rows.dim() == 2):
+        raise ValueError("bind_fold_rows_repeat needs a contiguous [nrows, width] float64 CUDA buffer")
+    nrows, width = (int(n) for n in rows.shape)
+    if rep is None:
+        rep = torch.empty((times * nrows, width), dtype=torch.float64, device=rows.device)
+    if not (rep.dtype == torch.float64 and rep.is_contiguous() and tuple(rep.shape) == (times * nrows, width)):
+        raise ValueError(f"rep must be a contiguous [{times * nrows}, {width}] float64 buffer")
+    if out is None:
+        out = torch.empty(width, dtype=torch.float64, device=rows.device)
+    if not (out.dtype == torch.float64 and out.is_contiguous() and out.numel() == width):
+        raise ValueError(f"out must be {width} contiguous float64 values")
+    lib = _native.load()
+    return _device.BoundLaunch(lib.fv3_fold_rows_repeat, (rows.data_ptr(), nrows, width, int(times), rep.data_ptr(),
+                                                          out.data_ptr()), [rows, rep, out], "fold_rows_repeat", out)
+
+
 def level_row_partials(field, stream=None, out=None):
     """Device float64 [nrows, nz] per-row level sums of a (nz, rows, row_len) field
     (uint8 flags such as specific_humidity_limiter_active, or float64) read in place.

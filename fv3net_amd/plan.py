@@ -19,6 +19,8 @@ _PLAN_OPS = {
     "fv3_area_weighted_row_sums_f64": "fv3_plan_add_area_weighted_row_sums_f64",
     "fv3_level_sums_u8": "fv3_plan_add_level_sums_u8",
     "fv3_fold_rows": "fv3_plan_add_fold_rows",
+    "fv3_step_partials_f64": "fv3_plan_add_step_partials_f64",
+    "fv3_fold_rows_repeat": "fv3_plan_add_fold_rows_repeat",
 }
 
 

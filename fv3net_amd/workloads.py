@@ -252,6 +252,13 @@ def make_stepper_workload(res: int = 96, seed: int = 0, device=None, group=None,
     return StepperWorkload(model, state, area, 900.0, 6 * res * res, group, precision=precision)
 
 
+class _Result:
+    """A fixed result buffer, read as ``.result`` like a bound launch's."""
+
+    def __init__(self, result):
+        self.result = result
+
+
 @dataclasses.dataclass
 class ShardedStepperWorkload:
     """BASELINE config #4 sharded as SURVEY.md 8(e) lays it out: this rank owns the rows
@@ -281,9 +288,9 @@ class ShardedStepperWorkload:
     # replicated for every rank, then folded: the fold sees the full gathered row count)
     stub_world: int = 1
     _epi: object = None
-    _rows: object = None
     _lev: object = None
     _fold: object = None
+    _diag: object = None
     _rep: object = None
     _res: object = None
     _plan: object = None
@@ -294,7 +301,7 @@ class ShardedStepperWorkload:
         buffer): a step is then a handful of C-ABI calls on fixed buffers, no per-call
         Python marshalling (which, on one rank's 6,912 columns, took longer than the
         kernels).  The precipitation accumulates in place in the epilogue's column buffer."""
-        from .distributed import bind_area_row_partials, bind_fold_rows, bind_level_sums
+        from .distributed import bind_fold_rows_repeat, bind_step_partials
         from .stepper import BoundEpilogue
 
         T, q = self.state["air_temperature"], self.state["specific_humidity"]
@@ -310,23 +317,28 @@ class ShardedStepperWorkload:
         nrows, nz = self.area.shape[0], q.shape[0]
         # [rows][3 (sum area*x, sum area) pairs]
         self.partials = torch.empty((nrows, 6), dtype=torch.float64, device=q.device)
-        self._rows = bind_area_row_partials([res["net_moistening_due_to_machine_learning"],
-                                             res["column_heating_due_to_machine_learning"],
-                                             res["total_precipitation"]], self.area, out=self.partials)
         limiter = res["specific_humidity_limiter_active"]
-        if self.stub_world > 1 and self.group is None:
+        stub = self.stub_world > 1 and self.group is None
+        if stub:
             self._rep = torch.empty((self.stub_world * nrows, 6), dtype=torch.float64, device=q.device)
             self._res = torch.empty(6 + nz, dtype=torch.float64, device=q.device)
-            self._fold = bind_fold_rows(self._rep, out=self._res[:6])
-            self._lev = bind_level_sums(limiter, out=self._res[6:])  # [nz] exact column counts
+            self._fold = bind_fold_rows_repeat(self.partials, self.stub_world, rep=self._rep, out=self._res[:6])
+            level_out = self._res[6:]  # [nz] exact column counts
             self.exchange_bytes = 8 * (nrows * 6 + nz)
         else:
-            self._lev = bind_level_sums(limiter)
-        # one C-ABI call per step: predict, epilogue, row partials, limiter counts (and,
-        # with the stubbed exchange, this band's partials copied for every rank + the fold)
-        self._plan = LaunchPlan([self.bound, self._epi, self._rows, self._lev])
+            level_out = torch.empty(nz, dtype=torch.float64, device=q.device)
+        # the row partials and the limiter level counts in one launch (each with the bits
+        # of its own: bind_area_row_partials / bind_level_sums)
+        self._diag = bind_step_partials([res["net_moistening_due_to_machine_learning"],
+                                         res["column_heating_due_to_machine_learning"],
+                                         res["total_precipitation"]], self.area, limiter, out=self.partials,
+                                        level_out=level_out)
+        self._lev = _Result(level_out)
+        # one C-ABI call per step: predict, epilogue, row partials + limiter counts (and,
+        # with the stubbed exchange, this band's partials copied for every rank + the
+        # fold, one launch)
+        self._plan = LaunchPlan([self.bound, self._epi, self._diag])
         if self._fold is not None:
-            self._plan.repeat(self._rep, self.partials, self.stub_world)
             self._plan.add(self._fold)
 
     def step(self):

@@ -58,7 +58,8 @@ int fv3_abi_version(void); /* bumped on any signature change (2: emulator fields
                               7: fv3_plan_*, 8: fv3_copy_to_host, fv3_copy_2d,
                               9: fv3_host_alloc / free / copy, the arena, replace
                                  fv3_host_register / unregister; wind rotation,
-                                 fv3_sum_squares, fv3_cos_zenith) */
+                                 fv3_sum_squares, fv3_cos_zenith,
+                              10: fv3_step_partials_f64, fv3_fold_rows_repeat) */
 const char* fv3_build_kind(void); /* "product" (fv3net_amd/build.py, no experiment knob compiled in)
                                      or "experiment" (a tools/ variant: results may be invalid) */
 
@@ -308,6 +309,18 @@ int fv3_level_row_sums_u8(const unsigned char* x, int nz, int64_t nrows, int row
 int fv3_level_row_sums_f64(const double* x, int nz, int64_t nrows, int row_len, int64_t level_stride,
                            double* out, int64_t out_ld, void* stream);
 int fv3_fold_rows(const double* rows, int64_t nrows, int width, double* out, void* stream);
+/* One stepper step's per-rank reductions in one launch: fv3_area_weighted_row_sums_f64
+ * of the n_diag diagnostics and fv3_level_sums_u8 of the (nz, ncol) limiter flags, each
+ * with the bits of its own call (replaces the two launches of
+ * runtime/steppers/machine_learning.py:301-303 + runtime/metrics.py:18-32's per-rank
+ * part; limiter rows not 16-byte aligned take the two launches). */
+int fv3_step_partials_f64(const double* const* diags, int n_diag, const double* area, int64_t nrows, int row_len,
+                          double* partial, int64_t partial_ld, const unsigned char* limiter, fv3_layout lim_l,
+                          int64_t ncol, int nz, double* level_out, void* stream);
+/* A stubbed all-gather and its fold in one launch: rep[t*nrows + r][j] = rows[r][j] for
+ * t < times (the bytes `times` ranks' partials move), out[j] = fv3_fold_rows(rep). */
+int fv3_fold_rows_repeat(const double* rows, int64_t nrows, int width, int times, double* rep, double* out,
+                         void* stream);
 
 /* TimeMask (external/emulation/emulation/_emulate/microphysics.py:37-47): out =
  * state * alpha + emulator * (1 - alpha) over n elements, each product in its array's
@@ -695,6 +708,12 @@ int fv3_plan_add_area_weighted_row_sums_f64(fv3_plan* plan, const double* const*
 int fv3_plan_add_level_sums_u8(fv3_plan* plan, const unsigned char* x, fv3_layout x_l, int64_t ncol, int nz,
                                double* out);
 int fv3_plan_add_fold_rows(fv3_plan* plan, const double* rows, int64_t nrows, int width, double* out);
+int fv3_plan_add_step_partials_f64(fv3_plan* plan, const double* const* diags, int n_diag, const double* area,
+                                   int64_t nrows, int row_len, double* partial, int64_t partial_ld,
+                                   const unsigned char* limiter, fv3_layout lim_l, int64_t ncol, int nz,
+                                   double* level_out);
+int fv3_plan_add_fold_rows_repeat(fv3_plan* plan, const double* rows, int64_t nrows, int width, int times,
+                                  double* rep, double* out);
 /* device-to-device copy of `bytes` */
 int fv3_plan_add_copy(fv3_plan* plan, void* dst, const void* src, size_t bytes);
 /* `times` back-to-back copies of `bytes` (a multiple of 4) of src into dst, one launch */

@@ -182,7 +182,9 @@ def test_two_lane_pair_kernel_rank_share_size(gpu, kn, monkeypatch):
     columns to the oracle, on columns that take every start of the second lane (a
     direct window, output kB above the top or below the bottom, kB's layer near either
     end) and columns that keep the single pass (unsorted pe2, a NaN edge); a
-    zero-thickness layer stays on two lanes."""
+    zero-thickness layer stays on two lanes.  The decreasing-pe2 and NaN-pe1 columns
+    fail the reference's layer search (undefined behaviour, excluded from oracle parity,
+    DESIGN.md §4): there the two kernels must agree with each other only."""
     import torch
 
     from fv3net_amd.mappm import mappm_device_multi
@@ -211,7 +213,7 @@ def test_two_lane_pair_kernel_rank_share_size(gpu, kn, monkeypatch):
     for x, y, z in zip(res["1"], res["0"], default):
         assert torch.equal(x.view(torch.int32), y.view(torch.int32))
         assert torch.equal(x.view(torch.int32), z.view(torch.int32))
-    idx = np.concatenate([np.arange(160), np.sort(rng.choice(np.arange(160, ncol), 1500, replace=False))])
+    idx = np.concatenate([np.arange(96, 160), np.sort(rng.choice(np.arange(160, ncol), 1500, replace=False))])
     for q, o in zip(qs, res["1"]):
         with np.errstate(all="ignore"):
             ref = oracle_mappm(pe1[:, idx], q[:, idx], pe2[:, idx], 1, 1)
