@@ -639,16 +639,15 @@ __global__ __launch_bounds__(256) void mappm_ppm_pair_split_kernel(MappmPairArgs
     mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0, true>(d, km, kn, a.iv, a.kord, kf, kl, Lf);
 }
 
-// the two-lane pair kernel between the level-parallel kernel's range and this many
-// columns (FV3_MAPPM_SPLIT=0|1 for A/B: never / from kLevelsMaxCols on)
-constexpr int64_t kSplitMaxCols = 262144;
-
-bool use_split_kernel(int64_t ncol)
+// The two-lane kernel is bit-identical and slower than one lane per column at every
+// column count above the level-parallel kernel's range (tools/mappm_split_time.py,
+// profiles/r05o_mappm_split.log: 110,592 columns 193 vs 166 us, C384 1.31 vs 0.78 ms;
+// the halves' remap branches diverge within the wave and the loop index is no longer
+// wave-uniform), so it runs only on request (FV3_MAPPM_SPLIT=1, A/B and tests).
+bool use_split_kernel(int64_t)
 {
     const char* p = fv3::variant_env("FV3_MAPPM_SPLIT");
-    if (p && p[0] == '0') return false;
-    if (p && p[0] == '1') return true;
-    return ncol < kSplitMaxCols;
+    return p && p[0] == '1';
 }
 
 }  // namespace fv3
