@@ -203,8 +203,10 @@ __global__ __launch_bounds__(64) void ml_epilogue_kernel(EpilogueArgs<DT> a)
 // adds its column's terms in level order from +0.0, the same additions as the column
 // kernel.  One rank's 6,912 columns are 108 waves in the column kernel (one per CU, a
 // serial 79-level chain each: 44 us); here 1,728.
-constexpr int kEpiCols = 16, kEpiLanes = 16, kEpiU = 3;
-template <typename DT>
+// kEpiU levels per thread per pass: 5 covers 79 levels in one pass of loads (3 took
+// two dependent rounds of them; one rank's 6,912 columns, tools/epi_ab.py)
+constexpr int kEpiCols = 16, kEpiLanes = 16;
+template <typename DT, int kEpiU>
 __global__ __launch_bounds__(kEpiCols * kEpiLanes) void ml_epilogue_levels_kernel(EpilogueArgs<DT> a)
 {
     extern __shared__ __align__(16) unsigned char epi_smem[];
@@ -313,8 +315,9 @@ int epilogue_impl(const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, int n
     if (path && path[0] == 'l') levels = true;
     if (levels && smem <= kEpiMaxSmem) {
         const int64_t grid = (ncol + kEpiCols - 1) / kEpiCols;
-        hipLaunchKernelGGL(ml_epilogue_levels_kernel<DT>, dim3((unsigned)grid), dim3(kEpiCols * kEpiLanes), smem,
-                           (hipStream_t)stream, a);
+        const char* u = fv3::variant_env("FV3_EPI_U");  // A/B: 3 (round 4) | 5
+        auto kfn = (u && u[0] == '3') ? ml_epilogue_levels_kernel<DT, 3> : ml_epilogue_levels_kernel<DT, 5>;
+        hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kEpiCols * kEpiLanes), smem, (hipStream_t)stream, a);
     } else {
         const int block = 64;  // one wave: C96's 864 waves spread over every CU (256-thread blocks left 40 idle)
         const int64_t grid = (ncol + block - 1) / block;

@@ -49,12 +49,15 @@ def _bits(a, b):
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("mse", [True, False])
 @pytest.mark.parametrize("hydrostatic", [False, True])
-@pytest.mark.parametrize("path", ["levels", "columns"])
+@pytest.mark.parametrize("path", ["levels", "levels-u3", "columns"])
 def test_epilogue_bit_identical_to_oracle(gpu, dtype, mse, hydrostatic, path, monkeypatch):
-    """Both epilogue kernels: level-parallel (the default) and one thread per column."""
+    """Both epilogue kernels: level-parallel (the default; 5 levels per lane per pass, and
+    round 4's 3) and one thread per column."""
     import torch
 
-    set_variant(monkeypatch, "FV3_EPILOGUE_PATH", path)
+    set_variant(monkeypatch, "FV3_EPILOGUE_PATH", path.split("-")[0])
+    if path.endswith("u3"):
+        set_variant(monkeypatch, "FV3_EPI_U", "3")
 
     from fv3net_amd.stepper import ml_epilogue
 
@@ -74,11 +77,11 @@ def test_epilogue_bit_identical_to_oracle(gpu, dtype, mse, hydrostatic, path, mo
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nz", [1, 3, 8, 9, 16, 17, 24, 33, 47, 48, 49, 79, 95, 96, 130])
+@pytest.mark.parametrize("nz", [1, 3, 5, 8, 9, 16, 17, 24, 33, 47, 48, 49, 79, 80, 81, 95, 96, 130])
 @pytest.mark.parametrize("path", ["levels", "columns"])
 def test_epilogue_level_batches(gpu, nz, path, monkeypatch):
     """The column kernel fetches levels in double-buffered batches of 8, the level-parallel
-    one in batches of 3 per level lane of 16 (and hands nz > 95 to the column kernel):
+    one in batches of 5 per level lane of 16 (and hands nz > 95 to the column kernel):
     every remainder of nz (fewer levels than one batch, exact multiples, one past) stays
     bit-identical, on 130 columns (a partial block of 16)."""
     import torch
