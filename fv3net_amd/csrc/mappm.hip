@@ -577,19 +577,20 @@ __global__ __launch_bounds__(256) void mappm_ppm_pair_kernel(MappmPairArgs a)
 
 // Small grids with one lane per column left the SIMDs short of waves (one rank's share
 // of C384 at world 8, 110,592 columns: 1.7 waves per SIMD, the serial remap's latency
-// unhidden).  Here each column runs on TWO lanes of one wave, l and l + 32 (each half
-// wave reads 32 consecutive columns): the first streams outputs 1 .. kB - 1, the second
-// kB .. kn from the input layer where the single pass begins output kB (mappm_multi.h,
-// "two lanes per column"), both on the same loop, so a wave's trip count is the longer
-// half's.  The pressure scans that prove the split exact are shared the same way (pe1
-// on the first lane, pe2 on the second, exchanged by a lane shuffle); a column that
-// fails them runs the single pass on its first lane.
-__global__ __launch_bounds__(256) void mappm_ppm_pair_split_kernel(MappmPairArgs a)
+// unhidden).  Here each column runs on TWO lanes: the first streams outputs 1 .. kB - 1,
+// the second kB .. kn from the input layer where the single pass begins output kB
+// (mappm_multi.h, "two lanes per column").  A block is two waves over the same 64
+// columns, wave 0 the first halves and wave 1 the second, so every lane of a wave is in
+// the same phase of its column (neighbouring columns' remap events mostly coincide; with
+// the halves mixed in one wave they diverge at every level).  The scans that prove the
+// split exact are shared through LDS (pe1 on wave 0, pe2 on wave 1); a column that fails
+// them runs the single pass on its first-half lane.
+__global__ __launch_bounds__(128) void mappm_ppm_pair_split_kernel(MappmPairArgs a)
 {
+    __shared__ int s_ok[2][64], s_cnt[64];
     const int lane = threadIdx.x & 63;
-    const int part = lane >> 5;
-    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int64_t c0 = wave * 32 + (lane & 31);
+    const int part = threadIdx.x >> 6;
+    const int64_t c0 = (int64_t)blockIdx.x * 64 + lane;
     const bool valid = c0 < a.ncol;
     const int64_t c = valid ? c0 : a.ncol - 1;  // spare lanes scan the last column, then leave
     DevColPair d;
@@ -614,12 +615,13 @@ __global__ __launch_bounds__(256) void mappm_ppm_pair_split_kernel(MappmPairArgs
         else
             ok = split_scan_pe2(d, kn);
     }
-    const int both = ok & __shfl_xor(ok, 32);
-    const int cnt0 = __shfl(cnt, lane & 31);  // the first lane's count
+    s_ok[part][lane] = ok;
+    if (part == 0) s_cnt[lane] = cnt;
+    __syncthreads();
+    const bool both = s_ok[0][lane] && s_ok[1][lane];
+    const int cnt0 = s_cnt[lane];
     if (!valid) return;
-    // this lane's outputs [kf, kl] and first input layer; ONE call site below, so the
-    // two halves of a wave run the same loop together (separate calls would run one
-    // after the other under the exec mask)
+    // this lane's outputs [kf, kl] and first input layer (one call site for every lane)
     int kf = 1, kl = kn, Lf = 1;
     if (both) {
         if (part == 0) {
@@ -639,15 +641,19 @@ __global__ __launch_bounds__(256) void mappm_ppm_pair_split_kernel(MappmPairArgs
     mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0, true>(d, km, kn, a.iv, a.kord, kf, kl, Lf);
 }
 
-// The two-lane kernel is bit-identical and slower than one lane per column at every
-// column count above the level-parallel kernel's range (tools/mappm_split_time.py,
-// profiles/r05o_mappm_split.log: 110,592 columns 193 vs 166 us, C384 1.31 vs 0.78 ms;
-// the halves' remap branches diverge within the wave and the loop index is no longer
-// wave-uniform), so it runs only on request (FV3_MAPPM_SPLIT=1, A/B and tests).
-bool use_split_kernel(int64_t)
+// Where the two-lane kernel pays (tools/mappm_split_time.py, profiles/r05r_mappm_split.log,
+// one box, interleaved; one lane per column vs two): 65,536 columns 142.7 vs 115.4 us,
+// 110,592 (one rank's C384 band at world 8) 165.7 vs 161.5 us, 147,456 213 vs 228 us,
+// C384 0.78 vs 1.06 ms.  Above the level-parallel kernel's range and below 131,072
+// columns it runs by default; FV3_MAPPM_SPLIT=0|1 forces it off / on (A/B, tests).
+constexpr int64_t kSplitMaxCols = 131072;
+
+bool use_split_kernel(int64_t ncol)
 {
     const char* p = fv3::variant_env("FV3_MAPPM_SPLIT");
-    return p && p[0] == '1';
+    if (p && p[0] == '0') return false;
+    if (p && p[0] == '1') return true;
+    return ncol < kSplitMaxCols;
 }
 
 }  // namespace fv3
@@ -710,9 +716,9 @@ extern "C" int fv3_mappm_multi(const float* pe1, fv3_layout pe1_l, const float* 
             fv3::MappmPairArgs a{pe1, pe2, pe1_l, pe2_l, {q1[f], q1[f + 1]}, {q2[f], q2[f + 1]},
                                  {q1_l[f], q1_l[f + 1]}, {q2_l[f], q2_l[f + 1]}, ncol, km, kn, iv, kord};
             const int block = 256;
-            if (fv3::use_split_kernel(ncol)) {  // two lanes per column: 64 threads per 32 columns
-                const int64_t grid = ((ncol + 31) / 32 * 64 + block - 1) / block;
-                hipLaunchKernelGGL(fv3::mappm_ppm_pair_split_kernel, dim3((unsigned)grid), dim3(block), 0, s, a);
+            if (fv3::use_split_kernel(ncol)) {  // two lanes per column: 128 threads per 64 columns
+                const int64_t grid = (ncol + 63) / 64;
+                hipLaunchKernelGGL(fv3::mappm_ppm_pair_split_kernel, dim3((unsigned)grid), dim3(128), 0, s, a);
             } else {
                 const int64_t grid = (ncol + block - 1) / block;
                 hipLaunchKernelGGL(fv3::mappm_ppm_pair_kernel, dim3((unsigned)grid), dim3(block), 0, s, a);

@@ -19,9 +19,9 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(params=["split", "serial", "levels"])
 def path(request, monkeypatch):
     """`split`: pairs of fields on the two-field streaming kernel, each column on two
-    lanes (FV3_MAPPM_SPLIT=1, measured slower: an A/B variant); `serial`: the same kernel
-    one lane per column (the default); `levels`: the small-grid kernel, one field per
-    launch."""
+    lanes (FV3_MAPPM_SPLIT=1; the default from 65,536 to 131,072 columns); `serial`: the
+    same kernel one lane per column (FV3_MAPPM_SPLIT=0, the default above);
+    `levels`: the small-grid kernel, one field per launch."""
     set_variant(monkeypatch, "FV3_MAPPM_PATH", "levels" if request.param == "levels" else "serial")
     if request.param != "levels":
         set_variant(monkeypatch, "FV3_MAPPM_SPLIT", "1" if request.param == "split" else "0")
@@ -178,8 +178,8 @@ def test_multi_on_a_side_stream(gpu, path):
 
 @pytest.mark.parametrize("kn", [79, 50, 2, 1])
 def test_two_lane_pair_kernel_rank_share_size(gpu, kn, monkeypatch):
-    """One rank's share of C384 at world 8 (110,592 columns): the two-lane kernel's
-    whole arrays bit-identical to the one-lane pair kernel (the default) and sampled
+    """One rank's share of C384 at world 8 (110,592 columns, the two-lane kernel by
+    default): whole arrays bit-identical to the one-lane pair kernel and sampled
     columns to the oracle, on columns that take every start of the second lane (a
     direct window, output kB above the top or below the bottom, kB's layer near either
     end) and columns that keep the single pass (unsorted pe2, a NaN edge); a
