@@ -257,8 +257,7 @@ _SIGNATURES = {
     "fv3_level_row_sums_u8": (_I, [_P, _I, _I64, _I, _I64, _P, _I64, _P]),
     "fv3_level_row_sums_f64": (_I, [_P, _I, _I64, _I, _I64, _P, _I64, _P]),
     "fv3_fold_rows": (_I, [_P, _I64, _I, _P, _P]),
-    "fv3_step_partials_f64": (_I, [ctypes.POINTER(_P), _I, _P, _I64, _I, _P, _I64, _P, Layout, _I64, _I, _P, _I, _P,
-                                   _P, _P, _P]),
+    "fv3_step_partials_f64": (_I, [ctypes.POINTER(_P), _I, _P, _I64, _I, _P, _I64, _P, Layout, _I64, _I, _P, _P]),
     "fv3_fold_rows_repeat": (_I, [_P, _I64, _I, _I, _P, _P, _P]),
     "fv3_time_blend": (_I, [_P, _I, _P, _I, _P, _I64, _D, _P]),
     "fv3_range_mask": (_I, [_P, _P, _I64, _D, _D, _I, _I, _I, _P]),
@@ -299,7 +298,7 @@ _SIGNATURES = {
     "fv3_plan_add_level_sums_u8": (_I, [_P, _P, Layout, _I64, _I, _P]),
     "fv3_plan_add_fold_rows": (_I, [_P, _P, _I64, _I, _P]),
     "fv3_plan_add_step_partials_f64": (_I, [_P, ctypes.POINTER(_P), _I, _P, _I64, _I, _P, _I64, _P, Layout, _I64, _I,
-                                            _P, _I, _P, _P, _P]),
+                                            _P]),
     "fv3_plan_add_fold_rows_repeat": (_I, [_P, _P, _I64, _I, _I, _P, _P]),
     "fv3_plan_add_copy": (_I, [_P, _P, _P, ctypes.c_size_t]),
     "fv3_plan_add_repeat": (_I, [_P, _P, _P, ctypes.c_size_t, _I]),

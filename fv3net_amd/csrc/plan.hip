@@ -155,8 +155,7 @@ extern "C" int fv3_plan_add_fold_rows(fv3_plan* plan, const double* rows, int64_
 extern "C" int fv3_plan_add_step_partials_f64(fv3_plan* plan, const double* const* diags, int n_diag,
                                               const double* area, int64_t nrows, int row_len, double* partial,
                                               int64_t partial_ld, const unsigned char* limiter, fv3_layout lim_l,
-                                              int64_t ncol, int nz, double* level_out, int fold_times, double* rep,
-                                              double* fold_out, unsigned* ticket)
+                                              int64_t ncol, int nz, double* level_out)
 {
     using namespace fv3;
     clear_error();
@@ -164,7 +163,7 @@ extern "C" int fv3_plan_add_step_partials_f64(fv3_plan* plan, const double* cons
     std::vector<const double*> d(diags, diags + n_diag);
     plan->ops.push_back([=](void* s) {
         return fv3_step_partials_f64(d.data(), n_diag, area, nrows, row_len, partial, partial_ld, limiter, lim_l,
-                                     ncol, nz, level_out, fold_times, rep, fold_out, ticket, s);
+                                     ncol, nz, level_out, s);
     });
     return FV3_OK;
 }

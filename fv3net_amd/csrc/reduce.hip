@@ -384,70 +384,46 @@ __global__ __launch_bounds__(64) void area_row_sums_kernel(DiagPtrs<T> d, int n_
     area_row_sum(d, n_diag, area, row_len, out, out_ld, blockIdx.x, threadIdx.x);
 }
 
-// rep[t * nrows + r][j] = rows[r][j] for t < times, and out[j] = the fold of rep's rows
-// for j = j0, j0 + jstep, ...: lane l the rows l, l + 64, ... in order, then the
-// butterfly (fv3_fold_rows' order); each lane sums the values it writes.  One wave.
-__device__ __forceinline__ void fold_rows_repeat_wave(const double* __restrict__ rows, int64_t nrows, int width,
-                                                      int times, double* __restrict__ rep, double* __restrict__ out,
-                                                      int j0, int jstep, int lane)
-{
-    const int64_t n = nrows * times;
-    for (int j = j0; j < width; j += jstep) {
-        double s = 0.0;
-        for (int64_t r = lane; r < n; r += 64) {
-            const double v = rows[(r % nrows) * width + j];
-            rep[r * width + j] = v;
-            s += v;
-        }
-        s = wave_sum(s);
-        if (lane == 0) out[j] = s;
-    }
-}
-
 // One step's per-rank reductions in ONE launch (the stepper step's area-weighted row
 // partials and limiter level counts): blocks [0, nb_rows) take four grid
 // rows each, one wave per row, exactly as area_row_sums_kernel (same lanes, same order);
 // the nz blocks after them one level's uint8 count each, exactly as level_counts_u8_vec.
-// With `fold_out` (one rank's share with the exchange stubbed), the last row block to
-// finish (a ticket, vector atomics; each writer's fence before it, the reader's after)
-// also runs the stub's copy and the fold, exactly as fold_rows_repeat_kernel, and resets
-// the ticket for the next launch.  Three launches of ~5 us became one.
+// Two launches of ~5 us became one on one rank's share.
 __global__ __launch_bounds__(kSumBlock) void step_partials_kernel(DiagPtrs<double> d, int n_diag,
                                                                   const double* __restrict__ area, int64_t nrows,
                                                                   int row_len, double* __restrict__ partial,
                                                                   int64_t partial_ld, const unsigned char* __restrict__ lim,
                                                                   int64_t lim_ld, int64_t ncol,
-                                                                  double* __restrict__ level_out, int times,
-                                                                  double* __restrict__ rep, double* __restrict__ fold_out,
-                                                                  unsigned* __restrict__ ticket)
+                                                                  double* __restrict__ level_out)
 {
     __shared__ double sh[kSumBlock / 64];
-    __shared__ int last;
     const int64_t nb_rows = (nrows + 3) / 4;
     if ((int64_t)blockIdx.x < nb_rows) {
         const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
         if (r < nrows) area_row_sum(d, n_diag, area, row_len, partial, partial_ld, r, threadIdx.x & 63);
-        if (fold_out == nullptr) return;  // uniform over the grid
-        __threadfence();  // this wave's partials visible device-wide before the ticket
-        __syncthreads();
-        if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == (unsigned)(nb_rows - 1);
-        __syncthreads();
-        if (!last) return;
-        __threadfence();  // every other row block's partials
-        fold_rows_repeat_wave(partial, nrows, (int)partial_ld, times, rep, fold_out, threadIdx.x >> 6, kSumBlock / 64,
-                              threadIdx.x & 63);
-        if (threadIdx.x == 0) atomicExch(ticket, 0u);
-        return;
+        return;  // no block-wide barrier on this side
     }
     level_count_u8(lim, lim_ld, ncol, (int)(blockIdx.x - nb_rows), level_out, sh);
 }
 
-// the stub exchange's copy and the fold in one launch (one wave per j)
+// the stub exchange's copy and the fold in one launch: rep[t * nrows + r][j] =
+// rows[r][j] for t < times (the bytes an all-gather of `times` ranks' partials moves),
+// and out[j] folded over rep's rows exactly as fold_rows_kernel (lane l the rows
+// l, l + 64, ... in order, then the butterfly): each lane sums the values it writes
 __global__ __launch_bounds__(64) void fold_rows_repeat_kernel(const double* __restrict__ rows, int64_t nrows, int width,
                                                               int times, double* __restrict__ rep,
                                                               double* __restrict__ out)
 {
-    fold_rows_repeat_wave(rows, nrows, width, times, rep, out, blockIdx.x, width, threadIdx.x);
+    const int j = blockIdx.x;
+    const int64_t n = nrows * times;
+    double s = 0.0;
+    for (int64_t r = threadIdx.x; r < n; r += 64) {
+        const double v = rows[(r % nrows) * width + j];
+        rep[r * width + j] = v;
+        s += v;
+    }
+    s = wave_sum(s);
+    if (threadIdx.x == 0) out[j] = s;
 }
 
 // per (row, level) sums of a (nz, nrows, row_len) float64 field: out[r][k], one wave each
@@ -583,8 +559,7 @@ extern "C" int fv3_fold_rows(const double* rows, int64_t nrows, int width, doubl
 
 extern "C" int fv3_step_partials_f64(const double* const* diags, int n_diag, const double* area, int64_t nrows,
                                      int row_len, double* partial, int64_t partial_ld, const unsigned char* limiter,
-                                     fv3_layout lim_l, int64_t ncol, int nz, double* level_out, int fold_times,
-                                     double* rep, double* fold_out, unsigned* ticket, void* stream)
+                                     fv3_layout lim_l, int64_t ncol, int nz, double* level_out, void* stream)
 {
     using namespace fv3;
     clear_error();
@@ -596,26 +571,20 @@ extern "C" int fv3_step_partials_f64(const double* const* diags, int n_diag, con
     FV3_REQUIRE(diags && area && partial && limiter && level_out, "step_partials: NULL array");
     FV3_REQUIRE(ncol == 0 || layout_ok(lim_l, ncol), "step_partials: bad limiter layout");
     for (int j = 0; j < n_diag; ++j) FV3_REQUIRE(diags[j], "step_partials: NULL diagnostic %d", j);
-    const bool fold = fold_out != nullptr;
-    FV3_REQUIRE(!fold || (fold_times >= 1 && rep && ticket && nrows * (int64_t)fold_times < ((int64_t)1 << 40)),
-                "step_partials: the fold needs times >= 1, rep and a ticket");
     // the fused launch reads the limiter rows as level_counts_u8_vec does; anything else
-    // takes the launches it fuses
+    // takes the two launches it fuses
     const bool vec = ncol > 0 && (lim_l.ncol_blk <= 0 || lim_l.ncol_blk >= ncol) && ((uintptr_t)limiter % 16) == 0 &&
                      (lim_l.ld % 16) == 0 && lim_l.ld >= 0 && ncol <= ((int64_t)1 << 24);
     if (!vec || variant_env("FV3_STEP_PARTIALS_SPLIT")) {
-        int st = fv3_area_weighted_row_sums_f64(diags, n_diag, area, nrows, row_len, partial, partial_ld, stream);
-        if (st == FV3_OK) st = fv3_level_sums_u8(limiter, lim_l, ncol, nz, level_out, stream);
-        if (st == FV3_OK && fold)
-            st = fv3_fold_rows_repeat(partial, nrows, (int)partial_ld, fold_times, rep, fold_out, stream);
-        return st;
+        const int st = fv3_area_weighted_row_sums_f64(diags, n_diag, area, nrows, row_len, partial, partial_ld, stream);
+        if (st != FV3_OK) return st;
+        return fv3_level_sums_u8(limiter, lim_l, ncol, nz, level_out, stream);
     }
     DiagPtrs<double> dp{};
     for (int j = 0; j < n_diag; ++j) dp.p[j] = diags[j];
     const int64_t nb = (nrows + 3) / 4 + nz;
     hipLaunchKernelGGL(step_partials_kernel, dim3((unsigned)nb), dim3(kSumBlock), 0, (hipStream_t)stream, dp, n_diag,
-                       area, nrows, row_len, partial, partial_ld, limiter, lim_l.ld, ncol, level_out, fold_times, rep,
-                       fold_out, ticket);
+                       area, nrows, row_len, partial, partial_ld, limiter, lim_l.ld, ncol, level_out);
     FV3_LAUNCH_CHECK();
     return FV3_OK;
 }

@@ -297,15 +297,12 @@ def bind_area_row_partials(diags: Sequence, area, out=None) -> "_device.BoundLau
     return _device.BoundLaunch(fn, args, keep, "area_weighted_row_sums", out)
 
 
-def bind_step_partials(diags: Sequence, area, limiter, out=None, level_out=None, fold=None) -> "_device.BoundLaunch":
+def bind_step_partials(diags: Sequence, area, limiter, out=None, level_out=None) -> "_device.BoundLaunch":
     """One launch for a stepper step's per-rank reductions (fv3_step_partials_f64): the
     area-weighted row partials of float64 ``diags`` over ``area`` (as
     bind_area_row_partials, into ``out``) and the per-level counts of the uint8
     ``limiter`` flags (as bind_level_sums, into ``level_out``), each with the bits of its
-    own launch.  ``fold=(times, rep, fold_out)``: the same launch also copies ``out``
-    ``times`` times into ``rep`` and folds them into ``fold_out`` (bind_fold_rows_repeat's
-    bits) once every row is written: one rank's step with the exchange stubbed.  The
-    result is ``(out, level_out)``."""
+    own launch.  The result is ``(out, level_out)``."""
     rfn, rargs, rkeep, out, work = _area_row_setup(diags, area, out)
     if not work:
         raise ValueError("no rows or diagnostics to reduce")
@@ -314,23 +311,9 @@ def bind_step_partials(diags: Sequence, area, limiter, out=None, level_out=None,
     lfn, largs, lkeep, level_out = _level_sums_setup(limiter, level_out)
     if lfn.__name__ != "fv3_level_sums_u8":
         raise ValueError("bind_step_partials: uint8 limiter flags")
-    keep = rkeep + lkeep
-    fargs = (0, None, None, None)
-    if fold is not None:
-        times, rep, fold_out = fold
-        nrows, width = int(out.shape[0]), int(rargs[6])
-        if not (out.dim() == 2 and out.is_contiguous() and out.shape[1] == width):
-            raise ValueError("bind_step_partials: the fold needs a contiguous [nrows, W] partials buffer")
-        if not (rep.dtype == torch.float64 and rep.is_contiguous() and tuple(rep.shape) == (times * nrows, width)):
-            raise ValueError(f"rep must be a contiguous [{times * nrows}, {width}] float64 buffer")
-        if not (fold_out.dtype == torch.float64 and fold_out.is_contiguous() and fold_out.numel() == width):
-            raise ValueError(f"fold_out must be {width} contiguous float64 values")
-        ticket = torch.zeros(1, dtype=torch.int32, device=out.device)  # left zeroed by every launch
-        fargs = (int(times), rep.data_ptr(), fold_out.data_ptr(), ticket.data_ptr())
-        keep = keep + [rep, fold_out, ticket]
     lib = _native.load()
-    args = rargs + (largs[0], largs[1], largs[2], largs[3], largs[4]) + fargs
-    return _device.BoundLaunch(lib.fv3_step_partials_f64, args, keep, "step_partials", (out, level_out))
+    args = rargs + (largs[0], largs[1], largs[2], largs[3], largs[4])
+    return _device.BoundLaunch(lib.fv3_step_partials_f64, args, rkeep + lkeep, "step_partials", (out, level_out))
 
 
 def bind_fold_rows_repeat(rows, times: int, rep=None, out=None) -> "_device.BoundLaunch":

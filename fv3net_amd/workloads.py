@@ -301,7 +301,7 @@ class ShardedStepperWorkload:
         buffer): a step is then a handful of C-ABI calls on fixed buffers, no per-call
         Python marshalling (which, on one rank's 6,912 columns, took longer than the
         kernels).  The precipitation accumulates in place in the epilogue's column buffer."""
-        from .distributed import bind_step_partials
+        from .distributed import bind_fold_rows_repeat, bind_step_partials
         from .stepper import BoundEpilogue
 
         T, q = self.state["air_temperature"], self.state["specific_humidity"]
@@ -319,27 +319,27 @@ class ShardedStepperWorkload:
         self.partials = torch.empty((nrows, 6), dtype=torch.float64, device=q.device)
         limiter = res["specific_humidity_limiter_active"]
         stub = self.stub_world > 1 and self.group is None
-        fold = None
         if stub:
             self._rep = torch.empty((self.stub_world * nrows, 6), dtype=torch.float64, device=q.device)
             self._res = torch.empty(6 + nz, dtype=torch.float64, device=q.device)
-            fold = (self.stub_world, self._rep, self._res[:6])
+            self._fold = bind_fold_rows_repeat(self.partials, self.stub_world, rep=self._rep, out=self._res[:6])
             level_out = self._res[6:]  # [nz] exact column counts
             self.exchange_bytes = 8 * (nrows * 6 + nz)
         else:
             level_out = torch.empty(nz, dtype=torch.float64, device=q.device)
         # the row partials and the limiter level counts in one launch (each with the bits
-        # of its own: bind_area_row_partials / bind_level_sums); with the stubbed exchange
-        # the same launch copies this band's partials for every rank and folds them
-        # (bind_fold_rows_repeat's bits)
+        # of its own: bind_area_row_partials / bind_level_sums)
         self._diag = bind_step_partials([res["net_moistening_due_to_machine_learning"],
                                          res["column_heating_due_to_machine_learning"],
                                          res["total_precipitation"]], self.area, limiter, out=self.partials,
-                                        level_out=level_out, fold=fold)
-        self._fold = fold
+                                        level_out=level_out)
         self._lev = _Result(level_out)
-        # one C-ABI call per step: predict, epilogue, the reductions (+ the stub exchange)
+        # one C-ABI call per step: predict, epilogue, row partials + limiter counts (and,
+        # with the stubbed exchange, this band's partials copied for every rank + the
+        # fold, one launch)
         self._plan = LaunchPlan([self.bound, self._epi, self._diag])
+        if self._fold is not None:
+            self._plan.add(self._fold)
 
     def step(self):
         from . import _device

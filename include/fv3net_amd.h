@@ -313,14 +313,10 @@ int fv3_fold_rows(const double* rows, int64_t nrows, int width, double* out, voi
  * of the n_diag diagnostics and fv3_level_sums_u8 of the (nz, ncol) limiter flags, each
  * with the bits of its own call (replaces the two launches of
  * runtime/steppers/machine_learning.py:301-303 + runtime/metrics.py:18-32's per-rank
- * part; limiter rows not 16-byte aligned take the separate launches).  fold_out != NULL
- * (one rank's share timed with the exchange stubbed): the same launch also runs
- * fv3_fold_rows_repeat(partial, nrows, partial_ld, fold_times, rep, fold_out) once every
- * row is written; `ticket` is one zeroed uint32 in device memory, left zeroed. */
+ * part; limiter rows not 16-byte aligned take the two launches). */
 int fv3_step_partials_f64(const double* const* diags, int n_diag, const double* area, int64_t nrows, int row_len,
                           double* partial, int64_t partial_ld, const unsigned char* limiter, fv3_layout lim_l,
-                          int64_t ncol, int nz, double* level_out, int fold_times, double* rep, double* fold_out,
-                          unsigned* ticket, void* stream);
+                          int64_t ncol, int nz, double* level_out, void* stream);
 /* A stubbed all-gather and its fold in one launch: rep[t*nrows + r][j] = rows[r][j] for
  * t < times (the bytes `times` ranks' partials move), out[j] = fv3_fold_rows(rep). */
 int fv3_fold_rows_repeat(const double* rows, int64_t nrows, int width, int times, double* rep, double* out,
@@ -715,8 +711,7 @@ int fv3_plan_add_fold_rows(fv3_plan* plan, const double* rows, int64_t nrows, in
 int fv3_plan_add_step_partials_f64(fv3_plan* plan, const double* const* diags, int n_diag, const double* area,
                                    int64_t nrows, int row_len, double* partial, int64_t partial_ld,
                                    const unsigned char* limiter, fv3_layout lim_l, int64_t ncol, int nz,
-                                   double* level_out, int fold_times, double* rep, double* fold_out,
-                                   unsigned* ticket);
+                                   double* level_out);
 int fv3_plan_add_fold_rows_repeat(fv3_plan* plan, const double* rows, int64_t nrows, int width, int times,
                                   double* rep, double* out);
 /* device-to-device copy of `bytes` */

@@ -34,22 +34,6 @@ def test_step_partials_equal_the_two_launches(gpu, nrows, row_len, nz, offset):
     assert torch.equal(part.view(torch.int64), want_rows.view(torch.int64))
     assert torch.equal(lev.view(torch.int64), want_lev.view(torch.int64))
     assert torch.equal(lev, lim.sum(1, dtype=torch.float64))
-    # with the stub exchange's copy and fold in the same launch (the last row block to
-    # finish runs them): bind_fold_rows_repeat's bits, every launch (the ticket is reset)
-    times = 8
-    rep = torch.full((times * nrows, 6), np.nan, dtype=torch.float64, device=dev)
-    fout = torch.full((6,), np.nan, dtype=torch.float64, device=dev)
-    fused_fold = D.bind_step_partials(diags, area, lim, out=part, level_out=lev, fold=(times, rep, fout))
-    want_fold = D.fold_rows(want_rows.repeat(times, 1))
-    for _ in range(3):
-        rep.fill_(np.nan)
-        fout.fill_(np.nan)
-        fused_fold()
-        torch.cuda.synchronize()
-        assert torch.equal(part.view(torch.int64), want_rows.view(torch.int64))
-        assert torch.equal(lev.view(torch.int64), want_lev.view(torch.int64))
-        assert torch.equal(rep, want_rows.repeat(times, 1))
-        assert torch.equal(fout.view(torch.int64), want_fold.view(torch.int64))
 
 
 @pytest.mark.parametrize("nrows,times", [(144, 8), (72, 8), (18, 4), (1, 3), (200, 1)])
