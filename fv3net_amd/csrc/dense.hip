@@ -329,90 +329,80 @@ typedef __attribute__((address_space(4))) const DenseArgs KArgs;
 // The fused stepper epilogue of one 32-column tile (the STEP variant, 8-wave blocks): the
 // tile's dQ1 / dQ2 (the output layer's de-normalised f32 values, in LDS) through the
 // stepper epilogue of stepper.hip with every column's state read and written in place.
-// The tile runs in two halves of 16 columns; in a half, thread (wave w, lane l) takes
-// column 2w + l / 32 and levels [3j, 3j + 3) for j = l % 32, each level through
-// epi::epi_level (the standalone kernels' own function).  The four column sums run over
-// the levels in order from +0.0 as in the standalone kernels: the 32 level lanes of a
-// column pass the running sums down the lanes by shuffles, lane j adding its levels in
-// order.  Bit-identical to fv3_dense_forward_f64in followed by fv3_ml_epilogue_ex by
-// construction (tests/test_stepper_fused_gpu.py).
+// Thread (wave w, lane l): column 4w + l / 16 of the tile, levels [5j, 5j + 5) for
+// j = l % 16; each level is epi::epi_level (the standalone kernels' own function).  The
+// four column sums run over the levels in order from +0.0 as in the standalone kernels:
+// the 16 level lanes of a column pass the running sums down the lanes by shuffles, lane
+// j adding its 5 levels in order.  Bit-identical to fv3_dense_forward_f64in followed by
+// fv3_ml_epilogue_ex by construction (tests/test_stepper_fused_gpu.py).
 typedef __attribute__((address_space(4))) const epi::EpilogueArgs<double> KEpi;
 template <int NCOL, int NT>
 __device__ __forceinline__ void step_epilogue_tile(KEpi& a, int64_t tile, const float* __restrict__ s_dq)
 {
     static_assert(NCOL == 32 && NT == 512, "the fused stepper epilogue runs on 8-wave 32-column tiles");
-    constexpr int U = 3;  // 32 lanes x 3 levels >= nz (the host requires nz <= 80 <= 96)
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int jl = l & 31;
-    fv3_layout lay;
-    lay.ncol_blk = a.lay.ncol_blk;
-    lay.ld = a.lay.ld;
-    lay.blk_stride = a.lay.blk_stride;
+    const int col = 4 * w + (l >> 4), jl = l & 15;
+    const int64_t c = tile * NCOL + col;
+    const bool valid = c < a.ncol;
+    const int64_t off = valid ? col_offset(a.lay, c) : 0;
     const int nz = a.nz;
-    const int64_t ncol = a.ncol;
     const bool want_t = a.temp_out != nullptr;
+    constexpr int U = 5;  // 16 lanes x 5 levels >= nz (the host requires nz <= 80)
+    double sp[U], dp[U], tt[U];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int col = 16 * h + 2 * w + (l >> 5);
-        const int64_t c = tile * NCOL + col;
-        const bool valid = c < ncol;
-        const int64_t off = valid ? col_offset(lay, c) : 0;
-        double sp[U], dp[U], tt[U];
+    for (int u = 0; u < U; ++u) {
+        const int k = U * jl + u;
+        const bool on = valid && k < nz;
+        const int64_t i = off + (int64_t)(on ? k : 0) * a.lay.ld;
+        sp[u] = on ? a.sphum[i] : 0.0;
+        dp[u] = on ? a.delp[i] : 0.0;
+        tt[u] = on && want_t ? a.temp[i] : 0.0;
+    }
+    epi::EpiLevel<double> r[U];
+    int n1 = 0, n2 = 0;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int k = U * jl + u;
-            const bool on = valid && k < nz;
-            const int64_t i = off + (int64_t)(on ? k : 0) * lay.ld;
-            sp[u] = on ? a.sphum[i] : 0.0;
-            dp[u] = on ? a.delp[i] : 0.0;
-            tt[u] = on && want_t ? a.temp[i] : 0.0;
+    for (int u = 0; u < U; ++u) {
+        const int k = U * jl + u;
+        if (valid && k < nz) {
+            r[u] = epi::epi_level(a, off + (int64_t)k * a.lay.ld, s_dq[k * NCOL + col], s_dq[(nz + k) * NCOL + col],
+                                  sp[u], dp[u], tt[u]);
+            n1 += r[u].nan1;
+            n2 += r[u].nan2;
+        } else {
+            r[u] = epi::EpiLevel<double>{0.0, 0.0, 0.0, 0.0, false, false};
         }
-        epi::EpiLevel<double> r[U];
-        int n1 = 0, n2 = 0;
+    }
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    const int base = l & ~15;
+    for (int jj = 0; jj < 16; ++jj) {
+        const int src = base + (jj > 0 ? jj - 1 : 0);
+        const double i0 = __shfl(s0, src), i1 = __shfl(s1, src), i2 = __shfl(s2, src), i3 = __shfl(s3, src);
+        if (jl == jj) {
+            s0 = jj > 0 ? i0 : 0.0;
+            s1 = jj > 0 ? i1 : 0.0;
+            s2 = jj > 0 ? i2 : 0.0;
+            s3 = jj > 0 ? i3 : 0.0;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int k = U * jl + u;
-            if (valid && k < nz) {
-                r[u] = epi::epi_level(a, off + (int64_t)k * lay.ld, s_dq[k * NCOL + col], s_dq[(nz + k) * NCOL + col],
-                                      sp[u], dp[u], tt[u]);
-                n1 += r[u].nan1;
-                n2 += r[u].nan2;
-            } else {
-                r[u] = epi::EpiLevel<double>{0.0, 0.0, 0.0, 0.0, false, false};
-            }
-        }
-        double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-        const int base = l & ~31;
-        for (int jj = 0; jj < 32; ++jj) {
-            const int src = base + (jj > 0 ? jj - 1 : 0);
-            const double i0 = __shfl(s0, src), i1 = __shfl(s1, src), i2 = __shfl(s2, src), i3 = __shfl(s3, src);
-            if (jl == jj) {
-                s0 = jj > 0 ? i0 : 0.0;
-                s1 = jj > 0 ? i1 : 0.0;
-                s2 = jj > 0 ? i2 : 0.0;
-                s3 = jj > 0 ? i3 : 0.0;
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    if (U * jl + u < nz) {
-                        s0 = s0 + r[u].h;
-                        s1 = s1 + r[u].m;
-                        if (a.has_dq2) s2 = s2 + r[u].nm;
-                        if (a.has_dq1) s3 = s3 + r[u].ch;
-                    }
+            for (int u = 0; u < U; ++u) {
+                if (U * jl + u < nz) {
+                    s0 = s0 + r[u].h;
+                    s1 = s1 + r[u].m;
+                    if (a.has_dq2) s2 = s2 + r[u].nm;
+                    if (a.has_dq1) s3 = s3 + r[u].ch;
                 }
             }
         }
+    }
 #pragma unroll
-        for (int m = 16; m >= 1; m >>= 1) {  // the filled-level counts: integers, any order
-            n1 += __shfl_xor(n1, m);
-            n2 += __shfl_xor(n2, m);
-        }
-        if (valid && a.col && jl == 31) {
-            epi::epi_column_out(a, c, 0, s0, n1);
-            epi::epi_column_out(a, c, 1, s1, n2);
-            epi::epi_column_out(a, c, 2, s2, 0);
-            epi::epi_column_out(a, c, 3, s3, 0);
-        }
+    for (int m = 8; m >= 1; m >>= 1) {  // the filled-level counts: integers, any order
+        n1 += __shfl_xor(n1, m);
+        n2 += __shfl_xor(n2, m);
+    }
+    if (valid && a.col && jl == 15) {
+        epi::epi_column_out(a, c, 0, s0, n1);
+        epi::epi_column_out(a, c, 1, s1, n2);
+        epi::epi_column_out(a, c, 2, s2, 0);
+        epi::epi_column_out(a, c, 3, s3, 0);
     }
 }
 

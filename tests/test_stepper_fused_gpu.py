@@ -3,7 +3,7 @@ fv3_dense_stepper_f64in / stepper.BoundPredictEpilogue) against the two launches
 replaces (fv3_dense_forward_f64in + fv3_ml_epilogue_ex): the updated state, the limited
 tendencies, the limiter flags and the column diagnostics (precipitation accumulated in
 place) bit for bit, over several steps; MSE-conserving and legacy limiters, hydrostatic
-or not, NaN inputs, ragged column counts."""
+or not, NaN tendencies (inputs that make the model emit NaN), ragged column counts."""
 import numpy as np
 import pytest
 
@@ -50,7 +50,7 @@ def test_fused_predict_epilogue_bit_identical_to_two_launches(gpu, mse, hydro, r
         b3 = lambda a: a.permute(1, 0, 2, 3).reshape(a.shape[1], -1, res)[:, r0:r1].contiguous()  # noqa: E731
         state = {k: (b3(v) if v.dim() == 4 else v.reshape(-1, res)[r0:r1].contiguous()) for k, v in state.items()}
         level_axis = 0
-    # NaN inputs in a few columns
+    # NaN inputs in a few columns: the model's tendencies there are NaN (the filled counts)
     T = state["air_temperature"]
     if level_axis == 1:
         T[0, 3:6, 2, 2] = float("nan")
@@ -71,6 +71,7 @@ def test_fused_predict_epilogue_bit_identical_to_two_launches(gpu, mse, hydro, r
         for k in ("dQ1", "dQ2", "specific_humidity_limiter_active"):
             _bits(ea.out[k], out[k], (step, k))
     assert torch.isnan(ca[0]).sum() == 0  # NaN-skipping sums
+    assert (ca[4] > 0).any()  # some filled levels were counted
 
 
 def test_fused_predict_epilogue_refuses_what_it_cannot_fuse(gpu):
