@@ -335,9 +335,9 @@ typedef __attribute__((address_space(4))) const DenseArgs KArgs;
 // the 16 level lanes of a column pass the running sums down the lanes by shuffles, lane
 // j adding its 5 levels in order.  Bit-identical to fv3_dense_forward_f64in followed by
 // fv3_ml_epilogue_ex by construction (tests/test_stepper_fused_gpu.py).
-typedef __attribute__((address_space(4))) const epi::EpilogueArgs<double> KEpi;
 template <int NCOL, int NT>
-__device__ __forceinline__ void step_epilogue_tile(KEpi& a, int64_t tile, const float* __restrict__ s_dq)
+__device__ __forceinline__ void step_epilogue_tile(const epi::EpilogueArgs<double>& a, int64_t tile,
+                                                   const float* __restrict__ s_dq)
 {
     static_assert(NCOL == 32 && NT == 512, "the fused stepper epilogue runs on 8-wave 32-column tiles");
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -938,12 +938,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         if (has_next) stage(tile + gridDim.x, false);
         if constexpr (STEP) {
             tile_sync();  // every wave's dQ1 / dQ2 rows of the tile are in LDS
-            // the epilogue's arguments read in the kernarg segment (scalar loads), through a
-            // pointer opaque to the compiler: reloaded per tile (scalar-cache hits), not
-            // hoisted out of the tile loop as loop-invariant registers for the whole kernel
-            KArgs* pe = &p;
-            asm volatile("" : "+s"(pe));
-            step_epilogue_tile<NCOL, NT>(pe->ep, tile, s_dq);
+            // the kernarg copy, through a generic pointer (the epilogue helpers take one)
+            const epi::EpilogueArgs<double>& ep = *(const epi::EpilogueArgs<double>*)(&p.ep);
+            step_epilogue_tile<NCOL, NT>(ep, tile, s_dq);
         }
         prime_ring<RD, NW, FT>(g1, rw, voff, p.w1_off);  // the next tile's layer 1
         tile_sync();         // the activations are free for the next tile's inputs

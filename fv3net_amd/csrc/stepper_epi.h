@@ -48,10 +48,9 @@ struct EpiLevel {
     bool nan1, nan2;
 };
 
-// `A`: an EpilogueArgs<DT>, in any address space (the fused dense kernel reads its copy
-// in the kernarg segment with scalar loads)
-template <typename DT, typename A>
-__device__ __forceinline__ EpiLevel<DT> epi_level(A& a, int64_t i, float q1, float q2, DT sp, DT dp, DT t)
+template <typename DT>
+__device__ __forceinline__ EpiLevel<DT> epi_level(const EpilogueArgs<DT>& a, int64_t i, float q1, float q2, DT sp,
+                                                  DT dp, DT t)
 {
     const float dtf = (float)a.dt;  // f32 array * Python float -> f32
     const DT dtd = (DT)a.dt;
@@ -95,8 +94,8 @@ __device__ __forceinline__ EpiLevel<DT> epi_level(A& a, int64_t i, float q1, flo
 }
 
 // the column diagnostics from the four sums and the filled-level counts
-template <typename DT, typename A>
-__device__ __forceinline__ void epi_column_out(A& a, int64_t c, int s, DT sum, int n)
+template <typename DT>
+__device__ __forceinline__ void epi_column_out(const EpilogueArgs<DT>& a, int64_t c, int s, DT sum, int n)
 {
     const DT cv = (DT)(kCp - kRdgas);
     const DT ch = a.hydrostatic ? (DT)kCp : cv;

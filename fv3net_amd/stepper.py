@@ -16,7 +16,6 @@ dQp) in one column pass each (``fv3_tendency_columns``).  State variables are de
 tensors (float64 like the FV3 state, or float32) or DataArrays over them; the model's
 tendencies are float32 (Keras output).
 """
-import ctypes
 import dataclasses
 from typing import Dict, Hashable, Iterable, Mapping, Optional, Sequence, Set, Tuple
 
