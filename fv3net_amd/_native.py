@@ -54,7 +54,6 @@ EXPORTED_SYMBOLS = (
     "fv3_level_row_sums_f64",
     "fv3_fold_rows",
     "fv3_step_partials_f64",
-    "fv3_dense_stepper_f64in",
     "fv3_fold_rows_repeat",
     "fv3_ml_epilogue",
     "fv3_ml_epilogue_ex",
@@ -276,8 +275,6 @@ _SIGNATURES = {
     "fv3_standard_denormalize_f64": (_I, [_P, Layout, _P, _P, _I, _P, Layout, _I64, _I, _P]),
     "fv3_ml_epilogue": (_I, [ctypes.POINTER(EpilogueIO), Layout, _I64, _I, _I, _D, _I, _I, _P]),
     "fv3_ml_epilogue_ex": (_I, [ctypes.POINTER(EpilogueIO), Layout, _I64, _I, _I, _D, _I, _I, _I, _P]),
-    "fv3_dense_stepper_f64in": (_I, [_P, ctypes.POINTER(_P), ctypes.POINTER(Layout), _I64, ctypes.POINTER(EpilogueIO),
-                                     Layout, _I, _D, _I, _I, _I, _P]),
     "fv3_tendency_columns": (_I, [_P, _P, _P, _P, _P, _P, Layout, _I64, _I, _I, _I, _D, _P]),
     "fv3_member_reduce": (_I, [ctypes.POINTER(_P), _I, _I64, _I, _I, _P, _P]),
     "fv3_scale_levels": (_I, [_P, _I, Layout, _P, _I64, _I, _P, _P]),
@@ -296,8 +293,6 @@ _SIGNATURES = {
     "fv3_plan_add_dense_forward": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(Layout), ctypes.POINTER(_P),
                                         ctypes.POINTER(Layout), _I64, _I, _I]),
     "fv3_plan_add_ml_epilogue": (_I, [_P, ctypes.POINTER(EpilogueIO), Layout, _I64, _I, _I, _D, _I, _I, _I]),
-    "fv3_plan_add_dense_stepper": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(Layout), _I64,
-                                        ctypes.POINTER(EpilogueIO), Layout, _I, _D, _I, _I, _I]),
     "fv3_plan_add_area_weighted_sums_f64": (_I, [_P, ctypes.POINTER(_P), _I, _P, _I64, _P]),
     "fv3_plan_add_area_weighted_row_sums_f64": (_I, [_P, ctypes.POINTER(_P), _I, _P, _I64, _I, _P, _I64]),
     "fv3_plan_add_level_sums_u8": (_I, [_P, _P, Layout, _I64, _I, _P]),

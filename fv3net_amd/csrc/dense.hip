@@ -326,87 +326,7 @@ typedef __attribute__((address_space(4))) const DenseArgs KArgs;
 // 3: <= 168, letting three blocks share a CU)
 // RD: weight ring depth (groups of 4 k-steps held; refilled RD-1 groups ahead)
 // NW: waves per block (4: one per SIMD; 8: two per SIMD sharing a tile, T4 halved)
-// The fused stepper epilogue of one 32-column tile (the STEP variant, 8-wave blocks): the
-// tile's dQ1 / dQ2 (the output layer's de-normalised f32 values, in LDS) through the
-// stepper epilogue of stepper.hip with every column's state read and written in place.
-// Thread (wave w, lane l): column 4w + l / 16 of the tile, levels [5j, 5j + 5) for
-// j = l % 16; each level is epi::epi_level (the standalone kernels' own function).  The
-// four column sums run over the levels in order from +0.0 as in the standalone kernels:
-// the 16 level lanes of a column pass the running sums down the lanes by shuffles, lane
-// j adding its 5 levels in order.  Bit-identical to fv3_dense_forward_f64in followed by
-// fv3_ml_epilogue_ex by construction (tests/test_stepper_fused_gpu.py).
-template <int NCOL, int NT>
-__device__ __forceinline__ void step_epilogue_tile(const epi::EpilogueArgs<double>& a, int64_t tile,
-                                                   const float* __restrict__ s_dq)
-{
-    static_assert(NCOL == 32 && NT == 512, "the fused stepper epilogue runs on 8-wave 32-column tiles");
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int col = 4 * w + (l >> 4), jl = l & 15;
-    const int64_t c = tile * NCOL + col;
-    const bool valid = c < a.ncol;
-    const int64_t off = valid ? col_offset(a.lay, c) : 0;
-    const int nz = a.nz;
-    const bool want_t = a.temp_out != nullptr;
-    constexpr int U = 5;  // 16 lanes x 5 levels >= nz (the host requires nz <= 80)
-    double sp[U], dp[U], tt[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int k = U * jl + u;
-        const bool on = valid && k < nz;
-        const int64_t i = off + (int64_t)(on ? k : 0) * a.lay.ld;
-        sp[u] = on ? a.sphum[i] : 0.0;
-        dp[u] = on ? a.delp[i] : 0.0;
-        tt[u] = on && want_t ? a.temp[i] : 0.0;
-    }
-    epi::EpiLevel<double> r[U];
-    int n1 = 0, n2 = 0;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int k = U * jl + u;
-        if (valid && k < nz) {
-            r[u] = epi::epi_level(a, off + (int64_t)k * a.lay.ld, s_dq[k * NCOL + col], s_dq[(nz + k) * NCOL + col],
-                                  sp[u], dp[u], tt[u]);
-            n1 += r[u].nan1;
-            n2 += r[u].nan2;
-        } else {
-            r[u] = epi::EpiLevel<double>{0.0, 0.0, 0.0, 0.0, false, false};
-        }
-    }
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-    const int base = l & ~15;
-    for (int jj = 0; jj < 16; ++jj) {
-        const int src = base + (jj > 0 ? jj - 1 : 0);
-        const double i0 = __shfl(s0, src), i1 = __shfl(s1, src), i2 = __shfl(s2, src), i3 = __shfl(s3, src);
-        if (jl == jj) {
-            s0 = jj > 0 ? i0 : 0.0;
-            s1 = jj > 0 ? i1 : 0.0;
-            s2 = jj > 0 ? i2 : 0.0;
-            s3 = jj > 0 ? i3 : 0.0;
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (U * jl + u < nz) {
-                    s0 = s0 + r[u].h;
-                    s1 = s1 + r[u].m;
-                    if (a.has_dq2) s2 = s2 + r[u].nm;
-                    if (a.has_dq1) s3 = s3 + r[u].ch;
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int m = 8; m >= 1; m >>= 1) {  // the filled-level counts: integers, any order
-        n1 += __shfl_xor(n1, m);
-        n2 += __shfl_xor(n2, m);
-    }
-    if (valid && a.col && jl == 15) {
-        epi::epi_column_out(a, c, 0, s0, n1);
-        epi::epi_column_out(a, c, 1, s1, n2);
-        epi::epi_column_out(a, c, 2, s2, 0);
-        epi::epi_column_out(a, c, 3, s3, 0);
-    }
-}
-
-template <int T4, int NC, int WPE, int RD, int NW, typename IT = float, bool STEP = false>
+template <int T4, int NC, int WPE, int RD, int NW, typename IT = float>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void dense_forward_kernel(DenseArgs pa)
 {
     // read the arguments in place in the kernarg segment (constant address space):
@@ -432,8 +352,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
     // not memory, so the bias reads after the next tile's input loads are issued do not
     // wait for those HBM loads (vector-memory loads complete in issue order)
     float* s_bias = s_ep + 6 * kop + 4;
-    float* s_dq = reinterpret_cast<float*>(lds) + p.lds_dq;  // STEP: [2][nz][NCOL] dQ1 / dQ2 of the tile
-    (void)s_dq;
 
     // issue priority over co-resident waves of other kernels (a VALU-bound remap beside
     // this MFMA-bound predict): s_setprio takes an immediate
@@ -881,10 +799,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
                 if (y >= hi[r]) y = hi[r];
                 y = y * mk[r];
                 const bool ok = cv_c[c] && row < onrow;  // padding rows of the last tile: no reads either
-                if constexpr (STEP) {  // the fused stepper epilogue takes the tile's dQ1 / dQ2 from LDS
-                    if (row < onrow) s_dq[(ovar * p.ep.nz + oz0 + row) * NCOL + 16 * c + (lane & 15)] = y;
-                    continue;
-                }
                 if (has_res) {  // after = before + to (Difference.backward)
                     const unsigned roff = ok ? (rb + (unsigned)(oz0 + row) * rld) * 4u : 0x80000000u;
                     y = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rres, (int)roff, 0, 0)) + y;
@@ -936,12 +850,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE, WP
         // ordered before the next tile's layer 1 by the barrier below.  Here, after the
         // output layer, rather than before it: C384 2,056 -> 2,044 us, C48 unchanged
         if (has_next) stage(tile + gridDim.x, false);
-        if constexpr (STEP) {
-            tile_sync();  // every wave's dQ1 / dQ2 rows of the tile are in LDS
-            // the kernarg copy, through a generic pointer (the epilogue helpers take one)
-            const epi::EpilogueArgs<double>& ep = *(const epi::EpilogueArgs<double>*)(&p.ep);
-            step_epilogue_tile<NCOL, NT>(ep, tile, s_dq);
-        }
         prime_ring<RD, NW, FT>(g1, rw, voff, p.w1_off);  // the next tile's layer 1
         tile_sync();         // the activations are free for the next tile's inputs
         trace_mark(p, tile, 4);
@@ -1228,10 +1136,8 @@ extern "C" int fv3_dense_k_in(const fv3_dense_model* m) { return m ? m->k_in : -
 extern "C" int fv3_dense_k_out(const fv3_dense_model* m) { return m ? m->k_out : -1; }
 
 // in64: inputs are float64 (read in place, cast to f32 in the staging)
-// step: the fused stepper epilogue (fv3_dense_stepper_f64in; outputs unused, may be NULL)
 static int dense_forward_impl(const fv3_dense_model* m, const void* const* inputs, bool in64, const fv3_layout* in_l,
-                              float* const* outputs, const fv3_layout* out_l, int64_t ncol, void* stream,
-                              const fv3::epi::EpilogueArgs<double>* step = nullptr)
+                              float* const* outputs, const fv3_layout* out_l, int64_t ncol, void* stream)
 {
     using namespace fv3;
     clear_error();
@@ -1243,17 +1149,8 @@ static int dense_forward_impl(const fv3_dense_model* m, const void* const* input
     FV3_REQUIRE(m, "dense_forward: NULL model");
     FV3_REQUIRE(ncol >= 0, "dense_forward: ncol < 0");
     if (ncol == 0) return FV3_OK;
-    FV3_REQUIRE(inputs && in_l && (step || (outputs && out_l)), "dense_forward: NULL argument");
+    FV3_REQUIRE(inputs && in_l && outputs && out_l, "dense_forward: NULL argument");
     DenseArgs a = m->tmpl;
-    if (step) {
-        // dQ1 / dQ2 (outputs 0 / 1) of nz <= 80 levels each, no residual: the tile's two
-        // tendencies fit the fused epilogue's LDS buffer and 16 lanes x 5 levels
-        FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED,
-                         in64 && m->n_out == 2 && m->out_nz[0] == step->nz && m->out_nz[1] == step->nz &&
-                             step->nz >= 1 && step->nz <= 80 && m->out_residual[0] < 0 && m->out_residual[1] < 0,
-                         "dense_stepper: needs float64 inputs and exactly two outputs of nz <= 80 levels (dQ1, dQ2)");
-        a.ep = *step;
-    }
     const int64_t nb = in_l[0].ncol_blk;
     for (int v = 0; v < m->n_in; ++v) {
         FV3_REQUIRE(inputs[v], "dense_forward: input %d is NULL", v);
@@ -1262,7 +1159,7 @@ static int dense_forward_impl(const fv3_dense_model* m, const void* const* input
         FV3_REQUIRE(in_l[v].ld < (1LL << 31) && in_l[v].blk_stride < (1LL << 31),
                     "dense_forward: input %d strides exceed 2^31 elements", v);
     }
-    for (int v = 0; v < (step ? 0 : m->n_out); ++v) {
+    for (int v = 0; v < m->n_out; ++v) {
         FV3_REQUIRE(outputs[v], "dense_forward: output %d is NULL", v);
         FV3_REQUIRE(layout_ok(out_l[v], ncol) && out_l[v].ncol_blk == nb,
                     "dense_forward: output %d layout invalid or ncol_blk differs", v);
@@ -1378,12 +1275,7 @@ static int dense_forward_impl(const fv3_dense_model* m, const void* const* input
     const size_t hbytes = (size_t)nc * 16 * 64 * (size_t)m->ht, xbytes = (size_t)nc * sizeof(float) * 16 * (size_t)m->kp;
     a.lds_s = (int)(hbytes / 16);
     a.lds_x = (int)((hbytes + xbytes) / 16);
-    size_t lds = lds_of(nc);
-    if (step) {  // + the tile's dQ1 / dQ2 for the fused epilogue, 16-byte aligned
-        lds = (lds + 15) / 16 * 16;
-        a.lds_dq = (int)(lds / sizeof(float));
-        lds += sizeof(float) * 2 * (size_t)step->nz * 16 * (size_t)nc;
-    }
+    const size_t lds = lds_of(nc);
     FV3_REQUIRE(lds <= 160 * 1024, "dense_forward: %d input features need too much LDS", m->kp);
     // (waves per SIMD targeted by register allocation, weight ring depth):
     // FV3_DENSE_CFG = "3,2" (default) | "2,3" | "4,2" (A/B)
@@ -1407,11 +1299,7 @@ static int dense_forward_impl(const fv3_dense_model* m, const void* const* input
     };
     FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, !in64 || nw == 8,
                      "dense_forward: float64 inputs need the 8-wave kernel (32-column tiles, width >= 128)");
-    FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, !step || (nw == 8 && nc == 2),
-                     "dense_stepper: the fused epilogue runs on the 8-wave kernel (32-column tiles, width >= 128)");
-    const void* kfn = step ? (m->ht / nw == 1 ? (const void*)dense_forward_kernel<1, 2, 4, 2, 8, double, true>
-                                               : (const void*)dense_forward_kernel<2, 2, 4, 2, 8, double, true>)
-                    : in64 ? (m->ht / nw == 1 ? (const void*)dense_forward_kernel<1, 2, 4, 2, 8, double>
+    const void* kfn = in64 ? (m->ht / nw == 1 ? (const void*)dense_forward_kernel<1, 2, 4, 2, 8, double>
                                               : (const void*)dense_forward_kernel<2, 2, 4, 2, 8, double>)
                            : kernel_of(m->ht / nw);
     // persistent blocks: resident blocks per CU x CUs (queried once per kernel);
@@ -1453,24 +1341,4 @@ extern "C" int fv3_dense_forward_f64in(const fv3_dense_model* m, const double* c
 {
     return dense_forward_impl(m, reinterpret_cast<const void* const*>(inputs), true, in_l, outputs, out_l, ncol,
                               stream);
-}
-
-// predict + the stepper epilogue in one launch (dense.hip STEP variant): the result of
-// fv3_dense_forward_f64in(m, inputs, ..., {dQ1, dQ2}) followed by fv3_ml_epilogue_ex(io,
-// lay, ncol, nz, state_f64 = 1, ...) except that the f32 dQ1 / dQ2 themselves are not
-// written (io->dq1 / io->dq2 are ignored)
-extern "C" int fv3_dense_stepper_f64in(const fv3_dense_model* m, const double* const* inputs, const fv3_layout* in_l,
-                                       int64_t ncol, const fv3_epilogue_io* io, fv3_layout lay, int nz, double dt,
-                                       int mse_conserving, int hydrostatic, int flags, void* stream)
-{
-    using namespace fv3;
-    clear_error();
-    FV3_REQUIRE(io, "dense_stepper: NULL io");
-    FV3_REQUIRE(io->sphum && io->delp && io->temperature,
-                "dense_stepper: specific humidity, delp and air temperature are required");
-    FV3_REQUIRE(ncol == 0 || layout_ok(lay, ncol), "dense_stepper: bad layout");
-    FV3_REQUIRE(!io->dq1_out == !io->dq2_out, "dense_stepper: dq1_out and dq2_out go together");
-    epi::EpilogueArgs<double> ep = epi::make_args<double>(*io, lay, ncol, nz, dt, mse_conserving, hydrostatic, flags);
-    return dense_forward_impl(m, reinterpret_cast<const void* const*>(inputs), true, in_l, nullptr, nullptr, ncol,
-                              stream, &ep);
 }

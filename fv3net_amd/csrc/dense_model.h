@@ -5,7 +5,6 @@
 #include <vector>
 
 #include "common.h"
-#include "stepper_epi.h"
 
 namespace fv3 {
 
@@ -70,11 +69,6 @@ struct DenseArgs {
     int fast_stage;         // every slot FPS-aligned: the short staging path
     long long* trace;       // profiling hook (fv3_dense_set_trace): [tiles][8] timestamps, or NULL
     int prio;               // wave issue priority (s_setprio 0..3) for the whole kernel (FV3_DENSE_PRIO)
-    // the fused stepper epilogue (fv3_dense_stepper_f64in; the kernel's STEP variant only):
-    // the epilogue's arguments, and the float offset of the [2][nz][NCOL] dQ1 / dQ2 tile
-    // buffer in LDS
-    epi::EpilogueArgs<double> ep;
-    int lds_dq;
 };
 static_assert(sizeof(DenseArgs) <= 4096, "kernel arguments are limited to 4 KiB");
 

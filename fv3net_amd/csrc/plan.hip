@@ -108,24 +108,6 @@ extern "C" int fv3_plan_add_ml_epilogue(fv3_plan* plan, const fv3_epilogue_io* i
     return FV3_OK;
 }
 
-extern "C" int fv3_plan_add_dense_stepper(fv3_plan* plan, const fv3_dense_model* m, const double* const* inputs,
-                                          const fv3_layout* in_l, int64_t ncol, const fv3_epilogue_io* io,
-                                          fv3_layout lay, int nz, double dt, int mse_conserving, int hydrostatic,
-                                          int flags)
-{
-    using namespace fv3;
-    clear_error();
-    FV3_REQUIRE(plan && m && inputs && in_l && io, "plan_add_dense_stepper: NULL argument");
-    std::vector<const double*> in(inputs, inputs + m->n_in);
-    std::vector<fv3_layout> inl(in_l, in_l + m->n_in);
-    const fv3_epilogue_io cp = *io;
-    plan->ops.push_back([=](void* s) {
-        return fv3_dense_stepper_f64in(m, in.data(), inl.data(), ncol, &cp, lay, nz, dt, mse_conserving, hydrostatic,
-                                       flags, s);
-    });
-    return FV3_OK;
-}
-
 extern "C" int fv3_plan_add_area_weighted_sums_f64(fv3_plan* plan, const double* const* diags, int n_diag,
                                                    const double* area, int64_t n, double* out)
 {

@@ -25,7 +25,7 @@ _PLAN_OPS = {
 
 
 class LaunchPlan:
-    """``add(bound)`` for a BoundForward, a BoundEpilogue, a BoundPredictEpilogue or a bound reduction
+    """``add(bound)`` for a BoundForward, a BoundEpilogue or a bound reduction
     (``distributed.bind_*``: the float64 sums, row sums, uint8 level sums and the row
     fold); ``copy(dst, src)`` for a device-to-device copy; calling the plan issues every
     op in order on the stream (a torch stream, a raw hipStream_t int, or None for the
@@ -45,14 +45,10 @@ class LaunchPlan:
 
     def add(self, bound):
         from .dense import BoundForward
-        from .stepper import BoundEpilogue, BoundPredictEpilogue
+        from .stepper import BoundEpilogue
 
         lib = self._lib
-        if isinstance(bound, BoundPredictEpilogue):
-            st = lib.fv3_plan_add_dense_stepper(self._h, *bound._plan_args)
-            if not st:
-                bound.bound.model._plans.add(self)  # the model refuses close() while this plan lives
-        elif isinstance(bound, BoundForward):
+        if isinstance(bound, BoundForward):
             st = lib.fv3_plan_add_dense_forward(
                 self._h, bound._handle, ctypes.cast(bound._in_ptrs, ctypes.POINTER(ctypes.c_void_p)), bound._in_l,
                 bound._out_ptrs, bound._out_l, bound._ncol, bound._prec, int(bound._in64))

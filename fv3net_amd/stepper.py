@@ -173,55 +173,6 @@ class BoundEpilogue:
         return self.out
 
 
-class BoundPredictEpilogue:
-    """A bound predict (``DenseColumnModel.bind`` on the float64 state, read in place)
-    and its ``BoundEpilogue`` as ONE launch: the dense kernel runs the stepper epilogue
-    on each 32-column tile right after its output layer (``fv3_dense_stepper_f64in``),
-    the tile's dQ1 / dQ2 kept in LDS.  The same state, limited tendencies, limiter flags
-    and column diagnostics as the two launches, bit for bit; the float32 dQ1 / dQ2 are not
-    written.  ``supported(bound, epi)`` says whether the pair qualifies (float64 state,
-    dQ1 / dQ2 the model's only outputs, nz <= 80); the workloads fall back to the two
-    launches otherwise (and with ``FV3_STEPPER_FUSED=0`` under ``FV3_VARIANTS=1``)."""
-
-    def __init__(self, bound, epi: BoundEpilogue):
-        ok, why = self.supported(bound, epi)
-        if not ok:
-            raise NotImplementedError(f"fused predict + epilogue: {why}")
-        self.bound, self.epi = bound, epi
-        _, lay, ncol, nz, _, dt, mse, hydro, flags = epi._args
-        self._fn = _native.load().fv3_dense_stepper_f64in
-        self._args = (bound._handle, ctypes.cast(bound._in_ptrs, ctypes.POINTER(ctypes.c_void_p)), bound._in_l,
-                      bound._ncol, ctypes_byref(epi._io), lay, nz, dt, mse, hydro, flags)
-        self._plan_args = self._args[:4] + (ctypes_byref(epi._io),) + self._args[5:]
-        self._keep = list(bound.inputs) + list(epi._keep)
-        self.out = epi.out
-
-    @staticmethod
-    def supported(bound, epi) -> Tuple[bool, str]:
-        if _native.variant("FV3_STEPPER_FUSED") == "0":
-            return False, "FV3_STEPPER_FUSED=0"
-        if not getattr(bound, "_in64", False):
-            return False, "the predict does not read a float64 state in place"
-        _, lay, ncol, nz, state_f64, *_ = epi._args
-        if not state_f64:
-            return False, "float32 state"
-        cfg = bound.model.config
-        if len(cfg.out_nz) != 2 or any(n != nz for n in cfg.out_nz) or nz > 80:
-            return False, "the model's outputs are not dQ1 / dQ2 of nz <= 80 levels"
-        if bound._ncol != ncol:
-            return False, "the predict and the epilogue disagree on the columns"
-        if bound.outputs[0].data_ptr() != epi._io.dq1 or bound.outputs[1].data_ptr() != epi._io.dq2:
-            return False, "the epilogue does not read the predict's outputs"
-        return True, ""
-
-    def __call__(self, stream=None) -> Dict[str, object]:
-        h = stream if isinstance(stream, int) else _device.stream_handle(stream, self._keep)
-        st_ = self._fn(*self._args, h)
-        if st_:
-            _native.check(st_, "dense_stepper")
-        return self.out
-
-
 def tendency_columns(tendency, delp, dt: float, mode: str, level_axis: int = 0, stream=None) -> Dict[str, object]:
     """One column pass over a non-(dQ1, dQ2) tendency (csrc/stepper.hip
     ``fv3_tendency_columns``).  ``mode`` "wind" (dQu / dQv): ``integral`` =

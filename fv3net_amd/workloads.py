@@ -209,9 +209,7 @@ class StepperWorkload:
         diags = [res["net_moistening_due_to_machine_learning"], res["column_heating_due_to_machine_learning"],
                  res["total_precipitation"]]
         self._part = bind_area_weighted_partials(diags, self.area)  # float64 diagnostics: the f64 reduction
-        # one C-ABI call per step; the predict and the epilogue as one launch where the
-        # dense kernel's fused epilogue applies (stepper.BoundPredictEpilogue)
-        self._plan = LaunchPlan(_predict_epilogue(self.bound, self._epi) + [self._part])
+        self._plan = LaunchPlan([self.bound, self._epi, self._part])  # one C-ABI call per step
 
     def step(self):
         from . import _device
@@ -252,16 +250,6 @@ def make_stepper_workload(res: int = 96, seed: int = 0, device=None, group=None,
     model = DenseColumnModel.random(dense_2x256_config(), seed=1, sample_inputs=[sample_T, sample_q],
                                     sample_outputs=sample_out)
     return StepperWorkload(model, state, area, 900.0, 6 * res * res, group, precision=precision)
-
-
-def _predict_epilogue(bound, epi) -> list:
-    """The step's predict + epilogue launches: one fused launch
-    (stepper.BoundPredictEpilogue: the dense kernel runs the epilogue on each tile) where
-    it applies, else the two."""
-    from .stepper import BoundPredictEpilogue
-
-    ok, _ = BoundPredictEpilogue.supported(bound, epi)
-    return [BoundPredictEpilogue(bound, epi)] if ok else [bound, epi]
 
 
 class _Result:
@@ -349,7 +337,7 @@ class ShardedStepperWorkload:
         # one C-ABI call per step: predict, epilogue, row partials + limiter counts (and,
         # with the stubbed exchange, this band's partials copied for every rank + the
         # fold, one launch)
-        self._plan = LaunchPlan(_predict_epilogue(self.bound, self._epi) + [self._diag])
+        self._plan = LaunchPlan([self.bound, self._epi, self._diag])
         if self._fold is not None:
             self._plan.add(self._fold)
 

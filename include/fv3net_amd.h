@@ -59,8 +59,7 @@ int fv3_abi_version(void); /* bumped on any signature change (2: emulator fields
                               9: fv3_host_alloc / free / copy, the arena, replace
                                  fv3_host_register / unregister; wind rotation,
                                  fv3_sum_squares, fv3_cos_zenith,
-                              10: fv3_step_partials_f64, fv3_fold_rows_repeat,
-                                  fv3_dense_stepper_f64in) */
+                              10: fv3_step_partials_f64, fv3_fold_rows_repeat) */
 const char* fv3_build_kind(void); /* "product" (fv3net_amd/build.py, no experiment knob compiled in)
                                      or "experiment" (a tools/ variant: results may be invalid) */
 
@@ -461,17 +460,6 @@ int fv3_ml_epilogue_ex(const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, 
  * skipped.  Any output may be NULL. */
 #define FV3_TEND_WIND 0
 #define FV3_TEND_MASS 1
-/* The stepper's predict and epilogue in ONE launch (the dense kernel's fused epilogue):
- * the state of fv3_dense_forward_f64in(model, inputs, in_l, {dQ1, dQ2}, ...) followed by
- * fv3_ml_epilogue_ex(io, lay, ncol, nz, state_f64 = 1, dt, mse_conserving, hydrostatic,
- * flags), bit for bit, except that the float32 dQ1 / dQ2 are not written (io->dq1 /
- * io->dq2 are ignored).  The model's outputs 0 and 1 are dQ1 and dQ2 of nz <= 80 levels
- * each (no residual); float64 inputs (the state read in place).  FV3_ERR_UNSUPPORTED
- * otherwise: take the two launches. */
-int fv3_dense_stepper_f64in(const fv3_dense_model* model, const double* const* inputs, const fv3_layout* in_l,
-                            int64_t ncol, const fv3_epilogue_io* io, fv3_layout lay, int nz, double dt,
-                            int mse_conserving, int hydrostatic, int flags, void* stream);
-
 int fv3_tendency_columns(const float* tendency, const void* delp, double* filled_out, void* state_out,
                          void* integral, void* filled_frac, fv3_layout lay, int64_t ncol, int nz,
                          int state_f64, int mode, double dt, void* stream);
@@ -712,9 +700,6 @@ int fv3_plan_add_dense_forward(fv3_plan* plan, const fv3_dense_model* model, con
                                int precision, int inputs_f64);
 int fv3_plan_add_ml_epilogue(fv3_plan* plan, const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, int nz,
                              int state_f64, double dt, int mse_conserving, int hydrostatic, int flags);
-int fv3_plan_add_dense_stepper(fv3_plan* plan, const fv3_dense_model* model, const double* const* inputs,
-                               const fv3_layout* in_l, int64_t ncol, const fv3_epilogue_io* io, fv3_layout lay,
-                               int nz, double dt, int mse_conserving, int hydrostatic, int flags);
 int fv3_plan_add_area_weighted_sums_f64(fv3_plan* plan, const double* const* diags, int n_diag, const double* area,
                                         int64_t n, double* out);
 int fv3_plan_add_area_weighted_row_sums_f64(fv3_plan* plan, const double* const* diags, int n_diag,
