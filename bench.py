@@ -314,9 +314,10 @@ def rank_share_legs(dev, settle_ms=150.0, world=8):
         "ratio_to_full_over_world": rec[world]["step_ms"] / (rec[1]["step_ms"] / world),
         "predict_ratio_to_full_over_world": rec[world]["predict_ms"] / (rec[1]["predict_ms"] / world),
         "exchange_bytes_per_rank_per_step": rec[world]["exchange_bytes"],
-        "note": "wall clock per step (predict + fused epilogue + row partials + limiter counts + fold, every "
-                "launch marshalled once: workloads.ShardedStepperWorkload._bind); exchange stubbed by a local "
-                "copy of the gathered bytes"}
+        "note": "wall clock per step: predict, the fused stepper epilogue, the row partials + limiter counts "
+                "(one launch), the stubbed exchange's copy + fold (one launch), all four issued by one launch "
+                "plan (workloads.ShardedStepperWorkload._bind); the exchange stubbed by a local copy of the "
+                "gathered bytes"}
     # config #5: C384 emulator, 110,592 columns per rank at world 8
     for prec in ("bf16x3", "f32"):
         rec = {}
