@@ -160,7 +160,6 @@ struct MappmArgs {
     int64_t ncol;
     int km, kn, iv, kord;
     float* scratch;  // kord > 7: [2][km+3][grid * block] (NULL: the LDS path)
-    int pdiv = 1;    // the short pressure-only divisions where in range (FV3_MAPPM_PDIV=0: never)
 };
 
 __device__ __forceinline__ DevCol make_col(const MappmArgs& a, int64_t c)
@@ -185,12 +184,7 @@ __global__ __launch_bounds__(256) void mappm_ppm_kernel(MappmArgs a)
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= a.ncol) return;
     DevCol col = make_col(a, c);
-    // the short pressure-only divisions when every column of the wave has its pressures
-    // in range (mappm_core.h pdiv: the same bits)
-    if (__all(a.pdiv && pressures_in_range(col, a.km, a.kn)))
-        mappm_ppm_column<DevCol, true, true, true>(col, a.km, a.kn, a.iv, a.kord);
-    else
-        mappm_ppm_column<DevCol, true, true, false>(col, a.km, a.kn, a.iv, a.kord);
+    mappm_ppm_column<DevCol, true, true>(col, a.km, a.kn, a.iv, a.kord);
 }
 
 // tools/mappm_small_time.py, kord 1 79->79: C48 (13,824 columns) 142 -> 38 us, C96
@@ -465,13 +459,6 @@ const void* cs_global_kernel(const MappmArgs& a, int64_t nlanes)
 
 // kord <= 7: the level-parallel kernel while one lane per column leaves the chip
 // mostly idle (FV3_MAPPM_PATH=serial|levels overrides, for tests and A/B).
-// the short pressure-only divisions (mappm_core.h pdiv), on unless FV3_MAPPM_PDIV=0 (A/B)
-int pdiv_enabled()
-{
-    const char* p = fv3::variant_env("FV3_MAPPM_PDIV");
-    return !(p && p[0] == '0');
-}
-
 bool use_levels_kernel(const MappmArgs& a)
 {
     const char* p = fv3::variant_env("FV3_MAPPM_PATH");
@@ -527,7 +514,6 @@ struct MappmPairArgs {
     fv3_layout l_q1[2], l_q2[2];
     int64_t ncol;
     int km, kn, iv, kord;
-    int pdiv = 1;  // as MappmArgs::pdiv
 };
 
 // DevCol for mappm_ppm_columns<2>: fields f = 0, 1 emit output k in turn, so each keeps
@@ -586,10 +572,7 @@ __global__ __launch_bounds__(256) void mappm_ppm_pair_kernel(MappmPairArgs a)
 #ifndef FV3_MAPPM_PAIR_CARRY
 #define FV3_MAPPM_PAIR_CARRY 1  // 0: tools A/B builds
 #endif
-    if (__all(a.pdiv && pressures_in_range(d, a.km, a.kn)))
-        mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0, false, true>(d, a.km, a.kn, a.iv, a.kord);
-    else
-        mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0, false, false>(d, a.km, a.kn, a.iv, a.kord);
+    mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0>(d, a.km, a.kn, a.iv, a.kord);
 }
 
 // Small grids with one lane per column left the SIMDs short of waves (one rank's share
@@ -655,10 +638,7 @@ __global__ __launch_bounds__(128) void mappm_ppm_pair_split_kernel(MappmPairArgs
     for (int f = 0; f < 2; ++f) d.q2_[f] += (int64_t)(kf - 1) * d.ld_q2[f];
     d.pe2_next = d.pe2_ + (int64_t)(kf + 1) * d.ld_pe2;
     d.nb = (kf + 2 <= kn + 1) ? *d.pe2_next : 0.0f;
-    if (__all(a.pdiv && pressures_in_range(d, km, kn)))
-        mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0, true, true>(d, km, kn, a.iv, a.kord, kf, kl, Lf);
-    else
-        mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0, true, false>(d, km, kn, a.iv, a.kord, kf, kl, Lf);
+    mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0, true>(d, km, kn, a.iv, a.kord, kf, kl, Lf);
 }
 
 // Where the two-lane kernel pays (tools/mappm_split_time.py, profiles/r05r_mappm_split.log,
@@ -696,7 +676,6 @@ extern "C" int fv3_mappm_ex(const float* pe1, fv3_layout pe1_l, const float* q1,
                 "mappm: invalid column layout");
     FV3_REQUIRE(ncol / 256 < (int64_t)0x7fffffff, "mappm: ncol too large");
     MappmArgs a{pe1, q1, pe2, q2, pe1_l, q1_l, pe2_l, q2_l, ncol, km, kn, iv, kord, nullptr};
-    a.pdiv = fv3::pdiv_enabled();
     return fv3::launch_mappm(a, (hipStream_t)stream);
 }
 
@@ -736,7 +715,6 @@ extern "C" int fv3_mappm_multi(const float* pe1, fv3_layout pe1_l, const float* 
         for (; f + 2 <= n_fields; f += 2) {
             fv3::MappmPairArgs a{pe1, pe2, pe1_l, pe2_l, {q1[f], q1[f + 1]}, {q2[f], q2[f + 1]},
                                  {q1_l[f], q1_l[f + 1]}, {q2_l[f], q2_l[f + 1]}, ncol, km, kn, iv, kord};
-            a.pdiv = fv3::pdiv_enabled();
             const int block = 256;
             if (fv3::use_split_kernel(ncol)) {  // two lanes per column: 128 threads per 64 columns
                 const int64_t grid = (ncol + 63) / 64;

@@ -36,53 +36,6 @@
 
 namespace fv3 {
 
-// n / d for the pressure-only divisions of the PPM profile and the remap (dp sums,
-// edge positions): with F, the IEEE division's own rcp and Newton steps without
-// v_div_scale / v_div_fmas / v_div_fixup (8 instructions for 11).  Those three only act
-// when an operand needs scaling or is special (zero, inf, NaN, denormal, |n / d| outside
-// [2^-126, 2^96)); the kernels take F only for a wave whose columns all pass
-// pressures_in_range (every pe1 / pe2 in [2^-20, 2^38], pe1 strictly increasing), where
-// every such operand is +0 or a normal number in [2^-44, 2^40] and no quotient leaves
-// [2^-84, 2^84]: the same operations on the same values, so the same bits.  On the host
-// (tests/native) both are the IEEE division.
-template <bool F>
-FV3_HD inline float pdiv(float n, float d)
-{
-#if defined(__HIP_DEVICE_COMPILE__)
-    if constexpr (F) {
-        float r = __builtin_amdgcn_rcpf(d);
-        const float e = __builtin_fmaf(-d, r, 1.0f);
-        r = __builtin_fmaf(e, r, r);
-        float q = n * r;
-        const float e2 = __builtin_fmaf(-d, q, n);
-        q = __builtin_fmaf(e2, r, q);
-        const float e3 = __builtin_fmaf(-d, q, n);
-        return __builtin_fmaf(e3, r, q);
-    }
-#endif
-    return n / d;
-}
-
-// the range the short divisions need (see pdiv), for one column
-template <class Col>
-FV3_HD inline bool pressures_in_range(Col& c, int km, int kn)
-{
-    const float lo = 9.5367431640625e-07f, hi = 274877906944.0f;  // 2^-20, 2^38
-    bool ok = true;
-    float prev = c.pe1(1);
-    ok = ok && prev >= lo && prev <= hi;
-    for (int k = 2; k <= km + 1; ++k) {
-        const float v = c.pe1(k);
-        ok = ok && v > prev && v <= hi;
-        prev = v;
-    }
-    for (int k = 1; k <= kn + 1; ++k) {
-        const float v = c.pe2(k);
-        ok = ok && v >= lo && v <= hi;
-    }
-    return ok;
-}
-
 FV3_HD inline float fmax2(float a, float b) { return a > b ? a : b; }
 FV3_HD inline int imin2(int a, int b) { return a < b ? a : b; }
 FV3_HD inline int imax2(int a, int b) { return a > b ? a : b; }
@@ -186,13 +139,12 @@ FV3_HD inline float a6_of(const Ppm& a) { return 3.0f * (2.0f * a.a1 - (a.al + a
 
 // dc(k), interior k = 2..km-1 (mappm.f90:658-668); qm1,q0,qp1 = q(k-1..k+1),
 // dm1,d0,dp1 = delp(k-1..k+1).
-template <bool PD = false>
 FV3_HD inline float ppm_dc(float qm1, float q0, float qp1, float dm1, float d0, float dp1)
 {
     const float d4k = dm1 + d0;    // d4(k)
     const float d4kp = d0 + dp1;   // d4(k+1)
-    const float c1 = pdiv<PD>(dm1 + 0.5f * d0, d4kp);
-    const float c2 = pdiv<PD>(dp1 + 0.5f * d0, d4k);
+    const float c1 = (dm1 + 0.5f * d0) / d4kp;
+    const float c2 = (dp1 + 0.5f * d0) / d4k;
     const float delq_k = qp1 - q0;   // delq(k)
     const float delq_km = q0 - qm1;  // delq(k-1)
     const float df2 = d0 * (c1 * delq_k + c2 * delq_km) / (d4k + dp1);
@@ -201,7 +153,6 @@ FV3_HD inline float ppm_dc(float qm1, float q0, float qp1, float dm1, float d0, 
 
 // provisional left edge a4(2,k), interior k = 3..km-1 (mappm.f90:674-683);
 // d(-2..1) = delp(k-2..k+1), qm1,q0 = q(k-1), q(k); dcm1,dc0 = dc(k-1), dc(k).
-template <bool PD = false>
 FV3_HD inline float ppm_al(float dm2, float dm1, float d0, float dp1, float qm1, float q0,
                            float dcm1, float dc0)
 {
@@ -209,9 +160,9 @@ FV3_HD inline float ppm_al(float dm2, float dm1, float d0, float dp1, float qm1,
     const float d4k = dm1 + d0;    // d4(k)
     const float d4kp = d0 + dp1;   // d4(k+1)
     const float c1 = (q0 - qm1) * dm1 / d4k;
-    const float a1 = pdiv<PD>(d4km, d4k + dm1);
-    const float a2 = pdiv<PD>(d4kp, d4k + d0);
-    return qm1 + c1 + pdiv<PD>(2.0f, d4km + d4kp) * (d0 * (c1 * (a1 - a2) + a2 * dcm1) - dm1 * a1 * dc0);
+    const float a1 = d4km / (d4k + dm1);
+    const float a2 = d4kp / (d4k + d0);
+    return qm1 + c1 + 2.0f / (d4km + d4kp) * (d0 * (c1 * (a1 - a2) + a2 * dcm1) - dm1 * a1 * dc0);
 }
 
 // h2(k) (mappm.f90:784-795), k = 2..km-1.
@@ -321,7 +272,7 @@ FV3_HD inline void remap_layer(RemapState& s, const LayerView& v, const ColumnEn
 //    so a wave needs one pass per layer unless a lane has several inside outputs.
 // Holds for every input (no ordering assumption): each value is computed by the
 // reference's expression on the same operands.
-template <class Out, bool PD = false>
+template <class Out>
 FV3_HD inline void remap_layer_fast(RemapState& s, const LayerView& v, const ColumnEnds& e, int kn, Out& out)
 {
     const float r3 = 1.0f / 3.0f, r23 = 2.0f / 3.0f;
@@ -336,7 +287,7 @@ FV3_HD inline void remap_layer_fast(RemapState& s, const LayerView& v, const Col
         }
         // bottom piece (mappm.f90:105-112)
         const float delp = s.b - v.pl0;
-        const float esl = pdiv<PD>(delp, v.dp);
+        const float esl = delp / v.dp;
         s.qsum = s.qsum + delp * (v.a.al + 0.5f * esl * (v.a.ar - v.a.al + v.a.a6 * (1.0f - r23 * esl)));
         s.dpsum = s.dpsum + delp;
         out.emit(s.k, s.qsum / s.dpsum);
@@ -360,11 +311,11 @@ FV3_HD inline void remap_layer_fast(RemapState& s, const LayerView& v, const Col
             s.xv = false;
             continue;
         }
-        if (!s.xv) s.xt = pdiv<PD>(s.t - v.pl0, v.dp);
+        if (!s.xv) s.xt = (s.t - v.pl0) / v.dp;
         if (s.b <= v.pl1) {
             // entire new layer inside input layer L (mappm.f90:76-83)
             const float pl = s.xt;
-            const float pr = pdiv<PD>(s.b - v.pl0, v.dp);
+            const float pr = (s.b - v.pl0) / v.dp;
             const float tt = r3 * (pr * (pr + pl) + pl * pl);
             out.emit(s.k, v.a.al + 0.5f * (v.a.a6 + v.a.ar - v.a.al) * (pr + pl) - v.a.a6 * tt);
             s.k += 1;
@@ -439,8 +390,7 @@ FV3_HD inline void layer_hook(C&, long) {}
 // back edge (the mappm kernel: measured faster there, 0.527 vs 0.535 ms at C384 kord 1)
 // or at the iteration's start (the coarsen kernels: 1 field 0.767 -> 0.753 ms,
 // profiles/r04o_remap_ab.log).  Same loads, same bits.
-// PD: the short pressure-only divisions (pdiv; the caller checked pressures_in_range).
-template <class Col, bool FAST = true, bool CARRY = false, bool PD = false>
+template <class Col, bool FAST = true, bool CARRY = false>
 FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
 {
     // window state E_L: q(L..L+3), dp(L..L+3), pe1(L..L+4), dc(L..L+2), ALraw(L..L+2), h2(L-1..L+1)
@@ -456,9 +406,9 @@ FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
     const ColumnEnds ends{pev[0], c.pe1(km + 1), qv[0], c.q1(km)};
 
     float dc1, dc2, dc3, al1, al2, al3;
-    dc2 = ppm_dc<PD>(qv[0], qv[1], qv[2], dpv[0], dpv[1], dpv[2]);
-    dc3 = ppm_dc<PD>(qv[1], qv[2], qv[3], dpv[1], dpv[2], dpv[3]);  // 3 <= km-1
-    al3 = ppm_al<PD>(dpv[0], dpv[1], dpv[2], dpv[3], qv[1], qv[2], dc2, dc3);
+    dc2 = ppm_dc(qv[0], qv[1], qv[2], dpv[0], dpv[1], dpv[2]);
+    dc3 = ppm_dc(qv[1], qv[2], qv[3], dpv[1], dpv[2], dpv[3]);  // 3 <= km-1
+    al3 = ppm_al(dpv[0], dpv[1], dpv[2], dpv[3], qv[1], qv[2], dc2, dc3);
     {   // top: area-preserving cubic (mappm.f90:689-725)
         const float d1 = dpv[0], d2 = dpv[1];
         const float q1 = qv[0], q2 = qv[1];
@@ -527,7 +477,7 @@ FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
         if (L <= kn) c.emit(L, v.a.al + v.a.ar + v.a.a6);
 #else
         if constexpr (FAST)
-            remap_layer_fast<Col, PD>(s, v, ends, kn, c);
+            remap_layer_fast(s, v, ends, kn, c);
         else
             remap_layer(s, v, ends, kn, c);
 #endif
@@ -555,8 +505,8 @@ FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
             dcm = qn - qv[3];
             alm = 0.5f * (qv[2] + qv[3]);
 #else
-            dcm = ppm_dc<PD>(qv[2], qv[3], qn, dpv[2], dpv[3], dpn);
-            alm = ppm_al<PD>(dpv[1], dpv[2], dpv[3], dpn, qv[2], qv[3], dcv[2], dcm);
+            dcm = ppm_dc(qv[2], qv[3], qn, dpv[2], dpv[3], dpn);
+            alm = ppm_al(dpv[1], dpv[2], dpv[3], dpn, qv[2], qv[3], dcv[2], dcm);
 #endif
         } else if (m == km) {
             // bottom: area-preserving cubic (mappm.f90:729-761)

@@ -32,12 +32,11 @@ namespace fv3 {
 struct DcShared {
     float c1, c2, den;
 };
-template <bool PD = false>
 FV3_HD inline DcShared ppm_dc_shared(float dm1, float d0, float dp1)
 {
     const float d4k = dm1 + d0;    // d4(k)
     const float d4kp = d0 + dp1;   // d4(k+1)
-    return DcShared{pdiv<PD>(dm1 + 0.5f * d0, d4kp), pdiv<PD>(dp1 + 0.5f * d0, d4k), d4k + dp1};
+    return DcShared{(dm1 + 0.5f * d0) / d4kp, (dp1 + 0.5f * d0) / d4k, d4k + dp1};
 }
 FV3_HD inline float ppm_dc_field(const DcShared& p, float qm1, float q0, float qp1, float d0)
 {
@@ -50,15 +49,14 @@ FV3_HD inline float ppm_dc_field(const DcShared& p, float qm1, float q0, float q
 struct AlShared {
     float d4k, s2, amd, a2, dm1a1;
 };
-template <bool PD = false>
 FV3_HD inline AlShared ppm_al_shared(float dm2, float dm1, float d0, float dp1)
 {
     const float d4km = dm2 + dm1;  // d4(k-1)
     const float d4k = dm1 + d0;    // d4(k)
     const float d4kp = d0 + dp1;   // d4(k+1)
-    const float a1 = pdiv<PD>(d4km, d4k + dm1);
-    const float a2 = pdiv<PD>(d4kp, d4k + d0);
-    return AlShared{d4k, pdiv<PD>(2.0f, d4km + d4kp), a1 - a2, a2, dm1 * a1};
+    const float a1 = d4km / (d4k + dm1);
+    const float a2 = d4kp / (d4k + d0);
+    return AlShared{d4k, 2.0f / (d4km + d4kp), a1 - a2, a2, dm1 * a1};
 }
 FV3_HD inline float ppm_al_field(const AlShared& p, float dm1, float d0, float qm1, float q0, float dcm1, float dc0)
 {
@@ -134,7 +132,7 @@ struct ColumnEndsN {
     float q_top[NF], q_bot[NF];
 };
 
-template <int NF, class Out, bool PD = false>
+template <int NF, class Out>
 FV3_HD inline void remap_layer_n(RemapStateN<NF>& s, const LayerViewN<NF>& v, const ColumnEndsN<NF>& e, int kn,
                                  Out& out)
 {
@@ -150,7 +148,7 @@ FV3_HD inline void remap_layer_n(RemapStateN<NF>& s, const LayerViewN<NF>& v, co
         }
         // bottom piece (mappm.f90:105-112)
         const float delp = s.b - v.pl0;
-        const float esl = pdiv<PD>(delp, v.dp);
+        const float esl = delp / v.dp;
         const float h = 0.5f * esl;
         const float w = 1.0f - r23 * esl;
         for (int f = 0; f < NF; ++f)
@@ -177,11 +175,11 @@ FV3_HD inline void remap_layer_n(RemapStateN<NF>& s, const LayerViewN<NF>& v, co
             s.xv = false;
             continue;
         }
-        if (!s.xv) s.xt = pdiv<PD>(s.t - v.pl0, v.dp);
+        if (!s.xv) s.xt = (s.t - v.pl0) / v.dp;
         if (s.b <= v.pl1) {
             // entire new layer inside input layer L (mappm.f90:76-83)
             const float pl = s.xt;
-            const float pr = pdiv<PD>(s.b - v.pl0, v.dp);
+            const float pr = (s.b - v.pl0) / v.dp;
             const float tt = r3 * (pr * (pr + pl) + pl * pl);
             const float x = pr + pl;
             for (int f = 0; f < NF; ++f)
@@ -287,9 +285,7 @@ FV3_HD inline int split_first_layer(Col& c, int km, float t, int cnt)
 // expression on the same operands as the streaming advance computes it) when
 // 4 <= L_first <= km - 3, else from layer 1 (the layers above output k_first's top edge
 // pass without a remap event).  A lane stops once it has emitted k_last.
-// PD: the short pressure-only divisions (mappm_core.h pdiv; the caller checked
-// pressures_in_range)
-template <int NF, class Col, bool CARRY = false, bool SPLIT = false, bool PD = false>
+template <int NF, class Col, bool CARRY = false, bool SPLIT = false>
 FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord, int k_first = 1, int k_last = 0,
                                      int L_first = 1)
 {
@@ -315,9 +311,9 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord, i
         for (int i = 0; i < 8; ++i) pw[i] = c.pe1(l0 + i);
         for (int i = 0; i < 7; ++i) dw[i] = pw[i + 1] - pw[i];
         DcShared pd[6];
-        for (int i = 1; i <= 5; ++i) pd[i] = ppm_dc_shared<PD>(dw[i - 1], dw[i], dw[i + 1]);  // dc(L0-2 .. L0+2)
+        for (int i = 1; i <= 5; ++i) pd[i] = ppm_dc_shared(dw[i - 1], dw[i], dw[i + 1]);  // dc(L0-2 .. L0+2)
         AlShared pa[6];
-        for (int i = 3; i <= 5; ++i) pa[i] = ppm_al_shared<PD>(dw[i - 2], dw[i - 1], dw[i], dw[i + 1]);  // AL(L0 .. L0+2)
+        for (int i = 3; i <= 5; ++i) pa[i] = ppm_al_shared(dw[i - 2], dw[i - 1], dw[i], dw[i + 1]);  // AL(L0 .. L0+2)
         for (int f = 0; f < NF; ++f) {
             float qw[7], dcw[6];
             for (int i = 0; i < 7; ++i) qw[i] = c.q1(f, l0 + i);
@@ -351,9 +347,9 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord, i
     for (int f = 0; f < NF; ++f) ends.q_top[f] = qv[f][0];
 
     {
-        const DcShared p2 = ppm_dc_shared<PD>(dpv[0], dpv[1], dpv[2]);
-        const DcShared p3 = ppm_dc_shared<PD>(dpv[1], dpv[2], dpv[3]);
-        const AlShared a3 = ppm_al_shared<PD>(dpv[0], dpv[1], dpv[2], dpv[3]);
+        const DcShared p2 = ppm_dc_shared(dpv[0], dpv[1], dpv[2]);
+        const DcShared p3 = ppm_dc_shared(dpv[1], dpv[2], dpv[3]);
+        const AlShared a3 = ppm_al_shared(dpv[0], dpv[1], dpv[2], dpv[3]);
         const float hden = dpv[1] + 0.5f * (dpv[0] + dpv[2]);
         const float d0sq = dpv[1] * dpv[1];
         for (int f = 0; f < NF; ++f) {
@@ -428,7 +424,7 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord, i
             v.ar[f] = a.ar;
             v.a6[f] = a.a6;
         }
-        remap_layer_n<NF, Col, PD>(s, v, ends, kn_out, c);
+        remap_layer_n<NF>(s, v, ends, kn_out, c);
         layer_hook(c, 0);
 
         if (L == km) break;
@@ -457,8 +453,8 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord, i
             alm[f] = 0.0f;
         }
         if (m <= km - 1) {
-            const DcShared pd = ppm_dc_shared<PD>(dpv[2], dpv[3], dpn);
-            const AlShared pa = ppm_al_shared<PD>(dpv[1], dpv[2], dpv[3], dpn);
+            const DcShared pd = ppm_dc_shared(dpv[2], dpv[3], dpn);
+            const AlShared pa = ppm_al_shared(dpv[1], dpv[2], dpv[3], dpn);
             for (int f = 0; f < NF; ++f) {
                 dcm[f] = ppm_dc_field(pd, qv[f][2], qv[f][3], qn[f], dpv[3]);
                 alm[f] = ppm_al_field(pa, dpv[2], dpv[3], qv[f][2], qv[f][3], dcv[f][2], dcm[f]);
