@@ -377,6 +377,13 @@ class DenseColumnModel:
     # ---- host arrays in, host arrays out (the drop-in call on numpy data) ----------
     _PIPELINE_MIN_BYTES = 64 << 20
 
+    @staticmethod
+    def _pipeline_two_min_bytes() -> int:
+        """Inputs from this size on (below _PIPELINE_MIN_BYTES) run as two pipelined
+        halves of the block axis; FV3_HOST_TWO_GROUPS_MIB under FV3_VARIANTS=1 for A/B."""
+        v = _native.variant("FV3_HOST_TWO_GROUPS_MIB")
+        return (int(v) << 20) if v else (8 << 20)
+
     def forward_host(self, arrays: Sequence, level_axes: Optional[Sequence[int]] = None,
                      precision: Optional[str] = None, out: Optional[Sequence[np.ndarray]] = None) -> List[np.ndarray]:
         """numpy inputs -> numpy float32 outputs (pure_keras.py:98-118 predicts on host
@@ -397,10 +404,19 @@ class DenseColumnModel:
         arrays = [np.ascontiguousarray(a) for a in arrays]
         axes = list(level_axes) if level_axes is not None else [0] * len(arrays)
         n0 = arrays[0].shape[0] if arrays[0].ndim else 0
-        blocks = (n0 >= 2 and all(a.ndim >= 2 and a.shape[0] == n0 and ax is not None and ax > 0
-                                  for a, ax in zip(arrays, axes))
-                  and sum(a.nbytes for a in arrays) >= self._PIPELINE_MIN_BYTES)
-        key = (tuple((a.shape, a.dtype.str, ax) for a, ax in zip(arrays, axes)), precision, blocks)
+        nbytes = sum(a.nbytes for a in arrays)
+        tiled = n0 >= 2 and all(a.ndim >= 2 and a.shape[0] == n0 and ax is not None and ax > 0
+                                for a, ax in zip(arrays, axes))
+        # pipeline groups of blocks: one block each from _PIPELINE_MIN_BYTES on, two halves
+        # from _PIPELINE_TWO_MIN_BYTES on (per-group host work ~60 us: fewer, larger groups
+        # for the mid sizes), else one call
+        groups = None
+        if tiled and nbytes >= self._PIPELINE_MIN_BYTES:
+            groups = tuple((t, t + 1) for t in range(n0))
+        elif tiled and nbytes >= self._pipeline_two_min_bytes():
+            groups = ((0, n0 // 2), (n0 // 2, n0))
+        blocks = groups is not None
+        key = (tuple((a.shape, a.dtype.str, ax) for a, ax in zip(arrays, axes)), precision, groups)
         ent = getattr(self, "_host_call", None)
         if ent is None or ent[0] != key or ent[1][0].device.index != torch.cuda.current_device():
             _device.require_gpu()
@@ -408,7 +424,8 @@ class DenseColumnModel:
             bufs = [torch.empty(a.shape, dtype=torch.from_numpy(a[:0].reshape(-1)).dtype, device=dev) for a in arrays]
             if blocks:
                 sub_axes = [ax - 1 for ax in axes]
-                runs = [self._bind_or_forward([b[t] for b in bufs], sub_axes, precision) for t in range(n0)]
+                runs = [self._bind_or_forward([b[g0] for b in bufs], sub_axes, precision) if g1 == g0 + 1 else
+                        self._bind_or_forward([b[g0:g1] for b in bufs], axes, precision) for g0, g1 in groups]
                 # (an idle stream for transfer.copy_fence, the out-copy stream)
                 streams = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
             else:
@@ -436,17 +453,19 @@ class DenseColumnModel:
         lib = _native.load()
         kernel_out = _native.variant("FV3_D2H_KERNEL") == "1"
         self._last_kernel_out = False
-        for t in range(n0):
-            # block t's inputs: the runtime's pageable copies, on the compute stream (the
-            # host waits for them while s_out copies block t - 1's outputs).  On a side
+        for gi, (g0, g1) in enumerate(groups):
+            t = slice(g0, g1) if g1 > g0 + 1 else g0
+            # group gi's inputs: the runtime's pageable copies, on the compute stream (the
+            # host waits for them while s_out copies group gi - 1's outputs).  On a side
             # stream of their own the two directions ran nearly in sequence: C384 30.3 ms
             # against 22.2 ms (profiles/r05g_host_ab.json, pipe_in_*)
             for a, b in zip(arrays, bufs):
                 st.h2d(a[t], out=b[t], stream=cur)
             transfer.copy_fence(cur, streams[0])
-            outs = runs[t](cur)
+            outs = runs[gi](cur)
             if host is None:
-                host = _host_outputs(out, [(n0,) + tuple(o.shape) for o in outs])
+                host = _host_outputs(out, [(n0,) + (tuple(o.shape[1:]) if g1 > g0 + 1 else tuple(o.shape))
+                                           for o in outs])
                 # FV3_D2H_KERNEL=1: out-copies as a kernel storing into the arena's pages
                 # on the compute stream (fv3_copy_to_host), the copy engines keeping the
                 # in-copies; default: the copy engines both ways

@@ -269,9 +269,11 @@ def test_dense_predictor_level_axis_anywhere(gpu, dims):
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("kernel_out", ["1", "0"])
-def test_forward_host_tile_pipeline_bit_identical(gpu, dtype, kernel_out, monkeypatch):
+@pytest.mark.parametrize("groups,ntile", [("tiles", 6), ("two", 6), ("two", 5)])
+def test_forward_host_tile_pipeline_bit_identical(gpu, dtype, kernel_out, groups, ntile, monkeypatch):
     """DenseColumnModel.forward_host over (tile, z, y, x) numpy arrays: the tile blocks
-    pipelined over three streams (threshold lowered so a C12 state takes the path) give
+    pipelined over two streams, one tile per group or two halves of the tile axis (the
+    thresholds lowered so a C12 state takes the path; 5 tiles: halves of 2 and 3), give
     the bits of the device-resident forward of the same values, on repeated calls, with
     fresh outputs each call; the out-copies by the fv3_copy_to_host kernel into the
     arena pages (FV3_D2H_KERNEL=1) or by the copy engines (0); a level-leading array
@@ -279,20 +281,24 @@ def test_forward_host_tile_pipeline_bit_identical(gpu, dtype, kernel_out, monkey
     import torch
 
     set_variant(monkeypatch, "FV3_D2H_KERNEL", kernel_out)
+    if groups == "two":
+        set_variant(monkeypatch, "FV3_HOST_TWO_GROUPS_MIB", "0")
 
     from fv3net_amd.dense import DenseColumnModel, DenseModelConfig
 
     rng = np.random.default_rng(12)
     cfg = DenseModelConfig(["T", "q"], ["dQ1", "dQ2"], [79, 79], [79, 79], width=256, depth=3)
-    T = rng.normal(260, 15, (6, 79, 12, 12)).astype(dtype)
-    q = rng.uniform(0, 0.02, (6, 79, 12, 12)).astype(dtype)
+    T = rng.normal(260, 15, (ntile, 79, 12, 12)).astype(dtype)
+    q = rng.uniform(0, 0.02, (ntile, 79, 12, 12)).astype(dtype)
     m = DenseColumnModel.random(cfg, seed=4, sample_inputs=[T[0].reshape(79, -1).T, q[0].reshape(79, -1).T])
     ref = m.forward([torch.from_numpy(T).cuda(), torch.from_numpy(q).cuda()], level_axes=[1, 1])
     ref = [r.cpu().numpy() for r in ref]
-    m._PIPELINE_MIN_BYTES = 0
+    if groups == "tiles":
+        m._PIPELINE_MIN_BYTES = 0
     a = m.forward_host([T, q], [1, 1])
     b = m.forward_host([T, q], [1, 1])
     assert m._host_call[3] is not None  # the pipelined path
+    assert len(m._host_call[2]) == (ntile if groups == "tiles" else 2)
     # fresh outputs live in the page-locked arena, so FV3_D2H_KERNEL=1 takes the kernel
     assert m._last_kernel_out == (kernel_out == "1")
     assert a[0] is not b[0]

@@ -1,5 +1,5 @@
-"""forward_host one call vs tile-pipelined (with the copy fence) by size: the crossover
-that sets DenseColumnModel._PIPELINE_MIN_BYTES.  Float64 (6, 79, n, n) T/q in, float32
+"""forward_host one call vs tile-pipelined (with the copy fence) vs two pipelined halves,
+by size: the crossovers that set DenseColumnModel._PIPELINE_MIN_BYTES and the two-group size.  Float64 (6, 79, n, n) T/q in, float32
 out (arena), wall ms, interleaved."""
 import json
 import os
@@ -26,8 +26,10 @@ def main():
         outs = [transfer.empty_host(T.shape, np.float32) for _ in range(2)]
         line = {}
         for rnd in range(3):
-            for mode, thr in (("one", 1 << 62), ("pipe", 0)):
+            for mode, thr, two in (("one", 1 << 62, "100000"), ("pipe", 0, "100000"), ("two", 1 << 62, "0")):
                 DenseColumnModel._PIPELINE_MIN_BYTES = thr
+                os.environ["FV3_VARIANTS"] = "1"
+                os.environ["FV3_HOST_TWO_GROUPS_MIB"] = two
                 reps = max(5, int(2000 / max(n * n / 64, 1)))
                 for _ in range(2):
                     wl.model.forward_host([T, q], [1, 1], out=outs)
