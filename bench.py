@@ -395,7 +395,7 @@ def host_to_host(dev, res, steps=10):
             "host_path": transfer.host_path(),
             "note": "float64 numpy in -> DenseColumnModel.forward_host: H2D (see host_path), the fused predict "
                     "(f64 read in place), D2H into float32 numpy outputs reused across calls (library arena "
-                    "when host_path is arena); tile blocks pipelined over two streams above 64 MiB (C384)"}
+                    "when host_path is arena); tile blocks pipelined over two streams from 128 MiB (C384), two halves from 48 MiB"}
 
 
 def predict_mappm_host_to_host(dev, res=384, steps=5, bands=6, fence=True):

@@ -375,14 +375,18 @@ class DenseColumnModel:
         return self._last_bound
 
     # ---- host arrays in, host arrays out (the drop-in call on numpy data) ----------
-    _PIPELINE_MIN_BYTES = 64 << 20
+    # one group per block from here on; two halves of the block axis from
+    # _pipeline_two_min_bytes() on; one call below (profiles/r05y_pipeline_groups.log,
+    # float64 (6, 79, n, n) T/q: C48 16 MiB one call 0.584 / two halves 0.62 / per tile
+    # 0.90 ms; C96 66 MiB 2.09 / 1.94 / 2.03; C192 266 MiB 8.08 / 7.09 / 6.44)
+    _PIPELINE_MIN_BYTES = 128 << 20
 
     @staticmethod
     def _pipeline_two_min_bytes() -> int:
         """Inputs from this size on (below _PIPELINE_MIN_BYTES) run as two pipelined
         halves of the block axis; FV3_HOST_TWO_GROUPS_MIB under FV3_VARIANTS=1 for A/B."""
         v = _native.variant("FV3_HOST_TWO_GROUPS_MIB")
-        return (int(v) << 20) if v else (8 << 20)
+        return (int(v) << 20) if v else (48 << 20)
 
     def forward_host(self, arrays: Sequence, level_axes: Optional[Sequence[int]] = None,
                      precision: Optional[str] = None, out: Optional[Sequence[np.ndarray]] = None) -> List[np.ndarray]:
@@ -392,8 +396,9 @@ class DenseColumnModel:
         by the kernel), cached per shape with the bound kernel.
 
         Inputs with a common leading block axis (tiles: ``(tile, z, y, x)``, level axis
-        > 0) over ``_PIPELINE_MIN_BYTES`` run pipelined over the blocks on two streams:
-        block b + 1's host-to-device copies and block b's device-to-host copies overlap
+        > 0) of ``_PIPELINE_MIN_BYTES`` and more run pipelined over the blocks on two
+        streams (from ``_pipeline_two_min_bytes()`` on, over two halves of the block axis):
+        group g + 1's host-to-device copies and group g's device-to-host copies overlap
         (PCIe is full duplex: in and out at once).  The
         same kernels on the same columns, so the outputs are bit-identical to one call.
         ``out``: float32 numpy arrays to write, else arrays in the library's page-locked
