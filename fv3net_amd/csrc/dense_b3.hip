@@ -100,7 +100,6 @@ constexpr int b3_in_bytes(bool gl, int nwv) { return gl ? 2 * nwv * 8 * 64 * 4 :
 struct B3Pack {
     void* dbuf = nullptr;
     int ns = 2;  // bf16 parts per weight (2: bf16x3, 3: bf16x6)
-    bool w32 = false;  // the dense_b3w_kernel stream (32x32x16 fragments)
     int hu = 0, hp = 0, kp1 = 0, n1 = 0, nhx = 0, n_oc = 0, kop = 0, nch = 0;
     int nconst = 0, wbytes = 0, any_log = 0;
     std::vector<int> gmeta;  // per 8-feature group: var | zstart << 4 | nvalid << 24
@@ -984,354 +983,6 @@ dense_b3_kernel(B3Args pa)
     }
 }
 
-// ------------------------------------------------------------------------------------
-// W32: the same graph and split arithmetic on v_mfma_f32_32x32x16_bf16 (bf16x3 only).
-// A 16x16x32 MFMA holds its SIMD's issue port for 8 of its 16 cycles, a 32x32x16 one for
-// 8 of 32 (MI355X_MICROARCH.md constants), so with 32 columns per wave the fragment reads,
-// splits and epilogue of a wave have three quarters of the issue slots beside its MFMAs,
-// and each 1 KiB A fragment read from LDS feeds twice the columns.
-// Mapping: 4-wave blocks (one wave per SIMD, one block per CU), 128-column tiles, wave w
-// owns columns [32w, 32w + 32) for the whole network.  A layer's 32-unit accumulator tile
-// (lane: column lane & 31, half h = lane >> 5; register r: unit 8(r >> 2) + 4h + (r & 3))
-// is, after bias + relu + split, the B operand of the next layer's two 16-deep k-steps:
-// registers 8s .. 8s + 7 are k-step s, element j <-> unit 16s + 8(j >> 2) + 4h + (j & 3)
-// (the packed weights carry that k order).  A chunk is 32 deep as in dense_b3_kernel:
-// layer chunks hold fragments i = 2t + s (unit tile t, k-step s), output chunks one
-// 32-row tile (two 16-row output tiles, each of one variable) over every k-step.
-// ------------------------------------------------------------------------------------
-typedef float b3f16 __attribute__((ext_vector_type(16)));
-
-template <int NS>
-__device__ __forceinline__ void mma32(const bf16x8 (&a)[NS], const bf16x8 (&b)[NS], b3f16& c)
-{
-    using T = SplitTerms<NS>;
-#pragma unroll
-    for (int t = 0; t < T::n; ++t) c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[T::a[t]], b[T::b[t]], c, 0, 0, 0);
-}
-
-constexpr int kW32Waves = 4, kW32Threads = 256, kW32Cols = 128;
-constexpr int w32_in_bytes() { return 2 * kW32Waves * 2 * 8 * 64 * 4; }  // [2][wave][step][level][lane]
-
-template <int HT, int NS>
-__global__ __launch_bounds__(kW32Threads) __attribute__((amdgpu_waves_per_eu(1, 1))) void
-dense_b3w_kernel(B3Args pa)
-{
-    (void)pa;
-    KB3& p = *(KB3*)(__builtin_amdgcn_kernarg_segment_ptr());
-    constexpr int NWV = kW32Waves, NT = kW32Threads;
-    constexpr int HP = 32 * HT;         // padded units
-    constexpr int KS = 2 * HT;          // 16-deep k-steps over HP units
-    constexpr int NF = 2 * HT;          // fragments per chunk
-    constexpr int CB = 1024 * NS * NF;  // chunk bytes
-    constexpr int NST = CB / (16 * NT);
-    constexpr int NSL = 3;
-    static_assert(CB % (16 * NT) == 0, "a chunk is a whole number of block-wide 16-byte loads");
-    extern __shared__ __attribute__((aligned(16))) b3f4 lds3[];
-    char* ring = reinterpret_cast<char*>(lds3);
-    float* s_in = reinterpret_cast<float*>(ring + NSL * CB);
-    float* s_mean = reinterpret_cast<float*>(ring + NSL * CB + w32_in_bytes());
-    float* s_rs = s_mean + p.kp1;
-    float* s_bias = s_rs + p.kp1;             // [nh][HP]
-    float* s_oc = s_bias + (1 + p.nhx) * HP;  // [6][kop]
-    B3Grp* s_grp = reinterpret_cast<B3Grp*>(reinterpret_cast<char*>(s_mean) + 4 * ((p.nconst + 7) & ~7));
-    const int kop = p.kop;
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int h = lane >> 5;   // lane half: k offset 8h of a k-step, rows 4h (+ 8g) of a tile
-    const int cl = lane & 31;  // column of this lane inside the wave's 32
-
-    for (int i = tid; i < p.nconst; i += NT) s_mean[i] = p.consts[i];
-    for (int g = tid; g < 4 * p.n1; g += NT) {
-        const int m = p.gmeta[g], v = m & 15;
-        B3Grp e;
-        e.ptr = p.in[v].ptr + (int64_t)((m >> 4) & 0xfffff) * p.in[v].ld;
-        e.bs = p.in[v].bs;
-        e.ld = (int)p.in[v].ld;
-        e.nv = m >> 24;
-        e.leps = p.in[v].leps;
-        e.klog = 0;
-        for (int i = 4 * (g / 4); i < 4 * (g / 4) + 4; ++i)
-            e.klog |= (p.gmeta[i] >> 24) > 0 && p.in[p.gmeta[i] & 15].leps > 0.0f;
-        s_grp[g] = e;
-    }
-    b3_barrier();  // the group table is read by the first tile's input DMA below
-
-    const char* wsrc = reinterpret_cast<const char*>(p.wstream);
-    auto glds_w = [&](int j, int sl) {
-#pragma unroll
-        for (int q = 0; q < NST; ++q)
-            b3_glds<16>(wsrc + (size_t)j * CB + q * 16 * NT + tid * 16, ring + sl * CB + q * 16 * NT + wave * 1024);
-    };
-    int slot = 0;
-    int jn2 = p.nch > 2 ? 2 : 2 % p.nch;
-    glds_w(0, 0);
-    glds_w(p.nch > 1 ? 1 : 0, 1);
-
-    b3f16 acc[HT];
-    auto zero_acc = [&]() {
-#pragma unroll
-        for (int t = 0; t < HT; ++t)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
-    };
-    auto frag = [&](int sl, int i, bf16x8 (&f)[NS]) {
-        const char* a = ring + sl * CB + i * 1024 * NS + lane * 16;
-#pragma unroll
-        for (int s = 0; s < NS; ++s) f[s] = *reinterpret_cast<const bf16x8*>(a + s * 1024);
-    };
-    auto stage_next = [&]() { glds_w(jn2, slot == 0 ? NSL - 1 : slot - 1); };
-    auto advance = [&](int younger) {
-        vm_wait_le(NST + younger);
-        b3_barrier();
-        slot = slot == NSL - 1 ? 0 : slot + 1;
-        jn2 = jn2 + 1 == p.nch ? 0 : jn2 + 1;
-    };
-    // layer chunk: unit tile t accumulates its two k-steps (fragments 2t, 2t + 1) against
-    // the chunk's B fragments; fragments read kFR - 2 ahead
-    auto step_layer = [&](const bf16x8 (&b0)[NS], const bf16x8 (&b1)[NS], auto&& after_stage) {
-        stage_next();
-        const int younger = after_stage();
-        bf16x8 fa[kFR][NS];
-        sfor<kFR - 2>([&](auto ic) { frag(slot, decltype(ic)::value, fa[decltype(ic)::value]); });
-        sfor<HT>([&](auto tc) {
-            constexpr int t = decltype(tc)::value, i0 = 2 * t, i1 = i0 + 1;
-            if constexpr (i0 + kFR - 2 < NF) {
-                frag(slot, i0 + kFR - 2, fa[(i0 + kFR - 2) % kFR]);
-                frag(slot, i1 + kFR - 2, fa[(i1 + kFR - 2) % kFR]);
-            }
-            mma32<NS>(fa[i0 % kFR], b0, acc[t]);
-            mma32<NS>(fa[i1 % kFR], b1, acc[t]);
-        });
-        advance(younger);
-    };
-
-    // ---- layer-1 inputs: chunk c, k-step s, lane half h: group 4c + 2s + h (8 levels) ----
-    unsigned lblk = 0, lii = 0;
-    bool lvalid = false;
-    auto set_load_tile = [&](int64_t tile) {
-        const int64_t c = tile * kW32Cols + wave * 32 + cl;
-        lvalid = c < p.ncol;
-        const int64_t cc = lvalid ? c : 0;
-        const int64_t b = p.ncol_blk < p.ncol ? cc / p.ncol_blk : 0;
-        lblk = (unsigned)b;
-        lii = (unsigned)(cc - b * p.ncol_blk);
-    };
-    auto in_row = [&](int buf, int s, int j) { return s_in + (((buf * NWV + wave) * 2 + s) * 8 + j) * 64; };
-    auto glds_in = [&](int buf, int c) {  // 16 4-byte LDS-DMAs per lane
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const B3Grp& g = s_grp[4 * c + 2 * s + h];
-            const int ld = g.ld;
-            const int nv = lvalid ? g.nv : 0;
-            const float* ptr = g.ptr + (int64_t)lblk * g.bs + lii;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) b3_glds<4>(ptr + (j < nv ? j * ld : 0), in_row(buf, s, j));
-        }
-    };
-    auto stage_in = [&](int buf, int c, int s, bf16x8 (&bx)[NS]) {
-        const int g = 4 * c + 2 * s + h;
-        const int nv = lvalid ? s_grp[g].nv : 0;
-        float y[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float x = in_row(buf, s, j)[lane];
-            y[j] = j < nv ? x : 0.0f;
-        }
-        const int f0 = 8 * g;
-        const b3f4 mu0 = *reinterpret_cast<const b3f4*>(s_mean + f0);
-        const b3f4 mu1 = *reinterpret_cast<const b3f4*>(s_mean + f0 + 4);
-        const b3f4 rs0 = *reinterpret_cast<const b3f4*>(s_rs + f0);
-        const b3f4 rs1 = *reinterpret_cast<const b3f4*>(s_rs + f0 + 4);
-        if (p.any_log && __builtin_amdgcn_readfirstlane(s_grp[4 * c].klog)) {
-            const float leps = s_grp[g].leps;
-#pragma unroll
-            for (int j = 0; j < 8; ++j)  // LogTransform.forward (transforms.py:123-124)
-                if (leps > 0.0f) y[j] = b3_log(y[j], leps);
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) y[j] = (y[j] - (j < 4 ? mu0[j] : mu1[j - 4])) * (j < 4 ? rs0[j] : rs1[j - 4]);
-        splitN<NS>(y, bx);
-    };
-
-    // ---- activations: k-step 2t + s = registers 8s .. 8s + 7 of unit tile t ----
-    bf16x8 B[KS][NS];
-    auto hidden_epi = [&](int l) {
-        sfor<HT>([&](auto tc) {
-            constexpr int t = decltype(tc)::value;
-            float y[16];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const b3f4 bb = *reinterpret_cast<const b3f4*>(s_bias + l * HP + 32 * t + 8 * g + 4 * h);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float v = acc[t][4 * g + r] + bb[r];
-                    y[4 * g + r] = v > 0.0f ? v : 0.0f;
-                }
-            }
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                float ys[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) ys[j] = y[8 * s + j];
-                splitN<NS>(ys, B[2 * t + s]);
-            }
-        });
-    };
-    b3f16 acco;
-    auto step_out = [&]() {  // one 32-row tile over every k-step (fragment q = k-step q)
-        bf16x8 fa[kFR][NS];
-        sfor<kFR - 2>([&](auto ic) { frag(slot, decltype(ic)::value, fa[decltype(ic)::value]); });
-        sfor<KS>([&](auto qc) {
-            constexpr int q = decltype(qc)::value;
-            if constexpr (q + kFR - 2 < KS) frag(slot, q + kFR - 2, fa[(q + kFR - 2) % kFR]);
-            mma32<NS>(fa[q % kFR], B[q], acco);
-        });
-    };
-
-    // ---- output epilogue: register r of lane (h, cl) is row 8(r >> 2) + 4h + (r & 3) of
-    //      the 32-row tile: 16-row output tile 2 oc + (r >> 3), row 8((r >> 2) & 1) + 4h + (r & 3) ----
-    unsigned oblk = 0, oii = 0;
-    bool ovalid = false;
-    auto res_load = [&](int oc, float (&r)[16]) -> int {  // the loads issued
-        int n = 0;
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-            const int e = p.otile[2 * oc + st];
-            const int v = e & 0xff, z0 = (e >> 8) & 0xffff, nrow = e >> 24;
-            if (v < kMaxVars && p.res_ptr[v]) {  // uniform
-                const Rsrc3 rr_ = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.res_ptr[v]), 0, 0x7ffffffc,
-                                                                    0x00020000);
-                const unsigned rb = oblk * (unsigned)p.res_bs[v] + oii;
-                const unsigned rld = (unsigned)p.res_ld[v];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const int row = 8 * (k >> 2) + 4 * h + (k & 3);
-                    const unsigned off = (ovalid & (row < nrow)) ? (rb + (unsigned)(z0 + row) * rld) * 4u : 0x80000000u;
-                    r[8 * st + k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr_, (int)off, 0, 0));
-                }
-                n += 8;
-            } else {
-#pragma unroll
-                for (int k = 0; k < 8; ++k) r[8 * st + k] = 0.0f;
-            }
-        }
-        return n;
-    };
-    auto out_tile = [&](const b3f16& a, int oc, const float (&r)[16]) -> int {  // the stores issued
-        int n = 0;
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-            const int T = 2 * oc + st;
-            const int e = p.otile[T];
-            const int v = e & 0xff, z0 = (e >> 8) & 0xffff, nrow = e >> 24;
-            if (v >= kMaxVars) continue;  // padding tile (uniform)
-            const Rsrc3 ro = __builtin_amdgcn_make_buffer_rsrc(p.out_ptr[v], 0, 0x7ffffffc, 0x00020000);
-            const unsigned ob = oblk * (unsigned)p.out_bs[v] + oii;
-            const unsigned old_ = (unsigned)p.out_ld[v];
-            const bool has_res = p.res_ptr[v] != nullptr;  // uniform
-#pragma unroll
-            for (int g = 0; g < 2; ++g) {
-                int R0 = 16 * T + 8 * g + 4 * h;
-                asm volatile("" : "+v"(R0));  // keep the constant reads next to their use
-                const b3f4 bo = *reinterpret_cast<const b3f4*>(s_oc + R0);
-                const b3f4 sg = *reinterpret_cast<const b3f4*>(s_oc + kop + R0);
-                const b3f4 mu = *reinterpret_cast<const b3f4*>(s_oc + 2 * kop + R0);
-                const b3f4 lo = *reinterpret_cast<const b3f4*>(s_oc + 3 * kop + R0);
-                const b3f4 hi = *reinterpret_cast<const b3f4*>(s_oc + 4 * kop + R0);
-                const b3f4 mk = *reinterpret_cast<const b3f4*>(s_oc + 5 * kop + R0);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int k = 4 * g + q;
-                    const int row = 8 * g + 4 * h + q;
-                    float y = a[8 * st + k] + bo[q];
-                    y = y * sg[q];
-                    y = y + mu[q];
-                    if (y < lo[q]) y = lo[q];
-                    if (y >= hi[q]) y = hi[q];
-                    y = y * mk[q];
-                    if (has_res) y = r[8 * st + k] + y;
-                    const unsigned off = (ovalid & (row < nrow)) ? (ob + (unsigned)(z0 + row) * old_) * 4u : 0x80000000u;
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, (int)off, 0, 0);
-                }
-            }
-            n += 8;
-        }
-        return n;
-    };
-
-    int64_t tile = blockIdx.x;
-    set_load_tile(tile);
-    if (tile < p.ntiles) {
-        glds_in(0, 0);
-        if (p.n1 > 1) glds_in(1, 1);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    b3_barrier();  // constants and chunk 0 visible
-
-    for (; tile < p.ntiles; tile += gridDim.x) {
-        oblk = lblk;
-        oii = lii;
-        ovalid = lvalid;
-        // ---- layer 1 ----
-        zero_acc();
-        for (int c = 0; c < p.n1; ++c) {
-            bf16x8 x0[NS], x1[NS];
-            stage_in(c & 1, c, 0, x0);
-            stage_in(c & 1, c, 1, x1);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the reads above before the DMA refills the buffer
-            step_layer(x0, x1, [&]() {
-                if (c + 2 < p.n1) {
-                    glds_in(c & 1, c + 2);
-                    return 16;
-                }
-                return 0;
-            });
-        }
-        hidden_epi(0);
-        // ---- further hidden layers ----
-        for (int l = 0; l < p.nhx; ++l) {
-            zero_acc();
-            sfor<HT>([&](auto cc) {
-                constexpr int c = decltype(cc)::value;
-                step_layer(B[2 * c], B[2 * c + 1], [] { return 0; });
-            });
-            hidden_epi(l + 1);
-        }
-        // ---- output layer, one 32-row tile per chunk; the next tile's inputs start loading ----
-        const int64_t nt = tile + gridDim.x;
-        if (nt < p.ntiles) set_load_tile(nt);
-        b3f16 accP;
-        float resN[16], resP[16];
-        for (int oc = 0; oc < p.n_oc; ++oc) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acco[r] = 0.0f;
-            stage_next();
-            int younger = res_load(oc, resN);
-            if (nt < p.ntiles) {
-                // the next tile's input chunks 0 and 1: one per chunk over the last two
-                if (oc == (p.n_oc >= 2 ? p.n_oc - 2 : 0)) {
-                    glds_in(0, 0);
-                    younger += 16;
-                }
-                if (oc == p.n_oc - 1 && p.n1 > 1) {
-                    glds_in(1, 1);
-                    younger += 16;
-                }
-            }
-            step_out();
-            if (oc > 0) younger += out_tile(accP, oc - 1, resP);
-            advance(younger);
-            accP = acco;
-#pragma unroll
-            for (int q = 0; q < 16; ++q) resP[q] = resN[q];
-        }
-        out_tile(accP, p.n_oc - 1, resP);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's inputs landed
-    }
-}
-
 uint16_t bf16_rne(float f)
 {
     uint32_t u;
@@ -1354,14 +1005,11 @@ float bf16_f(uint16_t h)
 // ------------------------------------------------------------------------------------
 // host: pack the model once (fv3_dense_create) into the bf16x3 and bf16x6 chunk streams
 // ------------------------------------------------------------------------------------
-// W32: the stream of dense_b3w_kernel (v_mfma_f32_32x32x16_bf16 fragments, the same chunk
-// sizes and order, see the kernel)
-static int pack_ns(fv3_dense_model* m, const fv3_dense_desc* d, int NS, B3Pack** dst, bool W32 = false)
+static int pack_ns(fv3_dense_model* m, const fv3_dense_desc* d, int NS, B3Pack** dst)
 {
     auto b = new B3Pack();
     std::unique_ptr<B3Pack> guard(b);
     b->ns = NS;
-    b->w32 = W32;
     const int W = d->width;
     b->hu = W <= 64 ? 4 : (W <= 128 ? 8 : 16);
     b->hp = 16 * b->hu;
@@ -1443,26 +1091,21 @@ static int pack_ns(fv3_dense_model* m, const fv3_dense_desc* d, int NS, B3Pack**
         for (int t = 0; t < HU; ++t)
             for (int lane = 0; lane < 64; ++lane)
                 for (int j = 0; j < 8; ++j) {
-                    // W32: fragment t = unit tile t / 2, k-step t & 1, lane half lane >> 5
-                    const int f = W32 ? 32 * c + 16 * (t & 1) + 8 * (lane >> 5) + j : 32 * c + 8 * (lane >> 4) + j;
-                    const int unit = W32 ? 32 * (t >> 1) + (lane & 31) : 16 * t + (lane & 15);
+                    const int f = 32 * c + 8 * (lane >> 4) + j;
+                    const int unit = 16 * t + (lane & 15);
                     const int src = fsrc[f];
                     put(c, t, lane, j, (src >= 0 && unit < W) ? K0[(size_t)src * W + unit] : 0.0f);
                 }
     // hidden and output layers: k-step c, element j of lane quarter q contracts over the
     // previous layer's unit 32c + 16(j>>2) + 4q + (j&3) (its accumulator layout)
     auto in_unit = [](int c, int lane, int j) { return 32 * c + 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3); };
-    // W32: 16-deep k-step q over the previous layer's 32x32 accumulator tiles (element j of
-    // lane half h is unit 16q + 8(j >> 2) + 4h + (j & 3))
-    auto in_unit32 = [](int q, int lane, int j) { return 16 * q + 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3); };
     for (int li = 0; li < b->nhx; ++li) {
         const float* K = d->hidden_kernel[li + 1];
         for (int c = 0; c < KS; ++c)
             for (int t = 0; t < HU; ++t)
                 for (int lane = 0; lane < 64; ++lane)
                     for (int j = 0; j < 8; ++j) {
-                        const int in = W32 ? in_unit32(2 * c + (t & 1), lane, j) : in_unit(c, lane, j);
-                        const int unit = W32 ? 32 * (t >> 1) + (lane & 31) : 16 * t + (lane & 15);
+                        const int in = in_unit(c, lane, j), unit = 16 * t + (lane & 15);
                         put(b->n1 + li * KS + c, t, lane, j, (in < W && unit < W) ? K[(size_t)in * W + unit] : 0.0f);
                     }
     }
@@ -1472,8 +1115,8 @@ static int pack_ns(fv3_dense_model* m, const fv3_dense_desc* d, int NS, B3Pack**
             for (int lane = 0; lane < 64; ++lane)
                 for (int j = 0; j < 8; ++j) {
                     const int q = i >> 1, ts = i & 1;
-                    const int in = W32 ? in_unit32(i, lane, j) : in_unit(q, lane, j);
-                    const int R = W32 ? 32 * oc + (lane & 31) : 16 * (2 * oc + ts) + (lane & 15);
+                    const int in = in_unit(q, lane, j);
+                    const int R = 16 * (2 * oc + ts) + (lane & 15);
                     float v = 0.0f;
                     if (in < W && ocol_var[R] >= 0) {
                         const int ov = ocol_var[R], oz = ocol_z[R];
@@ -1586,13 +1229,6 @@ int b3_pack(fv3_dense_model* m, const fv3_dense_desc* d)
     if (st != FV3_OK) {
         m->b3 = nullptr;
         clear_error();
-    } else {
-        const int sw = pack_ns(m, d, 2, &m->b3w, true);
-        if (sw == FV3_ERR_HIP) return sw;
-        if (sw != FV3_OK) {
-            m->b3w = nullptr;
-            clear_error();
-        }
     }
     m->b6_src = copy_desc(m, d);
     return FV3_OK;
@@ -1620,7 +1256,7 @@ static int b6_stream(const fv3_dense_model* cm, const B3Pack** out)
 void b3_free(fv3_dense_model* m)
 {
     if (!m) return;
-    for (B3Pack** pk : {&m->b3, &m->b6, &m->b3w}) {
+    for (B3Pack** pk : {&m->b3, &m->b6}) {
         if (!*pk) continue;
         if ((*pk)->dbuf) (void)hipFree((*pk)->dbuf);
         delete *pk;
@@ -1718,30 +1354,6 @@ extern "C" int fv3_dense_forward_ex(const fv3_dense_model* m, const float* const
             int dev = 0;
             FV3_HIP(hipGetDevice(&dev));
             FV3_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-        }
-    }
-    // FV3_B3_SHAPE=32: the 32x32x16 kernel (bf16x3 only; A/B)
-    if (precision == FV3_DENSE_BF16X3 && m->b3w) {
-        const char* shp = fv3::variant_env("FV3_B3_SHAPE");
-        if (shp && atoi(shp) == 32) {
-            const B3Pack& w = *m->b3w;
-            a.wstream = w.dbuf;
-            a.consts = reinterpret_cast<const float*>((const char*)w.dbuf + w.consts_off);
-            a.ntiles = (ncol + kW32Cols - 1) / kW32Cols;
-            const size_t lds = (size_t)3 * 1024 * w.ns * w.hu + (size_t)w32_in_bytes() +
-                               (size_t)4 * ((w.nconst + 7) & ~7) + sizeof(B3Grp) * 4 * w.n1;
-            FV3_REQUIRE(lds <= 160 * 1024, "dense_forward_ex: model needs %zu bytes of LDS (32x32 kernel)", lds);
-            const void* kfn = w.hu == 4 ? (const void*)dense_b3w_kernel<2, 2>
-                            : w.hu == 8 ? (const void*)dense_b3w_kernel<4, 2>
-                                        : (const void*)dense_b3w_kernel<8, 2>;
-            int res = 0;
-            FV3_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&res, kfn, kW32Threads, lds));
-            int64_t grid = std::min<int64_t>(a.ntiles, (int64_t)std::max(1, res) * n_cu);
-            if (const char* e = fv3::variant_env("FV3_B3_GRID")) grid = std::min<int64_t>(a.ntiles, std::max(1, atoi(e)));
-            void* kargs[] = {&a};
-            FV3_HIP(hipLaunchKernel(kfn, dim3((unsigned)grid), dim3(kW32Threads), kargs, lds, (hipStream_t)stream));
-            FV3_LAUNCH_CHECK();
-            return FV3_OK;
         }
     }
     // 4-wave blocks of 64 columns where 128-column tiles would leave CUs idle (C48: 108

@@ -88,7 +88,6 @@ struct fv3_dense_model {
     fv3::DenseArgs tmpl{};  // device pointers filled, per-call fields empty
     fv3::B3Pack* b3 = nullptr;  // bf16x3 weight stream (2 bf16 parts per weight)
     fv3::B3Pack* b6 = nullptr;  // bf16x6 weight stream (3 parts), packed on the first bf16x6 forward
-    fv3::B3Pack* b3w = nullptr;  // bf16x3 stream of the 32x32x16 kernel (dense_b3w_kernel)
     fv3::B3Desc* b6_src = nullptr;  // what b6 is packed from (released once packed)
 };
 

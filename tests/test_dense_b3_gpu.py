@@ -1,6 +1,5 @@
 """GPU parity of the bf16 split fused dense kernel (csrc/dense_b3.hip: each f32 operand split
-into bf16 hi + lo, products hi*hi + lo*hi + hi*lo on v_mfma_f32_16x16x32_bf16, or on
-v_mfma_f32_32x32x16_bf16 in dense_b3w_kernel) against
+into bf16 hi + lo, products hi*hi + lo*hi + hi*lo on v_mfma_f32_16x16x32_bf16) against
 the float64 evaluation of the reference graph (oracle/dense.py; reference
 external/fv3fit/fv3fit/keras/_models/dense.py:234-305).
 
@@ -41,24 +40,21 @@ def _check(gpu_out, ref64, rtol=None):
         assert_per_level(g, r, rtol, f"output {o}")
 
 
-@pytest.fixture(autouse=True, params=[("glds", None, None, None), ("glds", "8", None, None), ("glds", "4", None, None),
-                                      ("glds", None, "0", None), ("reg", None, None, None), ("glds", None, None, "32")],
-                ids=["glds", "glds-w8", "glds-w4", "glds-rows", "reg", "mfma32"])
+@pytest.fixture(autouse=True, params=[("glds", None, None), ("glds", "8", None), ("glds", "4", None),
+                                      ("glds", None, "0"), ("reg", None, None)],
+                ids=["glds", "glds-w8", "glds-w4", "glds-rows", "reg"])
 def b3_stage(request, monkeypatch):
     """Every test on both staging pipelines of the kernel (FV3_B3_STAGE): LDS-DMA (the
     default) and register staging; the LDS-DMA one also with the block shape forced
     (FV3_B3_WAVES: 8-wave blocks of 128 columns, 4-wave blocks of 64, which the host picks
     for grids with fewer 128-column tiles than CUs) and with the row-per-lane output layer
-    instead of the transposed one (FV3_B3_TR=0); and on the 32x32x16 kernel
-    (FV3_B3_SHAPE=32, dense_b3w_kernel: bf16x3 only, the bf16x6 runs keep the default)."""
-    stage, waves, tr, shape = request.param
+    instead of the transposed one (FV3_B3_TR=0)."""
+    stage, waves, tr = request.param
     set_variant(monkeypatch, "FV3_B3_STAGE", stage)
     if waves:
         set_variant(monkeypatch, "FV3_B3_WAVES", waves)
     if tr:
         set_variant(monkeypatch, "FV3_B3_TR", tr)
-    if shape:
-        set_variant(monkeypatch, "FV3_B3_SHAPE", shape)
     return request.param
 
 

@@ -207,26 +207,6 @@ def test_emulator_split_kernel_variants_agree(gpu, monkeypatch, precision, rtol)
 
 
 @pytest.mark.gpu
-def test_emulator_mfma32_kernel(gpu, monkeypatch):
-    """The bf16x3 emulator on the 32x32x16 kernel (FV3_B3_SHAPE=32, dense_b3w_kernel): a
-    ragged grid (2,085 columns) on its default grid and forced to 4 persistent blocks
-    (every block walks >= 4 tiles of 128, so the cross-tile input DMA, the residual reads
-    and the weight ring wrap around) agree bit for bit, within the oracle bound."""
-    import torch
-
-    emu, raw = _emulator(ncol=2085, seed=11, precision="bf16x3")
-    state = {k: torch.from_numpy(np.ascontiguousarray(v.T)).cuda() for k, v in raw.items()}
-    set_variant(monkeypatch, "FV3_B3_SHAPE", "32")
-    base = emu(state)
-    set_variant(monkeypatch, "FV3_B3_GRID", "4")
-    forced = emu(state)
-    torch.cuda.synchronize()
-    for k in base:
-        assert torch.equal(base[k], forced[k]), k
-    _check_columns(forced, state, emu, np.arange(2085), 1e-4)
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("precision,rtol,env", [("bf16x3", 1e-4, "FV3_B3_GRID"), ("bf16x6", 1e-5, "FV3_B3_GRID"),
                                                 ("f32", 1e-5, "FV3_DENSE_GRID")])
 def test_emulator_forced_multi_tile_blocks(gpu, precision, rtol, env, monkeypatch):

@@ -1,7 +1,8 @@
 """The bf16x3 split kernel on 16x16x32 MFMAs (dense_b3_kernel, the default) against the
 32x32x16 kernel (dense_b3w_kernel, FV3_B3_SHAPE=32): output agreement and mean launch
 time, interleaved on one box (config #5 emulator at C384, the 2x256 DenseModel at C384 and
-C96)."""
+C96).  The 32x32x16 kernel was built in commit d385025 and removed after this A/B
+(profiles/r05zc_b3_mfma32_ab.log); run it against that tree."""
 import os
 import sys
 import time
