@@ -101,7 +101,7 @@ struct B3Pack {
     void* dbuf = nullptr;
     int ns = 2;  // bf16 parts per weight (2: bf16x3, 3: bf16x6)
     int hu = 0, hp = 0, kp1 = 0, n1 = 0, nhx = 0, n_oc = 0, kop = 0, nch = 0;
-    int nconst = 0, wbytes = 0, any_log = 0;
+    int nconst = 0, wbytes = 0, any_log = 0;  // any_log: 1 every epsilon normal (fast log), 2 some not
     std::vector<int> gmeta;  // per 8-feature group: var | zstart << 4 | nvalid << 24
     std::vector<int> otile;  // per 16-row output tile: var | z0 << 8 | nrow << 24 (var 255: padding)
     size_t consts_off = 0;
@@ -188,7 +188,17 @@ __device__ __forceinline__ void b3_barrier()
 __device__ __forceinline__ void b3_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 #endif
 
-__device__ __forceinline__ float b3_log(float x, float eps) { return x != x ? x : logf(x > eps ? x : eps); }
+// LogTransform.forward: log(max(x, eps)).  fast (every LogTransform epsilon of the model
+// normal, the host's any_log == 1): v_log_f32 (log2, ~1 ulp) times ln 2, 4 instructions a
+// value instead of the library's logf (denormal scaling and an extended-precision product,
+// ~14): about 1e-7 rel of the log, far inside the split's own rounding (bf16x3 ~1e-5,
+// bf16x6 ~6e-8 per operand, both held to their per-level bounds by the tests); emulator
+// C384 2.41-2.42 -> 2.38 ms (profiles/r05ze_b3_fastlog_ab.log).  Otherwise logf.
+__device__ __forceinline__ float b3_log(float x, float eps, bool fast)
+{
+    const float v = x > eps ? x : eps;
+    return x != x ? x : (fast ? __builtin_amdgcn_logf(v) * 0.6931471805599453f : logf(v));
+}
 
 // y -> NS bf16 parts: part 0 = rne(y), part s = rne(y - parts 0..s-1) (every residual is
 // exact in f32).  NS = 2: hi + lo (~16 mantissa bits); NS = 3: hi + mid + lo (~24 bits).
@@ -596,7 +606,7 @@ dense_b3_kernel(B3Args pa)
             const float leps = s_grp[4 * c + hq].leps;
 #pragma unroll
             for (int j = 0; j < 8; ++j)  // LogTransform.forward (transforms.py:123-124)
-                if (leps > 0.0f) y[j] = b3_log(y[j], leps);
+                if (leps > 0.0f) y[j] = b3_log(y[j], leps, p.any_log == 1);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) y[j] = (y[j] - (j < 4 ? mu0[j] : mu1[j - 4])) * (j < 4 ? rs0[j] : rs1[j - 4]);
@@ -1026,7 +1036,7 @@ static int pack_ns(fv3_dense_model* m, const fv3_dense_desc* d, int NS, B3Pack**
             b->gmeta.push_back(v | ((z0 + g0) << 4) | (nv << 24));
             for (int j = 0; j < 8; ++j) fsrc.push_back(j < nv ? kbase + g0 + j : -1);
         }
-        b->any_log |= m->in_log_eps[v] > 0.0f;
+        if (m->in_log_eps[v] > 0.0f) b->any_log = std::max(b->any_log, m->in_log_eps[v] >= 0x1p-126f ? 1 : 2);
         kbase += nkeep;
     }
     while (b->gmeta.size() % 4) {

@@ -144,6 +144,26 @@ def test_deep_wide_model_falls_back_to_register_staging(gpu):
     _check(got, dense_predict(xs, m.oracle_params(), np.float64), rtol=1e-3)
 
 
+@pytest.mark.parametrize("eps", [1e-8, 1e-40], ids=["normal-eps", "denormal-eps"])
+def test_log_transform_inputs(gpu, eps):
+    """LogTransform inputs (log(max(x, eps)), transforms.py:123-126): a normal epsilon runs
+    the kernel's v_log_f32 path, a denormal one (the library's logf, which scales denormal
+    operands) the exact one; zeros in the input take the epsilon's log."""
+    import torch
+
+    rng = np.random.default_rng(21)
+    n = 611
+    x1 = (rng.uniform(0.0, 0.02, (n, 24)) * (rng.uniform(size=(n, 24)) > 0.2)).astype(np.float32)
+    x2 = rng.normal(5, 1, (n, 9)).astype(np.float32)
+    lx1 = np.log(np.maximum(x1, np.float32(eps)).astype(np.float64)).astype(np.float32)
+    m = _model(dict(input_variables=["q", "b"], output_variables=["y1", "y2"], in_nz=[24, 9],
+                    out_nz=[24, 3], width=64, depth=2, input_log_eps={"q": eps}), samples=[lx1, x2])
+    outs = m.forward([torch.from_numpy(x1.T.copy()).cuda(), torch.from_numpy(x2.T.copy()).cuda()])
+    got = [o.cpu().numpy().T for o in outs]
+    _check(got, dense_predict([np.log(np.maximum(x1, np.float32(eps)).astype(np.float64)), x2],
+                              m.oracle_params(), np.float64))
+
+
 def test_clip_limits_mask_and_scalar_input(gpu):
     import torch
 
