@@ -609,6 +609,14 @@ __global__ __launch_bounds__(128) void mappm_ppm_pair_split_kernel(MappmPairArgs
     const int km = a.km, kn = a.kn;
     const int kB = kn / 2 + 1;
     int ok = 0, cnt = 0;
+#ifdef FV3_MAPPM_SPLIT_NOSCAN  // experiment only (valid for sorted edges): no scans, L0 by search
+    (void)s_ok;
+    (void)s_cnt;
+    ok = kn >= 2;
+    if (part == 1 && ok) cnt = split_count_sorted(d, km, d.pe2(kB));
+    const bool both = ok;
+    const int cnt0 = cnt;
+#else
     if (kn >= 2) {
         if (part == 0)
             split_scan_pe1(d, km, d.pe2(kB), ok, cnt);
@@ -620,6 +628,7 @@ __global__ __launch_bounds__(128) void mappm_ppm_pair_split_kernel(MappmPairArgs
     __syncthreads();
     const bool both = s_ok[0][lane] && s_ok[1][lane];
     const int cnt0 = s_cnt[lane];
+#endif
     if (!valid) return;
     // this lane's outputs [kf, kl] and first input layer (one call site for every lane)
     int kf = 1, kl = kn, Lf = 1;

@@ -268,6 +268,21 @@ FV3_HD inline int split_scan_pe2(Col& c, int kn)
     return ok;
 }
 
+// #{L in 1..km : pe1(L + 1) < t} for non-decreasing pe1 in two rounds of loads: every 8th
+// edge, then the 8 edges of the block where the count stops (split_scan_pe1's count when
+// pe1 is sorted)
+template <class Col>
+FV3_HD inline int split_count_sorted(Col& c, int km, float t)
+{
+    int c1 = 0;  // sampled edges j = 2 + 8m below t
+    for (int m = 0; 2 + 8 * m <= km + 1; ++m) c1 += c.pe1(2 + 8 * m) < t;
+    if (c1 == 0) return 0;
+    const int j0 = 2 + 8 * (c1 - 1);
+    int n = 0;
+    for (int i = 0; i < 8; ++i) n += (j0 + i <= km + 1) && c.pe1(j0 + i <= km + 1 ? j0 + i : km + 1) < t;
+    return j0 - 2 + n;
+}
+
 // the second lane's first input layer from the pe1 count (pe2(kB) outside (pe1(1),
 // pe1(km + 1)): the boundary outputs, emitted from layer 1 on as the single pass does)
 template <class Col>
