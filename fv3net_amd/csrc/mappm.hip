@@ -582,17 +582,19 @@ __global__ __launch_bounds__(256) void mappm_ppm_pair_kernel(MappmPairArgs a)
 // (mappm_multi.h, "two lanes per column").  A block is two waves over the same 64
 // columns, wave 0 the first halves and wave 1 the second, so every lane of a wave is in
 // the same phase of its column (neighbouring columns' remap events mostly coincide; with
-// the halves mixed in one wave they diverge at every level).  The scans that prove the
-// split exact are shared through LDS (pe1 on wave 0, pe2 on wave 1); a column that fails
-// them runs the single pass on its first-half lane.
+// the halves mixed in one wave they diverge at every level).  The second lane finds its
+// start layer in two rounds of loads; both lanes check the sortedness that start layer
+// relies on on the edges they stream, and after the block barrier the first lane re-runs
+// the single pass on any column the checks did not prove (unsorted or NaN edges).  The
+// host runs this kernel for kn >= 2 only.
 __global__ __launch_bounds__(128) void mappm_ppm_pair_split_kernel(MappmPairArgs a)
 {
-    __shared__ int s_ok[2][64], s_cnt[64];
+    __shared__ int s_ok[64], s_l0[64];
     const int lane = threadIdx.x & 63;
     const int part = threadIdx.x >> 6;
     const int64_t c0 = (int64_t)blockIdx.x * 64 + lane;
     const bool valid = c0 < a.ncol;
-    const int64_t c = valid ? c0 : a.ncol - 1;  // spare lanes scan the last column, then leave
+    const int64_t c = valid ? c0 : a.ncol - 1;  // spare lanes only pass the barrier
     DevColPair d;
     d.pe1_ = a.pe1 + col_offset(a.l_pe1, c);
     d.pe2_ = a.pe2 + col_offset(a.l_pe2, c);
@@ -608,54 +610,48 @@ __global__ __launch_bounds__(128) void mappm_ppm_pair_split_kernel(MappmPairArgs
     d.kn = a.kn;
     const int km = a.km, kn = a.kn;
     const int kB = kn / 2 + 1;
-    int ok = 0, cnt = 0;
-#ifdef FV3_MAPPM_SPLIT_NOSCAN  // experiment only (valid for sorted edges): no scans, L0 by search
-    (void)s_ok;
-    (void)s_cnt;
-    ok = kn >= 2;
-    if (part == 1 && ok) cnt = split_count_sorted(d, km, d.pe2(kB));
-    const bool both = ok;
-    const int cnt0 = cnt;
-#else
-    if (kn >= 2) {
-        if (part == 0)
-            split_scan_pe1(d, km, d.pe2(kB), ok, cnt);
-        else
-            ok = split_scan_pe2(d, kn);
-    }
-    s_ok[part][lane] = ok;
-    if (part == 0) s_cnt[lane] = cnt;
-    __syncthreads();
-    const bool both = s_ok[0][lane] && s_ok[1][lane];
-    const int cnt0 = s_cnt[lane];
-#endif
-    if (!valid) return;
     // this lane's outputs [kf, kl] and first input layer (one call site for every lane)
-    int kf = 1, kl = kn, Lf = 1;
-    if (both) {
-        if (part == 0) {
-            kl = kB - 1;
-        } else {
-            kf = kB;
-            Lf = split_first_layer(d, km, d.pe2(kB), cnt0);
-        }
-    } else if (part == 1) {
-        return;  // unsorted or NaN edges, or one output layer: the single pass on the first lane
+    int kf = 1, kl = kB - 1, Lf = 1;
+    if (part == 1) {
+        kf = kB;
+        kl = kn;
+        const float t = d.pe2(kB);
+        Lf = split_first_layer(d, km, t, split_count_sorted(d, km, t));
     }
-    // the output pointers and the edge cursor where the single pass has them once
-    // output kf - 1 is written
-    for (int f = 0; f < 2; ++f) d.q2_[f] += (int64_t)(kf - 1) * d.ld_q2[f];
-    d.pe2_next = d.pe2_ + (int64_t)(kf + 1) * d.ld_pe2;
-    d.nb = (kf + 2 <= kn + 1) ? *d.pe2_next : 0.0f;
-    mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0, true>(d, km, kn, a.iv, a.kord, kf, kl, Lf);
+    SplitCheck chk{1, km};
+    if (valid) {
+        // the output pointers and the edge cursor where the single pass has them once
+        // output kf - 1 is written
+        float* q2c[2] = {d.q2_[0], d.q2_[1]};
+        for (int f = 0; f < 2; ++f) d.q2_[f] += (int64_t)(kf - 1) * d.ld_q2[f];
+        d.pe2_next = d.pe2_ + (int64_t)(kf + 1) * d.ld_pe2;
+        d.nb = (kf + 2 <= kn + 1) ? *d.pe2_next : 0.0f;
+        mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0, true>(d, km, kn, a.iv, a.kord, kf, kl, Lf, &chk);
+        for (int f = 0; f < 2; ++f) d.q2_[f] = q2c[f];
+    }
+    if (part == 1) {
+        s_ok[lane] = chk.mono;
+        s_l0[lane] = Lf;
+    }
+    __syncthreads();
+    if (part == 0 && valid && !split_exact(chk, SplitCheck{s_ok[lane], km}, s_l0[lane], km)) {
+        // the fix-up: this column's single pass, over what the halves wrote
+        d.pe2_next = d.pe2_ + 2 * d.ld_pe2;
+        d.nb = kn >= 2 ? *d.pe2_next : 0.0f;
+        mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0>(d, km, kn, a.iv, a.kord);
+    }
 }
 
-// Where the two-lane kernel pays (tools/mappm_split_time.py, profiles/r05r_mappm_split.log,
-// one box, interleaved; one lane per column vs two): 65,536 columns 142.7 vs 115.4 us,
-// 110,592 (one rank's C384 band at world 8) 165.7 vs 161.5 us, 147,456 213 vs 228 us,
-// C384 0.78 vs 1.06 ms.  Above the level-parallel kernel's range and below 131,072
-// columns it runs by default; FV3_MAPPM_SPLIT=0|1 forces it off / on (A/B, tests).
-constexpr int64_t kSplitMaxCols = 131072;
+// Where the two-lane kernel pays (tools/mappm_split_time.py, one box, interleaved; one
+// lane per column vs two).  With whole-column sortedness scans up front
+// (profiles/r05r_mappm_split.log): 65,536 columns 142.7 vs 115.4 us, 110,592 (one rank's
+// C384 band at world 8) 165.7 vs 161.5 us, 147,456 213 vs 228 us, C384 0.78 vs 1.06 ms.
+// With the start layer searched and the checks on the streamed edges
+// (profiles/r05zi_mappm_split.log): 65,536 columns 142.7 vs 99 us, 110,592 165.8 vs
+// 142 us, 147,456 215 vs 215 us, 221,184 262 vs 280 us, C384 0.78 vs 0.93 ms.  Above the
+// level-parallel kernel's range and below kSplitMaxCols columns it runs by default;
+// FV3_MAPPM_SPLIT=0|1 forces it off / on (A/B, tests).
+constexpr int64_t kSplitMaxCols = 147456;
 
 bool use_split_kernel(int64_t ncol)
 {
@@ -725,7 +721,7 @@ extern "C" int fv3_mappm_multi(const float* pe1, fv3_layout pe1_l, const float* 
             fv3::MappmPairArgs a{pe1, pe2, pe1_l, pe2_l, {q1[f], q1[f + 1]}, {q2[f], q2[f + 1]},
                                  {q1_l[f], q1_l[f + 1]}, {q2_l[f], q2_l[f + 1]}, ncol, km, kn, iv, kord};
             const int block = 256;
-            if (fv3::use_split_kernel(ncol)) {  // two lanes per column: 128 threads per 64 columns
+            if (kn >= 2 && fv3::use_split_kernel(ncol)) {  // two lanes per column: 128 threads per 64 columns
                 const int64_t grid = (ncol + 63) / 64;
                 hipLaunchKernelGGL(fv3::mappm_ppm_pair_split_kernel, dim3((unsigned)grid), dim3(128), 0, s, a);
             } else {

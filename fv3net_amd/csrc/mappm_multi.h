@@ -239,38 +239,21 @@ FV3_HD inline void remap_finish_n(RemapStateN<NF>& s, const ColumnEndsN<NF>& e, 
 // begins output kB.  With non-decreasing pe1 and pe2 that is the first L with
 // pe2(kB) <= pe1(L + 1) (pe1(1) < pe2(kB) < pe1(km + 1); an output's top edge lies in the
 // layer where the previous output ended, and no earlier layer reaches it), i.e.
-// L0 = 1 + #{L : pe1(L + 1) < pe2(kB)}.  The scan is split so each lane does one half:
-// split_scan_pe1 (non-decreasing pe1, the count), split_scan_pe2 (non-decreasing pe2);
-// a column failing either (or holding NaNs) runs the single pass on one lane.
-template <class Col>
-FV3_HD inline void split_scan_pe1(Col& c, int km, float t, int& ok, int& cnt)
-{
-    float prev = c.pe1(1);
-    ok = 1;
-    cnt = 0;
-    for (int k = 2; k <= km + 1; ++k) {
-        const float v = c.pe1(k);
-        ok &= prev <= v;
-        cnt += v < t;
-        prev = v;
-    }
-}
-template <class Col>
-FV3_HD inline int split_scan_pe2(Col& c, int kn)
-{
-    float prev = c.pe2(1);
-    int ok = 1;
-    for (int k = 2; k <= kn + 1; ++k) {
-        const float v = c.pe2(k);
-        ok &= prev <= v;
-        prev = v;
-    }
-    return ok;
-}
+// L0 = 1 + #{L : pe1(L + 1) < pe2(kB)}, found by split_count_sorted in two rounds of
+// loads.  Whether pe1 and pe2 are in fact non-decreasing is checked on the values the
+// lanes stream anyway (SplitCheck, in mappm_ppm_columns): the first lane's pe1 pairs run
+// from the top to its last window, the second lane's from its start window to the bottom
+// (a tail it did not stream is read at its exit), and the two ranges must meet; every
+// output edge pair is checked by the lane that consumes it.  A column that fails (or
+// holds NaNs) is run again by the single pass (the kernel's fix-up).
+struct SplitCheck {
+    int mono;    // every pe1 / pe2 pair this lane checked is non-decreasing (NaN: 0)
+    int l_exit;  // the input layer after which the lane stopped (km: it ran to the end)
+};
 
 // #{L in 1..km : pe1(L + 1) < t} for non-decreasing pe1 in two rounds of loads: every 8th
-// edge, then the 8 edges of the block where the count stops (split_scan_pe1's count when
-// pe1 is sorted)
+// edge, then the 8 edges of the block where the count stops (any value in 0..km for
+// unsorted pe1, which the checks then reject)
 template <class Col>
 FV3_HD inline int split_count_sorted(Col& c, int km, float t)
 {
@@ -283,6 +266,34 @@ FV3_HD inline int split_count_sorted(Col& c, int km, float t)
     return j0 - 2 + n;
 }
 
+// the split's two ranges of checked pe1 pairs meet: the first lane (from layer 1) checked
+// the pairs (j, j + 1) for j <= l_exit + 3, the second (its window built at L0, when
+// 4 <= L0 <= km - 3; else it walked from layer 1 itself) those from j = L0 - 3
+FV3_HD inline bool split_exact(const SplitCheck& a, const SplitCheck& b, int L0, int km)
+{
+    return a.mono && b.mono && (L0 < 4 || L0 > km - 3 || a.l_exit + 7 >= L0);
+}
+
+// SPLIT: the remap consumer's view of the column with every output edge it takes checked
+// against the one before (the split's pe2 sortedness, on the edges it streams)
+template <class Col>
+struct EdgeCheckOut {
+    Col& c;
+    int kn;
+    float last;
+    int& mono;
+    FV3_HD void emit(int f, int k, float v) { c.emit(f, k, v); }
+    FV3_HD float next_edge(int k)
+    {
+        const float r = c.next_edge(k);
+        if (k + 1 <= kn + 1) {
+            mono &= last <= r;
+            last = r;
+        }
+        return r;
+    }
+};
+
 // the second lane's first input layer from the pe1 count (pe2(kB) outside (pe1(1),
 // pe1(km + 1)): the boundary outputs, emitted from layer 1 on as the single pass does)
 template <class Col>
@@ -294,7 +305,8 @@ FV3_HD inline int split_first_layer(Col& c, int km, float t, int cnt)
 // ---- NF columns on one pressure column, kord <= 7, fully streaming ----
 // CARRY: as mappm_ppm_column's (level L + 4's loads one iteration ahead, carried across
 // the back edge, or at the iteration's start); same loads, same bits.
-// SPLIT: this lane emits outputs k_first .. k_last only (a column on two lanes, above).
+// SPLIT: this lane emits outputs k_first .. k_last only (a column on two lanes, above),
+// and records in *chk whether the pe1 / pe2 pairs it streams are non-decreasing.
 // k_first > 1 starts the remap fresh at output k_first: from input layer L_first with
 // the window E_{L_first} built directly from its local stencil (every entry the same
 // expression on the same operands as the streaming advance computes it) when
@@ -302,8 +314,9 @@ FV3_HD inline int split_first_layer(Col& c, int km, float t, int cnt)
 // pass without a remap event).  A lane stops once it has emitted k_last.
 template <int NF, class Col, bool CARRY = false, bool SPLIT = false>
 FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord, int k_first = 1, int k_last = 0,
-                                     int L_first = 1)
+                                     int L_first = 1, SplitCheck* chk = nullptr)
 {
+    int mono = 1;  // SPLIT: the pairs checked so far are non-decreasing
     // window state E_L as in mappm_ppm_column, the q-dependent parts per field
     float qv[NF][4], dcv[NF][3], alv[NF][3], h2v[NF][3], ar_km[NF];
     float dpv[4], pev[5];
@@ -325,6 +338,7 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord, i
         float pw[8], dw[7];
         for (int i = 0; i < 8; ++i) pw[i] = c.pe1(l0 + i);
         for (int i = 0; i < 7; ++i) dw[i] = pw[i + 1] - pw[i];
+        for (int i = 0; i < 7; ++i) mono &= pw[i] <= pw[i + 1];
         DcShared pd[6];
         for (int i = 1; i <= 5; ++i) pd[i] = ppm_dc_shared(dw[i - 1], dw[i], dw[i + 1]);  // dc(L0-2 .. L0+2)
         AlShared pa[6];
@@ -357,6 +371,8 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord, i
         for (int i = 0; i < 4; ++i) qv[f][i] = c.q1(f, 1 + i);
     for (int i = 0; i < 5; ++i) pev[i] = c.pe1(1 + i);
     for (int i = 0; i < 4; ++i) dpv[i] = pev[i + 1] - pev[i];
+    if constexpr (SPLIT)
+        for (int i = 0; i < 4; ++i) mono &= pev[i] <= pev[i + 1];
 
     ends.pe_top = pev[0];
     for (int f = 0; f < NF; ++f) ends.q_top[f] = qv[f][0];
@@ -393,6 +409,8 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord, i
     s.dpsum = 0.0f;
     s.t = c.pe2(s.k);
     s.b = c.pe2(s.k + 1);
+    if constexpr (SPLIT) mono &= s.t <= s.b;
+    EdgeCheckOut<Col> eo{c, kn, s.b, mono};
     s.xt = 0.0f;
     s.xv = false;
     for (int f = 0; f < NF; ++f) s.qsum[f] = 0.0f;
@@ -439,12 +457,27 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord, i
             v.ar[f] = a.ar;
             v.a6[f] = a.a6;
         }
-        remap_layer_n<NF>(s, v, ends, kn_out, c);
+        if constexpr (SPLIT)
+            remap_layer_n<NF>(s, v, ends, kn_out, eo);
+        else
+            remap_layer_n<NF>(s, v, ends, kn_out, c);
         layer_hook(c, 0);
 
         if (L == km) break;
         if constexpr (SPLIT) {
-            if (s.k > kn_out) return;  // this lane's outputs are done
+            if (s.k > kn_out) {  // this lane's outputs are done
+                if (k_last == kn) {  // the column's last lane: the pe1 pairs below its window
+                    float prev = pev[4];
+                    for (int jj = L + 5; jj <= km + 1; ++jj) {
+                        const float x = c.pe1(jj);
+                        mono &= prev <= x;
+                        prev = x;
+                    }
+                }
+                chk->mono = mono;
+                chk->l_exit = L;
+                return;
+            }
         }
         // ---- advance the window E_L -> E_{L+1} ----
         const int j = L + 4;
@@ -454,6 +487,7 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord, i
             for (int f = 0; f < NF; ++f) qn[f] = q_pf[f];
             pen = pe_pf;
             dpn = pen - pev[4];
+            if constexpr (SPLIT) mono &= pev[4] <= pen;
         }
         if constexpr (CARRY) {
             if (j + 1 <= km) {  // level j + 1, for the next iteration
@@ -501,7 +535,13 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord, i
         dpv[0] = dpv[1]; dpv[1] = dpv[2]; dpv[2] = dpv[3]; dpv[3] = dpn;
         pev[0] = pev[1]; pev[1] = pev[2]; pev[2] = pev[3]; pev[3] = pev[4]; pev[4] = pen;
     }
-    remap_finish_n<NF>(s, ends, kn_out, c);
+    if constexpr (SPLIT) {
+        remap_finish_n<NF>(s, ends, kn_out, eo);
+        chk->mono = mono;
+        chk->l_exit = km;
+    } else {
+        remap_finish_n<NF>(s, ends, kn_out, c);
+    }
 }
 
 // A one-field view of an NF-interface column, so NF = 1 runs the single-field

@@ -171,25 +171,26 @@ extern "C" int host_mappm_multi(int nf, int km, const float* pe1, const float* q
 }
 
 // a column on two lanes (mappm_ppm_columns<NF, .., SPLIT>, the small-grid pair kernel):
-// the two halves one after the other, with the kernel's scans and start layer; kb = 0:
-// the kernel's split point kn / 2 + 1; walk = 1: the second half always from layer 1
+// the two halves one after the other, with the kernel's start-layer search, streamed
+// sortedness checks and single-pass fix-up; kb = 0: the kernel's split point kn / 2 + 1;
+// walk = 1: the second half always from layer 1
 template <int NF>
 static void run_split(int km, const float* pe1, const float* q1, int kn, const float* pe2, float* q2, int64_t ncol,
                       int iv, int kord, int kb, int walk)
 {
     for (int64_t i = 0; i < ncol; ++i) {
         ColN c{pe1, q1, pe2, q2, ncol, i, km, kn};
-        const int kB = kb > 0 ? kb : kn / 2 + 1;
-        int ok1 = 0, cnt = 0;
-        if (kn >= 2) fv3::split_scan_pe1(c, km, c.pe2(kB), ok1, cnt);
-        const int ok2 = kn >= 2 ? fv3::split_scan_pe2(c, kn) : 0;
-        if (!(ok1 && ok2) || kn < 2) {
+        if (kn < 2) {  // the host runs the single-lane kernel
             fv3::mappm_ppm_columns<NF, ColN, true>(c, km, kn, iv, kord);
             continue;
         }
-        fv3::mappm_ppm_columns<NF, ColN, true, true>(c, km, kn, iv, kord, 1, kB - 1, 1);
-        const int L0 = walk ? 1 : fv3::split_first_layer(c, km, c.pe2(kB), cnt);
-        fv3::mappm_ppm_columns<NF, ColN, true, true>(c, km, kn, iv, kord, kB, kn, L0);
+        const int kB = kb > 0 ? kb : kn / 2 + 1;
+        const float t = c.pe2(kB);
+        const int L0 = walk ? 1 : fv3::split_first_layer(c, km, t, fv3::split_count_sorted(c, km, t));
+        fv3::SplitCheck a{1, km}, b{1, km};
+        fv3::mappm_ppm_columns<NF, ColN, true, true>(c, km, kn, iv, kord, 1, kB - 1, 1, &a);
+        fv3::mappm_ppm_columns<NF, ColN, true, true>(c, km, kn, iv, kord, kB, kn, L0, &b);
+        if (!fv3::split_exact(a, b, L0, km)) fv3::mappm_ppm_columns<NF, ColN, true>(c, km, kn, iv, kord);
     }
 }
 extern "C" int host_mappm_split(int nf, int km, const float* pe1, const float* q1, int kn, const float* pe2,

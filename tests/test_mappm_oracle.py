@@ -328,7 +328,8 @@ def test_two_lane_column_split_bit_identical(host_lib, nf, km, kn):
     built from the local stencil (or, walk = 1 / out of the direct range, from layer 1).
     Every split point, both start modes, every PPM kord and iv, on columns with
     zero-thickness layers, shared edges, edges beyond both ends, unsorted and NaN edges
-    (which keep the single pass): the single pass's bits."""
+    anywhere (which the streamed checks send back to the single pass): the single pass's
+    bits."""
     fn = host_lib.host_mappm_split
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
@@ -355,6 +356,17 @@ def test_two_lane_column_split_bit_identical(host_lib, nf, km, kn):
             pe2[:, 10:13] = pe2[::-1, 10:13]  # decreasing output edges: single pass
             pe1[km // 2, 13] = np.nan  # NaN input edge: single pass
             pe1[1:, 14] = pe1[:-1, 14]  # a repeated edge: zero-thickness first layer
+            # unsorted edges only where one half of the split streams (the streamed checks
+            # and the single-pass fix-up): the bottom input edge, just below the middle,
+            # the bottom / top output edge, a NaN bottom input edge
+            pe1[-1, 15] = pe1[km // 3, 15]
+            pe1[km // 2 + 2, 16] = pe1[max(0, km // 2 - 6), 16]
+            pe2[-1, 17] = pe2[0, 17]
+            pe2[0, 18] = pe2[-1, 18]
+            pe1[-1, 19] = np.nan
+            # a raised run of input edges: the first lane stops inside it, the second starts
+            # well below it (the two checked ranges do not meet: the fix-up)
+            pe1[km // 4: km // 4 + 6, 20] += 1e7
             q = (rng.normal(0, 1, (nf, km, ncol)) * rng.choice([1e-4, 1, 300], (nf, km, ncol))).astype(np.float32)
             ref = np.empty((nf, kn, ncol), np.float32)
             with np.errstate(all="ignore"):
