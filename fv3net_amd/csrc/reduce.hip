@@ -377,39 +377,6 @@ __device__ __forceinline__ void area_row_sum(const DiagPtrs<T>& d, int n_diag, c
     }
 }
 
-// area_row_sum for a fixed number ND of diagnostics: one pass over the row with the area
-// and every diagnostic loaded together (the per-diagnostic passes waited for one round
-// trip each), every sum taken in the same order (lane l: columns l, l + 64, ..., then the
-// butterfly), so the same bits
-template <int ND, typename T>
-__device__ __forceinline__ void area_row_sum_n(const DiagPtrs<T>& d, const T* __restrict__ area, int row_len,
-                                               double* __restrict__ out, int64_t out_ld, int64_t r, int lane)
-{
-    const T* a = area + r * row_len;
-    double sa = 0.0, s[ND];
-#pragma unroll
-    for (int j = 0; j < ND; ++j) s[j] = 0.0;
-    for (int c = lane; c < row_len; c += 64) {
-        const T av = a[c];
-        T xv[ND];
-#pragma unroll
-        for (int j = 0; j < ND; ++j) xv[j] = d.p[j][r * row_len + c];
-        sa += (double)av;
-#pragma unroll
-        for (int j = 0; j < ND; ++j) s[j] += (double)(av * xv[j]);  // area * x in T (numpy's product)
-    }
-    sa = wave_sum(sa);
-    double* o = out + r * out_ld;
-#pragma unroll
-    for (int j = 0; j < ND; ++j) {
-        const double t = wave_sum(s[j]);
-        if (lane == 0) {
-            o[2 * j] = t;
-            o[2 * j + 1] = sa;
-        }
-    }
-}
-
 template <typename T>
 __global__ __launch_bounds__(64) void area_row_sums_kernel(DiagPtrs<T> d, int n_diag, const T* __restrict__ area,
                                                            int row_len, double* __restrict__ out, int64_t out_ld)
@@ -433,12 +400,7 @@ __global__ __launch_bounds__(kSumBlock) void step_partials_kernel(DiagPtrs<doubl
     const int64_t nb_rows = (nrows + 3) / 4;
     if ((int64_t)blockIdx.x < nb_rows) {
         const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-        if (r < nrows) {
-            if (n_diag == 3)  // the stepper's three diagnostics (uniform)
-                area_row_sum_n<3>(d, area, row_len, partial, partial_ld, r, threadIdx.x & 63);
-            else
-                area_row_sum(d, n_diag, area, row_len, partial, partial_ld, r, threadIdx.x & 63);
-        }
+        if (r < nrows) area_row_sum(d, n_diag, area, row_len, partial, partial_ld, r, threadIdx.x & 63);
         return;  // no block-wide barrier on this side
     }
     level_count_u8(lim, lim_ld, ncol, (int)(blockIdx.x - nb_rows), level_out, sh);
@@ -455,28 +417,10 @@ __global__ __launch_bounds__(64) void fold_rows_repeat_kernel(const double* __re
     const int j = blockIdx.x;
     const int64_t n = nrows * times;
     double s = 0.0;
-    // the source row r % nrows carried along (a 64-bit remainder per row), and 8 rows'
-    // loads in flight before their sums (in the same order): the loop was a chain of
-    // dependent round trips, 5.1 us for 6 x 1,152 rows (profiles/r05zj_steptrace)
-    constexpr int U = 8;
-    int64_t src = threadIdx.x % nrows;
-    for (int64_t r0 = threadIdx.x; r0 < n; r0 += 64 * U) {
-        double v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t r = r0 + 64 * u;
-            v[u] = r < n ? rows[src * width + j] : 0.0;
-            src += 64;
-            while (src >= nrows) src -= nrows;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t r = r0 + 64 * u;
-            if (r < n) {
-                rep[r * width + j] = v[u];
-                s += v[u];
-            }
-        }
+    for (int64_t r = threadIdx.x; r < n; r += 64) {
+        const double v = rows[(r % nrows) * width + j];
+        rep[r * width + j] = v;
+        s += v;
     }
     s = wave_sum(s);
     if (threadIdx.x == 0) out[j] = s;
