@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(params=["split", "serial", "levels"])
 def path(request, monkeypatch):
     """`split`: pairs of fields on the two-field streaming kernel, each column on two
-    lanes (FV3_MAPPM_SPLIT=1; the default from 65,536 to 131,072 columns); `serial`: the
+    lanes (FV3_MAPPM_SPLIT=1; the default from 65,536 to 147,456 columns); `serial`: the
     same kernel one lane per column (FV3_MAPPM_SPLIT=0, the default above);
     `levels`: the small-grid kernel, one field per launch."""
     set_variant(monkeypatch, "FV3_MAPPM_PATH", "levels" if request.param == "levels" else "serial")
@@ -182,8 +182,9 @@ def test_two_lane_pair_kernel_rank_share_size(gpu, kn, monkeypatch):
     default): whole arrays bit-identical to the one-lane pair kernel and sampled
     columns to the oracle, on columns that take every start of the second lane (a
     direct window, output kB above the top or below the bottom, kB's layer near either
-    end) and columns that keep the single pass (unsorted pe2, a NaN edge); a
-    zero-thickness layer stays on two lanes.  The decreasing-pe2 and NaN-pe1 columns
+    end) and columns that the streamed checks send back to the single pass (unsorted
+    pe2, a NaN edge, an unsorted bottom input or output edge, a raised run of input
+    edges); a zero-thickness layer stays on two lanes.  The unsorted and NaN columns can
     fail the reference's layer search (undefined behaviour, excluded from oracle parity,
     DESIGN.md §4): there the two kernels must agree with each other only."""
     import torch
@@ -204,6 +205,12 @@ def test_two_lane_pair_kernel_rank_share_size(gpu, kn, monkeypatch):
     pe2[:, :64] = pe2[::-1, :64]  # decreasing
     pe1[40, 64:96] = np.nan
     pe1[20, 96:128] = pe1[19, 96:128]  # a zero-thickness layer: still sorted
+    # unsorted only where one lane streams (the streamed checks and the single-pass
+    # fix-up): the bottom input edge, a raised run of input edges (the two lanes' checked
+    # ranges do not meet), the bottom output edge
+    pe1[-1, 160:192] = pe1[30, 160:192]
+    pe1[20:26, 192:224] += 1e7
+    pe2[-1, 224:256] = pe2[0, 224:256]
     qs = [rng.normal(250, 10, (km, ncol)).astype(np.float32), rng.uniform(0, 0.02, (km, ncol)).astype(np.float32)]
     d = [torch.from_numpy(x).cuda() for x in (pe1, pe2, *qs)]
     default = mappm_device_multi(d[0], d[2:], d[1], 1, 1)
@@ -214,7 +221,7 @@ def test_two_lane_pair_kernel_rank_share_size(gpu, kn, monkeypatch):
     for x, y, z in zip(res["1"], res["0"], default):
         assert torch.equal(x.view(torch.int32), y.view(torch.int32))
         assert torch.equal(x.view(torch.int32), z.view(torch.int32))
-    idx = np.concatenate([np.arange(96, 160), np.sort(rng.choice(np.arange(160, ncol), 1500, replace=False))])
+    idx = np.concatenate([np.arange(96, 160), np.sort(rng.choice(np.arange(256, ncol), 1500, replace=False))])
     for q, o in zip(qs, res["1"]):
         with np.errstate(all="ignore"):
             ref = oracle_mappm(pe1[:, idx], q[:, idx], pe2[:, idx], 1, 1)
