@@ -423,9 +423,6 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord, i
             pec_pf = c.pe1(L_start + 5);
         }
     }
-#ifdef FV3_MAPPM_LUNROLL  // tools A/B: the layer loop unrolled (window shifts as renames)
-#pragma unroll FV3_MAPPM_LUNROLL
-#endif
     for (int L = L_start; L <= km; ++L) {
         // level L + 4's q1 / pe1: carried from the previous iteration (CARRY) or read at
         // this iteration's start, as in mappm_ppm_column
