@@ -212,6 +212,8 @@ class StepperWorkload:
         self._plan = LaunchPlan([self.bound, self._epi, self._part])  # one C-ABI call per step
 
     def step(self):
+        """One step; returns the global [n_diag, 2] partials.  Without a process group this
+        is the bound result buffer itself (valid until the next step: copy it to keep it)."""
         from . import _device
         from .distributed import combine_partials
 
@@ -345,6 +347,9 @@ class ShardedStepperWorkload:
             self._plan.add(self._fold)
 
     def step(self):
+        """One step; returns the 6 global partials followed by the nz limiter counts.  With
+        the stubbed exchange this is the fold's result buffer itself (valid until the next
+        step: copy it to keep it)."""
         from . import _device
         from .distributed import global_count_sums, global_row_sums, row_counts
 
