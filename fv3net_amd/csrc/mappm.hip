@@ -459,14 +459,21 @@ const void* cs_global_kernel(const MappmArgs& a, int64_t nlanes)
 
 // kord <= 7: the level-parallel kernel while one lane per column leaves the chip
 // mostly idle (FV3_MAPPM_PATH=serial|levels overrides, for tests and A/B).
-bool use_levels_kernel(const MappmArgs& a)
+bool use_levels_kernel(const MappmArgs& a, int64_t max_cols = kLevelsMaxCols)
 {
     const char* p = fv3::variant_env("FV3_MAPPM_PATH");
     if (p && p[0] == 's') return false;
     if (a.km > 1000 || a.kn > 1000) return false;
     if (p && p[0] == 'l') return true;
-    return a.ncol < kLevelsMaxCols;
+    return a.ncol < max_cols;
 }
+
+// Pairs of fields: the pair kernel on two or three lanes per column beats the
+// level-parallel kernel (one field per launch) from ~10,000 columns
+// (tools/mappm_small_lanes.py, profiles/r05zr_mappm_small_lanes.log and
+// r05zs_mappm_small_lanes.log, two fields, levels / three lanes: 6,912 columns 47 / 59 us,
+// 10,368 63 / 59 us, C48 13,824 77 / 60 us, C96 55,296 252 / 86 us)
+constexpr int64_t kLevelsMaxColsPairs = 10240;
 
 int launch_mappm(MappmArgs a, hipStream_t stream)
 {
@@ -642,6 +649,65 @@ __global__ __launch_bounds__(128) void mappm_ppm_pair_split_kernel(MappmPairArgs
     }
 }
 
+// The same on THREE lanes per column (three waves over 64 columns; outputs split at
+// kB1 = kn / 3 + 1 and kB2 = 2 kn / 3 + 1, each later lane starting where the single pass
+// begins its first output): more waves for grids too small to fill the SIMDs even on
+// two.  The host runs it for kn >= 3 only.
+__global__ __launch_bounds__(192) void mappm_ppm_pair_split3_kernel(MappmPairArgs a)
+{
+    __shared__ int s_ok[2][64], s_l0[2][64], s_exit[64];
+    const int lane = threadIdx.x & 63;
+    const int part = threadIdx.x >> 6;
+    const int64_t c0 = (int64_t)blockIdx.x * 64 + lane;
+    const bool valid = c0 < a.ncol;
+    const int64_t c = valid ? c0 : a.ncol - 1;  // spare lanes only pass the barrier
+    DevColPair d;
+    d.pe1_ = a.pe1 + col_offset(a.l_pe1, c);
+    d.pe2_ = a.pe2 + col_offset(a.l_pe2, c);
+    d.ld_pe1 = a.l_pe1.ld;
+    d.ld_pe2 = a.l_pe2.ld;
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+        d.q1_[f] = a.q1[f] + col_offset(a.l_q1[f], c);
+        d.q2_[f] = a.q2[f] + col_offset(a.l_q2[f], c);
+        d.ld_q1[f] = a.l_q1[f].ld;
+        d.ld_q2[f] = a.l_q2[f].ld;
+    }
+    d.kn = a.kn;
+    const int km = a.km, kn = a.kn;
+    const int kB1 = kn / 3 + 1, kB2 = 2 * kn / 3 + 1;
+    int kf = 1, kl = kB1 - 1, Lf = 1;
+    if (part > 0) {
+        kf = part == 1 ? kB1 : kB2;
+        kl = part == 1 ? kB2 - 1 : kn;
+        const float t = d.pe2(kf);
+        Lf = split_first_layer(d, km, t, split_count_sorted(d, km, t));
+    }
+    SplitCheck chk{1, km};
+    if (valid) {
+        float* q2c[2] = {d.q2_[0], d.q2_[1]};
+        for (int f = 0; f < 2; ++f) d.q2_[f] += (int64_t)(kf - 1) * d.ld_q2[f];
+        d.pe2_next = d.pe2_ + (int64_t)(kf + 1) * d.ld_pe2;
+        d.nb = (kf + 2 <= kn + 1) ? *d.pe2_next : 0.0f;
+        mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0, true>(d, km, kn, a.iv, a.kord, kf, kl, Lf, &chk);
+        for (int f = 0; f < 2; ++f) d.q2_[f] = q2c[f];
+    }
+    if (part > 0) {
+        s_ok[part - 1][lane] = chk.mono;
+        s_l0[part - 1][lane] = Lf;
+    }
+    if (part == 1) s_exit[lane] = chk.l_exit;
+    __syncthreads();
+    if (part == 0 && valid &&
+        !split3_exact(chk, SplitCheck{s_ok[0][lane], s_exit[lane]}, SplitCheck{s_ok[1][lane], km}, s_l0[0][lane],
+                      s_l0[1][lane], km)) {
+        // the fix-up: this column's single pass, over what the lanes wrote
+        d.pe2_next = d.pe2_ + 2 * d.ld_pe2;
+        d.nb = kn >= 2 ? *d.pe2_next : 0.0f;
+        mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0>(d, km, kn, a.iv, a.kord);
+    }
+}
+
 // Where the two-lane kernel pays (tools/mappm_split_time.py, one box, interleaved; one
 // lane per column vs two).  With whole-column sortedness scans up front
 // (profiles/r05r_mappm_split.log): 65,536 columns 142.7 vs 115.4 us, 110,592 (one rank's
@@ -652,13 +718,32 @@ __global__ __launch_bounds__(128) void mappm_ppm_pair_split_kernel(MappmPairArgs
 // level-parallel kernel's range and below kSplitMaxCols columns it runs by default;
 // FV3_MAPPM_SPLIT=0|1 forces it off / on (A/B, tests).
 constexpr int64_t kSplitMaxCols = 147456;
+// Three lanes (profiles/r05zq_mappm_split3.log, one / two / three lanes): 65,536 columns
+// 142.7 / 99 / 86.5 us, 110,592 166 / 141 / 150.5 us, 147,456 214 / 213 / 194 us.  Both
+// split kernels hold 4 waves per SIMD (124-126 VGPRs); three lanes pay while all their
+// waves are resident at once (3 ncol / 64 <= 4 waves x 4 SIMDs x CUs), which 110,592
+// columns exceed.
+constexpr int kSplitWavesPerSimd = 4;
 
-bool use_split_kernel(int64_t ncol)
+// lanes per column of the pair kernel: 1, 2 or 3 (FV3_MAPPM_SPLIT=0|1|3 forces one)
+int split_lanes(int64_t ncol, int kn)
 {
+    static int n_cu = 0;
+    if (!n_cu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            n_cu = 256;
+    }
     const char* p = fv3::variant_env("FV3_MAPPM_SPLIT");
-    if (p && p[0] == '0') return false;
-    if (p && p[0] == '1') return true;
-    return ncol < kSplitMaxCols;
+    int n = ncol < kSplitMaxCols ? 2 : 1;
+    if (n == 2 && 3 * ncol <= (int64_t)64 * kSplitWavesPerSimd * 4 * n_cu) n = 3;
+    if (p && p[0] == '0') n = 1;
+    if (p && p[0] == '1') n = 2;
+    if (p && p[0] == '3') n = 3;
+    if (n == 3 && kn < 3) n = 2;
+    if (n == 2 && kn < 2) n = 1;
+    return n;
 }
 
 }  // namespace fv3
@@ -716,12 +801,16 @@ extern "C" int fv3_mappm_multi(const float* pe1, fv3_layout pe1_l, const float* 
     // pairs on the streaming kord <= 7 kernel; the level-parallel (small grids) and
     // cs_profile (kord > 7) paths, and an odd last field, one field per launch
     MappmArgs one{pe1, nullptr, pe2, nullptr, pe1_l, {}, pe2_l, {}, ncol, km, kn, iv, kord, nullptr};
-    if (kord <= 7 && !fv3::use_levels_kernel(one)) {
+    if (kord <= 7 && !fv3::use_levels_kernel(one, fv3::kLevelsMaxColsPairs)) {
         for (; f + 2 <= n_fields; f += 2) {
             fv3::MappmPairArgs a{pe1, pe2, pe1_l, pe2_l, {q1[f], q1[f + 1]}, {q2[f], q2[f + 1]},
                                  {q1_l[f], q1_l[f + 1]}, {q2_l[f], q2_l[f + 1]}, ncol, km, kn, iv, kord};
             const int block = 256;
-            if (kn >= 2 && fv3::use_split_kernel(ncol)) {  // two lanes per column: 128 threads per 64 columns
+            const int lanes = fv3::split_lanes(ncol, kn);
+            if (lanes == 3) {  // three lanes per column: 192 threads per 64 columns
+                const int64_t grid = (ncol + 63) / 64;
+                hipLaunchKernelGGL(fv3::mappm_ppm_pair_split3_kernel, dim3((unsigned)grid), dim3(192), 0, s, a);
+            } else if (lanes == 2) {  // two lanes per column: 128 threads per 64 columns
                 const int64_t grid = (ncol + 63) / 64;
                 hipLaunchKernelGGL(fv3::mappm_ppm_pair_split_kernel, dim3((unsigned)grid), dim3(128), 0, s, a);
             } else {

@@ -269,9 +269,20 @@ FV3_HD inline int split_count_sorted(Col& c, int km, float t)
 // the split's two ranges of checked pe1 pairs meet: the first lane (from layer 1) checked
 // the pairs (j, j + 1) for j <= l_exit + 3, the second (its window built at L0, when
 // 4 <= L0 <= km - 3; else it walked from layer 1 itself) those from j = L0 - 3
+FV3_HD inline bool split_meets(const SplitCheck& a, int L0, int km)
+{
+    return L0 < 4 || L0 > km - 3 || a.l_exit + 7 >= L0;
+}
 FV3_HD inline bool split_exact(const SplitCheck& a, const SplitCheck& b, int L0, int km)
 {
-    return a.mono && b.mono && (L0 < 4 || L0 > km - 3 || a.l_exit + 7 >= L0);
+    return a.mono && b.mono && split_meets(a, L0, km);
+}
+// three lanes (outputs split at kB1 and kB2; L0b / L0c the second and third lanes'
+// start layers): every lane's checks passed and each lane's range meets the next one's
+FV3_HD inline bool split3_exact(const SplitCheck& a, const SplitCheck& b, const SplitCheck& c, int L0b, int L0c,
+                                int km)
+{
+    return a.mono && b.mono && c.mono && split_meets(a, L0b, km) && split_meets(b, L0c, km);
 }
 
 // SPLIT: the remap consumer's view of the column with every output edge it takes checked

@@ -193,6 +193,38 @@ static void run_split(int km, const float* pe1, const float* q1, int kn, const f
         if (!fv3::split_exact(a, b, L0, km)) fv3::mappm_ppm_columns<NF, ColN, true>(c, km, kn, iv, kord);
     }
 }
+// a column on three lanes (the kernel's split points kn / 3 + 1 and 2 kn / 3 + 1, kn >= 3)
+template <int NF>
+static void run_split3(int km, const float* pe1, const float* q1, int kn, const float* pe2, float* q2, int64_t ncol,
+                       int iv, int kord, int walk)
+{
+    for (int64_t i = 0; i < ncol; ++i) {
+        ColN c{pe1, q1, pe2, q2, ncol, i, km, kn};
+        if (kn < 3) {
+            fv3::mappm_ppm_columns<NF, ColN, true>(c, km, kn, iv, kord);
+            continue;
+        }
+        const int kB1 = kn / 3 + 1, kB2 = 2 * kn / 3 + 1;
+        const float t1 = c.pe2(kB1), t2 = c.pe2(kB2);
+        const int L1 = walk ? 1 : fv3::split_first_layer(c, km, t1, fv3::split_count_sorted(c, km, t1));
+        const int L2 = walk ? 1 : fv3::split_first_layer(c, km, t2, fv3::split_count_sorted(c, km, t2));
+        fv3::SplitCheck a{1, km}, b{1, km}, d{1, km};
+        fv3::mappm_ppm_columns<NF, ColN, true, true>(c, km, kn, iv, kord, 1, kB1 - 1, 1, &a);
+        fv3::mappm_ppm_columns<NF, ColN, true, true>(c, km, kn, iv, kord, kB1, kB2 - 1, L1, &b);
+        fv3::mappm_ppm_columns<NF, ColN, true, true>(c, km, kn, iv, kord, kB2, kn, L2, &d);
+        if (!fv3::split3_exact(a, b, d, L1, L2, km)) fv3::mappm_ppm_columns<NF, ColN, true>(c, km, kn, iv, kord);
+    }
+}
+extern "C" int host_mappm_split3(int nf, int km, const float* pe1, const float* q1, int kn, const float* pe2,
+                                 float* q2, int64_t ncol, int iv, int kord, int walk)
+{
+    if (km < 4 || kn < 1 || kord > 7) return -1;
+    switch (nf) {
+        case 1: run_split3<1>(km, pe1, q1, kn, pe2, q2, ncol, iv, kord, walk); return 0;
+        case 2: run_split3<2>(km, pe1, q1, kn, pe2, q2, ncol, iv, kord, walk); return 0;
+    }
+    return -1;
+}
 extern "C" int host_mappm_split(int nf, int km, const float* pe1, const float* q1, int kn, const float* pe2,
                                 float* q2, int64_t ncol, int iv, int kord, int kb, int walk)
 {

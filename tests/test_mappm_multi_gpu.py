@@ -16,15 +16,16 @@ from tests.test_mappm_gpu import _bits_equal, _columns
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["split", "serial", "levels"])
+@pytest.fixture(params=["split", "split3", "serial", "levels"])
 def path(request, monkeypatch):
     """`split`: pairs of fields on the two-field streaming kernel, each column on two
     lanes (FV3_MAPPM_SPLIT=1; the default from 65,536 to 147,456 columns); `serial`: the
     same kernel one lane per column (FV3_MAPPM_SPLIT=0, the default above);
-    `levels`: the small-grid kernel, one field per launch."""
+    `split3`: three lanes per column (FV3_MAPPM_SPLIT=3); `levels`: the small-grid kernel,
+    one field per launch."""
     set_variant(monkeypatch, "FV3_MAPPM_PATH", "levels" if request.param == "levels" else "serial")
     if request.param != "levels":
-        set_variant(monkeypatch, "FV3_MAPPM_SPLIT", "1" if request.param == "split" else "0")
+        set_variant(monkeypatch, "FV3_MAPPM_SPLIT", {"split": "1", "split3": "3"}.get(request.param, "0"))
     return request.param
 
 
@@ -215,12 +216,13 @@ def test_two_lane_pair_kernel_rank_share_size(gpu, kn, monkeypatch):
     d = [torch.from_numpy(x).cuda() for x in (pe1, pe2, *qs)]
     default = mappm_device_multi(d[0], d[2:], d[1], 1, 1)
     res = {}
-    for split in ("1", "0"):
+    for split in ("1", "0", "3"):  # two lanes, one, three
         set_variant(monkeypatch, "FV3_MAPPM_SPLIT", split)
         res[split] = mappm_device_multi(d[0], d[2:], d[1], 1, 1)
-    for x, y, z in zip(res["1"], res["0"], default):
+    for x, y, z, w in zip(res["1"], res["0"], default, res["3"]):
         assert torch.equal(x.view(torch.int32), y.view(torch.int32))
         assert torch.equal(x.view(torch.int32), z.view(torch.int32))
+        assert torch.equal(w.view(torch.int32), y.view(torch.int32))
     idx = np.concatenate([np.arange(96, 160), np.sort(rng.choice(np.arange(256, ncol), 1500, replace=False))])
     for q, o in zip(qs, res["1"]):
         with np.errstate(all="ignore"):

@@ -323,7 +323,7 @@ def test_cs_register_tail_is_bit_identical(host_lib, km, kn):
 @pytest.mark.parametrize("nf", [1, 2])
 @pytest.mark.parametrize("km,kn", [(4, 40), (79, 79), (79, 50), (20, 5), (12, 2), (79, 120)])
 def test_two_lane_column_split_bit_identical(host_lib, nf, km, kn):
-    """A column on two lanes (the small-grid pair kernel): outputs 1 .. kB-1 streamed from
+    """A column on two (and three) lanes (the small-grid pair kernels): outputs 1 .. kB-1 streamed from
     layer 1, kB .. kn from the layer where the single pass begins output kB, its window
     built from the local stencil (or, walk = 1 / out of the direct range, from layer 1).
     Every split point, both start modes, every PPM kord and iv, on columns with
@@ -334,6 +334,10 @@ def test_two_lane_column_split_bit_identical(host_lib, nf, km, kn):
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                    ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    f3 = host_lib.host_mappm_split3
+    f3.restype = ctypes.c_int
+    f3.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int]
     mf = host_lib.host_mappm_multi
     mf.restype = ctypes.c_int
     mf.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
@@ -378,3 +382,8 @@ def test_two_lane_column_split_bit_identical(host_lib, nf, km, kn):
                         assert fn(nf, km, pe1.ctypes.data, q.ctypes.data, kn, pe2.ctypes.data, out.ctypes.data,
                                   ncol, iv, kord, kb, walk) == 0
                         assert _bits_equal(out, ref), (kord, iv, kb, walk)
+                for walk in (0, 1):  # three lanes (outputs split at kn/3 + 1 and 2kn/3 + 1)
+                    out = np.full((nf, kn, ncol), 7.0, np.float32)
+                    assert f3(nf, km, pe1.ctypes.data, q.ctypes.data, kn, pe2.ctypes.data, out.ctypes.data,
+                              ncol, iv, kord, walk) == 0
+                    assert _bits_equal(out, ref), (kord, iv, "three lanes", walk)
