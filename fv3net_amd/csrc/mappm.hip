@@ -475,6 +475,8 @@ bool use_levels_kernel(const MappmArgs& a, int64_t max_cols = kLevelsMaxCols)
 // 10,368 63 / 59 us, C48 13,824 77 / 60 us, C96 55,296 252 / 86 us)
 constexpr int64_t kLevelsMaxColsPairs = 10240;
 
+bool launch_split_single(const MappmArgs& a, hipStream_t stream);  // below the split kernels
+
 int launch_mappm(MappmArgs a, hipStream_t stream)
 {
     if (a.ncol == 0) return FV3_OK;
@@ -495,6 +497,8 @@ int launch_mappm(MappmArgs a, hipStream_t stream)
         FV3_REQUIRE(lds <= 160 * 1024, "mappm: km=%d too large for the kord>7 LDS path", a.km);
         const int64_t grid = (a.ncol + block - 1) / block;
         hipLaunchKernelGGL(mappm_cs_kernel, dim3((unsigned)grid), dim3(block), lds, stream, a);
+    } else if (launch_split_single(a, stream)) {
+        // one field on two or three lanes per column
     } else if (use_levels_kernel(a)) {
         const int block = a.km + 1 > 64 ? 128 : 64;
         const size_t lds = sizeof(float) * (9 * (size_t)(a.km + 2) + (size_t)(a.kn + 2));
@@ -523,14 +527,15 @@ struct MappmPairArgs {
     int km, kn, iv, kord;
 };
 
-// DevCol for mappm_ppm_columns<2>: fields f = 0, 1 emit output k in turn, so each keeps
-// its own running output pointer
-struct DevColPair {
+// DevCol for mappm_ppm_columns<NF> (NF = 1, 2): fields f emit output k in turn, so each
+// keeps its own running output pointer
+template <int NF>
+struct DevColN {
     const float* pe1_;
     const float* pe2_;
-    const float* q1_[2];
-    float* q2_[2];
-    int64_t ld_pe1, ld_pe2, ld_q1[2], ld_q2[2];
+    const float* q1_[NF];
+    float* q2_[NF];
+    int64_t ld_pe1, ld_pe2, ld_q1[NF], ld_q2[NF];
     int kn;
     const float* pe2_next;
     float nb;  // as DevCol::nb
@@ -556,6 +561,7 @@ struct DevColPair {
         return r;
     }
 };
+using DevColPair = DevColN<2>;
 
 __global__ __launch_bounds__(256) void mappm_ppm_pair_kernel(MappmPairArgs a)
 {
@@ -594,6 +600,7 @@ __global__ __launch_bounds__(256) void mappm_ppm_pair_kernel(MappmPairArgs a)
 // relies on on the edges they stream, and after the block barrier the first lane re-runs
 // the single pass on any column the checks did not prove (unsorted or NaN edges).  The
 // host runs this kernel for kn >= 2 only.
+template <int NF>
 __global__ __launch_bounds__(128) void mappm_ppm_pair_split_kernel(MappmPairArgs a)
 {
     __shared__ int s_ok[64], s_l0[64];
@@ -602,13 +609,13 @@ __global__ __launch_bounds__(128) void mappm_ppm_pair_split_kernel(MappmPairArgs
     const int64_t c0 = (int64_t)blockIdx.x * 64 + lane;
     const bool valid = c0 < a.ncol;
     const int64_t c = valid ? c0 : a.ncol - 1;  // spare lanes only pass the barrier
-    DevColPair d;
+    DevColN<NF> d;
     d.pe1_ = a.pe1 + col_offset(a.l_pe1, c);
     d.pe2_ = a.pe2 + col_offset(a.l_pe2, c);
     d.ld_pe1 = a.l_pe1.ld;
     d.ld_pe2 = a.l_pe2.ld;
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
+    for (int f = 0; f < NF; ++f) {
         d.q1_[f] = a.q1[f] + col_offset(a.l_q1[f], c);
         d.q2_[f] = a.q2[f] + col_offset(a.l_q2[f], c);
         d.ld_q1[f] = a.l_q1[f].ld;
@@ -629,12 +636,15 @@ __global__ __launch_bounds__(128) void mappm_ppm_pair_split_kernel(MappmPairArgs
     if (valid) {
         // the output pointers and the edge cursor where the single pass has them once
         // output kf - 1 is written
-        float* q2c[2] = {d.q2_[0], d.q2_[1]};
-        for (int f = 0; f < 2; ++f) d.q2_[f] += (int64_t)(kf - 1) * d.ld_q2[f];
+        float* q2c[NF];
+        for (int f = 0; f < NF; ++f) {
+            q2c[f] = d.q2_[f];
+            d.q2_[f] += (int64_t)(kf - 1) * d.ld_q2[f];
+        }
         d.pe2_next = d.pe2_ + (int64_t)(kf + 1) * d.ld_pe2;
         d.nb = (kf + 2 <= kn + 1) ? *d.pe2_next : 0.0f;
-        mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0, true>(d, km, kn, a.iv, a.kord, kf, kl, Lf, &chk);
-        for (int f = 0; f < 2; ++f) d.q2_[f] = q2c[f];
+        mappm_ppm_columns<NF, DevColN<NF>, FV3_MAPPM_PAIR_CARRY != 0, true>(d, km, kn, a.iv, a.kord, kf, kl, Lf, &chk);
+        for (int f = 0; f < NF; ++f) d.q2_[f] = q2c[f];
     }
     if (part == 1) {
         s_ok[lane] = chk.mono;
@@ -645,7 +655,7 @@ __global__ __launch_bounds__(128) void mappm_ppm_pair_split_kernel(MappmPairArgs
         // the fix-up: this column's single pass, over what the halves wrote
         d.pe2_next = d.pe2_ + 2 * d.ld_pe2;
         d.nb = kn >= 2 ? *d.pe2_next : 0.0f;
-        mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0>(d, km, kn, a.iv, a.kord);
+        mappm_ppm_columns<NF, DevColN<NF>, FV3_MAPPM_PAIR_CARRY != 0>(d, km, kn, a.iv, a.kord);
     }
 }
 
@@ -653,6 +663,7 @@ __global__ __launch_bounds__(128) void mappm_ppm_pair_split_kernel(MappmPairArgs
 // kB1 = kn / 3 + 1 and kB2 = 2 kn / 3 + 1, each later lane starting where the single pass
 // begins its first output): more waves for grids too small to fill the SIMDs even on
 // two.  The host runs it for kn >= 3 only.
+template <int NF>
 __global__ __launch_bounds__(192) void mappm_ppm_pair_split3_kernel(MappmPairArgs a)
 {
     __shared__ int s_ok[2][64], s_l0[2][64], s_exit[64];
@@ -661,13 +672,13 @@ __global__ __launch_bounds__(192) void mappm_ppm_pair_split3_kernel(MappmPairArg
     const int64_t c0 = (int64_t)blockIdx.x * 64 + lane;
     const bool valid = c0 < a.ncol;
     const int64_t c = valid ? c0 : a.ncol - 1;  // spare lanes only pass the barrier
-    DevColPair d;
+    DevColN<NF> d;
     d.pe1_ = a.pe1 + col_offset(a.l_pe1, c);
     d.pe2_ = a.pe2 + col_offset(a.l_pe2, c);
     d.ld_pe1 = a.l_pe1.ld;
     d.ld_pe2 = a.l_pe2.ld;
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
+    for (int f = 0; f < NF; ++f) {
         d.q1_[f] = a.q1[f] + col_offset(a.l_q1[f], c);
         d.q2_[f] = a.q2[f] + col_offset(a.l_q2[f], c);
         d.ld_q1[f] = a.l_q1[f].ld;
@@ -685,12 +696,15 @@ __global__ __launch_bounds__(192) void mappm_ppm_pair_split3_kernel(MappmPairArg
     }
     SplitCheck chk{1, km};
     if (valid) {
-        float* q2c[2] = {d.q2_[0], d.q2_[1]};
-        for (int f = 0; f < 2; ++f) d.q2_[f] += (int64_t)(kf - 1) * d.ld_q2[f];
+        float* q2c[NF];
+        for (int f = 0; f < NF; ++f) {
+            q2c[f] = d.q2_[f];
+            d.q2_[f] += (int64_t)(kf - 1) * d.ld_q2[f];
+        }
         d.pe2_next = d.pe2_ + (int64_t)(kf + 1) * d.ld_pe2;
         d.nb = (kf + 2 <= kn + 1) ? *d.pe2_next : 0.0f;
-        mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0, true>(d, km, kn, a.iv, a.kord, kf, kl, Lf, &chk);
-        for (int f = 0; f < 2; ++f) d.q2_[f] = q2c[f];
+        mappm_ppm_columns<NF, DevColN<NF>, FV3_MAPPM_PAIR_CARRY != 0, true>(d, km, kn, a.iv, a.kord, kf, kl, Lf, &chk);
+        for (int f = 0; f < NF; ++f) d.q2_[f] = q2c[f];
     }
     if (part > 0) {
         s_ok[part - 1][lane] = chk.mono;
@@ -704,7 +718,7 @@ __global__ __launch_bounds__(192) void mappm_ppm_pair_split3_kernel(MappmPairArg
         // the fix-up: this column's single pass, over what the lanes wrote
         d.pe2_next = d.pe2_ + 2 * d.ld_pe2;
         d.nb = kn >= 2 ? *d.pe2_next : 0.0f;
-        mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0>(d, km, kn, a.iv, a.kord);
+        mappm_ppm_columns<NF, DevColN<NF>, FV3_MAPPM_PAIR_CARRY != 0>(d, km, kn, a.iv, a.kord);
     }
 }
 
@@ -725,16 +739,23 @@ constexpr int64_t kSplitMaxCols = 147456;
 // columns exceed.
 constexpr int kSplitWavesPerSimd = 4;
 
-// lanes per column of the pair kernel: 1, 2 or 3 (FV3_MAPPM_SPLIT=0|1|3 forces one)
-int split_lanes(int64_t ncol, int kn)
+int device_cus()
 {
     static int n_cu = 0;
     if (!n_cu) {
-        int dev = 0;
+        int dev = 0, n = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            n_cu = 256;
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        n_cu = n;
     }
+    return n_cu;
+}
+
+// lanes per column of the pair kernel: 1, 2 or 3 (FV3_MAPPM_SPLIT=0|1|3 forces one)
+int split_lanes(int64_t ncol, int kn)
+{
+    const int n_cu = device_cus();
     const char* p = fv3::variant_env("FV3_MAPPM_SPLIT");
     int n = ncol < kSplitMaxCols ? 2 : 1;
     if (n == 2 && 3 * ncol <= (int64_t)64 * kSplitWavesPerSimd * 4 * n_cu) n = 3;
@@ -744,6 +765,41 @@ int split_lanes(int64_t ncol, int kn)
     if (n == 3 && kn < 3) n = 2;
     if (n == 2 && kn < 2) n = 1;
     return n;
+}
+
+// One field (fv3_mappm_ex, kord <= 7) on the split kernels (profiles/r05zw_mappm_single_lanes.log,
+// levels / one lane / two / three lanes, us): 13,824 columns 38.6 / 105 / 70 / 49.6,
+// 27,648 67.8 / 108 / 76 / 56.6, C96 55,296 126 / 110 / 81 / 70, 82,944 184 / 127 / 113 /
+// 98, 110,592 242 / 128 / 115 / 119, 147,456 320 / 152 / 139 / 149, 221,184 589 / 190 /
+// 204 / 210.  The one-field split kernels hold 5 waves per SIMD (91 VGPRs): three lanes
+// while all their waves are resident (3 ncol / 64 <= 5 x 4 SIMDs x CUs), then two while
+// theirs are, from 20,480 columns (the level-parallel kernel below).  FV3_MAPPM_SPLIT1=0|2|3
+// forces none / two / three lanes (A/B); a forced FV3_MAPPM_PATH keeps its kernel.
+// Returns false where the host keeps the level-parallel or one-lane kernel.
+constexpr int64_t kSplit1MinCols = 20480;
+constexpr int kSplit1WavesPerSimd = 5;
+
+bool launch_split_single(const MappmArgs& a, hipStream_t stream)
+{
+    if (a.kord > 7 || a.kn < 2) return false;
+    const char* p = variant_env("FV3_MAPPM_SPLIT1");
+    int lanes = 0;
+    if (p) {
+        lanes = atoi(p);
+    } else if (!variant_env("FV3_MAPPM_PATH") && a.ncol >= kSplit1MinCols) {
+        const int64_t resident = (int64_t)64 * kSplit1WavesPerSimd * 4 * device_cus();
+        lanes = 3 * a.ncol <= resident ? 3 : (2 * a.ncol <= resident ? 2 : 0);
+    }
+    if (lanes == 3 && a.kn < 3) lanes = 2;
+    if (lanes != 2 && lanes != 3) return false;
+    MappmPairArgs pa{a.pe1, a.pe2, a.l_pe1, a.l_pe2, {a.q1, nullptr}, {a.q2, nullptr}, {a.l_q1, {}}, {a.l_q2, {}},
+                     a.ncol, a.km, a.kn, a.iv, a.kord};
+    const int64_t grid = (a.ncol + 63) / 64;
+    if (lanes == 3)
+        hipLaunchKernelGGL(mappm_ppm_pair_split3_kernel<1>, dim3((unsigned)grid), dim3(192), 0, stream, pa);
+    else
+        hipLaunchKernelGGL(mappm_ppm_pair_split_kernel<1>, dim3((unsigned)grid), dim3(128), 0, stream, pa);
+    return true;
 }
 
 }  // namespace fv3
@@ -809,10 +865,10 @@ extern "C" int fv3_mappm_multi(const float* pe1, fv3_layout pe1_l, const float* 
             const int lanes = fv3::split_lanes(ncol, kn);
             if (lanes == 3) {  // three lanes per column: 192 threads per 64 columns
                 const int64_t grid = (ncol + 63) / 64;
-                hipLaunchKernelGGL(fv3::mappm_ppm_pair_split3_kernel, dim3((unsigned)grid), dim3(192), 0, s, a);
+                hipLaunchKernelGGL(fv3::mappm_ppm_pair_split3_kernel<2>, dim3((unsigned)grid), dim3(192), 0, s, a);
             } else if (lanes == 2) {  // two lanes per column: 128 threads per 64 columns
                 const int64_t grid = (ncol + 63) / 64;
-                hipLaunchKernelGGL(fv3::mappm_ppm_pair_split_kernel, dim3((unsigned)grid), dim3(128), 0, s, a);
+                hipLaunchKernelGGL(fv3::mappm_ppm_pair_split_kernel<2>, dim3((unsigned)grid), dim3(128), 0, s, a);
             } else {
                 const int64_t grid = (ncol + block - 1) / block;
                 hipLaunchKernelGGL(fv3::mappm_ppm_pair_kernel, dim3((unsigned)grid), dim3(block), 0, s, a);

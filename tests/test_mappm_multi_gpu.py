@@ -228,3 +228,53 @@ def test_two_lane_pair_kernel_rank_share_size(gpu, kn, monkeypatch):
         with np.errstate(all="ignore"):
             ref = oracle_mappm(pe1[:, idx], q[:, idx], pe2[:, idx], 1, 1)
         assert _bits_equal(o.cpu().numpy()[:, idx], ref)
+
+
+@pytest.mark.parametrize("ncol", [27648, 55296, 110592])
+def test_single_field_split_lanes_default(gpu, ncol, monkeypatch):
+    """One field (fv3_mappm_ex) on the split kernels the host picks by size (three lanes at
+    27,648 and 55,296 columns, two at 110,592) and forced to two / three lanes: whole
+    arrays bit-identical to one lane per column on sorted columns and, over the unsorted /
+    NaN / raised-run columns (the streamed checks' fix-up), to the multi-field single pass
+    (the one-lane pair kernel); sampled sorted columns equal the oracle."""
+    import torch
+
+    from fv3net_amd.mappm import mappm_device
+
+    rng = np.random.default_rng(ncol)
+    km, kn = 79, 79
+    base = np.linspace(200, 1800, km, dtype=np.float32)[:, None]
+    delp = (base * rng.uniform(0.9, 1.1, (km, ncol))).astype(np.float32)
+    pe1 = np.concatenate([np.full((1, ncol), 300, np.float32), 300 + np.cumsum(delp, 0, dtype=np.float32)])
+    frac = np.sort(rng.uniform(-0.1, 1.1, (kn + 1, ncol)), 0)
+    pe2 = (pe1[0] + (pe1[-1] - pe1[0]) * frac).astype(np.float32)
+    bad = np.arange(0, 160)
+    pe2[:, :32] = pe2[::-1, :32]
+    pe1[40, 32:64] = np.nan
+    pe1[20:26, 64:96] += 1e7
+    pe1[-1, 96:128] = pe1[30, 96:128]
+    pe2[-1, 128:160] = pe2[0, 128:160]
+    q = rng.normal(250, 10, (km, ncol)).astype(np.float32)
+    d = [torch.from_numpy(x).cuda() for x in (pe1, q, pe2)]
+    runs = {}
+    for name, env in (("default", {}), ("two", {"FV3_MAPPM_SPLIT1": "2"}), ("three", {"FV3_MAPPM_SPLIT1": "3"}),
+                      ("one", {"FV3_MAPPM_PATH": "serial", "FV3_MAPPM_SPLIT1": "0"})):
+        for k in ("FV3_MAPPM_SPLIT1", "FV3_MAPPM_PATH"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            set_variant(monkeypatch, k, v)
+        runs[name] = mappm_device(d[0], d[1], d[2], 1, 1).cpu().numpy()
+    good = np.setdiff1d(np.arange(ncol), bad)
+    for name in ("default", "two", "three"):
+        assert _bits_equal(runs[name][:, good], runs["one"][:, good]), name
+    # the unsorted columns: the fix-up's single pass is the multi-field streaming code's
+    # (the one-lane pair kernel on two copies of the field)
+    monkeypatch.delenv("FV3_MAPPM_SPLIT1", raising=False)
+    set_variant(monkeypatch, "FV3_MAPPM_PATH", "serial")
+    set_variant(monkeypatch, "FV3_MAPPM_SPLIT", "0")
+    from fv3net_amd.mappm import mappm_device_multi
+    multi = mappm_device_multi(d[0], [d[1], d[1]], d[2], 1, 1)[0].cpu().numpy()
+    for name in ("default", "two", "three"):
+        assert _bits_equal(runs[name][:, bad], multi[:, bad]), name
+    idx = np.sort(rng.choice(good, 1000, replace=False))
+    assert _bits_equal(runs["default"][:, idx], oracle_mappm(pe1[:, idx], q[:, idx], pe2[:, idx], 1, 1))
