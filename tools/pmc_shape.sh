@@ -1,4 +1,6 @@
 #!/bin/bash
+# (FV3_B3_SHAPE=32 selected dense_b3w_kernel, built in commit d385025 and removed after this
+# comparison: profiles/r05zd_b3_mfma32_pmc.txt; on later trees both passes run the default kernel)
 # PMC passes of the emulator on both split-kernel shapes
 set -u
 export TMPDIR=/tmp FV3_VARIANTS=1
