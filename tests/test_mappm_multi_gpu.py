@@ -19,10 +19,12 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(params=["split", "split3", "serial", "levels"])
 def path(request, monkeypatch):
     """`split`: pairs of fields on the two-field streaming kernel, each column on two
-    lanes (FV3_MAPPM_SPLIT=1; the default from 65,536 to 147,456 columns); `serial`: the
-    same kernel one lane per column (FV3_MAPPM_SPLIT=0, the default above);
-    `split3`: three lanes per column (FV3_MAPPM_SPLIT=3); `levels`: the small-grid kernel,
-    one field per launch."""
+    lanes (FV3_MAPPM_SPLIT=1; the default for pairs from ~87,000 to 147,456 columns on 256
+    CUs); `split3`: three lanes per column (FV3_MAPPM_SPLIT=3; the default for pairs from
+    10,240 columns up to ~87,000); `serial`: the same kernel one lane per column
+    (FV3_MAPPM_SPLIT=0, the default above 147,456); `levels`: the small-grid kernel, one
+    field per launch (the default for pairs below 10,240 columns and single fields below
+    20,480).  Single-field calls under a forced FV3_MAPPM_PATH keep that path's kernel."""
     set_variant(monkeypatch, "FV3_MAPPM_PATH", "levels" if request.param == "levels" else "serial")
     if request.param != "levels":
         set_variant(monkeypatch, "FV3_MAPPM_SPLIT", {"split": "1", "split3": "3"}.get(request.param, "0"))
