@@ -599,7 +599,8 @@ __global__ __launch_bounds__(256) void mappm_ppm_pair_kernel(MappmPairArgs a)
 // start layer in two rounds of loads; both lanes check the sortedness that start layer
 // relies on on the edges they stream, and after the block barrier the first lane re-runs
 // the single pass on any column the checks did not prove (unsorted or NaN edges).  The
-// host runs this kernel for kn >= 2 only.
+// host runs this kernel for kn >= 2 only, on NF = 2 fields (fv3_mappm_multi's pairs) or
+// one (fv3_mappm_ex).
 template <int NF>
 __global__ __launch_bounds__(128) void mappm_ppm_pair_split_kernel(MappmPairArgs a)
 {
