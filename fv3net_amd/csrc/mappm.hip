@@ -740,16 +740,16 @@ constexpr int64_t kSplitMaxCols = 147456;
 // columns exceed.
 constexpr int kSplitWavesPerSimd = 4;
 
+// CUs of the current device, queried once (thread-safe static initialisation)
 int device_cus()
 {
-    static int n_cu = 0;
-    if (!n_cu) {
+    static const int n_cu = [] {
         int dev = 0, n = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
             n = 256;
-        n_cu = n;
-    }
+        return n;
+    }();
     return n_cu;
 }
 
