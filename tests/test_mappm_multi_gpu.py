@@ -280,3 +280,35 @@ def test_single_field_split_lanes_default(gpu, ncol, monkeypatch):
         assert _bits_equal(runs[name][:, bad], multi[:, bad]), name
     idx = np.sort(rng.choice(good, 1000, replace=False))
     assert _bits_equal(runs["default"][:, idx], oracle_mappm(pe1[:, idx], q[:, idx], pe2[:, idx], 1, 1))
+
+
+@pytest.mark.parametrize("km,kn", [(4, 2), (4, 3), (5, 9), (12, 2), (40, 79)])
+def test_split_defaults_small_level_counts(gpu, km, kn, monkeypatch):
+    """The split kernels the host picks at 30,000 columns (one field: three lanes, or two
+    for kn = 2; a pair: three lanes) on few or unequal level counts, including kn = 2
+    (the smallest a split takes) and km = 4 (no direct start window): bit-identical to
+    one lane per column, and to the oracle on sampled columns."""
+    import torch
+
+    from fv3net_amd.mappm import mappm_device, mappm_device_multi
+
+    rng = np.random.default_rng(km * 100 + kn)
+    ncol = 30000
+    pe1, q0, pe2 = _columns(rng, km, kn, ncol)
+    q1 = _fields(rng, km, ncol, 1)[0]
+    d = [torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (pe1, q0, q1, pe2)]
+    for kord in (1, 5, 7):
+        for iv in (0, 1):
+            monkeypatch.delenv("FV3_MAPPM_PATH", raising=False)
+            monkeypatch.delenv("FV3_MAPPM_SPLIT", raising=False)
+            one_default = mappm_device(d[0], d[1], d[3], iv, kord).cpu().numpy()
+            pair_default = [o.cpu().numpy() for o in mappm_device_multi(d[0], [d[1], d[2]], d[3], iv, kord)]
+            set_variant(monkeypatch, "FV3_MAPPM_PATH", "serial")
+            set_variant(monkeypatch, "FV3_MAPPM_SPLIT", "0")
+            one_ref = mappm_device(d[0], d[1], d[3], iv, kord).cpu().numpy()
+            pair_ref = [o.cpu().numpy() for o in mappm_device_multi(d[0], [d[1], d[2]], d[3], iv, kord)]
+            assert _bits_equal(one_default, one_ref), (kord, iv)
+            for a, b in zip(pair_default, pair_ref):
+                assert _bits_equal(a, b), (kord, iv)
+            idx = np.sort(rng.choice(ncol, 300, replace=False))
+            assert _bits_equal(one_default[:, idx], oracle_mappm(pe1[:, idx], q0[:, idx], pe2[:, idx], iv, kord))
