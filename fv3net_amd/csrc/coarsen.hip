@@ -269,16 +269,21 @@ __global__ __launch_bounds__(512) void regrid_coarsen_kernel(CoarsenArgs<DT> a)
 //           the masked-area denominators of every level (field-independent) once.
 //   per field: each lane runs the streaming mappm (remap_layer_fast) on its column;
 //           emit(k) applies the level's mask weight and drops nan0(q * w) into a
-//           per-wave ring of kRing levels; after every input layer, once all lanes
+//           per-wave ring of ring_levels(NF) levels; after every input layer, once all lanes
 //           have emitted kcons + NB levels, those NB levels are summed per cell in
 //           numpy order (lane = row of (cell, level)) and written.  A lane that runs
-//           kRing levels ahead of the slowest (e.g. a much shallower column in a
+//           ring_levels(NF) levels ahead of the slowest (e.g. a much shallower column in a
 //           steep cell) writes from then on into a per-lane global column instead
 //           (sticky, recorded in LDS); the sums read those entries from there.
 // Same arithmetic and order as regrid_coarsen_kernel, so the same bits.
 // ====================================================================================
 
-constexpr int kRing = 16;     // output levels held per wave
+// output levels held per wave and field: 16 for one field; 12 for the two-field pass,
+// whose 16-level rings (8.3 KB of LDS per one-wave block) held it to 15 blocks per CU
+// against the 16 its registers allow (4 fields 2.29 -> 2.11 ms; 1 field with 12 levels
+// 0.757 -> 0.761 ms, so it keeps 16; profiles/r05zzh_coarsen_ring_ab.log).  A lane
+// running that many levels ahead of its cell's slowest writes to its global column.
+constexpr int ring_levels(int nf) { return nf >= 2 ? 12 : 16; }
 constexpr int kRingLd = 65;   // ring row stride (floats): rows of one cell read bank-free
 
 // per-level cell sums in numpy's order for nb consecutive levels of G cells:
@@ -316,7 +321,7 @@ struct CellCtx {
     int64_t cplane;
     const DT* pc;       // [G][km+1] coarse phalf
     const float* den;   // [G][km] masked-area sums
-    float* ring;        // [NF][kRing][kRingLd]
+    float* ring;        // [NF][ring_levels(NF)][kRingLd]
     const int* ovf;     // [NF][64] first level a lane wrote to its global column (km: none)
     float* rowbuf;      // [64]
     float* scr;         // global columns [NF][km][gridDim * 64], or NULL
@@ -329,7 +334,7 @@ struct CellCtx {
         const int gl0 = blockIdx.x * 64;
         const int f = FF ? FF : this->f, ff = f * f, G = 64 / ff;
         for (int fi = 0; fi < NF; ++fi) {
-            const float* rg = ring + fi * (kRing * kRingLd);
+            const float* rg = ring + fi * (ring_levels(NF) * kRingLd);
             const int* ov = ovf + fi * 64;
             const float* sc = scr + (int64_t)fi * km * sstride;
             float* o = out[fi];
@@ -338,7 +343,7 @@ struct CellCtx {
                 [&](int g, int kk, int j) {
                     const int l = g * ff + j, k = k0 + kk;
                     if (k >= ov[l]) return sc[(int64_t)k * sstride + gl0 + l];
-                    return rg[(k % kRing) * kRingLd + l];
+                    return rg[(k % ring_levels(NF)) * kRingLd + l];
                 },
                 [&](int g, int kk, float num) {
                     const int k = k0 + kk, X = X0 + g;
@@ -372,14 +377,14 @@ struct CellCol : FineCol<DT> {
         // _mask_weights (regridz.py:150-161): area where phalf_c[k0+1] < phalf_f[-1]
         const float w = (this->pc[k] < this->pbot) ? area : 0.0f;
         const float x = nan0(v * w);
-        if (k0 >= ovf_k[fi] || k0 - kcons >= kRing) {
+        if (k0 >= ovf_k[fi] || k0 - kcons >= ring_levels(NF)) {
             if (ovf_k[fi] > k0) {
                 ovf_k[fi] = k0;
                 ovf_lds[fi * 64 + ctx->lane] = k0;
             }
             mine[((int64_t)fi * ctx->km + k0) * ctx->sstride] = x;
         } else {
-            ctx->ring[fi * (kRing * kRingLd) + (k0 % kRing) * kRingLd + ctx->lane] = x;
+            ctx->ring[fi * (ring_levels(NF) * kRingLd) + (k0 % ring_levels(NF)) * kRingLd + ctx->lane] = x;
         }
     }
 
@@ -471,8 +476,8 @@ __global__ __launch_bounds__(64) void regrid_coarsen_cells_kernel(CoarsenArgs<DT
     DT* pc = reinterpret_cast<DT*>(smem);                   // [G][km+1]
     DT* lpb = pc + G * (km + 1);                              // [64] fine surface phalf
     DT* buf = lpb + 64;                                       // [CH][kRingLd] pass-1 staging ...
-    float* ring = reinterpret_cast<float*>(buf);              // ... aliased by the rings [NF][kRing][kRingLd]
-    char* after = reinterpret_cast<char*>(buf) + std::max(sizeof(DT) * CH * kRingLd, sizeof(float) * NF * kRing * kRingLd);
+    float* ring = reinterpret_cast<float*>(buf);              // ... aliased by the rings [NF][ring_levels(NF)][kRingLd]
+    char* after = reinterpret_cast<char*>(buf) + std::max(sizeof(DT) * CH * kRingLd, sizeof(float) * NF * ring_levels(NF) * kRingLd);
     DT* rowd = reinterpret_cast<DT*>(after);                  // [64] row sums (DT)
     float* rowf = reinterpret_cast<float*>(rowd + 64);        // [64] row sums (f32)
     float* lar = rowf + 64;                                   // [64] fine area
@@ -837,11 +842,11 @@ int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* f
         const int CH = std::min(8, 64 / (G * factor));
         const int64_t cblocks = (int64_t)ntile * (ny / factor) * ((nxc + G - 1) / G);
         const size_t lds_c = sizeof(DT) * ((size_t)G * (km + 1) + 64 + 64) +
-                             std::max(sizeof(DT) * CH * kRingLd, sizeof(float) * NF * kRing * kRingLd) +
+                             std::max(sizeof(DT) * CH * kRingLd, sizeof(float) * NF * ring_levels(NF) * kRingLd) +
                              sizeof(float) * (64 * 3 + (size_t)G * km) + sizeof(int) * 64 * NF;
         FV3_REQUIRE(lds_c <= 64 * 1024, "regrid_coarsen: %zu B of LDS needed", lds_c);
         FV3_REQUIRE(cblocks < (int64_t)0x7fffffff, "regrid_coarsen: grid too large");
-        // per-lane overflow columns: only written by lanes that run kRing levels ahead
+        // per-lane overflow columns: only written by lanes that run ring_levels(NF) levels ahead
         if (n_fields > 0)
             FV3_HIP(hipMallocAsync(&scratch, sizeof(float) * NF * (size_t)km * (size_t)cblocks * 64, s));
         a.scratch = (float*)scratch;
