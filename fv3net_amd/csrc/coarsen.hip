@@ -36,6 +36,7 @@
 // divisions dominates).
 #define FV3_HD __host__ __device__
 #include <cstdlib>
+#include <type_traits>
 
 #include "blocks.h"
 #include "common.h"
@@ -446,8 +447,11 @@ __device__ __forceinline__ void cells_field_group(const CoarsenArgs<DT>& a, int 
 
 // FF: the coarsening factor at compile time (8, config #3: all index arithmetic folds),
 // or 0 (runtime a.f)
-template <typename DT, int FF, int NF>
-__global__ __launch_bounds__(64) void regrid_coarsen_cells_kernel(CoarsenArgs<DT> a)
+// WPE: the waves per SIMD its registers are allocated for (the one-field pass on float32
+// delp at 6: 80 VGPRs against 91, a 48-byte spill, see the launch below)
+template <typename DT, int FF, int NF, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void
+regrid_coarsen_cells_kernel(CoarsenArgs<DT> a)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int f = FF ? FF : a.f, km = a.km, ff = f * f;
@@ -851,14 +855,18 @@ int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* f
             FV3_HIP(hipMallocAsync(&scratch, sizeof(float) * NF * (size_t)km * (size_t)cblocks * 64, s));
         a.scratch = (float*)scratch;
         const dim3 grid((unsigned)cblocks), block(64);
+        // register targets: the two-field pass 4 waves per SIMD (118 VGPRs; at 6 it spills
+        // its remap state, 3.4 ms for 4 fields), the one-field pass 6 on float32 delp
+        // (0.756 -> 0.716 ms at C384, profiles/r05zzk_coarsen_wpe_ab.log) and 5 on float64
+        constexpr int W1 = std::is_same<DT, float>::value ? 6 : 5;
         if (factor == 8 && NF == 2)
-            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 8, 2>), grid, block, lds_c, s, a);
+            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 8, 2, 4>), grid, block, lds_c, s, a);
         else if (factor == 8)
-            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 8, 1>), grid, block, lds_c, s, a);
+            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 8, 1, W1>), grid, block, lds_c, s, a);
         else if (NF == 2)
-            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 0, 2>), grid, block, lds_c, s, a);
+            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 0, 2, 4>), grid, block, lds_c, s, a);
         else
-            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 0, 1>), grid, block, lds_c, s, a);
+            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 0, 1, W1>), grid, block, lds_c, s, a);
         FV3_LAUNCH_CHECK();
         if (scratch) FV3_HIP(hipFreeAsync(scratch, s));
         return FV3_OK;
