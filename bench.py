@@ -23,9 +23,13 @@ Rank 0 prints ONE JSON line on stdout (everything else goes to stderr), with
   extra:        other configs measured on the same GPU (N=1, rank 0).
 """
 import argparse
+import hashlib
 import json
 import os
+import re
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -33,6 +37,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+HEADLINE_KERNEL = ("fv3::dense_forward_kernel<2,2,4,2,8,float> (csrc/dense.hip: 8-wave blocks, 32-column tiles, "
+                   "f32 inputs)")
 METRIC = "grid-columns/s ML-physics step (C48 & C384, 79L); HBM GB/s vs gfx950 peak"
 
 
@@ -51,6 +57,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--settle-ms", type=float, default=300.0,
                    help="untimed clock-settle phase before the W warmup steps (see timed_steps)")
+    p.add_argument("--legs-out", default=None, help="write the verbose per-leg records (JSON) here")
+    p.add_argument("--legs-timeout", type=float, default=480.0, help="seconds allowed for the legs' child process")
+    p.add_argument("--legs-only", default=None, help=argparse.SUPPRESS)
     return p.parse_args()
 
 
@@ -123,21 +132,76 @@ def timed_steps(step, steps, warmup, dist=None, settle_ms=0.0):
     return wall, e0.elapsed_time(e1) * 1e-3 / steps
 
 
-def pmc_record(leg):
+# the translation unit that defines each profiled kernel (csrc/); a PMC record carries the
+# hash of that file and every csrc/ header it includes, taken when the counters were
+# published (tools/pmc_publish.py), so a record of a kernel changed since is detectable
+KERNEL_TU = {
+    "dense_forward_kernel": "dense.hip",
+    "dense_b3_kernel": "dense_b3.hip",
+    "mappm_": "mappm.hip",
+    "regrid_coarsen": "coarsen.hip",
+    "ml_epilogue": "stepper.hip",
+    "area_": "reduce.hip",
+    "level_": "reduce.hip",
+    "fold_rows": "reduce.hip",
+}
+
+
+def kernel_sources(kernel):
+    """csrc/ files the kernel's code depends on: its translation unit and the csrc/
+    headers it includes, transitively (the public ABI header is not hashed)."""
+    csrc = os.path.join(ROOT, "fv3net_amd", "csrc")
+    tu = next((f for k, f in KERNEL_TU.items() if kernel.startswith(k)), None)
+    if tu is None:
+        return []
+    seen, todo = [], [tu]
+    while todo:
+        f = todo.pop()
+        if f in seen or not os.path.exists(os.path.join(csrc, f)):
+            continue
+        seen.append(f)
+        with open(os.path.join(csrc, f)) as fh:
+            for line in fh:
+                m = re.match(r'\s*#include\s+"([^"/]+)"', line)
+                if m:
+                    todo.append(m.group(1))
+    return sorted(seen)
+
+
+def kernel_source_hash(kernel):
+    """sha256 (first 16 hex digits) of the kernel's csrc/ sources, or None."""
+    files = kernel_sources(kernel)
+    if not files:
+        return None
+    h = hashlib.sha256()
+    for f in files:
+        h.update(f.encode())
+        with open(os.path.join(ROOT, "fv3net_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_record(leg, path=None):
     """The committed PMC record of a bench leg (profiles/pmc_traffic.json, written by
-    tools/pmc_all.sh + tools/pmc_publish.py), or {}."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    tools/pmc_all.sh + tools/pmc_publish.py), or {}.  ``stale`` is True when the record
+    carries no source hash or one that differs from the tree's sources of its kernel."""
+    path = path or os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get(leg, {})
+            r = dict(json.load(f).get(leg, {}))
     except (OSError, ValueError):
         return {}
+    if r:
+        r["stale"] = r.get("src_hash") is None or r.get("src_hash") != kernel_source_hash(r.get("kernel", ""))
+    return r
 
 
 def pmc_traffic(leg):
     """HBM bytes per launch of the leg's dominant kernel from the committed PMC passes
-    (FETCH_SIZE x calibrated read factor + WRITE_SIZE), or None."""
-    return pmc_record(leg).get("hbm_bytes_per_launch")
+    (FETCH_SIZE x calibrated read factor + WRITE_SIZE), or None when there is no record
+    or the record describes an older version of the kernel's sources."""
+    r = pmc_record(leg)
+    return None if r.get("stale", True) else r.get("hbm_bytes_per_launch")
 
 
 def with_counters(leg, rec, alg_bytes=None):
@@ -147,6 +211,10 @@ def with_counters(leg, rec, alg_bytes=None):
     r = pmc_record(leg)
     if not r:
         rec["traffic"] = None
+        return rec
+    if r["stale"]:  # counters of an older version of the kernel: reported, never as traffic
+        rec["traffic"] = None
+        rec["pmc_stale"] = {"profile": r.get("profile"), "hbm_bytes_per_launch": r.get("hbm_bytes_per_launch")}
         return rec
     rec["traffic"] = r.get("hbm_bytes_per_launch")
     if alg_bytes and rec["traffic"]:
@@ -671,12 +739,12 @@ def reference_mappm_cpu(seconds=5.0):
                       f"(flang -O2, oracle/_ref) in 512-column chunks via ctypes, {dt:.1f} s, 1 core"}
 
 
-def extra_measurements(dev, settle_ms=150.0):
+def extra_measurements(dev, settle_ms=150.0, out=None):
     import torch
 
     from fv3net_amd import workloads as W
 
-    out = {}
+    out = {} if out is None else out
     # config #2 at C384 (one GPU, 884,736 columns): MFMA-bound predict
     wl = W.make_dense_workload(384, seed=3, device=dev)
     wall, t = timed_steps(wl.step, 10, 3, settle_ms=settle_ms)
@@ -697,8 +765,8 @@ def extra_measurements(dev, settle_ms=150.0):
                                          "frac_hbm_peak": gbs / W.HBM_PEAK_GBS}, wl.bytes_per_column * ncol)
         del wl
     try:
-        out["mappm_c384_79to79_kord1"]["cpu_baseline"] = reference_mappm_cpu()
-        out["mappm_c384_79to79_kord1"]["cpu_baseline_8proc"] = reference_mappm_cpu_procs()
+        out["mappm_c384_79to79_kord1"] = dict(out["mappm_c384_79to79_kord1"], cpu_baseline=reference_mappm_cpu(),
+                                              cpu_baseline_8proc=reference_mappm_cpu_procs())
     except Exception as e:  # a report, never fatal
         log("reference mappm cpu baseline failed:", repr(e))
     # config #4: one ML-stepper step (predict + fused limiter/diagnostics/apply + global
@@ -710,7 +778,7 @@ def extra_measurements(dev, settle_ms=150.0):
         "note": "wall clock per step (predict, fused epilogue, area partials: three C-ABI calls marshalled once, "
                 "workloads.StepperWorkload._bind); counters: the fused epilogue kernel"})
     try:
-        out["stepper_c96"]["cpu_baseline"] = stepper_cpu_baseline(wl)
+        out["stepper_c96"] = dict(out["stepper_c96"], cpu_baseline=stepper_cpu_baseline(wl))
     except Exception as e:  # a report, never fatal
         log("stepper cpu baseline failed:", repr(e))
     del wl
@@ -740,7 +808,7 @@ def extra_measurements(dev, settle_ms=150.0):
         out[leg] = with_counters(leg, rec, wl.ncol * wl.bytes_per_column)
         if prec == "bf16x3":
             try:
-                out[leg]["cpu_baseline"] = emulator_cpu_baseline(wl)
+                out[leg] = dict(out[leg], cpu_baseline=emulator_cpu_baseline(wl))
             except Exception as e:  # a report, never fatal
                 log("emulator cpu baseline failed:", repr(e))
         del wl
@@ -775,7 +843,8 @@ def extra_measurements(dev, settle_ms=150.0):
             "frac_hbm_peak": gbs / W.HBM_PEAK_GBS}, wl.bytes_per_column * wl.ncol_fine)
         del wl
     try:
-        out["coarsen_c384_to_c48_1field"]["cpu_baseline"] = coarsen_cpu_baseline()
+        out["coarsen_c384_to_c48_1field"] = dict(out["coarsen_c384_to_c48_1field"],
+                                                 cpu_baseline=coarsen_cpu_baseline())
     except Exception as e:  # a report, never fatal
         log("coarsen cpu baseline failed:", repr(e))
     # host -> host (numpy float64 in, numpy float32 out) beside the device-resident legs
@@ -784,12 +853,145 @@ def extra_measurements(dev, settle_ms=150.0):
     out["dense_c48_rank_call_host_to_host"] = rank_call_host_to_host(dev)
     out["predict_mappm_c384_host_to_host"] = predict_mappm_host_to_host(dev)
     torch.cuda.empty_cache()
-    out.update(rank_share_legs(dev, settle_ms))
+    for k, v in rank_share_legs(dev, settle_ms).items():
+        out[k] = v
     return out
+
+
+LINE_BUDGET = 7500  # characters of the final stdout line (the driver keeps ~8 KB of stdout)
+
+
+class LegRecorder(dict):
+    """The legs' records as they are produced: every assignment is also written as one
+    JSON line to ``path`` (and a ``BENCH_LEG`` line on stderr), so the parent keeps every
+    leg that finished even if a later one takes the child process down."""
+
+    def __init__(self, path):
+        super().__init__()
+        self.path = path
+
+    def __setitem__(self, key, value):
+        super().__setitem__(key, value)
+        self.emit(key, value)
+
+    def emit(self, key, value):
+        line = json.dumps({key: value})
+        with open(self.path, "a") as f:
+            f.write(line + "\n")
+        log("BENCH_LEG", line)
+
+
+def _sig(x, n=4):
+    if isinstance(x, bool) or not isinstance(x, (int, float)):
+        return x
+    return float(f"{x:.{n}g}")
+
+
+def compact_leg(rec):
+    """One leg's record reduced to what the driver line carries: ms, the roofline
+    fraction, the rank-share ratio, traffic over algorithmic bytes, VALU issue fraction,
+    the CPU baseline's value, and whether the counters are fresh."""
+    if not isinstance(rec, dict):
+        return rec
+    out = {}
+    for k in ("ms_per_step", "ms_per_call"):
+        if rec.get(k) is not None:
+            out["ms"] = _sig(rec[k])
+            break
+    for k in ("columns_per_s", "fine_columns_per_s", "columns_per_s_per_gpu"):
+        if rec.get(k) is not None:
+            out["cps"] = _sig(rec[k], 3)
+            break
+    frac = [k for k in rec if k.startswith("frac_") or k.startswith("dense_frac_") or k.startswith("predict_frac_")]
+    if frac:
+        out["frac"] = _sig(rec[frac[0]], 3)
+    for src, dst in (("ratio_to_full_over_world", "ratio"), ("dense_ratio_to_full_over_world", "dense_ratio"),
+                     ("mappm_ratio_to_full_over_world", "mappm_ratio"), ("traffic_over_algorithmic", "tx"),
+                     ("valu_issue_frac", "valu"), ("max_rel_err", "err"), ("bit_identical_to_device_resident", "same")):
+        if rec.get(src) is not None:
+            out[dst] = _sig(rec[src], 3)
+    if rec.get("pmc_profile"):
+        out["pmc"] = rec["pmc_profile"]
+    if rec.get("pmc_stale"):
+        out["pmc"] = f"{rec['pmc_stale'].get('profile')} (stale)"
+    for k in ("cpu_baseline", "cpu_baseline_8proc"):
+        if isinstance(rec.get(k), dict):
+            out["cpu" if k == "cpu_baseline" else "cpu8"] = _sig(rec[k]["value"], 3)
+    if isinstance(rec.get("kernels"), dict):
+        for name, kr in rec["kernels"].items():
+            if isinstance(kr, dict) and kr.get("traffic"):
+                out[f"{name}_traffic"] = _sig(kr["traffic"], 3)
+    return out
+
+
+def compact_line(result):
+    """The driver's line: the contract fields, roofline, cpu_baseline and a terse
+    summary of every leg (the verbose records go to stderr / --legs-out)."""
+    line = {k: v for k, v in result.items() if k not in ("extra", "extra_scaling")}
+    for sec in ("extra_scaling", "extra"):
+        if isinstance(result.get(sec), dict):
+            line[sec] = {k: compact_leg(v) for k, v in result[sec].items()}
+        elif result.get(sec) is not None:
+            line[sec] = result[sec]
+    return json.dumps(line)
+
+
+def run_legs_child(args, timeout):
+    """The world-1 legs (extra_scaling + extra) in a child process: a sticky GPU fault or
+    a hang in any of them cannot take the headline with it.  Returns (scaling, extra)."""
+    fd, path = tempfile.mkstemp(prefix="bench_legs_", suffix=".jsonl")
+    os.close(fd)
+    cmd = [sys.executable, os.path.abspath(__file__), "--legs-only", path, "--settle-ms", str(args.settle_ms)]
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    status = None
+    try:
+        p = subprocess.run(cmd, stdout=sys.stderr, stderr=sys.stderr, timeout=timeout, env=env)
+        if p.returncode != 0:
+            status = f"legs child exited with {p.returncode}"
+    except subprocess.TimeoutExpired:
+        status = f"legs child killed after {timeout} s"
+    legs = {}
+    try:
+        with open(path) as f:
+            for ln in f:
+                legs.update(json.loads(ln))
+    except (OSError, ValueError) as e:
+        status = (status or "") + f"; legs file unreadable: {e!r}"
+    finally:
+        try:
+            os.unlink(path)
+        except OSError:
+            pass
+    scaling = {k[len("scaling/"):]: v for k, v in legs.items() if k.startswith("scaling/")}
+    extra = {k: v for k, v in legs.items() if not k.startswith("scaling/")}
+    if status:
+        log(status)
+        extra["_status"] = status
+    return scaling, extra
+
+
+def legs_only(args):
+    """Child mode: run every world-1 leg, recording each as it finishes."""
+    import torch
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    rec = LegRecorder(args.legs_only)
+    settle = min(args.settle_ms, 150.0)
+    try:
+        for k, v in scaling_legs(dev, None, 0, 1, settle_ms=settle).items():
+            rec["scaling/" + k] = v
+    except Exception as e:
+        log("scaling legs failed:", repr(e))
+    extra_measurements(dev, settle_ms=settle, out=rec)
 
 
 def main():
     args = parse()
+    if args.legs_only:
+        return legs_only(args)
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -817,6 +1019,7 @@ def main():
     value = total_cols / wall
     flops_launch = wl.ncol * wl.flops_per_column
     achieved = flops_launch / kmean / 1e12
+    pmc = pmc_record("dense_c48")
 
     result = {
         "metric": METRIC,
@@ -841,13 +1044,14 @@ def main():
             "parallelism": f"columns sharded, 1 process/GPU x {world}",
         },
         "roofline": {
-            "kernel": "fv3::dense_forward_kernel<2,2,4,2,8,float> (csrc/dense.hip: 8-wave blocks, 32-column tiles, f32 inputs)",
+            "kernel": HEADLINE_KERNEL,
             "bound": "mfma",
             "achieved": achieved,
             "peak": W.FP32_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved / W.FP32_MFMA_PEAK_TFLOPS,
             "traffic": pmc_traffic("dense_c48"),
+            "traffic_profile": pmc.get("profile") if not pmc.get("stale", True) else None,
             "algorithmic_flop_per_launch": flops_launch,
             "algorithmic_bytes_per_launch": wl.ncol * wl.bytes_per_column,
             "mean_launch_us": kmean * 1e6,
@@ -859,20 +1063,29 @@ def main():
             result["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds)
         except Exception as e:  # the baseline is a report, never fatal
             log("cpu_baseline failed:", repr(e))
+    del wl
+    torch.cuda.empty_cache()
+    if rank == 0:  # the headline alone, on stderr, before any leg runs
+        log("BENCH_HEADLINE", compact_line(result))
     if not args.no_extra:
-        del wl
-        torch.cuda.empty_cache()
-        try:  # every rank takes part: one global problem sharded over the ranks
-            result["extra_scaling"] = scaling_legs(dev, dist, rank, world, settle_ms=min(args.settle_ms, 150.0))
-        except Exception as e:
-            log("scaling legs failed:", repr(e))
-    if rank == 0 and world == 1 and not args.no_extra:
-        try:
-            result["extra"] = extra_measurements(dev, settle_ms=min(args.settle_ms, 150.0))
-        except Exception as e:
-            log("extra measurements failed:", repr(e))
+        if world == 1:
+            result["extra_scaling"], result["extra"] = run_legs_child(args, args.legs_timeout)
+        else:
+            try:  # every rank takes part: one global problem sharded over the ranks
+                result["extra_scaling"] = scaling_legs(dev, dist, rank, world,
+                                                       settle_ms=min(args.settle_ms, 150.0))
+            except Exception as e:
+                log("scaling legs failed:", repr(e))
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        if args.legs_out:
+            with open(args.legs_out, "w") as f:
+                json.dump(result, f)
+        line = compact_line(result)
+        if len(line) > LINE_BUDGET:  # never let the legs cost the headline its parse
+            log(f"compact line {len(line)} chars > {LINE_BUDGET}: dropping the per-leg summary")
+            result = {k: v for k, v in result.items() if k not in ("extra", "extra_scaling")}
+            line = compact_line(result)
+        print(line, flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

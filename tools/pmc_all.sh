@@ -16,6 +16,11 @@ if [ ! -f tools/variants/libcalib.so ]; then
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 -o tools/variants/libcalib.so tools/calib.hip
 fi
 mkdir -p "$OUT"; export TMPDIR=/tmp
+# the sources each profiled kernel was built from (bench.kernel_source_hash)
+python3 -c "import json, bench; print(json.dumps({k: bench.kernel_source_hash(k) for k in
+  ['dense_forward_kernel', 'dense_b3_kernel', 'mappm_ppm_kernel', 'mappm_cs_global_kernel', 'mappm_ppm_levels_kernel',
+   'mappm_ppm_pair_kernel', 'mappm_ppm_pair_split_kernel', 'regrid_coarsen_cells_kernel', 'ml_epilogue_kernel',
+   'ml_epilogue_levels_kernel']}))" > "$OUT/src_hashes.json"
 SETS=("FETCH_SIZE"
       "WRITE_SIZE"
       "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE"

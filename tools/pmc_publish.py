@@ -18,6 +18,8 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
 
 # bench leg -> (pmc_drive leg, dominant kernel short name)
 LEGS = {
@@ -75,6 +77,11 @@ def main(src, tag):
             traffic = json.load(f)
     except (OSError, ValueError):
         traffic = {}
+    try:
+        with open(os.path.join(src, "src_hashes.json")) as f:
+            hashes = json.load(f)
+    except (OSError, ValueError):
+        hashes = {}
     for bench_leg, (leg, kernel) in LEGS.items():
         ks = s["legs"].get(leg)
         if not ks:
@@ -92,6 +99,9 @@ def main(src, tag):
             "valu_busy_pct": e.get("VALUBusy"),
             "valu_utilization_pct": e.get("VALUUtilization"),
             "profile": tag,
+            # the kernel's sources as they were when the counters ran (pmc_all.sh writes
+            # src_hashes.json on the box); bench.with_counters marks a mismatch stale
+            "src_hash": hashes.get(kernel) or bench.kernel_source_hash(kernel),
         }
         if e.get("valu_issue_cu_cycles") is not None:
             # issue floor: the mix at the measured per-class peaks (tools/valu_calib.py)
