@@ -755,10 +755,13 @@ def extra_measurements(dev, settle_ms=150.0, out=None):
     }, wl.ncol * wl.bytes_per_column)
     del wl
     # mappm: config #3 fine columns (C384 79->79) and config #1 (C12 79->50)
-    for name, ncol, kn, kord in (("mappm_c384_79to79_kord1", W.c_columns(384), 79, 1),
-                                 ("mappm_c384_79to79_kord10", W.c_columns(384), 79, 10),
-                                 ("mappm_c12_79to50_kord1", W.c_columns(12), 50, 1)):
-        wl = W.make_mappm_workload(ncol, 79, kn, kord, seed=5, device=dev)
+    # the default (tolerance-contract) arithmetic, and the bit-exact one beside it (_exact)
+    for name, ncol, kn, kord, exact in (("mappm_c384_79to79_kord1", W.c_columns(384), 79, 1, False),
+                                        ("mappm_c384_79to79_kord1_exact", W.c_columns(384), 79, 1, True),
+                                        ("mappm_c384_79to79_kord10", W.c_columns(384), 79, 10, False),
+                                        ("mappm_c384_79to79_kord10_exact", W.c_columns(384), 79, 10, True),
+                                        ("mappm_c12_79to50_kord1", W.c_columns(12), 50, 1, False)):
+        wl = W.make_mappm_workload(ncol, 79, kn, kord, seed=5, device=dev, exact=exact)
         wall, t = timed_steps(wl.step, 10, 3, settle_ms=settle_ms)
         gbs = wl.bytes_per_column * ncol / t / 1e9
         out[name] = with_counters(name, {"columns_per_s": ncol / t, "ms_per_step": t * 1e3, "hbm_gbs": gbs,
@@ -833,11 +836,11 @@ def extra_measurements(dev, settle_ms=150.0, out=None):
             "tflops_f32_equiv_over_f32_peak": tf / W.FP32_MFMA_PEAK_TFLOPS}, wl.ncol * wl.bytes_per_column)
         del wl
     # config #3: fused C384 -> C48 pressure-level coarsen (1 and 4 fields), fine columns/s
-    for nf in (1, 4):
-        wl = W.make_coarsen_workload(384, 8, nf, seed=7, device=dev)
+    for nf, exact in ((1, False), (4, False), (1, True), (4, True)):
+        wl = W.make_coarsen_workload(384, 8, nf, seed=7, device=dev, exact=exact)
         wall, t = timed_steps(wl.step, 10, 3, settle_ms=settle_ms)
         gbs = wl.bytes_per_column * wl.ncol_fine / t / 1e9
-        leg = f"coarsen_c384_to_c48_{nf}field"
+        leg = f"coarsen_c384_to_c48_{nf}field" + ("_exact" if exact else "")
         out[leg] = with_counters(leg, {
             "fine_columns_per_s": wl.ncol_fine / t, "ms_per_step": t * 1e3, "hbm_gbs": gbs,
             "frac_hbm_peak": gbs / W.HBM_PEAK_GBS}, wl.bytes_per_column * wl.ncol_fine)

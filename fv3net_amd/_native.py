@@ -88,7 +88,14 @@ EXPORTED_SYMBOLS = (
     "fv3_sum_squares",
     "fv3_cos_zenith",
 )
-ABI_VERSION = 10
+ABI_VERSION = 11
+# the remap arithmetic of fv3_mappm_ex / _multi and the fused coarsen entries
+ARITH_EXACT = 0  # bit-identical to the reference build (mappm.f90 under flang)
+ARITH_FAST = 1   # north_star's 1e-5 rel contract: reciprocal divisions, FMA, hardware MAX / MIN
+
+
+def arith(exact: bool) -> int:
+    return ARITH_EXACT if exact else ARITH_FAST
 
 # fv3_dense_forward_ex precisions
 DENSE_F32 = 0
@@ -215,9 +222,9 @@ _SIGNATURES = {
     "fv3_abi_version": (_I, []),
     "fv3_build_kind": (ctypes.c_char_p, []),
     "fv3_mappm": (_I, [_P, _P, _P, _P, _I64, _I, _I, _I, _I, _F, _P]),
-    "fv3_mappm_ex": (_I, [_P, Layout, _P, Layout, _P, Layout, _P, Layout, _I64, _I, _I, _I, _I, _F, _P]),
+    "fv3_mappm_ex": (_I, [_P, Layout, _P, Layout, _P, Layout, _P, Layout, _I64, _I, _I, _I, _I, _F, _I, _P]),
     "fv3_mappm_multi": (_I, [_P, Layout, ctypes.POINTER(_P), ctypes.POINTER(Layout), _P, Layout, ctypes.POINTER(_P),
-                             ctypes.POINTER(Layout), _I, _I64, _I, _I, _I, _I, _F, _P]),
+                             ctypes.POINTER(Layout), _I, _I64, _I, _I, _I, _I, _F, _I, _P]),
     "fv3_dense_create": (_I, [ctypes.POINTER(DenseDesc), ctypes.POINTER(_P)]),
     "fv3_dense_destroy": (_I, [_P]),
     "fv3_dense_set_trace": (_I, [_P, _P]),
@@ -230,19 +237,19 @@ _SIGNATURES = {
     "fv3_dense_forward_ex": (_I, [_P, ctypes.POINTER(_P), ctypes.POINTER(Layout), ctypes.POINTER(_P),
                                   ctypes.POINTER(Layout), _I64, _I, _P]),
     "fv3_regrid_coarsen": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _P, _I, _I, _I,
-                                _I, _I, _I, _I, _D, _P]),
+                                _I, _I, _I, _I, _D, _I, _P]),
     "fv3_regrid_coarsen_f64": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _P, _I, _I, _I,
-                                    _I, _I, _I, _I, _D, _P]),
+                                    _I, _I, _I, _I, _D, _I, _P]),
     "fv3_regrid_coarsen_f64d": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _P, _I, _I, _I,
-                                     _I, _I, _I, _I, _D, _P]),
+                                     _I, _I, _I, _I, _D, _I, _P]),
     "fv3_weighted_block_average": (_I, [ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _P, _I, _I, _I, _I, _I, _P]),
     "fv3_weighted_block_average_f64": (_I, [ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _P, _I, _I, _I, _I, _I,
                                             _P]),
     "fv3_hydrostatic_balance": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _D, _P]),
     "fv3_regrid_coarsen_edge": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _I, _I, _I, _I,
-                                     _I, _I, _I, _I, _D, _P]),
+                                     _I, _I, _I, _I, _D, _I, _P]),
     "fv3_regrid_coarsen_edge_f64": (_I, [_P, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _I, _I, _I, _I,
-                                         _I, _I, _I, _I, _D, _P]),
+                                         _I, _I, _I, _I, _D, _I, _P]),
     "fv3_interpolate_2d": (_I, [_P, _I64, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _I, _D, _P]),
     "fv3_interpolate_levels": (_I, [_P, _I64, _P, _I64, _I, _P, _I, _I, _P, _I64, _I64, _I, _D, _P]),
     "fv3_pressure_midpoint_log": (_I, [_P, _I, _I64, _P, _I64, _I64, _I, _D, _P]),

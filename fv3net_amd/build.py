@@ -56,9 +56,15 @@ def _read(p):
         return f.read()
 
 
+_INC_HIP = re.compile(rb'#include\s+"([^"/]+\.hip)"')
+
+
 def _obj_digest(src, hdr_blob):
     h = hashlib.sha256()
     h.update(_read(src) + hdr_blob + " ".join(CFLAGS).encode())
+    # a *_fast.hip unit includes its exact sibling's source (csrc/mappm_fast.hip)
+    for inc in _INC_HIP.findall(_read(src)):
+        h.update(_read(os.path.join(CSRC, inc.decode())))
     return h.hexdigest()[:20]
 
 

@@ -108,8 +108,10 @@ struct FineCol {
         while (next < k - 1) {  // interface k-1 (0-based) = ptop + sum delp[0..k-2]
             run = run + dl;
             ++next;
-            dnx += plane;
-            if (next < km) dl = *dnx;
+            // unconditional (the last level re-read past the end): no phi on the loaded
+            // value, so its wait stays at the next call's use instead of right here
+            if (next < km) dnx += plane;
+            dl = *dnx;
         }
         return (float)run;
     }
@@ -407,7 +409,7 @@ __device__ __forceinline__ void cells_field_group(const CoarsenArgs<DT>& a, int 
                                                   int Y, int X0, int nxc, int64_t cplane, const DT* pc,
                                                   const DT* pcg, const float* den, float* ring, int* ovf,
                                                   float* rowf, int64_t off, const DT* dp, int64_t plane, DT ptop,
-                                                  DT pbot, float area, bool active)
+                                                  DT pbot, float area, bool active, int iv, int kord)
 {
     const int km = a.km;
     const int64_t sstride = (int64_t)gridDim.x * 64;
@@ -437,9 +439,9 @@ __device__ __forceinline__ void cells_field_group(const CoarsenArgs<DT>& a, int 
     col.mine = a.scratch + (int64_t)blockIdx.x * 64 + lane;
     if constexpr (NF == 1) {
         FirstField<CellCol<DT, FF, NF>> one{col};
-        mappm_ppm_column(one, km, km, a.iv, a.kord);
+        mappm_ppm_column(one, km, km, iv, kord);
     } else {
-        mappm_ppm_columns<NF>(col, km, km, a.iv, a.kord);
+        mappm_ppm_columns<NF>(col, km, km, iv, kord);
     }
     __syncthreads();
     for (int k0 = col.kcons; k0 < km; k0 += nb) ctx.consume(k0, min(nb, km - k0));
@@ -449,7 +451,8 @@ __device__ __forceinline__ void cells_field_group(const CoarsenArgs<DT>& a, int 
 // or 0 (runtime a.f)
 // WPE: the waves per SIMD its registers are allocated for (the one-field pass on float32
 // delp at 6: 80 VGPRs against 91, a 48-byte spill, see the launch below)
-template <typename DT, int FF, int NF, int WPE>
+// K1: kord 1 and iv 1 (the reference's default, regridz.py:25) at compile time
+template <typename DT, int FF, int NF, int WPE, bool K1>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void
 regrid_coarsen_cells_kernel(CoarsenArgs<DT> a)
 {
@@ -560,14 +563,15 @@ regrid_coarsen_cells_kernel(CoarsenArgs<DT> a)
 
     // ---- per group of NF fields: stream the remap, sum finished levels per cell ----
     const int64_t off = (int64_t)tile * km * plane + fine;
+    const int iv = K1 ? 1 : a.iv, kord = K1 ? 1 : a.kord;
     int v0 = 0;
     for (; v0 + NF <= a.n_fields; v0 += NF)
         cells_field_group<NF, DT, FF>(a, v0, lane, f, CH, tile, Y, X0, nxc, cplane, pc, pc + gg * (km + 1), den,
-                                      ring, ovf, rowf, off, dp, plane, ptop, pbot, area, active);
+                                      ring, ovf, rowf, off, dp, plane, ptop, pbot, area, active, iv, kord);
     if constexpr (NF > 1) {
         for (; v0 < a.n_fields; ++v0)
             cells_field_group<1, DT, FF>(a, v0, lane, f, CH, tile, Y, X0, nxc, cplane, pc, pc + gg * (km + 1), den,
-                                         ring, ovf, rowf, off, dp, plane, ptop, pbot, area, active);
+                                         ring, ovf, rowf, off, dp, plane, ptop, pbot, area, active, iv, kord);
     }
 }
 
@@ -779,6 +783,8 @@ __global__ __launch_bounds__(64) void regrid_coarsen_edge_kernel(EdgeArgs<DT> a)
 
 }  // namespace
 
+namespace FV3_ARITH_NS {
+
 template <typename DT>
 int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* fields, float* const* out,
                         int n_fields, float* delp_out, double* delp_out64, int ntile, int km, int ny, int nx,
@@ -859,14 +865,17 @@ int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* f
         // its remap state, 3.4 ms for 4 fields), the one-field pass 6 on float32 delp
         // (0.756 -> 0.716 ms at C384, profiles/r05zzk_coarsen_wpe_ab.log) and 5 on float64
         constexpr int W1 = std::is_same<DT, float>::value ? 6 : 5;
+        const bool k1 = iv == 1 && kord == 1;
         if (factor == 8 && NF == 2)
-            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 8, 2, 4>), grid, block, lds_c, s, a);
+            hipLaunchKernelGGL((k1 ? regrid_coarsen_cells_kernel<DT, 8, 2, 4, true>
+                                  : regrid_coarsen_cells_kernel<DT, 8, 2, 4, false>), grid, block, lds_c, s, a);
         else if (factor == 8)
-            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 8, 1, W1>), grid, block, lds_c, s, a);
+            hipLaunchKernelGGL((k1 ? regrid_coarsen_cells_kernel<DT, 8, 1, W1, true>
+                                  : regrid_coarsen_cells_kernel<DT, 8, 1, W1, false>), grid, block, lds_c, s, a);
         else if (NF == 2)
-            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 0, 2, 4>), grid, block, lds_c, s, a);
+            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 0, 2, 4, false>), grid, block, lds_c, s, a);
         else
-            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 0, 1, W1>), grid, block, lds_c, s, a);
+            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 0, 1, W1, false>), grid, block, lds_c, s, a);
         FV3_LAUNCH_CHECK();
         if (scratch) FV3_HIP(hipFreeAsync(scratch, s));
         return FV3_OK;
@@ -882,10 +891,6 @@ int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* f
     if (scratch) FV3_HIP(hipFreeAsync(scratch, s));
     return FV3_OK;
 }
-
-}  // namespace fv3
-
-namespace fv3 {
 
 template <typename DT>
 int regrid_coarsen_edge_impl(const DT* delp, const float* spacing, const float* const* fields, float* const* out,
@@ -947,44 +952,111 @@ int regrid_coarsen_edge_impl(const DT* delp, const float* spacing, const float* 
     return FV3_OK;
 }
 
+// explicit instantiations: the C ABI below (exact unit) calls the fast unit's
+template int regrid_coarsen_impl<float>(const float*, const float*, const float* const*, float* const*, int, float*,
+                                        double*, int, int, int, int, int, int, int, double, void*);
+template int regrid_coarsen_impl<double>(const double*, const float*, const float* const*, float* const*, int,
+                                         float*, double*, int, int, int, int, int, int, int, double, void*);
+template int regrid_coarsen_edge_impl<float>(const float*, const float*, const float* const*, float* const*, int,
+                                             int, int, int, int, int, int, int, int, double, void*);
+template int regrid_coarsen_edge_impl<double>(const double*, const float*, const float* const*, float* const*,
+                                              int, int, int, int, int, int, int, int, int, double, void*);
+
+}  // namespace FV3_ARITH_NS
+
+#ifndef FV3_FAST_ARITH
+namespace fast {  // coarsen_fast.hip
+template <typename DT>
+int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* fields, float* const* out,
+                        int n_fields, float* delp_out, double* delp_out64, int ntile, int km, int ny, int nx,
+                        int factor, int iv, int kord, double ptop_toa, void* stream);
+template <typename DT>
+int regrid_coarsen_edge_impl(const DT* delp, const float* spacing, const float* const* fields, float* const* out,
+                             int n_fields, int ntile, int km, int ny, int nx, int factor, int edge, int iv, int kord,
+                             double ptop_toa, void* stream);
+extern template int regrid_coarsen_impl<float>(const float*, const float*, const float* const*, float* const*, int,
+                                               float*, double*, int, int, int, int, int, int, int, double, void*);
+extern template int regrid_coarsen_impl<double>(const double*, const float*, const float* const*, float* const*,
+                                                int, float*, double*, int, int, int, int, int, int, int, double,
+                                                void*);
+extern template int regrid_coarsen_edge_impl<float>(const float*, const float*, const float* const*,
+                                                    float* const*, int, int, int, int, int, int, int, int, int,
+                                                    double, void*);
+extern template int regrid_coarsen_edge_impl<double>(const double*, const float*, const float* const*,
+                                                     float* const*, int, int, int, int, int, int, int, int, int,
+                                                     double, void*);
+}  // namespace fast
+#endif
+
 }  // namespace fv3
+
+#ifndef FV3_FAST_ARITH  // the C ABI: one definition, dispatching on the arithmetic
+namespace {
+template <typename DT>
+int coarsen_arith(int arith, const DT* delp, const float* area, const float* const* fields, float* const* out,
+                  int n_fields, float* delp_out, double* delp_out64, int ntile, int km, int ny, int nx, int factor,
+                  int iv, int kord, double ptop_toa, void* stream)
+{
+    fv3::clear_error();
+    FV3_REQUIRE(arith == FV3_ARITH_EXACT || arith == FV3_ARITH_FAST, "regrid_coarsen: unknown arithmetic %d", arith);
+    auto f = arith == FV3_ARITH_FAST ? fv3::fast::regrid_coarsen_impl<DT> : fv3::exact::regrid_coarsen_impl<DT>;
+    return f(delp, area, fields, out, n_fields, delp_out, delp_out64, ntile, km, ny, nx, factor, iv, kord, ptop_toa,
+             stream);
+}
+template <typename DT>
+int coarsen_edge_arith(int arith, const DT* delp, const float* spacing, const float* const* fields, float* const* out,
+                       int n_fields, int ntile, int km, int ny, int nx, int factor, int edge, int iv, int kord,
+                       double ptop_toa, void* stream)
+{
+    fv3::clear_error();
+    FV3_REQUIRE(arith == FV3_ARITH_EXACT || arith == FV3_ARITH_FAST, "regrid_coarsen_edge: unknown arithmetic %d",
+                arith);
+    auto f = arith == FV3_ARITH_FAST ? fv3::fast::regrid_coarsen_edge_impl<DT>
+                                     : fv3::exact::regrid_coarsen_edge_impl<DT>;
+    return f(delp, spacing, fields, out, n_fields, ntile, km, ny, nx, factor, edge, iv, kord, ptop_toa, stream);
+}
+}  // namespace
 
 extern "C" int fv3_regrid_coarsen_edge(const float* delp, const float* spacing, const float* const* fields,
                                        float* const* out, int n_fields, int ntile, int km, int ny, int nx,
-                                       int factor, int edge, int iv, int kord, double ptop_toa, void* stream)
+                                       int factor, int edge, int iv, int kord, double ptop_toa, int arith,
+                                       void* stream)
 {
-    return fv3::regrid_coarsen_edge_impl<float>(delp, spacing, fields, out, n_fields, ntile, km, ny, nx, factor,
-                                                edge, iv, kord, ptop_toa, stream);
+    return coarsen_edge_arith<float>(arith, delp, spacing, fields, out, n_fields, ntile, km, ny, nx, factor, edge,
+                                     iv, kord, ptop_toa, stream);
 }
 
 extern "C" int fv3_regrid_coarsen_edge_f64(const double* delp, const float* spacing, const float* const* fields,
                                            float* const* out, int n_fields, int ntile, int km, int ny, int nx,
-                                           int factor, int edge, int iv, int kord, double ptop_toa, void* stream)
+                                           int factor, int edge, int iv, int kord, double ptop_toa, int arith,
+                                           void* stream)
 {
-    return fv3::regrid_coarsen_edge_impl<double>(delp, spacing, fields, out, n_fields, ntile, km, ny, nx, factor,
-                                                 edge, iv, kord, ptop_toa, stream);
+    return coarsen_edge_arith<double>(arith, delp, spacing, fields, out, n_fields, ntile, km, ny, nx, factor, edge,
+                                      iv, kord, ptop_toa, stream);
 }
 
 extern "C" int fv3_regrid_coarsen(const float* delp, const float* area, const float* const* fields,
                                   float* const* out, int n_fields, float* delp_out, int ntile, int km, int ny,
-                                  int nx, int factor, int iv, int kord, double ptop_toa, void* stream)
+                                  int nx, int factor, int iv, int kord, double ptop_toa, int arith, void* stream)
 {
-    return fv3::regrid_coarsen_impl<float>(delp, area, fields, out, n_fields, delp_out, nullptr, ntile, km, ny, nx,
-                                           factor, iv, kord, ptop_toa, stream);
+    return coarsen_arith<float>(arith, delp, area, fields, out, n_fields, delp_out, nullptr, ntile, km, ny, nx,
+                                factor, iv, kord, ptop_toa, stream);
 }
 
 extern "C" int fv3_regrid_coarsen_f64(const double* delp, const float* area, const float* const* fields,
                                       float* const* out, int n_fields, float* delp_out, int ntile, int km, int ny,
-                                      int nx, int factor, int iv, int kord, double ptop_toa, void* stream)
+                                      int nx, int factor, int iv, int kord, double ptop_toa, int arith, void* stream)
 {
-    return fv3::regrid_coarsen_impl<double>(delp, area, fields, out, n_fields, delp_out, nullptr, ntile, km, ny, nx,
-                                            factor, iv, kord, ptop_toa, stream);
+    return coarsen_arith<double>(arith, delp, area, fields, out, n_fields, delp_out, nullptr, ntile, km, ny, nx,
+                                 factor, iv, kord, ptop_toa, stream);
 }
 
 extern "C" int fv3_regrid_coarsen_f64d(const double* delp, const float* area, const float* const* fields,
                                        float* const* out, int n_fields, double* delp_out, int ntile, int km, int ny,
-                                       int nx, int factor, int iv, int kord, double ptop_toa, void* stream)
+                                       int nx, int factor, int iv, int kord, double ptop_toa, int arith,
+                                       void* stream)
 {
-    return fv3::regrid_coarsen_impl<double>(delp, area, fields, out, n_fields, nullptr, delp_out, ntile, km, ny, nx,
-                                            factor, iv, kord, ptop_toa, stream);
+    return coarsen_arith<double>(arith, delp, area, fields, out, n_fields, nullptr, delp_out, ntile, km, ny, nx,
+                                 factor, iv, kord, ptop_toa, stream);
 }
+#endif  // FV3_FAST_ARITH

@@ -26,7 +26,7 @@ const char* variant_env(const char* name)
 }  // namespace fv3
 
 extern "C" const char* fv3_last_error(void) { return g_err; }
-extern "C" int fv3_abi_version(void) { return 10; }
+extern "C" int fv3_abi_version(void) { return 11; }
 
 // "product": built by fv3net_amd/build.py with FV3_PRODUCT_BUILD and no experiment knob
 // (common.h refuses one); anything else is a tools/ variant.

@@ -21,6 +21,42 @@
 #include <cstdlib>
 
 namespace fv3 {
+
+// launch arguments, shared by the exact and the fast-arithmetic translation units
+// (mappm.hip, mappm_fast.hip: the same kernels under mappm_core.h's two policies)
+struct MappmArgs {
+    const float* pe1;
+    const float* q1;
+    const float* pe2;
+    float* q2;
+    fv3_layout l_pe1, l_q1, l_pe2, l_q2;
+    int64_t ncol;
+    int km, kn, iv, kord;
+    float* scratch;  // kord > 7: [2][km+3][grid * block] (NULL: the LDS path)
+};
+
+struct MappmPairArgs {
+    const float* pe1;
+    const float* pe2;
+    fv3_layout l_pe1, l_pe2;
+    const float* q1[2];
+    float* q2[2];
+    fv3_layout l_q1[2], l_q2[2];
+    int64_t ncol;
+    int km, kn, iv, kord;
+};
+
+namespace FV3_ARITH_NS {
+int launch_mappm(MappmArgs a, hipStream_t stream);
+int launch_mappm_pairs(const MappmPairArgs& a, hipStream_t stream);
+}  // namespace FV3_ARITH_NS
+#ifndef FV3_FAST_ARITH
+namespace fast {  // mappm_fast.hip
+int launch_mappm(MappmArgs a, hipStream_t stream);
+int launch_mappm_pairs(const MappmPairArgs& a, hipStream_t stream);
+}  // namespace fast
+#endif
+
 namespace {
 
 // The remap consumer emits q2(k) for k = 1, 2, ... and asks for next_edge(k) for
@@ -151,17 +187,6 @@ struct GlobalScr {
     __device__ __forceinline__ float& g(int k) { return base[plane + k * stride]; }
 };
 
-struct MappmArgs {
-    const float* pe1;
-    const float* q1;
-    const float* pe2;
-    float* q2;
-    fv3_layout l_pe1, l_q1, l_pe2, l_q2;
-    int64_t ncol;
-    int km, kn, iv, kord;
-    float* scratch;  // kord > 7: [2][km+3][grid * block] (NULL: the LDS path)
-};
-
 __device__ __forceinline__ DevCol make_col(const MappmArgs& a, int64_t c)
 {
     DevCol d;
@@ -179,13 +204,18 @@ __device__ __forceinline__ DevCol make_col(const MappmArgs& a, int64_t c)
     return d;
 }
 
+// K1: kord 1 and iv 1 (the default of regrid_vertical and of the pressure-level coarsen)
+// as compile-time constants, so every branch of mappm.f90 on kord / iv folds away
+template <bool K1>
 __global__ __launch_bounds__(256) void mappm_ppm_kernel(MappmArgs a)
 {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= a.ncol) return;
     DevCol col = make_col(a, c);
-    mappm_ppm_column<DevCol, true, true>(col, a.km, a.kn, a.iv, a.kord);
+    mappm_ppm_column<DevCol, true, true>(col, a.km, a.kn, K1 ? 1 : a.iv, K1 ? 1 : a.kord);
 }
+
+bool is_k1(int iv, int kord) { return iv == 1 && kord == 1; }
 
 // tools/mappm_small_time.py, kord 1 79->79: C48 (13,824 columns) 142 -> 38 us, C96
 // (55,296) 168 -> 118 us; at C384 the serial kernel (0.70 ms) wins.
@@ -254,46 +284,16 @@ __global__ __launch_bounds__(128) void mappm_ppm_levels_kernel(MappmArgs a)
         al[m] = ppm_al(dp[m - 2], dp[m - 1], dp[m], dp[m + 1], q[m - 1], q[m], dc[m - 1], dc[m]);
     __syncthreads();
     if (tid == 0) {  // top: area-preserving cubic (mappm.f90:689-725), as in mappm_ppm_column
-        const float d1 = dp[1], d2 = dp[2];
-        const float q1 = q[1], q2 = q[2];
-        const float qm = (d2 * q1 + d1 * q2) / (d1 + d2);
-        const float dq = 2.0f * (q2 - q1) / (d1 + d2);
-        const float c1 = 4.0f * (al[3] - qm - d2 * dq) / (d2 * (2.0f * d2 * d2 + d1 * (d2 + 3.0f * d1)));
-        const float c3 = dq - 0.5f * c1 * (d2 * (5.0f * d1 + d2) - 3.0f * d1 * d1);
-        float al2 = qm - 0.25f * c1 * d1 * d2 * (d2 + 3.0f * d1);
-        float al1 = d1 * (2.0f * c1 * (d1 * d1) - c3) + al2;
-        al2 = fmax2(al2, fmin2(q1, q2));
-        al2 = fmin2(al2, fmax2(q1, q2));
-        dc[1] = 0.5f * (al2 - q1);
-        if (iv == 0) {
-            al1 = fmax2(0.0f, al1);
-            al2 = fmax2(0.0f, al2);
-        } else if (iv == -1) {
-            if (al1 * q1 <= 0.0f) al1 = 0.0f;
-        } else if (iv == 2 || iv == -2) {
-            al1 = q1;
-        }
+        float al1, al2, dc1;
+        ppm_top_cubic(q[1], q[2], dp[1], dp[2], al[3], iv, al1, al2, dc1);
+        dc[1] = dc1;
         al[1] = al1;
         al[2] = al2;
     }
     if (tid == (1 % nt)) {  // bottom: area-preserving cubic (mappm.f90:729-761)
-        const float d1 = dp[km], d2 = dp[km - 1];
-        const float qk = q[km], qk1 = q[km - 1];
-        const float qm = (d2 * qk + d1 * qk1) / (d1 + d2);
-        const float dq = 2.0f * (qk1 - qk) / (d1 + d2);
-        const float c1 = (al[km - 1] - qm - d2 * dq) / (d2 * (2.0f * d2 * d2 + d1 * (d2 + 3.0f * d1)));
-        const float c3 = dq - 2.0f * c1 * (d2 * (5.0f * d1 + d2) - 3.0f * d1 * d1);
-        float alm = qm - c1 * d1 * d2 * (d2 + 3.0f * d1);
-        float ar = d1 * (8.0f * c1 * (d1 * d1) - c3) + alm;
-        alm = fmax2(alm, fmin2(qk, qk1));
-        alm = fmin2(alm, fmax2(qk, qk1));
-        dc[km] = 0.5f * (qk - alm);
-        if (iv == 0) {
-            alm = fmax2(0.0f, alm);
-            ar = fmax2(0.0f, ar);
-        } else if (iv < 0) {
-            if (qk * ar <= 0.0f) ar = 0.0f;
-        }
+        float alm, ar, dcm;
+        ppm_bottom_cubic(q[km], q[km - 1], dp[km], dp[km - 1], al[km - 1], iv, alm, ar, dcm);
+        dc[km] = dcm;
         al[km] = alm;
         al[km + 1] = ar;
     }
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(128) void mappm_ppm_levels_kernel(MappmArgs a)
                     s.qsum = s.qsum + delp * ends.q_bot;
                     s.dpsum = s.dpsum + delp;
                 }
-                val = s.qsum / s.dpsum;
+                val = FV3_DIVQ(s.qsum, s.dpsum);
             }
         } else {
             val = (s.t <= ends.pe_top) ? ends.q_top : ends.q_bot;
@@ -457,6 +457,8 @@ const void* cs_global_kernel(const MappmArgs& a, int64_t nlanes)
 
 }  // namespace
 
+namespace FV3_ARITH_NS {
+
 // kord <= 7: the level-parallel kernel while one lane per column leaves the chip
 // mostly idle (FV3_MAPPM_PATH=serial|levels overrides, for tests and A/B).
 bool use_levels_kernel(const MappmArgs& a, int64_t max_cols = kLevelsMaxCols)
@@ -508,24 +510,16 @@ int launch_mappm(MappmArgs a, hipStream_t stream)
     } else {
         const int block = 256;
         const int64_t grid = (a.ncol + block - 1) / block;
-        hipLaunchKernelGGL(mappm_ppm_kernel, dim3((unsigned)grid), dim3(block), 0, stream, a);
+        if (is_k1(a.iv, a.kord))
+            hipLaunchKernelGGL(mappm_ppm_kernel<true>, dim3((unsigned)grid), dim3(block), 0, stream, a);
+        else
+            hipLaunchKernelGGL(mappm_ppm_kernel<false>, dim3((unsigned)grid), dim3(block), 0, stream, a);
     }
     FV3_LAUNCH_CHECK();
     return FV3_OK;
 }
 
 // ---- two fields on one column's edges (fv3_mappm_multi) ----
-
-struct MappmPairArgs {
-    const float* pe1;
-    const float* pe2;
-    fv3_layout l_pe1, l_pe2;
-    const float* q1[2];
-    float* q2[2];
-    fv3_layout l_q1[2], l_q2[2];
-    int64_t ncol;
-    int km, kn, iv, kord;
-};
 
 // DevCol for mappm_ppm_columns<NF> (NF = 1, 2): fields f emit output k in turn, so each
 // keeps its own running output pointer
@@ -563,6 +557,7 @@ struct DevColN {
 };
 using DevColPair = DevColN<2>;
 
+template <bool K1>
 __global__ __launch_bounds__(256) void mappm_ppm_pair_kernel(MappmPairArgs a)
 {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -585,7 +580,7 @@ __global__ __launch_bounds__(256) void mappm_ppm_pair_kernel(MappmPairArgs a)
 #ifndef FV3_MAPPM_PAIR_CARRY
 #define FV3_MAPPM_PAIR_CARRY 1  // 0: tools A/B builds
 #endif
-    mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0>(d, a.km, a.kn, a.iv, a.kord);
+    mappm_ppm_columns<2, DevColPair, FV3_MAPPM_PAIR_CARRY != 0>(d, a.km, a.kn, K1 ? 1 : a.iv, K1 ? 1 : a.kord);
 }
 
 // Small grids with one lane per column left the SIMDs short of waves (one rank's share
@@ -601,9 +596,10 @@ __global__ __launch_bounds__(256) void mappm_ppm_pair_kernel(MappmPairArgs a)
 // the single pass on any column the checks did not prove (unsorted or NaN edges).  The
 // host runs this kernel for kn >= 2 only, on NF = 2 fields (fv3_mappm_multi's pairs) or
 // one (fv3_mappm_ex).
-template <int NF>
+template <int NF, bool K1>
 __global__ __launch_bounds__(128) void mappm_ppm_pair_split_kernel(MappmPairArgs a)
 {
+    const int iv = K1 ? 1 : a.iv, kord = K1 ? 1 : a.kord;
     __shared__ int s_ok[64], s_l0[64];
     const int lane = threadIdx.x & 63;
     const int part = threadIdx.x >> 6;
@@ -644,7 +640,7 @@ __global__ __launch_bounds__(128) void mappm_ppm_pair_split_kernel(MappmPairArgs
         }
         d.pe2_next = d.pe2_ + (int64_t)(kf + 1) * d.ld_pe2;
         d.nb = (kf + 2 <= kn + 1) ? *d.pe2_next : 0.0f;
-        mappm_ppm_columns<NF, DevColN<NF>, FV3_MAPPM_PAIR_CARRY != 0, true>(d, km, kn, a.iv, a.kord, kf, kl, Lf, &chk);
+        mappm_ppm_columns<NF, DevColN<NF>, FV3_MAPPM_PAIR_CARRY != 0, true>(d, km, kn, iv, kord, kf, kl, Lf, &chk);
         for (int f = 0; f < NF; ++f) d.q2_[f] = q2c[f];
     }
     if (part == 1) {
@@ -656,7 +652,7 @@ __global__ __launch_bounds__(128) void mappm_ppm_pair_split_kernel(MappmPairArgs
         // the fix-up: this column's single pass, over what the halves wrote
         d.pe2_next = d.pe2_ + 2 * d.ld_pe2;
         d.nb = kn >= 2 ? *d.pe2_next : 0.0f;
-        mappm_ppm_columns<NF, DevColN<NF>, FV3_MAPPM_PAIR_CARRY != 0>(d, km, kn, a.iv, a.kord);
+        mappm_ppm_columns<NF, DevColN<NF>, FV3_MAPPM_PAIR_CARRY != 0>(d, km, kn, iv, kord);
     }
 }
 
@@ -664,9 +660,10 @@ __global__ __launch_bounds__(128) void mappm_ppm_pair_split_kernel(MappmPairArgs
 // kB1 = kn / 3 + 1 and kB2 = 2 kn / 3 + 1, each later lane starting where the single pass
 // begins its first output): more waves for grids too small to fill the SIMDs even on
 // two.  The host runs it for kn >= 3 only.
-template <int NF>
+template <int NF, bool K1>
 __global__ __launch_bounds__(192) void mappm_ppm_pair_split3_kernel(MappmPairArgs a)
 {
+    const int iv = K1 ? 1 : a.iv, kord = K1 ? 1 : a.kord;
     __shared__ int s_ok[2][64], s_l0[2][64], s_exit[64];
     const int lane = threadIdx.x & 63;
     const int part = threadIdx.x >> 6;
@@ -704,7 +701,7 @@ __global__ __launch_bounds__(192) void mappm_ppm_pair_split3_kernel(MappmPairArg
         }
         d.pe2_next = d.pe2_ + (int64_t)(kf + 1) * d.ld_pe2;
         d.nb = (kf + 2 <= kn + 1) ? *d.pe2_next : 0.0f;
-        mappm_ppm_columns<NF, DevColN<NF>, FV3_MAPPM_PAIR_CARRY != 0, true>(d, km, kn, a.iv, a.kord, kf, kl, Lf, &chk);
+        mappm_ppm_columns<NF, DevColN<NF>, FV3_MAPPM_PAIR_CARRY != 0, true>(d, km, kn, iv, kord, kf, kl, Lf, &chk);
         for (int f = 0; f < NF; ++f) d.q2_[f] = q2c[f];
     }
     if (part > 0) {
@@ -719,7 +716,7 @@ __global__ __launch_bounds__(192) void mappm_ppm_pair_split3_kernel(MappmPairArg
         // the fix-up: this column's single pass, over what the lanes wrote
         d.pe2_next = d.pe2_ + 2 * d.ld_pe2;
         d.nb = kn >= 2 ? *d.pe2_next : 0.0f;
-        mappm_ppm_columns<NF, DevColN<NF>, FV3_MAPPM_PAIR_CARRY != 0>(d, km, kn, a.iv, a.kord);
+        mappm_ppm_columns<NF, DevColN<NF>, FV3_MAPPM_PAIR_CARRY != 0>(d, km, kn, iv, kord);
     }
 }
 
@@ -796,24 +793,65 @@ bool launch_split_single(const MappmArgs& a, hipStream_t stream)
     MappmPairArgs pa{a.pe1, a.pe2, a.l_pe1, a.l_pe2, {a.q1, nullptr}, {a.q2, nullptr}, {a.l_q1, {}}, {a.l_q2, {}},
                      a.ncol, a.km, a.kn, a.iv, a.kord};
     const int64_t grid = (a.ncol + 63) / 64;
+    const bool k1 = is_k1(a.iv, a.kord);
     if (lanes == 3)
-        hipLaunchKernelGGL(mappm_ppm_pair_split3_kernel<1>, dim3((unsigned)grid), dim3(192), 0, stream, pa);
+        hipLaunchKernelGGL((k1 ? mappm_ppm_pair_split3_kernel<1, true> : mappm_ppm_pair_split3_kernel<1, false>),
+                           dim3((unsigned)grid), dim3(192), 0, stream, pa);
     else
-        hipLaunchKernelGGL(mappm_ppm_pair_split_kernel<1>, dim3((unsigned)grid), dim3(128), 0, stream, pa);
+        hipLaunchKernelGGL((k1 ? mappm_ppm_pair_split_kernel<1, true> : mappm_ppm_pair_split_kernel<1, false>),
+                           dim3((unsigned)grid), dim3(128), 0, stream, pa);
     return true;
 }
 
+// pairs of fields on the streaming kord <= 7 kernel (fv3_mappm_multi)
+int launch_mappm_pairs(const MappmPairArgs& a, hipStream_t s)
+{
+    const int lanes = split_lanes(a.ncol, a.kn);
+    const bool k1 = is_k1(a.iv, a.kord);
+    if (lanes == 3) {  // three lanes per column: 192 threads per 64 columns
+        const int64_t grid = (a.ncol + 63) / 64;
+        hipLaunchKernelGGL((k1 ? mappm_ppm_pair_split3_kernel<2, true> : mappm_ppm_pair_split3_kernel<2, false>),
+                           dim3((unsigned)grid), dim3(192), 0, s, a);
+    } else if (lanes == 2) {  // two lanes per column: 128 threads per 64 columns
+        const int64_t grid = (a.ncol + 63) / 64;
+        hipLaunchKernelGGL((k1 ? mappm_ppm_pair_split_kernel<2, true> : mappm_ppm_pair_split_kernel<2, false>),
+                           dim3((unsigned)grid), dim3(128), 0, s, a);
+    } else {
+        const int block = 256;
+        const int64_t grid = (a.ncol + block - 1) / block;
+        hipLaunchKernelGGL((k1 ? mappm_ppm_pair_kernel<true> : mappm_ppm_pair_kernel<false>), dim3((unsigned)grid),
+                           dim3(block), 0, s, a);
+    }
+    FV3_LAUNCH_CHECK();
+    return FV3_OK;
+}
+
+}  // namespace FV3_ARITH_NS
 }  // namespace fv3
 
+#ifndef FV3_FAST_ARITH  // the C ABI: one definition, dispatching on the arithmetic
 using fv3::MappmArgs;
+
+namespace {
+// FV3_ARITH_FAST covers the ppm_profile path (kord <= 7) only.  cs_profile (kord > 7)
+// flattens a layer or switches its Huynh constraint on flags (extm, ext5, ext6,
+// mappm.f90:269-288) computed from the solved edges, a discontinuous choice: 1-ulp
+// changes to the edges flip it (tools/remap_fast_study.py, C384 kord 10: 7e-3 per level,
+// 1 % of the values moved).  So kord > 7 always runs the exact arithmetic.
+int launch_arith(const MappmArgs& a, int arith, hipStream_t s)
+{
+    return arith == FV3_ARITH_FAST && a.kord <= 7 ? fv3::fast::launch_mappm(a, s) : fv3::exact::launch_mappm(a, s);
+}
+}  // namespace
 
 extern "C" int fv3_mappm_ex(const float* pe1, fv3_layout pe1_l, const float* q1, fv3_layout q1_l,
                             const float* pe2, fv3_layout pe2_l, float* q2, fv3_layout q2_l,
-                            int64_t ncol, int km, int kn, int iv, int kord, float ptop,
+                            int64_t ncol, int km, int kn, int iv, int kord, float ptop, int arith,
                             void* stream)
 {
     (void)ptop;  // unused by the reference too (regridz.py:270)
     fv3::clear_error();
+    FV3_REQUIRE(arith == FV3_ARITH_EXACT || arith == FV3_ARITH_FAST, "mappm: unknown arithmetic %d", arith);
     FV3_REQUIRE(ncol >= 0, "mappm: ncol must be >= 0 (got %lld)", (long long)ncol);
     FV3_REQUIRE(km >= 4, "mappm: km must be >= 4 (got %d)", km);
     FV3_REQUIRE(kn >= 1, "mappm: kn must be >= 1 (got %d)", kn);
@@ -823,22 +861,24 @@ extern "C" int fv3_mappm_ex(const float* pe1, fv3_layout pe1_l, const float* q1,
                 "mappm: invalid column layout");
     FV3_REQUIRE(ncol / 256 < (int64_t)0x7fffffff, "mappm: ncol too large");
     MappmArgs a{pe1, q1, pe2, q2, pe1_l, q1_l, pe2_l, q2_l, ncol, km, kn, iv, kord, nullptr};
-    return fv3::launch_mappm(a, (hipStream_t)stream);
+    return launch_arith(a, arith, (hipStream_t)stream);
 }
 
+// the f2py signature of the reference's mappm.mappm: the reference's arithmetic
 extern "C" int fv3_mappm(const float* pe1, const float* q1, const float* pe2, float* q2,
                          int64_t ncol, int km, int kn, int iv, int kord, float ptop, void* stream)
 {
     const fv3_layout l = fv3::plain_layout(ncol > 0 ? ncol : 1);
-    return fv3_mappm_ex(pe1, l, q1, l, pe2, l, q2, l, ncol, km, kn, iv, kord, ptop, stream);
+    return fv3_mappm_ex(pe1, l, q1, l, pe2, l, q2, l, ncol, km, kn, iv, kord, ptop, FV3_ARITH_EXACT, stream);
 }
 
 extern "C" int fv3_mappm_multi(const float* pe1, fv3_layout pe1_l, const float* const* q1, const fv3_layout* q1_l,
                                const float* pe2, fv3_layout pe2_l, float* const* q2, const fv3_layout* q2_l,
-                               int n_fields, int64_t ncol, int km, int kn, int iv, int kord, float ptop,
+                               int n_fields, int64_t ncol, int km, int kn, int iv, int kord, float ptop, int arith,
                                void* stream)
 {
     fv3::clear_error();
+    FV3_REQUIRE(arith == FV3_ARITH_EXACT || arith == FV3_ARITH_FAST, "mappm: unknown arithmetic %d", arith);
     FV3_REQUIRE(n_fields >= 1 && n_fields <= 64, "mappm_multi: n_fields must be in 1..64 (got %d)", n_fields);
     FV3_REQUIRE(q1 && q1_l && q2 && q2_l, "mappm_multi: NULL field array");
     FV3_REQUIRE(ncol >= 0, "mappm: ncol must be >= 0 (got %lld)", (long long)ncol);
@@ -858,29 +898,20 @@ extern "C" int fv3_mappm_multi(const float* pe1, fv3_layout pe1_l, const float* 
     // pairs on the streaming kord <= 7 kernel; the level-parallel (small grids) and
     // cs_profile (kord > 7) paths, and an odd last field, one field per launch
     MappmArgs one{pe1, nullptr, pe2, nullptr, pe1_l, {}, pe2_l, {}, ncol, km, kn, iv, kord, nullptr};
-    if (kord <= 7 && !fv3::use_levels_kernel(one, fv3::kLevelsMaxColsPairs)) {
+    if (kord <= 7 && !fv3::exact::use_levels_kernel(one, fv3::exact::kLevelsMaxColsPairs)) {
         for (; f + 2 <= n_fields; f += 2) {
             fv3::MappmPairArgs a{pe1, pe2, pe1_l, pe2_l, {q1[f], q1[f + 1]}, {q2[f], q2[f + 1]},
                                  {q1_l[f], q1_l[f + 1]}, {q2_l[f], q2_l[f + 1]}, ncol, km, kn, iv, kord};
-            const int block = 256;
-            const int lanes = fv3::split_lanes(ncol, kn);
-            if (lanes == 3) {  // three lanes per column: 192 threads per 64 columns
-                const int64_t grid = (ncol + 63) / 64;
-                hipLaunchKernelGGL(fv3::mappm_ppm_pair_split3_kernel<2>, dim3((unsigned)grid), dim3(192), 0, s, a);
-            } else if (lanes == 2) {  // two lanes per column: 128 threads per 64 columns
-                const int64_t grid = (ncol + 63) / 64;
-                hipLaunchKernelGGL(fv3::mappm_ppm_pair_split_kernel<2>, dim3((unsigned)grid), dim3(128), 0, s, a);
-            } else {
-                const int64_t grid = (ncol + block - 1) / block;
-                hipLaunchKernelGGL(fv3::mappm_ppm_pair_kernel, dim3((unsigned)grid), dim3(block), 0, s, a);
-            }
-            FV3_LAUNCH_CHECK();
+            const int st = arith == FV3_ARITH_FAST ? fv3::fast::launch_mappm_pairs(a, s)
+                                                   : fv3::exact::launch_mappm_pairs(a, s);
+            if (st != FV3_OK) return st;
         }
     }
     for (; f < n_fields; ++f) {
         const int st = fv3_mappm_ex(pe1, pe1_l, q1[f], q1_l[f], pe2, pe2_l, q2[f], q2_l[f], ncol, km, kn, iv, kord,
-                                    ptop, stream);
+                                    ptop, arith, stream);
         if (st != FV3_OK) return st;
     }
     return FV3_OK;
 }
+#endif  // FV3_FAST_ARITH

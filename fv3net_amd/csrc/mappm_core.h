@@ -34,12 +34,69 @@
 #include <cstdint>
 #endif
 
+// ---- arithmetic policy (one per translation unit) ----
+// Default (namespace fv3::exact): the reference build's arithmetic, bit for bit (the rules
+// above).  With FV3_FAST_ARITH defined before the include (namespace fv3::fast, compiled
+// in csrc/*_fast.hip): north_star's floating-point tolerance contract (1e-5 rel; the
+// reference's own test accepts cross-platform differences in mappm,
+// external/vcm/tests/test_coarsen_restarts.py:115-122) instead of bit parity:
+//   * every division a / b as a * rcp(b) (v_rcp_f32, 1 ulp: 2 instructions for the 11 of
+//     a correctly rounded division), identical denominators sharing one reciprocal;
+//   * a * b + c contracted to one FMA within an expression (fp contract(on));
+//   * MAX / MIN as the hardware's v_max_f32 / v_min_f32 (v_max3 / v_min3 for three
+//     operands).  These equal the reference's a > b ? a : b for finite operands; a NaN
+//     operand is dropped instead of propagated by position, so non-finite inputs need the
+//     exact path.
+// Same algorithm, same order of operations, same limiter branches (a comparison near its
+// switching point may take the other branch; the PPM limiters are continuous there).
+#ifdef FV3_FAST_ARITH
+#define FV3_ARITH_NS fast
+#if defined(__HIP_DEVICE_COMPILE__)
+#define FV3_RCP(b) __builtin_amdgcn_rcpf(b)
+#else
+#define FV3_RCP(b) (1.0f / (b))
+#endif
 namespace fv3 {
+// a / b from the 1-ulp reciprocal plus one Newton step on the quotient (4 instructions):
+// within ~1 ulp of the correctly rounded quotient.  The profile's divisions (dc, the
+// edge estimates, h2, the end cubics) feed differences that cancel on irregular
+// thicknesses; with the bare a * rcp(b) a rough 79-level column (delp over 3 decades)
+// reached 1.35e-5 per level, with this step 2.8e-6 (tools/remap_fast_random.py).
+FV3_HD inline float div_refined(float a, float b)
+{
+    const float r = FV3_RCP(b);
+    const float q = a * r;
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_fmaf(__builtin_fmaf(-b, q, a), r, q);
+#else
+    return a / b;
+#endif
+}
+}  // namespace fv3
+#define FV3_DIV(a, b) (::fv3::div_refined((a), (b)))
+// the remap consumer's quotients: a position inside a layer ((t - pe1) / dp, in [0, 1])
+// and the final mean qsum / dpsum, where a 1-ulp quotient stays a 1-ulp result
+#define FV3_DIVQ(a, b) ((a) * FV3_RCP(b))
+#define FV3_DIVX(a, b) ((a) / (b))  // the reference's division in either policy
+#else
+#define FV3_ARITH_NS exact
+#define FV3_DIV(a, b) ((a) / (b))
+#define FV3_DIVQ(a, b) ((a) / (b))
+#define FV3_DIVX(a, b) ((a) / (b))
+#endif
 
+namespace fv3 {
+namespace FV3_ARITH_NS {
+#ifdef FV3_FAST_ARITH
+#pragma clang fp contract(on)
+FV3_HD inline float fmax2(float a, float b) { return __builtin_fmaxf(a, b); }
+FV3_HD inline float fmin2(float a, float b) { return __builtin_fminf(a, b); }
+#else
 FV3_HD inline float fmax2(float a, float b) { return a > b ? a : b; }
+FV3_HD inline float fmin2(float a, float b) { return a < b ? a : b; }
+#endif
 FV3_HD inline int imin2(int a, int b) { return a < b ? a : b; }
 FV3_HD inline int imax2(int a, int b) { return a > b ? a : b; }
-FV3_HD inline float fmin2(float a, float b) { return a < b ? a : b; }
 FV3_HD inline float fmax3(float a, float b, float c) { return fmax2(fmax2(a, b), c); }
 FV3_HD inline float fmin3(float a, float b, float c) { return fmin2(fmin2(a, b), c); }
 FV3_HD inline float fsign(float a, float b) { return copysignf(fabsf(a), b); }
@@ -77,7 +134,7 @@ FV3_HD inline void ppm_limit(float dm, Ppm& a, int lmt)
     } else if (lmt == 2) {
         if (fabsf(a.ar - a.al) < -a.a6) {
             const float d = a.ar - a.al;
-            const float fmin = a.a1 + 0.25f * (d * d) / a.a6 + a.a6 * r12;
+            const float fmin = a.a1 + FV3_DIV(0.25f * (d * d), a.a6) + a.a6 * r12;
             if (fmin < 0.0f) {
                 if (a.a1 < a.ar && a.a1 < a.al) {
                     a.ar = a.a1; a.al = a.a1; a.a6 = 0.0f;
@@ -102,7 +159,7 @@ FV3_HD inline void cs_limit(bool extm, Ppm& a, int iv)
             a.al = a.a1; a.ar = a.a1; a.a6 = 0.0f;
         } else if (fabsf(a.ar - a.al) < -a.a6) {
             const float d = a.ar - a.al;
-            if ((a.a1 + 0.25f * (d * d) / a.a6 + a.a6 * r12) < 0.0f) {
+            if ((a.a1 + FV3_DIV(0.25f * (d * d), a.a6) + a.a6 * r12) < 0.0f) {
                 if (a.a1 < a.ar && a.a1 < a.al) {
                     a.ar = a.a1; a.al = a.a1; a.a6 = 0.0f;
                 } else if (a.ar > a.al) {
@@ -143,11 +200,11 @@ FV3_HD inline float ppm_dc(float qm1, float q0, float qp1, float dm1, float d0, 
 {
     const float d4k = dm1 + d0;    // d4(k)
     const float d4kp = d0 + dp1;   // d4(k+1)
-    const float c1 = (dm1 + 0.5f * d0) / d4kp;
-    const float c2 = (dp1 + 0.5f * d0) / d4k;
+    const float c1 = FV3_DIV(dm1 + 0.5f * d0, d4kp);
+    const float c2 = FV3_DIV(dp1 + 0.5f * d0, d4k);
     const float delq_k = qp1 - q0;   // delq(k)
     const float delq_km = q0 - qm1;  // delq(k-1)
-    const float df2 = d0 * (c1 * delq_k + c2 * delq_km) / (d4k + dp1);
+    const float df2 = FV3_DIV(d0 * (c1 * delq_k + c2 * delq_km), d4k + dp1);
     return fsign(fmin3(fabsf(df2), fmax3(qm1, q0, qp1) - q0, q0 - fmin3(qm1, q0, qp1)), df2);
 }
 
@@ -159,16 +216,16 @@ FV3_HD inline float ppm_al(float dm2, float dm1, float d0, float dp1, float qm1,
     const float d4km = dm2 + dm1;  // d4(k-1)
     const float d4k = dm1 + d0;    // d4(k)
     const float d4kp = d0 + dp1;   // d4(k+1)
-    const float c1 = (q0 - qm1) * dm1 / d4k;
-    const float a1 = d4km / (d4k + dm1);
-    const float a2 = d4kp / (d4k + d0);
-    return qm1 + c1 + 2.0f / (d4km + d4kp) * (d0 * (c1 * (a1 - a2) + a2 * dcm1) - dm1 * a1 * dc0);
+    const float c1 = FV3_DIV((q0 - qm1) * dm1, d4k);
+    const float a1 = FV3_DIV(d4km, d4k + dm1);
+    const float a2 = FV3_DIV(d4kp, d4k + d0);
+    return qm1 + c1 + FV3_DIV(2.0f, d4km + d4kp) * (d0 * (c1 * (a1 - a2) + a2 * dcm1) - dm1 * a1 * dc0);
 }
 
 // h2(k) (mappm.f90:784-795), k = 2..km-1.
 FV3_HD inline float ppm_h2(float dcm1, float dcp1, float dm1, float d0, float dp1)
 {
-    return 2.0f * (dcp1 / dp1 - dcm1 / dm1) / (d0 + 0.5f * (dm1 + dp1)) * (d0 * d0);
+    return FV3_DIV(2.0f * (FV3_DIV(dcp1, dp1) - FV3_DIV(dcm1, dm1)), d0 + 0.5f * (dm1 + dp1)) * (d0 * d0);
 }
 
 // Huynh's 2nd constraint for an interior PPM layer (mappm.f90:799-821).
@@ -183,6 +240,58 @@ FV3_HD inline void ppm_huynh(Ppm& a, float dc, float h2m, float h2p)
     lac = a.a1 + fac * h2p - dc;
     a.al = fmin2(fmax2(a.al, fmin3(a.a1, qmp, lac)), fmax3(a.a1, qmp, lac));
     a.a6 = a6_of(a);
+}
+
+// ---- the area-preserving end cubics, one field (mappm.f90:689-725, 729-761) ----
+// Always the reference's arithmetic (IEEE division, no contraction), in both policies:
+// they run once per column, and their clamps (al2 onto [min, max](q1, q2), and likewise
+// at the bottom) decide whether dc of an end layer is exactly 0, which flattens that
+// layer (ppm_limiters lmt 0, `dm == 0`).  Computed in the fast arithmetic, an edge value
+// within an ulp of its clamp bound could land on the other side and flip the layer.
+
+FV3_HD inline void ppm_top_cubic(float q1, float q2, float d1, float d2, float al3, int iv, float& al1,
+                                 float& al2, float& dc1)
+{
+#pragma clang fp contract(off)
+    const float qm = FV3_DIVX(d2 * q1 + d1 * q2, d1 + d2);
+    const float dq = FV3_DIVX(2.0f * (q2 - q1), d1 + d2);
+    const float c1 = FV3_DIVX(4.0f * (al3 - qm - d2 * dq), d2 * (2.0f * d2 * d2 + d1 * (d2 + 3.0f * d1)));
+    const float c3 = dq - 0.5f * c1 * (d2 * (5.0f * d1 + d2) - 3.0f * d1 * d1);
+    al2 = qm - 0.25f * c1 * d1 * d2 * (d2 + 3.0f * d1);
+    al1 = d1 * (2.0f * c1 * (d1 * d1) - c3) + al2;
+    al2 = fmax2(al2, fmin2(q1, q2));
+    al2 = fmin2(al2, fmax2(q1, q2));
+    dc1 = 0.5f * (al2 - q1);
+    if (iv == 0) {
+        al1 = fmax2(0.0f, al1);
+        al2 = fmax2(0.0f, al2);
+    } else if (iv == -1) {
+        if (al1 * q1 <= 0.0f) al1 = 0.0f;
+    } else if (iv == 2 || iv == -2) {
+        al1 = q1;
+    }
+}
+
+// d1 = dp(km), d2 = dp(km-1), qk = q(km), qk1 = q(km-1), alk1 = ALraw(km-1)
+FV3_HD inline void ppm_bottom_cubic(float qk, float qk1, float d1, float d2, float alk1, int iv, float& alm,
+                                    float& ar, float& dcm)
+{
+#pragma clang fp contract(off)
+    const float qm = FV3_DIVX(d2 * qk + d1 * qk1, d1 + d2);
+    const float dq = FV3_DIVX(2.0f * (qk1 - qk), d1 + d2);
+    const float c1 = FV3_DIVX(alk1 - qm - d2 * dq, d2 * (2.0f * d2 * d2 + d1 * (d2 + 3.0f * d1)));
+    const float c3 = dq - 2.0f * c1 * (d2 * (5.0f * d1 + d2) - 3.0f * d1 * d1);
+    alm = qm - c1 * d1 * d2 * (d2 + 3.0f * d1);
+    ar = d1 * (8.0f * c1 * (d1 * d1) - c3) + alm;
+    alm = fmax2(alm, fmin2(qk, qk1));
+    alm = fmin2(alm, fmax2(qk, qk1));
+    dcm = 0.5f * (qk - alm);
+    if (iv == 0) {
+        alm = fmax2(0.0f, alm);
+        ar = fmax2(0.0f, ar);
+    } else if (iv < 0) {
+        if (qk * ar <= 0.0f) ar = 0.0f;
+    }
 }
 
 // ---- remap consumer: the output-layer loop of mappm.f90:58-124, lockstep over L ----
@@ -220,10 +329,10 @@ FV3_HD inline void remap_layer(RemapState& s, const LayerView& v, const ColumnEn
             } else if (s.t >= e.pe_bot) {
                 out.emit(s.k, e.q_bot);
             } else if (s.t >= v.pl0 && s.t <= v.pl1) {
-                const float pl = (s.t - v.pl0) / v.dp;
+                const float pl = FV3_DIVQ(s.t - v.pl0, v.dp);
                 if (s.b <= v.pl1) {
                     // entire new layer inside input layer L (mappm.f90:76-83)
-                    const float pr = (s.b - v.pl0) / v.dp;
+                    const float pr = FV3_DIVQ(s.b - v.pl0, v.dp);
                     const float tt = r3 * (pr * (pr + pl) + pl * pl);
                     out.emit(s.k, v.a.al + 0.5f * (v.a.a6 + v.a.ar - v.a.al) * (pr + pl) - v.a.a6 * tt);
                 } else {
@@ -247,10 +356,10 @@ FV3_HD inline void remap_layer(RemapState& s, const LayerView& v, const ColumnEn
             }
             // bottom piece (mappm.f90:105-112)
             const float delp = s.b - v.pl0;
-            const float esl = delp / v.dp;
+            const float esl = FV3_DIVQ(delp, v.dp);
             s.qsum = s.qsum + delp * (v.a.al + 0.5f * esl * (v.a.ar - v.a.al + v.a.a6 * (1.0f - r23 * esl)));
             s.dpsum = s.dpsum + delp;
-            out.emit(s.k, s.qsum / s.dpsum);
+            out.emit(s.k, FV3_DIVQ(s.qsum, s.dpsum));
             s.accum = false;
         }
         // advance to the next output layer; its search restarts at this L (k0 = L)
@@ -287,10 +396,10 @@ FV3_HD inline void remap_layer_fast(RemapState& s, const LayerView& v, const Col
         }
         // bottom piece (mappm.f90:105-112)
         const float delp = s.b - v.pl0;
-        const float esl = delp / v.dp;
+        const float esl = FV3_DIVQ(delp, v.dp);
         s.qsum = s.qsum + delp * (v.a.al + 0.5f * esl * (v.a.ar - v.a.al + v.a.a6 * (1.0f - r23 * esl)));
         s.dpsum = s.dpsum + delp;
-        out.emit(s.k, s.qsum / s.dpsum);
+        out.emit(s.k, FV3_DIVQ(s.qsum, s.dpsum));
         s.accum = false;
         s.k += 1;
         s.t = s.b;
@@ -311,11 +420,11 @@ FV3_HD inline void remap_layer_fast(RemapState& s, const LayerView& v, const Col
             s.xv = false;
             continue;
         }
-        if (!s.xv) s.xt = (s.t - v.pl0) / v.dp;
+        if (!s.xv) s.xt = FV3_DIVQ(s.t - v.pl0, v.dp);
         if (s.b <= v.pl1) {
             // entire new layer inside input layer L (mappm.f90:76-83)
             const float pl = s.xt;
-            const float pr = (s.b - v.pl0) / v.dp;
+            const float pr = FV3_DIVQ(s.b - v.pl0, v.dp);
             const float tt = r3 * (pr * (pr + pl) + pl * pl);
             out.emit(s.k, v.a.al + 0.5f * (v.a.a6 + v.a.ar - v.a.al) * (pr + pl) - v.a.a6 * tt);
             s.k += 1;
@@ -354,7 +463,7 @@ FV3_HD inline void remap_finish(RemapState& s, const ColumnEnds& e, int kn, Out&
                 s.qsum = s.qsum + delp * e.q_bot;
                 s.dpsum = s.dpsum + delp;
             }
-            out.emit(s.k, s.qsum / s.dpsum);
+            out.emit(s.k, FV3_DIVQ(s.qsum, s.dpsum));
             s.accum = false;
         } else if (s.t <= e.pe_top) {
             out.emit(s.k, e.q_top);
@@ -409,27 +518,8 @@ FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
     dc2 = ppm_dc(qv[0], qv[1], qv[2], dpv[0], dpv[1], dpv[2]);
     dc3 = ppm_dc(qv[1], qv[2], qv[3], dpv[1], dpv[2], dpv[3]);  // 3 <= km-1
     al3 = ppm_al(dpv[0], dpv[1], dpv[2], dpv[3], qv[1], qv[2], dc2, dc3);
-    {   // top: area-preserving cubic (mappm.f90:689-725)
-        const float d1 = dpv[0], d2 = dpv[1];
-        const float q1 = qv[0], q2 = qv[1];
-        const float qm = (d2 * q1 + d1 * q2) / (d1 + d2);
-        const float dq = 2.0f * (q2 - q1) / (d1 + d2);
-        const float c1 = 4.0f * (al3 - qm - d2 * dq) / (d2 * (2.0f * d2 * d2 + d1 * (d2 + 3.0f * d1)));
-        const float c3 = dq - 0.5f * c1 * (d2 * (5.0f * d1 + d2) - 3.0f * d1 * d1);
-        al2 = qm - 0.25f * c1 * d1 * d2 * (d2 + 3.0f * d1);
-        al1 = d1 * (2.0f * c1 * (d1 * d1) - c3) + al2;
-        al2 = fmax2(al2, fmin2(q1, q2));
-        al2 = fmin2(al2, fmax2(q1, q2));
-        dc1 = 0.5f * (al2 - q1);
-        if (iv == 0) {
-            al1 = fmax2(0.0f, al1);
-            al2 = fmax2(0.0f, al2);
-        } else if (iv == -1) {
-            if (al1 * q1 <= 0.0f) al1 = 0.0f;
-        } else if (iv == 2 || iv == -2) {
-            al1 = q1;
-        }
-    }
+    // top: area-preserving cubic (mappm.f90:689-725)
+    ppm_top_cubic(qv[0], qv[1], dpv[0], dpv[1], al3, iv, al1, al2, dc1);
     dcv[0] = dc1; dcv[1] = dc2; dcv[2] = dc3;
     alv[0] = al1; alv[1] = al2; alv[2] = al3;
     h2v[0] = 0.0f; h2v[1] = 0.0f;
@@ -510,24 +600,7 @@ FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
 #endif
         } else if (m == km) {
             // bottom: area-preserving cubic (mappm.f90:729-761)
-            const float d1 = dpv[3], d2 = dpv[2];
-            const float qk = qv[3], qk1 = qv[2];
-            const float qm = (d2 * qk + d1 * qk1) / (d1 + d2);
-            const float dq = 2.0f * (qk1 - qk) / (d1 + d2);
-            const float c1 = (alv[2] - qm - d2 * dq) / (d2 * (2.0f * d2 * d2 + d1 * (d2 + 3.0f * d1)));
-            const float c3 = dq - 2.0f * c1 * (d2 * (5.0f * d1 + d2) - 3.0f * d1 * d1);
-            alm = qm - c1 * d1 * d2 * (d2 + 3.0f * d1);
-            float ar = d1 * (8.0f * c1 * (d1 * d1) - c3) + alm;
-            alm = fmax2(alm, fmin2(qk, qk1));
-            alm = fmin2(alm, fmax2(qk, qk1));
-            dcm = 0.5f * (qk - alm);
-            if (iv == 0) {
-                alm = fmax2(0.0f, alm);
-                ar = fmax2(0.0f, ar);
-            } else if (iv < 0) {
-                if (qk * ar <= 0.0f) ar = 0.0f;
-            }
-            ar_km = ar;
+            ppm_bottom_cubic(qv[3], qv[2], dpv[3], dpv[2], alv[2], iv, alm, ar_km, dcm);
         }
         float h2n = 0.0f;  // h2(L+2)
         if (huynh && L + 2 <= km - 1) h2n = ppm_h2(dcv[1], dcm, dpv[1], dpv[2], dpv[3]);
@@ -566,9 +639,9 @@ FV3_HD inline bool remap_one(RemapState& s, const LayerView& v, const ColumnEnds
         } else if (s.t >= e.pe_bot) {
             val = e.q_bot;
         } else if (s.t >= v.pl0 && s.t <= v.pl1) {
-            const float pl = (s.t - v.pl0) / v.dp;
+            const float pl = FV3_DIVQ(s.t - v.pl0, v.dp);
             if (s.b <= v.pl1) {
-                const float pr = (s.b - v.pl0) / v.dp;
+                const float pr = FV3_DIVQ(s.b - v.pl0, v.dp);
                 const float tt = r3 * (pr * (pr + pl) + pl * pl);
                 val = v.a.al + 0.5f * (v.a.a6 + v.a.ar - v.a.al) * (pr + pl) - v.a.a6 * tt;
             } else {
@@ -589,10 +662,10 @@ FV3_HD inline bool remap_one(RemapState& s, const LayerView& v, const ColumnEnds
             return false;
         }
         const float delp = s.b - v.pl0;
-        const float esl = delp / v.dp;
+        const float esl = FV3_DIVQ(delp, v.dp);
         s.qsum = s.qsum + delp * (v.a.al + 0.5f * esl * (v.a.ar - v.a.al + v.a.a6 * (1.0f - r23 * esl)));
         s.dpsum = s.dpsum + delp;
-        val = s.qsum / s.dpsum;
+        val = FV3_DIVQ(s.qsum, s.dpsum);
         s.accum = false;
     }
     s.k += 1;
@@ -626,27 +699,8 @@ struct PpmCursor {
         dc2 = ppm_dc(qv[0], qv[1], qv[2], dpv[0], dpv[1], dpv[2]);
         dc3 = ppm_dc(qv[1], qv[2], qv[3], dpv[1], dpv[2], dpv[3]);
         al3 = ppm_al(dpv[0], dpv[1], dpv[2], dpv[3], qv[1], qv[2], dc2, dc3);
-        {   // top: area-preserving cubic (mappm.f90:689-725)
-            const float d1 = dpv[0], d2 = dpv[1];
-            const float q1 = qv[0], q2 = qv[1];
-            const float qm = (d2 * q1 + d1 * q2) / (d1 + d2);
-            const float dq = 2.0f * (q2 - q1) / (d1 + d2);
-            const float c1 = 4.0f * (al3 - qm - d2 * dq) / (d2 * (2.0f * d2 * d2 + d1 * (d2 + 3.0f * d1)));
-            const float c3 = dq - 0.5f * c1 * (d2 * (5.0f * d1 + d2) - 3.0f * d1 * d1);
-            al2 = qm - 0.25f * c1 * d1 * d2 * (d2 + 3.0f * d1);
-            al1 = d1 * (2.0f * c1 * (d1 * d1) - c3) + al2;
-            al2 = fmax2(al2, fmin2(q1, q2));
-            al2 = fmin2(al2, fmax2(q1, q2));
-            dc1 = 0.5f * (al2 - q1);
-            if (iv == 0) {
-                al1 = fmax2(0.0f, al1);
-                al2 = fmax2(0.0f, al2);
-            } else if (iv == -1) {
-                if (al1 * q1 <= 0.0f) al1 = 0.0f;
-            } else if (iv == 2 || iv == -2) {
-                al1 = q1;
-            }
-        }
+        // top: area-preserving cubic (mappm.f90:689-725)
+        ppm_top_cubic(qv[0], qv[1], dpv[0], dpv[1], al3, iv, al1, al2, dc1);
         dcv[0] = dc1; dcv[1] = dc2; dcv[2] = dc3;
         alv[0] = al1; alv[1] = al2; alv[2] = al3;
         h2v[0] = 0.0f; h2v[1] = 0.0f;
@@ -697,24 +751,7 @@ struct PpmCursor {
             dcm = ppm_dc(qv[2], qv[3], qn, dpv[2], dpv[3], dpn);
             alm = ppm_al(dpv[1], dpv[2], dpv[3], dpn, qv[2], qv[3], dcv[2], dcm);
         } else if (m == km) {
-            const float d1 = dpv[3], d2 = dpv[2];
-            const float qk = qv[3], qk1 = qv[2];
-            const float qm = (d2 * qk + d1 * qk1) / (d1 + d2);
-            const float dq = 2.0f * (qk1 - qk) / (d1 + d2);
-            const float c1 = (alv[2] - qm - d2 * dq) / (d2 * (2.0f * d2 * d2 + d1 * (d2 + 3.0f * d1)));
-            const float c3 = dq - 2.0f * c1 * (d2 * (5.0f * d1 + d2) - 3.0f * d1 * d1);
-            alm = qm - c1 * d1 * d2 * (d2 + 3.0f * d1);
-            float ar = d1 * (8.0f * c1 * (d1 * d1) - c3) + alm;
-            alm = fmax2(alm, fmin2(qk, qk1));
-            alm = fmin2(alm, fmax2(qk, qk1));
-            dcm = 0.5f * (qk - alm);
-            if (iv == 0) {
-                alm = fmax2(0.0f, alm);
-                ar = fmax2(0.0f, ar);
-            } else if (iv < 0) {
-                if (qk * ar <= 0.0f) ar = 0.0f;
-            }
-            ar_km = ar;
+            ppm_bottom_cubic(qv[3], qv[2], dpv[3], dpv[2], alv[2], iv, alm, ar_km, dcm);
         }
         float h2n = 0.0f;
         if (huynh && L + 2 <= km - 1) h2n = ppm_h2(dcv[1], dcm, dpv[1], dpv[2], dpv[3]);
@@ -743,7 +780,7 @@ struct PpmCursor {
                 s.qsum = s.qsum + delp * ends.q_bot;
                 s.dpsum = s.dpsum + delp;
             }
-            val = s.qsum / s.dpsum;
+            val = FV3_DIVQ(s.qsum, s.dpsum);
             s.accum = false;
         } else if (s.t <= ends.pe_top) {
             val = ends.q_top;
@@ -816,18 +853,18 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
                 const float qk = c.q1(k);
                 const float pen = c.pe1(k + 1);
                 const float dpk = pen - pek;
-                const float grat = dpm1 / dpk;
+                const float grat = FV3_DIV(dpm1, dpk);
                 const float bet = 2.0f + grat + grat - gk;
-                qprev = (3.0f * (qm1 + qk) - qprev) / bet;
+                qprev = FV3_DIV(3.0f * (qm1 + qk) - qprev, bet);
                 scr.e(k) = qprev;
-                gk = grat / bet;
+                gk = FV3_DIV(grat, bet);
                 scr.g(k + 1) = gk;
                 qm1 = qk; dpm1 = dpk; pek = pen;
             }
             const float qkm = c.q1(km);
             const float dpkm = c.pe1(km + 1) - pek;
-            const float grat = dpm1 / dpkm;
-            qprev = (3.0f * (qm1 + qkm) - grat * qs - qprev) / (2.0f + grat + grat - gk);
+            const float grat = FV3_DIV(dpm1, dpkm);
+            qprev = FV3_DIV(3.0f * (qm1 + qkm) - grat * qs - qprev, 2.0f + grat + grat - gk);
             scr.e(km) = qprev;
             scr.e(km + 1) = qs;
             float qn = qprev;
@@ -839,10 +876,10 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
             float q2v = c.q1(2);
             float pe2v = c.pe1(3);
             float dp2 = pe2v - pe1v;
-            float grat = dp2 / dpm1;
+            float grat = FV3_DIV(dp2, dpm1);
             float bet = grat * (grat + 0.5f);
-            float qprev = ((grat + grat) * (grat + 1.0f) * qm1 + q2v) / bet;
-            float gprev = (1.0f + grat * (grat + 1.5f)) / bet;
+            float qprev = FV3_DIV((grat + grat) * (grat + 1.0f) * qm1 + q2v, bet);
+            float gprev = FV3_DIV(1.0f + grat * (grat + 1.5f), bet);
             scr.e(1) = qprev;
             scr.g(1) = gprev;
             float d4 = 0.0f;
@@ -852,10 +889,10 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
             auto sweep_v = [&](float qkv, float pen, auto&& e_out, auto&& g_out) {
                 qk = qkv;
                 const float dpk = pen - pek;
-                d4 = dpm1 / dpk;
+                d4 = FV3_DIV(dpm1, dpk);
                 bet = 2.0f + d4 + d4 - gprev;
-                qprev = (3.0f * (qkm1 + d4 * qk) - qprev) / bet;
-                gprev = d4 / bet;
+                qprev = FV3_DIV(3.0f * (qkm1 + d4 * qk) - qprev, bet);
+                gprev = FV3_DIV(d4, bet);
                 e_out = qprev;
                 g_out = gprev;
                 qkm1 = qk; dpm1 = dpk; pek = pen;
@@ -910,7 +947,7 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
             // qkm1 == qk == q(km) here; need q(km-1)
             const float a_bot = 1.0f + d4 * (d4 + 1.5f);
             const float qkmm1 = c.q1(km - 1);
-            float qn = (2.0f * d4 * (d4 + 1.0f) * qk + qkmm1 - a_bot * qprev) / (d4 * (d4 + 0.5f) - a_bot * gprev);
+            float qn = FV3_DIV(2.0f * d4 * (d4 + 1.0f) * qk + qkmm1 - a_bot * qprev, d4 * (d4 + 0.5f) - a_bot * gprev);
             int kb = km;  // back-substitution continues in the scratch from here
             if constexpr (NT > 0) {
                 if (tail) {
@@ -1182,4 +1219,9 @@ FV3_HD inline void mappm_cs_column(Col& c, Scr& scr, int km, int kn, int iv, int
     remap_finish(s, ends, kn, c);
 }
 
+#ifdef FV3_FAST_ARITH
+#pragma clang fp contract(off)
+#endif
+}  // namespace FV3_ARITH_NS
+using namespace FV3_ARITH_NS;
 }  // namespace fv3

@@ -26,6 +26,10 @@
 #include "mappm_core.h"
 
 namespace fv3 {
+namespace FV3_ARITH_NS {  // the arithmetic policy of mappm_core.h
+#ifdef FV3_FAST_ARITH
+#pragma clang fp contract(on)
+#endif
 
 // ---- pressure-only / field parts of ppm_dc, ppm_al, ppm_h2 (mappm.f90:658-683, 784-795) ----
 
@@ -36,13 +40,13 @@ FV3_HD inline DcShared ppm_dc_shared(float dm1, float d0, float dp1)
 {
     const float d4k = dm1 + d0;    // d4(k)
     const float d4kp = d0 + dp1;   // d4(k+1)
-    return DcShared{(dm1 + 0.5f * d0) / d4kp, (dp1 + 0.5f * d0) / d4k, d4k + dp1};
+    return DcShared{FV3_DIV(dm1 + 0.5f * d0, d4kp), FV3_DIV(dp1 + 0.5f * d0, d4k), d4k + dp1};
 }
 FV3_HD inline float ppm_dc_field(const DcShared& p, float qm1, float q0, float qp1, float d0)
 {
     const float delq_k = qp1 - q0;
     const float delq_km = q0 - qm1;
-    const float df2 = d0 * (p.c1 * delq_k + p.c2 * delq_km) / p.den;
+    const float df2 = FV3_DIV(d0 * (p.c1 * delq_k + p.c2 * delq_km), p.den);
     return fsign(fmin3(fabsf(df2), fmax3(qm1, q0, qp1) - q0, q0 - fmin3(qm1, q0, qp1)), df2);
 }
 
@@ -54,59 +58,14 @@ FV3_HD inline AlShared ppm_al_shared(float dm2, float dm1, float d0, float dp1)
     const float d4km = dm2 + dm1;  // d4(k-1)
     const float d4k = dm1 + d0;    // d4(k)
     const float d4kp = d0 + dp1;   // d4(k+1)
-    const float a1 = d4km / (d4k + dm1);
-    const float a2 = d4kp / (d4k + d0);
-    return AlShared{d4k, 2.0f / (d4km + d4kp), a1 - a2, a2, dm1 * a1};
+    const float a1 = FV3_DIV(d4km, d4k + dm1);
+    const float a2 = FV3_DIV(d4kp, d4k + d0);
+    return AlShared{d4k, FV3_DIV(2.0f, d4km + d4kp), a1 - a2, a2, dm1 * a1};
 }
 FV3_HD inline float ppm_al_field(const AlShared& p, float dm1, float d0, float qm1, float q0, float dcm1, float dc0)
 {
-    const float c1 = (q0 - qm1) * dm1 / p.d4k;
+    const float c1 = FV3_DIV((q0 - qm1) * dm1, p.d4k);
     return qm1 + c1 + p.s2 * (d0 * (c1 * p.amd + p.a2 * dcm1) - p.dm1a1 * dc0);
-}
-
-// ---- the area-preserving end cubics, one field (mappm.f90:689-725, 729-761) ----
-
-FV3_HD inline void ppm_top_cubic(float q1, float q2, float d1, float d2, float al3, int iv, float& al1,
-                                 float& al2, float& dc1)
-{
-    const float qm = (d2 * q1 + d1 * q2) / (d1 + d2);
-    const float dq = 2.0f * (q2 - q1) / (d1 + d2);
-    const float c1 = 4.0f * (al3 - qm - d2 * dq) / (d2 * (2.0f * d2 * d2 + d1 * (d2 + 3.0f * d1)));
-    const float c3 = dq - 0.5f * c1 * (d2 * (5.0f * d1 + d2) - 3.0f * d1 * d1);
-    al2 = qm - 0.25f * c1 * d1 * d2 * (d2 + 3.0f * d1);
-    al1 = d1 * (2.0f * c1 * (d1 * d1) - c3) + al2;
-    al2 = fmax2(al2, fmin2(q1, q2));
-    al2 = fmin2(al2, fmax2(q1, q2));
-    dc1 = 0.5f * (al2 - q1);
-    if (iv == 0) {
-        al1 = fmax2(0.0f, al1);
-        al2 = fmax2(0.0f, al2);
-    } else if (iv == -1) {
-        if (al1 * q1 <= 0.0f) al1 = 0.0f;
-    } else if (iv == 2 || iv == -2) {
-        al1 = q1;
-    }
-}
-
-// d1 = dp(km), d2 = dp(km-1), qk = q(km), qk1 = q(km-1), alk1 = ALraw(km-1)
-FV3_HD inline void ppm_bottom_cubic(float qk, float qk1, float d1, float d2, float alk1, int iv, float& alm,
-                                    float& ar, float& dcm)
-{
-    const float qm = (d2 * qk + d1 * qk1) / (d1 + d2);
-    const float dq = 2.0f * (qk1 - qk) / (d1 + d2);
-    const float c1 = (alk1 - qm - d2 * dq) / (d2 * (2.0f * d2 * d2 + d1 * (d2 + 3.0f * d1)));
-    const float c3 = dq - 2.0f * c1 * (d2 * (5.0f * d1 + d2) - 3.0f * d1 * d1);
-    alm = qm - c1 * d1 * d2 * (d2 + 3.0f * d1);
-    ar = d1 * (8.0f * c1 * (d1 * d1) - c3) + alm;
-    alm = fmax2(alm, fmin2(qk, qk1));
-    alm = fmin2(alm, fmax2(qk, qk1));
-    dcm = 0.5f * (qk - alm);
-    if (iv == 0) {
-        alm = fmax2(0.0f, alm);
-        ar = fmax2(0.0f, ar);
-    } else if (iv < 0) {
-        if (qk * ar <= 0.0f) ar = 0.0f;
-    }
 }
 
 // ---- remap consumer for NF fields (remap_layer_fast / remap_finish semantics) ----
@@ -148,13 +107,13 @@ FV3_HD inline void remap_layer_n(RemapStateN<NF>& s, const LayerViewN<NF>& v, co
         }
         // bottom piece (mappm.f90:105-112)
         const float delp = s.b - v.pl0;
-        const float esl = delp / v.dp;
+        const float esl = FV3_DIVQ(delp, v.dp);
         const float h = 0.5f * esl;
         const float w = 1.0f - r23 * esl;
         for (int f = 0; f < NF; ++f)
             s.qsum[f] = s.qsum[f] + delp * (v.al[f] + h * (v.ar[f] - v.al[f] + v.a6[f] * w));
         s.dpsum = s.dpsum + delp;
-        for (int f = 0; f < NF; ++f) out.emit(f, s.k, s.qsum[f] / s.dpsum);
+        for (int f = 0; f < NF; ++f) out.emit(f, s.k, FV3_DIVQ(s.qsum[f], s.dpsum));
         s.accum = false;
         s.k += 1;
         s.t = s.b;
@@ -175,11 +134,11 @@ FV3_HD inline void remap_layer_n(RemapStateN<NF>& s, const LayerViewN<NF>& v, co
             s.xv = false;
             continue;
         }
-        if (!s.xv) s.xt = (s.t - v.pl0) / v.dp;
+        if (!s.xv) s.xt = FV3_DIVQ(s.t - v.pl0, v.dp);
         if (s.b <= v.pl1) {
             // entire new layer inside input layer L (mappm.f90:76-83)
             const float pl = s.xt;
-            const float pr = (s.b - v.pl0) / v.dp;
+            const float pr = FV3_DIVQ(s.b - v.pl0, v.dp);
             const float tt = r3 * (pr * (pr + pl) + pl * pl);
             const float x = pr + pl;
             for (int f = 0; f < NF; ++f)
@@ -218,7 +177,7 @@ FV3_HD inline void remap_finish_n(RemapStateN<NF>& s, const ColumnEndsN<NF>& e, 
                 for (int f = 0; f < NF; ++f) s.qsum[f] = s.qsum[f] + delp * e.q_bot[f];
                 s.dpsum = s.dpsum + delp;
             }
-            for (int f = 0; f < NF; ++f) out.emit(f, s.k, s.qsum[f] / s.dpsum);
+            for (int f = 0; f < NF; ++f) out.emit(f, s.k, FV3_DIVQ(s.qsum[f], s.dpsum));
             s.accum = false;
         } else if (s.t <= e.pe_top) {
             for (int f = 0; f < NF; ++f) out.emit(f, s.k, e.q_top[f]);
@@ -368,7 +327,7 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord, i
                 if (huynh && k <= km - 1) {
                     const float hden = dw[j] + 0.5f * (dw[j - 1] + dw[j + 1]);
                     const float d0sq = dw[j] * dw[j];
-                    h2v[f][i] = 2.0f * (dcw[j + 1] / dw[j + 1] - dcw[j - 1] / dw[j - 1]) / hden * d0sq;
+                    h2v[f][i] = FV3_DIV(2.0f * (FV3_DIV(dcw[j + 1], dw[j + 1]) - FV3_DIV(dcw[j - 1], dw[j - 1])), hden) * d0sq;
                 } else {
                     h2v[f][i] = 0.0f;
                 }
@@ -404,7 +363,7 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord, i
             alv[f][0] = al1; alv[f][1] = al2; alv[f][2] = al3;
             h2v[f][0] = 0.0f; h2v[f][1] = 0.0f;
             // h2(2) = ppm_h2(dc1, dc3, dp(1), dp(2), dp(3))
-            h2v[f][2] = huynh ? 2.0f * (dc3 / dpv[2] - dc1 / dpv[0]) / hden * d0sq : 0.0f;
+            h2v[f][2] = huynh ? FV3_DIV(2.0f * (FV3_DIV(dc3, dpv[2]) - FV3_DIV(dc1, dpv[0])), hden) * d0sq : 0.0f;
             ar_km[f] = 0.0f;
         }
     }
@@ -530,7 +489,7 @@ FV3_HD inline void mappm_ppm_columns(Col& c, int km, int kn, int iv, int kord, i
             const float hden = dpv[2] + 0.5f * (dpv[1] + dpv[3]);
             const float d0sq = dpv[2] * dpv[2];
             for (int f = 0; f < NF; ++f) {
-                const float h2n = 2.0f * (dcm[f] / dpv[3] - dcv[f][1] / dpv[1]) / hden * d0sq;
+                const float h2n = FV3_DIV(2.0f * (FV3_DIV(dcm[f], dpv[3]) - FV3_DIV(dcv[f][1], dpv[1])), hden) * d0sq;
                 h2v[f][0] = h2v[f][1]; h2v[f][1] = h2v[f][2]; h2v[f][2] = h2n;
             }
         } else {
@@ -568,4 +527,8 @@ struct FirstField {
     FV3_HD void layer_done() { layer_hook(c, 0); }
 };
 
+#ifdef FV3_FAST_ARITH
+#pragma clang fp contract(off)
+#endif
+}  // namespace FV3_ARITH_NS
 }  // namespace fv3

@@ -18,11 +18,16 @@ except ImportError:  # pragma: no cover
     torch = None
 
 
-def mappm_device(pe1, q1, pe2, iv: int = 1, kord: int = 1, out=None, stream=None):
+def mappm_device(pe1, q1, pe2, iv: int = 1, kord: int = 1, out=None, stream=None, exact: bool = False):
     """Remap on device.  ``pe1 [km+1, ncol]``, ``q1 [km, ncol]``, ``pe2 [kn+1, ncol]``
     float32 CUDA tensors (column fastest, the Fortran pe1(i,k) order; strided views
     such as a column slice are read in place); returns ``q2 [kn, ncol]`` (or writes
-    ``out``).  Asynchronous on the current stream."""
+    ``out``).  Asynchronous on the current stream.
+
+    ``exact=False`` (default): north_star's floating-point contract (within 1e-5 rel of
+    the reference; reciprocal divisions, FMA, hardware MAX / MIN, csrc/mappm_core.h) for
+    finite inputs.  ``exact=True``: the reference build's arithmetic, bit for bit, for
+    every input (NaNs included)."""
     _device.require_gpu()
     for a in (pe1, q1, pe2):
         if len(getattr(a, "shape", ())) != 2:
@@ -42,7 +47,8 @@ def mappm_device(pe1, q1, pe2, iv: int = 1, kord: int = 1, out=None, stream=None
     lo, _, _ = _device.level_layout(out, 0)
     lib = _native.load()
     st = lib.fv3_mappm_ex(_device.ptr(pe1), l1, _device.ptr(q1), lq, _device.ptr(pe2), l2, _device.ptr(out), lo,
-                          ncol, km, kn, int(iv), int(kord), 0.0, _device.stream_handle(stream, [pe1, q1, pe2, out]))
+                          ncol, km, kn, int(iv), int(kord), 0.0, _native.arith(exact),
+                          _device.stream_handle(stream, [pe1, q1, pe2, out]))
     _native.check(st, "mappm")
     return out
 
@@ -54,8 +60,8 @@ class MappmPlan:
     C12 kernel itself).  The buffers must stay alive and keep their shapes; their
     contents may change between calls.  Same results as ``mappm_device``."""
 
-    def __init__(self, pe1, q1, pe2, iv: int = 1, kord: int = 1, out=None, stream=None):
-        self.out = mappm_device(pe1, q1, pe2, iv, kord, out=out, stream=stream)  # validates, first run
+    def __init__(self, pe1, q1, pe2, iv: int = 1, kord: int = 1, out=None, stream=None, exact: bool = False):
+        self.out = mappm_device(pe1, q1, pe2, iv, kord, out=out, stream=stream, exact=exact)  # validates, first run
         views = [_device.column_view(a, 0) for a in (pe1, q1, pe2)]
         for name, a, v in zip(("pe1", "q1", "pe2"), (pe1, q1, pe2), views):
             if not (torch.is_tensor(a) and a.is_cuda and v[0].data_ptr() == a.data_ptr()):
@@ -68,7 +74,7 @@ class MappmPlan:
         self._stream = stream
         self._fn = _native.load().fv3_mappm_ex
         self._args = (_device.ptr(pe1), l1, _device.ptr(q1), lq, _device.ptr(pe2), l2, _device.ptr(self.out), lo,
-                      ncol, km, kp2 - 1, int(iv), int(kord), 0.0, _device.stream_handle(stream))
+                      ncol, km, kp2 - 1, int(iv), int(kord), 0.0, _native.arith(exact), _device.stream_handle(stream))
 
     def __call__(self):
         if self._stream is not None:
@@ -79,7 +85,7 @@ class MappmPlan:
         return self.out
 
 
-def _multi_args(pe1, q1s, pe2, iv, kord, outs, stream):
+def _multi_args(pe1, q1s, pe2, iv, kord, outs, stream, exact):
     """Validated argument tuple of fv3_mappm_multi (+ the outputs and the tensors read)."""
     _device.require_gpu()
     q1s = list(q1s)
@@ -113,17 +119,18 @@ def _multi_args(pe1, q1s, pe2, iv, kord, outs, stream):
     op = (ctypes.c_void_p * nf)(*[_device.ptr(o) for o in outs])
     ol = (_native.Layout * nf)(*lo)
     args = (_device.ptr(pe1), l1, qp, ql, _device.ptr(pe2), l2, op, ol, nf, ncol, views[0][3], kn, int(iv),
-            int(kord), 0.0, _device.stream_handle(stream))
+            int(kord), 0.0, _native.arith(exact), _device.stream_handle(stream))
     return args, outs, [pe1, pe2] + [v[0] for v in views]
 
 
-def mappm_device_multi(pe1, q1s, pe2, iv: int = 1, kord: int = 1, out=None, stream=None):
+def mappm_device_multi(pe1, q1s, pe2, iv: int = 1, kord: int = 1, out=None, stream=None, exact: bool = False):
     """``mappm_device`` for several fields on the same ``pe1`` / ``pe2`` (one reference
     ``mappm.mappm`` call per field, as ``coarsen_restarts_on_pressure`` issues them,
     coarsen_restarts.py:411-516): for kord <= 7 the fields go two per streaming pass,
-    sharing the pressure-only arithmetic; each result is bit-identical to
-    ``mappm_device`` on that field.  Returns the list of ``[kn, ncol]`` outputs."""
-    args, outs, keep = _multi_args(pe1, q1s, pe2, iv, kord, out, stream)
+    sharing the pressure-only arithmetic; with ``exact=True`` each result is
+    bit-identical to ``mappm_device(..., exact=True)`` on that field (the default
+    arithmetic as in ``mappm_device``).  Returns the list of ``[kn, ncol]`` outputs."""
+    args, outs, keep = _multi_args(pe1, q1s, pe2, iv, kord, out, stream, exact)
     _native.check(_native.load().fv3_mappm_multi(*args), "mappm")
     _device.keep_for(stream, keep + outs)
     return outs
@@ -133,9 +140,9 @@ class MappmMultiPlan:
     """``MappmPlan`` for ``mappm_device_multi``: one C-ABI call per step on fixed
     float32 CUDA buffers (read in place; a copy would go stale, so it is refused)."""
 
-    def __init__(self, pe1, q1s, pe2, iv: int = 1, kord: int = 1, out=None, stream=None):
+    def __init__(self, pe1, q1s, pe2, iv: int = 1, kord: int = 1, out=None, stream=None, exact: bool = False):
         q1s = list(q1s)
-        args, self.out, keep = _multi_args(pe1, q1s, pe2, iv, kord, out, stream)
+        args, self.out, keep = _multi_args(pe1, q1s, pe2, iv, kord, out, stream, exact)
         for name, a, v in zip(["pe1", "pe2"] + [f"q1[{i}]" for i in range(len(q1s))], [pe1, pe2] + q1s, keep):
             if not (torch.is_tensor(a) and a.is_cuda and v.data_ptr() == a.data_ptr()):
                 raise ValueError(f"MappmMultiPlan: {name} is read through a copy (host, float64 or an "
@@ -159,7 +166,8 @@ def mappm(pe1, q1, pe2, i1, i2, iv, kord, ptop):
     ``pe1 (ncol, km+1)``, ``q1 (ncol, km)``, ``pe2 (ncol, kn+1)`` host arrays.  As in the
     f2py signature (``pe1(i1:i2, km+1)``), the arrays hold exactly the columns
     ``i1..i2`` (1-based, inclusive): ``ncol == i2 - i1 + 1``; returns float32
-    ``(ncol, kn)``.
+    ``(ncol, kn)``.  The reference's own arithmetic (``exact=True``): this is the drop-in
+    for the f2py module, bit-identical to it.
     """
     i1 = int(i1)
     i2 = int(i2)
@@ -170,5 +178,5 @@ def mappm(pe1, q1, pe2, i1, i2, iv, kord, ptop):
         raise ValueError("mappm expects 2-D (column, level) arrays")
     if not (pe1.shape[0] == q1.shape[0] == pe2.shape[0] == i2 - i1 + 1):
         raise ValueError(f"mappm: arrays hold {pe1.shape[0]} columns, i1..i2 = {i1}..{i2} names {i2 - i1 + 1}")
-    res = mappm_device(pe1.T, q1.T, pe2.T, iv=int(iv), kord=int(kord))
+    res = mappm_device(pe1.T, q1.T, pe2.T, iv=int(iv), kord=int(kord), exact=True)
     return res.T.contiguous().cpu().numpy()

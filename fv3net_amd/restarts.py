@@ -106,9 +106,11 @@ def impose_hydrostatic_balance(temperature, sphum, delp, dz, phis, ptop: float =
 
 def coarsen_restarts_on_pressure(coarsening_factor: int, grid_spec: Mapping[str, object],
                                  restarts: Mapping[str, Mapping[str, object]], coarsen_agrid_winds: bool = False,
-                                 iv: int = 1, kord: int = 1, stream=None) -> Dict[str, Dict[str, object]]:
+                                 iv: int = 1, kord: int = 1, stream=None,
+                                 exact: bool = False) -> Dict[str, Dict[str, object]]:
     """coarsen_restarts_on_pressure (coarsen_restarts.py:152-225) for fv_core.res,
-    fv_tracer.res and (if given) fv_srf_wnd.res.  Returns {category: {name: tensor}}."""
+    fv_tracer.res and (if given) fv_srf_wnd.res.  Returns {category: {name: tensor}}.
+    ``exact`` selects the pressure remap's arithmetic (``coarsen.coarsen_on_pressure``)."""
     _device.require_gpu()
     if "sfc_data" in restarts:
         raise NotImplementedError("sfc_data ('complex' surface coarsening) is outside this build's scope; "
@@ -139,14 +141,14 @@ def coarsen_restarts_on_pressure(coarsening_factor: int, grid_spec: Mapping[str,
     keys = list(fused)
     names = [f"{c}:{n}" for c, n in keys]
     res, delp_c = coarsen_on_pressure(delp, area, dict(zip(names, (fused[k] for k in keys))), f, iv, kord,
-                                      stream=stream, coarse_delp_f64=True)
+                                      stream=stream, coarse_delp_f64=True, exact=exact)
     out_core = {n: res[f"c:{n}"] for n in masked}
     out_tracer = {n: res[f"t:{n}"] for n in tracer_names}
     out_core["delp"] = delp_c
     out_core["u"] = coarsen_edges_on_pressure(delp, grid_spec["dx"], {"u": strip(core["u"])}, f, "x", iv, kord,
-                                              stream=stream)["u"]
+                                              stream=stream, exact=exact)["u"]
     out_core["v"] = coarsen_edges_on_pressure(delp, grid_spec["dy"], {"v": strip(core["v"])}, f, "y", iv, kord,
-                                              stream=stream)["v"]
+                                              stream=stream, exact=exact)["v"]
     plain = weighted_block_average({"phis": strip(core["phis"]), "DZ": strip(core["DZ"])}, area, f, stream)
     out_core["DZ"], out_core["phis"] = impose_hydrostatic_balance(out_core["T"], out_tracer["sphum"], delp_c,
                                                                   plain["DZ"], plain["phis"], stream=stream)

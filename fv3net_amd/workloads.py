@@ -90,6 +90,7 @@ class MappmWorkload:
     kn: int
     kord: int
     iv: int = 1
+    exact: bool = False  # the remap arithmetic (mappm_device)
 
     @property
     def bytes_per_column(self) -> int:
@@ -101,12 +102,13 @@ class MappmWorkload:
         from .mappm import MappmPlan
 
         if self.plan is None:  # prepared once: each step is one C-ABI call
-            self.plan = MappmPlan(self.pe1, self.q1, self.pe2, self.iv, self.kord, out=self.q2)
+            self.plan = MappmPlan(self.pe1, self.q1, self.pe2, self.iv, self.kord, out=self.q2, exact=self.exact)
         else:
             self.plan()
 
 
-def make_mappm_workload(ncol: int, km: int = NZ, kn: int = NZ, kord: int = 1, seed: int = 0, device=None):
+def make_mappm_workload(ncol: int, km: int = NZ, kn: int = NZ, kord: int = 1, seed: int = 0, device=None,
+                        exact: bool = False):
     """Monotone columns: delp ~ D(k) * U(0.99, 1.01) (a 79-level reference profile,
     cf. synth/_restarts.py:36-38), p_out = a neighbour's edges (kn == km) or kn+1
     evenly spaced edges (config #1), shared 300 Pa top."""
@@ -125,7 +127,7 @@ def make_mappm_workload(ncol: int, km: int = NZ, kn: int = NZ, kord: int = 1, se
         pe2 = pe1[:1] + frac * (pe1[-1:] - pe1[:1])
     q1 = torch.randn((km, ncol), generator=g, device=device) * 10.0 + 250.0
     q2 = torch.empty((kn, ncol), device=device)
-    return MappmWorkload(pe1.contiguous(), q1, pe2.contiguous(), q2, ncol, km, kn, kord)
+    return MappmWorkload(pe1.contiguous(), q1, pe2.contiguous(), q2, ncol, km, kn, kord, exact=exact)
 
 
 @dataclasses.dataclass
@@ -137,6 +139,7 @@ class CoarsenWorkload:
     factor: int
     ncol_fine: int
     km: int
+    exact: bool = False  # the remap arithmetic (coarsen_on_pressure)
 
     @property
     def bytes_per_column(self) -> float:
@@ -148,10 +151,11 @@ class CoarsenWorkload:
     def step(self):
         from .coarsen import coarsen_on_pressure
 
-        return coarsen_on_pressure(self.delp, self.area, self.fields, self.factor)
+        return coarsen_on_pressure(self.delp, self.area, self.fields, self.factor, exact=self.exact)
 
 
-def make_coarsen_workload(res: int = 384, factor: int = 8, nfields: int = 1, seed: int = 0, device=None):
+def make_coarsen_workload(res: int = 384, factor: int = 8, nfields: int = 1, seed: int = 0, device=None,
+                          exact: bool = False):
     """delp ~ D(k) * U(0.99, 1.01) (79-level profile), area ~ U(0.5, 1), T ~ N(250, 10); float32."""
     device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
     g = torch.Generator(device=device)
@@ -161,7 +165,7 @@ def make_coarsen_workload(res: int = 384, factor: int = 8, nfields: int = 1, see
     delp = base * (0.99 + 0.02 * torch.rand(shape, generator=g, device=device))
     area = 0.5 + 0.5 * torch.rand((6, res, res), generator=g, device=device)
     fields = {f"f{i}": torch.randn(shape, generator=g, device=device) * 10.0 + 250.0 for i in range(nfields)}
-    return CoarsenWorkload(delp, area, fields, factor, 6 * res * res, NZ)
+    return CoarsenWorkload(delp, area, fields, factor, 6 * res * res, NZ, exact)
 
 
 @dataclasses.dataclass

@@ -59,7 +59,9 @@ int fv3_abi_version(void); /* bumped on any signature change (2: emulator fields
                               9: fv3_host_alloc / free / copy, the arena, replace
                                  fv3_host_register / unregister; wind rotation,
                                  fv3_sum_squares, fv3_cos_zenith,
-                              10: fv3_step_partials_f64, fv3_fold_rows_repeat) */
+                              10: fv3_step_partials_f64, fv3_fold_rows_repeat,
+                              11: the `arith` argument of fv3_mappm_ex / _multi and of the
+                                  fused coarsen entries) */
 const char* fv3_build_kind(void); /* "product" (fv3net_amd/build.py, no experiment knob compiled in)
                                      or "experiment" (a tools/ variant: results may be invalid) */
 
@@ -80,14 +82,26 @@ typedef struct {
  * pe1 [km+1][ncol] input edge pressures (top -> surface), q1 [km][ncol] layer means,
  * pe2 [kn+1][ncol] output edges, q2 [kn][ncol] result.  float32, column fastest
  * (exactly the Fortran pe1(i,k) order).  iv, kord as in the reference; ptop is
- * accepted and ignored, as in the reference (regridz.py:270).  km >= 4. */
+ * accepted and ignored, as in the reference (regridz.py:270).  km >= 4.
+ *
+ * `arith` selects the remap arithmetic (fv3_mappm_ex, fv3_mappm_multi and the fused
+ * coarsen entries; fv3_mappm, the f2py signature, is always FV3_ARITH_EXACT):
+ *   FV3_ARITH_EXACT  the reference build's arithmetic: IEEE divisions, no FMA
+ *                    contraction, Fortran's order-dependent MAX / MIN -> bit-identical
+ *                    to the flang-compiled mappm.f90 for every input, NaNs included;
+ *   FV3_ARITH_FAST   north_star's floating-point contract (1e-5 rel): divisions by
+ *                    v_rcp_f32 reciprocals, FMA within an expression, hardware MAX / MIN
+ *                    (csrc/mappm_core.h).  Same algorithm and limiter logic; finite
+ *                    inputs only (a NaN operand of MAX / MIN is dropped, not propagated). */
+#define FV3_ARITH_EXACT 0
+#define FV3_ARITH_FAST 1
 int fv3_mappm(const float* pe1, const float* q1, const float* pe2, float* q2, int64_t ncol,
               int km, int kn, int iv, int kord, float ptop, void* stream);
 
 /* Same with an explicit layout per array (e.g. (tile, z, y, x) data in place). */
 int fv3_mappm_ex(const float* pe1, fv3_layout pe1_l, const float* q1, fv3_layout q1_l,
                  const float* pe2, fv3_layout pe2_l, float* q2, fv3_layout q2_l, int64_t ncol,
-                 int km, int kn, int iv, int kord, float ptop, void* stream);
+                 int km, int kn, int iv, int kord, float ptop, int arith, void* stream);
 
 /* n_fields fields remapped onto the same edges: one mappm.mappm call per variable on a
  * shared p_in / p_out, as regrid_vertical is used by coarsen_restarts_on_pressure
@@ -98,7 +112,8 @@ int fv3_mappm_ex(const float* pe1, fv3_layout pe1_l, const float* q1, fv3_layout
  * the bits of fv3_mappm_ex on that field alone.  1 <= n_fields <= 64. */
 int fv3_mappm_multi(const float* pe1, fv3_layout pe1_l, const float* const* q1, const fv3_layout* q1_l,
                     const float* pe2, fv3_layout pe2_l, float* const* q2, const fv3_layout* q2_l,
-                    int n_fields, int64_t ncol, int km, int kn, int iv, int kord, float ptop, void* stream);
+                    int n_fields, int64_t ncol, int km, int kn, int iv, int kord, float ptop, int arith,
+                    void* stream);
 
 /* ---- dense column model: DenseModel predict graph (dense.py:234-305) ----------
  * inputs -> per-input clip (clip.py:65-83) -> StandardNormLayer (x-mean)/(sigma+eps)
@@ -193,25 +208,26 @@ int fv3_dense_forward_ex(const fv3_dense_model* model, const float* const* input
  * kernel, nothing is allocated per call); 4 <= km <= 128, 1 <= factor <= 8, kord <= 7.
  * Arithmetic follows the reference's dtype flow: delp products, delp_c and the phalf
  * cumsums in delp's dtype, area and field sums in float32, block sums in numpy's
- * order for the reshaped coarsen().sum() — bit-exact to oracle/coarsen.py. */
+ * order for the reshaped coarsen().sum() — bit-exact to oracle/coarsen.py with
+ * FV3_ARITH_EXACT; FV3_ARITH_FAST remaps under the tolerance contract (see fv3_mappm). */
 int fv3_regrid_coarsen(const float* delp, const float* area, const float* const* fields,
                        float* const* out, int n_fields, float* delp_out, int ntile, int km,
                        int ny, int nx, int factor, int iv, int kord, double ptop_toa,
-                       void* stream);
+                       int arith, void* stream);
 
 /* Same with float64 delp (FV3 fv_core restarts store delp in double precision; the
  * pressures are cumulated in float64 either way). */
 int fv3_regrid_coarsen_f64(const double* delp, const float* area, const float* const* fields,
                            float* const* out, int n_fields, float* delp_out, int ntile, int km,
                            int ny, int nx, int factor, int iv, int kord, double ptop_toa,
-                           void* stream);
+                           int arith, void* stream);
 
 /* Same, with the coarse delp returned in float64 (restart precision, as
  * weighted_block_average(delp, area) gives it in coarsen_restarts.py:480-486). */
 int fv3_regrid_coarsen_f64d(const double* delp, const float* area, const float* const* fields,
                             float* const* out, int n_fields, double* delp_out, int ntile, int km,
                             int ny, int nx, int factor, int iv, int kord, double ptop_toa,
-                            void* stream);
+                            int arith, void* stream);
 
 /* ---- the rest of coarsen_restarts_on_pressure (coarsen_restarts.py:152-225) -------
  * fv3_weighted_block_average[_f64]: sum(obj * w) / sum(w) over factor x factor blocks
@@ -253,11 +269,12 @@ int fv3_hydrostatic_balance(const float* temperature, const float* sphum, const 
  * coarsen_edges_on_pressure. */
 int fv3_regrid_coarsen_edge(const float* delp, const float* spacing, const float* const* fields,
                             float* const* out, int n_fields, int ntile, int km, int ny, int nx,
-                            int factor, int edge, int iv, int kord, double ptop_toa, void* stream);
+                            int factor, int edge, int iv, int kord, double ptop_toa, int arith,
+                            void* stream);
 int fv3_regrid_coarsen_edge_f64(const double* delp, const float* spacing,
                                 const float* const* fields, float* const* out, int n_fields,
                                 int ntile, int km, int ny, int nx, int factor, int edge, int iv,
-                                int kord, double ptop_toa, void* stream);
+                                int kord, double ptop_toa, int arith, void* stream);
 
 /* ---- per-column reductions for stepper diagnostics --------------------------------
  * out[c] = sum_k field[k][c] * delp[k][c] * scale  (vcm mass_integrate,

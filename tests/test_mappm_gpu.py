@@ -51,7 +51,7 @@ def test_reference_kats_through_f2py_signature(gpu):
 
 
 def test_golden_vectors_bit_exact(gpu):
-    from fv3net_amd.mappm import mappm_device
+    from tests.remap_exact import mappm_device
 
     g = np.load(os.path.join(GOLDEN, "mappm_golden.npz"))
     for ci in range(len(g["cases"])):
@@ -79,7 +79,7 @@ def _columns(rng, km, kn, ncol):
 
 @pytest.mark.parametrize("km,kn,ncol", [(4, 3, 1), (5, 9, 257), (79, 50, 1000), (79, 79, 777), (127, 40, 300)])
 def test_random_vs_oracle_bit_exact(gpu, km, kn, ncol):
-    from fv3net_amd.mappm import mappm_device
+    from tests.remap_exact import mappm_device
 
     rng = np.random.default_rng(km + kn + ncol)
     pe1, q, pe2 = _columns(rng, km, kn, ncol)
@@ -93,7 +93,7 @@ def test_random_vs_oracle_bit_exact(gpu, km, kn, ncol):
 def test_cs_lds_path_vs_oracle_bit_exact(gpu, km, kn, ncol, monkeypatch):
     """kord > 7 with the edge-solve scratch in LDS (FV3_MAPPM_LDS=1) instead of the
     default global scratch: the same arithmetic, bit-identical."""
-    from fv3net_amd.mappm import mappm_device
+    from tests.remap_exact import mappm_device
 
     set_variant(monkeypatch, "FV3_MAPPM_LDS", "1")
     rng = np.random.default_rng(km * kn + ncol)
@@ -113,7 +113,7 @@ def test_cs_kernel_variants_vs_oracle_bit_exact(gpu, nt, pf, c32, kspec, monkeyp
     offsets or 64-bit addresses, the column specialised for kord 10 (the default load
     distances with buffer operations) or not: the same bits as the oracle, on level counts
     around the blocks' remainders."""
-    from fv3net_amd.mappm import mappm_device
+    from tests.remap_exact import mappm_device
 
     if mappm_path != "serial":
         pytest.skip("kord > 7 has one kernel family; run once")
@@ -136,7 +136,7 @@ def test_c384_scale_kord10_sampled_bit_exact(gpu):
     bit-exact against the oracle."""
     import torch
 
-    from fv3net_amd.mappm import mappm_device
+    from tests.remap_exact import mappm_device
 
     rng = np.random.default_rng(3841)
     ncol, km = 6 * 384 * 384, 79
@@ -174,7 +174,8 @@ def test_tile_layout_in_place(gpu):
     lays = [_device.level_layout(t, 1)[0] for t in dev + [out]]
     lib = _native.load()
     st = lib.fv3_mappm_ex(dev[0].data_ptr(), lays[0], dev[1].data_ptr(), lays[1], dev[2].data_ptr(), lays[2],
-                          out.data_ptr(), lays[3], ncol, km, km, 1, 1, 0.0, _device.stream_handle())
+                          out.data_ptr(), lays[3], ncol, km, km, 1, 1, 0.0, _native.ARITH_EXACT,
+                          _device.stream_handle())
     _native.check(st)
     got = out.cpu().numpy().reshape(ntile, km, ny * nx).transpose(1, 0, 2).reshape(km, ncol)
     assert _bits_equal(got, oracle_mappm(pe1, q, pe2, 1, 1))
@@ -183,7 +184,7 @@ def test_tile_layout_in_place(gpu):
 def test_empty_and_errors(gpu):
     import torch
 
-    from fv3net_amd.mappm import mappm_device
+    from tests.remap_exact import mappm_device
 
     e = mappm_device(np.zeros((80, 0)), np.zeros((79, 0)), np.zeros((51, 0)))
     assert tuple(e.shape) == (50, 0)
@@ -201,7 +202,7 @@ def test_c384_scale_sampled_bit_exact(gpu):
     bit-exact against the oracle, plus whole-array finiteness."""
     import torch
 
-    from fv3net_amd.mappm import mappm_device
+    from tests.remap_exact import mappm_device
 
     rng = np.random.default_rng(384)
     ncol, km = 6 * 384 * 384, 79
@@ -228,7 +229,7 @@ def test_unsorted_edges_fall_back_per_column(gpu, monkeypatch):
     (mappm.f90:58-124 leaves q2 undefined), where the product writes NaN, so there only
     the two kernels are compared."""
 
-    from fv3net_amd.mappm import mappm_device
+    from tests.remap_exact import mappm_device
 
     rng = np.random.default_rng(5)
     km, kn, ncol = 79, 50, 300
@@ -254,7 +255,7 @@ def test_prepared_plan_matches_and_tracks_contents(gpu):
     mappm_device, and it sees in-place updates of the inputs."""
     import torch
 
-    from fv3net_amd.mappm import MappmPlan, mappm_device
+    from tests.remap_exact import MappmPlan, mappm_device
 
     rng = np.random.default_rng(21)
     pe1, q, pe2 = _columns(rng, 79, 50, 864)
@@ -272,7 +273,7 @@ def test_prepared_plan_refuses_copies(gpu):
     snapshot: MappmPlan refuses it."""
     import torch
 
-    from fv3net_amd.mappm import MappmPlan
+    from tests.remap_exact import MappmPlan
 
     rng = np.random.default_rng(22)
     pe1, q, pe2 = _columns(rng, 79, 50, 64)

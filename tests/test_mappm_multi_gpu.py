@@ -39,7 +39,7 @@ def _fields(rng, km, ncol, n):
 @pytest.mark.parametrize("km,kn,ncol,nf", [(4, 3, 1, 2), (5, 9, 257, 3), (79, 50, 1000, 2), (79, 79, 777, 5),
                                            (127, 40, 300, 4)])
 def test_multi_equals_single_and_oracle(gpu, path, km, kn, ncol, nf):
-    from fv3net_amd.mappm import mappm_device, mappm_device_multi
+    from tests.remap_exact import mappm_device, mappm_device_multi
 
     rng = np.random.default_rng(km * 7 + kn + ncol + nf)
     pe1, q0, pe2 = _columns(rng, km, kn, ncol)
@@ -59,7 +59,7 @@ def test_multi_c384_pair_kernel_sampled(gpu, monkeypatch):
     whole arrays equal to the single-field kernel, sampled columns to the oracle."""
     import torch
 
-    from fv3net_amd.mappm import mappm_device, mappm_device_multi
+    from tests.remap_exact import mappm_device, mappm_device_multi
 
     set_variant(monkeypatch, "FV3_MAPPM_PATH", "serial")
     rng = np.random.default_rng(385)
@@ -85,7 +85,7 @@ def test_multi_tile_layout_in_place(gpu, monkeypatch):
     output written into a slice of a larger array)."""
     import torch
 
-    from fv3net_amd.mappm import mappm_device_multi
+    from tests.remap_exact import mappm_device_multi
 
     set_variant(monkeypatch, "FV3_MAPPM_PATH", "serial")
     rng = np.random.default_rng(8)
@@ -114,7 +114,7 @@ def test_multi_tile_layout_in_place(gpu, monkeypatch):
     op = (ctypes.c_void_p * 2)(outs[0].data_ptr(), outs[1].data_ptr())
     ol = (_native.Layout * 2)(lays[4], lays[5])
     st = _native.load().fv3_mappm_multi(pe1_t.data_ptr(), lays[0], qp, ql, pe2_t.data_ptr(), lays[1], op, ol, 2,
-                                         ncol, km, km, 1, 1, 0.0, _device.stream_handle())
+                                         ncol, km, km, 1, 1, 0.0, _native.ARITH_EXACT, _device.stream_handle())
     _native.check(st)
     for q, o in zip((q0, q1), outs):
         assert _bits_equal(from_t(o), oracle_mappm(pe1, q, pe2, 1, 1))
@@ -123,7 +123,7 @@ def test_multi_tile_layout_in_place(gpu, monkeypatch):
 def test_multi_plan_tracks_contents_and_refuses_copies(gpu, path):
     import torch
 
-    from fv3net_amd.mappm import MappmMultiPlan
+    from tests.remap_exact import MappmMultiPlan
 
     rng = np.random.default_rng(24)
     pe1, q0, pe2 = _columns(rng, 79, 50, 864)
@@ -145,7 +145,7 @@ def test_multi_plan_tracks_contents_and_refuses_copies(gpu, path):
 def test_multi_errors(gpu):
     import torch
 
-    from fv3net_amd.mappm import mappm_device_multi
+    from tests.remap_exact import mappm_device_multi
 
     z = lambda *s: torch.zeros(s, device="cuda")  # noqa: E731
     assert [tuple(o.shape) for o in mappm_device_multi(z(80, 0), [z(79, 0)] * 3, z(51, 0))] == [(50, 0)] * 3
@@ -165,7 +165,7 @@ def test_multi_on_a_side_stream(gpu, path):
     there) and keeps its temporaries alive until that stream is done: same bits."""
     import torch
 
-    from fv3net_amd.mappm import mappm_device, mappm_device_multi
+    from tests.remap_exact import mappm_device, mappm_device_multi
 
     rng = np.random.default_rng(31)
     pe1, q0, pe2 = _columns(rng, 79, 50, 3000)
@@ -192,7 +192,7 @@ def test_two_lane_pair_kernel_rank_share_size(gpu, kn, monkeypatch):
     DESIGN.md §4): there the two kernels must agree with each other only."""
     import torch
 
-    from fv3net_amd.mappm import mappm_device_multi
+    from tests.remap_exact import mappm_device_multi
 
     rng = np.random.default_rng(110592 + kn)
     ncol, km = 110592, 79
@@ -241,7 +241,7 @@ def test_single_field_split_lanes_default(gpu, ncol, monkeypatch):
     (the one-lane pair kernel); sampled sorted columns equal the oracle."""
     import torch
 
-    from fv3net_amd.mappm import mappm_device
+    from tests.remap_exact import mappm_device
 
     rng = np.random.default_rng(ncol)
     km, kn = 79, 79
@@ -274,7 +274,7 @@ def test_single_field_split_lanes_default(gpu, ncol, monkeypatch):
     monkeypatch.delenv("FV3_MAPPM_SPLIT1", raising=False)
     set_variant(monkeypatch, "FV3_MAPPM_PATH", "serial")
     set_variant(monkeypatch, "FV3_MAPPM_SPLIT", "0")
-    from fv3net_amd.mappm import mappm_device_multi
+    from tests.remap_exact import mappm_device_multi
     multi = mappm_device_multi(d[0], [d[1], d[1]], d[2], 1, 1)[0].cpu().numpy()
     for name in ("default", "two", "three"):
         assert _bits_equal(runs[name][:, bad], multi[:, bad]), name
@@ -290,7 +290,7 @@ def test_split_defaults_small_level_counts(gpu, km, kn, monkeypatch):
     one lane per column, and to the oracle on sampled columns."""
     import torch
 
-    from fv3net_amd.mappm import mappm_device, mappm_device_multi
+    from tests.remap_exact import mappm_device, mappm_device_multi
 
     rng = np.random.default_rng(km * 100 + kn)
     ncol = 30000

@@ -69,7 +69,7 @@ def test_oracle_tracer_set_is_the_reference_list():
 
 @pytest.mark.gpu
 def test_device_tracer_set_is_the_reference_list(gpu):
-    from fv3net_amd.restarts import FRACTION_TRACERS, NON_FRACTION_TRACERS, coarsen_restarts_on_pressure
+    from tests.remap_exact import FRACTION_TRACERS, NON_FRACTION_TRACERS, coarsen_restarts_on_pressure
 
     grid, restarts = OR.kat_inputs()
     extra = dict(restarts["fv_tracer.res"], extra_tracer=restarts["fv_tracer.res"]["sphum"])
@@ -111,7 +111,7 @@ def _compare_to_oracle(got, ref):
 def test_device_matches_reference_regression_data(gpu, tag, agrid):
     """Every variable of both regression files, at the reference test's tolerance, and
     the device result against the oracle (bitwise except the log-based DZ / phis)."""
-    from fv3net_amd.restarts import coarsen_restarts_on_pressure
+    from tests.remap_exact import coarsen_restarts_on_pressure
 
     grid, restarts = OR.kat_inputs()
     got = _to_np(coarsen_restarts_on_pressure(2, grid, restarts, coarsen_agrid_winds=agrid))
@@ -151,7 +151,7 @@ def test_device_matches_oracle_79_levels(gpu, with_time):
     every output variable against the oracle; inputs with or without the Time axis."""
     import torch
 
-    from fv3net_amd.restarts import coarsen_restarts_on_pressure
+    from tests.remap_exact import coarsen_restarts_on_pressure
 
     grid, restarts, with_t = _random_restarts(np.random.default_rng(32), 32, 79, with_time)
     got = coarsen_restarts_on_pressure(4, grid, restarts, coarsen_agrid_winds=True)
@@ -167,7 +167,7 @@ def test_device_matches_oracle_79_levels(gpu, with_time):
 @pytest.mark.parametrize("factor", [1, 2, 3, 8])
 def test_weighted_block_average_bitwise(gpu, dtype, factor):
     """fv3_weighted_block_average[_f64] vs numpy's nansum order, NaN inputs skipped."""
-    from fv3net_amd.restarts import weighted_block_average
+    from tests.remap_exact import weighted_block_average
 
     rng = np.random.default_rng(factor)
     n = 8 * factor
@@ -186,7 +186,7 @@ def test_weighted_block_average_bitwise(gpu, dtype, factor):
 
 @pytest.mark.gpu
 def test_errors_match_reference(gpu):
-    from fv3net_amd.restarts import coarsen_restarts_on_pressure
+    from tests.remap_exact import coarsen_restarts_on_pressure
 
     grid, restarts = OR.kat_inputs()
     no_ua = dict(restarts)
