@@ -81,12 +81,15 @@ EXPORTED_SYMBOLS = (
     "fv3_host_alloc",
     "fv3_host_free",
     "fv3_host_arena_limit",
+    "fv3_host_arena_cap",
     "fv3_host_memory_stats",
     "fv3_copy_to_host",
     "fv3_copy_2d",
     "fv3_center_rotate_winds",
     "fv3_sum_squares",
     "fv3_cos_zenith",
+    "fv3_minmax_scores",
+    "fv3_taper_columns",
 )
 ABI_VERSION = 11
 # the remap arithmetic of fv3_mappm_ex / _multi and the fused coarsen entries
@@ -197,6 +200,25 @@ class Field(ctypes.Structure):
 
 MAX_DIMS = 6
 
+# the out-of-sample composite (fv3_minmax_scores / fv3_taper_columns)
+NOV_MAX_VARS = 16
+NOV_MAX_FIELDS = 16
+TAPER_MASK = 0
+TAPER_RAMP = 1
+TAPER_DECAY = 2
+
+
+class NovVar(ctypes.Structure):
+    """fv3_nov_var: one input variable of the min-max detector, levels [z0, z0 + nfeat)."""
+    _fields_ = [("data", ctypes.c_void_p), ("layout", Layout), ("data_f64", ctypes.c_int), ("z0", ctypes.c_int),
+                ("nfeat", ctypes.c_int)]
+
+
+class TaperField(ctypes.Structure):
+    """fv3_taper_field: one base-model output and its tapered result."""
+    _fields_ = [("inp", ctypes.c_void_p), ("in_layout", Layout), ("in_f64", ctypes.c_int), ("out", ctypes.c_void_p),
+                ("out_layout", Layout), ("nz", ctypes.c_int)]
+
 
 class Strided(ctypes.Structure):
     """fv3_strided: a float32 / float64 operand addressed by element strides over the dims
@@ -292,6 +314,7 @@ _SIGNATURES = {
     "fv3_host_alloc": (_I, [ctypes.c_size_t, ctypes.POINTER(_P)]),
     "fv3_host_free": (_I, [_P]),
     "fv3_host_arena_limit": (_I, [ctypes.c_size_t]),
+    "fv3_host_arena_cap": (_I, [ctypes.c_size_t]),
     "fv3_host_memory_stats": (_I, [ctypes.POINTER(ctypes.c_uint64)]),
     "fv3_plan_create": (_I, [ctypes.POINTER(_P)]),
     "fv3_plan_destroy": (_I, [_P]),
@@ -317,6 +340,8 @@ _SIGNATURES = {
     "fv3_center_rotate_winds": (_I, [_I, ctypes.POINTER(_I64), Strided, _I64, Strided, _I64, ctypes.POINTER(Strided),
                                      _P, _I, _P, _I, _P]),
     "fv3_sum_squares": (_I, [ctypes.POINTER(_P), ctypes.POINTER(_I), _I, _I64, _P, _P]),
+    "fv3_minmax_scores": (_I, [ctypes.POINTER(NovVar), _I, _P, _P, _I, _I, _I64, _P, _P]),
+    "fv3_taper_columns": (_I, [_P, _I, _I64, _I, _D, _D, _P, ctypes.POINTER(TaperField), _I, _P]),
     "fv3_cos_zenith": (_I, [_I, ctypes.POINTER(_I64), Strided, _I, Strided, _I, ctypes.POINTER(_I64), _P, _I64, _P,
                             _P]),
 }

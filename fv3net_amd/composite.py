@@ -16,8 +16,8 @@ the device; host arrays come back as host arrays).
 
 ``DerivedModel`` ("derived_model") and ``TransformedPredictor``
 ("output_transformed_model") live in derived.py, over the vcm.DerivedMapping /
-vcm.DataTransform catalogues.  Not mirrored: ``OutOfSampleModel`` (it needs a novelty
-detector, an sklearn model).
+vcm.DataTransform catalogues; ``OutOfSampleModel`` ("out_of_sample") with the min-max
+novelty detector in novelty.py.
 """
 import ctypes
 import dataclasses

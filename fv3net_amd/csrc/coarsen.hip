@@ -387,7 +387,7 @@ struct CellCol : FineCol<DT> {
             }
             mine[((int64_t)fi * ctx->km + k0) * ctx->sstride] = x;
         } else {
-            ctx->ring[fi * (ring_levels(NF) * kRingLd) + (k0 % ring_levels(NF)) * kRingLd + ctx->lane] = x;
+            ctx->ring[fi * (ring_levels(NF) * kRingLd) + ((unsigned)k0 % (unsigned)ring_levels(NF)) * kRingLd + ctx->lane] = x;
         }
     }
 

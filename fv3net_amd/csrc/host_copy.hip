@@ -28,6 +28,21 @@ __global__ __launch_bounds__(64) void copy_tail_kernel(const unsigned char* __re
     if ((int)threadIdx.x < n) dst[threadIdx.x] = src[threadIdx.x];
 }
 
+// Host memory page-locked by someone other than the library (torch pin_memory, a
+// hipHostRegister'ed buffer): the runtime's copy from / to it is a true asynchronous DMA,
+// unlike the staged pageable copy.  The copies below promise completion on return for
+// every non-arena host buffer, so those are waited for explicitly.
+bool foreign_page_locked(const void* host, size_t bytes)
+{
+    if (hostmem::inside((uintptr_t)host, bytes)) return false;  // the arena: asynchronous by contract
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, host) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory is unknown to the runtime
+        return false;
+    }
+    return at.type == hipMemoryTypeHost;
+}
+
 }  // namespace
 }  // namespace fv3
 
@@ -38,10 +53,12 @@ extern "C" int fv3_host_copy(void* dst, const void* src, size_t bytes, int kind,
     FV3_REQUIRE(dst && src, "host_copy: NULL pointer");
     FV3_REQUIRE(kind == 1 || kind == 2, "host_copy: kind %d (1: host to device, 2: device to host)", kind);
     if (!bytes) return FV3_OK;
-    // arena memory: asynchronous DMA; anything else: the runtime's pageable copy, which it
-    // completes before returning (the caller's buffer is free on return)
+    // arena memory: asynchronous DMA; pageable memory: the runtime's staged copy, which it
+    // completes before returning; memory page-locked elsewhere: waited for here, so the
+    // caller's buffer is free on return in both of the latter cases
     FV3_HIP(hipMemcpyAsync(dst, src, bytes, kind == 1 ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost,
                            (hipStream_t)stream));
+    if (foreign_page_locked(kind == 1 ? src : dst, bytes)) FV3_HIP(hipStreamSynchronize((hipStream_t)stream));
     return FV3_OK;
 }
 
@@ -87,7 +104,8 @@ extern "C" int fv3_copy_to_host(void* host_dst, const void* dev_src, size_t byte
 // [level][column] array is such a copy, one row per level (the pipelined host call over
 // column bands, bench.py predict + mappm host-to-host).  kind 1: host to device, 2:
 // device to host.  Asynchronous when the host rows are arena memory (fv3_host_alloc);
-// otherwise the runtime's pageable copy.
+// otherwise complete on return (the runtime's pageable copy, or waited for when the rows
+// are page-locked by someone else).
 extern "C" int fv3_copy_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height,
                            int kind, void* stream)
 {
@@ -99,5 +117,7 @@ extern "C" int fv3_copy_2d(void* dst, size_t dpitch, const void* src, size_t spi
     if (!width || !height) return FV3_OK;
     FV3_HIP(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height,
                              kind == 1 ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, (hipStream_t)stream));
+    const size_t span = (height - 1) * (kind == 1 ? spitch : dpitch) + width;
+    if (foreign_page_locked(kind == 1 ? src : dst, span)) FV3_HIP(hipStreamSynchronize((hipStream_t)stream));
     return FV3_OK;
 }

@@ -49,7 +49,11 @@ std::map<uintptr_t, Seg> g_segs;  // start -> block; blocks never overlap
 uint64_t g_next_id = 1;
 std::multimap<size_t, uintptr_t> g_free;  // cached arena blocks by size
 size_t g_cached = 0, g_live = 0;
-size_t g_limit = size_t(8) << 30;  // cached arena bytes kept registered
+size_t g_limit = size_t(2) << 30;  // cached arena bytes kept registered
+// live + cached bytes of page-locked memory this library holds at most: arrays a caller
+// keeps (diagnostics across steps) stay pinned, so the total is bounded; past it
+// fv3_host_alloc fails and the caller uses pageable memory (transfer.empty_host)
+size_t g_cap = size_t(32) << 30;
 
 size_t page_size()
 {
@@ -123,6 +127,17 @@ extern "C" int fv3_host_alloc(size_t bytes, void** out)
             return FV3_OK;
         }
     }
+    {
+        std::vector<uintptr_t> drop;
+        {
+            std::lock_guard<std::mutex> g(g_mu);
+            FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, g_live + n <= g_cap,
+                             "host_alloc: %zu live page-locked bytes + %zu exceed the arena cap %zu "
+                             "(fv3_host_arena_cap)", g_live, n, g_cap);
+            trim_locked(g_cap - g_live - n, drop);  // make room from the cache first
+        }
+        for (uintptr_t q : drop) free_block(q);
+    }
     void* p = nullptr;
     FV3_HIP(hipHostMalloc(&p, n, hipHostMallocDefault));
     std::lock_guard<std::mutex> g(g_mu);
@@ -161,6 +176,19 @@ extern "C" int fv3_host_arena_limit(size_t cached_bytes)
         std::lock_guard<std::mutex> g(g_mu);
         g_limit = cached_bytes;
         trim_locked(g_limit, drop);
+    }
+    for (uintptr_t p : drop) free_block(p);
+    return FV3_OK;
+}
+
+extern "C" int fv3_host_arena_cap(size_t total_bytes)
+{
+    clear_error();
+    std::vector<uintptr_t> drop;
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        g_cap = total_bytes;
+        trim_locked(g_cap > g_live ? g_cap - g_live : 0, drop);
     }
     for (uintptr_t p : drop) free_block(p);
     return FV3_OK;

@@ -14,6 +14,7 @@ semantics that matter for parity are xarray 0.19's (the reference pins
 
 Data may be numpy arrays or torch tensors (CUDA tensors stay on device).
 """
+import types
 from collections import OrderedDict
 from typing import Dict, Hashable, Iterable, Mapping, Optional, Sequence, Tuple
 
@@ -145,7 +146,9 @@ class Dataset:
 
     @property
     def data_vars(self):
-        return self._vars
+        """Read-only view of the variables (assign through ``ds[name] = ...``, which keeps
+        the dimension sizes and their conflict check in step)."""
+        return types.MappingProxyType(self._vars)
 
     def keys(self):
         return self._vars.keys()

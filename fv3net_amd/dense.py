@@ -458,37 +458,42 @@ class DenseColumnModel:
         lib = _native.load()
         kernel_out = _native.variant("FV3_D2H_KERNEL") == "1"
         self._last_kernel_out = False
-        for gi, (g0, g1) in enumerate(groups):
-            t = slice(g0, g1) if g1 > g0 + 1 else g0
-            # group gi's inputs: the runtime's pageable copies, on the compute stream (the
-            # host waits for them while s_out copies group gi - 1's outputs).  On a side
-            # stream of their own the two directions ran nearly in sequence: C384 30.3 ms
-            # against 22.2 ms (profiles/r05g_host_ab.json, pipe_in_*)
-            for a, b in zip(arrays, bufs):
-                st.h2d(a[t], out=b[t], stream=cur)
-            transfer.copy_fence(cur, streams[0])
-            outs = runs[gi](cur)
-            if host is None:
-                host = _host_outputs(out, [(n0,) + (tuple(o.shape[1:]) if g1 > g0 + 1 else tuple(o.shape))
-                                           for o in outs])
-                # FV3_D2H_KERNEL=1: out-copies as a kernel storing into the arena's pages
-                # on the compute stream (fv3_copy_to_host), the copy engines keeping the
-                # in-copies; default: the copy engines both ways
-                kernel_out = kernel_out and all(transfer.is_arena(h) for h in host)
-            done = False
-            if kernel_out:
-                done = all(lib.fv3_copy_to_host(h[t].ctypes.data, o.data_ptr(), o.numel() * 4, hcur) == 0
-                           for h, o in zip(host, outs))
-                kernel_out = done
-                self._last_kernel_out = done
-            if not done:
-                ev = torch.cuda.Event()
-                ev.record(cur)
-                s_out.wait_event(ev)
-                for h, o in zip(host, outs):
-                    transfer.host_copy(h[t], o, s_out.cuda_stream)
-        cur.wait_stream(s_out)
-        cur.synchronize()
+        try:
+            for gi, (g0, g1) in enumerate(groups):
+                t = slice(g0, g1) if g1 > g0 + 1 else g0
+                # group gi's inputs: the runtime's pageable copies, on the compute stream (the
+                # host waits for them while s_out copies group gi - 1's outputs).  On a side
+                # stream of their own the two directions ran nearly in sequence: C384 30.3 ms
+                # against 22.2 ms (profiles/r05g_host_ab.json, pipe_in_*)
+                for a, b in zip(arrays, bufs):
+                    st.h2d(a[t], out=b[t], stream=cur)
+                transfer.copy_fence(cur, streams[0])
+                outs = runs[gi](cur)
+                if host is None:
+                    host = _host_outputs(out, [(n0,) + (tuple(o.shape[1:]) if g1 > g0 + 1 else tuple(o.shape))
+                                               for o in outs])
+                    # FV3_D2H_KERNEL=1: out-copies as a kernel storing into the arena's pages
+                    # on the compute stream (fv3_copy_to_host), the copy engines keeping the
+                    # in-copies; default: the copy engines both ways
+                    kernel_out = kernel_out and all(transfer.is_arena(h) for h in host)
+                done = False
+                if kernel_out:
+                    done = all(lib.fv3_copy_to_host(h[t].ctypes.data, o.data_ptr(), o.numel() * 4, hcur) == 0
+                               for h, o in zip(host, outs))
+                    kernel_out = done
+                    self._last_kernel_out = done
+                if not done:
+                    ev = torch.cuda.Event()
+                    ev.record(cur)
+                    s_out.wait_event(ev)
+                    for h, o in zip(host, outs):
+                        transfer.host_copy(h[t], o, s_out.cuda_stream)
+        finally:
+            # every DMA into the arena `host` arrays has landed before they can be dropped
+            # (an exception above would otherwise return their blocks to the cache with
+            # copies still writing into them)
+            cur.wait_stream(s_out)
+            cur.synchronize()
         return host
 
     def _bind_or_forward(self, bufs, axes, precision):

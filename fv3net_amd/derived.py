@@ -588,8 +588,9 @@ def cos_zenith_angle(time, lon, lat, ctx: _Ctx = None):
         (ctypes.c_int64 * len(shape))(*tstride), terms.data_ptr(), nt, out.data_ptr(), _device.stream_handle(None))
     _native.check(st, "cos_zenith")
     if not as_da:
-        res = out.cpu().numpy()
-        return res.reshape(np.broadcast_shapes(np.asarray(time, dtype=object).shape, np.shape(lon), np.shape(lat)))
+        res = out.cpu().numpy().reshape(
+            np.broadcast_shapes(np.asarray(time, dtype=object).shape, np.shape(lon), np.shape(lat)))
+        return res[()]  # scalar inputs: a numpy float64 scalar, as _star_cos_zenith returns
     coords = {}
     for da in parts:
         for d, v in da.coords.items():

@@ -96,7 +96,7 @@ class _Register:
         return return_name
 
     def load(self, path: str):
-        from . import composite, derived, pytorch_predictor  # noqa: F401  register the composites, "pytorch_predictor"
+        from . import composite, derived, novelty, pytorch_predictor  # noqa: F401  register the composites, "pytorch_predictor"
 
         name_file = os.path.join(path, _NAME_PATH)
         if not os.path.exists(name_file):

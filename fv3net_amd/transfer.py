@@ -100,6 +100,19 @@ def is_arena(a) -> bool:
     return isinstance(a, _ArenaBlock)
 
 
+def set_arena_limits(cached_bytes=None, total_bytes=None) -> None:
+    """Bound the library's page-locked memory: ``cached_bytes`` kept for reuse after the
+    caller drops arrays (default 2 GiB), ``total_bytes`` live + cached at most (default
+    32 GiB).  Arrays the caller keeps (outputs held across steps) stay page-locked; past
+    the total, ``empty_host`` hands out pageable ``np.empty`` arrays instead."""
+    from . import _native
+
+    if cached_bytes is not None:
+        _native.check(_lib().fv3_host_arena_limit(int(cached_bytes)), "host_arena_limit")
+    if total_bytes is not None:
+        _native.check(_lib().fv3_host_arena_cap(int(total_bytes)), "host_arena_cap")
+
+
 def memory_stats() -> dict:
     """The arena's counters: live / cached bytes and blocks (fv3_host_memory_stats)."""
     st = (ctypes.c_uint64 * 3)()

@@ -524,6 +524,44 @@ int fv3_pressure_midpoint_log(const void* delp, int dtype, int64_t ld_in, void* 
 int fv3_member_reduce(const void* const* members, int n_members, int64_t n, int dtype_f64, int op,
                       void* out, void* stream);
 
+/* ---- out-of-sample composite (OutOfSampleModel, _shared/models.py:340-400) -----------
+ * fv3_minmax_scores replaces MinMaxNoveltyDetector.predict
+ *   (fv3fit/sklearn/_min_max_novelty_detector.py:86-115): per column, the packed features
+ *   (variables in order, levels [z0, z0 + nfeat) of each: packer clip), MinMaxScaler's
+ *   X *= scale_; X += min_ in X's dtype (x_f64: any float64 input), and
+ *   score = max(max X - 1, 0) + max(-1 * min X, 0) (NaN propagates as in numpy).
+ *   score: [ncol] in X's dtype.  1 <= n_vars <= FV3_NOV_MAX_VARS.
+ * fv3_taper_columns replaces taper_mask / taper_ramp / taper_decay
+ *   (_shared/taper_function.py:6-35; mode FV3_TAPER_*, p0/p1 = cutoff / (ramp_min,
+ *   ramp_max) / (threshold, rate)) and OutOfSampleModel.predict's output * taper
+ *   (models.py:392-398): taper_out (or NULL) receives the taper values (int64 for the
+ *   mask, else the score's dtype); every field is multiplied per column in numpy's
+ *   promoted dtype (float64 unless both the field and the taper are float32). */
+#define FV3_NOV_MAX_VARS 16
+#define FV3_NOV_MAX_FIELDS 16
+#define FV3_TAPER_MASK 0
+#define FV3_TAPER_RAMP 1
+#define FV3_TAPER_DECAY 2
+typedef struct {
+    const void* data;    /* [level][column] under `layout` */
+    fv3_layout layout;
+    int data_f64;
+    int z0;              /* first kept level */
+    int nfeat;           /* kept levels (1 for a 2-D variable) */
+} fv3_nov_var;
+typedef struct {
+    const void* in;      /* [level][column] base-model output */
+    fv3_layout in_layout;
+    int in_f64;
+    void* out;           /* [level][column] tapered output, float64 or float32 (see above) */
+    fv3_layout out_layout;
+    int nz;
+} fv3_taper_field;
+int fv3_minmax_scores(const fv3_nov_var* vars, int n_vars, const void* scale, const void* min, int scale_f64,
+                      int x_f64, int64_t ncol, void* score, void* stream);
+int fv3_taper_columns(const void* score, int score_f64, int64_t ncol, int mode, double p0, double p1,
+                      void* taper_out, const fv3_taper_field* fields, int n_fields, void* stream);
+
 /* fv3_scale_levels replaces TaperConfig.apply (_shared/config.py:21-29, TaperedModel
  * models.py:95-100): out[k][c] (float64, contiguous [nz][ncol]) = scale[k] * x(c, k),
  * x float32 or float64 under `lay` with its levels on the taper dimension. */
@@ -668,16 +706,21 @@ int fv3_cos_zenith(int ndim, const int64_t* shape, fv3_strided lon, int lon_rad,
  * fv3_host_alloc: a page-locked, page-aligned host block (hipHostMalloc) owned by the
  * library, cached after fv3_host_free for reuse by a later fv3_host_alloc of the same
  * page-rounded size: the arrays a host call hands back, and staging.
- * fv3_host_arena_limit sets the cached bytes kept (default 8 GiB; beyond it blocks are
- * released).  stats[3]: live bytes, cached bytes, blocks.
+ * fv3_host_arena_limit sets the cached bytes kept (default 2 GiB; beyond it blocks are
+ * released); fv3_host_arena_cap the live + cached bytes held at most (default 32 GiB:
+ * arrays a caller keeps stay page-locked; past the cap fv3_host_alloc returns
+ * FV3_ERR_UNSUPPORTED and the caller uses pageable memory).  stats[3]: live bytes,
+ * cached bytes, blocks.
  *
  * fv3_host_copy: one host <-> device copy on `stream` (kind 1: host to device, 2: device
- * to host): asynchronous DMA for arena memory, the runtime's pageable copy (complete on
- * return) otherwise.
+ * to host): asynchronous DMA for arena memory; complete on return for any other host
+ * memory (the runtime's pageable copy, or waited for when the buffer is page-locked by
+ * someone else, e.g. torch pin_memory()).
  */
 int fv3_host_alloc(size_t bytes, void** out);
 int fv3_host_free(void* ptr);
 int fv3_host_arena_limit(size_t cached_bytes);
+int fv3_host_arena_cap(size_t total_bytes);
 int fv3_host_memory_stats(uint64_t* stats);
 int fv3_host_copy(void* dst, const void* src, size_t bytes, int kind, void* stream);
 
@@ -692,8 +735,8 @@ int fv3_copy_to_host(void* host_dst, const void* dev_src, size_t bytes, void* st
 /* Pitched copy between host and device on `stream` (hipMemcpy2DAsync): `height` rows of
  * `width` bytes, `spitch` / `dpitch` bytes apart; kind 1 host to device, 2 device to
  * host.  A column band of a [level][column] array, one row per level: the pipelined
- * host call over column bands.  Asynchronous for arena rows (fv3_host_alloc), the
- * runtime's pageable copy otherwise.  No reference counterpart (transport). */
+ * host call over column bands.  Asynchronous for arena rows (fv3_host_alloc), complete on
+ * return otherwise (as fv3_host_copy).  No reference counterpart (transport). */
 int fv3_copy_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height, int kind,
                 void* stream);
 

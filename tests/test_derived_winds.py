@@ -242,6 +242,8 @@ def test_cos_zenith_kats_and_oracle(gpu):
         for time in (JulianTime(*t), datetime.datetime(*t)):
             got = cos_zenith_angle(time, lon, lat)
             assert float(got) == pytest.approx(expected, abs=1e-3)
+            # scalar inputs give a numpy float64 scalar, not a 0-d array (_star_cos_zenith)
+            assert isinstance(got, np.float64) and not isinstance(got, np.ndarray)
     time = JulianTime(2020, 3, 21, 12)
     da = cos_zenith_angle(D.DataArray(np.array(time, dtype=object), []), D.DataArray(np.array([0]), ["x"]),
                           D.DataArray(np.array([0]), ["x"]))

@@ -118,3 +118,49 @@ def test_copy_band_pitched_both_ways(gpu, dtype):
         transfer.copy_band(d[:, :10], a[:, :11])
     with pytest.raises(ValueError):
         transfer.copy_band(d[:, ::2], a[:, ::2])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nbytes", [4096, 1 << 20])
+def test_h2d_from_memory_pinned_elsewhere_complete_on_return(gpu, nbytes):
+    """A caller's array in memory page-locked by someone else (torch pin_memory): the copy
+    is a real asynchronous DMA there, so h2d must wait for it before returning; the
+    caller overwrites the array at once and the device must still hold the old bytes."""
+    import torch
+
+    from fv3net_amd import transfer
+
+    n = nbytes // 4
+    pinned = torch.empty(n, dtype=torch.float32).pin_memory()
+    a = pinned.numpy()
+    rng = np.random.default_rng(nbytes)
+    for _ in range(5):
+        vals = rng.normal(0, 1, n).astype(np.float32)
+        a[:] = vals
+        # a long kernel ahead of the copy on the same stream keeps the DMA pending
+        big = torch.randn(4096, 4096, device="cuda")
+        _ = big @ big
+        t = transfer.h2d(a)
+        a[:] = -1.0  # the caller reuses its buffer right after the call
+        assert np.array_equal(t.cpu().numpy(), vals)
+
+
+@pytest.mark.gpu
+def test_arena_cap_falls_back_to_pageable(gpu):
+    """Past the arena's live + cached cap, empty_host hands out pageable arrays."""
+    import gc
+
+    from fv3net_amd import transfer
+
+    gc.collect()
+    live = transfer.memory_stats()["arena_live"]
+    try:
+        transfer.set_arena_limits(total_bytes=live + (4 << 20))
+        small = transfer.empty_host((1 << 20,), np.float32)  # 4 MiB: fits
+        assert transfer.is_arena(small)
+        big = transfer.empty_host((2 << 20,), np.float32)  # 8 MiB more: past the cap
+        assert not transfer.is_arena(big) and big.shape == (2 << 20,)
+        del small
+        gc.collect()
+    finally:
+        transfer.set_arena_limits(cached_bytes=2 << 30, total_bytes=32 << 30)
