@@ -155,6 +155,9 @@ def kernel_sources(kernel):
     if tu is None:
         return []
     seen, todo = [], [tu]
+    fast = tu.replace(".hip", "_fast.hip")  # the fast-arithmetic unit that includes it (mappm_fast.hip)
+    if os.path.exists(os.path.join(csrc, fast)):
+        todo.append(fast)
     while todo:
         f = todo.pop()
         if f in seen or not os.path.exists(os.path.join(csrc, f)):

@@ -44,6 +44,7 @@
 #include "mappm_multi.h"
 
 namespace fv3 {
+namespace FV3_ARITH_NS {  // kernels named fv3::exact::... / fv3::fast::... in traces
 namespace {
 
 constexpr int kMaxLev = 128;
@@ -783,7 +784,7 @@ __global__ __launch_bounds__(64) void regrid_coarsen_edge_kernel(EdgeArgs<DT> a)
 
 }  // namespace
 
-namespace FV3_ARITH_NS {
+
 
 template <typename DT>
 int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* fields, float* const* out,
@@ -864,16 +865,27 @@ int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* f
         // register targets: the two-field pass 4 waves per SIMD (118 VGPRs; at 6 it spills
         // its remap state, 3.4 ms for 4 fields), the one-field pass 6 on float32 delp
         // (0.756 -> 0.716 ms at C384, profiles/r05zzk_coarsen_wpe_ab.log) and 5 on float64
-        constexpr int W1 = std::is_same<DT, float>::value ? 6 : 5;
+#ifndef FV3_COARSEN_W1F
+#define FV3_COARSEN_W1F 6  // tools/ variant builds: the register targets under A/B
+#endif
+#ifndef FV3_COARSEN_W2
+#ifdef FV3_FAST_ARITH  // 113 VGPRs at 4; 5 waves per SIMD measured 1.633-1.645 -> 1.595 ms for 4 fields
+#define FV3_COARSEN_W2 5  // (profiles/r06l_coarsen_wpe_ab.log); the exact pass (119 VGPRs) stays at 4
+#else
+#define FV3_COARSEN_W2 4
+#endif
+#endif
+        constexpr int W1 = std::is_same<DT, float>::value ? FV3_COARSEN_W1F : 5;
+        constexpr int W2 = FV3_COARSEN_W2;
         const bool k1 = iv == 1 && kord == 1;
         if (factor == 8 && NF == 2)
-            hipLaunchKernelGGL((k1 ? regrid_coarsen_cells_kernel<DT, 8, 2, 4, true>
-                                  : regrid_coarsen_cells_kernel<DT, 8, 2, 4, false>), grid, block, lds_c, s, a);
+            hipLaunchKernelGGL((k1 ? regrid_coarsen_cells_kernel<DT, 8, 2, W2, true>
+                                  : regrid_coarsen_cells_kernel<DT, 8, 2, W2, false>), grid, block, lds_c, s, a);
         else if (factor == 8)
             hipLaunchKernelGGL((k1 ? regrid_coarsen_cells_kernel<DT, 8, 1, W1, true>
                                   : regrid_coarsen_cells_kernel<DT, 8, 1, W1, false>), grid, block, lds_c, s, a);
         else if (NF == 2)
-            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 0, 2, 4, false>), grid, block, lds_c, s, a);
+            hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 0, 2, W2, false>), grid, block, lds_c, s, a);
         else
             hipLaunchKernelGGL((regrid_coarsen_cells_kernel<DT, 0, 1, W1, false>), grid, block, lds_c, s, a);
         FV3_LAUNCH_CHECK();

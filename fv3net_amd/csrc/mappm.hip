@@ -57,6 +57,7 @@ int launch_mappm_pairs(const MappmPairArgs& a, hipStream_t stream);
 }  // namespace fast
 #endif
 
+namespace FV3_ARITH_NS {  // kernels named fv3::exact::... / fv3::fast::... in traces
 namespace {
 
 // The remap consumer emits q2(k) for k = 1, 2, ... and asks for next_edge(k) for
@@ -457,7 +458,7 @@ const void* cs_global_kernel(const MappmArgs& a, int64_t nlanes)
 
 }  // namespace
 
-namespace FV3_ARITH_NS {
+
 
 // kord <= 7: the level-parallel kernel while one lane per column leaves the chip
 // mostly idle (FV3_MAPPM_PATH=serial|levels overrides, for tests and A/B).

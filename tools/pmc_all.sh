@@ -7,7 +7,10 @@ set -uo pipefail
 TAG=$1; shift
 LEGS=("$@")
 if [ ${#LEGS[@]} -eq 0 ]; then
-  LEGS=(calib dense_c48 dense_c384 dense_c384_bf16x3 emulator_c384 emulator_c384_f32 mappm_c384_k1 mappm_c384_k10 mappm_c12 coarsen_1f coarsen_4f stepper_c96)
+  LEGS=(calib dense_c48 dense_c384 dense_c384_bf16x3 emulator_c384 emulator_c384_f32 mappm_c384_k1 mappm_c384_k10 mappm_c12
+        coarsen_1f coarsen_4f stepper_c96 predict_mappm_c384 dense_c48_bf16x6 dense_c384_bf16x6 emulator_c384_bf16x6
+        predict_mappm_c384_bf16x6 stepper_c96_r8 emulator_c384_r8 emulator_c384_f32_r8 predict_mappm_c384_r8
+        predict_mappm_c384_bf16x6_r8 mappm_c384_k1_exact mappm_c384_k10_exact coarsen_1f_exact coarsen_4f_exact)
 fi
 OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out/pmc_${TAG}
 # the calibration kernels of the "calib" leg (tools only; git-ignored build)

@@ -40,6 +40,11 @@ def make(leg, dev):
         return W.make_mappm_workload(W.c_columns(384), 79, 79, 1, seed=5, device=dev)
     if leg == "mappm_c384_k10":
         return W.make_mappm_workload(W.c_columns(384), 79, 79, 10, seed=5, device=dev)
+    if leg in ("mappm_c384_k1_exact", "mappm_c384_k10_exact"):
+        return W.make_mappm_workload(W.c_columns(384), 79, 79, 1 if "k1_" in leg else 10, seed=5, device=dev,
+                                     exact=True)
+    if leg in ("coarsen_1f_exact", "coarsen_4f_exact"):
+        return W.make_coarsen_workload(384, 8, 1 if "1f" in leg else 4, seed=7, device=dev, exact=True)
     if leg == "mappm_c12":
         return W.make_mappm_workload(W.c_columns(12), 79, 50, 1, seed=5, device=dev)
     if leg == "coarsen_0f":  # pass 1 only (coarse delp / phalf, denominators)

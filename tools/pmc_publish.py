@@ -31,6 +31,10 @@ LEGS = {
     "mappm_c384_79to79_kord1": ("mappm_c384_k1", "mappm_ppm_kernel"),
     "mappm_c384_79to79_kord10": ("mappm_c384_k10", "mappm_cs_global_kernel"),
     "mappm_c12_79to50_kord1": ("mappm_c12", "mappm_ppm_levels_kernel"),
+    "mappm_c384_79to79_kord1_exact": ("mappm_c384_k1_exact", "mappm_ppm_kernel"),
+    "mappm_c384_79to79_kord10_exact": ("mappm_c384_k10_exact", "mappm_cs_global_kernel"),
+    "coarsen_c384_to_c48_1field_exact": ("coarsen_1f_exact", "regrid_coarsen_cells_kernel"),
+    "coarsen_c384_to_c48_4field_exact": ("coarsen_4f_exact", "regrid_coarsen_cells_kernel"),
     "coarsen_c384_to_c48_1field": ("coarsen_1f", "regrid_coarsen_cells_kernel"),
     "coarsen_c384_to_c48_4field": ("coarsen_4f", "regrid_coarsen_cells_kernel"),
     "stepper_c96": ("stepper_c96", "ml_epilogue_kernel"),
@@ -46,7 +50,7 @@ LEGS = {
     "emulator_c384_rank_of_8_f32": ("emulator_c384_f32_r8", "dense_forward_kernel"),
     "predict_mappm_c384_rank_of_8": ("predict_mappm_c384_r8", "dense_forward_kernel"),
     "predict_mappm_c384_rank_of_8_bf16x6": ("predict_mappm_c384_bf16x6_r8", "dense_b3_kernel"),
-    "predict_mappm_c384_rank_of_8_mappm": ("predict_mappm_c384_r8", "mappm_ppm_pair_kernel"),
+    "predict_mappm_c384_rank_of_8_mappm": ("predict_mappm_c384_r8", "mappm_ppm_pair_split_kernel"),
 }
 KEEP = ("fv3::", "calib_")
 

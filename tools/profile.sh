@@ -17,4 +17,9 @@ timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fe
     python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-extra "${ARGS[@]}" > "$OUT/bench_fetch.json" 2> "$OUT/bench_fetch.err"
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
     python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-extra "${ARGS[@]}" > "$OUT/bench_write.json" 2> "$OUT/bench_write.err"
-echo "profile done: $OUT"
+echo "headline profile done: $OUT"
+# the legs (bench.py runs them in a child process, which the trace above does not follow):
+# their kernels traced in a run of the child mode itself
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/legs" -o legs -- \
+    python3 bench.py --legs-only /tmp/bench_legs_profile.jsonl > "$OUT/legs.out" 2> "$OUT/legs.err"
+echo "legs profile done: $OUT/legs"
