@@ -66,3 +66,60 @@ def test_abi_version_and_constants_match_the_header(lib):
     assert d["FV3_DENSE_BF16X3"] == _native.DENSE_BF16X3
     assert d["FV3_DENSE_BF16X6"] == _native.DENSE_BF16X6
     assert d["FV3_OK"] == _native.FV3_OK
+
+
+_STRUCTS = {  # header typedef -> _native ctypes mirror
+    "fv3_layout": "Layout",
+    "fv3_dense_desc": "DenseDesc",
+    "fv3_epilogue_io": "EpilogueIO",
+    "fv3_adapter_target": "AdapterTarget",
+    "fv3_field": "Field",
+    "fv3_nov_var": "NovVar",
+    "fv3_taper_field": "TaperField",
+    "fv3_strided": "Strided",
+}
+_RENAMED = {"inp": "in"}  # ctypes field -> C member (a Python keyword in C)
+
+
+def test_ctypes_struct_layouts_match_the_header(tmp_path):
+    """Every struct the host side passes by pointer has the header's size and field
+    offsets (the header compiled by gcc against the ctypes mirrors)."""
+    import ctypes
+    import shutil
+    import subprocess
+
+    from fv3net_amd import _native
+
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "fv3net_amd.h"', "int main(void) {"]
+    want = {}
+    for cname, pyname in _STRUCTS.items():
+        cls = getattr(_native, pyname)
+        want[f"{cname} sizeof"] = ctypes.sizeof(cls)
+        lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
+        for fname, _ in cls._fields_:
+            c_field = _RENAMED.get(fname, fname)
+            want[f"{cname} {c_field}"] = getattr(cls, fname).offset
+            lines.append(f'printf("{cname} {c_field} %zu\\n", offsetof({cname}, {c_field}));')
+    lines += ["return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = {}
+    for ln in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines():
+        k, v = ln.rsplit(" ", 1)
+        got[k] = int(v)
+    bad = {k: (got.get(k), v) for k, v in want.items() if got.get(k) != v}
+    assert not bad, f"(header, ctypes) differ: {bad}"
+
+
+def test_novelty_constants():
+    from fv3net_amd import _native
+
+    d = _defines(_header_text())
+    assert d["FV3_NOV_MAX_VARS"] == _native.NOV_MAX_VARS
+    assert d["FV3_NOV_MAX_FIELDS"] == _native.NOV_MAX_FIELDS
+    assert (d["FV3_TAPER_MASK"], d["FV3_TAPER_RAMP"], d["FV3_TAPER_DECAY"]) == (
+        _native.TAPER_MASK, _native.TAPER_RAMP, _native.TAPER_DECAY)
