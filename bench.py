@@ -74,7 +74,7 @@ def timed_steps(step, steps, warmup, dist=None, settle_ms=0.0):
     Settle: the same step runs untimed for ``settle_ms`` of wall time first.  The
     MI355X shader clock ramps over ~100 ms of sustained load: a C48 launch measured
     after 20 launches runs at ~2.13 GHz, after 3,000 at ~2.38 GHz (52.9 vs 47.3 us,
-    tools/dense_trace.py), so without it a short K times the ramp, not the kernel."""
+    tools/pmc_drive.py), so without it a short K times the ramp, not the kernel."""
     import torch
 
     # the settle keeps the GPU busy without a gap: the host waits on the event recorded

@@ -30,6 +30,18 @@
 #endif
 #endif
 
+// Variant kernels: alternatives that only an A/B knob selects (FV3_VARIANTS=1 plus the
+// knob), never the product's own heuristics -- other register targets, load distances,
+// register-tail depths, LDS scratch.  Every one gives the product kernel's bits; they
+// are instantiated in the tools/ variant builds only, so the product library holds the
+// kernels its host code can pick and nothing else (a knob naming an absent variant is
+// ignored there; tests that pin a variant skip on the product build).
+#ifdef FV3_PRODUCT_BUILD
+#define FV3_VARIANT_KERNELS 0
+#else
+#define FV3_VARIANT_KERNELS 1
+#endif
+
 namespace fv3 {
 
 void set_error(const char* fmt, ...);

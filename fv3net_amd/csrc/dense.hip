@@ -138,7 +138,7 @@ __device__ __forceinline__ void tile_sync()
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// column data: plain loads / stores.  Measured (tools/et_ab.sh): nontemporal input
+// column data: plain loads / stores.  Measured (tools/ab.py): nontemporal input
 // loads cost the emulator 4% (its residual outputs re-read the inputs), nontemporal
 // stores cost the stepper 8% (its next kernel reads the tendencies); C48 gains < 1%
 __device__ __forceinline__ float in_load(const float* p)
@@ -1280,21 +1280,24 @@ static int dense_forward_impl(const fv3_dense_model* m, const void* const* input
     // (waves per SIMD targeted by register allocation, weight ring depth):
     // FV3_DENSE_CFG = "3,2" (default) | "2,3" | "4,2" (A/B)
     int wpe = 3, rd = 2;  // measured best at C48 and C384
+#if FV3_VARIANT_KERNELS
     if (const char* e = fv3::variant_env("FV3_DENSE_CFG")) {
         if (!strcmp(e, "2,3")) wpe = 2, rd = 3;
         else if (!strcmp(e, "4,2")) wpe = 4, rd = 2;
     }
+#endif
     auto kernel_of = [&](int t4) -> const void* {
 #define FV3_K(T4, NC, W, R) (const void*)dense_forward_kernel<T4, NC, W, R, 4>
         if (nw == 8) return t4 == 1 ? (const void*)dense_forward_kernel<1, 2, 4, 2, 8> : (const void*)dense_forward_kernel<2, 2, 4, 2, 8>;
-        if (nc == 1) {
-            if (wpe == 3) return t4 == 1 ? FV3_K(1, 1, 3, 2) : t4 == 2 ? FV3_K(2, 1, 3, 2) : FV3_K(4, 1, 3, 2);
-            if (wpe == 4) return t4 == 1 ? FV3_K(1, 1, 4, 2) : t4 == 2 ? FV3_K(2, 1, 4, 2) : FV3_K(4, 1, 4, 2);
-            return t4 == 1 ? FV3_K(1, 1, 2, 3) : t4 == 2 ? FV3_K(2, 1, 2, 3) : FV3_K(4, 1, 2, 3);
-        }
-        if (wpe == 3) return t4 == 1 ? FV3_K(1, 2, 3, 2) : t4 == 2 ? FV3_K(2, 2, 3, 2) : FV3_K(4, 2, 3, 2);
+#if FV3_VARIANT_KERNELS  // the other register targets / ring depths (A/B)
+        if (wpe == 4 && nc == 1) return t4 == 1 ? FV3_K(1, 1, 4, 2) : t4 == 2 ? FV3_K(2, 1, 4, 2) : FV3_K(4, 1, 4, 2);
+        if (wpe == 2 && nc == 1) return t4 == 1 ? FV3_K(1, 1, 2, 3) : t4 == 2 ? FV3_K(2, 1, 2, 3) : FV3_K(4, 1, 2, 3);
         if (wpe == 4) return t4 == 1 ? FV3_K(1, 2, 4, 2) : t4 == 2 ? FV3_K(2, 2, 4, 2) : FV3_K(4, 2, 4, 2);
-        return t4 == 1 ? FV3_K(1, 2, 2, 3) : t4 == 2 ? FV3_K(2, 2, 2, 3) : FV3_K(4, 2, 2, 3);
+        if (wpe == 2) return t4 == 1 ? FV3_K(1, 2, 2, 3) : t4 == 2 ? FV3_K(2, 2, 2, 3) : FV3_K(4, 2, 2, 3);
+#endif
+        (void)wpe, (void)rd;
+        if (nc == 1) return t4 == 1 ? FV3_K(1, 1, 3, 2) : t4 == 2 ? FV3_K(2, 1, 3, 2) : FV3_K(4, 1, 3, 2);
+        return t4 == 1 ? FV3_K(1, 2, 3, 2) : t4 == 2 ? FV3_K(2, 2, 3, 2) : FV3_K(4, 2, 3, 2);
 #undef FV3_K
     };
     FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, !in64 || nw == 8,

@@ -218,7 +218,7 @@ __global__ __launch_bounds__(256) void mappm_ppm_kernel(MappmArgs a)
 
 bool is_k1(int iv, int kord) { return iv == 1 && kord == 1; }
 
-// tools/mappm_small_time.py, kord 1 79->79: C48 (13,824 columns) 142 -> 38 us, C96
+// tools/ab.py, kord 1 79->79: C48 (13,824 columns) 142 -> 38 us, C96
 // (55,296) 168 -> 118 us; at C384 the serial kernel (0.70 ms) wins.
 constexpr int64_t kLevelsMaxCols = 65536;
 
@@ -357,6 +357,13 @@ __global__ __launch_bounds__(128) void mappm_ppm_levels_kernel(MappmArgs a)
     }
 }
 
+#ifdef FV3_FAST_ARITH
+#define FV3_MAPPM_CS 0  // kord > 7 always takes the exact kernels (launch_arith): none here
+#else
+#define FV3_MAPPM_CS 1
+#endif
+
+#if FV3_MAPPM_CS && FV3_VARIANT_KERNELS  // the solve's scratch in LDS (A/B: FV3_MAPPM_LDS)
 __global__ __launch_bounds__(64) void mappm_cs_kernel(MappmArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -366,7 +373,9 @@ __global__ __launch_bounds__(64) void mappm_cs_kernel(MappmArgs a)
     DevCol col = make_col(a, c);
     mappm_cs_column(col, scr, a.km, a.kn, a.iv, a.kord);
 }
+#endif
 
+#if FV3_MAPPM_CS
 // NT > 0: the bottom NT edges of the solve stay in registers (mappm_cs_column), 6 NT
 // fewer scratch accesses per column; the scratch keeps its full [2][km+3] shape
 // PF > 0: loads run PF levels ahead in the solve, one layer ahead in the main loop
@@ -403,7 +412,7 @@ __global__ __launch_bounds__(256) void mappm_cs_global_kernel(MappmArgs a)
 }
 
 // register-tail depth of the kord > 7 kernel (every depth gives the same bits).  Measured
-// on MI355X (tools/mappm_nt_ab.py, profiles/r04c_mappm_nt.log), C384 79 -> 79: at
+// on MI355X (tools/ab.py, profiles/r04c_mappm_nt.log), C384 79 -> 79: at
 // 884,736 columns NT = 0 / 16 / 32 / 48 take 0.89 / 0.97 / 1.12 / 1.24 ms (the registers
 // cost occupancy: 60 -> 78 / 100 / 132 VGPRs, 8 -> 6 / 4 / 3 waves per SIMD, and the
 // launch needs it more than the scratch bytes saved); at one rank's 110,592 columns,
@@ -413,15 +422,16 @@ const void* cs_global_kernel(const MappmArgs& a, int64_t nlanes)
 {
     const int64_t ncol = a.ncol;
     int nt = ncol < 262144 ? 48 : 0;
-    if (const char* e = fv3::variant_env("FV3_MAPPM_CS_NT")) nt = atoi(e);
-    // load distance (tools/mappm_pf_ab.py; C384 79 -> 79 kord 10, buffer operations):
+    // load distance (tools/ab.py; C384 79 -> 79 kord 10, buffer operations):
     // before the rolling subgrid flags (profiles/r04l_mappm_pf.log) 884,736 columns PF =
     // 0 / 2 / 4 / 8 0.909 / 0.761 / 0.798 / 0.836 ms (64-bit addresses, PF = 0: 0.871),
     // 110,592 columns (register tail) 0.224 / 0.185 / 0.182 / 0.182 ms; with them
     // (profiles/r04q_mappm_kord_ab.log) PF = 2 / 4 0.772 / 0.765 ms and 0.175 / 0.170 ms
     int pf = 4;
+#if FV3_VARIANT_KERNELS
+    if (const char* e = fv3::variant_env("FV3_MAPPM_CS_NT")) nt = atoi(e);
     if (const char* e = fv3::variant_env("FV3_MAPPM_CS_PF")) pf = atoi(e);
-    // 32-bit lane byte offsets when every column offset (and the scratch) fits
+#endif
     // buffer operations at 32-bit byte offsets when every array (and the scratch) spans
     // < 4 GiB: the last column's offset plus km levels
     auto fits = [&](const fv3_layout& l, int nlev) {
@@ -432,6 +442,7 @@ const void* cs_global_kernel(const MappmArgs& a, int64_t nlanes)
     };
     bool c32 = fits(a.l_pe1, a.km + 1) && fits(a.l_q1, a.km) && 4 * nlanes * 2 * (int64_t)(a.km + 3) < (1ll << 32) - 4;
     if (const char* e = fv3::variant_env("FV3_MAPPM_CS_C32")) c32 = c32 && atoi(e) != 0;
+#if FV3_VARIANT_KERNELS  // the other depths and load distances (A/B)
 #define FV3_CS_PF(NT_, C_)                                                        \
     switch (pf) {                                                                 \
     case 0: return (const void*)mappm_cs_global_kernel<NT_, 0, C_>;               \
@@ -439,22 +450,28 @@ const void* cs_global_kernel(const MappmArgs& a, int64_t nlanes)
     case 8: return (const void*)mappm_cs_global_kernel<NT_, 8, C_>;               \
     default: return (const void*)mappm_cs_global_kernel<NT_, 2, C_>;              \
     }
+    if (pf != 4 || (nt != 0 && nt != 48)) {
+        if (c32) {
+            if (nt == 8) { FV3_CS_PF(8, true) }
+            if (nt == 16) { FV3_CS_PF(16, true) }
+            if (nt) { FV3_CS_PF(48, true) } else { FV3_CS_PF(0, true) }
+        }
+        if (nt) { FV3_CS_PF(48, false) }
+        FV3_CS_PF(0, false)
+    }
+#undef FV3_CS_PF
+#endif
     // kord 10 under the register tail at the default load distance: the column
     // specialised for it (0.170 -> 0.168 ms at 110,592 columns; on the full grid the
     // specialised build measured slower, 0.772 -> 0.806 ms at PF = 2, so it is not used
     // there; profiles/r04q_mappm_kord_ab.log).  FV3_MAPPM_CS_KORD=0: the generic column.
     const char* ke = fv3::variant_env("FV3_MAPPM_CS_KORD");
-    if (c32 && nt == 48 && pf == 4 && (a.kord == 10 || a.kord == -10) && !(ke && atoi(ke) == 0))
+    if (c32 && nt == 48 && (a.kord == 10 || a.kord == -10) && !(ke && atoi(ke) == 0))
         return (const void*)mappm_cs_global_kernel<48, 4, true, 10>;
-    if (c32) {
-        if (nt == 8) { FV3_CS_PF(8, true) }    // A/B only (FV3_MAPPM_CS_NT=8|16)
-        if (nt == 16) { FV3_CS_PF(16, true) }
-        if (nt) { FV3_CS_PF(48, true) } else { FV3_CS_PF(0, true) }
-    }
-    if (nt) { FV3_CS_PF(48, false) }
-    FV3_CS_PF(0, false)
-#undef FV3_CS_PF
+    if (c32) return nt ? (const void*)mappm_cs_global_kernel<48, 4, true> : (const void*)mappm_cs_global_kernel<0, 4, true>;
+    return nt ? (const void*)mappm_cs_global_kernel<48, 4, false> : (const void*)mappm_cs_global_kernel<0, 4, false>;
 }
+#endif  // FV3_MAPPM_CS
 
 }  // namespace
 
@@ -473,7 +490,7 @@ bool use_levels_kernel(const MappmArgs& a, int64_t max_cols = kLevelsMaxCols)
 
 // Pairs of fields: the pair kernel on two or three lanes per column beats the
 // level-parallel kernel (one field per launch) from ~10,000 columns
-// (tools/mappm_small_lanes.py, profiles/r05zr_mappm_small_lanes.log and
+// (tools/ab.py, profiles/r05zr_mappm_small_lanes.log and
 // r05zs_mappm_small_lanes.log, two fields, levels / three lanes: 6,912 columns 47 / 59 us,
 // 10,368 63 / 59 us, C48 13,824 77 / 60 us, C96 55,296 252 / 86 us)
 constexpr int64_t kLevelsMaxColsPairs = 10240;
@@ -483,7 +500,8 @@ bool launch_split_single(const MappmArgs& a, hipStream_t stream);  // below the 
 int launch_mappm(MappmArgs a, hipStream_t stream)
 {
     if (a.ncol == 0) return FV3_OK;
-    if (a.kord > 7 && !fv3::variant_env("FV3_MAPPM_LDS")) {
+#if FV3_MAPPM_CS
+    if (a.kord > 7 && !(FV3_VARIANT_KERNELS && fv3::variant_env("FV3_MAPPM_LDS"))) {
         const int block = 256;
         const int64_t grid = (a.ncol + block - 1) / block;
         FV3_HIP(hipMallocAsync((void**)&a.scratch, sizeof(float) * 2 * (size_t)(a.km + 3) * (size_t)grid * block,
@@ -494,12 +512,17 @@ int launch_mappm(MappmArgs a, hipStream_t stream)
         FV3_HIP(hipFreeAsync(a.scratch, stream));
         return FV3_OK;
     }
+#endif
     if (a.kord > 7) {
+#if FV3_MAPPM_CS && FV3_VARIANT_KERNELS
         const int block = 64;
         const size_t lds = sizeof(float) * 2 * (size_t)(a.km + 3) * block;
         FV3_REQUIRE(lds <= 160 * 1024, "mappm: km=%d too large for the kord>7 LDS path", a.km);
         const int64_t grid = (a.ncol + block - 1) / block;
         hipLaunchKernelGGL(mappm_cs_kernel, dim3((unsigned)grid), dim3(block), lds, stream, a);
+#else
+        FV3_REQUIRE_CODE(FV3_ERR_UNSUPPORTED, false, "mappm: kord > 7 runs on the exact kernels only");
+#endif
     } else if (launch_split_single(a, stream)) {
         // one field on two or three lanes per column
     } else if (use_levels_kernel(a)) {
@@ -721,7 +744,7 @@ __global__ __launch_bounds__(192) void mappm_ppm_pair_split3_kernel(MappmPairArg
     }
 }
 
-// Where the two-lane kernel pays (tools/mappm_split_time.py, one box, interleaved; one
+// Where the two-lane kernel pays (tools/ab.py, one box, interleaved; one
 // lane per column vs two).  With whole-column sortedness scans up front
 // (profiles/r05r_mappm_split.log): 65,536 columns 142.7 vs 115.4 us, 110,592 (one rank's
 // C384 band at world 8) 165.7 vs 161.5 us, 147,456 213 vs 228 us, C384 0.78 vs 1.06 ms.

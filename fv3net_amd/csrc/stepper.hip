@@ -204,7 +204,7 @@ __global__ __launch_bounds__(64) void ml_epilogue_kernel(EpilogueArgs<DT> a)
 // kernel.  One rank's 6,912 columns are 108 waves in the column kernel (one per CU, a
 // serial 79-level chain each: 44 us); here 1,728.
 // kEpiU levels per thread per pass: 5 covers 79 levels in one pass of loads (3 took
-// two dependent rounds of them; one rank's 6,912 columns, tools/epi_ab.py)
+// two dependent rounds of them; one rank's 6,912 columns, tools/ab.py)
 constexpr int kEpiCols = 16, kEpiLanes = 16;
 template <typename DT, int kEpiU>
 __global__ __launch_bounds__(kEpiCols * kEpiLanes) void ml_epilogue_levels_kernel(EpilogueArgs<DT> a)
@@ -306,7 +306,7 @@ int epilogue_impl(const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, int n
     a.dt = dt;
     // level-parallel on small grids (one rank's share of C96 over 8, 6,912 columns: step
     // 0.092 -> 0.061 ms), the column kernel on large ones (full C96, 55,296 columns:
-    // 0.2065 vs 0.2080 ms) (tools/epi_ab.py, profiles/r04j_epi_ab.log);
+    // 0.2065 vs 0.2080 ms) (tools/ab.py, profiles/r04j_epi_ab.log);
     // FV3_EPILOGUE_PATH=levels|columns forces one
     const size_t smem = epi_levels_smem(nz, sizeof(DT));
     const char* path = fv3::variant_env("FV3_EPILOGUE_PATH");
@@ -315,8 +315,11 @@ int epilogue_impl(const fv3_epilogue_io* io, fv3_layout lay, int64_t ncol, int n
     if (path && path[0] == 'l') levels = true;
     if (levels && smem <= kEpiMaxSmem) {
         const int64_t grid = (ncol + kEpiCols - 1) / kEpiCols;
+        auto kfn = ml_epilogue_levels_kernel<DT, 5>;
+#if FV3_VARIANT_KERNELS
         const char* u = fv3::variant_env("FV3_EPI_U");  // A/B: 3 (round 4) | 5
-        auto kfn = (u && u[0] == '3') ? ml_epilogue_levels_kernel<DT, 3> : ml_epilogue_levels_kernel<DT, 5>;
+        if (u && u[0] == '3') kfn = ml_epilogue_levels_kernel<DT, 3>;
+#endif
         hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kEpiCols * kEpiLanes), smem, (hipStream_t)stream, a);
     } else {
         const int block = 64;  // one wave: C96's 864 waves spread over every CU (256-thread blocks left 40 idle)

@@ -303,7 +303,7 @@ def copy_fence(stream, idle):
     but with it the runtime's pageable in-copies run at full rate while the previous
     block's out-copies (arena DMA on another stream) drain; without it the two
     directions shared the link as if in sequence.  Measured on the pipelined C384 call
-    (two float64 fields in, two float32 out, six tile blocks; tools/h2h_overlap_ab.py,
+    (two float64 fields in, two float32 out, six tile blocks; tools/host_ab.py,
     profiles/r05l_h2h_overlap.json): 32.55 -> 24.46 ms, the host's time inside the
     in-copy calls 30.2 -> 22.0 ms; the same wait on the out-copy stream, a second kernel
     or fresh streams changed nothing."""

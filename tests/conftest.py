@@ -22,6 +22,16 @@ def set_variant(monkeypatch, name: str, value: str) -> None:
     monkeypatch.setenv(name, value)
 
 
+def require_variant_kernels() -> None:
+    """Skip unless the loaded library holds the variant kernels (csrc/common.h
+    FV3_VARIANT_KERNELS: tools/ variant builds only; the product library keeps the kernels
+    its own heuristics pick)."""
+    from fv3net_amd import _native
+
+    if _native.load().fv3_build_kind() == b"product":
+        pytest.skip("variant kernel: not in the product library (tools/build_variant.sh builds it)")
+
+
 @pytest.fixture(scope="session")
 def gpu():
     import torch

@@ -17,7 +17,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import ROOT, set_variant
+from conftest import ROOT, require_variant_kernels, set_variant
 from oracle import coarsen as OC
 from oracle.dense import dense_predict
 from oracle.mappm import oracle_mappm
@@ -197,6 +197,7 @@ def test_mappm_ignores_stale_lds(gpu, dirty, kord, path, monkeypatch):
     from tests.remap_exact import mappm_device
 
     if path == "lds":
+        require_variant_kernels()
         set_variant(monkeypatch, "FV3_MAPPM_LDS", "1")
     else:
         set_variant(monkeypatch, "FV3_MAPPM_PATH", path)
