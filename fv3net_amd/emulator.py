@@ -81,6 +81,41 @@ def zhao_carr_outputs(nz: int = 79) -> List[EmulatorOutput]:
     ]
 
 
+def features_outputs_from_config(train_config: Mapping, out_nz: Mapping[str, int], nz: int = 79):
+    """(features, outputs) of a microphysics training configuration
+    (fv3fit/train_microphysics.py's ``TrainConfig``, e.g. projects/microphysics/train/
+    dense.yaml, read with yaml.safe_load): ``model.input_variables`` sorted by name (the
+    order combine_inputs concatenates them, architecture.py:27-50), each a raw variable
+    or the ``to`` of a ``tensor_transform`` LogTransform entry (``source``,
+    ``transform.epsilon``); ``model.direct_out_variables`` in order, each a direct output
+    or the ``to`` of a Difference entry (``before`` / ``after``: the kernel adds the raw
+    ``before`` and names the result ``after``).  ``out_nz``: levels per direct output (1
+    for a surface field such as total_precipitation; default ``nz``)."""
+    transforms = {t["to"]: t for t in (train_config.get("tensor_transform") or [])}
+    model = train_config.get("model") or {}
+    feats = []
+    for name in model.get("input_variables") or []:
+        t = transforms.get(name)
+        if t is not None and "source" in t:
+            eps = float((t.get("transform") or {}).get("epsilon", 1e-30))
+            feats.append(EmulatorFeature(name, t["source"], eps))
+        elif t is not None:
+            raise NotImplementedError(f"input {name!r}: only LogTransform inputs are supported")
+        else:
+            feats.append(EmulatorFeature(name, name))
+    outs = []
+    for name in model.get("direct_out_variables") or []:
+        t = transforms.get(name)
+        n = int(out_nz.get(name, nz))
+        if t is not None and "before" in t:
+            outs.append(EmulatorOutput(name, n, t["before"], t["after"]))
+        elif t is not None:
+            raise NotImplementedError(f"output {name!r}: only Difference transforms are supported")
+        else:
+            outs.append(EmulatorOutput(name, n))
+    return sorted(feats, key=lambda f: f.name), outs
+
+
 def fit_center_per_feature(x) -> np.ndarray:
     """MeanMethod.per_feature (normalization2.py:75-77), float32."""
     x = np.asarray(x)
@@ -174,6 +209,30 @@ class MicrophysicsEmulator:
                       out_biases=[np.zeros(o.nz, np.float32) for o in outputs],
                       out_mean=out_mean, out_sigma=out_sigma, in_mean=in_mean, in_sigma=in_sigma)
         return cls(features, outputs, DenseColumnModel(cfg, params), precision=precision)
+
+    def predictor(self):
+        """This emulator as a registered predictor: the drop-in for the reference's
+        ``all-keras-dict`` emulator model (``PureKerasDictPredictor``,
+        pure_keras.py:181-258): raw variables in, after-states and direct outputs out,
+        ``predict`` on (z, ...) datasets, ``dump`` / ``load`` through the registry
+        (``mi355x-dense`` with input sources, its precision kept)."""
+        from .predictor import DenseColumnPredictor
+
+        return DenseColumnPredictor(self.raw_inputs, [o.after or o.name for o in self.outputs], self.model,
+                                    input_sources=[f.source for f in self.features])
+
+    @classmethod
+    def from_predictor(cls, pred) -> "MicrophysicsEmulator":
+        """The emulator behind a loaded ``predictor()`` (its outputs named by their
+        after-state, the name the kernel writes)."""
+        cfg = pred.model.config
+        sources = dict(zip(cfg.input_variables, pred._sources))
+        feats = [EmulatorFeature(n, sources[n], cfg.input_log_eps.get(n)) for n in cfg.input_variables]
+        outs = []
+        for name, nz in zip(cfg.output_variables, cfg.out_nz):
+            r = cfg.output_residuals.get(name)
+            outs.append(EmulatorOutput(name, nz, sources[r], name) if r else EmulatorOutput(name, nz))
+        return cls(feats, outs, pred.model)
 
     def params_by_name(self) -> dict:
         """Weights/normalisations keyed like the oracle (tests)."""

@@ -210,13 +210,20 @@ def _level_dim(dims, unstacked_dims):
 @register("mi355x-dense")
 class DenseColumnPredictor(Predictor):
     """fv3fit DenseModel (``PureKerasModel`` with ``unstacked_dims=("z",)``, n_halo 0)
-    predicting on MI355X through the fused HIP kernel."""
+    predicting on MI355X through the fused HIP kernel.
+
+    ``input_sources``: for a model whose input features are derived from the dataset's
+    variables in the graph -- the microphysics emulator's dict model (``all-keras-dict``,
+    ``PureKerasDictPredictor``, pure_keras.py:181-258) takes raw variables and logs some
+    of them inside (transforms.py:111-129) -- the dataset variable each model feature
+    reads (``cfg.input_variables`` order; the kernel applies the feature's LogTransform).
+    The predictor's ``input_variables`` are then those variables, each once, in order."""
 
     _CONFIG_FILENAME = "config.yaml"
     _MODEL_DIR = "dense"
 
     def __init__(self, input_variables, output_variables, model, unstacked_dims: Sequence[str] = ("z",),
-                 n_halo: int = 0):
+                 n_halo: int = 0, input_sources: Optional[Sequence[str]] = None):
         super().__init__(input_variables, output_variables)
         if n_halo != 0:
             raise NotImplementedError("halo models (n_halo > 0) are out of scope (SURVEY.md §8(e))")
@@ -226,7 +233,12 @@ class DenseColumnPredictor(Predictor):
         self._unstacked_dims = tuple(unstacked_dims)
         self._n_halo = n_halo
         cfg = model.config
-        if list(cfg.input_variables) != self.input_variables or list(cfg.output_variables) != self.output_variables:
+        features = list(cfg.input_variables)
+        self._sources = list(input_sources) if input_sources is not None else features
+        if len(self._sources) != len(features):
+            raise ValueError(f"{len(self._sources)} input sources for {len(features)} model inputs")
+        if list(dict.fromkeys(self._sources)) != self.input_variables or \
+                list(cfg.output_variables) != self.output_variables:
             raise ValueError("model variables do not match the predictor's")
 
     # -- predict ----------------------------------------------------------------
@@ -293,11 +305,11 @@ class DenseColumnPredictor(Predictor):
                 raise ValueError(f"{name} will be broadcast to include unallowed dimensions {missing}. "
                                  "This could greatly increase the size of dataset.")
         # one common column order: the first input's horizontal dims
-        first = sub[self.input_variables[0]]
+        first = sub[self._sources[0]]
         col_dims = [d for d in first.dims if d not in self._unstacked_dims]
         col_shape = [dict(zip(first.dims, first.shape))[d] for d in col_dims]
         in_specs, axes, host = [], [], True
-        for v, name in enumerate(self.input_variables):
+        for v, name in enumerate(self._sources):  # per model feature: the variable it reads
             da = sub[name]
             lv = _level_dim(da.dims, self._unstacked_dims)
             if set(d for d in da.dims if d != lv) != set(col_dims):
@@ -344,9 +356,14 @@ class DenseColumnPredictor(Predictor):
         os.makedirs(path, exist_ok=True)
         self.model.dump(os.path.join(path, self._MODEL_DIR))
         with open(os.path.join(path, self._CONFIG_FILENAME), "w") as f:
-            yaml.safe_dump({"input_variables": list(self.input_variables),
-                            "output_variables": list(self.output_variables),
-                            "unstacked_dims": list(self._unstacked_dims), "n_halo": self._n_halo}, f)
+            config = {"input_variables": list(self.input_variables),
+                      "output_variables": list(self.output_variables),
+                      "unstacked_dims": list(self._unstacked_dims), "n_halo": self._n_halo}
+            if self._sources != list(self.model.config.input_variables):
+                config["input_sources"] = list(self._sources)
+            if getattr(self.model, "precision", "f32") != "f32":
+                config["precision"] = self.model.precision
+            yaml.safe_dump(config, f)
 
     @classmethod
     def load(cls, path: str) -> "DenseColumnPredictor":
@@ -355,8 +372,11 @@ class DenseColumnPredictor(Predictor):
         with open(os.path.join(path, cls._CONFIG_FILENAME)) as f:
             config = yaml.safe_load(f)
         model = DenseColumnModel.load(os.path.join(path, cls._MODEL_DIR))
+        if config.get("precision"):
+            model.precision = config["precision"]
         return cls(config["input_variables"], config["output_variables"], model,
-                   unstacked_dims=config.get("unstacked_dims") or ("z",), n_halo=config.get("n_halo", 0))
+                   unstacked_dims=config.get("unstacked_dims") or ("z",), n_halo=config.get("n_halo", 0),
+                   input_sources=config.get("input_sources"))
 
 
 def _as_contig(t):

@@ -153,3 +153,83 @@ def test_pytorch_column_predictor_matches_torch(gpu, tmp_path):
         got = got.reshape(nt * nx * ny, nf)
         err = np.abs(got - ref) / (np.abs(ref - sc[n].mean).max(axis=0) + 1e-30)
         assert err.max() < 1e-5, (n, err.max())
+
+
+def _training_config_from_spec(spec):
+    """A microphysics TrainConfig (train_microphysics.py:127-166, the dense.yaml shape)
+    rebuilt from the emulator restatement's spec (oracle/emulator.py): the model inputs
+    in a scrambled order, a LogTransform entry per log feature, a Difference entry per
+    after-state output."""
+    tt = []
+    for f in spec["features"]:
+        if f.get("log_eps"):
+            tt.append({"to": f["name"], "source": f["source"], "transform": {"epsilon": f["log_eps"]}})
+    for o in spec["outputs"]:
+        if o.get("after"):
+            tt.append({"to": o["name"], "before": o["residual_of"], "after": o["after"]})
+    names = [f["name"] for f in spec["features"]]
+    return {"tensor_transform": tt,
+            "model": {"architecture": {"name": "dense", "kwargs": {"width": 256, "depth": 2}},
+                      "input_variables": names[::-1],
+                      "direct_out_variables": [o["name"] for o in spec["outputs"]]}}
+
+
+def test_emulator_training_config_parse():
+    """fv3net_amd.emulator.features_outputs_from_config on a training configuration
+    gives the product's Zhao-Carr features and outputs (sorted inputs, LogTransform
+    sources and epsilons, Difference before / after), as the restatement specifies."""
+    from fv3net_amd import emulator as E
+    from oracle import emulator as OE
+
+    spec = OE.zhao_carr_spec()
+    feats, outs = E.features_outputs_from_config(_training_config_from_spec(spec), {"total_precipitation": 1})
+    assert feats == E.zhao_carr_features()
+    assert outs == E.zhao_carr_outputs()
+    with pytest.raises(NotImplementedError):
+        E.features_outputs_from_config({"tensor_transform": [{"to": "x", "before": "a", "after": "b"}],
+                                        "model": {"input_variables": ["x"]}}, {})
+
+
+def test_emulator_dict_exporter_writer_round_trip(tmp_path):
+    """write_emulator_predictor (the all-keras-dict path of tools/export_keras_dense.py
+    after the TF read) -> an mi355x-dense directory with input sources -> load: raw
+    variables in, after-states out, the weights and scalar norm scales broadcast per
+    level, the bf16x3 precision kept."""
+    from export_keras_dense import write_emulator_predictor
+    from fv3net_amd.emulator import MicrophysicsEmulator
+    from fv3net_amd.predictor import DenseColumnPredictor, load
+    from oracle import emulator as OE
+
+    spec = OE.zhao_carr_spec(nz=12)
+    cfg = _training_config_from_spec(spec)
+    rng = np.random.default_rng(3)
+    nz, w = 12, 32
+    feats = [f["name"] for f in spec["features"]]
+    outs = {o["name"]: o["nz"] for o in spec["outputs"]}
+    params = {"hidden_kernels": [rng.normal(size=(nz * len(feats), w)), rng.normal(size=(w, w))],
+              "hidden_biases": [rng.normal(size=w), rng.normal(size=w)],
+              "in_center": {n: rng.normal(size=nz) for n in feats},
+              "in_scale": {n: np.float32(rng.uniform(1, 2)) for n in feats},
+              "out_kernels": {n: rng.normal(size=(w, k)) for n, k in outs.items()},
+              "out_biases": {n: rng.normal(size=k) for n, k in outs.items()},
+              "out_center": {n: rng.normal(size=k) for n, k in outs.items()},
+              "out_scale": {n: np.float32(rng.uniform(1, 2)) for n, k in outs.items()}}
+    write_emulator_predictor(str(tmp_path), cfg, outs, nz, params)
+    pred = load(str(tmp_path))
+    assert isinstance(pred, DenseColumnPredictor)
+    # the raw variables, each once, in the order the sorted features first read them
+    assert pred.input_variables == list(dict.fromkeys(f["source"] for f in spec["features"]))
+    assert len(pred.input_variables) == 6
+    assert pred.output_variables[0] == "total_precipitation"
+    assert pred.output_variables[1:] == [o["after"] for o in spec["outputs"][1:]]
+    assert pred.model.precision == "bf16x3"
+    emu = MicrophysicsEmulator.from_predictor(pred)
+    assert [(f.name, f.source, f.log_eps) for f in emu.features] == \
+        [(f["name"], f["source"], f.get("log_eps")) for f in spec["features"]]
+    p = emu.params_by_name()
+    for n in feats:
+        np.testing.assert_array_equal(p["in_center"][n], np.asarray(params["in_center"][n], np.float32))
+        assert p["in_scale"][n] == params["in_scale"][n]
+    for o in spec["outputs"]:
+        key = o.get("after") or o["name"]
+        np.testing.assert_array_equal(p["out_kernels"][key], np.asarray(params["out_kernels"][o["name"]], np.float32))

@@ -255,3 +255,41 @@ def test_emulator_workload_c12(gpu):
     assert res["total_precipitation"].shape == (W.c_columns(12),)
     assert all(torch.isfinite(v).all() for v in res.values())
     assert wl.flops_per_column == 2 * (711 * 256 + 256 * 256 + 256 * 396)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["torch", "numpy"])
+def test_emulator_as_registered_predictor(gpu, tmp_path, kind):
+    """The emulator as the drop-in for the reference's all-keras-dict model
+    (PureKerasDictPredictor, pure_keras.py:181-258): ``emulator.predictor()`` predicts on a
+    (z, y, x) dataset of the raw variables, and after dump / load through the registry,
+    bit for bit what the emulator gives on the same columns (device tensors and host
+    numpy arrays); the loaded predictor keeps bf16x3 and rebuilds the same emulator."""
+    import torch
+
+    from fv3net_amd import dataset as D
+    from fv3net_amd.emulator import MicrophysicsEmulator
+    from fv3net_amd.predictor import dump, load
+
+    emu, raw = _emulator(ncol=24 * 24, seed=4)
+    state = {k: torch.from_numpy(np.ascontiguousarray(v.T)).cuda() for k, v in raw.items()}  # [nz, ncol]
+    want = {k: v.clone() for k, v in emu(state).items()}
+    torch.cuda.synchronize()
+    ds = D.Dataset()
+    for k, v in state.items():
+        arr = v.reshape(v.shape[0], 24, 24)
+        ds[k] = D.DataArray(arr if kind == "torch" else arr.cpu().numpy(), ["z", "y", "x"])
+    pred = emu.predictor()
+    dump(pred, str(tmp_path))
+    loaded = load(str(tmp_path))
+    assert loaded.model.precision == "bf16x3"
+    for p in (pred, loaded):
+        out = p.predict(ds)
+        for name, w in want.items():
+            got = out[name].data
+            got = got if isinstance(got, torch.Tensor) else torch.from_numpy(np.asarray(got)).cuda()
+            assert tuple(out[name].dims) == (("z", "y", "x") if w.dim() == 2 else ("y", "x")), name
+            assert torch.equal(got.reshape(w.shape).contiguous().view(torch.int32), w.view(torch.int32)), name
+    again = MicrophysicsEmulator.from_predictor(loaded)(state)
+    for name, w in want.items():
+        assert torch.equal(again[name].view(torch.int32), w.view(torch.int32)), name
