@@ -23,6 +23,7 @@ Rank 0 prints ONE JSON line on stdout (everything else goes to stderr), with
   extra:        other configs measured on the same GPU (N=1, rank 0).
 """
 import argparse
+import datetime
 import hashlib
 import json
 import os
@@ -1010,7 +1011,10 @@ def main():
         import torch.distributed as tdist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        tdist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        # a rank that fails outside a collective ends the job in minutes, not at the
+        # default 10-minute watchdog
+        tdist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev,
+                                 timeout=datetime.timedelta(minutes=5))
         dist = tdist
 
     from fv3net_amd import workloads as W
