@@ -202,3 +202,50 @@ def test_restarts_reference_regression_data(gpu, tag, agrid):
     grid, restarts = OR.kat_inputs()
     got = _to_np(coarsen_restarts_on_pressure(2, grid, restarts, coarsen_agrid_winds=agrid))
     _check_against_reference(got, _expected(_golden(), tag))
+
+
+def test_regrid_vertical_default_vs_oracle(gpu):
+    """regridz.regrid_vertical (z last) on the default arithmetic: within 1e-6 per level
+    of the oracle on rough columns, and exact=True bit-identical to it."""
+    from fv3net_amd.coarsen import regrid_vertical
+
+    rng = np.random.default_rng(31)
+    km, kn = 79, 40
+    delp = rng.uniform(1, 3000, (6, 8, km))
+    p_in = 300 + np.concatenate([np.zeros((6, 8, 1)), np.cumsum(delp, -1)], -1)
+    f_in = 250 + rng.normal(0, 10, (6, 8, km))
+    p_out = np.sort(rng.uniform(p_in[..., :1] * 0.9, p_in[..., -1:] * 1.05, (6, 8, kn + 1)), -1)
+    col = lambda a: np.ascontiguousarray(a.reshape(-1, a.shape[-1]).T).astype(np.float32)  # noqa: E731
+    ref = oracle_mappm(col(p_in), col(f_in), col(p_out)).T.reshape(6, 8, kn)
+    got = regrid_vertical(p_in, f_in, p_out).cpu().numpy()
+    assert _rel(got, ref, axis=2) <= 1e-6
+    exact = regrid_vertical(p_in, f_in, p_out, exact=True).cpu().numpy()
+    assert (exact.view(np.uint32) == ref.view(np.uint32)).all()
+
+
+def test_prepared_plans_default_arithmetic(gpu):
+    """MappmPlan / MappmMultiPlan on their default arithmetic: bit-identical to
+    mappm_device / mappm_device_multi on the same buffers (the same fast kernels), and
+    exact=True bit-identical to the exact calls."""
+    import torch
+
+    from fv3net_amd.mappm import MappmMultiPlan, MappmPlan, mappm_device, mappm_device_multi
+
+    rng = np.random.default_rng(32)
+    km, kn, ncol = 79, 79, 30000
+    delp = rng.uniform(1, 3000, (km, ncol)).astype(np.float32)
+    pe1 = np.concatenate([np.full((1, ncol), 300, np.float32), 300 + np.cumsum(delp, 0, dtype=np.float32)])
+    pe2 = np.sort(rng.uniform(pe1[0] * 0.9, pe1[-1] * 1.05, (kn + 1, ncol)), 0).astype(np.float32)
+    qa = (250 + rng.normal(0, 10, (km, ncol))).astype(np.float32)
+    qb = (rng.normal(0, 1e-3, (km, ncol))).astype(np.float32)
+    d1, da, db, d2 = (torch.from_numpy(a).cuda() for a in (pe1, qa, qb, pe2))
+    eq = lambda x, y: torch.equal(x.view(torch.int32), y.view(torch.int32))  # noqa: E731
+    for exact in (False, True):
+        assert eq(MappmPlan(d1, da, d2, 1, 1, exact=exact)(), mappm_device(d1, da, d2, 1, 1, exact=exact))
+        outs = MappmMultiPlan(d1, [da, db], d2, 1, 1, exact=exact)()
+        want = mappm_device_multi(d1, [da, db], d2, 1, 1, exact=exact)
+        assert all(eq(o, w) for o, w in zip(outs, want))
+    fast = mappm_device(d1, da, d2, 1, 1)
+    ref = mappm_device(d1, da, d2, 1, 1, exact=True)
+    assert not torch.equal(fast, ref)  # the default is the fast kernel
+    assert ((fast.double() - ref.double()).abs().amax(1) / ref.double().abs().amax(1)).max().item() <= 1e-6
