@@ -24,6 +24,7 @@
 // the layer search fails (NaN here), qs for iv=-2 with kord>7 (0 here), and a
 // non-monotone pe2 that leaves the column below the old surface and re-enters.
 #pragma once
+#include <type_traits>
 
 #ifndef FV3_HD
 #define FV3_HD
@@ -499,18 +500,34 @@ FV3_HD inline void layer_hook(C&, long) {}
 // back edge (the mappm kernel: measured faster there, 0.527 vs 0.535 ms at C384 kord 1)
 // or at the iteration's start (the coarsen kernels: 1 field 0.767 -> 0.753 ms,
 // profiles/r04o_remap_ab.log).  Same loads, same bits.
-template <class Col, bool FAST = true, bool CARRY = false>
+// RING: the window E_L in rings of 5 registers -- element i of the window at layer L in
+// slot (L - 1 + i) % 5, so advancing it writes the one new element and moves nothing --
+// with the layer loop run in groups of 5 (one per ring phase, every slot index a
+// compile-time constant).  Shifting the arrays (RING = false) costs ~14 v_mov_b32 per
+// layer.  Same operations on the same values: the same bits.  Measured (one box,
+// interleaved): the fast single-field mappm kernel 0.384 -> 0.367 ms at C384 kord 1
+// (profiles/r06zk_ring_ab.log); with it the exact kernel went 0.499 -> 0.533 and the
+// one-field coarsen 0.577 -> 0.662 ms (five copies of their larger layer bodies,
+// profiles/r06zi_ring_ab.log), so only the former takes it.
+template <class Col, bool FAST = true, bool CARRY = false, bool RING = false>
 FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
 {
-    // window state E_L: q(L..L+3), dp(L..L+3), pe1(L..L+4), dc(L..L+2), ALraw(L..L+2), h2(L-1..L+1)
-    float qv[4], dpv[4], pev[5], dcv[3], alv[3], h2v[3];
+    // window state E_L: q(L..L+3), dp(L..L+3), pe1(L..L+4), dc(L..L+2), ALraw(L..L+2),
+    // h2(L-1..L+1) (RING: in their ring slots; else element i at index i)
+    constexpr int R = 5;
+    constexpr int RQ = RING ? R : 4, RD = RING ? R : 3;  // the shifting window's own sizes otherwise
+    float qv[RQ], dpv[RQ], pev[R], dcv[RD], alv[RD], h2v[RD];
     float ar_km = 0.0f;
     const bool huynh = kord >= 7;
 
-    // prologue (levels 1..4 exist because km >= 4)
+    // prologue (levels 1..4 exist because km >= 4): phase 0, element i in slot i
     for (int i = 0; i < 4; ++i) qv[i] = c.q1(1 + i);
     for (int i = 0; i < 5; ++i) pev[i] = c.pe1(1 + i);
     for (int i = 0; i < 4; ++i) dpv[i] = pev[i + 1] - pev[i];
+    if constexpr (RING) {
+        qv[RQ - 1] = dpv[RQ - 1] = 0.0f;
+        for (int i = 3; i < RD; ++i) dcv[i] = alv[i] = h2v[i] = 0.0f;
+    }
 
     const ColumnEnds ends{pev[0], c.pe1(km + 1), qv[0], c.q1(km)};
 
@@ -541,7 +558,10 @@ FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
             pec_pf = c.pe1(6);
         }
     }
-    for (int L = 1; L <= km; ++L) {
+    // layer L at ring phase P = (L - 1) % 5 (RING; else 0); returns true after the last layer
+    auto layer = [&](int L, auto phase) -> bool {
+        constexpr int P = RING ? decltype(phase)::value : 0;
+#define FV3_W(arr, i) arr[(P + (i)) % R]  // RING: slot of element i; else (P = 0) index i
         float q_pf = qc_pf, pe_pf = pec_pf;
         if constexpr (!CARRY) {
             if (L + 4 <= km) {
@@ -550,19 +570,19 @@ FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
             }
         }
         // ---- emit the final coefficients of layer L ----
-        Ppm a{qv[0], alv[0], (L < km) ? alv[1] : ar_km, 0.0f};
-        const float dcL = dcv[0];
+        Ppm a{FV3_W(qv, 0), FV3_W(alv, 0), (L < km) ? FV3_W(alv, 1) : ar_km, 0.0f};
+        const float dcL = FV3_W(dcv, 0);
         if (L <= 2 || L >= km - 1) {
             a.a6 = a6_of(a);
             ppm_limit(dcL, a, 0);
         } else if (huynh) {
-            ppm_huynh(a, dcL, h2v[0], h2v[2]);
+            ppm_huynh(a, dcL, FV3_W(h2v, 0), FV3_W(h2v, 2));
             if (iv == 0) ppm_limit(dcL, a, 2);
         } else {
             if (kord != 4) a.a6 = a6_of(a);
             if (kord != 6) ppm_limit(dcL, a, lmt);
         }
-        const LayerView v{pev[0], pev[1], dpv[0], qv[0], a};
+        const LayerView v{FV3_W(pev, 0), FV3_W(pev, 1), FV3_W(dpv, 0), FV3_W(qv, 0), a};
 #ifdef FV3_EXP_NOREMAP  // experiment only (results invalid): profile cost without the consumer
         if (L <= kn) c.emit(L, v.a.al + v.a.ar + v.a.a6);
 #else
@@ -573,14 +593,14 @@ FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
 #endif
         layer_hook(c, 0);
 
-        if (L == km) break;
-        // ---- advance the window E_L -> E_{L+1} ----
+        if (L == km) return true;
+        // ---- advance the window E_L -> E_{L+1}: one new element per ring ----
         const int j = L + 4;  // level to ingest
         float qn = 0.0f, pen = 0.0f, dpn = 0.0f;
         if (j <= km) {
             qn = q_pf;
             pen = pe_pf;
-            dpn = pen - pev[4];
+            dpn = pen - FV3_W(pev, 4);
         }
         if constexpr (CARRY) {
             if (j + 1 <= km) {  // level j + 1, for the next iteration
@@ -592,25 +612,52 @@ FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
         float dcm = 0.0f, alm = 0.0f;
         if (m <= km - 1) {
 #ifdef FV3_EXP_NOPROFILE  // experiment only (results invalid): consumer cost without dc/al
-            dcm = qn - qv[3];
-            alm = 0.5f * (qv[2] + qv[3]);
+            dcm = qn - FV3_W(qv, 3);
+            alm = 0.5f * (FV3_W(qv, 2) + FV3_W(qv, 3));
 #else
-            dcm = ppm_dc(qv[2], qv[3], qn, dpv[2], dpv[3], dpn);
-            alm = ppm_al(dpv[1], dpv[2], dpv[3], dpn, qv[2], qv[3], dcv[2], dcm);
+            dcm = ppm_dc(FV3_W(qv, 2), FV3_W(qv, 3), qn, FV3_W(dpv, 2), FV3_W(dpv, 3), dpn);
+            alm = ppm_al(FV3_W(dpv, 1), FV3_W(dpv, 2), FV3_W(dpv, 3), dpn, FV3_W(qv, 2), FV3_W(qv, 3),
+                         FV3_W(dcv, 2), dcm);
 #endif
         } else if (m == km) {
             // bottom: area-preserving cubic (mappm.f90:729-761)
-            ppm_bottom_cubic(qv[3], qv[2], dpv[3], dpv[2], alv[2], iv, alm, ar_km, dcm);
+            ppm_bottom_cubic(FV3_W(qv, 3), FV3_W(qv, 2), FV3_W(dpv, 3), FV3_W(dpv, 2), FV3_W(alv, 2), iv, alm, ar_km,
+                             dcm);
         }
         float h2n = 0.0f;  // h2(L+2)
-        if (huynh && L + 2 <= km - 1) h2n = ppm_h2(dcv[1], dcm, dpv[1], dpv[2], dpv[3]);
+        if (huynh && L + 2 <= km - 1) h2n = ppm_h2(FV3_W(dcv, 1), dcm, FV3_W(dpv, 1), FV3_W(dpv, 2), FV3_W(dpv, 3));
 
-        qv[0] = qv[1]; qv[1] = qv[2]; qv[2] = qv[3]; qv[3] = qn;
-        dpv[0] = dpv[1]; dpv[1] = dpv[2]; dpv[2] = dpv[3]; dpv[3] = dpn;
-        pev[0] = pev[1]; pev[1] = pev[2]; pev[2] = pev[3]; pev[3] = pev[4]; pev[4] = pen;
-        dcv[0] = dcv[1]; dcv[1] = dcv[2]; dcv[2] = dcm;
-        alv[0] = alv[1]; alv[1] = alv[2]; alv[2] = alm;
-        h2v[0] = h2v[1]; h2v[1] = h2v[2]; h2v[2] = h2n;
+        if constexpr (RING) {
+            // window at L + 1: element i in slot (P + 1 + i) % 5; the new last elements
+            FV3_W(qv, 4) = qn;    // q(L+4)   = element 3 at L + 1
+            FV3_W(dpv, 4) = dpn;  // dp(L+4)
+            FV3_W(pev, 5) = pen;  // pe1(L+5) = element 4 at L + 1 (pe1(L)'s slot, now dead)
+            FV3_W(dcv, 3) = dcm;  // dc(L+3)  = element 2 at L + 1
+            FV3_W(alv, 3) = alm;
+            FV3_W(h2v, 3) = h2n;  // h2(L+2)  = element 2 at L + 1
+        } else {
+            qv[0] = qv[1]; qv[1] = qv[2]; qv[2] = qv[3]; qv[3] = qn;
+            dpv[0] = dpv[1]; dpv[1] = dpv[2]; dpv[2] = dpv[3]; dpv[3] = dpn;
+            pev[0] = pev[1]; pev[1] = pev[2]; pev[2] = pev[3]; pev[3] = pev[4]; pev[4] = pen;
+            dcv[0] = dcv[1]; dcv[1] = dcv[2]; dcv[2] = dcm;
+            alv[0] = alv[1]; alv[1] = alv[2]; alv[2] = alm;
+            h2v[0] = h2v[1]; h2v[1] = h2v[2]; h2v[2] = h2n;
+        }
+#undef FV3_W
+        return false;
+    };
+    using std::integral_constant;
+    if constexpr (RING) {
+        for (int L = 1;; L += R) {
+            if (layer(L, integral_constant<int, 0>{})) break;
+            if (layer(L + 1, integral_constant<int, 1>{})) break;
+            if (layer(L + 2, integral_constant<int, 2>{})) break;
+            if (layer(L + 3, integral_constant<int, 3>{})) break;
+            if (layer(L + 4, integral_constant<int, 4>{})) break;
+        }
+    } else {
+        for (int L = 1; L <= km; ++L)
+            if (layer(L, integral_constant<int, 0>{})) break;
     }
 #ifndef FV3_EXP_NOREMAP
     remap_finish(s, ends, kn, c);

@@ -122,6 +122,18 @@ extern "C" int host_mappm_carry(int km, const float* pe1, const float* q1, int k
     return 0;
 }
 
+// the window in register rings (RING: the fast single-field kernel's column), with CARRY
+extern "C" int host_mappm_ring(int km, const float* pe1, const float* q1, int kn, const float* pe2, float* q2,
+                               int64_t ncol, int iv, int kord)
+{
+    if (km < 4 || kn < 1 || kord > 7) return -1;
+    for (int64_t i = 0; i < ncol; ++i) {
+        Col c{pe1, q1, pe2, q2, ncol, i, kn};
+        fv3::mappm_ppm_column<Col, true, true, true>(c, km, kn, iv, kord);
+    }
+    return 0;
+}
+
 // NF fields on one pressure column in one pass (mappm_multi.h), as the fused coarsen
 // kernel runs them: q1 / q2 hold NF arrays [km][ncol] / [kn][ncol] back to back
 #include "../../fv3net_amd/csrc/mappm_multi.h"

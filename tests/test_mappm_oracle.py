@@ -89,7 +89,8 @@ def host_lib():
     os.replace(tmp, own)
     lib = ctypes.CDLL(own)
     os.unlink(own)  # the mapping stays valid; nothing is left behind
-    for fn in (lib.host_mappm, lib.host_mappm_cursor, lib.host_mappm_generic, lib.host_mappm_carry):
+    for fn in (lib.host_mappm, lib.host_mappm_cursor, lib.host_mappm_generic, lib.host_mappm_carry,
+               lib.host_mappm_ring):
         fn.restype = ctypes.c_int
         fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                        ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
@@ -107,7 +108,7 @@ def _host(lib, pe1, q, pe2, iv, kord, cursor=False):
     pe1, q, pe2 = (np.ascontiguousarray(a, np.float32) for a in (pe1, q, pe2))
     out = np.empty((pe2.shape[0] - 1, q.shape[1]), np.float32)
     fn = {True: lib.host_mappm_cursor, False: lib.host_mappm, "generic": lib.host_mappm_generic,
-          "carry": lib.host_mappm_carry}[cursor]
+          "carry": lib.host_mappm_carry, "ring": lib.host_mappm_ring}[cursor]
     rc = fn(q.shape[0], pe1.ctypes.data, q.ctypes.data, pe2.shape[0] - 1, pe2.ctypes.data, out.ctypes.data,
             q.shape[1], iv, kord)
     assert rc == 0
@@ -126,6 +127,32 @@ def test_streaming_algorithm_matches_golden(host_lib):
                     if kord <= 7:  # the device mappm kernel's build (loads carried one level ahead)
                         res = _host(host_lib, pe1, g[f"c{ci}_{qn}"], pe2, int(iv), int(kord), cursor="carry")
                         assert _bits_equal(res, g[f"c{ci}_{qn}_k{kord}_iv{iv}"]), (ci, qn, kord, iv, "carry")
+                        # the fast single-field kernel's build (window in register rings)
+                        res = _host(host_lib, pe1, g[f"c{ci}_{qn}"], pe2, int(iv), int(kord), cursor="ring")
+                        assert _bits_equal(res, g[f"c{ci}_{qn}_k{kord}_iv{iv}"]), (ci, qn, kord, iv, "ring")
+
+
+@pytest.mark.parametrize("km", [4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 17, 33, 79, 80, 127])
+def test_ring_window_is_bit_identical(host_lib, km):
+    """The column with its window in register rings (mappm_ppm_column<.., RING>: the layer
+    loop in groups of 5 ring phases) gives the shifting window's bits for every kord <= 7
+    and iv, for level counts around the group boundaries, on rough columns with shared
+    and unsorted output edges."""
+    rng = np.random.default_rng(km)
+    ncol = 64
+    for kn in (max(1, km // 2), km, km + 7):
+        for kord in (1, 2, 3, 4, 5, 6, 7):
+            for iv in (0, 1, -1, 2):
+                delp = rng.uniform(1, 3000, (km, ncol)).astype(np.float32)
+                pe1 = np.concatenate([np.full((1, ncol), 300, np.float32),
+                                      300 + np.cumsum(delp, 0, dtype=np.float32)])
+                pe2 = np.sort(rng.uniform(pe1[0] * 0.8, pe1[-1] * 1.1, (kn + 1, ncol)), 0).astype(np.float32)
+                pe2[:, :3] = pe2[::-1, :3]
+                q = (rng.normal(0, 1, (km, ncol)) * rng.choice([1e-4, 1, 300], (km, ncol))).astype(np.float32)
+                with np.errstate(all="ignore"):
+                    ref = _host(host_lib, pe1, q, pe2, iv, kord)
+                    ring = _host(host_lib, pe1, q, pe2, iv, kord, cursor="ring")
+                assert _bits_equal(ring, ref), (km, kn, kord, iv)
 
 
 @pytest.mark.parametrize("kat", KATS, ids=["identity", "out_of_bounds", "nans"])
