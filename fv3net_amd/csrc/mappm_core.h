@@ -508,7 +508,9 @@ FV3_HD inline void layer_hook(C&, long) {}
 // interleaved): the fast single-field mappm kernel 0.384 -> 0.367 ms at C384 kord 1
 // (profiles/r06zk_ring_ab.log); with it the exact kernel went 0.499 -> 0.533 and the
 // one-field coarsen 0.577 -> 0.662 ms (five copies of their larger layer bodies,
-// profiles/r06zi_ring_ab.log), so only the former takes it.
+// profiles/r06zi_ring_ab.log), so only the former takes it.  The same rings in the
+// multi-field column (mappm_multi.h) measured no faster on the C384 pair kernel and 9 %
+// slower on one rank's split-lane kernels (profiles/r06zl_ring_ab.log): not kept.
 template <class Col, bool FAST = true, bool CARRY = false, bool RING = false>
 FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
 {
