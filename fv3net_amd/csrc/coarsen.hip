@@ -404,6 +404,16 @@ struct CellCol : FineCol<DT> {
     }
 };
 
+// the one-field pass's PPM window: shifting (0, default) or register rings (1,
+// mappm_core.h RING).  At 6 waves per SIMD the rings spill (34 VGPRs against 7; 21 with
+// the layer hook once per ring group): 0.577 -> 0.662 / 0.653 ms.  At 5 they fit (95
+// VGPRs, 2 spilled) and beat the shifting window at 5 (0.612 -> 0.599 ms, hook per group),
+// but not the default's 6 (0.576 ms): profiles/r06zi_ring_ab.log, r06zo_coarsen_ring_ab.log.
+// tools/ variant builds set it (and FV3_COARSEN_W1F) for A/B.
+#ifndef FV3_COARSEN_RING
+#define FV3_COARSEN_RING 0
+#endif
+
 // one pass of the streaming remap for fields [v0, v0 + NF), then the last levels' sums
 template <int NF, typename DT, int FF>
 __device__ __forceinline__ void cells_field_group(const CoarsenArgs<DT>& a, int v0, int lane, int f, int nb, int tile,
@@ -440,7 +450,7 @@ __device__ __forceinline__ void cells_field_group(const CoarsenArgs<DT>& a, int 
     col.mine = a.scratch + (int64_t)blockIdx.x * 64 + lane;
     if constexpr (NF == 1) {
         FirstField<CellCol<DT, FF, NF>> one{col};
-        mappm_ppm_column(one, km, km, iv, kord);
+        mappm_ppm_column<FirstField<CellCol<DT, FF, NF>>, true, false, (bool)FV3_COARSEN_RING>(one, km, km, iv, kord);
     } else {
         mappm_ppm_columns<NF>(col, km, km, iv, kord);
     }

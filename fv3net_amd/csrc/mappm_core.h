@@ -507,8 +507,10 @@ FV3_HD inline void layer_hook(C&, long) {}
 // layer.  Same operations on the same values: the same bits.  Measured (one box,
 // interleaved): the fast single-field mappm kernel 0.384 -> 0.367 ms at C384 kord 1
 // (profiles/r06zk_ring_ab.log); with it the exact kernel went 0.499 -> 0.533 and the
-// one-field coarsen 0.577 -> 0.662 ms (five copies of their larger layer bodies,
-// profiles/r06zi_ring_ab.log), so only the former takes it.  The same rings in the
+// one-field coarsen 0.577 -> 0.662 ms (five copies of their larger layer bodies; the
+// coarsen's rings spill at its 6 waves per SIMD and lose at 5 too, coarsen.hip
+// FV3_COARSEN_RING, profiles/r06zi_ring_ab.log, r06zo_coarsen_ring_ab.log), so only the
+// former takes it.  The same rings in the
 // multi-field column (mappm_multi.h) measured no faster on the C384 pair kernel and 9 %
 // slower on one rank's split-lane kernels (profiles/r06zl_ring_ab.log): not kept.
 template <class Col, bool FAST = true, bool CARRY = false, bool RING = false>
@@ -593,7 +595,9 @@ FV3_HD inline void mappm_ppm_column(Col& c, int km, int kn, int iv, int kord)
         else
             remap_layer(s, v, ends, kn, c);
 #endif
-        layer_hook(c, 0);
+        // RING: once per group of R layers (a hook is free to lag: the coarsen's takes
+        // whatever whole levels every lane has emitted, and drains the rest at the end)
+        if constexpr (!RING || P == R - 1) layer_hook(c, 0);
 
         if (L == km) return true;
         // ---- advance the window E_L -> E_{L+1}: one new element per ring ----
