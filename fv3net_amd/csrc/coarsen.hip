@@ -65,6 +65,16 @@ struct CoarsenArgs {
 
 constexpr int kChunk = 16;  // delp*area levels staged per pass-1 round
 
+// the one-field cells kernel's loads as buffer operations at 32-bit offsets (1, default)
+// or through 64-bit addresses (0, A/B); the host checks every tile's array spans < 4 GiB.
+// One field 0.558 -> 0.546 ms; the two-field pass measured 1.542 -> 1.550 ms with them
+// (profiles/r06zr_coarsen_ops_ab.log), so it keeps its addresses (coarsen_bufload<NF>)
+#ifndef FV3_COARSEN_BUFLOAD
+#define FV3_COARSEN_BUFLOAD 1
+#endif
+template <int NF>
+constexpr bool coarsen_bufload() { return FV3_COARSEN_BUFLOAD && NF == 1; }
+
 // the same row sum across the f lanes of this lane's cell (every lane of the cell
 // gets the identical value): f == 8 pairwise == xor tree over aligned 8-lane groups
 template <typename T>
@@ -288,16 +298,37 @@ __global__ __launch_bounds__(512) void regrid_coarsen_kernel(CoarsenArgs<DT> a)
 // 0.757 -> 0.761 ms, so it keeps 16; profiles/r05zzh_coarsen_ring_ab.log).  A lane
 // running that many levels ahead of its cell's slowest writes to its global column.
 constexpr int ring_levels(int nf) { return nf >= 2 ? 12 : 16; }
+// levels per cell-sum batch for a compile-time factor FF (G * CH * FF <= 64), 0: run time
+constexpr int cells_batch(int ff) { return ff ? (64 / ((64 / (ff * ff)) * ff) < 8 ? 64 / ((64 / (ff * ff)) * ff) : 8) : 0; }
 constexpr int kRingLd = 65;   // ring row stride (floats): rows of one cell read bank-free
 
+typedef __amdgpu_buffer_rsrc_t MRsrc;
+__device__ __forceinline__ MRsrc mrsrc(const void* p)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0xffffffffu, 0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ T bload(MRsrc r, uint32_t voff, uint32_t soff)
+{
+    if constexpr (sizeof(T) == 8)
+        return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0));
+    else
+        return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
+}
+
 // per-level cell sums in numpy's order for nb consecutive levels of G cells:
-// val(g, kk, j) = element j = dy * f + dx of cell g at level kk; res(g, kk, sum)
-template <typename T, typename Val, typename Res>
+// val(g, kk, j) = element j = dy * f + dx of cell g at level kk; res(g, kk, sum).
+// NBM > 0: a compile-time bound on nb (the layout of NBM levels, levels >= nb skipped),
+// so no index needs a division by the run-time nb (a ~10-instruction sequence each);
+// G * NBM * f <= 64.  Same sums in the same order either way.
+template <typename T, int NBM = 0, typename Val, typename Res>
 __device__ __forceinline__ void cell_sums(int lane, int G, int f, int nb, T* rowbuf, Val val, Res res)
 {
-    const int nrow = G * nb * f;
+    const int nbl = NBM ? NBM : nb;  // levels in the row layout
+    const int nrow = G * nbl * f;
     for (int i = lane; i < nrow; i += 64) {
-        const int dy = i % f, kk = (i / f) % nb, g = i / (f * nb);
+        const int dy = i % f, kk = (i / f) % nbl, g = i / (f * nbl);
+        if (NBM && kk >= nb) continue;
         const int b = dy * f;
         T r;
         if (f == 8) {
@@ -310,11 +341,12 @@ __device__ __forceinline__ void cell_sums(int lane, int G, int f, int nb, T* row
         rowbuf[i] = r;
     }
     __syncthreads();
-    for (int i = lane; i < G * nb; i += 64) {
-        const T* rr = rowbuf + i * f;  // rows of (cell, level) i = g * nb + kk
+    for (int i = lane; i < G * nbl; i += 64) {
+        if (NBM && i % nbl >= nb) continue;
+        const T* rr = rowbuf + i * f;  // rows of (cell, level) i = g * nbl + kk
         T acc = rr[0];
         for (int dy = 1; dy < f; ++dy) acc = acc + rr[dy];
-        res(i / nb, i % nb, acc);
+        res(i / nbl, i % nbl, acc);
     }
     __syncthreads();
 }
@@ -332,8 +364,9 @@ struct CellCtx {
     int64_t sstride;    // gridDim * 64
     float* out[NF];     // the fields' outputs
 
-    // sum and write levels [k0, k0 + nb) of every cell of the block, for every field
-    __device__ void consume(int k0, int nb_) const
+    // sum and write levels [k0, k0 + nb) of every cell of the block, for every field;
+    // bit fi of ovm: some lane wrote field fi to its global column (else the ring only)
+    __device__ void consume(int k0, int nb_, unsigned ovm) const
     {
         const int gl0 = blockIdx.x * 64;
         const int f = FF ? FF : this->f, ff = f * f, G = 64 / ff;
@@ -342,11 +375,12 @@ struct CellCtx {
             const int* ov = ovf + fi * 64;
             const float* sc = scr + (int64_t)fi * km * sstride;
             float* o = out[fi];
-            cell_sums<float>(
+            const bool any = (ovm >> fi) & 1u;
+            cell_sums<float, cells_batch(FF)>(
                 lane, G, f, nb_, rowbuf,
                 [&](int g, int kk, int j) {
                     const int l = g * ff + j, k = k0 + kk;
-                    if (k >= ov[l]) return sc[(int64_t)k * sstride + gl0 + l];
+                    if (any && k >= ov[l]) return sc[(int64_t)k * sstride + gl0 + l];
                     return rg[(k % ring_levels(NF)) * kRingLd + l];
                 },
                 [&](int g, int kk, float num) {
@@ -371,8 +405,42 @@ struct CellCol : FineCol<DT> {
     int ovf_k[NF];  // first level this lane sent to its global column (km: none)
     int* ovf_lds;
     float* mine;  // this lane's global column (field 0, level 0)
+    // coarsen_bufload<NF>: loads as buffer operations: resource over this tile's array
+    // (SGPRs), the lane's byte offset (VGPR), the level's byte offset (SGPR): no per-load
+    // 64-bit address
+    MRsrc rq[NF], rdp;
+    uint32_t vq, vdp;  // lane byte offsets in a field / in delp
+    uint32_t lbq, lbdp;  // level strides in bytes
+    __device__ __forceinline__ float q1(int f, int k) const
+    {
+        if constexpr (coarsen_bufload<NF>())
+            return bload<float>(rq[f], vq, (uint32_t)(k - 1) * lbq);
+        else
+            return fields[f][off + (int64_t)(k - 1) * this->plane];
+    }
+    __device__ __forceinline__ float pe1(int k)
+    {
+        if constexpr (!coarsen_bufload<NF>()) return FineCol<DT>::pe1(k);
+        // FineCol::pe1 with the next level read at a uniform level offset
+        if (k == 1) return (float)this->ptop;
+        if (k == this->km + 1) return (float)this->pbot;
+        while (this->next < k - 1) {
+            this->run = this->run + this->dl;
+            ++this->next;
+            const int lv = __builtin_amdgcn_readfirstlane(min(this->next, this->km - 1));  // uniform
+            this->dl = bload<DT>(rdp, vdp, (uint32_t)lv * lbdp);
+        }
+        return (float)this->run;
+    }
+    // bit fi: some lane has sent field fi to its global column
+    __device__ __forceinline__ unsigned ovf_mask() const
+    {
+        unsigned m = 0;
+        for (int fi = 0; fi < NF; ++fi)
+            if (__any(ovf_k[fi] < ctx->km)) m |= 1u << fi;
+        return m;
+    }
 
-    __device__ __forceinline__ float q1(int f, int k) const { return fields[f][off + (int64_t)(k - 1) * this->plane]; }
     __device__ __forceinline__ void emit(int fi, int k, float v)
     {
         const int k0 = k - 1;
@@ -398,20 +466,29 @@ struct CellCol : FineCol<DT> {
         const int nb = FF ? std::min(8, 64 / ((64 / (FF * FF)) * FF)) : ctx->nb;
         if (__all(nemit >= kcons + nb)) {
             __syncthreads();
-            ctx->consume(kcons, nb);
+            ctx->consume(kcons, nb, ovf_mask());
             kcons += nb;
         }
     }
 };
 
-// the one-field pass's PPM window: shifting (0, default) or register rings (1,
-// mappm_core.h RING).  At 6 waves per SIMD the rings spill (34 VGPRs against 7; 21 with
-// the layer hook once per ring group): 0.577 -> 0.662 / 0.653 ms.  At 5 they fit (95
-// VGPRs, 2 spilled) and beat the shifting window at 5 (0.612 -> 0.599 ms, hook per group),
-// but not the default's 6 (0.576 ms): profiles/r06zi_ring_ab.log, r06zo_coarsen_ring_ab.log.
-// tools/ variant builds set it (and FV3_COARSEN_W1F) for A/B.
+// the one-field pass's PPM window: register rings (1, mappm_core.h RING, the default on
+// the fast arithmetic) or shifting (0, the exact kernels).  Before the buffer loads and
+// the compile-time batch freed registers, the rings spilled at 6 waves per SIMD (34 VGPRs
+// against 7; 21 with the layer hook once per ring group) and lost, 0.577 -> 0.662 / 0.653
+// ms (at 5 waves: 0.612 -> 0.599, still behind 6), profiles/r06zi_ring_ab.log,
+// r06zo_coarsen_ring_ab.log; after them (10 VGPRs spilled) they win, 0.546 -> 0.534 ms
+// (profiles/r06zr_coarsen_ops_ab.log).  tools/ variant builds set it for A/B.
 #ifndef FV3_COARSEN_RING
+#ifdef FV3_FAST_ARITH
+#define FV3_COARSEN_RING 1
+#else
 #define FV3_COARSEN_RING 0
+#endif
+#endif
+// pass 1's delp prefetch distance in 8-level chunks (1 default; 2 for A/B)
+#ifndef FV3_COARSEN_P1_DEPTH
+#define FV3_COARSEN_P1_DEPTH 1
 #endif
 
 // one pass of the streaming remap for fields [v0, v0 + NF), then the last levels' sums
@@ -448,6 +525,16 @@ __device__ __forceinline__ void cells_field_group(const CoarsenArgs<DT>& a, int 
     for (int fi = 0; fi < NF; ++fi) col.ovf_k[fi] = km;
     col.ovf_lds = ovf;
     col.mine = a.scratch + (int64_t)blockIdx.x * 64 + lane;
+    if constexpr (coarsen_bufload<NF>()) {
+        const int64_t tbase = (int64_t)tile * km * plane;  // this tile's level 0
+        for (int fi = 0; fi < NF; ++fi) col.rq[fi] = mrsrc(a.fields[v0 + fi] + tbase);
+        col.rdp = mrsrc(a.delp + tbase);
+        col.vq = (uint32_t)(off - tbase) * (uint32_t)sizeof(float);
+        col.vdp = (uint32_t)(off - tbase) * (uint32_t)sizeof(DT);
+        col.lbq = (uint32_t)plane * (uint32_t)sizeof(float);
+        col.lbdp = (uint32_t)plane * (uint32_t)sizeof(DT);
+        col.dl = bload<DT>(col.rdp, col.vdp, 0);  // start(): delp[0]
+    }
     if constexpr (NF == 1) {
         FirstField<CellCol<DT, FF, NF>> one{col};
         mappm_ppm_column<FirstField<CellCol<DT, FF, NF>>, true, false, (bool)FV3_COARSEN_RING>(one, km, km, iv, kord);
@@ -455,7 +542,8 @@ __device__ __forceinline__ void cells_field_group(const CoarsenArgs<DT>& a, int 
         mappm_ppm_columns<NF>(col, km, km, iv, kord);
     }
     __syncthreads();
-    for (int k0 = col.kcons; k0 < km; k0 += nb) ctx.consume(k0, min(nb, km - k0));
+    const unsigned ovm = col.ovf_mask();
+    for (int k0 = col.kcons; k0 < km; k0 += nb) ctx.consume(k0, min(nb, km - k0), ovm);
 }
 
 // FF: the coarsening factor at compile time (8, config #3: all index arithmetic folds),
@@ -514,18 +602,24 @@ regrid_coarsen_cells_kernel(CoarsenArgs<DT> a)
     DT run = ptop;  // fine phalf = cumsum([ptop, delp]) (vertically_dependent.py:62-63)
     DT crun = ptop;  // lanes < G: coarse phalf = cumsum([ptop, delp_c]), sequential like np.cumsum
     if (lane < G) pc[lane * (km + 1)] = ptop;
-    // the chunk after the current one is loaded before the current one is reduced
+    // the chunk after the current one (FV3_COARSEN_P1_DEPTH 2: the one after that) is
+    // loaded before the current one is reduced
     constexpr int kCH = 8;
-    DT dcur[kCH], dnxt[kCH];
-    auto load_chunk = [&](DT* dst, int k0) {
+    const MRsrc rdp = mrsrc(a.delp + (int64_t)tile * km * plane);
+    const uint32_t vdp = (uint32_t)(fine * (int64_t)sizeof(DT)), lbdp = (uint32_t)(plane * (int64_t)sizeof(DT));
+    auto load_chunk = [&](DT (&dst)[kCH], int k0) {
 #pragma unroll
-        for (int kk = 0; kk < kCH; ++kk)
-            if (kk < CH && k0 + kk < km) dst[kk] = dp[(int64_t)(k0 + kk) * plane];
+        for (int kk = 0; kk < kCH; ++kk) {
+            if (kk < CH && k0 + kk < km) {
+                if constexpr (coarsen_bufload<NF>())
+                    dst[kk] = bload<DT>(rdp, vdp, (uint32_t)(k0 + kk) * lbdp);
+                else
+                    dst[kk] = dp[(int64_t)(k0 + kk) * plane];
+            }
+        }
     };
-    load_chunk(dcur, 0);
-    for (int k0 = 0; k0 < km; k0 += CH) {
+    auto chunk = [&](const DT (&dcur)[kCH], int k0) {
         const int nk = min(CH, km - k0);
-        if (k0 + CH < km) load_chunk(dnxt, k0 + CH);
 #pragma unroll
         for (int kk = 0; kk < kCH; ++kk) {
             if (kk < nk) {
@@ -535,7 +629,7 @@ regrid_coarsen_cells_kernel(CoarsenArgs<DT> a)
             }
         }
         __syncthreads();
-        cell_sums<DT>(
+        cell_sums<DT, cells_batch(FF)>(
             lane, G, f, nk, rowd, [&](int gi, int kk, int jj) { return buf[kk * kRingLd + gi * ff + jj]; },
             [&](int gi, int kk, DT acc) {
                 const int k = k0 + kk, Xg = X0 + gi;
@@ -554,16 +648,40 @@ regrid_coarsen_cells_kernel(CoarsenArgs<DT> a)
                 p[kk] = crun;
             }
         }
+    };
+#if FV3_COARSEN_P1_DEPTH == 2
+    // three register chunks in rotating roles (the loop unrolled by three, so no chunk is
+    // copied: a copy waits for its loads at the end of the chunk before)
+    DT d0[kCH], d1[kCH], d2[kCH];
+    load_chunk(d0, 0);
+    if (CH < km) load_chunk(d1, CH);
+    for (int k0 = 0; k0 < km; k0 += 3 * CH) {
+        if (k0 + 2 * CH < km) load_chunk(d2, k0 + 2 * CH);
+        chunk(d0, k0);
+        if (k0 + CH >= km) break;
+        if (k0 + 3 * CH < km) load_chunk(d0, k0 + 3 * CH);
+        chunk(d1, k0 + CH);
+        if (k0 + 2 * CH >= km) break;
+        if (k0 + 4 * CH < km) load_chunk(d1, k0 + 4 * CH);
+        chunk(d2, k0 + 2 * CH);
+    }
+#else
+    DT dcur[kCH], dnxt[kCH];
+    load_chunk(dcur, 0);
+    for (int k0 = 0; k0 < km; k0 += CH) {
+        if (k0 + CH < km) load_chunk(dnxt, k0 + CH);
+        chunk(dcur, k0);
 #pragma unroll
         for (int kk = 0; kk < kCH; ++kk) dcur[kk] = dnxt[kk];
     }
+#endif
     const DT pbot = run;  // phalf_fine[-1] of this fine column
     lpb[lane] = pbot;
     __syncthreads();
     // masked-area denominators of every level (the same for every field)
     for (int k0 = 0; k0 < km; k0 += CH) {
         const int nk = min(CH, km - k0);
-        cell_sums<float>(
+        cell_sums<float, cells_batch(FF)>(
             lane, G, f, nk, rowf,
             [&](int gi, int kk, int jj) {
                 const int l = gi * ff + jj;
@@ -867,6 +985,9 @@ int regrid_coarsen_impl(const DT* delp, const float* area, const float* const* f
                              sizeof(float) * (64 * 3 + (size_t)G * km) + sizeof(int) * 64 * NF;
         FV3_REQUIRE(lds_c <= 64 * 1024, "regrid_coarsen: %zu B of LDS needed", lds_c);
         FV3_REQUIRE(cblocks < (int64_t)0x7fffffff, "regrid_coarsen: grid too large");
+        // buffer loads: a tile's levels at 32-bit byte offsets (FV3_COARSEN_BUFLOAD)
+        FV3_REQUIRE((int64_t)km * ny * nx * (int64_t)sizeof(DT) <= (int64_t)0xffffffff,
+                    "regrid_coarsen: one tile of %d levels spans more than 4 GiB", km);
         // per-lane overflow columns: only written by lanes that run ring_levels(NF) levels ahead
         if (n_fields > 0)
             FV3_HIP(hipMallocAsync(&scratch, sizeof(float) * NF * (size_t)km * (size_t)cblocks * 64, s));

@@ -205,6 +205,37 @@ __device__ __forceinline__ DevCol make_col(const MappmArgs& a, int64_t c)
     return d;
 }
 
+// DevColBuf of column c: q1 / pe1 through buffer loads at 32-bit offsets (the host checks
+// fits_c32), pe2 / q2 through per-lane pointers as in DevCol
+__device__ __forceinline__ DevColBuf make_col_buf(const MappmArgs& a, int64_t c)
+{
+    DevColBuf d;
+    d.r_pe1 = mrsrc(a.pe1);
+    d.r_q1 = mrsrc(a.q1);
+    d.o_pe1 = (uint32_t)(col_offset(a.l_pe1, c) * 4);
+    d.o_q1 = (uint32_t)(col_offset(a.l_q1, c) * 4);
+    d.lb_pe1 = (uint32_t)(a.l_pe1.ld * 4);
+    d.lb_q1 = (uint32_t)(a.l_q1.ld * 4);
+    d.pe2_ = a.pe2 + col_offset(a.l_pe2, c);
+    d.q2_ = a.q2 + col_offset(a.l_q2, c);
+    d.ld_pe2 = a.l_pe2.ld;
+    d.ld_q2 = a.l_q2.ld;
+    d.kn = a.kn;
+    d.pe2_next = d.pe2_ + 2 * d.ld_pe2;
+    d.nb = a.kn >= 2 ? *d.pe2_next : 0.0f;
+    return d;
+}
+
+// buffer operations at 32-bit byte offsets reach every element of an array in layout l
+// over ncol columns and nlev levels: its last column's offset plus nlev levels < 4 GiB
+inline bool fits_c32(const fv3_layout& l, int64_t ncol, int nlev)
+{
+    if (l.ld < 0 || l.blk_stride < 0) return false;
+    const int64_t c = ncol - 1;
+    const int64_t off = (l.ncol_blk <= 0 || c < l.ncol_blk) ? c : (c / l.ncol_blk) * l.blk_stride + c % l.ncol_blk;
+    return 4 * (off + (int64_t)nlev * l.ld) < (1ll << 32) - 4;
+}
+
 // the single-field column's window in register rings (mappm_core.h, RING): on the fast
 // arithmetic only, where it measured faster (0.384 -> 0.367 ms at C384 kord 1)
 #ifdef FV3_FAST_ARITH
@@ -215,13 +246,30 @@ constexpr bool kRingWindow = false;
 
 // K1: kord 1 and iv 1 (the default of regrid_vertical and of the pressure-level coarsen)
 // as compile-time constants, so every branch of mappm.f90 on kord / iv folds away
-template <bool K1>
-__global__ __launch_bounds__(256) void mappm_ppm_kernel(MappmArgs a)
+// BUF: q1 / pe1 through buffer loads at SGPR level offsets (DevColBuf), when every array
+// fits 32-bit offsets; else 64-bit addresses.  C384 kord 1: fast 0.370 -> 0.368 ms, exact
+// 0.501 -> 0.497 (profiles/r06zt_mappm_buf_ab.log)
+#ifndef FV3_MAPPM_PPM_WPE
+#define FV3_MAPPM_PPM_WPE 0  // register target in waves per SIMD (0: the compiler's, 66 VGPRs, 7 waves;
+                             // 8 spills 5 and measured 0.365 -> 0.398 ms, profiles/r06zu_mappm_wpe_ab.log)
+#endif
+#if FV3_MAPPM_PPM_WPE
+#define FV3_PPM_WPE_ATTR __attribute__((amdgpu_waves_per_eu(FV3_MAPPM_PPM_WPE, FV3_MAPPM_PPM_WPE)))
+#else
+#define FV3_PPM_WPE_ATTR
+#endif
+template <bool K1, bool BUF>
+__global__ __launch_bounds__(256) FV3_PPM_WPE_ATTR void mappm_ppm_kernel(MappmArgs a)
 {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= a.ncol) return;
-    DevCol col = make_col(a, c);
-    mappm_ppm_column<DevCol, true, true, kRingWindow>(col, a.km, a.kn, K1 ? 1 : a.iv, K1 ? 1 : a.kord);
+    if constexpr (BUF) {
+        DevColBuf col = make_col_buf(a, c);
+        mappm_ppm_column<DevColBuf, true, true, kRingWindow>(col, a.km, a.kn, K1 ? 1 : a.iv, K1 ? 1 : a.kord);
+    } else {
+        DevCol col = make_col(a, c);
+        mappm_ppm_column<DevCol, true, true, kRingWindow>(col, a.km, a.kn, K1 ? 1 : a.iv, K1 ? 1 : a.kord);
+    }
 }
 
 bool is_k1(int iv, int kord) { return iv == 1 && kord == 1; }
@@ -397,20 +445,7 @@ __global__ __launch_bounds__(256) void mappm_cs_global_kernel(MappmArgs a)
     if constexpr (C32) {
         GlobalScrBuf scr{mrsrc(a.scratch), (uint32_t)(c * 4), (uint32_t)(stride * 4),
                          (uint32_t)((a.km + 3) * stride * 4)};
-        DevColBuf d;
-        d.r_pe1 = mrsrc(a.pe1);
-        d.r_q1 = mrsrc(a.q1);
-        d.o_pe1 = (uint32_t)(col_offset(a.l_pe1, c) * 4);
-        d.o_q1 = (uint32_t)(col_offset(a.l_q1, c) * 4);
-        d.lb_pe1 = (uint32_t)(a.l_pe1.ld * 4);
-        d.lb_q1 = (uint32_t)(a.l_q1.ld * 4);
-        d.pe2_ = a.pe2 + col_offset(a.l_pe2, c);
-        d.q2_ = a.q2 + col_offset(a.l_q2, c);
-        d.ld_pe2 = a.l_pe2.ld;
-        d.ld_q2 = a.l_q2.ld;
-        d.kn = a.kn;
-        d.pe2_next = d.pe2_ + 2 * d.ld_pe2;
-        d.nb = a.kn >= 2 ? *d.pe2_next : 0.0f;
+        DevColBuf d = make_col_buf(a, c);
         mappm_cs_column<DevColBuf, GlobalScrBuf, NT, PF, KORD>(d, scr, a.km, a.kn, a.iv, a.kord);
     } else {
         GlobalScr scr{a.scratch + c, stride, (int64_t)(a.km + 3) * stride};
@@ -442,12 +477,7 @@ const void* cs_global_kernel(const MappmArgs& a, int64_t nlanes)
 #endif
     // buffer operations at 32-bit byte offsets when every array (and the scratch) spans
     // < 4 GiB: the last column's offset plus km levels
-    auto fits = [&](const fv3_layout& l, int nlev) {
-        if (l.ld < 0 || l.blk_stride < 0) return false;
-        const int64_t c = ncol - 1;
-        const int64_t off = (l.ncol_blk <= 0 || c < l.ncol_blk) ? c : (c / l.ncol_blk) * l.blk_stride + c % l.ncol_blk;
-        return 4 * (off + (int64_t)nlev * l.ld) < (1ll << 32) - 4;
-    };
+    auto fits = [&](const fv3_layout& l, int nlev) { return fits_c32(l, ncol, nlev); };
     bool c32 = fits(a.l_pe1, a.km + 1) && fits(a.l_q1, a.km) && 4 * nlanes * 2 * (int64_t)(a.km + 3) < (1ll << 32) - 4;
     if (const char* e = fv3::variant_env("FV3_MAPPM_CS_C32")) c32 = c32 && atoi(e) != 0;
 #if FV3_VARIANT_KERNELS  // the other depths and load distances (A/B)
@@ -542,10 +572,15 @@ int launch_mappm(MappmArgs a, hipStream_t stream)
     } else {
         const int block = 256;
         const int64_t grid = (a.ncol + block - 1) / block;
-        if (is_k1(a.iv, a.kord))
-            hipLaunchKernelGGL(mappm_ppm_kernel<true>, dim3((unsigned)grid), dim3(block), 0, stream, a);
-        else
-            hipLaunchKernelGGL(mappm_ppm_kernel<false>, dim3((unsigned)grid), dim3(block), 0, stream, a);
+        // q1 / pe1 by buffer loads wherever they fit 32-bit offsets (FV3_MAPPM_PPM_BUF=0:
+        // 64-bit addresses, A/B)
+        bool buf = fits_c32(a.l_pe1, a.ncol, a.km + 1) && fits_c32(a.l_q1, a.ncol, a.km);
+        if (const char* e = fv3::variant_env("FV3_MAPPM_PPM_BUF")) buf = buf && atoi(e) != 0;
+        const bool k1 = is_k1(a.iv, a.kord);
+        const void* kfn = k1 ? (buf ? (const void*)mappm_ppm_kernel<true, true> : (const void*)mappm_ppm_kernel<true, false>)
+                             : (buf ? (const void*)mappm_ppm_kernel<false, true> : (const void*)mappm_ppm_kernel<false, false>);
+        void* kargs[] = {&a};
+        FV3_HIP(hipLaunchKernel(kfn, dim3((unsigned)grid), dim3(block), kargs, 0, stream));
     }
     FV3_LAUNCH_CHECK();
     return FV3_OK;
