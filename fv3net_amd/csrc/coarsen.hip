@@ -403,6 +403,7 @@ struct CellCol : FineCol<DT> {
     int nemit;   // output levels emitted so far by this lane (every field alike)
     int kcons;   // levels [0, kcons) summed and written (wave-uniform)
     int ovf_k[NF];  // first level this lane sent to its global column (km: none)
+    int lim[NF];    // min(ovf_k, kcons + ring_levels): levels from here go to the global column
     int* ovf_lds;
     float* mine;  // this lane's global column (field 0, level 0)
     // coarsen_bufload<NF>: loads as buffer operations: resource over this tile's array
@@ -449,9 +450,10 @@ struct CellCol : FineCol<DT> {
         // _mask_weights (regridz.py:150-161): area where phalf_c[k0+1] < phalf_f[-1]
         const float w = (this->pc[k] < this->pbot) ? area : 0.0f;
         const float x = nan0(v * w);
-        if (k0 >= ovf_k[fi] || k0 - kcons >= ring_levels(NF)) {
+        if (k0 >= lim[fi]) {  // = k0 >= ovf_k[fi] || k0 - kcons >= ring_levels(NF)
             if (ovf_k[fi] > k0) {
                 ovf_k[fi] = k0;
+                lim[fi] = min(k0, kcons + ring_levels(NF));
                 ovf_lds[fi * 64 + ctx->lane] = k0;
             }
             mine[((int64_t)fi * ctx->km + k0) * ctx->sstride] = x;
@@ -468,6 +470,7 @@ struct CellCol : FineCol<DT> {
             __syncthreads();
             ctx->consume(kcons, nb, ovf_mask());
             kcons += nb;
+            for (int fi = 0; fi < NF; ++fi) lim[fi] = min(ovf_k[fi], kcons + ring_levels(NF));
         }
     }
 };
@@ -522,7 +525,10 @@ __device__ __forceinline__ void cells_field_group(const CoarsenArgs<DT>& a, int 
     col.active = active;
     col.nemit = 0;
     col.kcons = 0;
-    for (int fi = 0; fi < NF; ++fi) col.ovf_k[fi] = km;
+    for (int fi = 0; fi < NF; ++fi) {
+        col.ovf_k[fi] = km;
+        col.lim[fi] = min(km, ring_levels(NF));
+    }
     col.ovf_lds = ovf;
     col.mine = a.scratch + (int64_t)blockIdx.x * 64 + lane;
     if constexpr (coarsen_bufload<NF>()) {
@@ -593,10 +599,10 @@ regrid_coarsen_cells_kernel(CoarsenArgs<DT> a)
 
     // ---- pass 1: fine phalf (per lane), area-weighted coarse delp and phalf ----
     const float area = active ? a.area[(int64_t)tile * plane + fine] : 0.0f;
-    lar[lane] = area;
+    lar[lane] = nan0(area);  // read only as nan0(area): the block sums and the denominators
     __syncthreads();
     if (lane < G)  // weights.coarsen().sum(): float32 (area's dtype)
-        asum[lane] = block_sum<float>(f, [&](int jj) { return nan0(lar[lane * ff + jj]); });
+        asum[lane] = block_sum<float>(f, [&](int jj) { return lar[lane * ff + jj]; });
     const DT* dp = a.delp + (int64_t)tile * km * plane + fine;
     const DT ptop = (DT)a.ptop;
     DT run = ptop;  // fine phalf = cumsum([ptop, delp]) (vertically_dependent.py:62-63)
@@ -685,7 +691,7 @@ regrid_coarsen_cells_kernel(CoarsenArgs<DT> a)
             lane, G, f, nk, rowf,
             [&](int gi, int kk, int jj) {
                 const int l = gi * ff + jj;
-                return (pc[gi * (km + 1) + k0 + kk + 1] < lpb[l]) ? nan0(lar[l]) : 0.0f;
+                return (pc[gi * (km + 1) + k0 + kk + 1] < lpb[l]) ? lar[l] : 0.0f;
             },
             [&](int gi, int kk, float s) { den[gi * km + k0 + kk] = s; });
     }
